@@ -1,0 +1,281 @@
+// ORACLE — test infrastructure only (see ojson.h header). C entry points for ctypes (oracle/oracle.py).
+// Every function returns a malloc'ed JSON string (free with oracle_free) or an int.
+#include <cstdlib>
+#include <cstring>
+
+#include "goutil.h"
+#include "oengine.h"
+#include "ojson.h"
+#include "opss.h"
+#include "ovalidate.h"
+
+using namespace orc;
+using oj::T;
+using oj::Value;
+using oj::VP;
+
+static char* dup(const std::string& s) {
+  char* p = (char*)malloc(s.size() + 1);
+  memcpy(p, s.c_str(), s.size() + 1);
+  return p;
+}
+
+static std::map<std::string, std::string> labels_of(const VP& v) {
+  std::map<std::string, std::string> m;
+  if (v && v->t == T::Obj)
+    for (auto& kv : v->o) m[kv.first] = kv.second && kv.second->t == T::Str ? kv.second->s : "";
+  return m;
+}
+
+static VP rule_result_json(const RuleResult& r) {
+  auto o = Value::obj();
+  o->o["name"] = Value::str(r.name);
+  o->o["status"] = Value::str(r.status);
+  o->o["message"] = Value::str(r.message);
+  o->o["path"] = Value::str(r.path);
+  o->o["nondeterministic"] = Value::boolean(r.nondeterministic);
+  o->o["message_unpinned"] = Value::boolean(r.message_unpinned);
+  auto bp = Value::arr();
+  for (auto& b : r.branch_paths) bp->a.push_back(Value::str(b));
+  o->o["branch_paths"] = bp;
+  auto checks = Value::arr();
+  for (auto& c : r.pss_checks) {
+    auto co = Value::obj();
+    co->o["id"] = Value::str(c.id);
+    co->o["reason"] = Value::str(c.r.reason);
+    co->o["detail"] = Value::str(c.r.detail);
+    checks->a.push_back(co);
+  }
+  o->o["pss_checks"] = checks;
+  return o;
+}
+
+extern "C" {
+
+void oracle_free(char* p) { free(p); }
+
+int oracle_wildcard(const char* pattern, const char* text) { return gou::wildcard_match(pattern, text) ? 1 : 0; }
+
+// value decoded with unstructured semantics, pattern with interface{} (float) semantics
+int oracle_pattern_validate(const char* value_json, const char* pattern_json) {
+  try {
+    VP v = oj::parse(value_json, false);
+    VP p = oj::parse(pattern_json, true);
+    return pattern_validate(v, p) ? 1 : 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
+// quantity compare: -1/0/1, or -2 when either side fails to parse
+int oracle_quantity_cmp(const char* a, const char* b) {
+  gou::Quantity qa, qb;
+  if (!gou::parse_quantity(a, qa) || !gou::parse_quantity(b, qb)) return -2;
+  return gou::quantity_cmp(qa, qb);
+}
+
+// duration: returns 1 and sets *ns on success
+int oracle_duration(const char* s, long long* ns) {
+  int64_t v;
+  if (!gou::parse_duration(s, v)) return 0;
+  *ns = v;
+  return 1;
+}
+
+char* oracle_format_float(double f, int kind) {  // 0:'E' 1:'g' 2:%f 3:json
+  switch (kind) {
+    case 0: return dup(gou::format_float_E(f));
+    case 1: return dup(gou::format_float_g(f));
+    case 2: return dup(gou::format_float_f6(f));
+    default: return dup(gou::format_float_json(f));
+  }
+}
+
+char* oracle_match_pattern(const char* resource_json, const char* pattern_json) {
+  auto o = Value::obj();
+  try {
+    VP r = oj::parse(resource_json, false);
+    VP p = oj::parse(pattern_json, true);
+    EvalFlags fl;
+    PatternResult pr = match_pattern(r, p, fl);
+    o->o["ok"] = Value::boolean(pr.ok);
+    o->o["skip"] = Value::boolean(pr.skip);
+    o->o["path"] = Value::str(pr.path);
+    o->o["err"] = Value::str(pr.err);
+    o->o["nondeterministic"] = Value::boolean(fl.nondeterministic);
+  } catch (RefPanic& e) {
+    o->o["panic"] = Value::str(e.what);
+  } catch (std::exception& e) {
+    o->o["exception"] = Value::str(e.what());
+  }
+  return dup(oj::dump(o));
+}
+
+char* oracle_pss(const char* rule_json, const char* pod_json) {
+  auto o = Value::obj();
+  try {
+    VP rule = oj::parse(rule_json, true);
+    VP pod = oj::parse(pod_json, false);
+    PSSEval ev = pss_evaluate(rule, pod->get("metadata"), pod->get("spec"));
+    o->o["ok"] = Value::boolean(ev.ok);
+    o->o["error"] = Value::str(ev.error + ev.decode_error);
+    o->o["allowed"] = Value::boolean(ev.allowed);
+    auto checks = Value::arr();
+    for (auto& c : ev.checks) {
+      auto co = Value::obj();
+      co->o["id"] = Value::str(c.id);
+      co->o["reason"] = Value::str(c.r.reason);
+      co->o["detail"] = Value::str(c.r.detail);
+      checks->a.push_back(co);
+    }
+    o->o["checks"] = checks;
+    o->o["message"] = Value::str(format_checks_print(ev.checks));
+  } catch (std::exception& e) {
+    o->o["exception"] = Value::str(e.what());
+  }
+  return dup(oj::dump(o));
+}
+
+// policy JSON -> computed rules (autogen) as JSON array
+char* oracle_compute_rules(const char* policy_json) {
+  try {
+    VP p = oj::parse(policy_json, true);
+    auto arr = Value::arr();
+    for (auto& r : compute_rules(p)) arr->a.push_back(r);
+    return dup(oj::dump(arr));
+  } catch (std::exception& e) {
+    return dup(std::string("{\"exception\":") + "\"" + e.what() + "\"}");
+  }
+}
+
+int oracle_rule_matches(const char* rule_json, const char* resource_json, const char* nslabels_json) {
+  try {
+    VP rule = oj::parse(rule_json, true);
+    VP res = resource_json && *resource_json ? oj::parse(resource_json, false) : nullptr;
+    VP nsl = nslabels_json && *nslabels_json ? oj::parse(nslabels_json, false) : nullptr;
+    bool nd = false;
+    return matches_resource_description(rule, res, labels_of(nsl), &nd) ? 1 : 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
+// engine.Validate for a list of policies against one resource:
+// -> [{"policy": name, "namespace_skipped": bool, "rules": [...]}]
+char* oracle_validate(const char* policies_json, const char* resource_json, const char* nslabels_json) {
+  auto out = Value::arr();
+  try {
+    VP pols = oj::parse(policies_json, true);
+    VP res = oj::parse(resource_json, false);
+    VP nsl = nslabels_json && *nslabels_json ? oj::parse(nslabels_json, false) : nullptr;
+    auto nsLabels = labels_of(nsl);
+    std::vector<VP> list;
+    if (pols->t == T::Arr) list = pols->a; else list.push_back(pols);
+    for (auto& p : list) {
+      PolicyResult pr = validate_policy(p, res, nsLabels);
+      auto po = Value::obj();
+      po->o["policy"] = Value::str(pr.name);
+      po->o["namespace_skipped"] = Value::boolean(pr.namespace_skipped);
+      auto rules = Value::arr();
+      for (auto& r : pr.rules) rules->a.push_back(rule_result_json(r));
+      po->o["rules"] = rules;
+      out->a.push_back(po);
+    }
+  } catch (std::exception& e) {
+    auto o = Value::obj();
+    o->o["exception"] = Value::str(e.what());
+    return dup(oj::dump(o));
+  }
+  return dup(oj::dump(out));
+}
+
+// Batch timing entry for the CPU baseline: evaluate every (policy, resource) pair; resources is a JSON
+// array. Returns the number of (resource x computed rule) evaluations performed (matched or not).
+long long oracle_validate_batch(const char* policies_json, const char* resources_json, const char* nslabels_json, int nthreads,
+                                long long* status_counts /* pass fail skip error other */, double* seconds);
+}
+
+#include <atomic>
+#include <chrono>
+#include <thread>
+
+// Batch entry for the CPU baseline (bench.py cpu_baseline leg): policies' computed rules are prepared once,
+// resources are decoded before the clock starts; the timed region is the per-(resource, rule) evaluation
+// exactly as engine.Validate performs it (match incl. OldResource retry, pattern walk / PSS).
+long long oracle_validate_batch(const char* policies_json, const char* resources_json, const char* nslabels_json, int nthreads,
+                                long long* status_counts, double* seconds) {
+  VP pols = oj::parse(policies_json, true);
+  VP res = oj::parse(resources_json, false);
+  VP nsl = nslabels_json && *nslabels_json ? oj::parse(nslabels_json, false) : nullptr;
+  auto nsLabels = labels_of(nsl);
+  std::vector<VP> rules;
+  std::vector<VP> list;
+  if (pols->t == T::Arr) list = pols->a; else list.push_back(pols);
+  for (auto& p : list) for (auto& r : compute_rules(p)) rules.push_back(r);
+  std::vector<VP>& rs = res->a;
+  if (nthreads < 1) nthreads = 1;
+  std::atomic<long long> cnt[5];
+  for (auto& c : cnt) c = 0;
+  std::atomic<size_t> next{0};
+  auto t0 = std::chrono::steady_clock::now();
+  auto work = [&]() {
+    long long local[5] = {0, 0, 0, 0, 0};
+    while (true) {
+      size_t i = next.fetch_add(64);
+      if (i >= rs.size()) break;
+      size_t e = std::min(rs.size(), i + 64);
+      for (size_t k = i; k < e; k++) {
+        for (auto& rule : rules) {
+          bool nd = false;
+          bool m = matches_resource_description(rule, rs[k], nsLabels, &nd);
+          if (!m) m = matches_resource_description(rule, nullptr, nsLabels, &nd);
+          if (!m) { local[4]++; continue; }
+          RuleResult rr = validate_rule(rule, rs[k]);
+          if (rr.status == "pass") local[0]++;
+          else if (rr.status == "fail") local[1]++;
+          else if (rr.status == "skip") local[2]++;
+          else if (rr.status == "error") local[3]++;
+          else local[4]++;
+        }
+      }
+    }
+    for (int j = 0; j < 5; j++) cnt[j] += local[j];
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; t++) th.emplace_back(work);
+  for (auto& t : th) t.join();
+  auto t1 = std::chrono::steady_clock::now();
+  if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+  if (status_counts) for (int j = 0; j < 5; j++) status_counts[j] = cnt[j];
+  return (long long)rs.size() * (long long)rules.size();
+}
+
+extern "C" {
+int oracle_leaf(const char* fn, const char* value_json, int value_float, const char* pattern_json, const char* op) {
+  try {
+    VP v = oj::parse(value_json, value_float != 0);
+    VP p = oj::parse(pattern_json, true);
+    return leaf_fn(fn, v, p, op) ? 1 : 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
+char* oracle_validate_entry(const char* entry, const char* resource_json, const char* pattern_json, int resource_float) {
+  auto o = Value::obj();
+  try {
+    VP r = oj::parse(resource_json, resource_float != 0);
+    VP p = oj::parse(pattern_json, true);
+    EvalFlags fl;
+    RawWalk w = validate_entry(entry, r, p, fl);
+    o->o["path"] = Value::str(w.path);
+    o->o["err"] = Value::boolean(w.err);
+    o->o["msg"] = Value::str(w.msg);
+  } catch (RefPanic& e) {
+    o->o["panic"] = Value::str(e.what);
+  } catch (std::exception& e) {
+    o->o["exception"] = Value::str(e.what());
+  }
+  return dup(oj::dump(o));
+}
+}

@@ -1,0 +1,798 @@
+// ORACLE — test infrastructure only (see ojson.h header).
+//
+// Engine-level restatement of the validate path for background-scan semantics (empty admission info,
+// no PolicyExceptions, no discovery subresources):
+//   pkg/engine/validation.go:39-183 (Validate/validateResource), :276-317 (validator.validate dispatch),
+//     :535-566 (validatePodSecurity), :600-615 (matches, incl. the always-taken OldResource retry),
+//     :618-702 (validatePatterns), :722-758 (messages)
+//   pkg/engine/utils.go:37-289 (match/exclude), pkg/utils/match/*.go, pkg/utils/kube/kind.go
+//   pkg/autogen/autogen.go:70-314 + rule.go:73-319 (ComputeRules)
+//   k8s.io/apimachinery v0.26.1 labels selectors (LabelSelectorAsSelector / Requirement.Matches) — restated
+#include "oengine.h"
+
+#include <algorithm>
+#include <set>
+
+#include "goutil.h"
+#include "opss.h"
+#include "ovalidate.h"
+
+namespace orc {
+using oj::T;
+using oj::Value;
+using oj::VP;
+
+static bool isnil(const VP& v) { return !v || v->t == T::Null; }
+
+static std::vector<std::string> str_list(const VP& v) {
+  std::vector<std::string> out;
+  if (v && v->t == T::Arr)
+    for (auto& e : v->a) out.push_back(e && e->t == T::Str ? e->s : "");
+  return out;
+}
+
+// ---------------- unstructured accessors (apimachinery unstructured helpers) ----------------
+static bool nested(const VP& obj, std::initializer_list<const char*> path, VP& out) {
+  VP cur = obj;
+  for (const char* f : path) {
+    if (!cur || cur->t != T::Obj) return false;
+    auto it = cur->o.find(f);
+    if (it == cur->o.end()) return false;
+    cur = it->second;
+  }
+  out = cur;
+  return true;
+}
+static std::string nested_string(const VP& obj, std::initializer_list<const char*> path) {
+  VP v;
+  if (!nested(obj, path, v) || !v || v->t != T::Str) return "";
+  return v->s;
+}
+// NestedStringMap -> nil on any error (non-map / non-string value)
+static bool nested_string_map(const VP& obj, std::initializer_list<const char*> path, std::map<std::string, std::string>& out) {
+  VP v;
+  out.clear();
+  if (!nested(obj, path, v)) return false;
+  if (isnil(v)) return false;
+  if (v->t != T::Obj) return false;
+  for (auto& kv : v->o) {
+    if (!kv.second || kv.second->t != T::Str) { out.clear(); return false; }
+    out[kv.first] = kv.second->s;
+  }
+  return true;
+}
+
+struct Res {
+  bool empty = true;
+  std::string kind, name, genName, ns;
+  std::string group, version, gvkKind;  // GroupVersionKind()
+  bool hasLabels = false, hasAnn = false;
+  std::map<std::string, std::string> labels, ann;
+};
+
+static Res res_info(const VP& obj) {
+  Res r;
+  if (!obj) return r;
+  r.empty = false;
+  r.kind = nested_string(obj, {"kind"});
+  r.name = nested_string(obj, {"metadata", "name"});
+  r.genName = nested_string(obj, {"metadata", "generateName"});
+  r.ns = nested_string(obj, {"metadata", "namespace"});
+  r.hasLabels = nested_string_map(obj, {"metadata", "labels"}, r.labels);
+  r.hasAnn = nested_string_map(obj, {"metadata", "annotations"}, r.ann);
+  std::string av = nested_string(obj, {"apiVersion"});
+  size_t slashes = std::count(av.begin(), av.end(), '/');
+  if (av.empty() || av == "/") { r.gvkKind = r.kind; }
+  else if (slashes == 0) { r.version = av; r.gvkKind = r.kind; }
+  else if (slashes == 1) { size_t i = av.find('/'); r.group = av.substr(0, i); r.version = av.substr(i + 1); r.gvkKind = r.kind; }
+  else { /* ParseGroupVersion error -> empty GVK */ }
+  return r;
+}
+
+// ---------------- kinds (pkg/utils/kube/kind.go, pkg/utils/match/kind.go) ----------------
+static bool version_regex(const std::string& s) {  // v\d((alpha|beta)\d)? unanchored
+  for (size_t i = 0; i + 1 < s.size(); i++) if (s[i] == 'v' && s[i + 1] >= '0' && s[i + 1] <= '9') return true;
+  return false;
+}
+static std::string format_subresource(std::string s) {
+  size_t i = s.find('.');
+  if (i != std::string::npos) s[i] = '/';
+  return s;
+}
+void get_kind_from_gvk(const std::string& str, std::string& gv, std::string& kind) {
+  auto parts = gou::split(str, '/');
+  gv.clear();
+  if (parts.size() == 2) {
+    if (version_regex(parts[0]) || parts[0] == "*") { gv = parts[0]; kind = format_subresource(parts[1]); }
+    else kind = parts[0] + "/" + parts[1];
+  } else if (parts.size() == 3) {
+    if (version_regex(parts[0]) || parts[0] == "*") { gv = parts[0]; kind = parts[1] + "/" + parts[2]; }
+    else { gv = parts[0] + "/" + parts[1]; kind = format_subresource(parts[2]); }
+  } else if (parts.size() == 4) {
+    gv = parts[0] + "/" + parts[1];
+    kind = parts[2] + "/" + parts[3];
+  } else {
+    kind = format_subresource(str);
+  }
+}
+static bool parse_gv(const std::string& s, std::string& g, std::string& v) {
+  g.clear(); v.clear();
+  if (s.empty() || s == "/") return true;
+  size_t n = std::count(s.begin(), s.end(), '/');
+  if (n == 0) { v = s; return true; }
+  if (n == 1) { size_t i = s.find('/'); g = s.substr(0, i); v = s.substr(i + 1); return true; }
+  return false;
+}
+static bool group_version_matches(const std::string& gv, const std::string& server) {
+  if (gv.find('*') != std::string::npos) {
+    std::string p = gv;
+    if (!p.empty() && p.back() == '*') p.pop_back();
+    return server.compare(0, p.size(), p) == 0;
+  }
+  std::string g1, v1, g2, v2;
+  if (parse_gv(gv, g1, v1)) {
+    parse_gv(server, g2, v2);
+    return g1 == g2 && v1 == v2;
+  }
+  return false;
+}
+static bool check_kind(const std::vector<std::string>& kinds, const Res& r) {
+  std::string serverGV = r.group.empty() ? r.version : r.group + "/" + r.version;
+  for (auto& k : kinds) {
+    bool result;
+    if (k != "*") {
+      std::string gv, kind;
+      get_kind_from_gvk(k, gv, kind);
+      result = kind == r.gvkKind;
+      if (!gv.empty()) result = result && group_version_matches(gv, serverGV);
+    } else {
+      result = true;
+    }
+    if (result) return true;
+  }
+  return false;
+}
+
+// ---------------- label selectors (apimachinery) ----------------
+static bool qname_char(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); }
+static bool qualified_name_part(const std::string& n) {  // ([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9], len<=63
+  if (n.empty() || n.size() > 63) return false;
+  if (!qname_char(n.front()) || !qname_char(n.back())) return false;
+  for (char c : n) if (!(qname_char(c) || c == '-' || c == '_' || c == '.')) return false;
+  return true;
+}
+static bool dns1123_subdomain(const std::string& s) {
+  if (s.empty() || s.size() > 253) return false;
+  for (auto& lab : gou::split(s, '.')) {
+    if (lab.empty()) return false;
+    auto alnum = [](char c) { return (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'); };
+    if (!alnum(lab.front()) || !alnum(lab.back())) return false;
+    for (char c : lab) if (!(alnum(c) || c == '-')) return false;
+  }
+  return true;
+}
+static bool valid_label_key(const std::string& k) {
+  auto parts = gou::split(k, '/');
+  if (parts.size() == 1) return qualified_name_part(parts[0]);
+  if (parts.size() == 2) return !parts[0].empty() && dns1123_subdomain(parts[0]) && qualified_name_part(parts[1]);
+  return false;
+}
+static bool valid_label_value(const std::string& v) { return v.empty() || qualified_name_part(v); }
+
+struct Req { std::string key, op; std::vector<std::string> vals; };
+
+// CheckSelector (pkg/utils/match/labels.go:10-24) incl. wildcards.ReplaceInSelector; returns 0 no match, 1 match,
+// -1 error (invalid selector), and flags nondeterminism when several labels can satisfy a wildcard entry.
+static int check_selector(const VP& sel, const std::map<std::string, std::string>& labels, bool* nd) {
+  if (isnil(sel)) return 0;
+  std::vector<Req> reqs;
+  VP ml = sel->get("matchLabels");
+  std::map<std::string, std::string> result;
+  if (ml && ml->t == T::Obj) {
+    for (auto& kv : ml->o) {
+      std::string k = kv.first, v = kv.second && kv.second->t == T::Str ? kv.second->s : "";
+      if (gou::contains_wildcard(k) || gou::contains_wildcard(v)) {
+        int n = 0;
+        std::string mk, mv;
+        for (auto& lv : labels)
+          if (gou::wildcard_match(k, lv.first) && gou::wildcard_match(v, lv.second)) {
+            if (n == 0) { mk = lv.first; mv = lv.second; }
+            n++;
+          }
+        if (n > 1 && nd) *nd = true;
+        if (n == 0) {
+          for (auto& c : k) if (c == '*' || c == '?') c = '0';
+          for (auto& c : v) if (c == '*' || c == '?') c = '0';
+          mk = k; mv = v;
+        }
+        if (result.count(mk) && nd) *nd = true;
+        result[mk] = mv;
+      } else {
+        if (result.count(k) && nd) *nd = true;
+        result[k] = v;
+      }
+    }
+  }
+  VP me = sel->get("matchExpressions");
+  size_t nexpr = me && me->t == T::Arr ? me->a.size() : 0;
+  if (result.empty() && nexpr == 0) return 1;  // Everything
+  for (auto& kv : result) reqs.push_back(Req{kv.first, "=", {kv.second}});
+  for (size_t i = 0; i < nexpr; i++) {
+    VP e = me->a[i];
+    std::string op = oj::get_str(e, "operator");
+    std::string o;
+    if (op == "In") o = "in";
+    else if (op == "NotIn") o = "notin";
+    else if (op == "Exists") o = "exists";
+    else if (op == "DoesNotExist") o = "!";
+    else return -1;
+    reqs.push_back(Req{oj::get_str(e, "key"), o, str_list(e ? e->get("values") : nullptr)});
+  }
+  for (auto& r : reqs) {  // NewRequirement validation
+    if (!valid_label_key(r.key)) return -1;
+    if ((r.op == "in" || r.op == "notin") && r.vals.empty()) return -1;
+    if (r.op == "=" && r.vals.size() != 1) return -1;
+    if ((r.op == "exists" || r.op == "!") && !r.vals.empty()) return -1;
+    for (auto& v : r.vals) if (!valid_label_value(v)) return -1;
+  }
+  for (auto& r : reqs) {
+    auto it = labels.find(r.key);
+    bool has = it != labels.end();
+    bool inset = has && std::find(r.vals.begin(), r.vals.end(), it->second) != r.vals.end();
+    bool ok;
+    if (r.op == "=" || r.op == "in") ok = inset;
+    else if (r.op == "notin") ok = !has || !inset;
+    else if (r.op == "exists") ok = has;
+    else ok = !has;
+    if (!ok) return 0;
+  }
+  return 1;
+}
+
+// ---------------- match / exclude (pkg/engine/utils.go) ----------------
+static bool rd_is_zero(const VP& rd) {
+  if (isnil(rd)) return true;
+  for (const char* k : {"kinds", "names", "namespaces", "annotations", "selector", "namespaceSelector"})
+    if (!isnil(rd->get(k))) return false;
+  return oj::get_str(rd, "name").empty();
+}
+static bool ui_is_zero(const VP& f) {
+  if (isnil(f)) return true;
+  for (const char* k : {"roles", "clusterRoles", "subjects"})
+    if (!isnil(f->get(k))) return false;
+  return true;
+}
+
+// doesResourceMatchConditionBlock (utils.go:71-160): true when no errors
+static bool condition_block(const VP& rd, const VP& ui, const Res& r, const std::map<std::string, std::string>& nsLabels,
+                            bool* nd) {
+  bool ok = true;
+  std::vector<std::string> kinds = str_list(rd ? rd->get("kinds") : nullptr);
+  if (!kinds.empty() && !check_kind(kinds, r)) ok = false;
+  std::string rname = r.name.empty() ? r.genName : r.name;
+  std::string name = oj::get_str(rd, "name");
+  if (!name.empty() && !gou::wildcard_match(name, rname)) ok = false;
+  auto names = str_list(rd ? rd->get("names") : nullptr);
+  if (!names.empty()) {
+    bool any = false;
+    for (auto& n : names) if (gou::wildcard_match(n, rname)) { any = true; break; }
+    if (!any) ok = false;
+  }
+  auto nss = str_list(rd ? rd->get("namespaces") : nullptr);
+  if (!nss.empty()) {
+    std::string rns = r.kind == "Namespace" ? r.name : r.ns;
+    bool any = false;
+    for (auto& n : nss) if (gou::wildcard_match(n, rns)) { any = true; break; }
+    if (!any) ok = false;
+  }
+  VP ann = rd ? rd->get("annotations") : nullptr;
+  if (ann && ann->t == T::Obj && !ann->o.empty()) {
+    for (auto& kv : ann->o) {
+      std::string v = kv.second && kv.second->t == T::Str ? kv.second->s : "";
+      bool m = false;
+      for (auto& a : r.ann)
+        if (gou::wildcard_match(kv.first, a.first) && gou::wildcard_match(v, a.second)) { m = true; break; }
+      if (!m) { ok = false; break; }
+    }
+  }
+  VP sel = rd ? rd->get("selector") : nullptr;
+  if (!isnil(sel)) {
+    if (check_selector(sel, r.labels, nd) != 1) ok = false;
+  }
+  VP nsel = rd ? rd->get("namespaceSelector") : nullptr;
+  if (!isnil(nsel) && r.kind != "Namespace" &&
+      (!r.kind.empty() || std::find(kinds.begin(), kinds.end(), "*") != kinds.end())) {
+    if (check_selector(nsel, nsLabels, nd) != 1) ok = false;
+  }
+  // userInfo with empty admission info: roles / clusterRoles / subjects never satisfied
+  if (!isnil(ui)) {
+    if (!str_list(ui->get("roles")).empty()) ok = false;
+    if (!str_list(ui->get("clusterRoles")).empty()) ok = false;
+    VP subj = ui->get("subjects");
+    if (subj && subj->t == T::Arr && !subj->a.empty()) ok = false;
+  }
+  return ok;
+}
+
+// matchesResourceDescriptionMatchHelper: errors? (true = matched)
+static bool match_helper(const VP& filter_rd, const Res& r, const std::map<std::string, std::string>& nsl, bool* nd) {
+  // empty admission info => userInfo cleared
+  if (rd_is_zero(filter_rd)) return false;  // "match cannot be empty"
+  return condition_block(filter_rd, nullptr, r, nsl, nd);
+}
+// matchesResourceDescriptionExcludeHelper: true = excluded
+static bool exclude_helper(const VP& filter_rd, const VP& ui, const Res& r, const std::map<std::string, std::string>& nsl,
+                           bool* nd) {
+  if (rd_is_zero(filter_rd) && ui_is_zero(ui)) return false;
+  return condition_block(filter_rd, ui, r, nsl, nd);
+}
+
+bool matches_resource_description(const VP& rule, const VP& resource, const std::map<std::string, std::string>& nsl,
+                                  bool* nd) {  // utils.go:185-256
+  Res r = res_info(resource);
+  VP match = rule->get("match"), exclude = rule->get("exclude");
+  bool failed = false;
+  VP any = match ? match->get("any") : nullptr, all = match ? match->get("all") : nullptr;
+  if (any && any->t == T::Arr && !any->a.empty()) {
+    bool one = false;
+    for (auto& f : any->a) if (match_helper(f ? f->get("resources") : nullptr, r, nsl, nd)) { one = true; break; }
+    if (!one) failed = true;
+  } else if (all && all->t == T::Arr && !all->a.empty()) {
+    for (auto& f : all->a) if (!match_helper(f ? f->get("resources") : nullptr, r, nsl, nd)) failed = true;
+  } else {
+    if (!match_helper(match ? match->get("resources") : nullptr, r, nsl, nd)) failed = true;
+  }
+  VP eany = exclude ? exclude->get("any") : nullptr, eall = exclude ? exclude->get("all") : nullptr;
+  if (eany && eany->t == T::Arr && !eany->a.empty()) {
+    for (auto& f : eany->a) if (exclude_helper(f ? f->get("resources") : nullptr, f, r, nsl, nd)) failed = true;
+  } else if (eall && eall->t == T::Arr && !eall->a.empty()) {
+    bool byAll = true;
+    for (auto& f : eall->a) if (!exclude_helper(f ? f->get("resources") : nullptr, f, r, nsl, nd)) { byAll = false; break; }
+    if (byAll) failed = true;
+  } else if (exclude) {
+    if (exclude_helper(exclude->get("resources"), exclude, r, nsl, nd)) failed = true;
+  }
+  return !failed;
+}
+
+// ---------------- autogen (pkg/autogen) ----------------
+static bool contains_kind(const std::vector<std::string>& list, const std::string& kind) {
+  for (auto& e : list) {
+    std::string gv, k;
+    get_kind_from_gvk(e, gv, k);
+    auto parts = gou::split(k, '/');
+    if (parts.size() == 2) k = parts[0];
+    if (k == kind) return true;
+  }
+  return false;
+}
+static std::vector<std::string> get_kinds(const VP& mr) {  // MatchResources.GetKinds
+  std::vector<std::string> out;
+  if (isnil(mr)) return out;
+  VP rd = mr->get("resources");
+  for (auto& k : str_list(rd ? rd->get("kinds") : nullptr)) out.push_back(k);
+  for (const char* blk : {"all", "any"}) {
+    VP l = mr->get(blk);
+    if (l && l->t == T::Arr)
+      for (auto& f : l->a) {
+        VP frd = f ? f->get("resources") : nullptr;
+        for (auto& k : str_list(frd ? frd->get("kinds") : nullptr)) out.push_back(k);
+      }
+  }
+  return out;
+}
+static bool check_autogen_support(bool& needed, const VP& rd) {
+  if (isnil(rd)) return true;
+  static const std::set<std::string> podctl = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet",
+                                               "ReplicationController", "CronJob", "Pod"};
+  auto kinds = str_list(rd->get("kinds"));
+  if (!oj::get_str(rd, "name").empty() || !str_list(rd->get("names")).empty() || !isnil(rd->get("selector")) ||
+      !isnil(rd->get("annotations")) || (kinds.size() > 1 && contains_kind(kinds, "Pod")))
+    return false;
+  for (auto& k : kinds) if (podctl.count(k)) needed = true;
+  return true;
+}
+static bool has_nonempty(const VP& o, const char* k) {
+  VP v = o ? o->get(k) : nullptr;
+  if (isnil(v)) return false;
+  if (v->t == T::Obj) return !v->o.empty();
+  if (v->t == T::Arr) return !v->a.empty();
+  if (v->t == T::Str) return !v->s.empty();
+  return true;
+}
+static bool can_autogen(const VP& spec, std::string& controllers) {  // autogen.go:70-136
+  bool needed = false;
+  VP rules = spec ? spec->get("rules") : nullptr;
+  if (rules && rules->t == T::Arr)
+    for (auto& rule : rules->a) {
+      VP mut = rule->get("mutate");
+      if ((mut && !oj::get_str(mut, "patchesJson6902").empty()) || has_nonempty(rule, "generate")) {
+        controllers = "none";
+        return false;
+      }
+      VP m = rule->get("match"), e = rule->get("exclude");
+      if (!check_autogen_support(needed, m ? m->get("resources") : nullptr) ||
+          !check_autogen_support(needed, e ? e->get("resources") : nullptr)) { controllers = ""; return false; }
+      for (VP blk : {m, e})
+        for (const char* w : {"any", "all"}) {
+          VP l = blk ? blk->get(w) : nullptr;
+          if (l && l->t == T::Arr)
+            for (auto& f : l->a)
+              if (!check_autogen_support(needed, f ? f->get("resources") : nullptr)) { controllers = ""; return false; }
+        }
+    }
+  if (!needed) { controllers = ""; return false; }
+  controllers = "DaemonSet,Deployment,Job,StatefulSet,ReplicaSet,ReplicationController,CronJob";
+  return true;
+}
+
+static std::string autogen_name(const std::string& prefix, const std::string& name) {
+  std::string n = prefix + "-" + name;
+  if (n.size() > 63) n = n.substr(0, 63);
+  return n;
+}
+
+static VP replace_kinds_in_filters(const VP& filters, const std::string& match, const std::vector<std::string>& kinds) {
+  VP out = oj::deep_copy(filters);
+  for (auto& f : out->a) {
+    VP rd = f ? f->get("resources") : nullptr;
+    if (rd && contains_kind(str_list(rd->get("kinds")), match)) {
+      auto arr = Value::arr();
+      for (auto& k : kinds) arr->a.push_back(Value::str(k));
+      rd->o["kinds"] = arr;
+    }
+  }
+  return out;
+}
+
+static VP kinds_arr(const std::vector<std::string>& kinds) {
+  auto arr = Value::arr();
+  for (auto& k : kinds) arr->a.push_back(Value::str(k));
+  return arr;
+}
+
+static bool validation_nonempty(const VP& v) { return v && v->t == T::Obj && !v->o.empty(); }
+
+// generateRule (rule.go:73-204)
+static VP generate_rule(const std::string& name, const VP& rule0, const std::string& tplKey, const std::vector<std::string>& kinds,
+                        const std::string& grfKind) {
+  if (!rule0) return nullptr;
+  VP rule = oj::deep_copy(rule0);
+  rule->o["name"] = Value::str(name);
+  VP m = rule->get("match");
+  if (!m) { m = Value::obj(); rule->o["match"] = m; }
+  if (m->get("any") && m->get("any")->t == T::Arr && !m->get("any")->a.empty()) m->o["any"] = replace_kinds_in_filters(m->get("any"), grfKind, kinds);
+  else if (m->get("all") && m->get("all")->t == T::Arr && !m->get("all")->a.empty()) m->o["all"] = replace_kinds_in_filters(m->get("all"), grfKind, kinds);
+  else {
+    VP rd = m->get("resources");
+    if (isnil(rd)) { rd = Value::obj(); m->o["resources"] = rd; }
+    rd->o["kinds"] = kinds_arr(kinds);
+  }
+  VP e = rule->get("exclude");
+  if (e) {
+    if (e->get("any") && e->get("any")->t == T::Arr && !e->get("any")->a.empty()) e->o["any"] = replace_kinds_in_filters(e->get("any"), grfKind, kinds);
+    else if (e->get("all") && e->get("all")->t == T::Arr && !e->get("all")->a.empty()) e->o["all"] = replace_kinds_in_filters(e->get("all"), grfKind, kinds);
+    else {
+      VP rd = e->get("resources");
+      if (rd && !str_list(rd->get("kinds")).empty()) rd->o["kinds"] = kinds_arr(kinds);
+    }
+  }
+  VP mut = rule->get("mutate");
+  if (mut && (!isnil(mut->get("patchStrategicMerge")) || has_nonempty(mut, "foreach"))) {
+    return rule;  // mutation branches keep the validation untouched (not exercised on the validate path)
+  }
+  VP val = rule->get("validate");
+  if (!val) return nullptr;
+  std::string msg = oj::get_str(val, "message");
+  auto wrap = [&](const VP& p) {
+    auto inner = Value::obj();
+    inner->o[tplKey] = p;
+    auto outer = Value::obj();
+    outer->o["spec"] = inner;
+    return outer;
+  };
+  auto nv = Value::obj();
+  if (!msg.empty()) nv->o["message"] = Value::str(msg);
+  if (!isnil(val->get("pattern"))) {
+    nv->o["pattern"] = wrap(val->get("pattern"));
+  } else if (!isnil(val->get("deny"))) {
+    nv->o["deny"] = val->get("deny");
+  } else if (!isnil(val->get("podSecurity"))) {
+    auto ps = Value::obj();
+    VP ops = val->get("podSecurity");
+    if (!oj::get_str(ops, "level").empty()) ps->o["level"] = Value::str(oj::get_str(ops, "level"));
+    if (!oj::get_str(ops, "version").empty()) ps->o["version"] = Value::str(oj::get_str(ops, "version"));
+    VP ex = ops->get("exclude");
+    if (ex && ex->t == T::Arr && !ex->a.empty()) ps->o["exclude"] = ex;
+    nv->o["podSecurity"] = ps;
+  } else if (!isnil(val->get("anyPattern"))) {
+    auto arr = Value::arr();
+    VP ap = val->get("anyPattern");
+    if (ap->t == T::Arr) for (auto& p : ap->a) arr->a.push_back(wrap(p));
+    nv->o["anyPattern"] = arr;
+  } else if (has_nonempty(val, "foreach")) {
+    nv->o["foreach"] = val->get("foreach");
+  } else if (has_nonempty(rule, "verifyImages")) {
+    return rule;
+  } else {
+    return nullptr;
+  }
+  rule->o["validate"] = nv;
+  return rule;
+}
+
+static VP generate_rule_for_controllers(const VP& rule, std::string controllers) {  // rule.go:228-279
+  std::string name = oj::get_str(rule, "name");
+  if (name.compare(0, 8, "autogen-") == 0 || controllers.empty()) return nullptr;
+  auto mk = get_kinds(rule->get("match")), ek = get_kinds(rule->get("exclude"));
+  if (!contains_kind(mk, "Pod") || (!ek.empty() && !contains_kind(ek, "Pod"))) return nullptr;
+  static const std::set<std::string> list = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet", "ReplicationController"};
+  if (controllers == "all") controllers = "DaemonSet,Deployment,Job,StatefulSet,ReplicaSet,ReplicationController";
+  else if (controllers != "none") {
+    std::vector<std::string> v;
+    for (auto& c : gou::split(controllers, ',')) if (list.count(c)) v.push_back(c);
+    if (!v.empty()) {
+      controllers.clear();
+      for (size_t i = 0; i < v.size(); i++) { if (i) controllers += ","; controllers += v[i]; }
+    }
+  }
+  return generate_rule(autogen_name("autogen", name), rule, "template", gou::split(controllers, ','), "Pod");
+}
+
+static VP generate_cronjob_rule(const VP& rule, const std::string& controllers) {  // rule.go:281-297
+  if (controllers.find("CronJob") == std::string::npos && controllers.find("all") == std::string::npos) return nullptr;
+  return generate_rule(autogen_name("autogen-cronjob", oj::get_str(rule, "name")), generate_rule_for_controllers(rule, controllers),
+                       "jobTemplate", {"CronJob"}, "Job");
+}
+
+static std::string replace_all(std::string s, const std::string& from, const std::string& to) {
+  size_t p = 0;
+  while ((p = s.find(from, p)) != std::string::npos) { s.replace(p, from.size(), to); p += to.size(); }
+  return s;
+}
+
+static VP convert_rule(const VP& rule, const std::string& kind) {  // autogen.go:238-276
+  std::string b = oj::dump(rule);
+  VP val = rule->get("validate");
+  bool pss = val && !isnil(val->get("podSecurity"));
+  if (pss) {
+    if (kind == "Pod") b = replace_all(b, "\"restrictedField\":\"spec", "\"restrictedField\":\"spec.template.spec");
+    else b = replace_all(b, "\"restrictedField\":\"spec", "\"restrictedField\":\"spec.jobTemplate.spec.template.spec");
+    b = replace_all(b, "metadata", "spec.template.metadata");
+  } else {
+    if (kind == "Pod") b = replace_all(b, "request.object.spec", "request.object.spec.template.spec");
+    else b = replace_all(b, "request.object.spec", "request.object.spec.jobTemplate.spec.template.spec");
+    b = replace_all(b, "request.object.metadata", "request.object.spec.template.metadata");
+  }
+  return oj::parse(b, true);
+}
+
+std::vector<VP> compute_rules(const VP& policy) {  // autogen.go:280-314
+  VP spec = policy->get("spec");
+  std::vector<VP> rules;
+  VP rl = spec ? spec->get("rules") : nullptr;
+  if (rl && rl->t == T::Arr) rules = rl->a;
+  std::string desired;
+  bool apply = can_autogen(spec, desired);
+  if (!apply) desired = "none";
+  std::string actual = desired;
+  VP ann = nullptr;
+  VP meta = policy->get("metadata");
+  if (meta) ann = meta->get("annotations");
+  VP a = ann ? ann->get("pod-policies.kyverno.io/autogen-controllers") : nullptr;
+  if (a && apply) actual = a->t == T::Str ? a->s : "";
+  if (actual == "none") return rules;
+  std::vector<VP> gen;
+  std::string stripped;
+  {
+    std::vector<std::string> v;
+    for (auto& c : gou::split(actual, ',')) if (c != "CronJob") v.push_back(c);
+    for (size_t i = 0; i < v.size(); i++) { if (i) stripped += ","; stripped += v[i]; }
+  }
+  for (auto& r : rules) {
+    VP g = generate_rule_for_controllers(r, stripped);
+    if (g) gen.push_back(convert_rule(g, "Pod"));
+    VP c = generate_cronjob_rule(r, actual);
+    if (c) gen.push_back(convert_rule(c, "Cronjob"));
+  }
+  if (gen.empty()) return rules;
+  std::vector<VP> out;
+  for (auto& r : rules) if (oj::get_str(r, "name").compare(0, 8, "autogen-") != 0) out.push_back(r);
+  for (auto& g : gen) out.push_back(g);
+  return out;
+}
+
+// ---------------- rule evaluation (validation.go) ----------------
+static bool contains_vars(const VP& v) {
+  if (!v) return false;
+  if (v->t == T::Str) return v->s.find("{{") != std::string::npos || v->s.find("$(") != std::string::npos;
+  if (v->t == T::Arr) { for (auto& e : v->a) if (contains_vars(e)) return true; return false; }
+  if (v->t == T::Obj) {
+    for (auto& kv : v->o) {
+      if (kv.first.find("{{") != std::string::npos || kv.first.find("$(") != std::string::npos) return true;
+      if (contains_vars(kv.second)) return true;
+    }
+  }
+  return false;
+}
+
+std::string rule_unsupported_reason(const VP& rule) {
+  VP val = rule->get("validate");
+  if (has_nonempty(rule, "context")) return "context";
+  if (!isnil(rule->get("preconditions"))) return "preconditions";
+  if (has_nonempty(rule, "verifyImages")) return "verifyImages";
+  if (!val) return "";
+  if (!isnil(val->get("deny"))) return "deny";
+  if (contains_vars(val->get("pattern")) || contains_vars(val->get("anyPattern"))) return "variables";
+  if (oj::get_str(val, "message").find("{{") != std::string::npos || oj::get_str(val, "message").find("$(") != std::string::npos)
+    return "message-variables";
+  if (isnil(val->get("pattern")) && isnil(val->get("anyPattern")) && isnil(val->get("podSecurity")) && has_nonempty(val, "foreach"))
+    return "foreach";
+  if (!isnil(val->get("manifests"))) return "manifests";
+  return "";
+}
+
+static std::string build_error_message(const std::string& rname, const std::string& msg0, const std::string& err, const std::string& path) {
+  if (msg0.empty()) {
+    if (!path.empty()) return "validation error: rule " + rname + " failed at path " + path;
+    return "validation error: rule " + rname + " execution error: " + err;
+  }
+  std::string msg = msg0;
+  if (msg.empty() || msg.back() != '.') msg += ".";
+  if (!path.empty()) return "validation error: " + msg + " rule " + rname + " failed at path " + path;
+  return "validation error: " + msg + " rule " + rname + " execution error: " + err;
+}
+
+RuleResult validate_rule(const VP& rule, const VP& resource) {
+  RuleResult out;
+  out.name = oj::get_str(rule, "name");
+  std::string why = rule_unsupported_reason(rule);
+  if (!why.empty()) { out.status = "unsupported"; out.message = why; return out; }
+  VP val = rule->get("validate");
+  std::string msg = oj::get_str(val, "message");
+  try {
+    if (!isnil(val->get("pattern"))) {  // validatePatterns single pattern (validation.go:619-641)
+      EvalFlags fl;
+      PatternResult pr = match_pattern(resource, val->get("pattern"), fl);
+      out.nondeterministic = fl.nondeterministic;
+      if (pr.ok) { out.status = "pass"; out.message = "validation rule '" + out.name + "' passed."; return out; }
+      if (pr.skip) { out.status = "skip"; out.message = pr.err; return out; }
+      if (pr.path.empty()) { out.status = "error"; out.message = build_error_message(out.name, msg, pr.err, ""); return out; }
+      out.status = "fail";
+      out.path = pr.path;
+      out.message = build_error_message(out.name, msg, pr.err, pr.path);
+      return out;
+    }
+    if (!isnil(val->get("anyPattern"))) {  // validation.go:644-701
+      VP ap = val->get("anyPattern");
+      if (ap->t != T::Arr) {
+        out.status = "error";
+        out.message = "failed to deserialize anyPattern, expected type array: json: cannot unmarshal into []interface {}";
+        return out;
+      }
+      std::vector<std::string> failed, skipped;
+      for (size_t idx = 0; idx < ap->a.size(); idx++) {
+        EvalFlags fl;
+        PatternResult pr = match_pattern(resource, ap->a[idx], fl);
+        out.nondeterministic |= fl.nondeterministic;
+        if (pr.ok) {
+          out.status = "pass";
+          out.message = "validation rule '" + out.name + "' anyPattern[" + std::to_string(idx) + "] passed.";
+          return out;
+        }
+        std::string pre = "rule " + out.name + "[" + std::to_string(idx) + "]";
+        if (pr.skip) skipped.push_back(pre + " skipped: " + pr.err);
+        else if (pr.path.empty()) failed.push_back(pre + " failed: " + pr.err);
+        else failed.push_back(pre + " failed at path " + pr.path);
+        out.branch_paths.push_back(pr.skip ? "<skip>" : pr.path);
+      }
+      if (!skipped.empty() && failed.empty()) {
+        out.status = "skip";
+        std::string s;
+        for (size_t i = 0; i < skipped.size(); i++) { if (i) s += " "; s += skipped[i]; }
+        out.message = s;
+        return out;
+      }
+      if (!failed.empty()) {
+        std::string s;
+        for (size_t i = 0; i < failed.size(); i++) { if (i) s += " "; s += failed[i]; }
+        out.status = "fail";
+        if (msg.empty()) out.message = "validation error: " + s;
+        else if (msg.back() == '.') out.message = "validation error: " + msg + " " + s;
+        else out.message = "validation error: " + msg + ". " + s;
+        return out;
+      }
+      out.status = "pass";
+      out.message = msg;
+      return out;
+    }
+    if (!isnil(val->get("podSecurity"))) {  // validatePodSecurity (validation.go:535-566)
+      // getSpec (validation.go:481-532): typed decode of the whole object; a non-object on the way to the
+      // pod template is a decode error
+      std::string kind = nested_string(resource, {"kind"});
+      VP meta, spec;
+      bool derr = false;
+      auto step = [&](const VP& o, const char* k) -> VP {
+        if (derr || isnil(o)) return nullptr;
+        if (o->t != T::Obj) { derr = true; return nullptr; }
+        VP v = o->get(k);
+        if (!isnil(v) && v->t != T::Obj) { derr = true; return nullptr; }
+        return v;
+      };
+      static const std::set<std::string> ctl = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet", "ReplicationController"};
+      VP outerMeta = step(resource, "metadata");
+      if (ctl.count(kind)) {
+        VP tpl = step(step(resource, "spec"), "template");
+        meta = step(tpl, "metadata");
+        spec = step(tpl, "spec");
+      } else if (kind == "CronJob") {
+        VP jt = step(step(resource, "spec"), "jobTemplate");
+        meta = step(jt, "metadata");
+        spec = step(step(step(jt, "spec"), "template"), "spec");
+      } else if (kind == "Pod") {
+        meta = outerMeta;
+        spec = step(resource, "spec");
+      } else {
+        out.status = "panic";
+        out.message = "nil pod spec";
+        return out;
+      }
+      if (derr) { out.status = "error"; out.message = "Error while getting new resource: json: cannot unmarshal"; out.message_unpinned = true; return out; }
+      VP ps = val->get("podSecurity");
+      PSSEval ev = pss_evaluate(ps, meta, spec, outerMeta);
+      if (!ev.decode_error.empty()) { out.status = "error"; out.message = "Error while getting new resource: " + ev.decode_error; out.message_unpinned = true; return out; }
+      if (!ev.ok) { out.status = "error"; out.message = ev.error; out.message_unpinned = true; return out; }
+      out.pss_checks = ev.checks;
+      out.message_unpinned = ev.order_nondeterministic;
+      std::string level = oj::get_str(ps, "level"), version = oj::get_str(ps, "version");
+      if (ev.allowed) { out.status = "pass"; out.message = "Validation rule '" + out.name + "' passed."; return out; }
+      out.status = "fail";
+      out.message = "Validation rule '" + out.name + "' failed. It violates PodSecurity \"" + level + ":" + version + "\": " +
+                    format_checks_print(ev.checks);
+      return out;
+    }
+  } catch (RefPanic& p) {
+    out.status = "panic";
+    out.message = p.what;
+    return out;
+  }
+  out.status = "none";  // "invalid validation rule": no response
+  return out;
+}
+
+static bool rule_has_validate(const VP& rule) {
+  VP v = rule->get("validate");
+  return v && v->t == T::Obj && !v->o.empty();
+}
+
+// Validate (validation.go:39-183) for one policy and one resource
+PolicyResult validate_policy(const VP& policy, const VP& resource, const std::map<std::string, std::string>& nsLabels) {
+  PolicyResult pr;
+  pr.name = nested_string(policy, {"metadata", "name"});
+  std::string kind = oj::get_str(policy, "kind");
+  if (kind == "Policy") {  // namespaced policy filter (validation.go:124-132)
+    std::string pns = nested_string(policy, {"metadata", "namespace"});
+    std::string rns = nested_string(resource, {"metadata", "namespace"});
+    if (rns != pns || rns.empty()) { pr.namespace_skipped = true; return pr; }
+  }
+  VP spec = policy->get("spec");
+  bool applyOne = oj::get_str(spec, "applyRules") == "One";
+  int applied = 0;
+  for (auto& rule : compute_rules(policy)) {
+    if (!rule_has_validate(rule) && !has_nonempty(rule, "verifyImages")) continue;
+    bool nd = false;
+    bool m = matches_resource_description(rule, resource, nsLabels, &nd);
+    if (!m) m = matches_resource_description(rule, nullptr, nsLabels, &nd);  // OldResource retry (validation.go:606)
+    if (!m) continue;
+    RuleResult rr = validate_rule(rule, resource);
+    rr.nondeterministic |= nd;
+    if (rr.status == "none") continue;
+    if (rr.status == "pass" || rr.status == "fail") applied++;
+    pr.rules.push_back(rr);
+    if (applyOne && applied > 0) break;
+    if (rr.status == "unsupported" && applyOne) { pr.truncated_unknown = true; break; }
+  }
+  return pr;
+}
+
+}  // namespace orc

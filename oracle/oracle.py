@@ -1,0 +1,117 @@
+"""ORACLE — test infrastructure only.
+
+ctypes wrapper over oracle/liboracle.so, the CPU restatement of the reference validate path
+(see oracle/*.cpp headers for the reference file:line each function follows).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker. The product (kyverno_amd/, libkyvgpu.so) never loads it.
+"""
+import ctypes
+import json
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        L.oracle_free.argtypes = [ctypes.c_void_p]
+        for name in ("oracle_match_pattern", "oracle_pss", "oracle_validate", "oracle_compute_rules"):
+            getattr(L, name).restype = ctypes.c_void_p
+        L.oracle_format_float.restype = ctypes.c_void_p
+        L.oracle_format_float.argtypes = [ctypes.c_double, ctypes.c_int]
+        L.oracle_duration.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)]
+        L.oracle_validate_batch.restype = ctypes.c_longlong
+        L.oracle_validate_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
+        _lib = L
+    return _lib
+
+
+def _s(x):
+    if isinstance(x, str):
+        return x.encode()
+    if isinstance(x, bytes):
+        return x
+    return json.dumps(x).encode()
+
+
+def _take(ptr):
+    L = lib()
+    try:
+        return ctypes.string_at(ptr).decode()
+    finally:
+        L.oracle_free(ptr)
+
+
+def wildcard(pattern, text):
+    return bool(lib().oracle_wildcard(_s(pattern), _s(text)))
+
+
+def pattern_validate(value, pattern):
+    """value/pattern: JSON text or python objects."""
+    r = lib().oracle_pattern_validate(_s(value), _s(pattern))
+    if r < 0:
+        raise ValueError("bad json")
+    return bool(r)
+
+
+def quantity_cmp(a, b):
+    return lib().oracle_quantity_cmp(_s(a), _s(b))
+
+
+def duration(s):
+    v = ctypes.c_longlong(0)
+    ok = lib().oracle_duration(_s(s), ctypes.byref(v))
+    return v.value if ok else None
+
+
+def format_float(f, kind):
+    return _take(lib().oracle_format_float(f, {"E": 0, "g": 1, "f": 2, "json": 3}[kind]))
+
+
+def match_pattern(resource, pattern):
+    return json.loads(_take(lib().oracle_match_pattern(_s(resource), _s(pattern))))
+
+
+def pss(rule, pod):
+    return json.loads(_take(lib().oracle_pss(_s(rule), _s(pod))))
+
+
+def compute_rules(policy):
+    return json.loads(_take(lib().oracle_compute_rules(_s(policy))))
+
+
+def rule_matches(rule, resource, ns_labels=None):
+    r = lib().oracle_rule_matches(_s(rule), _s(resource) if resource is not None else b"",
+                                  _s(ns_labels) if ns_labels is not None else b"")
+    if r < 0:
+        raise ValueError("bad json")
+    return bool(r)
+
+
+def validate(policies, resource, ns_labels=None):
+    out = json.loads(_take(lib().oracle_validate(_s(policies), _s(resource),
+                                                 _s(ns_labels) if ns_labels is not None else b"")))
+    if isinstance(out, dict) and "exception" in out:
+        raise ValueError(out["exception"])
+    return out
+
+
+def validate_batch(policies, resources, ns_labels=None, threads=1):
+    counts = (ctypes.c_longlong * 5)()
+    secs = ctypes.c_double(0)
+    n = lib().oracle_validate_batch(_s(policies), _s(resources), _s(ns_labels) if ns_labels else b"",
+                                    threads, counts, ctypes.byref(secs))
+    return n, list(counts), secs.value

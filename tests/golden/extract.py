@@ -1,0 +1,340 @@
+#!/usr/bin/env python3
+"""Golden-vector extractor (test infrastructure).
+
+Reads the reference's own Go test sources and YAML fixtures AS TEXT (nothing from the reference is
+executed or imported) and writes small JSON fixtures next to this script:
+
+  wildcard.json      pkg/utils/wildcard/match_test.go            (go-wildcard v1.0.3 semantics)
+  pattern_leaf.json  pkg/engine/pattern/pattern_test.go           (leaf comparison semantics)
+  validate_walk.json pkg/engine/validate/validate_test.go         (pattern walk: paths, skip/pass)
+  engine.json        pkg/engine/validation_test.go                (end-to-end statuses + messages)
+  pss.json           pkg/pss/evaluate_test.go                     (PSS verdicts)
+  cli.json           test/cli/test/*/kyverno-test.yaml + inputs   (CLI `kyverno test` results)
+  best_practices.json test/best_practices/*.yaml                  (C1 / C3 policy set)
+  chart_restricted.json charts/kyverno-policies/templates/**      (hand-rendered PSS restricted profile)
+
+Usage: python tests/golden/extract.py [/root/reference]
+"""
+import ast
+import glob
+import json
+import os
+import re
+import sys
+
+import yaml
+
+REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def read(p):
+    with open(os.path.join(REF, p), encoding="utf-8") as f:
+        return f.read()
+
+
+def write(name, data):
+    with open(os.path.join(OUT, name), "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    print(f"{name}: {len(data)} records")
+
+
+def go_unquote(s):
+    """Go interpreted string literal (with quotes) -> str."""
+    return ast.literal_eval(s)
+
+
+def functions(src):
+    """split Go source into (name, body) for top-level funcs."""
+    out = []
+    for m in re.finditer(r"^func (\w+)\(", src, re.M):
+        start = m.start()
+        nxt = re.search(r"^func \w+\(", src[m.end():], re.M)
+        end = m.end() + nxt.start() if nxt else len(src)
+        out.append((m.group(1), src[start:end]))
+    return out
+
+
+# ---------------------------------------------------------------- wildcard
+def extract_wildcard():
+    src = read("pkg/utils/wildcard/match_test.go")
+    recs = []
+    for m in re.finditer(r'pattern:\s*("(?:[^"\\]|\\.)*"),\s*text:\s*("(?:[^"\\]|\\.)*"),\s*matched:\s*(true|false)', src):
+        recs.append({"pattern": go_unquote(m.group(1)), "text": go_unquote(m.group(2)), "matched": m.group(3) == "true"})
+    src2 = read("pkg/utils/match/name_test.go") if os.path.exists(os.path.join(REF, "pkg/utils/match/name_test.go")) else ""
+    write("wildcard.json", recs)
+
+
+# ---------------------------------------------------------------- pattern leaf
+GO_LIT = r'("(?:[^"\\]|\\.)*"|-?\d+\.\d+|-?\d+|true|false|nil|\w+)'
+OPS = {"operator.Equal": "", "operator.NotEqual": "!", "operator.More": ">", "operator.Less": "<",
+       "operator.MoreEqual": ">=", "operator.LessEqual": "<="}
+
+
+def go_value(tok, env):
+    if tok.startswith('"'):
+        return {"json": json.dumps(go_unquote(tok))}
+    if tok in ("true", "false"):
+        return {"json": tok}
+    if tok == "nil":
+        return {"json": "null"}
+    if re.fullmatch(r"-?\d+\.\d+", tok):
+        return {"json": tok}  # float64 (decimal point kept -> float)
+    if re.fullmatch(r"-?\d+", tok):
+        return {"json": tok}  # Go int
+    if tok in env:
+        return env[tok]
+    return None
+
+
+def extract_pattern_leaf():
+    src = read("pkg/engine/pattern/pattern_test.go")
+    recs = []
+    for fname, body in functions(src):
+        env = {}
+        raws = dict(re.findall(r"(\w+) := \[\]byte\(`(.*?)`\)", body, re.S))
+        for line in body.splitlines():
+            line = line.strip()
+            m = re.match(r'(\w+) :?= ("(?:[^"\\]|\\.)*")$', line)
+            if m:
+                env[m.group(1)] = {"json": json.dumps(go_unquote(m.group(2)))}
+                continue
+            m = re.match(r"assert\.Assert\(t, (!?)(\w+)\(logger, (.*)\)\)$", line)
+            if not m:
+                continue
+            neg, fn, args = m.group(1) == "!", m.group(2), m.group(3)
+            if fn == "Validate" and 'value["key"]' in args:
+                v = json.loads(raws["rawValue"])["key"]
+                p = json.loads(raws["rawPattern"])["key"]
+                recs.append({"test": fname, "fn": "Validate", "value": json.dumps(v), "value_float": True,
+                             "pattern": json.dumps(p), "expect": not neg})
+                continue
+            toks = [t.strip() for t in re.findall(r'"(?:[^"\\]|\\.)*"|[^,]+', args)]
+            toks = [t for t in toks if t]
+            if fn in ("Validate", "validateFloatPattern", "validateStringPattern", "validateStringPatterns"):
+                v, p = go_value(toks[0], env), go_value(toks[1], env)
+                if v is None or p is None:
+                    continue
+                recs.append({"test": fname, "fn": fn, "value": v["json"], "pattern": p["json"], "expect": not neg})
+            elif fn == "validateNilPattern":
+                v = go_value(toks[0], env)
+                recs.append({"test": fname, "fn": fn, "value": v["json"], "pattern": "null", "expect": not neg})
+            elif fn in ("validateString", "compareString"):
+                v, p = go_value(toks[0], env), go_value(toks[1], env)
+                op = OPS[toks[2]]
+                recs.append({"test": fname, "fn": fn, "value": v["json"], "pattern": p["json"], "op": op, "expect": not neg})
+    write("pattern_leaf.json", recs)
+
+
+# ---------------------------------------------------------------- validate walk
+def extract_validate_walk():
+    src = read("pkg/engine/validate/validate_test.go")
+    recs = []
+    for fname, body in functions(src):
+        if fname.startswith("testMatchPattern"):
+            continue
+        if "testCases := []struct" in body:
+            for m in re.finditer(r'name:\s*"([^"]*)",\s*pattern:\s*\[\]byte\(`(.*?)`\),\s*resource:\s*\[\]byte\(`(.*?)`\),\s*status:\s*engineapi\.RuleStatus(\w+)', body, re.S):
+                recs.append({"test": f"{fname}/{m.group(1)}", "entry": "MatchPattern", "pattern": m.group(2),
+                             "resource": m.group(3), "status": m.group(4).lower()})
+            continue
+        if "SubstituteAll" in body or "$(" in body:
+            continue  # reference/variable tests -> CPU fallback path, not the GPU walk
+        raws = dict(re.findall(r"(\w+) := \[\]byte\(`(.*?)`\)", body, re.S))
+        if "rawPattern" not in raws:
+            continue
+        res_key = next((k for k in ("rawMap", "rawResource", "rawArray") if k in raws), None)
+        if res_key is None:
+            continue
+        call = re.search(r"(validateMap|validateResourceElement|validateArray|MatchPattern)\(", body)
+        if not call:
+            continue
+        mpath = re.search(r'assert\.Equal\(t, path, "([^"]*)"\)', body)
+        errnil = None
+        if re.search(r"assert\.Assert\(t, err != nil\)", body):
+            errnil = False
+        elif re.search(r"assert\.(NilError\(t, err\)|Assert\(t, err == nil\))", body[call.start():]):
+            errnil = True
+        recs.append({"test": fname, "entry": call.group(1), "pattern": raws["rawPattern"], "resource": raws[res_key],
+                     "path": mpath.group(1) if mpath else None, "err_nil": errnil})
+    write("validate_walk.json", recs)
+
+
+# ---------------------------------------------------------------- engine (validation_test.go)
+def extract_engine():
+    src = read("pkg/engine/validation_test.go")
+    recs = []
+    for fname, body in functions(src):
+        raws = dict(re.findall(r"(\w+) := \[\]byte\(`(.*?)`\)", body, re.S))
+        if "rawPolicy" in raws and "rawResource" in raws and "testCases" not in body:
+            m = re.search(r"msgs := \[\]string\{(.*?)\}\n", body, re.S)
+            msgs = [go_unquote(x) for x in re.findall(r'"(?:[^"\\]|\\.)*"', m.group(1))] if m else None
+            succ = None
+            if re.search(r"assert\.Assert\(t, !er\.IsSuccessful\(\)\)", body):
+                succ = False
+            elif re.search(r"assert\.Assert\(t, er\.IsSuccessful\(\)\)", body):
+                succ = True
+            if msgs is None and succ is None:
+                continue
+            recs.append({"test": fname, "policy": raws["rawPolicy"], "resource": raws["rawResource"],
+                         "msgs": msgs, "successful": succ})
+        elif "testCases" in body and "expectedFailed" in body:
+            pol = raws.get("rawPolicy")
+            for m in re.finditer(r'description:\s*"([^"]*)",\s*rawPolicy:\s*(\w+),\s*rawResource:\s*\[\]byte\(`(.*?)`\),\s*expected(\w+):\s*true', body, re.S):
+                recs.append({"test": f"{fname}/{m.group(1)}", "policy": raws.get(m.group(2), pol), "resource": m.group(3),
+                             "msgs": None, "expect": m.group(4).lower()})
+    write("engine.json", recs)
+
+
+# ---------------------------------------------------------------- PSS
+def extract_pss():
+    src = read("pkg/pss/evaluate_test.go")
+    recs = []
+    for m in re.finditer(r'name:\s*"([^"]*)",\s*rawRule:\s*\[\]byte\(`(.*?)`\),\s*rawPod:\s*\[\]byte\(`(.*?)`\),\s*allowed:\s*(true|false)', src, re.S):
+        recs.append({"name": m.group(1), "rule": m.group(2), "pod": m.group(3), "allowed": m.group(4) == "true"})
+    write("pss.json", recs)
+
+
+# ---------------------------------------------------------------- YAML helpers
+def yaml_docs(path):
+    with open(path, encoding="utf-8") as f:
+        return [d for d in yaml.safe_load_all(f) if d is not None]
+
+
+def normalize_numbers(x):
+    """sigs.k8s.io/yaml converts YAML to JSON through json.Marshal: integral float64 values < 1e21 are
+    written without a fraction and then decode as int64 in unstructured objects."""
+    if isinstance(x, dict):
+        return {str(k): normalize_numbers(v) for k, v in x.items()}
+    if isinstance(x, list):
+        return [normalize_numbers(v) for v in x]
+    if isinstance(x, float) and x == int(x) and abs(x) < 1e21:
+        return int(x)
+    return x
+
+
+def json_safe(x):
+    return json.loads(json.dumps(x, default=str))
+
+
+# ---------------------------------------------------------------- CLI goldens
+def extract_cli():
+    recs = []
+    for d in sorted(glob.glob(os.path.join(REF, "test/cli/test/*"))):
+        kt = os.path.join(d, "kyverno-test.yaml")
+        if not os.path.exists(kt):
+            continue
+        try:
+            spec = yaml_docs(kt)[0]
+        except Exception:
+            continue
+        if spec.get("variables") or spec.get("userinfo"):
+            continue
+        policies, resources = [], []
+        ok = True
+        for p in spec.get("policies", []):
+            fp = os.path.join(d, p)
+            if not os.path.exists(fp):
+                ok = False
+                break
+            policies += [json_safe(x) for x in yaml_docs(fp)]
+        for r in spec.get("resources", []):
+            fp = os.path.join(d, r)
+            if not os.path.exists(fp):
+                ok = False
+                break
+            resources += [json_safe(normalize_numbers(x)) for x in yaml_docs(fp)]
+        if not ok:
+            continue
+        results = []
+        for res in spec.get("results", []):
+            names = res.get("resources") or ([res["resource"]] if res.get("resource") else [])
+            for n in names:
+                results.append({"policy": res.get("policy"), "rule": res.get("rule"), "resource": n,
+                                "kind": res.get("kind"), "result": res.get("result"),
+                                "namespace": res.get("namespace")})
+        recs.append({"dir": os.path.basename(d), "policies": policies, "resources": resources, "results": results})
+    write("cli.json", recs)
+
+
+def extract_best_practices():
+    recs = []
+    for p in sorted(glob.glob(os.path.join(REF, "test/best_practices/*.yaml"))):
+        for doc in yaml_docs(p):
+            if isinstance(doc, dict) and doc.get("kind") in ("ClusterPolicy", "Policy"):
+                recs.append({"file": os.path.basename(p), "policy": json_safe(doc)})
+    write("best_practices.json", recs)
+
+
+# ---------------------------------------------------------------- chart (hand-rendered)
+def render_chart_template(text, name, level):
+    """Render charts/kyverno-policies templates with values.yaml defaults (podSecurityStandard=<level>,
+    validationFailureAction=audit, background=true, failurePolicy=Fail, no excludes/preconditions,
+    autogenControllers empty). Only the constructs these templates use are handled."""
+    def cond(expr):
+        expr = expr.strip()
+        if expr.startswith("with"):
+            return False  # every `with` reads an empty value (excludes, overrides, autogenControllers, ...)
+        if expr.startswith("if eq (include"):
+            return True  # the policy is part of the selected profile
+        if expr.startswith("if .Values.podSecuritySeverity"):
+            return True
+        return False  # $preconditionsN, .all: empty
+
+    out = []
+    stack = []  # list of [active_now, parent_active, taken]
+    active = True
+    for line in text.splitlines():
+        s = line.strip()
+        m = re.fullmatch(r"\{\{-?\s*(.*?)\s*-?\}\}", s)
+        if m and not s.startswith("{{`"):
+            d = m.group(1)
+            if d.startswith("if ") or d.startswith("with "):
+                c = cond(d)
+                stack.append([active, c])
+                active = active and c
+            elif d.startswith("else"):
+                parent, c = stack[-1]
+                stack[-1][1] = not c
+                active = parent and not c
+            elif d.startswith("end"):
+                parent, _ = stack.pop()
+                active = parent
+            continue  # $name :=, include, toYaml ... lines produce nothing with empty values
+        if not active:
+            continue
+        if "labels: {{ include" in line:
+            continue
+        line = line.replace("{{ $name }}", name)
+        line = line.replace("{{ .Values.background }}", "true")
+        line = line.replace("{{ .Values.failurePolicy }}", "Fail")
+        line = line.replace("{{ .Values.validationFailureAction }}", "audit")
+        line = line.replace("{{ .Values.podSecuritySeverity | quote }}", '"medium"')
+        line = line.replace("{{ .Values.podSecuritySeverity }}", "medium")
+        line = line.replace("{{`{{`}}", "{{").replace("{{`}}`}}", "}}")
+        line = re.sub(r"\{\{`(.*?)`\}\}", r"\1", line)
+        out.append(line)
+    return yaml.safe_load("\n".join(out))
+
+
+def extract_chart():
+    recs = []
+    base = os.path.join(REF, "charts/kyverno-policies/templates")
+    for level_dir in ("baseline", "restricted"):
+        for p in sorted(glob.glob(os.path.join(base, level_dir, "*.yaml"))):
+            text = open(p, encoding="utf-8").read()
+            name = re.search(r'\$name := "([^"]+)"', text).group(1)
+            doc = render_chart_template(text, name, "restricted")
+            recs.append({"file": f"{level_dir}/{os.path.basename(p)}", "policy": json_safe(doc)})
+    write("chart_restricted.json", recs)
+
+
+if __name__ == "__main__":
+    extract_wildcard()
+    extract_pattern_leaf()
+    extract_validate_walk()
+    extract_engine()
+    extract_pss()
+    extract_cli()
+    extract_best_practices()
+    extract_chart()
