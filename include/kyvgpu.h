@@ -1,0 +1,152 @@
+/*
+ * kyvgpu — C ABI of the MI355X batched Kyverno validate evaluator (libkyvgpu.so).
+ *
+ * Drop-in boundary for the reference's validate hot path. Each entry point names the reference
+ * interface it replaces (paths relative to the reference repository):
+ *
+ *   kyv_ruleset_compile  replaces the per-call policy preparation inside engine.Validate:
+ *                        autogen.ComputeRules (pkg/autogen/autogen.go:280), rule.DeepCopy + GetPattern
+ *                        JSON decode (pkg/engine/validation.go:225-240, api/kyverno/v1/common_types.go:423),
+ *                        anchor/operator parsing (pkg/engine/anchor/anchor.go:37, operator/operator.go:35).
+ *                        Done once per policy set instead of once per (policy, resource).
+ *   kyv_batch_build      replaces the per-resource PolicyContext/JSON-context setup of the background
+ *                        scanner and CLI (pkg/controllers/report/utils/scanner.go:87-100,
+ *                        cmd/cli/kubectl-kyverno/utils/common/common.go:434-462): N resources at once,
+ *                        flattened into device node tables.
+ *   kyv_eval             replaces the loop  for policy { for rule { matches(); validate() } }  of
+ *                        engine.Validate (pkg/engine/validation.go:39-183) for every (resource, rule)
+ *                        pair of the batch: match/exclude (pkg/engine/utils.go:185-256), pattern /
+ *                        anyPattern (validation.go:618-702 -> pkg/engine/validate/validate.go:31) and
+ *                        podSecurity (validation.go:535-566 -> pkg/pss/evaluate.go:83).
+ *   kyv_results_*        the per-rule part of engineapi.RuleResponse (pkg/engine/api/ruleresponse.go:23):
+ *                        status, message, failing path; plus the summary counters used by
+ *                        pkg/utils/report/results.go:38 (CalculateSummary).
+ *
+ * Rules that need the reference CPU engine (variables/JMESPath, context, preconditions, deny, foreach,
+ * image verification) are classified at compile time; their pairs report KYV_ST_FALLBACK and the caller
+ * runs engine.Validate for them.
+ *
+ * Threading: a kyv_ruleset is immutable after compile and may be shared; batches and results are per
+ * call. No C++ exception crosses this ABI; failures return a non-zero code and kyv_last_error()
+ * (thread-local) describes them.
+ */
+#ifndef KYVGPU_H
+#define KYVGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KYV_ABI_VERSION 1u
+
+typedef struct kyv_ruleset kyv_ruleset;
+typedef struct kyv_batch kyv_batch;
+typedef struct kyv_results kyv_results;
+
+/* return codes */
+enum { KYV_OK = 0, KYV_EINVAL = 1, KYV_EPARSE = 2, KYV_EDEVICE = 3, KYV_EINTERNAL = 4, KYV_ERANGE = 5 };
+
+/* per (resource, rule) verdicts; KYV_ST_NONE = rule not applicable (no RuleResponse) */
+enum {
+  KYV_ST_NONE = 0,
+  KYV_ST_PASS = 1,
+  KYV_ST_FAIL = 2,
+  KYV_ST_SKIP = 3,
+  KYV_ST_ERROR = 4,
+  KYV_ST_FALLBACK = 5,   /* rule needs the reference CPU engine */
+  KYV_ST_PANIC = 6,      /* the reference would panic on this input */
+  KYV_ST_ND = 7          /* the reference result depends on Go map iteration order */
+};
+
+/* rule kinds */
+enum { KYV_RULE_PATTERN = 1, KYV_RULE_ANYPATTERN = 2, KYV_RULE_PSS = 3, KYV_RULE_FALLBACK = 4, KYV_RULE_PANIC = 5,
+       KYV_RULE_ERROR = 6 };
+
+enum { KYV_BACKEND_GPU = 0, KYV_BACKEND_CPU = 1 };
+enum { KYV_EVAL_NO_COPYBACK = 1u, KYV_EVAL_ACCOUNT_BYTES = 2u };
+
+typedef struct {
+  uint32_t abi_version;
+  uint32_t flags;
+} kyv_compile_opts;
+
+typedef struct {
+  uint32_t abi_version;
+  int32_t threads;       /* flattener threads (<=0: hardware concurrency) */
+} kyv_batch_opts;
+
+typedef struct {
+  uint32_t abi_version;
+  int32_t backend;       /* KYV_BACKEND_GPU (default). KYV_BACKEND_CPU only when explicitly requested. */
+  int32_t device;        /* HIP device ordinal */
+  int32_t iterations;    /* timed kernel launches (>=1); results are those of the last launch */
+  int32_t threads;       /* CPU backend threads */
+  uint32_t flags;        /* KYV_EVAL_NO_COPYBACK: keep verdicts on the device (timing);
+                            KYV_EVAL_ACCOUNT_BYTES (CPU backend): sum algorithmic bytes per pair */
+} kyv_eval_opts;
+
+typedef struct {
+  const char* name;      /* rule name (autogen names included) */
+  uint32_t policy;       /* policy index */
+  int32_t kind;          /* KYV_RULE_* */
+  const char* reason;    /* fallback / error reason, "" otherwise */
+} kyv_rule_info;
+
+typedef struct {
+  const char* name;
+  const char* namespace_;   /* "" for ClusterPolicy */
+  uint32_t first_rule;      /* compiled validate rules [first_rule, first_rule + nrules) */
+  uint32_t nrules;
+  int32_t apply_one;        /* spec.applyRules == One */
+  int32_t scored_false;     /* policies.kyverno.io/scored: "false" (fail -> warn in reports) */
+} kyv_policy_info;
+
+typedef struct {
+  uint64_t resources, nodes, strings, heap_bytes, device_bytes;
+} kyv_batch_stats;
+
+/* ---- ruleset: replaces per-call ComputeRules + pattern decoding ---- */
+int kyv_ruleset_compile(const char* policies_json, size_t len, const kyv_compile_opts* opts, kyv_ruleset** out);
+void kyv_ruleset_free(kyv_ruleset* rs);
+uint32_t kyv_ruleset_num_rules(const kyv_ruleset* rs);
+uint32_t kyv_ruleset_num_policies(const kyv_ruleset* rs);
+int kyv_ruleset_rule_info(const kyv_ruleset* rs, uint32_t rule, kyv_rule_info* out);
+int kyv_ruleset_policy_info(const kyv_ruleset* rs, uint32_t policy, kyv_policy_info* out);
+
+/* ---- batch: resources (JSON array or NDJSON) + namespace labels ({"ns": {"k": "v"}}) ---- */
+int kyv_batch_build(const kyv_ruleset* rs, const char* resources_json, size_t len, const char* ns_labels_json,
+                    size_t ns_len, const kyv_batch_opts* opts, kyv_batch** out);
+void kyv_batch_free(kyv_batch* b);
+uint32_t kyv_batch_num_resources(const kyv_batch* b);
+int kyv_batch_stats_get(const kyv_batch* b, kyv_batch_stats* out);
+
+/* ---- evaluation: engine.Validate over every (resource, rule) pair ---- */
+int kyv_eval(const kyv_ruleset* rs, const kyv_batch* b, const kyv_eval_opts* opts, kyv_results** out);
+void kyv_results_free(kyv_results* r);
+/* verdict bytes, rule-major: out[rule * nres + res]; low 3 bits = KYV_ST_*, high 5 bits = anyPattern
+ * alternative that passed (31 = none) */
+int kyv_results_status(const kyv_results* r, uint8_t* out, size_t cap);
+int64_t kyv_results_count(const kyv_results* r, int status);
+double kyv_results_kernel_ms(const kyv_results* r);
+/* CPU backend with KYV_EVAL_ACCOUNT_BYTES: algorithmic bytes of all pairs (header fields, distinct node rows,
+ * verdict, PSS mask, failure records); 0 otherwise */
+uint64_t kyv_results_alg_bytes(const kyv_results* r);
+/* RuleResponse.Message for one pair; returns the full length (may exceed cap), -1 if unavailable */
+int64_t kyv_results_message(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,
+                            uint32_t rule, char* buf, size_t cap);
+/* failing path of a single-pattern FAIL ("" otherwise); returns the full length */
+int64_t kyv_results_path(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res, uint32_t rule,
+                         char* buf, size_t cap);
+/* PodSecurity rules: failing (check, version) slot mask after exclusions */
+uint32_t kyv_results_pss_mask(const kyv_results* r, const kyv_ruleset* rs, uint32_t res, uint32_t rule);
+
+const char* kyv_last_error(void);
+const char* kyv_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KYVGPU_H */

@@ -1,0 +1,101 @@
+"""ctypes binding of libkyvgpu.so (include/kyvgpu.h). This is the same binding a cgo shim declares."""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkyvgpu.so")
+
+KYV_ABI_VERSION = 1
+BACKEND_GPU, BACKEND_CPU = 0, 1
+EVAL_NO_COPYBACK = 1
+EVAL_ACCOUNT_BYTES = 2
+
+ST_NONE, ST_PASS, ST_FAIL, ST_SKIP, ST_ERROR, ST_FALLBACK, ST_PANIC, ST_ND = range(8)
+STATUS_NAMES = ["none", "pass", "fail", "skip", "error", "fallback", "panic", "nondeterministic"]
+RULE_KINDS = {1: "pattern", 2: "anyPattern", 3: "podSecurity", 4: "fallback", 5: "panic", 6: "error"}
+
+
+class CompileOpts(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class BatchOpts(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_uint32), ("threads", ctypes.c_int32)]
+
+
+class EvalOpts(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_uint32), ("backend", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("iterations", ctypes.c_int32), ("threads", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class RuleInfo(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("policy", ctypes.c_uint32), ("kind", ctypes.c_int32), ("reason", ctypes.c_char_p)]
+
+
+class PolicyInfo(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("namespace_", ctypes.c_char_p), ("first_rule", ctypes.c_uint32),
+                ("nrules", ctypes.c_uint32), ("apply_one", ctypes.c_int32), ("scored_false", ctypes.c_int32)]
+
+
+class BatchStats(ctypes.Structure):
+    _fields_ = [("resources", ctypes.c_uint64), ("nodes", ctypes.c_uint64), ("strings", ctypes.c_uint64),
+                ("heap_bytes", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64)]
+
+
+EXPORTS = [
+    "kyv_ruleset_compile", "kyv_ruleset_free", "kyv_ruleset_num_rules", "kyv_ruleset_num_policies",
+    "kyv_ruleset_rule_info", "kyv_ruleset_policy_info", "kyv_batch_build", "kyv_batch_free",
+    "kyv_batch_num_resources", "kyv_batch_stats_get", "kyv_eval", "kyv_results_free", "kyv_results_status",
+    "kyv_results_count", "kyv_results_kernel_ms", "kyv_results_alg_bytes", "kyv_results_message", "kyv_results_path",
+    "kyv_results_pss_mask", "kyv_last_error", "kyv_version",
+]
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree HIP library; fails loudly if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libkyvgpu.so not built: run `python -m kyverno_amd.build` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u32, i32, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int64
+    L.kyv_ruleset_compile.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(CompileOpts), ctypes.POINTER(vp)]
+    L.kyv_ruleset_free.argtypes = [vp]
+    L.kyv_ruleset_num_rules.argtypes = [vp]
+    L.kyv_ruleset_num_rules.restype = u32
+    L.kyv_ruleset_num_policies.argtypes = [vp]
+    L.kyv_ruleset_num_policies.restype = u32
+    L.kyv_ruleset_rule_info.argtypes = [vp, u32, ctypes.POINTER(RuleInfo)]
+    L.kyv_ruleset_policy_info.argtypes = [vp, u32, ctypes.POINTER(PolicyInfo)]
+    L.kyv_batch_build.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
+    L.kyv_batch_free.argtypes = [vp]
+    L.kyv_batch_num_resources.argtypes = [vp]
+    L.kyv_batch_num_resources.restype = u32
+    L.kyv_batch_stats_get.argtypes = [vp, ctypes.POINTER(BatchStats)]
+    L.kyv_eval.argtypes = [vp, vp, ctypes.POINTER(EvalOpts), ctypes.POINTER(vp)]
+    L.kyv_results_free.argtypes = [vp]
+    L.kyv_results_status.argtypes = [vp, ctypes.c_void_p, sz]
+    L.kyv_results_count.argtypes = [vp, i32]
+    L.kyv_results_count.restype = i64
+    L.kyv_results_kernel_ms.argtypes = [vp]
+    L.kyv_results_kernel_ms.restype = ctypes.c_double
+    L.kyv_results_alg_bytes.argtypes = [vp]
+    L.kyv_results_alg_bytes.restype = ctypes.c_uint64
+    L.kyv_results_message.argtypes = [vp, vp, vp, u32, u32, ctypes.c_char_p, sz]
+    L.kyv_results_message.restype = i64
+    L.kyv_results_path.argtypes = [vp, vp, vp, u32, u32, ctypes.c_char_p, sz]
+    L.kyv_results_path.restype = i64
+    L.kyv_results_pss_mask.argtypes = [vp, vp, u32, u32]
+    L.kyv_results_pss_mask.restype = u32
+    L.kyv_last_error.restype = ctypes.c_char_p
+    L.kyv_version.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError("kyvgpu error %d: %s" % (rc, lib().kyv_last_error().decode(errors="replace")))

@@ -1,0 +1,472 @@
+// Flattener: resource JSON -> columnar node tables + interned dictionary (host, multithreaded).
+//
+// Reference accessors restated for the per-resource header (k8s.io/apimachinery unstructured, used by
+// pkg/engine/utils.go:71-160): GetKind/GetName/GetGenerateName/GetNamespace (NestedString -> "" unless a
+// string), GetLabels/GetAnnotations (NestedStringMap -> nil unless a map of strings), GroupVersionKind
+// (ParseGroupVersion; more than one '/' -> empty GVK).
+#include <algorithm>
+#include <atomic>
+#include <thread>
+
+#include "kyv_host.h"
+
+namespace kyv {
+using pj::T;
+using pj::Value;
+
+Batch::~Batch() {}
+
+namespace {
+
+bool magic(const std::string& s) {
+  return s.find("negation anchor matched in resource") != std::string::npos ||
+         s.find("conditional anchor mismatch") != std::string::npos || s.find("global anchor mismatch") != std::string::npos;
+}
+
+bool is_anchor_key(const std::string& raw, const char* tag) {  // key that anchor.Parse() maps onto tag
+  std::string s = pj::go_trim_space(raw);
+  if (s.size() < 3 || s.back() != ')') return false;
+  size_t p = (s[0] == '+' || s[0] == '<' || s[0] == '=' || s[0] == 'X' || s[0] == '^') ? 1 : 0;
+  if (s[p] != '(') return false;
+  return s.substr(p + 1, s.size() - p - 2) == tag;
+}
+
+// chunk-local interning, remapped to global ids after the parallel phase
+struct Chunk {
+  std::vector<std::string> strs;
+  std::unordered_map<std::string, uint32_t> ids;
+  std::vector<Node> nodes;
+  std::vector<ResHeader> hdr;
+  std::vector<FloatAux> faux;
+  std::vector<uint32_t> ns_names;  // local sid of namespace per resource
+  std::string err;
+  uint32_t local(const std::string& s) {
+    auto it = ids.find(s);
+    if (it != ids.end()) return it->second;
+    uint32_t id = (uint32_t)strs.size();
+    strs.push_back(s);
+    ids.emplace(s, id);
+    return id;
+  }
+};
+
+struct Emitter {
+  Chunk& ch;
+  std::vector<Node> out;
+  bool magicflag = false;
+  uint32_t put_children_map(const Value& v) {
+    uint32_t first = (uint32_t)out.size();
+    out.resize(first + v.o.size());
+    for (size_t k = 0; k < v.o.size(); k++) {
+      if (magic(v.o[k].first)) magicflag = true;
+      fill(first + (uint32_t)k, v.o[k].second, (ch.local(v.o[k].first) << 4));
+    }
+    return first;
+  }
+  void fill(uint32_t idx, const Value& v, uint32_t keybits) {
+    Node n{};
+    switch (v.t) {
+      case T::Null: n.tk = N_NULL; break;
+      case T::Bool: n.tk = v.b ? N_TRUE : N_FALSE; n.a = v.b; break;
+      case T::Int: {
+        n.tk = N_INT;
+        uint64_t u = (uint64_t)v.i;
+        n.a = (uint32_t)u;
+        n.b = (uint32_t)(u >> 32);
+        n.c = ch.local(std::to_string(v.i));
+        break;
+      }
+      case T::Float: {
+        n.tk = N_FLOAT;
+        uint64_t u = __builtin_bit_cast(uint64_t, v.f);
+        n.a = (uint32_t)u;
+        n.b = (uint32_t)(u >> 32);
+        n.c = (uint32_t)ch.faux.size();
+        ch.faux.push_back(FloatAux{ch.local(pj::go_fmt_E(v.f)), ch.local(pj::go_fmt_f6(v.f))});
+        break;
+      }
+      case T::Str:
+        n.tk = N_STR;
+        n.a = ch.local(v.s);
+        if (magic(v.s)) magicflag = true;
+        break;
+      case T::Obj: {
+        n.tk = N_MAP;
+        n.b = (uint32_t)v.o.size();
+        out[idx] = n;  // reserve before recursion (out may grow)
+        uint32_t first = put_children_map(v);
+        out[idx].a = first;
+        out[idx].tk |= keybits;
+        return;
+      }
+      case T::Arr: {
+        n.tk = N_ARR;
+        n.b = (uint32_t)v.a.size();
+        out[idx] = n;
+        uint32_t first = (uint32_t)out.size();
+        out.resize(first + v.a.size());
+        for (size_t k = 0; k < v.a.size(); k++) fill(first + (uint32_t)k, v.a[k], (uint32_t)k << 4);
+        out[idx].a = first;
+        out[idx].tk |= keybits;
+        return;
+      }
+    }
+    n.tk |= keybits;
+    out[idx] = n;
+  }
+};
+
+const Value* nested(const Value& o, std::initializer_list<const char*> path) {
+  const Value* cur = &o;
+  for (const char* f : path) {
+    if (cur->t != T::Obj) return nullptr;
+    cur = cur->get(f);
+    if (!cur) return nullptr;
+  }
+  return cur;
+}
+std::string nested_str(const Value& o, std::initializer_list<const char*> path) {
+  const Value* v = nested(o, path);
+  return v && v->t == T::Str ? v->s : "";
+}
+
+// relative node index of a string map at metadata.<key> (NestedStringMap), NONE otherwise
+uint32_t string_map_node(const std::vector<Node>& R, uint32_t meta, uint32_t keysid_local, const Value* v) {
+  if (!v || v->t != T::Obj) return NONE;
+  for (auto& kv : v->o) if (kv.second.t != T::Str) return NONE;
+  const Node& m = R[meta];
+  for (uint32_t i = 0; i < m.b; i++)
+    if (node_key(R[m.a + i]) == keysid_local) return m.a + i;
+  return NONE;
+}
+
+void flatten_one(Chunk& ch, const Value& doc) {
+  Emitter em{ch};
+  em.out.resize(1);
+  em.fill(0, doc, 0);
+  ResHeader h{};
+  h.root = (uint32_t)ch.nodes.size();
+  h.nnodes = (uint32_t)em.out.size();
+  std::string kind = nested_str(doc, {"kind"});
+  h.kind = ch.local(kind);
+  std::string av = nested_str(doc, {"apiVersion"});
+  size_t sl = std::count(av.begin(), av.end(), '/');
+  std::string g, ver;
+  bool gvok = true;
+  if (av.empty() || av == "/") {}
+  else if (sl == 0) ver = av;
+  else if (sl == 1) { g = av.substr(0, av.find('/')); ver = av.substr(av.find('/') + 1); }
+  else gvok = false;
+  h.gvk_kind = ch.local(gvok ? kind : "");
+  h.group = ch.local(g);
+  h.version = ch.local(ver);
+  h.gv = ch.local(g.empty() ? ver : g + "/" + ver);
+  h.name = ch.local(nested_str(doc, {"metadata", "name"}));
+  h.gen_name = ch.local(nested_str(doc, {"metadata", "generateName"}));
+  std::string ns = nested_str(doc, {"metadata", "namespace"});
+  h.ns = ch.local(ns);
+  h.labels = h.ann = NONE;
+  h.nsl = NONE;
+  h.flags = em.magicflag ? RF_MAGIC : 0;
+  const Value* meta = nested(doc, {"metadata"});
+  if (meta && meta->t == T::Obj) {
+    uint32_t mnode = NONE;
+    const Node& root = em.out[0];
+    uint32_t msid = ch.local("metadata");
+    for (uint32_t i = 0; i < root.b; i++) if (node_key(em.out[root.a + i]) == msid) mnode = root.a + i;
+    if (mnode != NONE) {
+      h.labels = string_map_node(em.out, mnode, ch.local("labels"), meta->get("labels"));
+      h.ann = string_map_node(em.out, mnode, ch.local("annotations"), meta->get("annotations"));
+    }
+  }
+  // any map key directly under a "metadata" map that anchor.Parse() resolves to labels/annotations
+  std::vector<const Value*> stack{&doc};
+  while (!stack.empty()) {
+    const Value* v = stack.back();
+    stack.pop_back();
+    if (v->t == T::Obj) {
+      for (auto& kv : v->o) {
+        if (kv.first == "metadata" && kv.second.t == T::Obj)
+          for (auto& m2 : kv.second.o)
+            if (is_anchor_key(m2.first, "labels") || is_anchor_key(m2.first, "annotations")) h.flags |= RF_ANCHORISH;
+        stack.push_back(&kv.second);
+      }
+    } else if (v->t == T::Arr) {
+      for (auto& e : v->a) stack.push_back(&e);
+    }
+  }
+  ch.hdr.push_back(h);
+  ch.ns_names.push_back(h.ns);
+  ch.nodes.insert(ch.nodes.end(), em.out.begin(), em.out.end());
+}
+
+// split a JSON array / NDJSON buffer into document byte ranges
+std::vector<std::pair<size_t, size_t>> split_docs(const char* p, size_t n) {
+  std::vector<std::pair<size_t, size_t>> out;
+  size_t i = 0;
+  while (i < n && isspace((unsigned char)p[i])) i++;
+  bool array = i < n && p[i] == '[';
+  if (array) i++;
+  while (i < n) {
+    while (i < n && (isspace((unsigned char)p[i]) || (array && p[i] == ','))) i++;
+    if (i >= n || (array && p[i] == ']')) break;
+    size_t st = i;
+    int depth = 0;
+    bool in_str = false;
+    for (; i < n; i++) {
+      char c = p[i];
+      if (in_str) {
+        if (c == '\\') i++;
+        else if (c == '"') in_str = false;
+        continue;
+      }
+      if (c == '"') in_str = true;
+      else if (c == '{' || c == '[') depth++;
+      else if (c == '}' || c == ']') {
+        depth--;
+        if (depth == 0) { i++; break; }
+      } else if (depth == 0 && (c == ',' || c == '\n')) break;
+    }
+    out.push_back({st, i - st});
+  }
+  return out;
+}
+
+}  // namespace
+
+void derive_strings(Batch& b, size_t from, int threads) {
+  size_t n = b.dict.strs.size();
+  b.str_flags.resize(n);
+  b.str_dur.resize(n);
+  b.str_qty.resize(2 * n);
+  b.str_f64.resize(n);
+  std::atomic<size_t> next{from};
+  auto work = [&]() {
+    for (;;) {
+      size_t s0 = next.fetch_add(4096);
+      if (s0 >= n) break;
+      size_t s1 = std::min(n, s0 + 4096);
+      for (size_t s = s0; s < s1; s++) {
+        const std::string& x = b.dict.strs[s];
+        uint32_t f = 0;
+        bool ascii = true;
+        for (unsigned char c : x) if (c >= 0x80) { ascii = false; break; }
+        if (ascii) f |= SF_ASCII;
+        int64_t d;
+        if (pj::go_parse_duration(x, &d)) { f |= SF_DUR; b.str_dur[s] = d; } else b.str_dur[s] = 0;
+        int64_t lo, hi;
+        int q = pj::go_parse_quantity(x, &lo, &hi);
+        if (q == 1) { f |= SF_QTY; b.str_qty[2 * s] = lo; b.str_qty[2 * s + 1] = hi; }
+        else { b.str_qty[2 * s] = 0; b.str_qty[2 * s + 1] = 0; if (q == 2) f |= SF_QTY_BIG; }
+        double fv;
+        if (pj::go_parse_float(x, &fv)) { f |= SF_FLOAT; b.str_f64[s] = fv; } else b.str_f64[s] = 0;
+        // label key / value validity (apimachinery validation.IsQualifiedName / IsValidLabelValue)
+        auto qn = [](const std::string& nm) {
+          if (nm.empty() || nm.size() > 63) return false;
+          auto an = [](char c) { return isalnum((unsigned char)c) != 0; };
+          if (!an(nm.front()) || !an(nm.back())) return false;
+          for (char c : nm) if (!(an(c) || c == '-' || c == '_' || c == '.')) return false;
+          return true;
+        };
+        auto dns = [](const std::string& z) {
+          if (z.empty() || z.size() > 253) return false;
+          size_t st = 0;
+          for (size_t i = 0; i <= z.size(); i++) {
+            if (i == z.size() || z[i] == '.') {
+              std::string l = z.substr(st, i - st);
+              st = i + 1;
+              if (l.empty()) return false;
+              auto ok = [](char c) { return (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'); };
+              if (!ok(l.front()) || !ok(l.back())) return false;
+              for (char c : l) if (!(ok(c) || c == '-')) return false;
+            }
+          }
+          return true;
+        };
+        size_t slash = x.find('/');
+        bool lkey;
+        if (slash == std::string::npos) lkey = qn(x);
+        else if (x.find('/', slash + 1) != std::string::npos) lkey = false;
+        else lkey = slash > 0 && dns(x.substr(0, slash)) && qn(x.substr(slash + 1));
+        if (lkey) f |= SF_LKEY;
+        if (x.empty() || qn(x)) f |= SF_LVAL;
+        if (magic(x)) f |= SF_MAGIC;
+        b.str_flags[s] = f;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < std::max(1, threads); t++) th.emplace_back(work);
+  for (auto& t : th) t.join();
+  // heap
+  b.str_off.resize(n);
+  b.str_len.resize(n);
+  size_t off = from ? b.heap.size() : 0;
+  if (!from) b.heap.clear();
+  size_t total = off;
+  for (size_t s = from; s < n; s++) total += b.dict.strs[s].size();
+  b.heap.resize(total + 16);
+  for (size_t s = from; s < n; s++) {
+    const std::string& x = b.dict.strs[s];
+    b.str_off[s] = (uint32_t)off;
+    b.str_len[s] = (uint32_t)x.size();
+    memcpy(b.heap.data() + off, x.data(), x.size());
+    off += x.size();
+  }
+  if (total > 0xFFFFFFFFull) throw std::runtime_error("string heap exceeds 4 GiB per batch");
+}
+
+Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* nsl_json, size_t nsl_len, int threads,
+                   std::string* err) {
+  auto b = std::make_unique<Batch>();
+  try {
+    b->rs = rs;
+    b->dict = rs->dict;
+    auto docs = split_docs(json, len);
+    int T = std::max(1, threads);
+    size_t nchunks = std::min(docs.size(), (size_t)T * 8);
+    if (nchunks == 0) nchunks = 1;
+    std::vector<Chunk> chunks(nchunks);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (;;) {
+        size_t c = next.fetch_add(1);
+        if (c >= nchunks) break;
+        size_t d0 = docs.size() * c / nchunks, d1 = docs.size() * (c + 1) / nchunks;
+        try {
+          for (size_t d = d0; d < d1; d++) {
+            Value doc = pj::parse(json + docs[d].first, docs[d].second, false);
+            flatten_one(chunks[c], doc);
+          }
+        } catch (std::exception& e) {
+          chunks[c].err = e.what();
+        }
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    for (auto& c : chunks) if (!c.err.empty()) throw std::runtime_error(c.err);
+    size_t seed = b->dict.strs.size();
+    // merge dictionaries
+    std::vector<std::vector<uint32_t>> remap(nchunks);
+    for (size_t c = 0; c < nchunks; c++) {
+      remap[c].resize(chunks[c].strs.size());
+      for (size_t s = 0; s < chunks[c].strs.size(); s++) remap[c][s] = b->dict.intern(chunks[c].strs[s]);
+    }
+    // namespace label sets
+    std::unordered_map<uint32_t, uint32_t> ns_set;
+    if (nsl_json && nsl_len) {
+      Value nsl = pj::parse(nsl_json, nsl_len, false);
+      b->nsl_off.push_back(0);
+      if (nsl.t == T::Obj)
+        for (auto& kv : nsl.o) {
+          ns_set[b->dict.intern(kv.first)] = (uint32_t)b->nsl_names.size();
+          b->nsl_names.push_back(kv.first);
+          if (kv.second.t == T::Obj)
+            for (auto& lv : kv.second.o) {
+              b->nsl_kv.push_back(b->dict.intern(lv.first));
+              b->nsl_kv.push_back(b->dict.intern(lv.second.t == T::Str ? lv.second.s : ""));
+            }
+          b->nsl_off.push_back((uint32_t)b->nsl_kv.size() / 2);
+        }
+    } else {
+      b->nsl_off.push_back(0);
+    }
+    // concatenate + remap + sort map entries
+    size_t total_nodes = 0, total_res = 0, total_faux = 0;
+    std::vector<size_t> node_base(nchunks), res_base(nchunks), faux_base(nchunks);
+    for (size_t c = 0; c < nchunks; c++) {
+      node_base[c] = total_nodes; res_base[c] = total_res; faux_base[c] = total_faux;
+      total_nodes += chunks[c].nodes.size();
+      total_res += chunks[c].hdr.size();
+      total_faux += chunks[c].faux.size();
+    }
+    if (total_nodes > 0xFFFFFFFFull) throw std::runtime_error("batch exceeds 2^32 nodes; split it");
+    b->nodes.resize(total_nodes);
+    b->hdr.resize(total_res);
+    b->faux.resize(total_faux);
+    next = 0;
+    auto fix = [&]() {
+      for (;;) {
+        size_t c = next.fetch_add(1);
+        if (c >= nchunks) break;
+        Chunk& ch = chunks[c];
+        const auto& rm = remap[c];
+        for (size_t k = 0; k < ch.faux.size(); k++)
+          b->faux[faux_base[c] + k] = FloatAux{rm[ch.faux[k].sid_E], rm[ch.faux[k].sid_F]};
+        for (size_t r = 0; r < ch.hdr.size(); r++) {
+          ResHeader h = ch.hdr[r];
+          Node* R = b->nodes.data() + node_base[c] + h.root;
+          const Node* src = ch.nodes.data() + h.root;
+          for (uint32_t i = 0; i < h.nnodes; i++) {
+            Node n = src[i];
+            uint32_t t = node_type(n);
+            // key bits hold a local sid for map entries: detect by parent type below; remap all key fields of
+            // map children after copying
+            if (t == N_STR) n.a = rm[n.a];
+            else if (t == N_INT) n.c = rm[n.c];
+            else if (t == N_FLOAT) n.c += (uint32_t)faux_base[c];
+            R[i] = n;
+          }
+          for (uint32_t i = 0; i < h.nnodes; i++) {
+            if (node_type(R[i]) != N_MAP) continue;
+            Node* ch0 = R + R[i].a;
+            for (uint32_t k = 0; k < R[i].b; k++) ch0[k].tk = (rm[ch0[k].tk >> 4] << 4) | (ch0[k].tk & 0xF);
+            std::sort(ch0, ch0 + R[i].b, [](const Node& x, const Node& y) { return (x.tk >> 4) < (y.tk >> 4); });
+          }
+          h.root = (uint32_t)(node_base[c] + h.root);
+          h.kind = rm[h.kind]; h.gvk_kind = rm[h.gvk_kind]; h.group = rm[h.group]; h.version = rm[h.version];
+          h.gv = rm[h.gv]; h.name = rm[h.name]; h.gen_name = rm[h.gen_name]; h.ns = rm[h.ns];
+          auto it = ns_set.find(h.ns);
+          h.nsl = it == ns_set.end() ? NONE : it->second;
+          b->hdr[res_base[c] + r] = h;
+        }
+      }
+    };
+    th.clear();
+    for (int t = 0; t < T; t++) th.emplace_back(fix);
+    for (auto& t : th) t.join();
+    // labels/annotations node indices moved when map entries were sorted: recompute from the sorted tables
+    for (auto& h : b->hdr) {
+      if (h.labels == NONE && h.ann == NONE) continue;
+      const Node* R = b->nodes.data() + h.root;
+      uint32_t meta = (node_type(R[0]) == N_MAP) ? [&]() {
+        for (uint32_t i = 0; i < R[0].b; i++) if (node_key(R[R[0].a + i]) == KSID(METADATA)) return R[0].a + i;
+        return NONE;
+      }() : NONE;
+      auto find = [&](uint32_t key) -> uint32_t {
+        if (meta == NONE || node_type(R[meta]) != N_MAP) return NONE;
+        for (uint32_t i = 0; i < R[meta].b; i++) if (node_key(R[R[meta].a + i]) == key) return R[meta].a + i;
+        return NONE;
+      };
+      if (h.labels != NONE) h.labels = find(KSID(LABELS));
+      if (h.ann != NONE) h.ann = find(KSID(ANNOTATIONS));
+    }
+    derive_strings(*b, 0, T);
+    (void)seed;
+    return b.release();
+  } catch (std::exception& e) {
+    if (err) *err = e.what();
+    return nullptr;
+  }
+}
+
+std::string format_path(const Ruleset& rs, const Batch& b, uint32_t tmpl, const uint16_t* idx, const uint32_t* key) {
+  if (tmpl == NONE) return "";
+  const std::string& t = rs.templates[tmpl];
+  std::string out;
+  for (size_t i = 0; i < t.size(); i++) {
+    if (t[i] == '\x01' && i + 1 < t.size()) { out += std::to_string(idx[t[i + 1] - '0']); i++; continue; }
+    if (t[i] == '\x02' && i + 1 < t.size()) {
+      uint32_t k = key[t[i + 1] - '0'];
+      out += k < b.dict.strs.size() ? b.dict.strs[k] : std::string("?");
+      i++;
+      continue;
+    }
+    out += t[i];
+  }
+  return out;
+}
+
+}  // namespace kyv

@@ -1,0 +1,252 @@
+// C-ABI (include/kyvgpu.h). No exception crosses this boundary.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "../../include/kyvgpu.h"
+#include "kyv_host.h"
+
+namespace kyv {
+void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back);
+void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool account);
+void free_device_images(Ruleset& rs, Batch* b);
+}  // namespace kyv
+
+using namespace kyv;
+
+struct kyv_ruleset { Ruleset* rs; };
+struct kyv_batch { Batch* b; };
+struct kyv_results {
+  Results r;
+  std::multimap<uint64_t, uint32_t> recidx;  // (rule<<32|res) -> record
+  bool indexed = false;
+  std::mutex mu;
+};
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& m) { g_err = m; return code; }
+
+static int hw_threads(int t) {
+  if (t > 0) return t;
+  unsigned h = std::thread::hardware_concurrency();
+  return h ? (int)std::min(h, 64u) : 4;
+}
+
+extern "C" {
+
+const char* kyv_last_error(void) { return g_err.c_str(); }
+const char* kyv_version(void) { return "kyvgpu 0.1 (gfx950)"; }
+
+int kyv_ruleset_compile(const char* json, size_t len, const kyv_compile_opts* opts, kyv_ruleset** out) {
+  (void)opts;
+  if (!json || !out) return fail(KYV_EINVAL, "null argument");
+  try {
+    std::string err;
+    Ruleset* rs = compile_ruleset(json, len, &err);
+    if (!rs) return fail(KYV_EPARSE, err);
+    *out = new kyv_ruleset{rs};
+    return KYV_OK;
+  } catch (std::exception& e) {
+    return fail(KYV_EINTERNAL, e.what());
+  }
+}
+
+void kyv_ruleset_free(kyv_ruleset* rs) {
+  if (!rs) return;
+  try { free_device_images(*rs->rs, nullptr); } catch (...) {}
+  delete rs->rs;
+  delete rs;
+}
+
+uint32_t kyv_ruleset_num_rules(const kyv_ruleset* rs) { return rs ? (uint32_t)rs->rs->rules.size() : 0; }
+uint32_t kyv_ruleset_num_policies(const kyv_ruleset* rs) { return rs ? (uint32_t)rs->rs->policies.size() : 0; }
+
+int kyv_ruleset_rule_info(const kyv_ruleset* rs, uint32_t k, kyv_rule_info* out) {
+  if (!rs || !out || k >= rs->rs->rules.size()) return fail(KYV_ERANGE, "rule index out of range");
+  const RuleMeta& m = rs->rs->meta[k];
+  out->name = m.name.c_str();
+  out->policy = m.policy;
+  out->kind = m.kind;
+  out->reason = m.reason.c_str();
+  return KYV_OK;
+}
+
+int kyv_ruleset_policy_info(const kyv_ruleset* rs, uint32_t p, kyv_policy_info* out) {
+  if (!rs || !out || p >= rs->rs->policies.size()) return fail(KYV_ERANGE, "policy index out of range");
+  const PolicyMeta& m = rs->rs->policies[p];
+  out->name = m.name.c_str();
+  out->namespace_ = m.kind == "Policy" ? m.ns.c_str() : "";
+  out->first_rule = m.first_rule;
+  out->nrules = m.nrules;
+  out->apply_one = m.apply_one;
+  out->scored_false = m.scored_false;
+  return KYV_OK;
+}
+
+int kyv_batch_build(const kyv_ruleset* rs, const char* json, size_t len, const char* nsl, size_t nsl_len,
+                    const kyv_batch_opts* opts, kyv_batch** out) {
+  if (!rs || !json || !out) return fail(KYV_EINVAL, "null argument");
+  try {
+    std::string err;
+    Batch* b = build_batch(rs->rs, json, len, nsl, nsl_len, hw_threads(opts ? opts->threads : 0), &err);
+    if (!b) return fail(KYV_EPARSE, err);
+    *out = new kyv_batch{b};
+    return KYV_OK;
+  } catch (std::exception& e) {
+    return fail(KYV_EINTERNAL, e.what());
+  }
+}
+
+void kyv_batch_free(kyv_batch* b) {
+  if (!b) return;
+  try { free_device_images(*const_cast<Ruleset*>(b->b->rs), b->b); } catch (...) {}
+  delete b->b;
+  delete b;
+}
+
+uint32_t kyv_batch_num_resources(const kyv_batch* b) { return b ? (uint32_t)b->b->hdr.size() : 0; }
+
+int kyv_batch_stats_get(const kyv_batch* b, kyv_batch_stats* out) {
+  if (!b || !out) return fail(KYV_EINVAL, "null argument");
+  const Batch& x = *b->b;
+  out->resources = x.hdr.size();
+  out->nodes = x.nodes.size();
+  out->strings = x.dict.strs.size();
+  out->heap_bytes = x.heap.size();
+  out->device_bytes = x.nodes.size() * sizeof(Node) + x.hdr.size() * sizeof(ResHeader) + x.heap.size() +
+                      x.dict.strs.size() * (4 + 4 + 4 + 8 + 16 + 8) + x.faux.size() * sizeof(FloatAux);
+  return KYV_OK;
+}
+
+int kyv_eval(const kyv_ruleset* rs, const kyv_batch* b, const kyv_eval_opts* opts, kyv_results** out) {
+  if (!rs || !b || !out) return fail(KYV_EINVAL, "null argument");
+  if (b->b->rs != rs->rs) return fail(KYV_EINVAL, "batch was built for a different ruleset");
+  int backend = opts ? opts->backend : KYV_BACKEND_GPU;
+  try {
+    auto* res = new kyv_results();
+    if (backend == KYV_BACKEND_CPU) {
+      eval_cpu(*rs->rs, *b->b, hw_threads(opts ? opts->threads : 0), &res->r, opts && (opts->flags & KYV_EVAL_ACCOUNT_BYTES));
+    } else {
+      int dev = opts ? opts->device : 0;
+      int iters = opts && opts->iterations > 0 ? opts->iterations : 1;
+      bool copy = !(opts && (opts->flags & KYV_EVAL_NO_COPYBACK));
+      double ms = 0;
+      eval_gpu(*rs->rs, *b->b, dev, iters, &res->r, &ms, copy);
+    }
+    *out = res;
+    return KYV_OK;
+  } catch (std::exception& e) {
+    return fail(backend == KYV_BACKEND_GPU ? KYV_EDEVICE : KYV_EINTERNAL, e.what());
+  }
+}
+
+void kyv_results_free(kyv_results* r) { delete r; }
+
+int kyv_results_status(const kyv_results* r, uint8_t* out, size_t cap) {
+  if (!r || !out) return fail(KYV_EINVAL, "null argument");
+  if (cap < r->r.status.size()) return fail(KYV_ERANGE, "buffer too small (or verdicts kept on device)");
+  memcpy(out, r->r.status.data(), r->r.status.size());
+  return KYV_OK;
+}
+
+int64_t kyv_results_count(const kyv_results* r, int s) {
+  if (!r || s < 0 || s >= NSTATUS) return -1;
+  return r->r.counts[s];
+}
+
+double kyv_results_kernel_ms(const kyv_results* r) { return r ? r->r.kernel_ms : 0; }
+
+uint64_t kyv_results_alg_bytes(const kyv_results* r) { return r ? r->r.alg_bytes : 0; }
+
+static void ensure_index(kyv_results* r) {
+  std::lock_guard<std::mutex> g(r->mu);
+  if (r->indexed) return;
+  for (uint32_t i = 0; i < r->r.fails.size(); i++) {
+    const FailRec& f = r->r.fails[i];
+    r->recidx.emplace(((uint64_t)f.rule << 32) | f.res, i);
+  }
+  r->indexed = true;
+}
+
+static int64_t put(const std::string& s, char* buf, size_t cap) {
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, s.size());
+    memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return (int64_t)s.size();
+}
+
+// validation.go:722-758 (buildErrorMessage / buildAnyPatternErrorMessage) and :640/:665 pass messages
+int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res, uint32_t rule,
+                            char* buf, size_t cap) {
+  auto* r = const_cast<kyv_results*>(cr);
+  if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
+  const Ruleset& rs = *crs->rs;
+  const Batch& b = *cb->b;
+  uint8_t sb = r->r.status[(size_t)rule * r->r.nres + res];
+  uint8_t st = sb & 7, alt = sb >> 3;
+  const RuleMeta& m = rs.meta[rule];
+  const RuleDesc& d = rs.rules[rule];
+  if (m.message_vars && st == ST_FAIL) return -1;  // message needs variable substitution (CPU engine)
+  std::string msg;
+  if (d.kind == RK_PSS) {
+    if (st == ST_PASS) return put("Validation rule '" + m.name + "' passed.", buf, cap);
+    return -1;  // PodSecurity failure details are formatted by the caller from kyv_results_pss_mask
+  }
+  if (st == ST_PASS) {
+    if (d.kind == RK_ANYPATTERN) {
+      if (alt == 31) return put(m.message, buf, cap);
+      return put("validation rule '" + m.name + "' anyPattern[" + std::to_string(alt) + "] passed.", buf, cap);
+    }
+    return put("validation rule '" + m.name + "' passed.", buf, cap);
+  }
+  if (st != ST_FAIL) return -1;  // skip / error texts embed the reference's error strings
+  ensure_index(r);
+  auto range = r->recidx.equal_range(((uint64_t)rule << 32) | res);
+  std::vector<const FailRec*> recs;
+  for (auto it = range.first; it != range.second; ++it) recs.push_back(&r->r.fails[it->second]);
+  std::sort(recs.begin(), recs.end(), [](const FailRec* a, const FailRec* b2) { return a->alt < b2->alt; });
+  if (recs.empty()) return -1;
+  if (d.kind == RK_PATTERN) {
+    std::string path = format_path(rs, b, recs[0]->tmpl, recs[0]->idx, recs[0]->key);
+    if (m.message.empty()) return put("validation error: rule " + m.name + " failed at path " + path, buf, cap);
+    std::string mm = m.message;
+    if (mm.back() != '.') mm += ".";
+    return put("validation error: " + mm + " rule " + m.name + " failed at path " + path, buf, cap);
+  }
+  std::string joined;
+  for (size_t i = 0; i < recs.size(); i++) {
+    if (recs[i]->tmpl == NONE) return -1;  // "failed: <err>" needs the reference error text
+    if (i) joined += " ";
+    joined += "rule " + m.name + "[" + std::to_string(recs[i]->alt) + "] failed at path " +
+              format_path(rs, b, recs[i]->tmpl, recs[i]->idx, recs[i]->key);
+  }
+  if (m.message.empty()) return put("validation error: " + joined, buf, cap);
+  if (m.message.back() == '.') return put("validation error: " + m.message + " " + joined, buf, cap);
+  return put("validation error: " + m.message + ". " + joined, buf, cap);
+}
+
+int64_t kyv_results_path(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res, uint32_t rule,
+                         char* buf, size_t cap) {
+  auto* r = const_cast<kyv_results*>(cr);
+  if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
+  ensure_index(r);
+  auto it = r->recidx.find(((uint64_t)rule << 32) | res);
+  if (it == r->recidx.end()) return put("", buf, cap);
+  const FailRec& f = r->r.fails[it->second];
+  return put(format_path(*crs->rs, *cb->b, f.tmpl, f.idx, f.key), buf, cap);
+}
+
+uint32_t kyv_results_pss_mask(const kyv_results* r, const kyv_ruleset* rs, uint32_t res, uint32_t rule) {
+  if (!r || !rs || rule >= r->r.nrules || res >= r->r.nres) return 0;
+  uint32_t slot = 0;
+  for (uint32_t k = 0; k < rule; k++) if (rs->rs->rules[k].kind == RK_PSS) slot++;
+  if (rs->rs->rules[rule].kind != RK_PSS) return 0;
+  size_t i = (size_t)slot * r->r.nres + res;
+  return i < r->r.pss_fails.size() ? r->r.pss_fails[i] : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1107 @@
+// Policy compiler: ClusterPolicy/Policy JSON -> autogen-expanded rules -> device rule programs.
+//
+// Reference behaviour restated here (paths relative to /root/reference):
+//   pkg/autogen/autogen.go:70-314, rule.go:73-319   ComputeRules (autogen-<rule>, autogen-cronjob-<rule>)
+//   pkg/engine/validation.go:276-317                 dispatch order deny > pattern/anyPattern > podSecurity > foreach
+//   pkg/engine/anchor/anchor.go:19,37-44             anchor grammar
+//   pkg/engine/validate/validate.go:118-161 + utils.go:11-69  map traversal order (compile-time resolved)
+//   pkg/engine/pattern/pattern.go, operator/operator.go       string pattern mini-language -> atoms
+//   pkg/engine/wildcards/wildcards.go:62-151          metadata wildcard keys -> run-time slots
+//   pkg/engine/utils.go:37-289, pkg/utils/match, pkg/utils/kube/kind.go   match/exclude programs
+//   pkg/pss/evaluate.go, pkg/pss/utils/mapping.go     PodSecurity descriptors
+// Rules needing variables, JMESPath, context, preconditions, deny, foreach or image verification are
+// classified RK_FALLBACK (counted, handed back to the reference CPU engine by the caller).
+#include <algorithm>
+#include <cmath>
+#include <list>
+#include <map>
+#include <set>
+
+#include "kyv_host.h"
+
+namespace kyv {
+using pj::T;
+using pj::Value;
+
+void seed_dict(Dict& d) {
+  const char* fixed[] = {"", "0", "true", "false", "*"};
+  for (const char* s : fixed) d.intern(s);
+  const char* wk[] = {
+#define KYV_WK_STR(id, s) s,
+      KYV_WELL_KNOWN(KYV_WK_STR)
+#undef KYV_WK_STR
+  };
+  for (const char* s : wk) d.intern(s);
+  const char* vs[] = {
+#define KYV_VS_STR(id) #id,
+      KYV_VOLUME_SOURCES(KYV_VS_STR)
+#undef KYV_VS_STR
+  };
+  for (const char* s : vs) d.intern(s);
+  if (d.strs.size() != SID_SEED_END) throw std::runtime_error("seed dictionary has duplicate entries");
+}
+
+Ruleset::~Ruleset() {}
+
+namespace {
+
+bool nil(const Value* v) { return !v || v->t == T::Null; }
+std::vector<std::string> strs(const Value* v) {
+  std::vector<std::string> out;
+  if (v && v->t == T::Arr) for (auto& e : v->a) out.push_back(e.t == T::Str ? e.s : "");
+  return out;
+}
+bool nonempty(const Value* v) {
+  if (nil(v)) return false;
+  if (v->t == T::Obj) return !v->o.empty();
+  if (v->t == T::Arr) return !v->a.empty();
+  if (v->t == T::Str) return !v->s.empty();
+  return true;
+}
+
+// ---------------------------------------------------------------- anchors (anchor.go)
+enum class AT { None, Cond, Global, Neg, Add, Eq, Exist };
+struct Anc { AT t = AT::None; std::string key; };
+Anc parse_anchor(const std::string& raw) {
+  Anc a;
+  std::string s = pj::go_trim_space(raw);
+  if (s.size() < 3 || s.back() != ')') return a;
+  size_t p = 0;
+  AT t = AT::Cond;
+  switch (s[0]) {
+    case '+': t = AT::Add; p = 1; break;
+    case '<': t = AT::Global; p = 1; break;
+    case '=': t = AT::Eq; p = 1; break;
+    case 'X': t = AT::Neg; p = 1; break;
+    case '^': t = AT::Exist; p = 1; break;
+    default: break;
+  }
+  if (s[p] != '(') return a;
+  std::string k = s.substr(p + 1, s.size() - p - 2);
+  if (k.empty() || k.find('\n') != std::string::npos) return a;
+  a.t = t;
+  a.key = k;
+  return a;
+}
+std::string anchor_str(AT t, const std::string& k) {
+  const char* m = t == AT::Global ? "<" : t == AT::Neg ? "X" : t == AT::Add ? "+" : t == AT::Eq ? "=" : t == AT::Exist ? "^" : "";
+  return std::string(m) + "(" + k + ")";
+}
+bool has_wild(const std::string& s) { return s.find('*') != std::string::npos || s.find('?') != std::string::npos; }
+bool has_magic(const std::string& s) {
+  return s.find("negation anchor matched in resource") != std::string::npos ||
+         s.find("conditional anchor mismatch") != std::string::npos || s.find("global anchor mismatch") != std::string::npos;
+}
+
+// ---------------------------------------------------------------- kinds (pkg/utils/kube/kind.go)
+bool version_like(const std::string& s) {
+  for (size_t i = 0; i + 1 < s.size(); i++) if (s[i] == 'v' && s[i + 1] >= '0' && s[i + 1] <= '9') return true;
+  return false;
+}
+std::vector<std::string> split(const std::string& s, char c) {
+  std::vector<std::string> out;
+  size_t st = 0;
+  for (size_t i = 0; i <= s.size(); i++)
+    if (i == s.size() || s[i] == c) { out.push_back(s.substr(st, i - st)); st = i + 1; }
+  return out;
+}
+std::string sub_dot(std::string s) {
+  size_t i = s.find('.');
+  if (i != std::string::npos) s[i] = '/';
+  return s;
+}
+void kind_from_gvk(const std::string& str, std::string& gv, std::string& kind) {
+  auto p = split(str, '/');
+  gv.clear();
+  if (p.size() == 2) {
+    if (version_like(p[0]) || p[0] == "*") { gv = p[0]; kind = sub_dot(p[1]); } else kind = p[0] + "/" + p[1];
+  } else if (p.size() == 3) {
+    if (version_like(p[0]) || p[0] == "*") { gv = p[0]; kind = p[1] + "/" + p[2]; }
+    else { gv = p[0] + "/" + p[1]; kind = sub_dot(p[2]); }
+  } else if (p.size() == 4) {
+    gv = p[0] + "/" + p[1];
+    kind = p[2] + "/" + p[3];
+  } else {
+    kind = sub_dot(str);
+  }
+}
+bool contains_kind(const std::vector<std::string>& l, const std::string& kind) {
+  for (auto& e : l) {
+    std::string gv, k;
+    kind_from_gvk(e, gv, k);
+    auto parts = split(k, '/');
+    if (parts.size() == 2) k = parts[0];
+    if (k == kind) return true;
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------- autogen (pkg/autogen)
+std::vector<std::string> match_kinds(const Value* mr) {  // MatchResources.GetKinds
+  std::vector<std::string> out;
+  if (nil(mr)) return out;
+  const Value* rd = mr->get("resources");
+  for (auto& k : strs(rd ? rd->get("kinds") : nullptr)) out.push_back(k);
+  for (const char* b : {"all", "any"}) {
+    const Value* l = mr->get(b);
+    if (l && l->t == T::Arr)
+      for (auto& f : l->a) {
+        const Value* frd = f.get("resources");
+        for (auto& k : strs(frd ? frd->get("kinds") : nullptr)) out.push_back(k);
+      }
+  }
+  return out;
+}
+bool autogen_subject_ok(bool& needed, const Value* rd) {  // checkAutogenSupport autogen.go:33-43
+  if (nil(rd)) return true;
+  static const std::set<std::string> pc = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet",
+                                           "ReplicationController", "CronJob", "Pod"};
+  auto kinds = strs(rd->get("kinds"));
+  if (!rd->str_or("name").empty() || !strs(rd->get("names")).empty() || !nil(rd->get("selector")) ||
+      !nil(rd->get("annotations")) || (kinds.size() > 1 && contains_kind(kinds, "Pod")))
+    return false;
+  for (auto& k : kinds) if (pc.count(k)) needed = true;
+  return true;
+}
+bool can_autogen(const Value* spec) {  // CanAutoGen autogen.go:70-136
+  bool needed = false;
+  const Value* rules = spec ? spec->get("rules") : nullptr;
+  if (rules && rules->t == T::Arr)
+    for (auto& r : rules->a) {
+      const Value* mut = r.get("mutate");
+      if ((mut && !mut->str_or("patchesJson6902").empty()) || nonempty(r.get("generate"))) return false;
+      const Value* m = r.get("match");
+      const Value* e = r.get("exclude");
+      if (!autogen_subject_ok(needed, m ? m->get("resources") : nullptr) ||
+          !autogen_subject_ok(needed, e ? e->get("resources") : nullptr))
+        return false;
+      for (const Value* blk : {m, e})
+        for (const char* w : {"any", "all"}) {
+          const Value* l = blk ? blk->get(w) : nullptr;
+          if (l && l->t == T::Arr)
+            for (auto& f : l->a) if (!autogen_subject_ok(needed, f.get("resources"))) return false;
+        }
+    }
+  return needed;
+}
+Value kinds_value(const std::vector<std::string>& k) {
+  Value a = Value::A();
+  for (auto& s : k) a.a.push_back(Value::S(s));
+  return a;
+}
+void replace_filter_kinds(Value& filters, const std::string& match, const std::vector<std::string>& kinds) {
+  for (auto& f : filters.a) {
+    Value* rd = f.getm("resources");
+    if (rd && contains_kind(strs(rd->get("kinds")), match)) rd->set("kinds", kinds_value(kinds));
+  }
+}
+bool nonempty_list(const Value* v) { return v && v->t == T::Arr && !v->a.empty(); }
+
+// generateRule (rule.go:73-204); returns false when no rule is generated
+bool generate_rule(const std::string& name, const Value& r0, const std::string& tplKey, const std::vector<std::string>& kinds,
+                   const std::string& grfKind, Value& out) {
+  out = r0;
+  out.set("name", Value::S(name));
+  Value* m = out.getm("match");
+  if (!m) { out.set("match", Value::O()); m = out.getm("match"); }
+  if (nonempty_list(m->get("any"))) replace_filter_kinds(*m->getm("any"), grfKind, kinds);
+  else if (nonempty_list(m->get("all"))) replace_filter_kinds(*m->getm("all"), grfKind, kinds);
+  else {
+    Value* rd = m->getm("resources");
+    if (!rd || rd->t != T::Obj) { m->set("resources", Value::O()); rd = m->getm("resources"); }
+    rd->set("kinds", kinds_value(kinds));
+  }
+  Value* e = out.getm("exclude");
+  if (e && e->t == T::Obj) {
+    if (nonempty_list(e->get("any"))) replace_filter_kinds(*e->getm("any"), grfKind, kinds);
+    else if (nonempty_list(e->get("all"))) replace_filter_kinds(*e->getm("all"), grfKind, kinds);
+    else {
+      Value* rd = e->getm("resources");
+      if (rd && !strs(rd->get("kinds")).empty()) rd->set("kinds", kinds_value(kinds));
+    }
+  }
+  const Value* mut = out.get("mutate");
+  if (mut && (!nil(mut->get("patchStrategicMerge")) || nonempty(mut->get("foreach")))) return true;
+  const Value* val = out.get("validate");
+  if (!val) return false;
+  std::string msg = val->str_or("message");
+  auto wrap = [&](const Value& p) {
+    Value inner = Value::O();
+    inner.set(tplKey, p);
+    Value outer = Value::O();
+    outer.set("spec", inner);
+    return outer;
+  };
+  Value nv = Value::O();
+  if (!msg.empty()) nv.set("message", Value::S(msg));
+  if (!nil(val->get("pattern"))) nv.set("pattern", wrap(*val->get("pattern")));
+  else if (!nil(val->get("deny"))) nv.set("deny", *val->get("deny"));
+  else if (!nil(val->get("podSecurity"))) {
+    const Value* ps = val->get("podSecurity");
+    Value np = Value::O();
+    if (!ps->str_or("level").empty()) np.set("level", Value::S(ps->str_or("level")));
+    if (!ps->str_or("version").empty()) np.set("version", Value::S(ps->str_or("version")));
+    if (nonempty_list(ps->get("exclude"))) np.set("exclude", *ps->get("exclude"));
+    nv.set("podSecurity", np);
+  } else if (!nil(val->get("anyPattern"))) {
+    Value arr = Value::A();
+    const Value* ap = val->get("anyPattern");
+    if (ap->t == T::Arr) for (auto& p : ap->a) arr.a.push_back(wrap(p));
+    nv.set("anyPattern", arr);
+  } else if (nonempty(val->get("foreach"))) {
+    nv.set("foreach", *val->get("foreach"));
+  } else if (nonempty(out.get("verifyImages"))) {
+    return true;
+  } else {
+    return false;
+  }
+  out.set("validate", nv);
+  return true;
+}
+
+std::string autogen_name(const std::string& prefix, const std::string& n) {
+  std::string s = prefix + "-" + n;
+  return s.size() > 63 ? s.substr(0, 63) : s;
+}
+
+bool gen_for_controllers(const Value& r, std::string controllers, Value& out) {  // rule.go:228-279
+  std::string name = r.str_or("name");
+  if (name.compare(0, 8, "autogen-") == 0 || controllers.empty()) return false;
+  auto mk = match_kinds(r.get("match")), ek = match_kinds(r.get("exclude"));
+  if (!contains_kind(mk, "Pod") || (!ek.empty() && !contains_kind(ek, "Pod"))) return false;
+  static const std::set<std::string> ok = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet", "ReplicationController"};
+  if (controllers == "all") controllers = "DaemonSet,Deployment,Job,StatefulSet,ReplicaSet,ReplicationController";
+  else if (controllers != "none") {
+    std::string v;
+    for (auto& c : split(controllers, ','))
+      if (ok.count(c)) v += (v.empty() ? "" : ",") + c;
+    if (!v.empty()) controllers = v;
+  }
+  return generate_rule(autogen_name("autogen", name), r, "template", split(controllers, ','), "Pod", out);
+}
+
+bool gen_cronjob(const Value& r, const std::string& controllers, Value& out) {  // rule.go:281-297
+  if (controllers.find("CronJob") == std::string::npos && controllers.find("all") == std::string::npos) return false;
+  Value mid;
+  if (!gen_for_controllers(r, controllers, mid)) return false;
+  return generate_rule(autogen_name("autogen-cronjob", r.str_or("name")), mid, "jobTemplate", {"CronJob"}, "Job", out);
+}
+
+std::string replace_all(std::string s, const std::string& a, const std::string& b) {
+  size_t p = 0;
+  while ((p = s.find(a, p)) != std::string::npos) { s.replace(p, a.size(), b); p += b.size(); }
+  return s;
+}
+
+Value convert_rule(const Value& r, bool cronjob) {  // convertRule autogen.go:238-276 (text rewrite on the JSON)
+  std::string b = pj::dump(r);
+  const Value* val = r.get("validate");
+  if (val && !nil(val->get("podSecurity"))) {
+    b = replace_all(b, "\"restrictedField\":\"spec", cronjob ? "\"restrictedField\":\"spec.jobTemplate.spec.template.spec"
+                                                             : "\"restrictedField\":\"spec.template.spec");
+    b = replace_all(b, "metadata", "spec.template.metadata");
+  } else {
+    b = replace_all(b, "request.object.spec", cronjob ? "request.object.spec.jobTemplate.spec.template.spec" : "request.object.spec.template.spec");
+    b = replace_all(b, "request.object.metadata", "request.object.spec.template.metadata");
+  }
+  return pj::parse(b, true);
+}
+
+std::vector<Value> compute_rules(const Value& policy) {  // ComputeRules autogen.go:280-314
+  const Value* spec = policy.get("spec");
+  std::vector<Value> rules;
+  if (spec && spec->get("rules") && spec->get("rules")->t == T::Arr) rules = spec->get("rules")->a;
+  bool apply = can_autogen(spec);
+  std::string actual = apply ? "DaemonSet,Deployment,Job,StatefulSet,ReplicaSet,ReplicationController,CronJob" : "none";
+  const Value* meta = policy.get("metadata");
+  const Value* ann = meta ? meta->get("annotations") : nullptr;
+  const Value* a = ann ? ann->get("pod-policies.kyverno.io/autogen-controllers") : nullptr;
+  if (a && apply) actual = a->t == T::Str ? a->s : "";
+  if (actual == "none") return rules;
+  std::string stripped;
+  for (auto& c : split(actual, ',')) if (c != "CronJob") stripped += (stripped.empty() ? "" : ",") + c;
+  std::vector<Value> gen;
+  for (auto& r : rules) {
+    Value g;
+    if (gen_for_controllers(r, stripped, g)) gen.push_back(convert_rule(g, false));
+    if (gen_cronjob(r, actual, g)) gen.push_back(convert_rule(g, true));
+  }
+  if (gen.empty()) return rules;
+  std::vector<Value> out;
+  for (auto& r : rules) if (r.str_or("name").compare(0, 8, "autogen-") != 0) out.push_back(r);
+  for (auto& g : gen) out.push_back(g);
+  return out;
+}
+
+// ---------------------------------------------------------------- compile state
+struct Fallback { std::string why; };
+
+struct Cx {
+  Ruleset& rs;
+  RuleDesc* rd = nullptr;
+  std::map<std::string, int> abits;  // raw anchor key -> bit (per pattern)
+  int nslots = 0;
+  uint32_t nmeta = 0;
+  std::vector<MetaSite> sites;
+  uint32_t tmpl(const std::string& s) {
+    rs.templates.push_back(s);
+    return (uint32_t)rs.templates.size() - 1;
+  }
+  uint32_t sid(const std::string& s) { return rs.dict.intern(s); }
+};
+
+std::string idx_ph(int level) { return std::string("\x01") + (char)('0' + level); }
+std::string key_ph(int slot) { return std::string("\x02") + (char)('0' + slot); }
+
+// glob classification for compareString atoms
+void classify_glob(Cx& c, Atom& a, const std::string& p) {
+  a.pat = c.sid(p);
+  a.lit = NONE;
+  if (p.empty()) { a.glob = G_EMPTY; return; }
+  if (!has_wild(p)) { a.glob = G_EXACT; return; }
+  bool allstar = true;
+  for (char ch : p) if (ch != '*') allstar = false;
+  if (allstar) { a.glob = G_ANY; return; }
+  if (p == "?*" || p == "*?") { a.glob = G_NONEMPTY; return; }
+  auto lit_ok = [](const std::string& s) { return !s.empty() && !has_wild(s); };
+  if (p.size() >= 2 && p.back() == '*' && lit_ok(p.substr(0, p.size() - 1))) { a.glob = G_PREFIX; a.lit = c.sid(p.substr(0, p.size() - 1)); return; }
+  if (p.size() >= 2 && p[0] == '*' && lit_ok(p.substr(1))) { a.glob = G_SUFFIX; a.lit = c.sid(p.substr(1)); return; }
+  if (p.size() >= 3 && p[0] == '*' && p.back() == '*' && lit_ok(p.substr(1, p.size() - 2))) {
+    a.glob = G_CONTAINS;
+    a.lit = c.sid(p.substr(1, p.size() - 2));
+    return;
+  }
+  a.glob = G_GENERAL;
+}
+
+// range regexes (operator.go:30-31): [-|\+]?\d+(?:\.\d+)?[A-Za-z]*
+bool range_side(const std::string& s, size_t& i) {
+  size_t st = i;
+  if (i < s.size() && (s[i] == '-' || s[i] == '|' || s[i] == '+')) i++;
+  size_t d = i;
+  while (i < s.size() && isdigit((unsigned char)s[i])) i++;
+  if (i == d) { i = st; return false; }
+  if (i + 1 < s.size() && s[i] == '.' && isdigit((unsigned char)s[i + 1])) { i++; while (i < s.size() && isdigit((unsigned char)s[i])) i++; }
+  while (i < s.size() && isalpha((unsigned char)s[i])) i++;
+  return true;
+}
+bool range_split(const std::string& s, const std::string& sep, std::string& l, std::string& r) {
+  size_t i = 0;
+  if (!range_side(s, i)) return false;
+  size_t le = i;
+  if (s.compare(i, sep.size(), sep) != 0) return false;
+  i += sep.size();
+  size_t rs = i;
+  if (!range_side(s, i) || i != s.size()) return false;
+  l = s.substr(0, le);
+  r = s.substr(rs);
+  return true;
+}
+
+Atom simple_atom(Cx& c, uint8_t op, const std::string& p) {
+  Atom a{};
+  a.op = op;
+  a.sub = NONE;
+  int64_t d;
+  if (pj::go_parse_duration(p, &d)) { a.flags |= AF_DUR; a.dur = d; }
+  int64_t lo, hi;
+  int q = pj::go_parse_quantity(p, &lo, &hi);
+  if (q == 2) throw Fallback{"pattern quantity beyond int128 nano range"};
+  if (q == 1) { a.flags |= AF_QTY; a.qlo = lo; a.qhi = hi; }
+  classify_glob(c, a, p);
+  return a;
+}
+
+// validateStringPattern (pattern.go:175-197) compiled to one atom
+uint32_t compile_atom(Cx& c, const std::string& atom) {
+  std::string l, r;
+  uint8_t op;
+  size_t oplen = 0;
+  if (atom.size() < 2) op = A_EQ;
+  else if (atom.compare(0, 2, ">=") == 0) { op = A_GE; oplen = 2; }
+  else if (atom.compare(0, 2, "<=") == 0) { op = A_LE; oplen = 2; }
+  else if (atom[0] == '>') { op = A_GT; oplen = 1; }
+  else if (atom[0] == '<') { op = A_LT; oplen = 1; }
+  else if (atom[0] == '!') { op = A_NE; oplen = 1; }
+  else if (range_split(atom, "!-", l, r)) op = A_RANGE_OUT;
+  else if (range_split(atom, "-", l, r)) op = A_RANGE_IN;
+  else op = A_EQ;
+  if (op == A_RANGE_IN || op == A_RANGE_OUT) {
+    Atom a{};
+    a.op = op;
+    a.sub = (uint32_t)c.rs.atoms.size() + 1;
+    uint32_t id = (uint32_t)c.rs.atoms.size();
+    c.rs.atoms.push_back(a);
+    // ">= "+left / "<= "+right  resp. "< "+left / "> "+right, operator stripped + TrimSpace
+    c.rs.atoms.push_back(simple_atom(c, op == A_RANGE_IN ? A_GE : A_LT, pj::go_trim_space(" " + l)));
+    c.rs.atoms.push_back(simple_atom(c, op == A_RANGE_IN ? A_LE : A_GT, pj::go_trim_space(" " + r)));
+    return id;
+  }
+  uint32_t id = (uint32_t)c.rs.atoms.size();
+  c.rs.atoms.push_back(simple_atom(c, op, pj::go_trim_space(atom.substr(oplen))));
+  return id;
+}
+
+std::string trim_sp(const std::string& s) {
+  size_t b = 0, e = s.size();
+  while (b < e && s[b] == ' ') b++;
+  while (e > b && s[e - 1] == ' ') e--;
+  return s.substr(b, e - b);
+}
+
+uint32_t compile_leaf(Cx& c, const Value& p) {  // pattern.Validate leaf types
+  Leaf L{};
+  L.exact = NONE;
+  switch (p.t) {
+    case T::Null: L.type = L_NIL; break;
+    case T::Bool: L.type = L_BOOL; L.bval = p.b; break;
+    case T::Int:
+      L.type = L_FLOAT; L.f = (double)p.i; L.fint = 1; L.fi = p.i;
+      break;
+    case T::Float: {
+      L.type = L_FLOAT;
+      L.f = p.f;
+      L.fint = p.f == std::trunc(p.f);
+      if (!(p.f > -9.223372036854775808e18 && p.f < 9.223372036854775807e18)) L.fi = INT64_MIN;
+      else L.fi = (int64_t)p.f;
+      break;
+    }
+    case T::Str: {
+      if (has_magic(p.s)) throw Fallback{"pattern text contains an anchor-error phrase"};
+      L.type = L_STR;
+      L.exact = c.sid(p.s);
+      std::vector<uint32_t> groups;
+      for (auto& g0 : split(p.s, '|')) {
+        std::string g = trim_sp(g0);
+        std::vector<uint32_t> atoms;
+        for (auto& a0 : split(g, '&')) atoms.push_back(compile_atom(c, trim_sp(a0)));
+        // atoms of one group must be consecutive: re-emit as a contiguous block of references
+        uint32_t first = (uint32_t)c.rs.atoms.size();
+        for (uint32_t id : atoms) {
+          Atom a = c.rs.atoms[id];
+          c.rs.atoms.push_back(a);
+        }
+        groups.push_back(first);
+        groups.push_back((uint32_t)atoms.size());
+      }
+      L.groups = (uint32_t)c.rs.pool.size();
+      L.ngroups = (uint32_t)groups.size() / 2;
+      for (auto g : groups) c.rs.pool.push_back(g);
+      break;
+    }
+    case T::Obj: L.type = L_MAP; break;
+    default: L.type = L_ARR; break;
+  }
+  c.rs.leaves.push_back(L);
+  return (uint32_t)c.rs.leaves.size() - 1;
+}
+
+uint32_t new_pnode(Cx& c, uint8_t kind, const std::string& path) {
+  PNode P{};
+  P.kind = kind;
+  P.tmpl = c.tmpl(path);
+  c.rs.pnodes.push_back(P);
+  return (uint32_t)c.rs.pnodes.size() - 1;
+}
+
+bool has_nested_anchors(const Value& p) {  // validate/utils.go:11-33
+  if (p.t == T::Obj) {
+    for (auto& kv : p.o) {
+      Anc a = parse_anchor(kv.first);
+      if (a.t == AT::Cond || a.t == AT::Exist || a.t == AT::Eq || a.t == AT::Neg || a.t == AT::Global) return true;
+    }
+    for (auto& kv : p.o) if (has_nested_anchors(kv.second)) return true;
+    return false;
+  }
+  if (p.t == T::Arr) for (auto& e : p.a) if (has_nested_anchors(e)) return true;
+  return false;
+}
+
+struct Loc {
+  int level = 0;     // enclosing array-of-maps nesting (dynamic index slots used)
+  bool loop = false; // inside a loop construct (array of maps / existence trial)
+  int depth = 0;
+};
+
+uint32_t compile_elem(Cx& c, const Value& p, const std::string& path, Loc loc, int wild_slot_base = -1);
+
+// which pattern key selects metadata/labels (getPatternValue, wildcards.go:85-96)
+const std::pair<std::string, Value>* pattern_value(const Value& m, const std::string& tag) {
+  const std::pair<std::string, Value>* hit = nullptr;
+  int n = 0;
+  for (auto& kv : m.o) {
+    Anc a = parse_anchor(kv.first);
+    if (kv.first == tag || (a.t != AT::None && a.key == tag)) { hit = &kv; n++; }
+  }
+  if (n > 1) throw Fallback{"pattern selects " + tag + " twice (Go map order decides)"};
+  return hit;
+}
+
+uint32_t compile_map(Cx& c, const Value& p, const std::string& path, Loc loc) {
+  for (auto& kv : p.o) if (has_magic(kv.first)) throw Fallback{"pattern key contains an anchor-error phrase"};
+  uint32_t id = new_pnode(c, P_MAP, path);
+  // ExpandInMetadata site (wildcards.go:62-83)
+  int meta_site = -1;
+  std::string meta_key;
+  int labels_slot0 = -1, ann_slot0 = -1;
+  std::string labels_pkey, ann_pkey;
+  if (auto mv = pattern_value(p, "metadata")) {
+    if (!mv->second.nil()) {
+      if (mv->second.t != T::Obj) throw Fallback{"pattern metadata is not a map (reference panics)"};
+      MetaSite ms{};
+      ms.wild_l = ms.wild_a = (uint32_t)c.rs.pool.size();
+      for (int tag = 0; tag < 2; tag++) {
+        auto lv = pattern_value(mv->second, tag == 0 ? "labels" : "annotations");
+        if (!lv || lv->second.nil()) continue;
+        if (lv->second.t != T::Obj) throw Fallback{"pattern labels/annotations is not a map (reference panics)"};
+        std::vector<std::pair<std::string, std::string>> wild;
+        for (auto& kv : lv->second.o) {
+          if (kv.second.t != T::Str) throw Fallback{"non-string metadata pattern value (reference panics)"};
+          if (has_wild(kv.first)) {
+            Anc a = parse_anchor(kv.first);
+            wild.push_back({a.t != AT::None ? a.key : kv.first, a.t != AT::None ? a.key : kv.first});
+          }
+        }
+        if (!wild.empty() && (loc.loop || lv->second.o.size() != 1))
+          throw Fallback{"wildcard metadata keys inside a loop or beside other keys (order/collision is run-time)"};
+        if (tag == 0) ms.has_labels = 1; else ms.has_ann = 1;
+        uint32_t off = (uint32_t)c.rs.pool.size();
+        for (auto& w : wild) { c.rs.pool.push_back(c.sid(w.first)); c.rs.pool.push_back(c.sid(w.second)); }
+        int slot0 = c.nslots;
+        c.nslots += (int)wild.size();
+        if (c.nslots > MAX_SLOTS) throw Fallback{"too many metadata wildcard keys"};
+        if (tag == 0) { ms.wild_l = off; ms.nwild_l = (uint32_t)wild.size(); ms.slot_l = slot0; labels_slot0 = wild.empty() ? -1 : slot0; labels_pkey = lv->first; }
+        else { ms.wild_a = off; ms.nwild_a = (uint32_t)wild.size(); ms.slot_a = slot0; ann_slot0 = wild.empty() ? -1 : slot0; ann_pkey = lv->first; }
+      }
+      if (ms.has_labels || ms.has_ann) {
+        meta_site = (int)c.sites.size();
+        c.sites.push_back(ms);
+        meta_key = mv->first;
+      }
+    }
+  }
+  // entry order: anchors sorted, then getSortedNestedAnchorResource (validate.go:118-161)
+  std::vector<std::string> anchors, others;
+  for (auto& kv : p.o) {
+    Anc a = parse_anchor(kv.first);
+    if (a.t == AT::Cond || a.t == AT::Exist || a.t == AT::Eq || a.t == AT::Neg) anchors.push_back(kv.first);
+    else others.push_back(kv.first);
+  }
+  std::sort(anchors.begin(), anchors.end());
+  std::sort(others.begin(), others.end());
+  std::list<std::string> order;
+  for (auto& k : others) {
+    if (parse_anchor(k).t == AT::Global || has_nested_anchors(*p.get(k))) order.push_front(k);
+    else order.push_back(k);
+  }
+  std::vector<std::string> keys = anchors;
+  for (auto& k : order) keys.push_back(k);
+  std::vector<PEntry> ents;
+  for (auto& k : keys) {
+    const Value& v = *p.get(k);
+    PEntry E{};
+    E.abit = 0xFF;
+    E.child = NONE;
+    Anc a = parse_anchor(k);
+    std::string lookup = (a.t == AT::None || a.t == AT::Add) ? k : a.key;
+    std::string cur = path + lookup + "/";
+    if (a.t == AT::Cond || a.t == AT::Exist || a.t == AT::Neg) {
+      auto it = c.abits.find(k);
+      int bit;
+      if (it == c.abits.end()) {
+        bit = (int)c.abits.size();
+        if (bit >= 64) throw Fallback{"more than 64 distinct anchor keys"};
+        c.abits[k] = bit;
+      } else bit = it->second;
+      E.abit = (uint8_t)bit;
+    }
+    E.key = c.sid(lookup);
+    Loc child = loc;
+    child.depth++;
+    switch (a.t) {
+      case AT::Cond: E.handler = H_CONDITION; break;
+      case AT::Global: E.handler = H_GLOBAL; break;
+      case AT::Eq: E.handler = H_EQUALITY; break;
+      case AT::Neg: E.handler = H_NEGATION; break;
+      case AT::Exist: E.handler = H_EXISTENCE; break;
+      default: E.handler = (v.t == T::Str && v.s == "*") ? H_STAR : H_DEFAULT; break;
+    }
+    E.tmpl = c.tmpl(cur);
+    if (E.handler == H_EXISTENCE) {
+      bool bad = v.t != T::Arr;
+      if (!bad) for (auto& e : v.a) if (e.t != T::Obj) bad = true;
+      if (bad) E.handler = H_EXIST_BADPAT;
+      else {
+        Loc tl = child;
+        tl.loop = true;
+        std::vector<uint32_t> maps;
+        for (auto& e : v.a) maps.push_back(compile_elem(c, e, cur + "\x03/", tl));  // trial paths never reported
+        E.child = (uint32_t)c.rs.pool.size();
+        c.rs.pool.push_back((uint32_t)maps.size());
+        for (auto m : maps) c.rs.pool.push_back(m);
+      }
+    } else if (E.handler != H_NEGATION && E.handler != H_STAR) {
+      E.child = compile_elem(c, v, cur, child);
+    }
+    ents.push_back(E);
+  }
+  // metadata expansion: wildcard entries of the labels/annotations maps read their key from a slot
+  if (meta_site >= 0) {
+    c.rs.pnodes[id].flags |= PF_META;
+    c.rs.pnodes[id].meta = (uint8_t)meta_site;
+    (void)meta_key;
+  }
+  PNode& P = c.rs.pnodes[id];
+  P.first = (uint32_t)c.rs.pentries.size();
+  P.n = (uint32_t)ents.size();
+  for (auto& e : ents) c.rs.pentries.push_back(e);
+  (void)labels_slot0; (void)ann_slot0; (void)labels_pkey; (void)ann_pkey;
+  return id;
+}
+
+uint32_t compile_elem(Cx& c, const Value& p, const std::string& path, Loc loc, int) {
+  if (loc.depth > 64) throw Fallback{"pattern nesting too deep"};
+  if (p.t == T::Obj) return compile_map(c, p, path, loc);
+  if (p.t == T::Arr) {
+    if (p.a.empty()) return new_pnode(c, P_ARR_EMPTY, path);
+    const Value& f = p.a[0];
+    if (f.t == T::Obj) {
+      if (loc.level >= MAX_IDX) throw Fallback{"arrays of maps nested deeper than the index slots"};
+      uint32_t id = new_pnode(c, P_ARR_MAPS, path);
+      Loc cl = loc;
+      cl.level++;
+      cl.loop = true;
+      cl.depth++;
+      uint32_t child = compile_elem(c, f, path + idx_ph(loc.level) + "/", cl);
+      c.rs.pnodes[id].first = child;
+      c.rs.pnodes[id].level = (uint8_t)loc.level;
+      return id;
+    }
+    if (f.t != T::Arr) {
+      uint32_t id = new_pnode(c, P_ARR_SCALAR, path);
+      uint32_t leaf = new_pnode(c, P_LEAF, path);
+      c.rs.pnodes[leaf].first = compile_leaf(c, f);
+      c.rs.pnodes[id].first = leaf;
+      return id;
+    }
+    uint32_t id = new_pnode(c, P_ARR_POS, path);
+    std::vector<uint32_t> kids;
+    Loc cl = loc;
+    cl.depth++;
+    for (size_t i = 0; i < p.a.size(); i++) kids.push_back(compile_elem(c, p.a[i], path + std::to_string(i) + "/", cl));
+    c.rs.pnodes[id].first = (uint32_t)c.rs.pool.size();
+    c.rs.pnodes[id].n = (uint32_t)kids.size();
+    for (auto k : kids) c.rs.pool.push_back(k);
+    return id;
+  }
+  uint32_t id = new_pnode(c, P_LEAF, path);
+  c.rs.pnodes[id].first = compile_leaf(c, p);
+  return id;
+}
+
+// mark EF_WILD entries: labels/annotations maps below a metadata site whose keys are wildcards
+void mark_wild_entries(Cx& c, uint32_t site_pnode) {
+  PNode& P = c.rs.pnodes[site_pnode];
+  const MetaSite& ms = c.sites[P.meta];
+  for (uint32_t e = 0; e < P.n; e++) {
+    PEntry& E = c.rs.pentries[P.first + e];
+    const std::string& key = c.rs.dict.strs[E.key];
+    if (key != "metadata" || E.child == NONE || c.rs.pnodes[E.child].kind != P_MAP) continue;
+    PNode& M = c.rs.pnodes[E.child];
+    for (uint32_t f = 0; f < M.n; f++) {
+      PEntry& L = c.rs.pentries[M.first + f];
+      const std::string& lk = c.rs.dict.strs[L.key];
+      int tag = lk == "labels" ? 0 : lk == "annotations" ? 1 : -1;
+      if (tag < 0 || L.child == NONE || c.rs.pnodes[L.child].kind != P_MAP) continue;
+      PNode& W = c.rs.pnodes[L.child];
+      uint32_t wl = tag == 0 ? ms.wild_l : ms.wild_a, nw = tag == 0 ? ms.nwild_l : ms.nwild_a;
+      uint32_t slot0 = tag == 0 ? ms.slot_l : ms.slot_a;
+      for (uint32_t g = 0; g < W.n; g++) {
+        PEntry& X = c.rs.pentries[W.first + g];
+        for (uint32_t w = 0; w < nw; w++) {
+          if (c.rs.pool[wl + 2 * w + 1] == X.key) {
+            X.flags |= EF_WILD;
+            X.slot = (uint8_t)(slot0 + w);
+            // currentPath uses the expanded key
+            std::string t = c.rs.templates[X.tmpl];
+            std::string unresolved = c.rs.dict.strs[X.key];
+            t = t.substr(0, t.size() - unresolved.size() - 1) + key_ph(slot0 + w) + "/";
+            X.tmpl = c.tmpl(t);
+            if (X.child != NONE) c.rs.pnodes[X.child].tmpl = X.tmpl;  // metadata values are leaves (strings)
+          }
+        }
+      }
+    }
+  }
+}
+
+uint32_t compile_pattern_root(Cx& c, const Value& p) {
+  c.abits.clear();
+  uint32_t root = compile_elem(c, p, "/", Loc());
+  for (uint32_t i = 0; i < c.rs.pnodes.size(); i++)
+    if (i >= root && (c.rs.pnodes[i].flags & PF_META)) mark_wild_entries(c, i);
+  return root;
+}
+
+// ---------------------------------------------------------------- match programs
+bool valid_qname(const std::string& n) {
+  if (n.empty() || n.size() > 63) return false;
+  auto an = [](char ch) { return isalnum((unsigned char)ch) != 0; };
+  if (!an(n.front()) || !an(n.back())) return false;
+  for (char ch : n) if (!(an(ch) || ch == '-' || ch == '_' || ch == '.')) return false;
+  return true;
+}
+bool valid_dns_sub(const std::string& s) {
+  if (s.empty() || s.size() > 253) return false;
+  for (auto& l : split(s, '.')) {
+    if (l.empty()) return false;
+    auto ok = [](char ch) { return (ch >= 'a' && ch <= 'z') || (ch >= '0' && ch <= '9'); };
+    if (!ok(l.front()) || !ok(l.back())) return false;
+    for (char ch : l) if (!(ok(ch) || ch == '-')) return false;
+  }
+  return true;
+}
+bool valid_label_key(const std::string& k) {
+  auto p = split(k, '/');
+  if (p.size() == 1) return valid_qname(p[0]);
+  if (p.size() == 2) return !p[0].empty() && valid_dns_sub(p[0]) && valid_qname(p[1]);
+  return false;
+}
+bool valid_label_value(const std::string& v) { return v.empty() || valid_qname(v); }
+
+uint32_t compile_selector(Cx& c, const Value* sel) {
+  SelDesc sd{};
+  sd.reqs = (uint32_t)c.rs.reqs.size();
+  const Value* ml = sel->get("matchLabels");
+  size_t nml = ml && ml->t == T::Obj ? ml->o.size() : 0;
+  bool anywild = false;
+  if (nml) {
+    for (auto& kv : ml->o) {
+      std::string k = kv.first, v = kv.second.t == T::Str ? kv.second.s : "";
+      SelReq r{};
+      if (has_wild(k) || has_wild(v)) {
+        anywild = true;
+        r.op = RQ_WILD;
+        r.key = c.sid(k);
+        r.vals = c.sid(v);
+        std::string k0 = k, v0 = v;
+        for (auto& ch : k0) if (ch == '*' || ch == '?') ch = '0';
+        for (auto& ch : v0) if (ch == '*' || ch == '?') ch = '0';
+        if (valid_label_key(k0) && valid_label_value(v0)) { r.rkey = c.sid(k0); r.rval = c.sid(v0); }
+        else { r.rkey = NONE; r.rval = NONE; }
+      } else {
+        r.op = RQ_EQ;
+        r.key = c.sid(k);
+        r.vals = (uint32_t)c.rs.pool.size();
+        r.nvals = 1;
+        c.rs.pool.push_back(c.sid(v));
+        if (!valid_label_key(k) || !valid_label_value(v)) sd.invalid = 1;
+      }
+      c.rs.reqs.push_back(r);
+    }
+    if (anywild && nml > 1) throw Fallback{"wildcard matchLabels beside other entries (collision decided by Go map order)"};
+  }
+  const Value* me = sel->get("matchExpressions");
+  if (me && me->t == T::Arr)
+    for (auto& e : me->a) {
+      SelReq r{};
+      std::string op = e.str_or("operator");
+      if (op == "In") r.op = RQ_IN;
+      else if (op == "NotIn") r.op = RQ_NOTIN;
+      else if (op == "Exists") r.op = RQ_EXISTS;
+      else if (op == "DoesNotExist") r.op = RQ_NOTEXISTS;
+      else { sd.invalid = 1; continue; }
+      std::string key = e.str_or("key");
+      r.key = c.sid(key);
+      auto vals = strs(e.get("values"));
+      r.vals = (uint32_t)c.rs.pool.size();
+      r.nvals = (uint32_t)vals.size();
+      for (auto& v : vals) { c.rs.pool.push_back(c.sid(v)); if (!valid_label_value(v)) sd.invalid = 1; }
+      if (!valid_label_key(key)) sd.invalid = 1;
+      if ((r.op == RQ_IN || r.op == RQ_NOTIN) && vals.empty()) sd.invalid = 1;
+      if ((r.op == RQ_EXISTS || r.op == RQ_NOTEXISTS) && !vals.empty()) sd.invalid = 1;
+      c.rs.reqs.push_back(r);
+    }
+  sd.nreqs = (uint32_t)c.rs.reqs.size() - sd.reqs;
+  c.rs.sels.push_back(sd);
+  return (uint32_t)c.rs.sels.size() - 1;
+}
+
+bool rd_zero(const Value* rd) {
+  if (nil(rd)) return true;
+  for (const char* k : {"kinds", "names", "namespaces", "annotations", "selector", "namespaceSelector"})
+    if (!nil(rd->get(k))) return false;
+  return rd->str_or("name").empty();
+}
+
+uint32_t compile_filter(Cx& c, const Value* f, const Value* rd, bool* empty_may) {
+  Filter F{};
+  F.name = NONE;
+  if (rd_zero(rd)) F.flags |= FF_ZERO_RD;
+  if (f && (!nil(f->get("roles")) || !nil(f->get("clusterRoles")) || !nil(f->get("subjects")))) {
+    bool any = !strs(f->get("roles")).empty() || !strs(f->get("clusterRoles")).empty() || nonempty_list(f->get("subjects"));
+    if (any) F.flags |= FF_USERINFO;
+    const Value* subj = f->get("subjects");
+    if (subj && subj->t == T::Arr)
+      for (auto& s : subj->a) if (s.str_or("name").empty()) throw Fallback{"subject with empty name (mock/user matching)"};
+  }
+  auto kinds = strs(rd ? rd->get("kinds") : nullptr);
+  F.kinds = (uint32_t)c.rs.kinds.size();
+  F.nkinds = (uint16_t)kinds.size();
+  bool star = false, emptykind = kinds.empty();
+  for (auto& k : kinds) {
+    KindDesc K{};
+    if (k == "*") { K.kind = NONE; star = true; }
+    else {
+      std::string gv, kind;
+      kind_from_gvk(k, gv, kind);
+      K.kind = c.sid(kind);
+      if (kind.empty()) emptykind = true;
+      if (gv.empty()) K.gv_mode = 0;
+      else if (gv.find('*') != std::string::npos) {
+        K.gv_mode = 2;
+        std::string pre = gv;
+        if (!pre.empty() && pre.back() == '*') pre.pop_back();
+        K.g = c.sid(pre);
+      } else {
+        size_t sl = std::count(gv.begin(), gv.end(), '/');
+        if (gv == "/") { K.gv_mode = 1; K.g = SID_EMPTY; K.v = SID_EMPTY; }
+        else if (sl == 0) { K.gv_mode = 1; K.g = SID_EMPTY; K.v = c.sid(gv); }
+        else if (sl == 1) { K.gv_mode = 1; K.g = c.sid(gv.substr(0, gv.find('/'))); K.v = c.sid(gv.substr(gv.find('/') + 1)); }
+        else K.gv_mode = 3;
+      }
+    }
+    c.rs.kinds.push_back(K);
+  }
+  if (star) F.flags |= FF_KINDS_STAR;
+  if (star || emptykind) *empty_may = true;
+  std::string name = rd ? rd->str_or("name") : "";
+  if (!name.empty()) F.name = c.sid(name);
+  auto names = strs(rd ? rd->get("names") : nullptr);
+  F.names = (uint32_t)c.rs.pool.size();
+  F.nnames = (uint32_t)names.size();
+  for (auto& n : names) c.rs.pool.push_back(c.sid(n));
+  auto nss = strs(rd ? rd->get("namespaces") : nullptr);
+  F.nss = (uint32_t)c.rs.pool.size();
+  F.nnss = (uint32_t)nss.size();
+  for (auto& n : nss) c.rs.pool.push_back(c.sid(n));
+  const Value* ann = rd ? rd->get("annotations") : nullptr;
+  F.ann = (uint32_t)c.rs.pool.size();
+  if (ann && ann->t == T::Obj) {
+    F.nann = (uint32_t)ann->o.size();
+    for (auto& kv : ann->o) { c.rs.pool.push_back(c.sid(kv.first)); c.rs.pool.push_back(c.sid(kv.second.t == T::Str ? kv.second.s : "")); }
+  }
+  const Value* sel = rd ? rd->get("selector") : nullptr;
+  const Value* nsel = rd ? rd->get("namespaceSelector") : nullptr;
+  // selector and namespaceSelector occupy two consecutive SelDesc slots
+  F.sel = (uint32_t)c.rs.sels.size();
+  {
+    Value emptysel = Value::O();
+    uint32_t a = compile_selector(c, nil(sel) ? &emptysel : sel);
+    uint32_t b = compile_selector(c, nil(nsel) ? &emptysel : nsel);
+    (void)a; (void)b;
+  }
+  if (!nil(sel)) F.flags |= FF_HAS_SEL;
+  if (!nil(nsel)) F.flags |= FF_HAS_NSSEL;
+  c.rs.filters.push_back(F);
+  return (uint32_t)c.rs.filters.size() - 1;
+}
+
+MatchBlock compile_block(Cx& c, const Value* mr, bool is_match, bool* empty_may) {
+  MatchBlock B{};
+  if (nil(mr)) { B.mode = is_match ? MM_PLAIN : MM_NONE; if (is_match) { B.filters = (uint32_t)c.rs.filters.size(); compile_filter(c, nullptr, nullptr, empty_may); B.nfilters = 1; } return B; }
+  const Value* any = mr->get("any");
+  const Value* all = mr->get("all");
+  std::vector<std::pair<const Value*, const Value*>> fl;
+  if (nonempty_list(any)) { B.mode = MM_ANY; for (auto& f : any->a) fl.push_back({&f, f.get("resources")}); }
+  else if (nonempty_list(all)) { B.mode = MM_ALL; for (auto& f : all->a) fl.push_back({&f, f.get("resources")}); }
+  else { B.mode = MM_PLAIN; fl.push_back({mr, mr->get("resources")}); }
+  // compile filters contiguously
+  std::vector<uint32_t> ids;
+  bool em = false;
+  for (auto& p : fl) ids.push_back(compile_filter(c, p.first, p.second, &em));
+  if (is_match && em) *empty_may = true;
+  // filters were appended in order; selectors appended inside keep filter indices contiguous
+  B.filters = ids.empty() ? (uint32_t)c.rs.filters.size() : ids[0];
+  B.nfilters = (uint32_t)ids.size();
+  return B;
+}
+
+// ---------------------------------------------------------------- PodSecurity
+uint32_t control_slots(const std::string& control) {  // pkg/pss/utils/mapping.go:45-111 -> check-version slots
+  auto S = [](std::initializer_list<int> l) { uint32_t m = 0; for (int s : l) m |= 1u << s; return m; };
+  // slot order as kyv_pss.h PssSlot
+  if (control == "Capabilities") return S({3, 4, 5});
+  if (control == "Seccomp") return S({15, 16, 17, 18});
+  if (control == "Privileged Containers") return S({9});
+  if (control == "Host Ports") return S({8});
+  if (control == "/proc Mount Type") return S({10});
+  if (control == "AppArmor") return S({2});
+  if (control == "SELinux") return S({14});
+  if (control == "Host Namespaces") return S({6});
+  if (control == "HostPath Volumes") return S({7});
+  if (control == "Sysctls") return S({19});
+  if (control == "HostProcess") return S({20});
+  if (control == "Privilege Escalation") return S({0, 1});
+  if (control == "Running as Non-root") return S({12});
+  if (control == "Running as Non-root user") return S({13});
+  if (control == "Volume Types") return S({11});
+  return 0;
+}
+
+bool pss_version_ok(const std::string& v) {  // api.ParseVersion / "latest"
+  if (v.empty() || v == "latest") return true;
+  if (v.size() < 4 || v.compare(0, 3, "v1.") != 0) return false;
+  std::string m = v.substr(3);
+  if (m.size() > 1 && m[0] == '0') return false;
+  for (char ch : m) if (!isdigit((unsigned char)ch)) return false;
+  return !m.empty() && m.size() < 10;
+}
+
+uint32_t compile_pss(Cx& c, const Value& ps) {
+  PssDesc d{};
+  if (ps.str_or("level") == "baseline") d.flags |= PSS_BASELINE;
+  if (!pss_version_ok(ps.str_or("version"))) d.flags |= PSS_BAD_VERSION;
+  const Value* ex = ps.get("exclude");
+  std::vector<uint32_t> recs;
+  if (ex && ex->t == T::Arr)
+    for (auto& e : ex->a) {
+      uint32_t off = (uint32_t)c.rs.pool.size();
+      auto imgs = strs(e.get("images"));
+      c.rs.pool.push_back(control_slots(e.str_or("controlName")));
+      c.rs.pool.push_back((uint32_t)imgs.size());
+      for (auto& i : imgs) c.rs.pool.push_back(c.sid(i));
+      recs.push_back(off);
+    }
+  d.excl = (uint32_t)c.rs.pool.size();
+  d.nexcl = (uint32_t)recs.size();
+  for (auto r : recs) c.rs.pool.push_back(r);
+  c.rs.pss.push_back(d);
+  return (uint32_t)c.rs.pss.size() - 1;
+}
+
+// ---------------------------------------------------------------- rule classification
+bool contains_vars(const Value& v) {
+  auto hit = [](const std::string& s) { return s.find("{{") != std::string::npos || s.find("$(") != std::string::npos; };
+  if (v.t == T::Str) return hit(v.s);
+  if (v.t == T::Arr) { for (auto& e : v.a) if (contains_vars(e)) return true; return false; }
+  if (v.t == T::Obj) { for (auto& kv : v.o) if (hit(kv.first) || contains_vars(kv.second)) return true; }
+  return false;
+}
+
+std::string fallback_reason(const Value& r) {  // validator.validate dispatch (validation.go:276-317)
+  const Value* val = r.get("validate");
+  if (nonempty(r.get("context"))) return "context";
+  if (!nil(r.get("preconditions"))) return "preconditions";
+  if (nonempty(r.get("verifyImages"))) return "verifyImages";
+  if (!val) return "";
+  if (!nil(val->get("deny"))) return "deny";
+  if ((val->get("pattern") && contains_vars(*val->get("pattern"))) || (val->get("anyPattern") && contains_vars(*val->get("anyPattern"))))
+    return "variables";
+  if (nil(val->get("pattern")) && nil(val->get("anyPattern")) && nil(val->get("podSecurity")) && nonempty(val->get("foreach")))
+    return "foreach";
+  if (!nil(val->get("manifests"))) return "manifests";
+  return "";
+}
+
+}  // namespace
+
+Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
+  auto rs = std::make_unique<Ruleset>();
+  try {
+    seed_dict(rs->dict);
+    std::vector<Value> docs = pj::parse_many(json, len, true);
+    Cx c{*rs};
+    for (auto& pol : docs) {
+      if (pol.t != T::Obj) continue;
+      std::string kind = pol.str_or("kind");
+      if (kind != "ClusterPolicy" && kind != "Policy") continue;
+      PolicyMeta pm;
+      const Value* meta = pol.get("metadata");
+      pm.name = meta ? meta->str_or("name") : "";
+      pm.ns = meta ? meta->str_or("namespace") : "";
+      pm.kind = kind;
+      const Value* ann = meta ? meta->get("annotations") : nullptr;
+      pm.scored_false = ann && ann->str_or("policies.kyverno.io/scored") == "false";
+      const Value* spec = pol.get("spec");
+      pm.apply_one = spec && spec->str_or("applyRules") == "One";
+      pm.failure_action = spec ? spec->str_or("validationFailureAction", "Audit") : "Audit";
+      uint32_t pidx = (uint32_t)rs->policies.size();
+      pm.first_rule = (uint32_t)rs->rules.size();
+      for (auto& r : compute_rules(pol)) {
+        pm.all_rule_names.push_back(r.str_or("name"));
+        const Value* val = r.get("validate");
+        bool hasValidate = val && val->t == T::Obj && !val->o.empty();
+        if (!hasValidate && !nonempty(r.get("verifyImages"))) continue;  // no response (validation.go:144-149)
+        RuleDesc rd{};
+        RuleMeta rm;
+        rm.name = r.str_or("name");
+        rm.message = val ? val->str_or("message") : "";
+        rm.policy = pidx;
+        rm.message_vars = rm.message.find("{{") != std::string::npos || rm.message.find("$(") != std::string::npos;
+        rd.policy = pidx;
+        size_t mark_p = rs->pnodes.size(), mark_e = rs->pentries.size(), mark_l = rs->leaves.size(),
+               mark_a = rs->atoms.size(), mark_pool = rs->pool.size(), mark_t = rs->templates.size();
+        try {
+          bool em = false;
+          rd.match = compile_block(c, r.get("match"), true, &em);
+          rd.exclude = compile_block(c, r.get("exclude"), false, &em);
+          rd.empty_may_match = em;
+          std::string why = fallback_reason(r);
+          c.nslots = 0;
+          c.sites.clear();
+          if (!why.empty()) {
+            rd.kind = RK_FALLBACK;
+            rm.reason = why;
+          } else if (val && !nil(val->get("pattern"))) {
+            rd.kind = RK_PATTERN;
+            rd.root = compile_pattern_root(c, *val->get("pattern"));
+          } else if (val && !nil(val->get("anyPattern"))) {
+            const Value* ap = val->get("anyPattern");
+            if (ap->t != T::Arr) {
+              rd.kind = RK_ERROR;
+              rm.reason = "failed to deserialize anyPattern, expected type array";
+            } else {
+              std::vector<uint32_t> roots;
+              for (auto& p : ap->a) roots.push_back(compile_pattern_root(c, p));
+              if (roots.size() > MAX_ALTS) throw Fallback{"too many anyPattern alternatives"};
+              rd.kind = RK_ANYPATTERN;
+              rd.root = (uint32_t)rs->pool.size();
+              rd.nalts = (uint32_t)roots.size();
+              for (auto x : roots) rs->pool.push_back(x);
+            }
+          } else if (val && !nil(val->get("podSecurity"))) {
+            rd.kind = RK_PSS;
+            rd.root = compile_pss(c, *val->get("podSecurity"));
+            rm.pss_level = val->get("podSecurity")->str_or("level");
+            rm.pss_version = val->get("podSecurity")->str_or("version");
+          } else {
+            continue;  // "invalid validation rule": no response
+          }
+          rd.meta_sites = (uint32_t)rs->metas.size();
+          rd.nmeta = (uint32_t)c.sites.size();
+          for (auto& s : c.sites) rs->metas.push_back(s);
+          rd.nslots = (uint8_t)c.nslots;
+          rd.uses_meta = c.sites.empty() ? 0 : 1;
+        } catch (Fallback& f) {
+          rs->pnodes.resize(mark_p); rs->pentries.resize(mark_e); rs->leaves.resize(mark_l);
+          rs->atoms.resize(mark_a); rs->templates.resize(mark_t);
+          (void)mark_pool;
+          rd.kind = RK_FALLBACK;
+          rm.reason = f.why;
+        }
+        rm.kind = rd.kind;
+        rs->rules.push_back(rd);
+        rs->meta.push_back(rm);
+      }
+      pm.nrules = (uint32_t)rs->rules.size() - pm.first_rule;
+      rs->policies.push_back(pm);
+    }
+    return rs.release();
+  } catch (std::exception& e) {
+    if (err) *err = e.what();
+    return nullptr;
+  }
+}
+
+}  // namespace kyv

@@ -1,0 +1,433 @@
+// HIP execution of the batched validate path on MI355X (gfx950).
+//
+// eval_kernel: one lane per resource, the rule index uniform across the wavefront, so every lane of a
+// wave walks the same compiled program over a different resource's node table (divergence only where
+// the resources differ: array trip counts, absent optional keys).  The per-lane DFS frame stack lives in
+// LDS (lane-strided, conflict-free), verdicts are written rule-major (coalesced bytes), failing-path
+// records are compacted with a wave ballot + one atomic per wave, and per-rule status counters are
+// reduced in LDS per block before one atomic per (block, rule, status).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kyv_host.h"
+#include "kyv_pss.h"
+
+namespace kyv {
+
+#define HIP_OK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+  } while (0)
+
+// ---------------------------------------------------------------- device images
+struct Packer {
+  std::vector<uint8_t> host;
+  template <class X>
+  size_t add(const std::vector<X>& v) {
+    size_t off = (host.size() + 255) & ~(size_t)255;
+    host.resize(off + v.size() * sizeof(X) + 16);
+    if (!v.empty()) memcpy(host.data() + off, v.data(), v.size() * sizeof(X));
+    return off;
+  }
+};
+
+struct DevRuleset {
+  int device = -1;
+  uint8_t* base = nullptr;
+  size_t bytes = 0;
+  size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool;
+};
+
+struct DeviceResults {
+  uint8_t* status = nullptr;
+  uint32_t* pss_fails = nullptr;
+  uint32_t* pss_slot = nullptr;
+  FailRec* recs = nullptr;
+  uint32_t* nrecs = nullptr;
+  unsigned long long* counts = nullptr;
+  uint32_t max_recs = 0;
+  uint32_t npss = 0;
+  size_t nres = 0, nrules = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+static void free_dev_results(DeviceResults& d) {
+  hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
+  if (d.e0) hipEventDestroy(d.e0);
+  if (d.e1) hipEventDestroy(d.e1);
+  if (d.stream) hipStreamDestroy(d.stream);
+  d = DeviceResults();
+}
+
+struct DevBatch {
+  int device = -1;
+  DeviceResults* out = nullptr;  // result buffers + stream, resident across evaluations
+  uint8_t* base = nullptr;
+  size_t bytes = 0;
+  size_t o_nodes, o_hdr, o_faux, o_soff, o_slen, o_sflags, o_sdur, o_sqty, o_sf64, o_heap, o_nsloff, o_nslkv;
+  double upload_ms = 0;
+};
+
+static DevRuleset* upload_ruleset(const Ruleset& rs, int device) {
+  HIP_OK(hipSetDevice(device));
+  auto* d = new DevRuleset();
+  d->device = device;
+  Packer p;
+  d->o_rules = p.add(rs.rules);
+  d->o_filters = p.add(rs.filters);
+  d->o_kinds = p.add(rs.kinds);
+  d->o_sels = p.add(rs.sels);
+  d->o_reqs = p.add(rs.reqs);
+  d->o_pn = p.add(rs.pnodes);
+  d->o_pe = p.add(rs.pentries);
+  d->o_leaves = p.add(rs.leaves);
+  d->o_atoms = p.add(rs.atoms);
+  d->o_metas = p.add(rs.metas);
+  d->o_pss = p.add(rs.pss);
+  d->o_pool = p.add(rs.pool);
+  d->bytes = p.host.size();
+  HIP_OK(hipMalloc(&d->base, d->bytes));
+  HIP_OK(hipMemcpy(d->base, p.host.data(), d->bytes, hipMemcpyHostToDevice));
+  return d;
+}
+
+static DevBatch* upload_batch(const Batch& b, int device) {
+  HIP_OK(hipSetDevice(device));
+  auto t0 = std::chrono::steady_clock::now();
+  auto* d = new DevBatch();
+  d->device = device;
+  Packer p;
+  d->o_nodes = p.add(b.nodes);
+  d->o_hdr = p.add(b.hdr);
+  d->o_faux = p.add(b.faux);
+  d->o_soff = p.add(b.str_off);
+  d->o_slen = p.add(b.str_len);
+  d->o_sflags = p.add(b.str_flags);
+  d->o_sdur = p.add(b.str_dur);
+  d->o_sqty = p.add(b.str_qty);
+  d->o_sf64 = p.add(b.str_f64);
+  d->o_heap = p.add(b.heap);
+  d->o_nsloff = p.add(b.nsl_off);
+  d->o_nslkv = p.add(b.nsl_kv);
+  d->bytes = p.host.size();
+  HIP_OK(hipMalloc(&d->base, d->bytes));
+  HIP_OK(hipMemcpy(d->base, p.host.data(), d->bytes, hipMemcpyHostToDevice));
+  d->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return d;
+}
+
+static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, const DevRuleset* dr, const uint8_t* bbase,
+                      const DevBatch* db) {
+  View v{};
+  if (db) {
+    v.nodes = (const Node*)(bbase + db->o_nodes);
+    v.hdr = (const ResHeader*)(bbase + db->o_hdr);
+    v.faux = (const FloatAux*)(bbase + db->o_faux);
+    v.str_off = (const uint32_t*)(bbase + db->o_soff);
+    v.str_len = (const uint32_t*)(bbase + db->o_slen);
+    v.str_flags = (const uint32_t*)(bbase + db->o_sflags);
+    v.str_dur = (const int64_t*)(bbase + db->o_sdur);
+    v.str_qty = (const int64_t*)(bbase + db->o_sqty);
+    v.str_f64 = (const double*)(bbase + db->o_sf64);
+    v.heap = bbase + db->o_heap;
+    v.nsl_off = (const uint32_t*)(bbase + db->o_nsloff);
+    v.nsl_kv = (const uint32_t*)(bbase + db->o_nslkv);
+  } else {
+    v.nodes = b.nodes.data(); v.hdr = b.hdr.data(); v.faux = b.faux.data();
+    v.str_off = b.str_off.data(); v.str_len = b.str_len.data(); v.str_flags = b.str_flags.data();
+    v.str_dur = b.str_dur.data(); v.str_qty = b.str_qty.data(); v.str_f64 = b.str_f64.data();
+    v.heap = b.heap.data(); v.nsl_off = b.nsl_off.data(); v.nsl_kv = b.nsl_kv.data();
+  }
+  v.nres = (uint32_t)b.hdr.size();
+  v.nrules = (uint32_t)rs.rules.size();
+  if (dr) {
+    v.rules = (const RuleDesc*)(rbase + dr->o_rules);
+    v.filters = (const Filter*)(rbase + dr->o_filters);
+    v.kinds = (const KindDesc*)(rbase + dr->o_kinds);
+    v.sels = (const SelDesc*)(rbase + dr->o_sels);
+    v.reqs = (const SelReq*)(rbase + dr->o_reqs);
+    v.pn = (const PNode*)(rbase + dr->o_pn);
+    v.pe = (const PEntry*)(rbase + dr->o_pe);
+    v.leaves = (const Leaf*)(rbase + dr->o_leaves);
+    v.atoms = (const Atom*)(rbase + dr->o_atoms);
+    v.metas = (const MetaSite*)(rbase + dr->o_metas);
+    v.pss = (const PssDesc*)(rbase + dr->o_pss);
+    v.pool = (const uint32_t*)(rbase + dr->o_pool);
+  } else {
+    v.rules = rs.rules.data(); v.filters = rs.filters.data(); v.kinds = rs.kinds.data(); v.sels = rs.sels.data();
+    v.reqs = rs.reqs.data(); v.pn = rs.pnodes.data(); v.pe = rs.pentries.data(); v.leaves = rs.leaves.data();
+    v.atoms = rs.atoms.data(); v.metas = rs.metas.data(); v.pss = rs.pss.data(); v.pool = rs.pool.data();
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------- kernels
+constexpr int WAVE = 64;
+constexpr int BLOCK = 64;        // one wave per workgroup; LDS = depth * 64 * 16 B
+constexpr int RECS_PER_PAIR = MAX_ALTS;
+
+struct DevOut {
+  uint8_t* status;         // [rule][res]
+  uint32_t* pss_fails;     // [pss rule slot][res]
+  const uint32_t* pss_slot;// rule -> pss slot or NONE
+  FailRec* recs;
+  uint32_t* nrecs;         // global record counter
+  uint32_t max_recs;
+  unsigned long long* counts;  // [rule][NSTATUS]
+  uint32_t rule_lo, rule_hi;   // rule range handled by this launch
+};
+
+__global__ void __launch_bounds__(BLOCK) eval_kernel(View v, DevOut o, int depth) {
+  extern __shared__ Frame lds_frames[];  // [depth][BLOCK]
+  const uint32_t lane = threadIdx.x;
+  const uint32_t r = blockIdx.x * BLOCK + lane;
+  const bool active = r < v.nres;
+  Stack stk{lds_frames + lane, BLOCK, depth};
+  __shared__ unsigned long long cnt[NSTATUS];
+  for (uint32_t k = o.rule_lo; k < o.rule_hi; k++) {
+    uint8_t st = ST_NONE;
+    uint32_t pf = 0, nrec = 0;
+    FailRec recs[RECS_PER_PAIR];
+    if (active) {
+      st = eval_pair(v, r, k, stk, &pf, recs, &nrec, RECS_PER_PAIR);
+      o.status[(size_t)k * v.nres + r] = st;
+      uint32_t ps = o.pss_slot[k];
+      if (ps != NONE) o.pss_fails[(size_t)ps * v.nres + r] = pf;
+    }
+    // compact failing-path records: one atomic per wave
+    unsigned long long has = __ballot(nrec > 0);
+    if (has) {
+      uint32_t mine = nrec;
+      // prefix sum of record counts across the wave (records are rare: lane-serial scan is fine)
+      uint32_t excl = 0, total = 0;
+      for (int l = 0; l < WAVE; l++) {
+        uint32_t n = __shfl(mine, l);
+        if (l < (int)lane) excl += n;
+        total += n;
+      }
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(o.nrecs, total);
+      base = __shfl(base, 0);
+      for (uint32_t i = 0; i < mine; i++) {
+        uint32_t at = base + excl + i;
+        if (at < o.max_recs) o.recs[at] = recs[i];
+      }
+    }
+    // per-rule status counts: wave ballots -> one atomic per status present
+    for (int s = 0; s < NSTATUS; s++) {
+      unsigned long long m = __ballot(active && (st & 7) == s);
+      if (m && lane == 0) atomicAdd(&o.counts[(size_t)k * NSTATUS + s], (unsigned long long)__popcll(m));
+    }
+  }
+  (void)cnt;
+}
+
+// ---------------------------------------------------------------- host entry
+// Frames the walk of one pattern node can push (eval_pattern): a map frame stays while its entries are
+// walked, array frames while their elements are, an existence frame while its candidates are.
+static int pattern_depth(const Ruleset& rs, uint32_t pn, int guard) {
+  if (pn == NONE || guard > MAX_DEPTH) return MAX_DEPTH + 1;
+  const PNode& P = rs.pnodes[pn];
+  int d = 0;
+  switch (P.kind) {
+    case P_MAP:
+      for (uint32_t e = 0; e < P.n; e++) {
+        const PEntry& E = rs.pentries[P.first + e];
+        if (E.handler == H_STAR || E.handler == H_NEGATION || E.child == NONE) continue;
+        if (E.handler == H_EXISTENCE || E.handler == H_EXIST_BADPAT) {
+          uint32_t npat = rs.pool[E.child];
+          for (uint32_t j = 0; j < npat; j++) d = std::max(d, 1 + pattern_depth(rs, rs.pool[E.child + 1 + j], guard + 2));
+        } else {
+          d = std::max(d, pattern_depth(rs, E.child, guard + 1));
+        }
+      }
+      return 1 + d;
+    case P_ARR_MAPS: return 1 + pattern_depth(rs, P.first, guard + 1);
+    case P_ARR_POS:
+      for (uint32_t i = 0; i < P.n; i++) d = std::max(d, pattern_depth(rs, rs.pool[P.first + i], guard + 1));
+      return 1 + d;
+    default: return 0;
+  }
+}
+
+// LDS frames per lane: the deepest compiled pattern (clamped; deeper walks end in ST_FALLBACK at run time)
+static int ruleset_depth(const Ruleset& rs) {
+  int d = 1;
+  for (auto& rd : rs.rules) {
+    if (rd.kind == RK_PATTERN) d = std::max(d, pattern_depth(rs, rd.root, 0));
+    else if (rd.kind == RK_ANYPATTERN)
+      for (uint32_t a = 0; a < rd.nalts; a++) d = std::max(d, pattern_depth(rs, rs.pool[rd.root + a], 0));
+  }
+  return std::min(d, (int)MAX_DEPTH);
+}
+
+
+// GPU evaluation of every (resource, rule) pair. Device images, result buffers and the stream stay resident
+// per batch; `copy_back` false keeps the verdicts on the device (bench mode).
+void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw std::runtime_error("no HIP device available (GPU backend requested)");
+  if (device < 0 || device >= ndev) throw std::runtime_error("device index out of range");
+  HIP_OK(hipSetDevice(device));
+  Ruleset& mrs = const_cast<Ruleset&>(rs);
+  Batch& mb = const_cast<Batch&>(b);
+  if ((int)mrs.dev.size() <= device) mrs.dev.resize(device + 1, nullptr);
+  if ((int)mb.dev.size() <= device) mb.dev.resize(device + 1, nullptr);
+  if (!mrs.dev[device]) mrs.dev[device] = upload_ruleset(rs, device);
+  if (!mb.dev[device]) mb.dev[device] = upload_batch(b, device);
+  DevRuleset* dr = (DevRuleset*)mrs.dev[device];
+  DevBatch* db = (DevBatch*)mb.dev[device];
+  View v = make_view(rs, b, dr->base, dr, db->base, db);
+  size_t nres = b.hdr.size(), nrules = rs.rules.size();
+  if (!db->out) {
+    // one record per failing pattern / anyPattern alternative at most: exact upper bound, no overflow
+    size_t per_res = 0;
+    for (auto& rd : rs.rules)
+      per_res += rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, RECS_PER_PAIR) : 0;
+    auto* dd = new DeviceResults();
+    DeviceResults& d = *dd;
+    d.nres = nres;
+    d.nrules = nrules;
+    std::vector<uint32_t> pss_slot(nrules, NONE);
+    for (size_t k = 0; k < nrules; k++) if (rs.rules[k].kind == RK_PSS) pss_slot[k] = d.npss++;
+    size_t mr = std::max<size_t>(nres * per_res, 1);
+    if (mr > 0xFFFFFFF0u) throw std::runtime_error("batch too large for one failure-record buffer");
+    d.max_recs = (uint32_t)mr;
+    HIP_OK(hipMalloc(&d.status, std::max<size_t>(1, nres * nrules)));
+    HIP_OK(hipMalloc(&d.pss_fails, std::max<size_t>(4, (size_t)d.npss * nres * 4)));
+    HIP_OK(hipMalloc(&d.pss_slot, std::max<size_t>(4, nrules * 4)));
+    HIP_OK(hipMalloc(&d.recs, (size_t)d.max_recs * sizeof(FailRec)));
+    HIP_OK(hipMalloc(&d.nrecs, 4));
+    HIP_OK(hipMalloc(&d.counts, std::max<size_t>(8, nrules * NSTATUS * 8)));
+    HIP_OK(hipMemcpy(d.pss_slot, pss_slot.data(), nrules * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&d.e0));
+    HIP_OK(hipEventCreate(&d.e1));
+    db->out = dd;
+  }
+  DeviceResults& d = *db->out;
+  hipStream_t stream = d.stream;
+  DevOut o{d.status, d.pss_fails, d.pss_slot, d.recs, d.nrecs, d.max_recs, d.counts, 0, (uint32_t)nrules};
+  int depth = ruleset_depth(rs);
+  size_t lds = (size_t)depth * BLOCK * sizeof(Frame);
+  dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
+  double total_ms = 0;
+  int n = std::max(1, iters);
+  for (int it = 0; it < n; it++) {
+    HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
+    HIP_OK(hipMemsetAsync(d.counts, 0, nrules * NSTATUS * 8, stream));
+    HIP_OK(hipEventRecord(d.e0, stream));
+    if (nres && nrules) hipLaunchKernelGGL(eval_kernel, grid, dim3(BLOCK), lds, stream, v, o, depth);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(d.e1, stream));
+    HIP_OK(hipEventSynchronize(d.e1));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, d.e0, d.e1));
+    total_ms += ms;
+  }
+  if (kernel_ms_avg) *kernel_ms_avg = total_ms / n;
+  if (out) {
+    out->nres = (uint32_t)nres;
+    out->nrules = (uint32_t)nrules;
+    out->kernel_ms = total_ms / n;
+    out->h2d_ms = db->upload_ms;
+    std::vector<unsigned long long> counts(nrules * NSTATUS);
+    HIP_OK(hipMemcpy(counts.data(), d.counts, counts.size() * 8, hipMemcpyDeviceToHost));
+    for (int s = 0; s < NSTATUS; s++) out->counts[s] = 0;
+    for (size_t k = 0; k < nrules; k++)
+      for (int s = 0; s < NSTATUS; s++) out->counts[s] += (int64_t)counts[k * NSTATUS + s];
+    if (copy_back) {
+      auto t0 = std::chrono::steady_clock::now();
+      out->status.resize(nres * nrules);
+      HIP_OK(hipMemcpy(out->status.data(), d.status, nres * nrules, hipMemcpyDeviceToHost));
+      out->pss_fails.resize((size_t)d.npss * nres);
+      if (d.npss) HIP_OK(hipMemcpy(out->pss_fails.data(), d.pss_fails, out->pss_fails.size() * 4, hipMemcpyDeviceToHost));
+      uint32_t nr = 0;
+      HIP_OK(hipMemcpy(&nr, d.nrecs, 4, hipMemcpyDeviceToHost));
+      if (nr > d.max_recs) throw std::runtime_error("failure record buffer overflow");
+      out->fails.resize(nr);
+      if (nr) HIP_OK(hipMemcpy(out->fails.data(), d.recs, (size_t)nr * sizeof(FailRec), hipMemcpyDeviceToHost));
+      out->d2h_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+  }
+}
+
+// Explicit CPU backend (development / message formatting only; never selected implicitly).
+// With `account` set it also sums the algorithmic bytes of SURVEY §8(d) per pair: the header fields the
+// match program reads (16 B), every distinct node-table row the pair touches (16 B each), the verdict byte,
+// the PSS fail mask (4 B) and any failing-path records (32 B each). Dictionary columns are excluded.
+void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool account) {
+  View v = make_view(rs, b, nullptr, nullptr, nullptr, nullptr);
+  size_t nres = b.hdr.size(), nrules = rs.rules.size();
+  out->nres = (uint32_t)nres;
+  out->nrules = (uint32_t)nrules;
+  out->status.assign(nres * nrules, ST_NONE);
+  std::vector<uint32_t> pss_slot(nrules, NONE);
+  uint32_t npss = 0;
+  for (size_t k = 0; k < nrules; k++) if (rs.rules[k].kind == RK_PSS) pss_slot[k] = npss++;
+  out->pss_fails.assign((size_t)npss * nres, 0);
+  int T = std::max(1, threads);
+  std::vector<std::vector<FailRec>> recs(T);
+  std::vector<uint64_t> bytes(T, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++)
+    th.emplace_back([&, t]() {
+      Frame frames[MAX_DEPTH];
+      Stack stk{frames, 1, MAX_DEPTH};
+      FailRec fr[RECS_PER_PAIR];
+      std::vector<uint8_t> seen;
+      TouchAcct acct{nullptr, 0, 0};
+      for (size_t r = t; r < nres; r += T)
+        for (size_t k = 0; k < nrules; k++) {
+          uint32_t pf, nrec;
+          if (account) {
+            uint32_t nn = b.hdr[r].nnodes;
+            seen.assign(nn, 0);
+            acct = TouchAcct{seen.data(), nn, 0};
+            g_touch = &acct;
+          }
+          uint8_t st = eval_pair(v, (uint32_t)r, (uint32_t)k, stk, &pf, fr, &nrec, RECS_PER_PAIR);
+          if (account) {
+            g_touch = nullptr;
+            bytes[t] += 16 + 16 * acct.rows + 1 + (pss_slot[k] != NONE ? 4 : 0) + (uint64_t)nrec * sizeof(FailRec);
+          }
+          out->status[k * nres + r] = st;
+          if (pss_slot[k] != NONE) out->pss_fails[(size_t)pss_slot[k] * nres + r] = pf;
+          for (uint32_t i = 0; i < nrec; i++) recs[t].push_back(fr[i]);
+        }
+    });
+  for (auto& x : th) x.join();
+  out->fails.clear();
+  for (auto& v2 : recs) out->fails.insert(out->fails.end(), v2.begin(), v2.end());
+  for (int s = 0; s < NSTATUS; s++) out->counts[s] = 0;
+  for (uint8_t s : out->status) out->counts[s & 7]++;
+  out->alg_bytes = 0;
+  for (auto x : bytes) out->alg_bytes += x;
+}
+
+void free_device_images(Ruleset& rs, Batch* b) {
+  if (b) {
+    for (auto* p : b->dev)
+      if (p) {
+        DevBatch* d = (DevBatch*)p;
+        hipSetDevice(d->device);
+        hipFree(d->base);
+        if (d->out) { free_dev_results(*d->out); delete d->out; }
+        delete d;
+      }
+    b->dev.clear();
+  } else {
+    for (auto* p : rs.dev) if (p) { DevRuleset* d = (DevRuleset*)p; hipSetDevice(d->device); hipFree(d->base); delete d; }
+    rs.dev.clear();
+  }
+}
+
+}  // namespace kyv

@@ -1,0 +1,114 @@
+// Host-side objects behind the C-ABI handles (kyv_ruleset / kyv_batch / kyv_results).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "kyv_layout.h"
+#include "pjson.h"
+
+namespace kyv {
+
+// String dictionary: seeded with the fixed/well-known ids, then the ruleset literals; every batch copies
+// the ruleset dictionary and appends its own strings.
+struct Dict {
+  std::vector<std::string> strs;
+  std::unordered_map<std::string, uint32_t> ids;
+  uint32_t intern(const std::string& s) {
+    auto it = ids.find(s);
+    if (it != ids.end()) return it->second;
+    uint32_t id = (uint32_t)strs.size();
+    strs.push_back(s);
+    ids.emplace(s, id);
+    return id;
+  }
+  uint32_t find(const std::string& s) const {
+    auto it = ids.find(s);
+    return it == ids.end() ? NONE : it->second;
+  }
+};
+void seed_dict(Dict& d);  // fixed + well-known + volume sources, in enum order
+
+struct RuleMeta {
+  std::string name;
+  std::string message;        // validate.message
+  uint32_t policy = 0;
+  uint8_t kind = RK_NONE;
+  std::string reason;         // RK_FALLBACK / RK_PANIC / RK_ERROR reason
+  bool message_vars = false;  // message needs variable substitution (CPU)
+  std::string pss_level, pss_version;
+};
+
+struct PolicyMeta {
+  std::string name, ns, kind;
+  bool apply_one = false;
+  bool scored_false = false;       // policies.kyverno.io/scored: "false" -> fail reported as warn
+  std::string failure_action;
+  uint32_t first_rule = 0, nrules = 0;  // computed rules (incl. non-validate ones, kind RK_NONE)
+  std::vector<std::string> all_rule_names;  // every computed rule name in order (CLI "rule absent -> skip")
+};
+
+struct Ruleset {
+  Dict dict;                    // seed dictionary (fixed ids + literals)
+  std::vector<RuleDesc> rules;
+  std::vector<RuleMeta> meta;
+  std::vector<PolicyMeta> policies;
+  std::vector<Filter> filters;
+  std::vector<KindDesc> kinds;
+  std::vector<SelDesc> sels;
+  std::vector<SelReq> reqs;
+  std::vector<PNode> pnodes;
+  std::vector<PEntry> pentries;
+  std::vector<Leaf> leaves;
+  std::vector<Atom> atoms;
+  std::vector<MetaSite> metas;
+  std::vector<PssDesc> pss;
+  std::vector<uint32_t> pool;
+  std::vector<std::string> templates;  // path templates: '\x01'+slot = array index, '\x02'+slot = resolved key
+  // device copies (one per device, lazily uploaded)
+  std::vector<void*> dev;
+  ~Ruleset();
+};
+
+struct Batch {
+  const Ruleset* rs = nullptr;
+  Dict dict;                      // ruleset dict + batch strings
+  std::vector<Node> nodes;
+  std::vector<ResHeader> hdr;
+  std::vector<FloatAux> faux;
+  std::vector<uint32_t> str_off, str_len, str_flags;
+  std::vector<int64_t> str_dur, str_qty;
+  std::vector<double> str_f64;
+  std::vector<uint8_t> heap;
+  std::vector<uint32_t> nsl_off, nsl_kv;
+  std::vector<std::string> nsl_names;  // namespace name per set id
+  std::vector<void*> dev;
+  ~Batch();
+};
+
+struct FailPath {  // decoded path record
+  uint32_t res, rule, alt;
+  uint32_t tmpl;
+  uint16_t idx[MAX_IDX];
+  uint32_t key[2];
+};
+
+struct Results {
+  uint32_t nres = 0, nrules = 0;
+  std::vector<uint8_t> status;      // [rule][res]
+  std::vector<uint32_t> pss_fails;  // [rule][res] for PSS rules (empty otherwise)
+  std::vector<FailRec> fails;
+  int64_t counts[NSTATUS] = {0};
+  double kernel_ms = 0, h2d_ms = 0, d2h_ms = 0;
+  uint64_t alg_bytes = 0;           // CPU backend with KYV_EVAL_ACCOUNT_BYTES
+};
+
+// compiler / flattener entry points
+Ruleset* compile_ruleset(const char* json, size_t len, std::string* err);
+Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* nsl_json, size_t nsl_len, int threads,
+                   std::string* err);
+void derive_strings(Batch& b, size_t from, int threads);
+std::string format_path(const Ruleset& rs, const Batch& b, uint32_t tmpl, const uint16_t* idx, const uint32_t* key);
+
+}  // namespace kyv

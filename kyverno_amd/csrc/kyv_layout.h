@@ -1,0 +1,294 @@
+// Device-resident data layout shared by the host compiler/flattener and the HIP kernels.
+//
+// Resources ("batch"): every resource is a position-independent table of 16-byte nodes in DFS order;
+// container children (map entries / array elements) are contiguous, addressed relative to the resource
+// root, and map entries are sorted by key id so a key lookup can stop early.  All strings (keys and
+// values, plus the decimal / %E / %f renderings of numbers) are interned in one per-batch dictionary
+// whose first entries are the ruleset's literals, so equality tests are id compares and only wildcard
+// globs touch string bytes.
+//
+// Rules ("ruleset"): each validate rule is compiled to a match program (filters over resource header
+// columns) plus either a pattern program (pnodes/entries/leaves/atoms, traversal order fully resolved at
+// compile time, reference validate/utils.go:36-58) or a PodSecurity descriptor.
+#pragma once
+#include <cstdint>
+
+namespace kyv {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// ---------------------------------------------------------------- resource nodes
+enum NodeType : uint32_t { N_NULL = 0, N_FALSE = 1, N_TRUE = 2, N_INT = 3, N_FLOAT = 4, N_STR = 5, N_MAP = 6, N_ARR = 7 };
+
+struct Node {     // 16 bytes
+  uint32_t tk;    // type (low 4 bits) | key sid << 4 (map entries) / array index << 4 (array elements)
+  uint32_t a;     // MAP/ARR: first child (relative); STR: sid; INT/FLOAT: low 32 bits; BOOL: 0/1
+  uint32_t b;     // MAP/ARR: child count; INT/FLOAT: high 32 bits
+  uint32_t c;     // INT: sid of decimal form; FLOAT: index into float aux table; STR: unused
+};
+static_assert(sizeof(Node) == 16, "node size");
+
+inline constexpr uint32_t node_type(const Node& n) { return n.tk & 0xF; }
+inline constexpr uint32_t node_key(const Node& n) { return n.tk >> 4; }
+
+struct FloatAux {   // per float node: string forms interned in the dictionary
+  uint32_t sid_E;   // strconv.FormatFloat(v,'E',-1,64)  (compareString, pattern.go:272)
+  uint32_t sid_F;   // fmt "%f"                           (convertNumberToString, pattern.go:311)
+};
+
+// per-dictionary-string flags
+enum StrFlag : uint32_t {
+  SF_ASCII = 1u << 0,
+  SF_DUR = 1u << 1,        // time.ParseDuration ok
+  SF_QTY = 1u << 2,        // resource.ParseQuantity ok and representable as int128 nano units
+  SF_QTY_BIG = 1u << 3,    // ParseQuantity ok but beyond int128 nano -> pair falls back
+  SF_FLOAT = 1u << 4,      // strconv.ParseFloat ok
+  SF_LKEY = 1u << 5,       // valid label key (IsQualifiedName)
+  SF_LVAL = 1u << 6,       // valid label value
+  SF_MAGIC = 1u << 7,      // contains an anchor-error phrase (error.go:20-26)
+};
+
+// fixed dictionary ids (seeded first in every batch)
+enum FixedSid : uint32_t { SID_EMPTY = 0, SID_ZERO = 1, SID_TRUE = 2, SID_FALSE = 3, SID_STAR = 4, SID_FIRST_FREE = 5 };
+
+// resource flags
+enum ResFlag : uint32_t {
+  RF_MAGIC = 1u << 0,       // some string/key contains an anchor-error phrase -> pattern pairs fall back
+  RF_ANCHORISH = 1u << 1,   // some key under metadata parses as an anchor -> metadata expansion falls back
+  RF_EMPTY = 1u << 2,
+  RF_TOO_DEEP = 1u << 3,
+};
+
+struct ResHeader {          // 64 bytes, one per resource (unstructured accessors, host-computed)
+  uint32_t root;            // node offset of the resource root in the batch node array
+  uint32_t nnodes;
+  uint32_t kind;            // GetKind()
+  uint32_t gvk_kind;        // GroupVersionKind().Kind ("" when apiVersion does not parse)
+  uint32_t group, version;  // parsed apiVersion
+  uint32_t gv;              // GroupVersion().String()
+  uint32_t name, gen_name, ns;
+  uint32_t labels;          // relative node of metadata.labels when it is a map of strings, else NONE
+  uint32_t ann;             // same for annotations
+  uint32_t nsl;             // namespace-label set id, NONE if unknown
+  uint32_t flags;
+  uint32_t pad0, pad1;
+};
+static_assert(sizeof(ResHeader) == 64, "header size");
+
+// ---------------------------------------------------------------- match programs
+enum MatchMode : uint8_t { MM_NONE = 0, MM_PLAIN = 1, MM_ANY = 2, MM_ALL = 3 };
+
+enum FilterFlag : uint16_t {
+  FF_ZERO_RD = 1 << 0,        // ResourceDescription is the zero value
+  FF_USERINFO = 1 << 1,       // roles / clusterRoles / subjects present (never satisfied in background scans)
+  FF_KINDS_STAR = 1 << 2,     // kinds contains "*"
+  FF_SEL_INVALID = 1 << 3,    // selector statically invalid -> CheckSelector error
+  FF_NSSEL_INVALID = 1 << 4,
+  FF_HAS_SEL = 1 << 5,
+  FF_HAS_NSSEL = 1 << 6,
+};
+
+struct KindDesc {         // compiled kinds[] entry (pkg/utils/kube/kind.go GetKindFromGVK)
+  uint32_t kind;          // sid of the kind part (exact compare against ResHeader.gvk_kind); NONE for "*"
+  uint32_t gv_mode;       // 0 none, 1 exact group/version, 2 prefix (gv contains '*'), 3 invalid gv (never)
+  uint32_t g, v;          // mode 1: group/version sids; mode 2: g = prefix string sid
+};
+
+struct Filter {
+  uint16_t flags;
+  uint16_t nkinds;
+  uint32_t kinds;          // first KindDesc
+  uint32_t name;           // glob sid or NONE
+  uint32_t names, nnames;  // sids in u32 pool
+  uint32_t nss, nnss;
+  uint32_t ann, nann;      // pairs (key glob sid, value glob sid) in u32 pool
+  uint32_t sel, nsel;      // selector descriptors
+};
+
+enum ReqOp : uint32_t { RQ_EQ = 0, RQ_IN = 1, RQ_NOTIN = 2, RQ_EXISTS = 3, RQ_NOTEXISTS = 4, RQ_WILD = 5 };
+struct SelReq {            // one requirement; values in u32 pool
+  uint32_t op;
+  uint32_t key;            // key sid (RQ_WILD: key glob sid)
+  uint32_t vals, nvals;    // RQ_WILD: vals = value glob sid
+  uint32_t rkey, rval;     // RQ_WILD: replacement ('*','?' -> '0') key/value sids, NONE if statically invalid
+};
+struct SelDesc {
+  uint32_t reqs, nreqs;
+  uint32_t invalid;        // statically invalid (-> error)
+  uint32_t pad;
+};
+
+struct MatchBlock {
+  uint8_t mode;
+  uint8_t pad[3];
+  uint32_t filters, nfilters;
+};
+
+// ---------------------------------------------------------------- pattern programs
+enum PKind : uint8_t { P_MAP = 0, P_ARR_MAPS = 1, P_ARR_SCALAR = 2, P_ARR_POS = 3, P_ARR_EMPTY = 4, P_LEAF = 5 };
+enum PFlag : uint8_t { PF_META = 1 };
+
+struct PNode {          // 16 bytes
+  uint8_t kind;
+  uint8_t flags;
+  uint8_t level;        // ARR_MAPS: dynamic index slot
+  uint8_t meta;         // PF_META: metadata-expansion site id
+  uint32_t first;       // MAP: first entry; ARR_MAPS/ARR_SCALAR: child pnode; ARR_POS: first of n consecutive pnode ids in pool; LEAF: leaf id
+  uint32_t n;           // MAP: entries; ARR_POS: pattern elements
+  uint32_t tmpl;        // path template of this node
+};
+
+enum Handler : uint8_t { H_DEFAULT = 0, H_STAR = 1, H_EQUALITY = 2, H_CONDITION = 3, H_GLOBAL = 4, H_NEGATION = 5,
+                         H_EXISTENCE = 6, H_EXIST_BADPAT = 7 };
+enum EntryFlag : uint8_t { EF_WILD = 1 };  // key resolved at run time by metadata expansion (slot in `slot`)
+
+struct PEntry {         // 16 bytes
+  uint8_t handler;
+  uint8_t flags;
+  uint8_t abit;         // anchor-map bit (0xFF none)
+  uint8_t slot;         // EF_WILD: expansion slot
+  uint32_t key;         // sid looked up in the resource map
+  uint32_t child;       // child pnode (EXISTENCE: first of n pattern maps in pool, n in `tmpl_n`)
+  uint32_t tmpl;        // currentPath template (path + key + "/")
+};
+
+enum LeafType : uint8_t { L_NIL = 0, L_BOOL = 1, L_FLOAT = 2, L_STR = 3, L_MAP = 4, L_ARR = 5 };
+struct Leaf {           // 32 bytes
+  uint8_t type;
+  uint8_t bval;
+  uint8_t fint;         // float pattern is integral
+  uint8_t pad;
+  uint32_t exact;       // L_STR: sid of the whole pattern string
+  uint32_t groups, ngroups;  // L_STR: OR-groups (each: atoms start,count in u32 pool pairs)
+  double f;
+  int64_t fi;           // int64(pattern) (Go conversion)
+};
+
+enum AtomOp : uint8_t { A_EQ = 0, A_NE = 1, A_GT = 2, A_LT = 3, A_GE = 4, A_LE = 5, A_RANGE_IN = 6, A_RANGE_OUT = 7, A_FALSE = 8 };
+enum GlobKind : uint8_t { G_ANY = 0, G_EMPTY = 1, G_EXACT = 2, G_PREFIX = 3, G_SUFFIX = 4, G_CONTAINS = 5, G_NONEMPTY = 6,
+                          G_GENERAL = 7 };
+enum AtomFlag : uint8_t { AF_DUR = 1, AF_QTY = 2 };
+
+struct Atom {           // 48 bytes; range atoms reference two simple atoms (a, a+1)
+  uint8_t op;
+  uint8_t flags;
+  uint8_t glob;
+  uint8_t pad;
+  uint32_t pat;         // sid of the (trimmed) pattern string for compareString
+  uint32_t lit;         // sid of the literal part for PREFIX/SUFFIX/CONTAINS
+  uint32_t sub;         // RANGE_*: index of first of two sub-atoms
+  int64_t dur;
+  int64_t qlo, qhi;     // int128 nano units
+};
+
+struct MetaSite {       // metadata-expansion site (wildcards.go:62-83)
+  uint32_t has_labels;  // pattern metadata carries a labels / annotations map (type-asserted at run time)
+  uint32_t has_ann;
+  uint32_t wild_l, nwild_l;  // wildcard entries (u32 pool pairs): key glob sid, unresolved key sid
+  uint32_t wild_a, nwild_a;
+  uint32_t slot_l, slot_a;   // first slot ids
+};
+
+// well-known strings, seeded right after the fixed sids in every dictionary (K_x sid = SID_FIRST_FREE + x)
+#define KYV_WELL_KNOWN(X)                                                                                    \
+  X(METADATA, "metadata") X(LABELS, "labels") X(ANNOTATIONS, "annotations") X(SPEC, "spec")                 \
+  X(TEMPLATE, "template") X(JOBTEMPLATE, "jobTemplate") X(POD, "Pod") X(CRONJOB, "CronJob")                 \
+  X(DAEMONSET, "DaemonSet") X(DEPLOYMENT, "Deployment") X(JOB, "Job") X(STATEFULSET, "StatefulSet")          \
+  X(REPLICASET, "ReplicaSet") X(RC, "ReplicationController") X(NAMESPACE, "Namespace")                      \
+  X(CONTAINERS, "containers") X(INITCONTAINERS, "initContainers") X(EPHEMERALCONTAINERS, "ephemeralContainers") \
+  X(NAME, "name") X(IMAGE, "image") X(PORTS, "ports") X(HOSTPORT, "hostPort") X(SECCTX, "securityContext")   \
+  X(PRIVILEGED, "privileged") X(APE, "allowPrivilegeEscalation") X(RUNASNONROOT, "runAsNonRoot")            \
+  X(RUNASUSER, "runAsUser") X(SELINUX, "seLinuxOptions") X(SECCOMP, "seccompProfile") X(TYPE, "type")       \
+  X(USER, "user") X(ROLE, "role") X(CAPS, "capabilities") X(ADD, "add") X(DROP, "drop")                     \
+  X(PROCMOUNT, "procMount") X(WINOPTS, "windowsOptions") X(HOSTPROCESS, "hostProcess")                     \
+  X(HOSTNETWORK, "hostNetwork") X(HOSTPID, "hostPID") X(HOSTIPC, "hostIPC") X(SYSCTLS, "sysctls")         \
+  X(VOLUMES, "volumes") X(OS, "os") X(WINDOWS, "windows") X(ALL, "ALL")             \
+  X(NET_BIND_SERVICE, "NET_BIND_SERVICE") X(LOCALHOST, "Localhost") X(RUNTIMEDEFAULT, "RuntimeDefault")     \
+  X(UNCONFINED, "Unconfined") X(DEFAULT, "Default") X(RUNTIME_DEFAULT_PROFILE, "runtime/default")           \
+  X(UNCONFINED_LC, "unconfined") X(SECCOMP_POD_ANN, "seccomp.security.alpha.kubernetes.io/pod")             \
+  X(LEVEL, "level") X(VALUE, "value") X(CONTAINERPORT, "containerPort") X(PROTOCOL, "protocol")             \
+  X(HOSTIP, "hostIP") X(RUNASGROUP, "runAsGroup") X(FSGROUP, "fsGroup") X(SUPPGROUPS, "supplementalGroups")  \
+  X(READONLYROOTFS, "readOnlyRootFilesystem") X(LOCALHOSTPROFILE, "localhostProfile")                       \
+  X(GMSA_NAME, "gmsaCredentialSpecName") X(GMSA, "gmsaCredentialSpec") X(RUNASUSERNAME, "runAsUserName")     \
+  X(NAMESPACE_KEY, "namespace") X(APPARMOR_PREFIX, "container.apparmor.security.beta.kubernetes.io/")        \
+  X(LOCALHOST_PREFIX, "localhost/") X(SECCOMP_CONTAINER_PREFIX, "container.seccomp.security.alpha.kubernetes.io/") \
+  X(CONTAINER_T, "container_t") X(CONTAINER_INIT_T, "container_init_t") X(CONTAINER_KVM_T, "container_kvm_t") \
+  X(CAP_AUDIT_WRITE, "AUDIT_WRITE") X(CAP_CHOWN, "CHOWN") X(CAP_DAC_OVERRIDE, "DAC_OVERRIDE")               \
+  X(CAP_FOWNER, "FOWNER") X(CAP_FSETID, "FSETID") X(CAP_KILL, "KILL") X(CAP_MKNOD, "MKNOD")                  \
+  X(CAP_SETFCAP, "SETFCAP") X(CAP_SETGID, "SETGID") X(CAP_SETPCAP, "SETPCAP") X(CAP_SETUID, "SETUID")        \
+  X(CAP_SYS_CHROOT, "SYS_CHROOT") X(SYSCTL_SHM, "kernel.shm_rmid_forced")                                    \
+  X(SYSCTL_PORTRANGE, "net.ipv4.ip_local_port_range") X(SYSCTL_SYNCOOKIES, "net.ipv4.tcp_syncookies")        \
+  X(SYSCTL_PINGRANGE, "net.ipv4.ping_group_range") X(SYSCTL_UNPRIV, "net.ipv4.ip_unprivileged_port_start")   \
+  X(FAKE, "fake")
+
+enum WellKnown : uint32_t {
+#define KYV_WK_ENUM(id, s) K_##id,
+  KYV_WELL_KNOWN(KYV_WK_ENUM)
+#undef KYV_WK_ENUM
+  K_COUNT
+};
+#define KSID(id) (SID_FIRST_FREE + K_##id)
+
+// typed VolumeSource members: the 8 allowed by restrictedVolumes first, then the reference switch order
+// used to name a forbidden source (pod-security-admission policy/check_restrictedVolumes.go)
+#define KYV_VOLUME_SOURCES(X)                                                                                \
+  X(configMap) X(csi) X(downwardAPI) X(emptyDir) X(ephemeral) X(persistentVolumeClaim) X(projected) X(secret) \
+  X(hostPath) X(gcePersistentDisk) X(awsElasticBlockStore) X(gitRepo) X(nfs) X(iscsi) X(glusterfs) X(rbd)     \
+  X(flexVolume) X(cinder) X(cephfs) X(flocker) X(fc) X(azureFile) X(vsphereVolume) X(quobyte) X(azureDisk)    \
+  X(photonPersistentDisk) X(portworxVolume) X(scaleIO) X(storageos)
+enum VolumeSource : uint32_t {
+#define KYV_VS_ENUM(id) V_##id,
+  KYV_VOLUME_SOURCES(KYV_VS_ENUM)
+#undef KYV_VS_ENUM
+  V_COUNT
+};
+constexpr uint32_t V_ALLOWED = 8;
+#define VSID(id) (SID_FIRST_FREE + K_COUNT + V_##id)
+constexpr uint32_t SID_SEED_END = SID_FIRST_FREE + K_COUNT + V_COUNT;
+
+// ---------------------------------------------------------------- PodSecurity
+enum PssFlag : uint32_t { PSS_BASELINE = 1, PSS_BAD_VERSION = 2 };
+struct PssDesc {
+  uint32_t flags;
+  uint32_t excl, nexcl;  // exclusions (u32 pool): control bits, nimages, images...
+  uint32_t pad;
+};
+
+// ---------------------------------------------------------------- rules
+enum RuleKind : uint8_t { RK_NONE = 0, RK_PATTERN = 1, RK_ANYPATTERN = 2, RK_PSS = 3, RK_FALLBACK = 4, RK_PANIC = 5,
+                          RK_ERROR = 6 };
+
+struct RuleDesc {
+  uint8_t kind;
+  uint8_t uses_meta;     // pattern contains metadata-expansion sites
+  uint8_t nslots;
+  uint8_t pad;
+  uint32_t policy;       // policy index
+  MatchBlock match, exclude;
+  uint32_t empty_may_match;  // evaluate the empty-OldResource retry (validation.go:606)
+  uint32_t root;         // RK_PATTERN: root pnode; RK_ANYPATTERN: first of nalts root ids in pool; RK_PSS: PssDesc
+  uint32_t nalts;
+  uint32_t meta_sites, nmeta;
+};
+
+// ---------------------------------------------------------------- results
+enum Status : uint8_t { ST_NONE = 0, ST_PASS = 1, ST_FAIL = 2, ST_SKIP = 3, ST_ERROR = 4, ST_FALLBACK = 5, ST_PANIC = 6,
+                        ST_ND = 7 };
+constexpr int NSTATUS = 8;
+
+constexpr int MAX_IDX = 4;
+constexpr int MAX_SLOTS = 2;
+constexpr int MAX_DEPTH = 24;
+constexpr int MAX_ALTS = 8;
+
+struct FailRec {        // 32 bytes; one per failing pattern (per failing anyPattern alternative)
+  uint32_t res, rule;
+  uint32_t tmpl;        // path template (NONE: no path, i.e. "failed: <err>" message)
+  uint16_t alt;         // anyPattern alternative (0 for single patterns)
+  uint16_t nalt;        // failing alternatives recorded for this pair
+  uint16_t idx[MAX_IDX];
+  uint32_t key[MAX_SLOTS];
+};
+static_assert(sizeof(FailRec) == 32, "fail record size");
+
+}  // namespace kyv

@@ -1,0 +1,548 @@
+// PodSecurity rules on the node table (__host__ __device__).
+//
+// Restates pkg/pss/evaluate.go (EvaluatePod :83, evaluatePSS :16, exemptKyvernoExclusion :39,
+// GetPodWithMatchingContainers :112) and the DefaultChecks() of k8s.io/pod-security-admission v0.26.1
+// (module not vendored in the reference; restated from its published algorithm and pinned by
+// pkg/pss/evaluate_test.go).  Every check runs ALL of its versions (evaluate.go:24), so the result is a
+// bitmask over (check, version) slots in DefaultChecks() registration order.  The typed decode of
+// validation.go:481-532 is modelled for the fields the checks read: a JSON type mismatch there is an error.
+#pragma once
+#include "kyv_eval.h"
+
+namespace kyv {
+
+enum PssSlot : uint32_t {
+  PS_APE_1_8 = 0, PS_APE_1_25, PS_APPARMOR, PS_CAPS_BASE, PS_CAPS_R_1_22, PS_CAPS_R_1_25, PS_HOSTNS, PS_HOSTPATH,
+  PS_HOSTPORTS, PS_PRIVILEGED, PS_PROCMOUNT, PS_RVOLUMES, PS_RUNASNONROOT, PS_RUNASUSER, PS_SELINUX, PS_SECCOMP_B_1_0,
+  PS_SECCOMP_B_1_19, PS_SECCOMP_R_1_19, PS_SECCOMP_R_1_25, PS_SYSCTLS, PS_WINHOSTPROCESS, PS_NSLOTS
+};
+constexpr uint32_t PSS_RESTRICTED_SLOTS = (1u << PS_APE_1_8) | (1u << PS_APE_1_25) | (1u << PS_CAPS_R_1_22) |
+                                          (1u << PS_CAPS_R_1_25) | (1u << PS_RVOLUMES) | (1u << PS_RUNASNONROOT) |
+                                          (1u << PS_RUNASUSER) | (1u << PS_SECCOMP_R_1_19) | (1u << PS_SECCOMP_R_1_25);
+
+KYV_HD uint32_t get(NodeTab R, uint32_t m, uint32_t key) {
+  if (m == NONE || node_type(R[m]) != N_MAP) return NONE;
+  return map_find(R, m, key);
+}
+KYV_HD bool nil(NodeTab R, uint32_t n) { return n == NONE || node_type(R[n]) == N_NULL; }
+
+struct Dec {        // typed-decode validator
+  NodeTab R;
+  bool bad;
+  KYV_HD bool obj(uint32_t n) { if (nil(R, n)) return false; if (node_type(R[n]) != N_MAP) { bad = true; return false; } return true; }
+  KYV_HD bool arr(uint32_t n) { if (nil(R, n)) return false; if (node_type(R[n]) != N_ARR) { bad = true; return false; } return true; }
+  KYV_HD uint32_t str(uint32_t n) { if (nil(R, n)) return SID_EMPTY; if (node_type(R[n]) != N_STR) { bad = true; return SID_EMPTY; } return R[n].a; }
+  KYV_HD int pbool(uint32_t n) {  // -1 nil
+    if (nil(R, n)) return -1;
+    uint32_t t = node_type(R[n]);
+    if (t == N_TRUE) return 1;
+    if (t == N_FALSE) return 0;
+    bad = true;
+    return -1;
+  }
+  KYV_HD bool i64(uint32_t n, int64_t lo, int64_t hi, int64_t* out) {
+    if (nil(R, n)) return false;
+    if (node_type(R[n]) != N_INT) { bad = true; return false; }
+    int64_t x = (int64_t)(((uint64_t)R[n].b << 32) | R[n].a);
+    if (x < lo || x > hi) { bad = true; return false; }
+    *out = x;
+    return true;
+  }
+};
+
+struct SecCtx {
+  bool set;
+  int privileged, ape, runAsNonRoot, hostProcess;
+  bool hasRunAsUser;
+  int64_t runAsUser;
+  bool selSet;
+  uint32_t selUser, selRole, selType;
+  bool secSet;
+  uint32_t secType;
+  uint32_t caps;       // capabilities map node or NONE
+  bool procSet;
+  uint32_t proc;
+};
+
+KYV_HD void dec_selinux(Dec& d, uint32_t n, bool& set, uint32_t& user, uint32_t& role, uint32_t& type) {
+  set = d.obj(n);
+  user = role = type = SID_EMPTY;
+  if (!set) return;
+  user = d.str(get(d.R, n, KSID(USER)));
+  role = d.str(get(d.R, n, KSID(ROLE)));
+  type = d.str(get(d.R, n, KSID(TYPE)));
+  d.str(get(d.R, n, KSID(LEVEL)));
+}
+KYV_HD void dec_seccomp(Dec& d, uint32_t n, bool& set, uint32_t& type) {
+  set = d.obj(n);
+  type = SID_EMPTY;
+  if (!set) return;
+  type = d.str(get(d.R, n, KSID(TYPE)));
+  d.str(get(d.R, n, KSID(LOCALHOSTPROFILE)));
+}
+KYV_HD int dec_win(Dec& d, uint32_t n) {
+  if (!d.obj(n)) return -1;
+  int hp = d.pbool(get(d.R, n, KSID(HOSTPROCESS)));
+  d.str(get(d.R, n, KSID(GMSA_NAME)));
+  d.str(get(d.R, n, KSID(GMSA)));
+  d.str(get(d.R, n, KSID(RUNASUSERNAME)));
+  return hp;
+}
+
+KYV_HD SecCtx dec_container_sc(Dec& d, uint32_t c) {
+  SecCtx s;
+  s.set = false; s.privileged = s.ape = s.runAsNonRoot = s.hostProcess = -1; s.hasRunAsUser = false; s.runAsUser = 0;
+  s.selSet = false; s.selUser = s.selRole = s.selType = SID_EMPTY; s.secSet = false; s.secType = SID_EMPTY;
+  s.caps = NONE; s.procSet = false; s.proc = SID_EMPTY;
+  uint32_t sc = get(d.R, c, KSID(SECCTX));
+  if (!d.obj(sc)) return s;
+  s.set = true;
+  NodeTab R = d.R;
+  s.privileged = d.pbool(get(R, sc, KSID(PRIVILEGED)));
+  s.ape = d.pbool(get(R, sc, KSID(APE)));
+  s.runAsNonRoot = d.pbool(get(R, sc, KSID(RUNASNONROOT)));
+  d.pbool(get(R, sc, KSID(READONLYROOTFS)));
+  s.hasRunAsUser = d.i64(get(R, sc, KSID(RUNASUSER)), INT64_MIN, INT64_MAX, &s.runAsUser);
+  int64_t g;
+  d.i64(get(R, sc, KSID(RUNASGROUP)), INT64_MIN, INT64_MAX, &g);
+  dec_selinux(d, get(R, sc, KSID(SELINUX)), s.selSet, s.selUser, s.selRole, s.selType);
+  dec_seccomp(d, get(R, sc, KSID(SECCOMP)), s.secSet, s.secType);
+  s.hostProcess = dec_win(d, get(R, sc, KSID(WINOPTS)));
+  uint32_t caps = get(R, sc, KSID(CAPS));
+  if (d.obj(caps)) {
+    s.caps = caps;
+    for (uint32_t key : {KSID(ADD), KSID(DROP)}) {
+      uint32_t l = get(R, caps, key);
+      if (d.arr(l)) for (uint32_t i = 0; i < R[l].b; i++) d.str(R[l].a + i);
+    }
+  }
+  uint32_t pm = get(R, sc, KSID(PROCMOUNT));
+  if (!nil(R, pm)) { s.procSet = true; s.proc = d.str(pm); }
+  return s;
+}
+
+// whole-pod typed decode check (fields the checks read, as oracle/opss.cpp dec_pod)
+KYV_HD bool decode_ok_meta(Dec& d, uint32_t meta) {
+  if (!d.obj(meta)) return !d.bad;
+  NodeTab R = d.R;
+  d.str(get(R, meta, KSID(NAME)));
+  d.str(get(R, meta, KSID(NAMESPACE_KEY)));
+  uint32_t ann = get(R, meta, KSID(ANNOTATIONS));
+  if (d.obj(ann)) for (uint32_t i = 0; i < R[ann].b; i++) d.str(R[ann].a + i);
+  uint32_t lab = get(R, meta, KSID(LABELS));
+  if (d.obj(lab)) for (uint32_t i = 0; i < R[lab].b; i++) d.str(R[lab].a + i);
+  return !d.bad;
+}
+
+KYV_HD void decode_container(Dec& d, uint32_t c) {
+  if (!d.obj(c)) return;
+  NodeTab R = d.R;
+  d.str(get(R, c, KSID(NAME)));
+  d.str(get(R, c, KSID(IMAGE)));
+  uint32_t ports = get(R, c, KSID(PORTS));
+  if (d.arr(ports))
+    for (uint32_t i = 0; i < R[ports].b; i++) {
+      uint32_t p = R[ports].a + i;
+      if (!d.obj(p)) continue;
+      int64_t x;
+      d.i64(get(R, p, KSID(HOSTPORT)), INT32_MIN, INT32_MAX, &x);
+      d.i64(get(R, p, KSID(CONTAINERPORT)), INT32_MIN, INT32_MAX, &x);
+      d.str(get(R, p, KSID(NAME)));
+      d.str(get(R, p, KSID(PROTOCOL)));
+      d.str(get(R, p, KSID(HOSTIP)));
+    }
+  dec_container_sc(d, c);
+}
+
+KYV_HD bool decode_ok_spec(Dec& d, uint32_t spec) {
+  if (!d.obj(spec)) return !d.bad;
+  NodeTab R = d.R;
+  d.pbool(get(R, spec, KSID(HOSTNETWORK)));
+  d.pbool(get(R, spec, KSID(HOSTPID)));
+  d.pbool(get(R, spec, KSID(HOSTIPC)));
+  uint32_t sc = get(R, spec, KSID(SECCTX));
+  if (d.obj(sc)) {
+    d.pbool(get(R, sc, KSID(RUNASNONROOT)));
+    int64_t x;
+    d.i64(get(R, sc, KSID(RUNASUSER)), INT64_MIN, INT64_MAX, &x);
+    d.i64(get(R, sc, KSID(RUNASGROUP)), INT64_MIN, INT64_MAX, &x);
+    d.i64(get(R, sc, KSID(FSGROUP)), INT64_MIN, INT64_MAX, &x);
+    uint32_t sg = get(R, sc, KSID(SUPPGROUPS));
+    if (d.arr(sg)) for (uint32_t i = 0; i < R[sg].b; i++) d.i64(R[sg].a + i, INT64_MIN, INT64_MAX, &x);
+    bool set; uint32_t a, b, c;
+    dec_selinux(d, get(R, sc, KSID(SELINUX)), set, a, b, c);
+    dec_seccomp(d, get(R, sc, KSID(SECCOMP)), set, a);
+    dec_win(d, get(R, sc, KSID(WINOPTS)));
+    uint32_t sy = get(R, sc, KSID(SYSCTLS));
+    if (d.arr(sy))
+      for (uint32_t i = 0; i < R[sy].b; i++) {
+        uint32_t e = R[sy].a + i;
+        if (!d.obj(e)) continue;
+        d.str(get(R, e, KSID(NAME)));
+        d.str(get(R, e, KSID(VALUE)));
+      }
+  }
+  for (uint32_t key : {KSID(CONTAINERS), KSID(INITCONTAINERS), KSID(EPHEMERALCONTAINERS)}) {
+    uint32_t l = get(R, spec, key);
+    if (d.arr(l)) for (uint32_t i = 0; i < R[l].b; i++) decode_container(d, R[l].a + i);
+  }
+  uint32_t vols = get(R, spec, KSID(VOLUMES));
+  if (d.arr(vols))
+    for (uint32_t i = 0; i < R[vols].b; i++) {
+      uint32_t vn = R[vols].a + i;
+      if (!d.obj(vn)) continue;
+      d.str(get(R, vn, KSID(NAME)));
+      for (uint32_t s = 0; s < V_COUNT; s++) d.obj(get(R, vn, SID_FIRST_FREE + K_COUNT + s));
+    }
+  uint32_t os = get(R, spec, KSID(OS));
+  if (d.obj(os)) d.str(get(R, os, KSID(NAME)));
+  return !d.bad;
+}
+
+// container source of a (sub-)pod: the real lists (optionally filtered by exclusion images) or the
+// single fake container of GetPodWithMatchingContainers (evaluate.go:112-146)
+struct PodView {
+  uint32_t meta;       // NONE for the image-exclusion sub-pod (ObjectMeta{Name, Namespace} only)
+  uint32_t spec;       // NONE: pod-level spec fields are empty
+  uint32_t lists[3];   // init, containers, ephemeral (visitContainers order)
+  bool fake;
+  uint32_t img, nimg;  // image globs (pool)
+};
+
+KYV_HD bool container_included(const View& v, NodeTab R, const PodView& pv, uint32_t c) {
+  if (pv.nimg == 0) return true;
+  uint32_t image = nil(R, get(R, c, KSID(IMAGE))) ? SID_EMPTY : R[get(R, c, KSID(IMAGE))].a;
+  for (uint32_t i = 0; i < pv.nimg; i++) if (glob_sid(v, v.pool[pv.img + i], image)) return true;
+  return false;
+}
+
+KYV_HD bool str_in(uint32_t s, const uint32_t* set, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) if (set[i] == s) return true;
+  return false;
+}
+
+KYV_HD bool has_prefix(const View& v, uint32_t s, uint32_t prefix) {
+  uint32_t ln = v.str_len[prefix];
+  return v.str_len[s] >= ln && bytes_eq(sbytes(v, s), sbytes(v, prefix), ln);
+}
+
+// evaluatePSS (evaluate.go:16-37): failing (check, version) slots
+KYV_BIG uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
+  Dec d{R, false};
+  uint32_t fails = 0;
+  uint32_t spec = pv.spec;
+  uint32_t psc = get(R, spec, KSID(SECCTX));
+  bool pscSet = !nil(R, psc) && node_type(R[psc]) == N_MAP;
+  bool windows = false;
+  {
+    uint32_t os = get(R, spec, KSID(OS));
+    uint32_t nm = get(R, os, KSID(NAME));
+    windows = !nil(R, nm) && node_type(R[nm]) == N_STR && R[nm].a == KSID(WINDOWS);
+  }
+  // pod-level security context
+  int podNonRoot = pscSet ? d.pbool(get(R, psc, KSID(RUNASNONROOT))) : -1;
+  int64_t podUser = 0;
+  bool podHasUser = pscSet && d.i64(get(R, psc, KSID(RUNASUSER)), INT64_MIN, INT64_MAX, &podUser);
+  bool podSelSet = false; uint32_t pu = SID_EMPTY, pr = SID_EMPTY, pt = SID_EMPTY;
+  if (pscSet) dec_selinux(d, get(R, psc, KSID(SELINUX)), podSelSet, pu, pr, pt);
+  bool podSecSet = false; uint32_t podSecType = SID_EMPTY;
+  if (pscSet) dec_seccomp(d, get(R, psc, KSID(SECCOMP)), podSecSet, podSecType);
+  int podHostProcess = pscSet ? dec_win(d, get(R, psc, KSID(WINOPTS))) : -1;
+
+  const uint32_t capsOK[13] = {KSID(CAP_AUDIT_WRITE), KSID(CAP_CHOWN), KSID(CAP_DAC_OVERRIDE), KSID(CAP_FOWNER),
+                               KSID(CAP_FSETID), KSID(CAP_KILL), KSID(CAP_MKNOD), KSID(NET_BIND_SERVICE),
+                               KSID(CAP_SETFCAP), KSID(CAP_SETGID), KSID(CAP_SETPCAP), KSID(CAP_SETUID),
+                               KSID(CAP_SYS_CHROOT)};
+  const uint32_t selOK[4] = {SID_EMPTY, KSID(CONTAINER_T), KSID(CONTAINER_INIT_T), KSID(CONTAINER_KVM_T)};
+  auto selValid = [&](uint32_t u, uint32_t r, uint32_t t) { return str_in(t, selOK, 4) && u == SID_EMPTY && r == SID_EMPTY; };
+  auto secValid = [&](uint32_t t) { return t == KSID(LOCALHOST) || t == KSID(RUNTIMEDEFAULT); };
+
+  bool apeBad = false, capsBaseBad = false, capsRBad = false, portsBad = false, privBad = false, procBad = false;
+  bool nonRootExplicitBad = false, nonRootImplicitBad = false, userBad = false, selBad = false;
+  bool secBaseBad = false, secRExplicitBad = false, secRImplicitBad = false, hpBad = false, secAnnBad = false;
+  bool podNonRootTrue = podNonRoot == 1;
+  bool podSecValid = podSecSet && secValid(podSecType);
+  uint32_t ann = pv.meta == NONE ? NONE : get(R, pv.meta, KSID(ANNOTATIONS));
+  bool annMap = !nil(R, ann) && node_type(R[ann]) == N_MAP;
+
+  auto visit = [&](uint32_t c, bool fake) {
+    SecCtx s;
+    uint32_t cname = SID_EMPTY;
+    if (fake) {
+      s.set = false; s.privileged = s.ape = s.runAsNonRoot = s.hostProcess = -1; s.hasRunAsUser = false;
+      s.selSet = false; s.secSet = false; s.caps = NONE; s.procSet = false;
+      cname = KSID(FAKE);
+    } else {
+      s = dec_container_sc(d, c);
+      uint32_t nm = get(R, c, KSID(NAME));
+      cname = nil(R, nm) ? SID_EMPTY : R[nm].a;
+    }
+    if (!s.set || s.ape != 0) apeBad = true;
+    if (s.set && s.caps != NONE) {
+      uint32_t add = get(R, s.caps, KSID(ADD));
+      if (!nil(R, add))
+        for (uint32_t i = 0; i < R[add].b; i++) {
+          uint32_t cap = R[R[add].a + i].a;
+          if (node_type(R[R[add].a + i]) != N_STR) cap = SID_EMPTY;
+          if (!str_in(cap, capsOK, 13)) capsBaseBad = true;
+          if (cap != KSID(NET_BIND_SERVICE)) capsRBad = true;
+        }
+      bool all = false;
+      uint32_t drop = get(R, s.caps, KSID(DROP));
+      if (!nil(R, drop))
+        for (uint32_t i = 0; i < R[drop].b; i++) {
+          const Node& e = R[R[drop].a + i];
+          if (node_type(e) == N_STR && e.a == KSID(ALL)) all = true;
+        }
+      if (!all) capsRBad = true;
+    } else {
+      capsRBad = true;
+    }
+    if (!fake) {
+      uint32_t ports = get(R, c, KSID(PORTS));
+      if (!nil(R, ports))
+        for (uint32_t i = 0; i < R[ports].b; i++) {
+          uint32_t hp = get(R, R[ports].a + i, KSID(HOSTPORT));
+          if (!nil(R, hp) && node_type(R[hp]) == N_INT && (R[hp].a | R[hp].b) != 0) portsBad = true;
+        }
+    }
+    if (s.set && s.privileged == 1) privBad = true;
+    if (s.set && s.procSet && s.proc != KSID(DEFAULT)) procBad = true;
+    if (s.set && s.runAsNonRoot != -1) { if (s.runAsNonRoot == 0) nonRootExplicitBad = true; }
+    else if (!podNonRootTrue) nonRootImplicitBad = true;
+    if (s.set && s.hasRunAsUser && s.runAsUser == 0) userBad = true;
+    if (s.set && s.selSet && !selValid(s.selUser, s.selRole, s.selType)) selBad = true;
+    if (s.set && s.secSet) {
+      if (s.secType == KSID(UNCONFINED)) secBaseBad = true;
+      if (!secValid(s.secType)) secRExplicitBad = true;
+    } else if (!podSecValid) {
+      secRImplicitBad = true;
+    }
+    if (s.set && s.hostProcess == 1) hpBad = true;
+    // container seccomp annotation: container.seccomp.security.alpha.kubernetes.io/<name> == "unconfined"
+    if (annMap) {
+      uint32_t pl = v.str_len[KSID(SECCOMP_CONTAINER_PREFIX)], nl = v.str_len[cname];
+      for (uint32_t i = 0; i < R[ann].b; i++) {
+        const Node& e = R[R[ann].a + i];
+        uint32_t k = node_key(e);
+        if (v.str_len[k] == pl + nl && has_prefix(v, k, KSID(SECCOMP_CONTAINER_PREFIX)) &&
+            bytes_eq(sbytes(v, k) + pl, sbytes(v, cname), nl) && node_type(e) == N_STR && e.a == KSID(UNCONFINED_LC))
+          secAnnBad = true;
+      }
+    }
+  };
+  if (pv.fake) {
+    visit(NONE, true);
+  } else {
+    for (int l = 0; l < 3; l++) {
+      uint32_t list = pv.lists[l];
+      if (nil(R, list) || node_type(R[list]) != N_ARR) continue;
+      for (uint32_t i = 0; i < R[list].b; i++) {
+        uint32_t c = R[list].a + i;
+        if (!container_included(v, R, pv, c)) continue;
+        visit(c, false);
+      }
+    }
+  }
+  if (apeBad) fails |= 1u << PS_APE_1_8;
+  if (apeBad && !windows) fails |= 1u << PS_APE_1_25;
+  // appArmorProfile: annotations with the apparmor prefix whose value is neither runtime/default nor localhost/*
+  if (annMap)
+    for (uint32_t i = 0; i < R[ann].b; i++) {
+      const Node& e = R[R[ann].a + i];
+      uint32_t val = node_type(e) == N_STR ? e.a : SID_EMPTY;
+      if (has_prefix(v, node_key(e), KSID(APPARMOR_PREFIX)) && val != KSID(RUNTIME_DEFAULT_PROFILE) &&
+          !has_prefix(v, val, KSID(LOCALHOST_PREFIX)))
+        fails |= 1u << PS_APPARMOR;
+      if (node_key(e) == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = true;
+    }
+  if (capsBaseBad) fails |= 1u << PS_CAPS_BASE;
+  if (capsRBad) fails |= 1u << PS_CAPS_R_1_22;
+  if (capsRBad && !windows) fails |= 1u << PS_CAPS_R_1_25;
+  {
+    bool hn = false;
+    for (uint32_t key : {KSID(HOSTNETWORK), KSID(HOSTPID), KSID(HOSTIPC)}) {
+      uint32_t n = get(R, spec, key);
+      if (!nil(R, n) && node_type(R[n]) == N_TRUE) hn = true;
+    }
+    if (hn) fails |= 1u << PS_HOSTNS;
+  }
+  uint32_t vols = get(R, spec, KSID(VOLUMES));
+  if (!nil(R, vols) && node_type(R[vols]) == N_ARR)
+    for (uint32_t i = 0; i < R[vols].b; i++) {
+      uint32_t vn = R[vols].a + i;
+      if (!nil(R, get(R, vn, VSID(hostPath)))) fails |= 1u << PS_HOSTPATH;
+      bool okv = false;
+      for (uint32_t s = 0; s < V_ALLOWED && !okv; s++) okv = !nil(R, get(R, vn, SID_FIRST_FREE + K_COUNT + s));
+      if (!okv) fails |= 1u << PS_RVOLUMES;
+    }
+  if (portsBad) fails |= 1u << PS_HOSTPORTS;
+  if (privBad) fails |= 1u << PS_PRIVILEGED;
+  if (procBad) fails |= 1u << PS_PROCMOUNT;
+  if (podNonRoot == 0 || nonRootExplicitBad || nonRootImplicitBad) fails |= 1u << PS_RUNASNONROOT;
+  if ((podHasUser && podUser == 0) || userBad) fails |= 1u << PS_RUNASUSER;
+  if ((podSelSet && !selValid(pu, pr, pt)) || selBad) fails |= 1u << PS_SELINUX;
+  if (secAnnBad) fails |= 1u << PS_SECCOMP_B_1_0;
+  if ((podSecSet && podSecType == KSID(UNCONFINED)) || secBaseBad) fails |= 1u << PS_SECCOMP_B_1_19;
+  bool secR = (podSecSet && !secValid(podSecType)) || secRExplicitBad || secRImplicitBad;
+  if (secR) fails |= 1u << PS_SECCOMP_R_1_19;
+  if (secR && !windows) fails |= 1u << PS_SECCOMP_R_1_25;
+  if (pscSet) {
+    uint32_t sy = get(R, psc, KSID(SYSCTLS));
+    const uint32_t ok5[5] = {KSID(SYSCTL_SHM), KSID(SYSCTL_PORTRANGE), KSID(SYSCTL_SYNCOOKIES), KSID(SYSCTL_PINGRANGE),
+                             KSID(SYSCTL_UNPRIV)};
+    if (!nil(R, sy) && node_type(R[sy]) == N_ARR)
+      for (uint32_t i = 0; i < R[sy].b; i++) {
+        uint32_t nm = get(R, R[sy].a + i, KSID(NAME));
+        uint32_t s = nil(R, nm) ? SID_EMPTY : R[nm].a;
+        if (!str_in(s, ok5, 5)) fails |= 1u << PS_SYSCTLS;
+      }
+  }
+  if (podHostProcess == 1 || hpBad) fails |= 1u << PS_WINHOSTPROCESS;
+  return fails;
+}
+
+// check-id groups: slots belonging to one check ID (exemptKyvernoExclusion removes whole IDs)
+KYV_HD uint32_t pss_id_slots(uint32_t slot) {
+  switch (slot) {
+    case PS_APE_1_8: case PS_APE_1_25: return (1u << PS_APE_1_8) | (1u << PS_APE_1_25);
+    case PS_CAPS_R_1_22: case PS_CAPS_R_1_25: return (1u << PS_CAPS_R_1_22) | (1u << PS_CAPS_R_1_25);
+    case PS_SECCOMP_B_1_0: case PS_SECCOMP_B_1_19: return (1u << PS_SECCOMP_B_1_0) | (1u << PS_SECCOMP_B_1_19);
+    case PS_SECCOMP_R_1_19: case PS_SECCOMP_R_1_25: return (1u << PS_SECCOMP_R_1_19) | (1u << PS_SECCOMP_R_1_25);
+    default: return 1u << slot;
+  }
+}
+
+// validatePodSecurity (validation.go:535-566) -> status; *fails receives the remaining failing slots
+KYV_BIG uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out) {
+  *fails_out = 0;
+  if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
+  uint32_t kind = h.kind;
+  uint32_t root = 0;
+  uint32_t meta = NONE, spec = NONE;
+  Dec d{R, false};
+  uint32_t outerMeta = get(R, root, KSID(METADATA));
+  auto step = [&](uint32_t o, uint32_t k) -> uint32_t {
+    if (d.bad || nil(R, o)) return NONE;
+    if (node_type(R[o]) != N_MAP) { d.bad = true; return NONE; }
+    uint32_t x = map_find(R, o, k);
+    if (!nil(R, x) && node_type(R[x]) != N_MAP) { d.bad = true; return NONE; }
+    return x;
+  };
+  if (!nil(R, outerMeta) && node_type(R[outerMeta]) != N_MAP) d.bad = true;
+  if (kind == KSID(DAEMONSET) || kind == KSID(DEPLOYMENT) || kind == KSID(JOB) || kind == KSID(STATEFULSET) ||
+      kind == KSID(REPLICASET) || kind == KSID(RC)) {
+    uint32_t tpl = step(step(root, KSID(SPEC)), KSID(TEMPLATE));
+    meta = step(tpl, KSID(METADATA));
+    spec = step(tpl, KSID(SPEC));
+  } else if (kind == KSID(CRONJOB)) {
+    uint32_t jt = step(step(root, KSID(SPEC)), KSID(JOBTEMPLATE));
+    meta = step(jt, KSID(METADATA));
+    spec = step(step(step(jt, KSID(SPEC)), KSID(TEMPLATE)), KSID(SPEC));
+  } else if (kind == KSID(POD)) {
+    meta = outerMeta;
+    spec = step(root, KSID(SPEC));
+  } else {
+    return ST_PANIC;  // nil pod spec dereference (validation.go:542-543)
+  }
+  if (d.bad) return ST_ERROR;
+  if (outerMeta != meta && !nil(R, outerMeta) && !decode_ok_meta(d, outerMeta)) return ST_ERROR;
+  if (!decode_ok_meta(d, meta) || !decode_ok_spec(d, spec)) return ST_ERROR;
+  PodView pv;
+  pv.meta = meta;
+  pv.spec = spec;
+  pv.lists[0] = get(R, spec, KSID(INITCONTAINERS));
+  pv.lists[1] = get(R, spec, KSID(CONTAINERS));
+  pv.lists[2] = get(R, spec, KSID(EPHEMERALCONTAINERS));
+  pv.fake = false;
+  pv.img = 0;
+  pv.nimg = 0;
+  uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
+  uint32_t fails = pss_checks(v, R, pv) & mask;
+  for (uint32_t x = 0; x < pd.nexcl; x++) {
+    // exclusion record in pool: [control slot mask, nimages, image sids...]
+    uint32_t rec = v.pool[pd.excl + x];
+    uint32_t ctl = v.pool[rec], nimg = v.pool[rec + 1];
+    PodView sub = pv;
+    if (nimg == 0) {
+      sub.fake = true;
+    } else {
+      sub.meta = NONE;
+      sub.spec = NONE;
+      sub.img = rec + 2;
+      sub.nimg = nimg;
+    }
+    uint32_t ex = pss_checks(v, R, sub) & mask;
+    for (uint32_t s = 0; s < PS_NSLOTS; s++)
+      if ((ctl >> s) & 1u) {
+        uint32_t ids = pss_id_slots(s);
+        if (ex & ids) fails &= ~ids;
+      }
+  }
+  *fails_out = fails;
+  return fails ? ST_FAIL : ST_PASS;
+}
+
+}  // namespace kyv
+
+namespace kyv {
+
+// One (resource, rule) pair: match (+ empty OldResource retry) then dispatch (validation.go:134-183, :276-317).
+// `recs`/`nrec` receive failing-path records (one per failing pattern / anyPattern alternative).
+KYV_BIG uint8_t eval_pair(const View& v, uint32_t r, uint32_t k, Stack stk, uint32_t* pss_fails, FailRec* recs, uint32_t* nrec,
+                         uint32_t maxrec) {
+  *nrec = 0;
+  *pss_fails = 0;
+  const RuleDesc& rd = v.rules[k];
+  if (rd.match.mode == MM_NONE) return ST_FALLBACK;  // match program could not be compiled
+  const ResHeader& h = v.hdr[r];
+  NodeTab R{v.nodes + h.root};
+  LabelSet nsl{nullptr, 0, nullptr, 0};
+  if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
+  bool nd = false;
+  bool m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
+  if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
+  if (!m) return ST_NONE;
+  if (nd) return ST_ND;
+  switch (rd.kind) {
+    case RK_FALLBACK: return ST_FALLBACK;
+    case RK_PANIC: return ST_PANIC;
+    case RK_ERROR: return ST_ERROR;
+    case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
+    case RK_PATTERN: case RK_ANYPATTERN: {
+      if (h.flags & RF_MAGIC) return ST_FALLBACK;
+      uint32_t nalts = rd.kind == RK_PATTERN ? 1 : rd.nalts;
+      uint32_t nfail = 0, nskip = 0;
+      for (uint32_t a = 0; a < nalts; a++) {
+        uint32_t root = rd.kind == RK_PATTERN ? rd.root : v.pool[rd.root + a];
+        PatOut po;
+        eval_pattern(v, root, R, h, rd, stk, po);
+        switch (po.status) {
+          case ST_PASS: *nrec = 0; return (uint8_t)(ST_PASS | ((a < 30 ? a : 30) << 3));  // alt index for the message
+          case ST_SKIP: nskip++; break;
+          case ST_FAIL: case ST_ERROR: {
+            if (rd.kind == RK_PATTERN && po.status == ST_ERROR) return ST_ERROR;
+            if (*nrec < maxrec) {
+              FailRec& fr = recs[*nrec];
+              fr.res = r; fr.rule = k; fr.tmpl = po.status == ST_FAIL ? po.tmpl : NONE; fr.alt = (uint16_t)a;
+              for (int i = 0; i < MAX_IDX; i++) fr.idx[i] = po.idx[i];
+              for (int i = 0; i < MAX_SLOTS; i++) fr.key[i] = po.key[i];
+              (*nrec)++;
+            }
+            nfail++;
+            break;
+          }
+          default: *nrec = 0; return po.status;  // fallback / panic / nondeterministic at this point of the walk
+        }
+      }
+      for (uint32_t i = 0; i < *nrec; i++) recs[i].nalt = (uint16_t)*nrec;
+      if (rd.kind == RK_PATTERN) return nfail ? ST_FAIL : ST_SKIP;
+      if (nfail) return ST_FAIL;
+      if (nskip) return ST_SKIP;
+      return (uint8_t)(ST_PASS | (31 << 3));  // empty anyPattern list: pass with the rule message (validation.go:701)
+    }
+    default: return ST_NONE;
+  }
+}
+
+}  // namespace kyv

@@ -1,0 +1,164 @@
+"""Host-side mirror of the reference validate interface over libkyvgpu.so.
+
+Reference surface mirrored (paths relative to the reference repository):
+  engine.Validate(ctx, loader, PolicyContext, cfg) -> *EngineResponse   pkg/engine/validation.go:39
+  EngineResponse / PolicyResponse / RuleResponse                         pkg/engine/api/*.go
+  background scan per resource x policy                                  pkg/controllers/report/utils/scanner.go:60
+  CLI apply counters (pass/fail/warn/error/skip)                         cmd/cli/kubectl-kyverno/utils/common/common.go:712-795
+
+`Engine(policies)` compiles once (autogen + rule programs); `engine.validate_batch(resources)` evaluates
+every (resource, rule) pair on the MI355X and returns per-resource EngineResponses in reference shape.
+Rules the device path does not cover come back with status "fallback" (the Go shim runs engine.Validate
+for exactly those pairs).
+"""
+import ctypes
+import json
+
+import numpy as np
+
+from . import _lib as K
+
+
+def _dumps(x):
+    if isinstance(x, (bytes, bytearray)):
+        return bytes(x)
+    if isinstance(x, str):
+        return x.encode()
+    return json.dumps(x, separators=(",", ":")).encode()
+
+
+class Ruleset:
+    def __init__(self, policies):
+        """policies: list of ClusterPolicy/Policy dicts (or JSON text)."""
+        L = K.lib()
+        data = _dumps(policies if not isinstance(policies, dict) else [policies])
+        h = ctypes.c_void_p()
+        opts = K.CompileOpts(K.KYV_ABI_VERSION, 0)
+        K.check(L.kyv_ruleset_compile(data, len(data), ctypes.byref(opts), ctypes.byref(h)))
+        self.h = h
+        self.rules = []
+        for k in range(L.kyv_ruleset_num_rules(h)):
+            ri = K.RuleInfo()
+            K.check(L.kyv_ruleset_rule_info(h, k, ctypes.byref(ri)))
+            self.rules.append({"name": ri.name.decode(), "policy": ri.policy, "kind": K.RULE_KINDS.get(ri.kind, "?"),
+                               "reason": ri.reason.decode()})
+        self.policies = []
+        for p in range(L.kyv_ruleset_num_policies(h)):
+            pi = K.PolicyInfo()
+            K.check(L.kyv_ruleset_policy_info(h, p, ctypes.byref(pi)))
+            self.policies.append({"name": pi.name.decode(), "namespace": pi.namespace_.decode(), "first_rule": pi.first_rule,
+                                  "nrules": pi.nrules, "apply_one": bool(pi.apply_one), "scored_false": bool(pi.scored_false)})
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            K.lib().kyv_ruleset_free(self.h)
+            self.h = None
+
+
+class Batch:
+    def __init__(self, ruleset, resources, ns_labels=None, threads=0):
+        """resources: list of dicts, or JSON array / NDJSON bytes."""
+        L = K.lib()
+        data = _dumps(resources)
+        nsl = _dumps(ns_labels) if ns_labels else b""
+        h = ctypes.c_void_p()
+        opts = K.BatchOpts(K.KYV_ABI_VERSION, threads)
+        K.check(L.kyv_batch_build(ruleset.h, data, len(data), nsl, len(nsl), ctypes.byref(opts), ctypes.byref(h)))
+        self.h = h
+        self.ruleset = ruleset
+        self.n = L.kyv_batch_num_resources(h)
+
+    def stats(self):
+        s = K.BatchStats()
+        K.check(K.lib().kyv_batch_stats_get(self.h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in K.BatchStats._fields_}
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            K.lib().kyv_batch_free(self.h)
+            self.h = None
+
+
+class Results:
+    def __init__(self, ruleset, batch, h, copied):
+        self.ruleset, self.batch, self.h = ruleset, batch, h
+        L = K.lib()
+        self.counts = {K.STATUS_NAMES[s]: L.kyv_results_count(h, s) for s in range(8)}
+        self.kernel_ms = L.kyv_results_kernel_ms(h)
+        self.alg_bytes = L.kyv_results_alg_bytes(h)
+        self.status = None
+        if copied:
+            nr, nres = len(ruleset.rules), batch.n
+            buf = np.empty(nr * nres, dtype=np.uint8)
+            K.check(L.kyv_results_status(h, buf.ctypes.data, buf.size))
+            self.raw = buf.reshape(nr, nres)
+            self.status = self.raw & 7
+
+    def message(self, res, rule):
+        L = K.lib()
+        buf = ctypes.create_string_buffer(4096)
+        n = L.kyv_results_message(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
+        if n < 0:
+            return None
+        if n >= len(buf):
+            buf = ctypes.create_string_buffer(n + 1)
+            L.kyv_results_message(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
+        return buf.value.decode(errors="replace")
+
+    def path(self, res, rule):
+        buf = ctypes.create_string_buffer(4096)
+        K.lib().kyv_results_path(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
+        return buf.value.decode(errors="replace")
+
+    def pss_mask(self, res, rule):
+        return K.lib().kyv_results_pss_mask(self.h, self.ruleset.h, res, rule)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            K.lib().kyv_results_free(self.h)
+            self.h = None
+
+
+def evaluate(ruleset, batch, backend="gpu", device=0, iterations=1, threads=0, copy_back=True, account_bytes=False):
+    """Evaluate every (resource, rule) pair. backend="gpu" is the product path; "cpu" must be explicit."""
+    L = K.lib()
+    flags = (0 if copy_back else K.EVAL_NO_COPYBACK) | (K.EVAL_ACCOUNT_BYTES if account_bytes else 0)
+    opts = K.EvalOpts(K.KYV_ABI_VERSION, K.BACKEND_GPU if backend == "gpu" else K.BACKEND_CPU, device, iterations,
+                      threads, flags)
+    h = ctypes.c_void_p()
+    K.check(L.kyv_eval(ruleset.h, batch.h, ctypes.byref(opts), ctypes.byref(h)))
+    return Results(ruleset, batch, h, copy_back)
+
+
+class Engine:
+    """engine.Validate over batches: compile once, evaluate many resources per call."""
+
+    def __init__(self, policies, backend="gpu", device=0):
+        self.ruleset = Ruleset(policies)
+        self.backend, self.device = backend, device
+
+    def validate_batch(self, resources, ns_labels=None):
+        """-> list (per resource) of list (per policy) of EngineResponse-like dicts (validation.go:39)."""
+        batch = Batch(self.ruleset, resources, ns_labels)
+        res = evaluate(self.ruleset, batch, backend=self.backend, device=self.device)
+        out = []
+        for r in range(batch.n):
+            per_policy = []
+            for pi, pol in enumerate(self.ruleset.policies):
+                rules = []
+                applied = 0
+                for k in range(pol["first_rule"], pol["first_rule"] + pol["nrules"]):
+                    st = int(res.status[k, r])
+                    if st == K.ST_NONE:
+                        continue
+                    name = K.STATUS_NAMES[st]
+                    rules.append({"name": self.ruleset.rules[k]["name"], "status": name, "message": res.message(r, k)})
+                    if st in (K.ST_PASS, K.ST_FAIL):
+                        applied += 1
+                    if pol["apply_one"] and applied > 0:  # validation.go:176-178
+                        break
+                    if pol["apply_one"] and st == K.ST_FALLBACK:
+                        break  # truncation depends on the CPU engine's verdict for this rule
+                per_policy.append({"policy": pol["name"], "rules": rules})
+            out.append(per_policy)
+        return out, res, batch

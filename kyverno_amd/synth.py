@@ -1,0 +1,294 @@
+"""Seeded synthetic Kubernetes resources (SURVEY.md 8(d) Pod model / mixed-kind model).
+
+Used by tests (parity corpora) and bench.py (workload). Not part of the evaluation path.
+`edge=True` mixes in the quirks the reference handles specially (nulls, wrong JSON types, numbers where
+strings are expected, float values, empty maps) so parity covers them.
+"""
+import json
+import random
+
+SEED = 0x4B59564E
+
+QTY = ["100m", "0.5", "1", "250m", "64Mi", "256Mi", "1Gi", "1.5Gi", "2G"]
+CAPS_ADD = ["NET_BIND_SERVICE", "SYS_ADMIN", "CHOWN", "NET_RAW"]
+SYSCTL_OK = ["kernel.shm_rmid_forced", "net.ipv4.ip_local_port_range", "net.ipv4.tcp_syncookies"]
+SYSCTL_BAD = ["kernel.msgmax", "net.core.somaxconn"]
+VOL_TYPES = ["configMap", "secret", "emptyDir", "persistentVolumeClaim", "projected", "downwardAPI", "csi", "nfs",
+             "gitRepo"]
+
+
+class Gen:
+    def __init__(self, seed=SEED, edge=False, namespaces=1000):
+        self.r = random.Random(seed)
+        self.edge = edge
+        self.namespaces = ["ns-%04d" % i for i in range(namespaces)]
+        self.repos = ["registry.example.com/team%d/app%d" % (i % 50, i) for i in range(2000)]
+
+    def p(self, x):
+        return self.r.random() < x
+
+    def ns_labels(self):
+        rr = random.Random(SEED ^ 0x55)
+        out = {}
+        for ns in self.namespaces:
+            n = rr.randint(2, 4)
+            lab = {"kubernetes.io/metadata.name": ns, "team": "team-%d" % rr.randint(0, 40)}
+            if n > 2:
+                lab["env"] = rr.choice(["prod", "dev", "staging"])
+            if n > 3:
+                lab["tier"] = rr.choice(["frontend", "backend", "data"])
+            out[ns] = lab
+        return out
+
+    def image(self):
+        repo = self.r.choice(self.repos)
+        u = self.r.random()
+        if u < 0.10:
+            return repo + ":latest"
+        if u < 0.15:
+            return repo
+        if u < 0.20:
+            return repo + "@sha256:" + "%064x" % self.r.getrandbits(256)
+        return repo + ":v%d.%d.%d" % (self.r.randint(0, 3), self.r.randint(0, 20), self.r.randint(0, 9))
+
+    def sec_ctx(self):
+        sc = {}
+        if self.p(0.02):
+            sc["privileged"] = True
+        elif self.p(0.05):
+            sc["privileged"] = False
+        u = self.r.random()
+        if u < 0.70:
+            sc["allowPrivilegeEscalation"] = False
+        elif u < 0.75:
+            sc["allowPrivilegeEscalation"] = True
+        if self.p(0.60):
+            sc["runAsNonRoot"] = True
+        elif self.p(0.05):
+            sc["runAsNonRoot"] = False
+        if self.p(0.03):
+            sc["runAsUser"] = 0
+        elif self.p(0.3):
+            sc["runAsUser"] = self.r.choice([1000, 65534, 1001])
+        if self.p(0.2):
+            sc["runAsGroup"] = self.r.choice([0, 1000, 3000])
+        caps = {}
+        if self.p(0.55):
+            caps["drop"] = ["ALL"]
+        u = self.r.random()
+        if u < 0.05:
+            caps["add"] = ["NET_BIND_SERVICE"]
+        elif u < 0.06:
+            caps["add"] = ["SYS_ADMIN"]
+        elif u < 0.065:
+            caps["add"] = ["CHOWN", "NET_RAW"]
+        if caps:
+            sc["capabilities"] = caps
+        u = self.r.random()
+        if u < 0.60:
+            sc["seccompProfile"] = {"type": "RuntimeDefault"}
+        elif u < 0.65:
+            sc["seccompProfile"] = {"type": "Localhost", "localhostProfile": "profiles/audit.json"}
+        elif u < 0.67:
+            sc["seccompProfile"] = {"type": "Unconfined"}
+        if self.p(0.03):
+            sc["seLinuxOptions"] = {"type": "spc_t" if self.p(0.33) else "container_t"}
+            if self.p(0.1):
+                sc["seLinuxOptions"]["user"] = "system_u"
+        if self.p(0.005):
+            sc["procMount"] = "Unmasked"
+        elif self.p(0.01):
+            sc["procMount"] = "Default"
+        if self.p(0.002):
+            sc["windowsOptions"] = {"hostProcess": True}
+        if self.edge:
+            if self.p(0.004):
+                sc["privileged"] = "true"  # wrong JSON type (string)
+            if self.p(0.004):
+                sc["runAsUser"] = "1000"
+            if self.p(0.003):
+                sc["runAsUser"] = 1000.0 if self.p(0.5) else 0.5
+            if self.p(0.003):
+                sc["allowPrivilegeEscalation"] = None
+            if self.p(0.002):
+                sc["capabilities"] = None
+        return sc
+
+    def container(self, i, kind="c"):
+        c = {"name": "%s%d" % (kind, i), "image": self.image()}
+        if self.p(0.7):
+            ports = []
+            for j in range(self.r.choice([1, 1, 2, 3])):
+                pt = {"containerPort": self.r.choice([80, 443, 8080, 9090, 5432]) + j, "protocol": "TCP"}
+                if self.p(0.02):
+                    pt["hostPort"] = self.r.choice([80, 8080, 30000])
+                elif self.p(0.05):
+                    pt["hostPort"] = 0
+                ports.append(pt)
+            c["ports"] = ports
+        if self.p(0.75):
+            c["securityContext"] = self.sec_ctx()
+        if self.p(0.8):
+            res = {}
+            if self.p(0.9):
+                res["requests"] = {"cpu": self.r.choice(QTY[:4]), "memory": self.r.choice(QTY[4:])}
+                if self.p(0.1):
+                    del res["requests"]["cpu"]
+            if self.p(0.85):
+                res["limits"] = {"memory": self.r.choice(QTY[4:])}
+                if self.p(0.5):
+                    res["limits"]["cpu"] = self.r.choice(QTY[:4])
+            if self.edge and self.p(0.01):
+                res["limits"] = {"memory": self.r.choice([1073741824, 0.5, "", None])}
+            c["resources"] = res
+        if self.p(0.3):
+            c["imagePullPolicy"] = self.r.choice(["Always", "IfNotPresent", "Never"])
+        if self.p(0.2):
+            c["env"] = [{"name": "E%d" % k, "value": str(self.r.randint(0, 99))} for k in range(self.r.randint(1, 4))]
+        return c
+
+    def pod_spec(self):
+        spec = {}
+        n = self.r.choices([1, 2, 3, 4], weights=[60, 25, 10, 5])[0]
+        spec["containers"] = [self.container(i) for i in range(n)]
+        if self.p(0.2):
+            spec["initContainers"] = [self.container(0, "init")]
+        if self.p(0.01):
+            spec["ephemeralContainers"] = [self.container(0, "debug")]
+        for f in ("hostNetwork", "hostPID", "hostIPC"):
+            if self.p(0.01):
+                spec[f] = True
+            elif self.p(0.05):
+                spec[f] = False
+        psc = {}
+        if self.p(0.4):
+            psc["runAsNonRoot"] = True
+        if self.p(0.01):
+            psc["runAsUser"] = 0
+        if self.p(0.3):
+            psc["fsGroup"] = self.r.choice([0, 2000])
+        if self.p(0.15):
+            psc["runAsGroup"] = self.r.choice([0, 3000])
+        if self.p(0.1):
+            psc["supplementalGroups"] = [self.r.choice([0, 4000])]
+        if self.p(0.3):
+            psc["seccompProfile"] = {"type": self.r.choice(["RuntimeDefault", "RuntimeDefault", "Localhost", "Unconfined"])}
+        if self.p(0.02):
+            psc["sysctls"] = [{"name": self.r.choice(SYSCTL_OK if self.p(0.5) else SYSCTL_BAD), "value": "1"}]
+        if self.p(0.01):
+            psc["seLinuxOptions"] = {"type": "container_t", "level": "s0:c123,c456"}
+        if psc or self.p(0.2):
+            spec["securityContext"] = psc
+        vols = []
+        for k in range(self.r.choice([0, 0, 1, 2, 3])):
+            t = self.r.choice(VOL_TYPES)
+            v = {"name": "vol%d" % k, t: {} if t not in ("nfs",) else {"server": "nfs.local", "path": "/x"}}
+            vols.append(v)
+        if self.p(0.03):
+            vols.append({"name": "hostvol", "hostPath": {"path": self.r.choice(["/var/run/docker.sock", "/data"])}})
+        if vols:
+            spec["volumes"] = vols
+        if self.p(0.01):
+            spec["os"] = {"name": "windows" if self.p(0.3) else "linux"}
+        if self.p(0.3):
+            spec["serviceAccountName"] = "sa-%d" % self.r.randint(0, 9)
+        if self.edge:
+            if self.p(0.003):
+                spec["hostNetwork"] = "false"
+            if self.p(0.003):
+                spec["containers"] = []
+            if self.p(0.002):
+                spec["volumes"] = None
+        return spec
+
+    def metadata(self, name, ns, pod=True, ncontainers=1):
+        labels = {"app": "app-%d" % self.r.randint(0, 300), "app.kubernetes.io/name": name.split("-")[0],
+                  "tier": self.r.choice(["frontend", "backend", "data"])}
+        for k in range(self.r.randint(0, 5)):
+            labels["label-%d" % k] = "v%d" % self.r.randint(0, 9)
+        if self.p(0.3):
+            labels["owner"] = "team-%d" % self.r.randint(0, 30)
+        md = {"name": name, "namespace": ns, "labels": labels}
+        ann = {}
+        for k in range(self.r.randint(0, 6)):
+            ann["example.com/a%d" % k] = "value-%d" % self.r.randint(0, 999)
+        if pod and self.p(0.05):
+            ann["container.apparmor.security.beta.kubernetes.io/c0"] = "unconfined" if self.p(0.2) else "runtime/default"
+        if pod and self.p(0.01):
+            ann["seccomp.security.alpha.kubernetes.io/pod"] = "unconfined" if self.p(0.5) else "runtime/default"
+        if ann:
+            md["annotations"] = ann
+        if self.edge and self.p(0.002):
+            md["labels"] = {"app": 7}  # non-string label value (apimachinery GetLabels -> nil)
+        return md
+
+    def pod(self, i):
+        ns = self.r.choice(self.namespaces)
+        name = "pod-%07d" % i
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": self.metadata(name, ns), "spec": self.pod_spec()}
+
+    def workload(self, i):
+        u = self.r.random() * 100
+        if u < 70:
+            return self.pod(i)
+        ns = self.r.choice(self.namespaces)
+        kinds = [(82, "apps/v1", "Deployment"), (86, "apps/v1", "ReplicaSet"), (89, "apps/v1", "StatefulSet"),
+                 (91, "apps/v1", "DaemonSet"), (94, "batch/v1", "Job"), (96, "batch/v1", "CronJob"),
+                 (97, "v1", "ReplicationController")]
+        for thr, av, kind in kinds:
+            if u < thr:
+                name = "%s-%07d" % (kind.lower(), i)
+                tpl = {"metadata": {"labels": {"app": name}}, "spec": self.pod_spec()}
+                if self.p(0.05):
+                    tpl["metadata"]["annotations"] = {"container.apparmor.security.beta.kubernetes.io/c0": "runtime/default"}
+                if kind == "CronJob":
+                    spec = {"schedule": "*/5 * * * *", "jobTemplate": {"spec": {"template": tpl}}}
+                elif kind == "Job":
+                    spec = {"template": tpl, "backoffLimit": 3}
+                else:
+                    spec = {"replicas": self.r.randint(1, 5), "selector": {"matchLabels": {"app": name}}, "template": tpl}
+                return {"apiVersion": av, "kind": kind, "metadata": self.metadata(name, ns, pod=False), "spec": spec}
+        k = self.r.choice(["ConfigMap", "Service", "Namespace"])
+        name = "%s-%07d" % (k.lower(), i)
+        if k == "ConfigMap":
+            return {"apiVersion": "v1", "kind": k, "metadata": self.metadata(name, ns, pod=False), "data": {"k": "v"}}
+        if k == "Service":
+            return {"apiVersion": "v1", "kind": k, "metadata": self.metadata(name, ns, pod=False),
+                    "spec": {"type": self.r.choice(["ClusterIP", "LoadBalancer"]), "ports": [{"port": 80}]}}
+        return {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": self.r.choice(self.namespaces)}}
+
+
+def pods(n, seed=SEED, edge=False):
+    g = Gen(seed, edge)
+    return [g.pod(i) for i in range(n)], g.ns_labels()
+
+
+def mixed(n, seed=SEED, edge=False):
+    g = Gen(seed, edge)
+    return [g.workload(i) for i in range(n)], g.ns_labels()
+
+
+def ndjson(docs):
+    return ("\n".join(json.dumps(d, separators=(",", ":")) for d in docs)).encode()
+
+
+def _chunk(args):
+    kind, seed, start, n, edge = args
+    g = Gen((seed * 1000003 + start) & 0xFFFFFFFFFFFF, edge)
+    make = g.pod if kind == "pods" else g.workload
+    return ("\n".join(json.dumps(make(start + i), separators=(",", ":")) for i in range(n)) + "\n").encode()
+
+
+def corpus_ndjson(n, kind="mixed", seed=SEED, edge=False, workers=None, chunk=20000):
+    """Large seeded corpus as NDJSON bytes, generated in parallel chunks (resource names stay unique:
+    the chunk's first index is part of every name). Returns (bytes, namespace labels)."""
+    import multiprocessing as mp
+    import os
+    jobs = [(kind, seed, s, min(chunk, n - s), edge) for s in range(0, n, chunk)]
+    workers = workers or min(len(jobs), int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1, 16)
+    if workers <= 1 or len(jobs) == 1:
+        parts = [_chunk(j) for j in jobs]
+    else:
+        with mp.get_context("fork").Pool(workers) as pool:
+            parts = pool.map(_chunk, jobs)
+    return b"".join(parts), Gen(seed).ns_labels()

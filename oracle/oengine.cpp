@@ -624,8 +624,6 @@ std::string rule_unsupported_reason(const VP& rule) {
   if (!val) return "";
   if (!isnil(val->get("deny"))) return "deny";
   if (contains_vars(val->get("pattern")) || contains_vars(val->get("anyPattern"))) return "variables";
-  if (oj::get_str(val, "message").find("{{") != std::string::npos || oj::get_str(val, "message").find("$(") != std::string::npos)
-    return "message-variables";
   if (isnil(val->get("pattern")) && isnil(val->get("anyPattern")) && isnil(val->get("podSecurity")) && has_nonempty(val, "foreach"))
     return "foreach";
   if (!isnil(val->get("manifests"))) return "manifests";
@@ -643,7 +641,7 @@ static std::string build_error_message(const std::string& rname, const std::stri
   return "validation error: " + msg + " rule " + rname + " execution error: " + err;
 }
 
-RuleResult validate_rule(const VP& rule, const VP& resource) {
+static RuleResult validate_rule_body(const VP& rule, const VP& resource) {
   RuleResult out;
   out.name = oj::get_str(rule, "name");
   std::string why = rule_unsupported_reason(rule);
@@ -757,6 +755,15 @@ RuleResult validate_rule(const VP& rule, const VP& resource) {
     return out;
   }
   out.status = "none";  // "invalid validation rule": no response
+  return out;
+}
+
+RuleResult validate_rule(const VP& rule, const VP& resource) {
+  RuleResult out = validate_rule_body(rule, resource);
+  // Variables in validate.message change only the message text (validation.go:469, :731), never the verdict:
+  // the verdict stays pinned, the rendered text is left to the JMESPath substitution on the host.
+  std::string msg = oj::get_str(rule->get("validate"), "message");
+  if (msg.find("{{") != std::string::npos || msg.find("$(") != std::string::npos) out.message_unpinned = true;
   return out;
 }
 

@@ -1,0 +1,77 @@
+"""Shared parity harness: evaluate (resource x rule) pairs through libkyvgpu and compare with the oracle.
+
+The oracle (oracle/, CPU restatement of the reference) is used here only as the checker.
+"""
+import json
+
+from kyverno_amd import _lib as K
+from kyverno_amd import engine as E
+from oracle import oracle as O
+
+ORACLE_STATUS = {"pass": K.ST_PASS, "fail": K.ST_FAIL, "skip": K.ST_SKIP, "error": K.ST_ERROR, "panic": K.ST_PANIC}
+
+
+def oracle_pairs(policies, resources, ns_labels):
+    """-> dict (policy name, rule name, resource index) -> oracle rule result (matched pairs only)."""
+    out = {}
+    for ri, res in enumerate(resources):
+        ns = (res.get("metadata") or {}).get("namespace") if isinstance(res.get("metadata"), dict) else None
+        nsl = ns_labels.get(ns) if (ns_labels and isinstance(ns, str)) else None
+        pr = O.validate(policies, json.dumps(res), nsl if nsl is not None else {})
+        for p in pr:
+            for rr in p["rules"]:
+                out[(p["policy"], rr["name"], ri)] = rr
+    return out
+
+
+def compare(policies, resources, ns_labels=None, backend="gpu", check_messages=True, max_report=20):
+    """Returns a stats dict; raises AssertionError on verdict/path/message mismatches."""
+    rs = E.Ruleset(policies)
+    b = E.Batch(rs, resources, ns_labels)
+    res = E.evaluate(rs, b, backend=backend)
+    ora = oracle_pairs(policies, resources, ns_labels or {})
+    st = res.status
+    stats = {"pairs": 0, "matched": 0, "compared": 0, "fallback": 0, "nd": 0, "messages": 0, "unsupported": 0}
+    bad = []
+    for k, rule in enumerate(rs.rules):
+        pol = rs.policies[rule["policy"]]["name"]
+        for ri in range(len(resources)):
+            stats["pairs"] += 1
+            s = int(st[k, ri])
+            o = ora.get((pol, rule["name"], ri))
+            if s == K.ST_NONE:
+                if o is not None:
+                    bad.append(("matched by oracle only", pol, rule["name"], ri, o["status"]))
+                continue
+            stats["matched"] += 1
+            if o is None:
+                if s not in (K.ST_FALLBACK,):
+                    bad.append(("matched by device only", pol, rule["name"], ri, K.STATUS_NAMES[s]))
+                continue
+            if s == K.ST_FALLBACK or o["status"] == "unsupported":
+                stats["fallback"] += 1
+                if o["status"] == "unsupported" and s != K.ST_FALLBACK:
+                    bad.append(("oracle unsupported, device verdict", pol, rule["name"], ri, K.STATUS_NAMES[s]))
+                continue
+            if s == K.ST_ND or o.get("nondeterministic"):
+                stats["nd"] += 1
+                continue
+            stats["compared"] += 1
+            want = ORACLE_STATUS.get(o["status"])
+            if want != s:
+                bad.append(("status", pol, rule["name"], ri, K.STATUS_NAMES[s], o["status"], o["message"][:160]))
+                continue
+            if s == K.ST_FAIL and rule["kind"] == "pattern":
+                p = res.path(ri, k)
+                if p != o["path"]:
+                    bad.append(("path", pol, rule["name"], ri, p, o["path"]))
+            if check_messages:
+                m = res.message(ri, k)
+                if m is not None:
+                    stats["messages"] += 1
+                    if m != o["message"] and not o.get("message_unpinned"):
+                        bad.append(("message", pol, rule["name"], ri, m[:200], o["message"][:200]))
+    stats["bad"] = bad[:max_report]
+    stats["nbad"] = len(bad)
+    stats["counts"] = res.counts
+    return stats, res
