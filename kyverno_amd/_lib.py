@@ -96,6 +96,10 @@ def lib():
     return L
 
 
+class KyvError(RuntimeError):
+    """A libkyvgpu call returned an error status (message from kyv_last_error)."""
+
+
 def check(rc):
     if rc != 0:
-        raise RuntimeError("kyvgpu error %d: %s" % (rc, lib().kyv_last_error().decode(errors="replace")))
+        raise KyvError("kyvgpu error %d: %s" % (rc, lib().kyv_last_error().decode(errors="replace")))

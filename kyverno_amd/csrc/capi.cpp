@@ -40,8 +40,8 @@ const char* kyv_last_error(void) { return g_err.c_str(); }
 const char* kyv_version(void) { return "kyvgpu 0.1 (gfx950)"; }
 
 int kyv_ruleset_compile(const char* json, size_t len, const kyv_compile_opts* opts, kyv_ruleset** out) {
-  (void)opts;
   if (!json || !out) return fail(KYV_EINVAL, "null argument");
+  if (opts && opts->abi_version != KYV_ABI_VERSION) return fail(KYV_EINVAL, "ABI version mismatch");
   try {
     std::string err;
     Ruleset* rs = compile_ruleset(json, len, &err);
@@ -88,6 +88,7 @@ int kyv_ruleset_policy_info(const kyv_ruleset* rs, uint32_t p, kyv_policy_info* 
 int kyv_batch_build(const kyv_ruleset* rs, const char* json, size_t len, const char* nsl, size_t nsl_len,
                     const kyv_batch_opts* opts, kyv_batch** out) {
   if (!rs || !json || !out) return fail(KYV_EINVAL, "null argument");
+  if (opts && opts->abi_version != KYV_ABI_VERSION) return fail(KYV_EINVAL, "ABI version mismatch");
   try {
     std::string err;
     Batch* b = build_batch(rs->rs, json, len, nsl, nsl_len, hw_threads(opts ? opts->threads : 0), &err);
@@ -123,6 +124,7 @@ int kyv_batch_stats_get(const kyv_batch* b, kyv_batch_stats* out) {
 int kyv_eval(const kyv_ruleset* rs, const kyv_batch* b, const kyv_eval_opts* opts, kyv_results** out) {
   if (!rs || !b || !out) return fail(KYV_EINVAL, "null argument");
   if (b->b->rs != rs->rs) return fail(KYV_EINVAL, "batch was built for a different ruleset");
+  if (opts && opts->abi_version != KYV_ABI_VERSION) return fail(KYV_EINVAL, "ABI version mismatch");
   int backend = opts ? opts->backend : KYV_BACKEND_GPU;
   try {
     auto* res = new kyv_results();

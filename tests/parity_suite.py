@@ -1,0 +1,57 @@
+"""Parity corpora run through libkyvgpu for a given backend and checked against the oracle (shared by
+test_cpu_backend_parity.py and test_gpu_parity.py)."""
+import cases
+import parity_util as PU
+
+
+def assert_clean(name, st):
+    assert st["nbad"] == 0, "%s: %d mismatches, first: %r" % (name, st["nbad"], st["bad"][:5])
+
+
+def run_engine_goldens(backend):
+    n = 0
+    for i, (pols, res) in enumerate(cases.engine_cases()):
+        st, _ = PU.compare(pols, res, None, backend=backend)
+        assert_clean("engine[%d]" % i, st)
+        n += st["compared"]
+    return n
+
+
+def run_cli_goldens(backend):
+    n = 0
+    for d, pols, res in cases.cli_cases():
+        st, _ = PU.compare(pols, res, None, backend=backend)
+        assert_clean("cli/" + d, st)
+        n += st["compared"]
+    return n
+
+
+def run_walk_goldens(backend):
+    pols, res = cases.walk_policy_cases()
+    n = 0
+    for i in range(len(pols)):
+        st, _ = PU.compare([pols[i]], [res[i]], None, backend=backend)
+        assert_clean("walk[%d]" % i, st)
+        n += st["compared"]
+    return n
+
+
+def run_pss_goldens(backend):
+    """pkg/pss/evaluate_test.go: device verdict must equal the oracle's and the reference's `allowed`."""
+    n = 0
+    for name, pol, pod, allowed in cases.pss_cases():
+        st, res = PU.compare([pol], [pod], None, backend=backend)
+        assert_clean("pss/" + name, st)
+        s = int(res.status[0, 0])
+        if s in (PU.K.ST_PASS, PU.K.ST_FAIL):
+            assert (s == PU.K.ST_PASS) == allowed, name
+        n += st["compared"]
+    return n
+
+
+def run_synthetic(backend, policies, n, seed, kind="mixed", edge=True):
+    from kyverno_amd import synth
+    docs, nsl = (synth.mixed if kind == "mixed" else synth.pods)(n, seed=seed, edge=edge)
+    st, res = PU.compare(policies, docs, nsl, backend=backend)
+    assert_clean("synthetic/%s/%d" % (kind, seed), st)
+    return st, res

@@ -1,0 +1,67 @@
+"""C-ABI boundary (include/kyvgpu.h): the library loads, exports every declared symbol, reports errors
+through return codes + kyv_last_error, and never falls back to the CPU when the GPU backend is asked for."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from kyverno_amd import _lib as K
+from kyverno_amd import engine as E
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "kyvgpu.h")) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(kyv_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported():
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    lib = ctypes.CDLL(K.LIB_PATH)
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(K.EXPORTS) == syms
+
+
+def test_version_and_errors():
+    L = K.lib()
+    assert L.kyv_version().decode().startswith("kyvgpu")
+    h = ctypes.c_void_p()
+    opts = K.CompileOpts(K.KYV_ABI_VERSION, 0)
+    rc = L.kyv_ruleset_compile(b"{not json", 9, ctypes.byref(opts), ctypes.byref(h))
+    assert rc != 0
+    assert L.kyv_last_error().decode()
+    with pytest.raises(K.KyvError):
+        E.Ruleset(b"[1,")
+
+
+def test_abi_version_checked():
+    L = K.lib()
+    h = ctypes.c_void_p()
+    opts = K.CompileOpts(K.KYV_ABI_VERSION + 100, 0)
+    assert L.kyv_ruleset_compile(b"[]", 2, ctypes.byref(opts), ctypes.byref(h)) != 0
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="host has a GPU")
+def test_gpu_backend_fails_loudly_without_device():
+    rs = E.Ruleset([{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "p"},
+                     "spec": {"rules": [{"name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                                         "validate": {"pattern": {"metadata": {"name": "?*"}}}}]}}])
+    b = E.Batch(rs, [{"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "x"}}])
+    with pytest.raises(K.KyvError, match="no HIP device"):
+        E.evaluate(rs, b, backend="gpu")
+
+
+def test_batch_for_other_ruleset_rejected():
+    p = [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "p"},
+          "spec": {"rules": [{"name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                              "validate": {"pattern": {"metadata": {"name": "?*"}}}}]}}]
+    a, b = E.Ruleset(p), E.Ruleset(p)
+    batch = E.Batch(a, [{"kind": "Pod", "metadata": {"name": "x"}}])
+    with pytest.raises(K.KyvError):
+        E.evaluate(b, batch, backend="cpu")

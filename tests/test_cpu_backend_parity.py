@@ -1,0 +1,32 @@
+"""The explicit CPU instantiation of the shared __host__ __device__ evaluator vs the oracle.
+
+This checks the compiler, flattener and evaluator logic without a GPU; the GPU kernel runs the same
+evaluator (tests/test_gpu_parity.py repeats these corpora on the device)."""
+import cases
+import parity_suite as S
+
+
+def test_engine_goldens():
+    assert S.run_engine_goldens("cpu") > 0
+
+
+def test_cli_goldens():
+    assert S.run_cli_goldens("cpu") > 0
+
+
+def test_walk_goldens():
+    assert S.run_walk_goldens("cpu") > 0
+
+
+def test_pss_goldens():
+    assert S.run_pss_goldens("cpu") > 0
+
+
+def test_c3_synthetic_edge():
+    st, _ = S.run_synthetic("cpu", cases.best_practices() + cases.chart_restricted(), 400, seed=21)
+    assert st["compared"] > 5000
+
+
+def test_quirk_policies():
+    st, _ = S.run_synthetic("cpu", cases.quirk_policies(), 400, seed=22)
+    assert st["compared"] > 2000

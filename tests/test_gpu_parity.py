@@ -1,0 +1,90 @@
+"""GPU parity: the HIP kernel (through the C-ABI) against the oracle, bit-exact verdicts, failing paths and
+messages, on the reference's golden corpora and on seeded synthetic corpora; plus size-independent checks at
+full batch sizes (GPU == explicit CPU instantiation of the same evaluator, count conservation, determinism)."""
+import numpy as np
+import pytest
+
+import cases
+import parity_suite as S
+from kyverno_amd import _lib as K
+from kyverno_amd import engine as E
+from kyverno_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def test_engine_goldens_gpu():
+    assert S.run_engine_goldens("gpu") > 0
+
+
+def test_cli_goldens_gpu():
+    assert S.run_cli_goldens("gpu") > 0
+
+
+def test_walk_goldens_gpu():
+    assert S.run_walk_goldens("gpu") > 0
+
+
+def test_pss_goldens_gpu():
+    assert S.run_pss_goldens("gpu") > 0
+
+
+def test_c3_synthetic_gpu():
+    st, res = S.run_synthetic("gpu", cases.best_practices() + cases.chart_restricted(), 3000, seed=31)
+    assert st["compared"] > 50000
+    assert res.kernel_ms > 0
+
+
+def test_c2_pss_pods_gpu():
+    pol = [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "psa"},
+            "spec": {"rules": [{"name": "restricted", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                                "validate": {"podSecurity": {"level": "restricted", "version": "latest"}}}]}}]
+    st, _ = S.run_synthetic("gpu", pol, 4000, seed=32, kind="pods")
+    assert st["compared"] >= 4000
+
+
+def test_quirk_policies_gpu():
+    st, _ = S.run_synthetic("gpu", cases.quirk_policies(), 3000, seed=33)
+    assert st["compared"] > 10000
+
+
+def test_gpu_equals_cpu_instantiation_at_scale():
+    """200k mixed resources x C3 rules: identical verdict bytes, PSS masks and failing paths."""
+    data, nsl = synth.corpus_ndjson(200_000, seed=34, edge=True)
+    rs = E.Ruleset(cases.best_practices() + cases.chart_restricted())
+    b = E.Batch(rs, data, nsl)
+    g = E.evaluate(rs, b, backend="gpu")
+    c = E.evaluate(rs, b, backend="cpu")
+    assert np.array_equal(g.raw, c.raw)
+    assert g.counts == c.counts
+    assert sum(g.counts.values()) == len(rs.rules) * b.n
+    rng = np.random.default_rng(0)
+    fail = np.argwhere(g.status == K.ST_FAIL)
+    for k, r in fail[rng.choice(len(fail), size=min(2000, len(fail)), replace=False)]:
+        assert g.path(int(r), int(k)) == c.path(int(r), int(k))
+        assert g.message(int(r), int(k)) == c.message(int(r), int(k))
+        if rs.rules[k]["kind"] == "pss":
+            assert g.pss_mask(int(r), int(k)) == c.pss_mask(int(r), int(k))
+
+
+def test_repeat_launches_deterministic():
+    data, nsl = synth.corpus_ndjson(50_000, seed=35)
+    rs = E.Ruleset(cases.best_practices() + cases.chart_restricted())
+    b = E.Batch(rs, data, nsl)
+    a = E.evaluate(rs, b, backend="gpu")
+    z = E.evaluate(rs, b, backend="gpu", iterations=3)
+    assert np.array_equal(a.raw, z.raw)
+    assert a.counts == z.counts
+    nc = E.evaluate(rs, b, backend="gpu", copy_back=False)
+    assert nc.counts == a.counts
+
+
+def test_empty_and_tiny_batches_gpu():
+    rs = E.Ruleset(cases.best_practices())
+    for docs in ([], [{}], [{"kind": "Pod"}], [{"apiVersion": "v1", "kind": "Pod", "metadata": None, "spec": []}]):
+        b = E.Batch(rs, docs)
+        g = E.evaluate(rs, b, backend="gpu")
+        c = E.evaluate(rs, b, backend="cpu")
+        assert b.n == len(docs)
+        if b.n:
+            assert np.array_equal(g.raw, c.raw)
