@@ -24,6 +24,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6300 GB/s mea
 SEED = 0x4B59564E
 
 
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
 def load_policies(workload):
     gdir = os.path.join(ROOT, "tests", "golden")
     if workload == "c2":
@@ -111,11 +115,13 @@ def main():
     t0 = time.time()
     data, nsl = synth.corpus_ndjson(nper, kind=kind, seed=SEED + rank)
     t_gen = time.time() - t0
+    log("rank %d: generated %d resources (%.1f MB) in %.1f s" % (rank, nper, len(data) / 1e6, t_gen))
     rs = E.Ruleset(policies)
     nrules = len(rs.rules)
     t0 = time.time()
     batch = E.Batch(rs, data, nsl)
     t_flat = time.time() - t0
+    log("rank %d: flattened %d resources into %d node rows in %.1f s" % (rank, batch.n, batch.stats()["nodes"], t_flat))
     pairs = nrules * batch.n
 
     # algorithmic bytes per eval: CPU accounting over a sample of this shard
@@ -124,12 +130,14 @@ def main():
     acct = E.evaluate(rs, sb, backend="cpu", account_bytes=True)
     bytes_per_eval = acct.alg_bytes / max(1, nrules * sb.n)
     del sb, acct
+    log("rank %d: %.1f algorithmic bytes per eval (CPU accounting over %d resources)" % (rank, bytes_per_eval, sample_n))
 
     # warmup (first call uploads the batch and allocates the resident result buffers)
     t0 = time.time()
     first = E.evaluate(rs, batch, backend="gpu", device=local, copy_back=False)
     t_upload = time.time() - t0
     counts = first.counts
+    log("rank %d: first GPU evaluation (incl. upload) %.2f s, kernel %.2f ms" % (rank, t_upload, first.kernel_ms))
     del first
     for _ in range(max(0, args.warmup - 1)):
         E.evaluate(rs, batch, backend="gpu", device=local, copy_back=False)

@@ -199,19 +199,37 @@ long long oracle_validate_batch(const char* policies_json, const char* resources
 #include <chrono>
 #include <thread>
 
-// Batch entry for the CPU baseline (bench.py cpu_baseline leg): policies' computed rules are prepared once,
-// resources are decoded before the clock starts; the timed region is the per-(resource, rule) evaluation
-// exactly as engine.Validate performs it (match incl. OldResource retry, pattern walk / PSS).
+// Batch entry for the CPU baseline (bench.py cpu_baseline leg). Policies' computed rules are prepared once
+// (generous to the CPU: engine.Validate recomputes them per call, validation.go:118) and resources are decoded
+// before the clock starts. The timed region is the per-(resource, policy) loop of engine.Validate
+// (validation.go:120-183): namespaced-policy filter, match incl. OldResource retry, pattern walk / PSS,
+// applyRules: One truncation. Returns resources x compiled validate rules (the bench's unit of work).
 long long oracle_validate_batch(const char* policies_json, const char* resources_json, const char* nslabels_json, int nthreads,
                                 long long* status_counts, double* seconds) {
   VP pols = oj::parse(policies_json, true);
   VP res = oj::parse(resources_json, false);
   VP nsl = nslabels_json && *nslabels_json ? oj::parse(nslabels_json, false) : nullptr;
-  auto nsLabels = labels_of(nsl);
-  std::vector<VP> rules;
+  std::map<std::string, std::map<std::string, std::string>> nsLabels;  // namespace -> labels
+  if (nsl && nsl->t == T::Obj) for (auto& kv : nsl->o) nsLabels[kv.first] = labels_of(kv.second);
+  static const std::map<std::string, std::string> kNoLabels;
+  struct Pol { VP policy; std::vector<VP> rules; bool namespaced; std::string ns; bool applyOne; };
+  std::vector<Pol> plist;
   std::vector<VP> list;
   if (pols->t == T::Arr) list = pols->a; else list.push_back(pols);
-  for (auto& p : list) for (auto& r : compute_rules(p)) rules.push_back(r);
+  size_t nrules = 0;
+  for (auto& p : list) {
+    if (!p || p->t != T::Obj) continue;
+    std::string kind = oj::get_str(p, "kind");
+    if (kind != "ClusterPolicy" && kind != "Policy") continue;
+    Pol x{p, {}, kind == "Policy", nested_string(p, {"metadata", "namespace"}),
+          oj::get_str(p->get("spec"), "applyRules") == "One"};
+    for (auto& r : compute_rules(p)) {
+      VP v = r->get("validate");
+      if ((v && v->t == T::Obj && !v->o.empty()) || has_nonempty(r, "verifyImages")) x.rules.push_back(r);
+    }
+    nrules += x.rules.size();
+    plist.push_back(std::move(x));
+  }
   std::vector<VP>& rs = res->a;
   if (nthreads < 1) nthreads = 1;
   std::atomic<long long> cnt[5];
@@ -225,17 +243,29 @@ long long oracle_validate_batch(const char* policies_json, const char* resources
       if (i >= rs.size()) break;
       size_t e = std::min(rs.size(), i + 64);
       for (size_t k = i; k < e; k++) {
-        for (auto& rule : rules) {
-          bool nd = false;
-          bool m = matches_resource_description(rule, rs[k], nsLabels, &nd);
-          if (!m) m = matches_resource_description(rule, nullptr, nsLabels, &nd);
-          if (!m) { local[4]++; continue; }
-          RuleResult rr = validate_rule(rule, rs[k]);
-          if (rr.status == "pass") local[0]++;
-          else if (rr.status == "fail") local[1]++;
-          else if (rr.status == "skip") local[2]++;
-          else if (rr.status == "error") local[3]++;
-          else local[4]++;
+        const VP& r = rs[k];
+        std::string rns = nested_string(r, {"metadata", "namespace"});
+        auto it = nsLabels.find(rns);
+        const auto& labels = it == nsLabels.end() ? kNoLabels : it->second;
+        for (auto& pol : plist) {
+          if (pol.namespaced && (rns != pol.ns || rns.empty())) { local[4] += pol.rules.size(); continue; }
+          int applied = 0;
+          size_t done = 0;
+          for (auto& rule : pol.rules) {
+            done++;
+            bool nd = false;
+            bool m = matches_resource_description(rule, r, labels, &nd);
+            if (!m) m = matches_resource_description(rule, nullptr, labels, &nd);
+            if (!m) { local[4]++; continue; }
+            RuleResult rr = validate_rule(rule, r);
+            if (rr.status == "pass") local[0]++, applied++;
+            else if (rr.status == "fail") local[1]++, applied++;
+            else if (rr.status == "skip") local[2]++;
+            else if (rr.status == "error") local[3]++;
+            else local[4]++;
+            if (pol.applyOne && applied > 0) break;
+          }
+          local[4] += pol.rules.size() - done;
         }
       }
     }
@@ -247,7 +277,7 @@ long long oracle_validate_batch(const char* policies_json, const char* resources
   auto t1 = std::chrono::steady_clock::now();
   if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
   if (status_counts) for (int j = 0; j < 5; j++) status_counts[j] = cnt[j];
-  return (long long)rs.size() * (long long)rules.size();
+  return (long long)rs.size() * (long long)nrules;
 }
 
 extern "C" {

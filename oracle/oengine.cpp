@@ -43,7 +43,7 @@ static bool nested(const VP& obj, std::initializer_list<const char*> path, VP& o
   out = cur;
   return true;
 }
-static std::string nested_string(const VP& obj, std::initializer_list<const char*> path) {
+std::string nested_string(const VP& obj, std::initializer_list<const char*> path) {
   VP v;
   if (!nested(obj, path, v) || !v || v->t != T::Str) return "";
   return v->s;
@@ -392,7 +392,7 @@ static bool check_autogen_support(bool& needed, const VP& rd) {
   for (auto& k : kinds) if (podctl.count(k)) needed = true;
   return true;
 }
-static bool has_nonempty(const VP& o, const char* k) {
+bool has_nonempty(const VP& o, const char* k) {
   VP v = o ? o->get(k) : nullptr;
   if (isnil(v)) return false;
   if (v->t == T::Obj) return !v->o.empty();
