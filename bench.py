@@ -81,7 +81,7 @@ def cpu_baseline(policies, data, nsl, nrules, target_s=10.0):
     """Oracle (CPU restatement of engine.Validate) on a bounded prefix of this rank's corpus."""
     from oracle import oracle as O
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
-    lines = data.split(b"\n", 4096)[:4096]
+    lines = data.split(b"\n", 400000)[:400000]
     probe = b"[" + b",".join(lines[:256]) + b"]"
     n, _, secs = O.validate_batch(policies, probe, nsl, threads)
     rate = n / max(secs, 1e-9)  # pairs / s
@@ -113,7 +113,7 @@ def main():
     policies = load_policies(args.workload)
 
     t0 = time.time()
-    data, nsl = synth.corpus_ndjson(nper, kind=kind, seed=SEED + rank)
+    data, nsl = synth.cached_corpus(nper, kind=kind, seed=SEED + rank)
     t_gen = time.time() - t0
     log("rank %d: generated %d resources (%.1f MB) in %.1f s" % (rank, nper, len(data) / 1e6, t_gen))
     rs = E.Ruleset(policies)

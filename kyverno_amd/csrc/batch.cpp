@@ -93,6 +93,7 @@ struct Emitter {
       case T::Obj: {
         n.tk = N_MAP;
         n.b = (uint32_t)v.o.size();
+        if (v.o.size() > 0xFFFF) magicflag = true;  // walk frames count entries in 16 bits
         out[idx] = n;  // reserve before recursion (out may grow)
         uint32_t first = put_children_map(v);
         out[idx].a = first;
@@ -102,6 +103,7 @@ struct Emitter {
       case T::Arr: {
         n.tk = N_ARR;
         n.b = (uint32_t)v.a.size();
+        if (v.a.size() > 0xFFFF) magicflag = true;  // walk frames count elements in 16 bits
         out[idx] = n;
         uint32_t first = (uint32_t)out.size();
         out.resize(first + v.a.size());

@@ -235,6 +235,9 @@ int64_t kyv_results_path(const kyv_results* cr, const kyv_ruleset* crs, const ky
                          char* buf, size_t cap) {
   auto* r = const_cast<kyv_results*>(cr);
   if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
+  // records exist for every failing alternative walked, also when a later anyPattern alternative passed
+  if ((r->r.status[(size_t)rule * r->r.nres + res] & 7) != ST_FAIL || crs->rs->rules[rule].kind != RK_PATTERN)
+    return put("", buf, cap);
   ensure_index(r);
   auto it = r->recidx.find(((uint64_t)rule << 32) | res);
   if (it == r->recidx.end()) return put("", buf, cap);

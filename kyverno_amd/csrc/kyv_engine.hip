@@ -57,10 +57,11 @@ struct DeviceResults {
   size_t nres = 0, nrules = 0;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  View* view = nullptr;  // device copy of the View the kernel reads
 };
 
 static void free_dev_results(DeviceResults& d) {
-  hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
+  hipFree(d.view); hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
   if (d.e0) hipEventDestroy(d.e0);
   if (d.e1) hipEventDestroy(d.e1);
   if (d.stream) hipStreamDestroy(d.stream);
@@ -185,41 +186,43 @@ struct DevOut {
   uint32_t rule_lo, rule_hi;   // rule range handled by this launch
 };
 
-__global__ void __launch_bounds__(BLOCK) eval_kernel(View v, DevOut o, int depth) {
+// Failing-path records of one wave, appended with one atomic per emit point that has any record.
+struct WaveSink {
+  FailRec* recs;
+  uint32_t* n;
+  uint32_t max;
+  __device__ __forceinline__ void emit(bool has, const FailRec& f) {
+    unsigned long long m = __ballot(has);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & (WAVE - 1);
+    const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(n, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (has) {
+      uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+      if (at < max) recs[at] = f;
+    }
+  }
+};
+
+// One lane per resource, the rule loop uniform across the wave. `vp` points at a device-resident View so
+// that its fields are read with scalar loads instead of being copied into per-lane private memory.
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) eval_kernel(const View* __restrict__ vp, DevOut o, int depth) {
   extern __shared__ Frame lds_frames[];  // [depth][BLOCK]
+  const View& v = *vp;
   const uint32_t lane = threadIdx.x;
   const uint32_t r = blockIdx.x * BLOCK + lane;
   const bool active = r < v.nres;
   Stack stk{lds_frames + lane, BLOCK, depth};
-  __shared__ unsigned long long cnt[NSTATUS];
+  WaveSink sink{o.recs, o.nrecs, o.max_recs};
   for (uint32_t k = o.rule_lo; k < o.rule_hi; k++) {
-    uint8_t st = ST_NONE;
-    uint32_t pf = 0, nrec = 0;
-    FailRec recs[RECS_PER_PAIR];
+    uint32_t pf = 0;
+    uint8_t st = eval_pair(v, active, r, k, stk, &pf, sink);
     if (active) {
-      st = eval_pair(v, r, k, stk, &pf, recs, &nrec, RECS_PER_PAIR);
       o.status[(size_t)k * v.nres + r] = st;
       uint32_t ps = o.pss_slot[k];
       if (ps != NONE) o.pss_fails[(size_t)ps * v.nres + r] = pf;
-    }
-    // compact failing-path records: one atomic per wave
-    unsigned long long has = __ballot(nrec > 0);
-    if (has) {
-      uint32_t mine = nrec;
-      // prefix sum of record counts across the wave (records are rare: lane-serial scan is fine)
-      uint32_t excl = 0, total = 0;
-      for (int l = 0; l < WAVE; l++) {
-        uint32_t n = __shfl(mine, l);
-        if (l < (int)lane) excl += n;
-        total += n;
-      }
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(o.nrecs, total);
-      base = __shfl(base, 0);
-      for (uint32_t i = 0; i < mine; i++) {
-        uint32_t at = base + excl + i;
-        if (at < o.max_recs) o.recs[at] = recs[i];
-      }
     }
     // per-rule status counts: wave ballots -> one atomic per status present
     for (int s = 0; s < NSTATUS; s++) {
@@ -227,7 +230,6 @@ __global__ void __launch_bounds__(BLOCK) eval_kernel(View v, DevOut o, int depth
       if (m && lane == 0) atomicAdd(&o.counts[(size_t)k * NSTATUS + s], (unsigned long long)__popcll(m));
     }
   }
-  (void)cnt;
 }
 
 // ---------------------------------------------------------------- host entry
@@ -311,6 +313,8 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.e0));
     HIP_OK(hipEventCreate(&d.e1));
+    HIP_OK(hipMalloc(&d.view, sizeof(View)));
+    HIP_OK(hipMemcpy(d.view, &v, sizeof(View), hipMemcpyHostToDevice));
     db->out = dd;
   }
   DeviceResults& d = *db->out;
@@ -325,7 +329,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
     HIP_OK(hipMemsetAsync(d.counts, 0, nrules * NSTATUS * 8, stream));
     HIP_OK(hipEventRecord(d.e0, stream));
-    if (nres && nrules) hipLaunchKernelGGL(eval_kernel, grid, dim3(BLOCK), lds, stream, v, o, depth);
+    if (nres && nrules) hipLaunchKernelGGL(eval_kernel, grid, dim3(BLOCK), lds, stream, (const View*)d.view, o, depth);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d.e1, stream));
     HIP_OK(hipEventSynchronize(d.e1));
@@ -360,6 +364,14 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   }
 }
 
+struct HostSink {
+  std::vector<FailRec>* out;
+  uint32_t emitted;
+  void emit(bool has, const FailRec& f) {
+    if (has) { out->push_back(f); emitted++; }
+  }
+};
+
 // Explicit CPU backend (development / message formatting only; never selected implicitly).
 // With `account` set it also sums the algorithmic bytes of SURVEY §8(d) per pair: the header fields the
 // match program reads (16 B), every distinct node-table row the pair touches (16 B each), the verdict byte,
@@ -382,26 +394,26 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
     th.emplace_back([&, t]() {
       Frame frames[MAX_DEPTH];
       Stack stk{frames, 1, MAX_DEPTH};
-      FailRec fr[RECS_PER_PAIR];
+      HostSink sink{&recs[t], 0};
       std::vector<uint8_t> seen;
       TouchAcct acct{nullptr, 0, 0};
       for (size_t r = t; r < nres; r += T)
         for (size_t k = 0; k < nrules; k++) {
-          uint32_t pf, nrec;
+          uint32_t pf;
+          sink.emitted = 0;
           if (account) {
             uint32_t nn = b.hdr[r].nnodes;
             seen.assign(nn, 0);
             acct = TouchAcct{seen.data(), nn, 0};
             g_touch = &acct;
           }
-          uint8_t st = eval_pair(v, (uint32_t)r, (uint32_t)k, stk, &pf, fr, &nrec, RECS_PER_PAIR);
+          uint8_t st = eval_pair(v, true, (uint32_t)r, (uint32_t)k, stk, &pf, sink);
           if (account) {
             g_touch = nullptr;
-            bytes[t] += 16 + 16 * acct.rows + 1 + (pss_slot[k] != NONE ? 4 : 0) + (uint64_t)nrec * sizeof(FailRec);
+            bytes[t] += 16 + 16 * acct.rows + 1 + (pss_slot[k] != NONE ? 4 : 0) + (uint64_t)sink.emitted * sizeof(FailRec);
           }
           out->status[k * nres + r] = st;
           if (pss_slot[k] != NONE) out->pss_fails[(size_t)pss_slot[k] * nres + r] = pf;
-          for (uint32_t i = 0; i < nrec; i++) recs[t].push_back(fr[i]);
         }
     });
   for (auto& x : th) x.join();

@@ -18,6 +18,17 @@ namespace kyv {
 
 #define KYV_HD __host__ __device__ inline
 #define KYV_BIG __host__ __device__ __attribute__((noinline))
+// Inlining policy of the large evaluator stages (overridable for experiments)
+// (everything on the pattern path inlines into the kernel; the PodSecurity checks stay out of line)
+#ifndef KYV_FN_MATCH
+#define KYV_FN_MATCH KYV_HD
+#endif
+#ifndef KYV_FN_PATTERN
+#define KYV_FN_PATTERN KYV_HD
+#endif
+#ifndef KYV_FN_PSS
+#define KYV_FN_PSS KYV_BIG
+#endif
 
 // Algorithmic-byte accounting (bench roofline): on the host backend with accounting on,
 // every node-table row a pair reads is marked once; the device build compiles the hook away.
@@ -426,7 +437,7 @@ KYV_HD bool condition_block(const View& v, const Filter& f, const ResView& rv, c
 }
 
 // MatchesResourceDescription (utils.go:185-256) with empty admission info
-KYV_BIG bool match_rule(const View& v, const RuleDesc& rd, const ResView& rv, const LabelSet& nsl, bool* nd) {
+KYV_FN_MATCH bool match_rule(const View& v, const RuleDesc& rd, const ResView& rv, const LabelSet& nsl, bool* nd) {
   bool failed = false;
   const MatchBlock& m = rd.match;
   if (m.mode == MM_ANY) {
@@ -494,8 +505,16 @@ KYV_HD bool ret_is_neg(const Ret& r) { return r.code != EC_NONE ? r.code == EC_N
 struct PatOut {
   uint8_t status;       // ST_PASS / ST_FAIL / ST_SKIP / ST_ERROR / ST_FALLBACK / ST_PANIC / ST_ND
   uint32_t tmpl;
-  uint16_t idx[MAX_IDX];
-  uint32_t key[MAX_SLOTS];
+  uint64_t idx;         // MAX_IDX packed u16 array indices (register-resident, no dynamic indexing)
+  uint32_t key0, key1;  // resolved metadata wildcard keys (MAX_SLOTS == 2)
+};
+static_assert(MAX_IDX == 4 && MAX_SLOTS == 2, "PatOut packing");
+
+// two metadata-key slots held in registers
+struct Keys {
+  uint32_t k0, k1;
+  KYV_HD uint32_t get(uint32_t s) const { return s ? k1 : k0; }
+  KYV_HD void set(uint32_t s, uint32_t val) { if (s) k1 = val; else k0 = val; }
 };
 
 // frame stack accessor: lane-strided (LDS on device, local array on host)
@@ -511,11 +530,11 @@ KYV_HD Ret ok_ret() { Ret r; r.err = false; r.code = EC_NONE; r.mask = 0; r.tmpl
 
 // ExpandInMetadata at one map level (wildcards.go:62-83): resolves wildcard keys into slots; returns a
 // status override (ST_PANIC / ST_ND / ST_FALLBACK) or ST_NONE.
-KYV_HD uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32_t rn, const ResHeader& h, uint32_t* keys) {
+KYV_HD uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32_t rn, const ResHeader& h, Keys& keys) {
   uint32_t meta = map_find(R, rn, KSID(METADATA));
   // slots default to "unresolved" (the pattern key itself, stored in the pool after the glob sid)
-  for (uint32_t i = 0; i < ms.nwild_l; i++) keys[ms.slot_l + i] = v.pool[ms.wild_l + 2 * i + 1];
-  for (uint32_t i = 0; i < ms.nwild_a; i++) keys[ms.slot_a + i] = v.pool[ms.wild_a + 2 * i + 1];
+  for (uint32_t i = 0; i < ms.nwild_l; i++) keys.set(ms.slot_l + i, v.pool[ms.wild_l + 2 * i + 1]);
+  for (uint32_t i = 0; i < ms.nwild_a; i++) keys.set(ms.slot_a + i, v.pool[ms.wild_a + 2 * i + 1]);
   if (meta == NONE || node_type(R[meta]) == N_NULL) return ST_NONE;
   if (node_type(R[meta]) != N_MAP) return ST_PANIC;
   if (h.flags & RF_ANCHORISH) return ST_FALLBACK;
@@ -536,19 +555,18 @@ KYV_HD uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32_
         if (glob_sid(v, gp, k)) { if (hit == NONE) hit = k; n++; }
       }
       if (n > 1) return ST_ND;
-      if (n == 1) keys[slot0 + w] = hit;
+      if (n == 1) keys.set(slot0 + w, hit);
     }
   }
   return ST_NONE;
 }
 
 // MatchPattern (validate.go:31-56) for one compiled pattern; a walk deeper than the stack ends in ST_FALLBACK
-KYV_BIG void eval_pattern(const View& v, uint32_t root, NodeTab R, const ResHeader& h, const RuleDesc& rd, Stack stk,
+KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const ResHeader& h, const RuleDesc& rd, Stack stk,
                          PatOut& out) {
   uint64_t seen = 0, found = 0;
-  uint32_t keys[MAX_SLOTS];
-  for (int s = 0; s < MAX_SLOTS; s++) keys[s] = NONE;
-  for (int s = 0; s < MAX_IDX; s++) out.idx[s] = 0;
+  Keys keys{NONE, NONE};
+  out.idx = 0;
   int sp = 0;
   Ret ret = ok_ret();
   bool fb = false;
@@ -568,7 +586,7 @@ KYV_BIG void eval_pattern(const View& v, uint32_t root, NodeTab R, const ResHead
             uint64_t b = 1ull << E.abit;
             seen |= b;
             if (!(found & b)) {
-              uint32_t key = (E.flags & EF_WILD) ? keys[E.slot] : E.key;
+              uint32_t key = (E.flags & EF_WILD) ? keys.get(E.slot) : E.key;
               if (map_find(R, ern, key) != NONE) found |= b;
             }
           }
@@ -625,7 +643,7 @@ KYV_BIG void eval_pattern(const View& v, uint32_t root, NodeTab R, const ResHead
         if (f.i == P.n) { sp--; ret = ok_ret(); action = 2; continue; }
         const PEntry& E = v.pe[P.first + f.i];
         f.i++;
-        uint32_t key = (E.flags & EF_WILD) ? keys[E.slot] : E.key;
+        uint32_t key = (E.flags & EF_WILD) ? keys.get(E.slot) : E.key;
         uint32_t c = map_find(R, f.rn, key);
         switch (E.handler) {
           case H_NEGATION:
@@ -667,7 +685,11 @@ KYV_BIG void eval_pattern(const View& v, uint32_t root, NodeTab R, const ResHead
           action = 2;
           continue;
         }
-        if (f.kind == F_AOM) { out.idx[P.level] = f.i; epn = P.first; }
+        if (f.kind == F_AOM) {
+          uint32_t sh = 16u * P.level;
+          out.idx = (out.idx & ~(0xFFFFull << sh)) | ((uint64_t)f.i << sh);
+          epn = P.first;
+        }
         else epn = v.pool[P.first + f.i];
         ern = R[f.rn].a + f.i;
         f.i++;
@@ -714,7 +736,8 @@ KYV_BIG void eval_pattern(const View& v, uint32_t root, NodeTab R, const ResHead
     f.i = 0;
     action = 1;
   }
-  for (int s = 0; s < MAX_SLOTS; s++) out.key[s] = keys[s];
+  out.key0 = keys.k0;
+  out.key1 = keys.k1;
   if (!ret.err) { out.status = ST_PASS; out.tmpl = NONE; return; }
   if (ret_is_skip(ret)) { out.status = ST_SKIP; out.tmpl = NONE; return; }
   if (ret_is_neg(ret)) { out.status = ST_FAIL; out.tmpl = ret.tmpl; return; }

@@ -53,7 +53,8 @@ enum FixedSid : uint32_t { SID_EMPTY = 0, SID_ZERO = 1, SID_TRUE = 2, SID_FALSE 
 
 // resource flags
 enum ResFlag : uint32_t {
-  RF_MAGIC = 1u << 0,       // some string/key contains an anchor-error phrase -> pattern pairs fall back
+  RF_MAGIC = 1u << 0,       // some string/key contains an anchor-error phrase, or a map/array exceeds 65535
+                            // entries -> pattern pairs fall back
   RF_ANCHORISH = 1u << 1,   // some key under metadata parses as an anchor -> metadata expansion falls back
   RF_EMPTY = 1u << 2,
   RF_TOO_DEEP = 1u << 3,

@@ -227,7 +227,7 @@ KYV_HD bool has_prefix(const View& v, uint32_t s, uint32_t prefix) {
 }
 
 // evaluatePSS (evaluate.go:16-37): failing (check, version) slots
-KYV_BIG uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
+KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
   Dec d{R, false};
   uint32_t fails = 0;
   uint32_t spec = pv.spec;
@@ -414,7 +414,7 @@ KYV_HD uint32_t pss_id_slots(uint32_t slot) {
 }
 
 // validatePodSecurity (validation.go:535-566) -> status; *fails receives the remaining failing slots
-KYV_BIG uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out) {
+KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out) {
   *fails_out = 0;
   if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
   uint32_t kind = h.kind;
@@ -488,61 +488,80 @@ KYV_BIG uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResH
 namespace kyv {
 
 // One (resource, rule) pair: match (+ empty OldResource retry) then dispatch (validation.go:134-183, :276-317).
-// `recs`/`nrec` receive failing-path records (one per failing pattern / anyPattern alternative).
-KYV_BIG uint8_t eval_pair(const View& v, uint32_t r, uint32_t k, Stack stk, uint32_t* pss_fails, FailRec* recs, uint32_t* nrec,
-                         uint32_t maxrec) {
-  *nrec = 0;
+// Every lane of a wave calls this for the same rule k (`active` false for lanes past the batch end), so the
+// failing-path records can be emitted through `sink` at wave-uniform points: one emit per anyPattern
+// alternative (trip count uniform per rule), with `has` set on the lanes whose alternative failed.
+template <class Sink>
+KYV_HD uint8_t eval_pair(const View& v, bool active, uint32_t r, uint32_t k, Stack stk, uint32_t* pss_fails, Sink& sink) {
   *pss_fails = 0;
   const RuleDesc& rd = v.rules[k];
-  if (rd.match.mode == MM_NONE) return ST_FALLBACK;  // match program could not be compiled
-  const ResHeader& h = v.hdr[r];
-  NodeTab R{v.nodes + h.root};
-  LabelSet nsl{nullptr, 0, nullptr, 0};
-  if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
-  bool nd = false;
-  bool m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
-  if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
-  if (!m) return ST_NONE;
-  if (nd) return ST_ND;
-  switch (rd.kind) {
-    case RK_FALLBACK: return ST_FALLBACK;
-    case RK_PANIC: return ST_PANIC;
-    case RK_ERROR: return ST_ERROR;
-    case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
-    case RK_PATTERN: case RK_ANYPATTERN: {
-      if (h.flags & RF_MAGIC) return ST_FALLBACK;
-      uint32_t nalts = rd.kind == RK_PATTERN ? 1 : rd.nalts;
-      uint32_t nfail = 0, nskip = 0;
-      for (uint32_t a = 0; a < nalts; a++) {
-        uint32_t root = rd.kind == RK_PATTERN ? rd.root : v.pool[rd.root + a];
-        PatOut po;
-        eval_pattern(v, root, R, h, rd, stk, po);
-        switch (po.status) {
-          case ST_PASS: *nrec = 0; return (uint8_t)(ST_PASS | ((a < 30 ? a : 30) << 3));  // alt index for the message
-          case ST_SKIP: nskip++; break;
-          case ST_FAIL: case ST_ERROR: {
-            if (rd.kind == RK_PATTERN && po.status == ST_ERROR) return ST_ERROR;
-            if (*nrec < maxrec) {
-              FailRec& fr = recs[*nrec];
-              fr.res = r; fr.rule = k; fr.tmpl = po.status == ST_FAIL ? po.tmpl : NONE; fr.alt = (uint16_t)a;
-              for (int i = 0; i < MAX_IDX; i++) fr.idx[i] = po.idx[i];
-              for (int i = 0; i < MAX_SLOTS; i++) fr.key[i] = po.key[i];
-              (*nrec)++;
-            }
-            nfail++;
-            break;
-          }
-          default: *nrec = 0; return po.status;  // fallback / panic / nondeterministic at this point of the walk
-        }
+  uint8_t st = ST_NONE;
+  bool walk = false;
+  NodeTab R{nullptr};
+  const ResHeader* hp = nullptr;
+  if (active) {
+    if (rd.match.mode == MM_NONE) {
+      st = ST_FALLBACK;  // match program could not be compiled
+    } else {
+      hp = &v.hdr[r];
+      const ResHeader& h = *hp;
+      R = NodeTab{v.nodes + h.root};
+      LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
+      if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
+      bool nd = false;
+      bool m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
+      if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
+      if (!m) st = ST_NONE;
+      else if (nd) st = ST_ND;
+      else switch (rd.kind) {
+        case RK_FALLBACK: st = ST_FALLBACK; break;
+        case RK_PANIC: st = ST_PANIC; break;
+        case RK_ERROR: st = ST_ERROR; break;
+        case RK_PSS: st = eval_pss(v, v.pss[rd.root], R, h, pss_fails); break;
+        case RK_PATTERN: case RK_ANYPATTERN:
+          if (h.flags & RF_MAGIC) st = ST_FALLBACK;
+          else walk = true;
+          break;
+        default: st = ST_NONE;
       }
-      for (uint32_t i = 0; i < *nrec; i++) recs[i].nalt = (uint16_t)*nrec;
-      if (rd.kind == RK_PATTERN) return nfail ? ST_FAIL : ST_SKIP;
-      if (nfail) return ST_FAIL;
-      if (nskip) return ST_SKIP;
-      return (uint8_t)(ST_PASS | (31 << 3));  // empty anyPattern list: pass with the rule message (validation.go:701)
     }
-    default: return ST_NONE;
   }
+  if (rd.kind != RK_PATTERN && rd.kind != RK_ANYPATTERN) return st;
+  uint32_t nalts = rd.kind == RK_PATTERN ? 1 : rd.nalts;  // uniform across the wave
+  uint32_t nfail = 0, nskip = 0;
+  for (uint32_t a = 0; a < nalts; a++) {
+    PatOut po;
+    po.status = ST_NONE;
+    if (walk) eval_pattern(v, rd.kind == RK_PATTERN ? rd.root : v.pool[rd.root + a], R, *hp, rd, stk, po);
+    bool rec = false;
+    if (walk) {
+      switch (po.status) {
+        case ST_PASS: st = (uint8_t)(ST_PASS | ((a < 30 ? a : 30) << 3)); walk = false; break;  // alt index for the message
+        case ST_SKIP: nskip++; break;
+        case ST_FAIL: case ST_ERROR:
+          if (rd.kind == RK_PATTERN && po.status == ST_ERROR) { st = ST_ERROR; walk = false; break; }
+          rec = true;
+          nfail++;
+          break;
+        default: st = po.status; walk = false;  // fallback / panic / nondeterministic at this point of the walk
+      }
+    }
+    FailRec fr;
+    if (rec) {
+      fr.res = r; fr.rule = k; fr.tmpl = po.status == ST_FAIL ? po.tmpl : NONE; fr.alt = (uint16_t)a; fr.nalt = 0;
+      for (int i = 0; i < MAX_IDX; i++) fr.idx[i] = (uint16_t)(po.idx >> (16 * i));
+      fr.key[0] = po.key0;
+      fr.key[1] = po.key1;
+    }
+    sink.emit(rec, fr);
+  }
+  if (walk) {
+    if (rd.kind == RK_PATTERN) st = nfail ? ST_FAIL : ST_SKIP;
+    else if (nfail) st = ST_FAIL;
+    else if (nskip) st = ST_SKIP;
+    else st = (uint8_t)(ST_PASS | (31 << 3));  // empty anyPattern list: pass with the rule message (validation.go:701)
+  }
+  return st;
 }
 
 }  // namespace kyv

@@ -289,6 +289,33 @@ def corpus_ndjson(n, kind="mixed", seed=SEED, edge=False, workers=None, chunk=20
     if workers <= 1 or len(jobs) == 1:
         parts = [_chunk(j) for j in jobs]
     else:
-        with mp.get_context("fork").Pool(workers) as pool:
+        pool = mp.get_context("fork").Pool(workers)
+        try:
             parts = pool.map(_chunk, jobs)
+        finally:
+            pool.close()  # let the workers exit on their own (no SIGTERM under profilers)
+            pool.join()
     return b"".join(parts), Gen(seed).ns_labels()
+
+
+def cached_corpus(n, kind="mixed", seed=SEED, edge=False, cache_dir=None):
+    """corpus_ndjson with an optional on-disk cache (KYV_CORPUS_CACHE): profiler runs reuse the corpus a
+    plain run generated, so no worker processes are forked under the profiler."""
+    import os
+    cache_dir = cache_dir or os.environ.get("KYV_CORPUS_CACHE")
+    if not cache_dir:
+        return corpus_ndjson(n, kind=kind, seed=seed, edge=edge)
+    base = os.path.join(cache_dir, "corpus_%s_%d_%x_%d" % (kind, n, seed, int(edge)))
+    if os.path.exists(base + ".ndjson") and os.path.exists(base + ".nsl.json"):
+        with open(base + ".ndjson", "rb") as f:
+            data = f.read()
+        with open(base + ".nsl.json") as f:
+            return data, json.load(f)
+    data, nsl = corpus_ndjson(n, kind=kind, seed=seed, edge=edge)
+    os.makedirs(cache_dir, exist_ok=True)
+    with open(base + ".ndjson.tmp", "wb") as f:
+        f.write(data)
+    os.replace(base + ".ndjson.tmp", base + ".ndjson")
+    with open(base + ".nsl.json", "w") as f:
+        json.dump(nsl, f)
+    return data, nsl
