@@ -78,17 +78,18 @@ def all_sum(pg, x):
 
 
 def cpu_baseline(policies, data, nsl, nrules, target_s=10.0):
-    """Oracle (CPU restatement of engine.Validate) on a bounded prefix of this rank's corpus."""
+    """Oracle (CPU restatement of engine.Validate) on a bounded prefix of this rank's corpus: the prefix grows
+    until one timed pass takes >= target_s (or the prefix cap is reached)."""
     from oracle import oracle as O
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
     lines = data.split(b"\n", 400000)[:400000]
-    probe = b"[" + b",".join(lines[:256]) + b"]"
-    n, _, secs = O.validate_batch(policies, probe, nsl, threads)
-    rate = n / max(secs, 1e-9)  # pairs / s
-    want = int(min(len(lines), max(256, target_s * rate / max(nrules, 1))))
-    sample = b"[" + b",".join(lines[:want]) + b"]"
-    if want > 256:
+    want = 512
+    while True:
+        sample = b"[" + b",".join(lines[:want]) + b"]"
         n, _, secs = O.validate_batch(policies, sample, nsl, threads)
+        if secs >= target_s or want >= len(lines):
+            break
+        want = min(len(lines), int(want * min(16.0, max(2.0, 1.2 * target_s / max(secs, 1e-3)))))
     return {"value": n / secs, "unit": "resource×rule evals/sec", "cores": threads, "kind": "port",
             "sample": "%d resources x %d compiled rules (first resources of the rank-0 corpus), %.1f s, oracle/ "
                       "tree-walk restatement of engine.Validate, %d threads" % (want, nrules, secs, threads)}

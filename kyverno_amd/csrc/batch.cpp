@@ -318,6 +318,92 @@ void derive_strings(Batch& b, size_t from, int threads) {
   if (total > 0xFFFFFFFFull) throw std::runtime_error("string heap exceeds 4 GiB per batch");
 }
 
+// Kind gate of one compiled rule: the gvk kinds its match block can accept (MatchesResourceDescription
+// checks kinds first, utils.go:81-85). `any` when some reachable filter has no kinds or "*", when the empty
+// OldResource retry may match, or when the match program fell back.
+struct KindGate {
+  bool any = false;
+  std::vector<uint32_t> kinds;
+};
+
+static KindGate rule_gate(const Ruleset& rs, const RuleDesc& rd) {
+  KindGate g;
+  if (rd.empty_may_match || rd.match.mode == MM_NONE) { g.any = true; return g; }
+  const MatchBlock& m = rd.match;
+  bool any_filter = false;
+  for (uint32_t i = 0; i < m.nfilters; i++) {
+    const Filter& f = rs.filters[m.filters + i];
+    if (m.mode == MM_ANY && (f.flags & FF_ZERO_RD)) continue;  // never matches in match.any
+    if (f.nkinds == 0) {
+      if (m.mode == MM_ANY) { g.any = true; return g; }
+      continue;  // match.all: another filter may still constrain the kind
+    }
+    std::vector<uint32_t> ks;
+    for (uint32_t j = 0; j < f.nkinds; j++) {
+      const KindDesc& k = rs.kinds[f.kinds + j];
+      if (k.kind == NONE) { ks.clear(); break; }
+      ks.push_back(k.kind);
+    }
+    if (ks.empty()) {  // "*"
+      if (m.mode == MM_ANY) { g.any = true; return g; }
+      continue;
+    }
+    if (m.mode == MM_ANY) {
+      g.kinds.insert(g.kinds.end(), ks.begin(), ks.end());
+      any_filter = true;
+    } else if (!any_filter) {  // all/plain: every filter must accept the kind; the first kinds list bounds it
+      g.kinds = ks;
+      any_filter = true;
+    }
+  }
+  if (!any_filter && m.mode != MM_ANY) g.any = true;  // no filter constrains kinds
+  return g;
+}
+
+// Stable sort of the headers by kind class + the per-class rule gate table.
+void order_by_kind(Batch& b) {
+  const Ruleset& rs = *b.rs;
+  size_t n = b.hdr.size(), nr = rs.rules.size();
+  std::unordered_map<uint32_t, uint32_t> cls;  // gvk_kind sid -> class
+  std::vector<uint32_t> cls_kind;
+  std::vector<uint32_t> cls_count;
+  for (auto& h : b.hdr) {
+    auto it = cls.find(h.gvk_kind);
+    if (it == cls.end()) {
+      it = cls.emplace(h.gvk_kind, (uint32_t)cls_kind.size()).first;
+      cls_kind.push_back(h.gvk_kind);
+      cls_count.push_back(0);
+    }
+    h.kclass = it->second;
+    cls_count[it->second]++;
+  }
+  b.nclass = (uint32_t)cls_kind.size();
+  b.gate_words = (uint32_t)((nr + 31) / 32);
+  b.gate.assign((size_t)std::max<uint32_t>(b.nclass, 1) * std::max<uint32_t>(b.gate_words, 1), 0);
+  for (size_t k = 0; k < nr; k++) {
+    KindGate g = rule_gate(rs, rs.rules[k]);
+    for (uint32_t c = 0; c < b.nclass; c++) {
+      bool on = g.any || std::find(g.kinds.begin(), g.kinds.end(), cls_kind[c]) != g.kinds.end();
+      if (on) b.gate[(size_t)c * b.gate_words + k / 32] |= 1u << (k % 32);
+    }
+  }
+  // counting sort by class (stable)
+  std::vector<uint32_t> start(b.nclass + 1, 0);
+  for (uint32_t c = 0; c < b.nclass; c++) start[c + 1] = start[c] + cls_count[c];
+  std::vector<ResHeader> sorted(n);
+  b.order.resize(n);
+  b.inv.resize(n);
+  for (size_t i = 0; i < n; i++) {
+    ResHeader h = b.hdr[i];
+    uint32_t pos = start[h.kclass]++;
+    h.orig = (uint32_t)i;
+    sorted[pos] = h;
+    b.order[pos] = (uint32_t)i;
+    b.inv[i] = pos;
+  }
+  b.hdr.swap(sorted);
+}
+
 Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* nsl_json, size_t nsl_len, int threads,
                    std::string* err) {
   auto b = std::make_unique<Batch>();
@@ -446,6 +532,7 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
       if (h.ann != NONE) h.ann = find(KSID(ANNOTATIONS));
     }
     derive_strings(*b, 0, T);
+    order_by_kind(*b);
     (void)seed;
     return b.release();
   } catch (std::exception& e) {

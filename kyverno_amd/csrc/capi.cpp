@@ -19,7 +19,8 @@ using namespace kyv;
 struct kyv_ruleset { Ruleset* rs; };
 struct kyv_batch { Batch* b; };
 struct kyv_results {
-  Results r;
+  Results r;                  // verdicts in the batch's kind-major order
+  std::vector<uint32_t> inv;  // input index -> kind-major position (copied from the batch)
   std::multimap<uint64_t, uint32_t> recidx;  // (rule<<32|res) -> record
   bool indexed = false;
   std::mutex mu;
@@ -137,6 +138,7 @@ int kyv_eval(const kyv_ruleset* rs, const kyv_batch* b, const kyv_eval_opts* opt
       double ms = 0;
       eval_gpu(*rs->rs, *b->b, dev, iters, &res->r, &ms, copy);
     }
+    res->inv = b->b->inv;
     *out = res;
     return KYV_OK;
   } catch (std::exception& e) {
@@ -149,7 +151,12 @@ void kyv_results_free(kyv_results* r) { delete r; }
 int kyv_results_status(const kyv_results* r, uint8_t* out, size_t cap) {
   if (!r || !out) return fail(KYV_EINVAL, "null argument");
   if (cap < r->r.status.size()) return fail(KYV_ERANGE, "buffer too small (or verdicts kept on device)");
-  memcpy(out, r->r.status.data(), r->r.status.size());
+  size_t nres = r->r.nres;
+  for (size_t k = 0; k < r->r.nrules; k++) {  // kind-major -> input order
+    const uint8_t* src = r->r.status.data() + k * nres;
+    uint8_t* dst = out + k * nres;
+    for (size_t i = 0; i < nres; i++) dst[i] = src[r->inv[i]];
+  }
   return KYV_OK;
 }
 
@@ -186,6 +193,7 @@ int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const
                             char* buf, size_t cap) {
   auto* r = const_cast<kyv_results*>(cr);
   if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
+  res = r->inv[res];
   const Ruleset& rs = *crs->rs;
   const Batch& b = *cb->b;
   uint8_t sb = r->r.status[(size_t)rule * r->r.nres + res];
@@ -235,6 +243,7 @@ int64_t kyv_results_path(const kyv_results* cr, const kyv_ruleset* crs, const ky
                          char* buf, size_t cap) {
   auto* r = const_cast<kyv_results*>(cr);
   if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
+  res = r->inv[res];
   // records exist for every failing alternative walked, also when a later anyPattern alternative passed
   if ((r->r.status[(size_t)rule * r->r.nres + res] & 7) != ST_FAIL || crs->rs->rules[rule].kind != RK_PATTERN)
     return put("", buf, cap);
@@ -247,6 +256,7 @@ int64_t kyv_results_path(const kyv_results* cr, const kyv_ruleset* crs, const ky
 
 uint32_t kyv_results_pss_mask(const kyv_results* r, const kyv_ruleset* rs, uint32_t res, uint32_t rule) {
   if (!r || !rs || rule >= r->r.nrules || res >= r->r.nres) return 0;
+  res = r->inv[res];
   uint32_t slot = 0;
   for (uint32_t k = 0; k < rule; k++) if (rs->rs->rules[k].kind == RK_PSS) slot++;
   if (rs->rs->rules[rule].kind != RK_PSS) return 0;

@@ -73,7 +73,7 @@ struct DevBatch {
   DeviceResults* out = nullptr;  // result buffers + stream, resident across evaluations
   uint8_t* base = nullptr;
   size_t bytes = 0;
-  size_t o_nodes, o_hdr, o_faux, o_soff, o_slen, o_sflags, o_sdur, o_sqty, o_sf64, o_heap, o_nsloff, o_nslkv;
+  size_t o_nodes, o_hdr, o_faux, o_soff, o_slen, o_sflags, o_sdur, o_sqty, o_sf64, o_heap, o_nsloff, o_nslkv, o_gate;
   double upload_ms = 0;
 };
 
@@ -118,6 +118,7 @@ static DevBatch* upload_batch(const Batch& b, int device) {
   d->o_heap = p.add(b.heap);
   d->o_nsloff = p.add(b.nsl_off);
   d->o_nslkv = p.add(b.nsl_kv);
+  d->o_gate = p.add(b.gate);
   d->bytes = p.host.size();
   HIP_OK(hipMalloc(&d->base, d->bytes));
   HIP_OK(hipMemcpy(d->base, p.host.data(), d->bytes, hipMemcpyHostToDevice));
@@ -141,12 +142,15 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
     v.heap = bbase + db->o_heap;
     v.nsl_off = (const uint32_t*)(bbase + db->o_nsloff);
     v.nsl_kv = (const uint32_t*)(bbase + db->o_nslkv);
+    v.gate = (const uint32_t*)(bbase + db->o_gate);
   } else {
     v.nodes = b.nodes.data(); v.hdr = b.hdr.data(); v.faux = b.faux.data();
     v.str_off = b.str_off.data(); v.str_len = b.str_len.data(); v.str_flags = b.str_flags.data();
     v.str_dur = b.str_dur.data(); v.str_qty = b.str_qty.data(); v.str_f64 = b.str_f64.data();
     v.heap = b.heap.data(); v.nsl_off = b.nsl_off.data(); v.nsl_kv = b.nsl_kv.data();
+    v.gate = b.gate.data();
   }
+  v.gate_words = b.gate_words;
   v.nres = (uint32_t)b.hdr.size();
   v.nrules = (uint32_t)rs.rules.size();
   if (dr) {
@@ -216,9 +220,12 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
   const bool active = r < v.nres;
   Stack stk{lds_frames + lane, BLOCK, depth};
   WaveSink sink{o.recs, o.nrecs, o.max_recs};
+  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
   for (uint32_t k = o.rule_lo; k < o.rule_hi; k++) {
     uint32_t pf = 0;
-    uint8_t st = eval_pair(v, active, r, k, stk, &pf, sink);
+    // kind gate: rules that cannot match this resource's kind are ST_NONE without running the match program
+    bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+    uint8_t st = eval_pair(v, gated, r, k, stk, &pf, sink);
     if (active) {
       o.status[(size_t)k * v.nres + r] = st;
       uint32_t ps = o.pss_slot[k];
@@ -407,7 +414,8 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
             acct = TouchAcct{seen.data(), nn, 0};
             g_touch = &acct;
           }
-          uint8_t st = eval_pair(v, true, (uint32_t)r, (uint32_t)k, stk, &pf, sink);
+          const uint32_t* gate = v.gate + (size_t)v.hdr[r].kclass * v.gate_words;
+          uint8_t st = eval_pair(v, ((gate[k >> 5] >> (k & 31)) & 1u) != 0, (uint32_t)r, (uint32_t)k, stk, &pf, sink);
           if (account) {
             g_touch = nullptr;
             bytes[t] += 16 + 16 * acct.rows + 1 + (pss_slot[k] != NONE ? 4 : 0) + (uint64_t)sink.emitted * sizeof(FailRec);

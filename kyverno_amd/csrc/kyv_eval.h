@@ -69,6 +69,8 @@ struct View {
   const uint8_t* heap;
   const uint32_t* nsl_off;  // namespace label sets: pairs (key sid, value sid)
   const uint32_t* nsl_kv;
+  const uint32_t* gate;     // [kind class][gate_words] rule bits (batch.cpp order_by_kind)
+  uint32_t gate_words;
   // ruleset
   const RuleDesc* rules;
   uint32_t nrules;

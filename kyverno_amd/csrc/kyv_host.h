@@ -83,6 +83,12 @@ struct Batch {
   std::vector<uint8_t> heap;
   std::vector<uint32_t> nsl_off, nsl_kv;
   std::vector<std::string> nsl_names;  // namespace name per set id
+  // kind-major order: headers are sorted by kind class so that a wave's lanes share kind (and so mostly share
+  // the rules that can match them); verdicts are produced in this order and un-permuted at the C ABI
+  std::vector<uint32_t> order;    // sorted position -> input index
+  std::vector<uint32_t> inv;      // input index -> sorted position
+  std::vector<uint32_t> gate;     // [kclass][gate_words] bit k: rule k can match a resource of this class
+  uint32_t gate_words = 0, nclass = 0;
   std::vector<void*> dev;
   ~Batch();
 };

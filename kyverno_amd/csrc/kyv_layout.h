@@ -72,7 +72,8 @@ struct ResHeader {          // 64 bytes, one per resource (unstructured accessor
   uint32_t ann;             // same for annotations
   uint32_t nsl;             // namespace-label set id, NONE if unknown
   uint32_t flags;
-  uint32_t pad0, pad1;
+  uint32_t orig;            // index of the resource in the caller's input order
+  uint32_t kclass;          // kind class (row of the batch's rule gate table)
 };
 static_assert(sizeof(ResHeader) == 64, "header size");
 
