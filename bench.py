@@ -95,6 +95,22 @@ def cpu_baseline(policies, data, nsl, nrules, target_s=10.0):
                       "tree-walk restatement of engine.Validate, %d threads" % (want, nrules, secs, threads)}
 
 
+def pmc_traffic(config):
+    """HBM-side bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/pmc_latest.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc passes of this
+    same command), used only when it was measured on the same workload configuration; else None."""
+    f = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(f):
+        return None, None
+    with open(f) as fh:
+        s = json.load(fh)
+    bc = s.get("bench_config") or {}
+    keys = ("workload", "resources_per_gpu", "compiled_rules")
+    if any(bc.get(k) != config.get(k) for k in keys):
+        return None, s.get("tag")
+    return s.get("traffic_bytes"), s.get("tag")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,6 +179,13 @@ def main():
     if rank == 0:
         alg_bytes_launch = bytes_per_eval * pairs
         achieved = alg_bytes_launch / (kernel_ms / 1e3) / 1e9
+        config = {"workload": "C3: charts/kyverno-policies restricted + test/best_practices (%d compiled rules) "
+                              "over %d mixed resources per GPU" % (nrules, batch.n) if args.workload == "c3" else
+                              "C2: podSecurity restricted/latest (%d compiled rules) over %d pods per GPU" %
+                              (nrules, batch.n),
+                  "resources_per_gpu": batch.n, "compiled_rules": nrules, "pairs_per_step": int(total_pairs),
+                  "parallelism": "shard%d" % world}
+        traffic, pmc_tag = pmc_traffic(config)
         line = {
             "metric": METRIC,
             "value": total_pairs * args.steps / dt_max,
@@ -176,14 +199,11 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (seeded generator kyverno_amd/synth.py, SURVEY §8(d) model; seed 0x4b59564e + rank)",
-            "config": {"workload": "C3: charts/kyverno-policies restricted + test/best_practices (%d compiled rules) "
-                                   "over %d mixed resources per GPU" % (nrules, batch.n) if args.workload == "c3" else
-                                   "C2: podSecurity restricted/latest (%d compiled rules) over %d pods per GPU" %
-                                   (nrules, batch.n),
-                       "resources_per_gpu": batch.n, "compiled_rules": nrules, "pairs_per_step": int(total_pairs),
-                       "parallelism": "shard%d" % world},
+            "config": config,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": "profiles/%s_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, bytes "
+                                           "per launch)" % pmc_tag if traffic else None,
                          "bytes_per_eval": bytes_per_eval, "kernel": "eval_kernel", "kernel_ms": kernel_ms,
                          "kernel_ms_max_rank": kernel_ms_max},
             "cpu_baseline": cpu,
