@@ -17,6 +17,7 @@
 
 #include "kyv_host.h"
 #include "kyv_pss.h"
+#include "kyv_wave.h"
 
 namespace kyv {
 
@@ -213,19 +214,19 @@ struct WaveSink {
 // One lane per resource, the rule loop uniform across the wave. `vp` points at a device-resident View so
 // that its fields are read with scalar loads instead of being copied into per-lane private memory.
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) eval_kernel(const View* __restrict__ vp, DevOut o, int depth) {
-  extern __shared__ Frame lds_frames[];  // [depth][BLOCK]
+  extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
   const uint32_t r = blockIdx.x * BLOCK + lane;
   const bool active = r < v.nres;
-  Stack stk{lds_frames + lane, BLOCK, depth};
+  WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth};
   WaveSink sink{o.recs, o.nrecs, o.max_recs};
   const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
   for (uint32_t k = o.rule_lo; k < o.rule_hi; k++) {
     uint32_t pf = 0;
     // kind gate: rules that cannot match this resource's kind are ST_NONE without running the match program
     bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
-    uint8_t st = eval_pair(v, gated, r, k, stk, &pf, sink);
+    uint8_t st = eval_pair(v, gated, r, k, wk, &pf, sink);
     if (active) {
       o.status[(size_t)k * v.nres + r] = st;
       uint32_t ps = o.pss_slot[k];
@@ -328,7 +329,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   hipStream_t stream = d.stream;
   DevOut o{d.status, d.pss_fails, d.pss_slot, d.recs, d.nrecs, d.max_recs, d.counts, 0, (uint32_t)nrules};
   int depth = ruleset_depth(rs);
-  size_t lds = (size_t)depth * BLOCK * sizeof(Frame);
+  size_t lds = (size_t)depth * (sizeof(UFrame) + BLOCK * sizeof(LaneFrame));
   dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
   double total_ms = 0;
   int n = std::max(1, iters);
@@ -400,7 +401,7 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
   for (int t = 0; t < T; t++)
     th.emplace_back([&, t]() {
       Frame frames[MAX_DEPTH];
-      Stack stk{frames, 1, MAX_DEPTH};
+      HostWalker wk{Stack{frames, 1, MAX_DEPTH}};
       HostSink sink{&recs[t], 0};
       std::vector<uint8_t> seen;
       TouchAcct acct{nullptr, 0, 0};
@@ -415,7 +416,7 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
             g_touch = &acct;
           }
           const uint32_t* gate = v.gate + (size_t)v.hdr[r].kclass * v.gate_words;
-          uint8_t st = eval_pair(v, ((gate[k >> 5] >> (k & 31)) & 1u) != 0, (uint32_t)r, (uint32_t)k, stk, &pf, sink);
+          uint8_t st = eval_pair(v, ((gate[k >> 5] >> (k & 31)) & 1u) != 0, (uint32_t)r, (uint32_t)k, wk, &pf, sink);
           if (account) {
             g_touch = nullptr;
             bytes[t] += 16 + 16 * acct.rows + 1 + (pss_slot[k] != NONE ? 4 : 0) + (uint64_t)sink.emitted * sizeof(FailRec);

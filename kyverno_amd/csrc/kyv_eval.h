@@ -114,7 +114,7 @@ KYV_HD int utf8_decode(const uint8_t* s, uint32_t n, uint32_t i, uint32_t* r) { 
 
 // go-wildcard v1.0.3 glob over runes ('*' any run, '?' one rune); iterative star-backtracking decides
 // the same language as the library's recursion.
-KYV_HD bool glob_runes(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_t sl) {
+KYV_BIG bool glob_runes(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_t sl) {
   uint32_t pi = 0, si = 0, star = NONE, mark = 0;
   while (si < sl) {
     uint32_t pr = 0, sr;
@@ -327,7 +327,7 @@ KYV_HD uint32_t ls_find(const LabelSet& s, uint32_t key) {
 }
 
 // CheckSelector incl. ReplaceInSelector (pkg/utils/match/labels.go:10-24, wildcards.go:13-50): 1 match, 0 no, -1 error
-KYV_HD int check_selector(const View& v, const SelDesc& sd, const LabelSet& ls, bool* nd) {
+KYV_BIG int check_selector(const View& v, const SelDesc& sd, const LabelSet& ls, bool* nd) {
   if (sd.invalid) return -1;
   int res = 1;
   for (uint32_t q = 0; q < sd.nreqs; q++) {
@@ -532,7 +532,7 @@ KYV_HD Ret ok_ret() { Ret r; r.err = false; r.code = EC_NONE; r.mask = 0; r.tmpl
 
 // ExpandInMetadata at one map level (wildcards.go:62-83): resolves wildcard keys into slots; returns a
 // status override (ST_PANIC / ST_ND / ST_FALLBACK) or ST_NONE.
-KYV_HD uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32_t rn, const ResHeader& h, Keys& keys) {
+KYV_BIG uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32_t rn, const ResHeader& h, Keys& keys) {
   uint32_t meta = map_find(R, rn, KSID(METADATA));
   // slots default to "unresolved" (the pattern key itself, stored in the pool after the glob sid)
   for (uint32_t i = 0; i < ms.nwild_l; i++) keys.set(ms.slot_l + i, v.pool[ms.wild_l + 2 * i + 1]);

@@ -491,8 +491,21 @@ namespace kyv {
 // Every lane of a wave calls this for the same rule k (`active` false for lanes past the batch end), so the
 // failing-path records can be emitted through `sink` at wave-uniform points: one emit per anyPattern
 // alternative (trip count uniform per rule), with `has` set on the lanes whose alternative failed.
-template <class Sink>
-KYV_HD uint8_t eval_pair(const View& v, bool active, uint32_t r, uint32_t k, Stack stk, uint32_t* pss_fails, Sink& sink) {
+//
+// `Walker::run(v, root, walk, R, hp, rd, out)` runs one compiled pattern for the lanes with `walk` set: the host
+// instantiation is the per-lane eval_pattern (HostWalker below), the kernel's is the wave-uniform walker
+// (kyv_wave.h). It is called by every lane at the same point (the alternative loop is wave-uniform).
+struct HostWalker {
+  Stack stk;
+  KYV_HD void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp, const RuleDesc& rd,
+                  PatOut& out) {
+    out.status = ST_NONE;
+    if (walk) eval_pattern(v, root, NodeTab{R}, *hp, rd, stk, out);
+  }
+};
+
+template <class Sink, class Walker>
+KYV_HD uint8_t eval_pair(const View& v, bool active, uint32_t r, uint32_t k, Walker& wk, uint32_t* pss_fails, Sink& sink) {
   *pss_fails = 0;
   const RuleDesc& rd = v.rules[k];
   uint8_t st = ST_NONE;
@@ -531,8 +544,7 @@ KYV_HD uint8_t eval_pair(const View& v, bool active, uint32_t r, uint32_t k, Sta
   uint32_t nfail = 0, nskip = 0;
   for (uint32_t a = 0; a < nalts; a++) {
     PatOut po;
-    po.status = ST_NONE;
-    if (walk) eval_pattern(v, rd.kind == RK_PATTERN ? rd.root : v.pool[rd.root + a], R, *hp, rd, stk, po);
+    wk.run(v, rd.kind == RK_PATTERN ? rd.root : v.pool[rd.root + a], walk, R.p, hp, rd, po);
     bool rec = false;
     if (walk) {
       switch (po.status) {
