@@ -66,7 +66,10 @@ enum { KYV_RULE_PATTERN = 1, KYV_RULE_ANYPATTERN = 2, KYV_RULE_PSS = 3, KYV_RULE
        KYV_RULE_ERROR = 6 };
 
 enum { KYV_BACKEND_GPU = 0, KYV_BACKEND_CPU = 1 };
-enum { KYV_EVAL_NO_COPYBACK = 1u, KYV_EVAL_ACCOUNT_BYTES = 2u };
+enum { KYV_EVAL_NO_COPYBACK = 1u, KYV_EVAL_ACCOUNT_BYTES = 2u,
+       /* GPU backend: pattern walks run in a kernel generated and compiled (hipRTC, gfx950) for this ruleset
+          on first use; default = on for batches of >= 65536 resources, else the interpreted walk kernel */
+       KYV_EVAL_JIT_OFF = 4u, KYV_EVAL_JIT_ON = 8u };
 
 typedef struct {
   uint32_t abi_version;
@@ -115,6 +118,11 @@ uint32_t kyv_ruleset_num_rules(const kyv_ruleset* rs);
 uint32_t kyv_ruleset_num_policies(const kyv_ruleset* rs);
 int kyv_ruleset_rule_info(const kyv_ruleset* rs, uint32_t rule, kyv_rule_info* out);
 int kyv_ruleset_policy_info(const kyv_ruleset* rs, uint32_t policy, kyv_policy_info* out);
+/* runtime-compiled walk kernel of a ruleset (diagnostics; kyv_eval compiles it on first use by itself):
+   the generated HIP source (returns its full length; rules it covers in *nrules_jit) and a hipRTC compile for
+   gfx950 that needs no GPU (seconds, code-object bytes) */
+int64_t kyv_ruleset_jit_source(const kyv_ruleset* rs, char* buf, size_t cap, uint32_t* nrules_jit);
+int kyv_ruleset_jit_compile(const kyv_ruleset* rs, double* seconds, size_t* code_bytes);
 
 /* ---- batch: resources (JSON array or NDJSON) + namespace labels ({"ns": {"k": "v"}}) ---- */
 int kyv_batch_build(const kyv_ruleset* rs, const char* resources_json, size_t len, const char* ns_labels_json,
@@ -131,6 +139,8 @@ void kyv_results_free(kyv_results* r);
 int kyv_results_status(const kyv_results* r, uint8_t* out, size_t cap);
 int64_t kyv_results_count(const kyv_results* r, int status);
 double kyv_results_kernel_ms(const kyv_results* r);
+/* 1 when the runtime-compiled walk kernel evaluated this result's pattern rules, 0 for the interpreter */
+int kyv_results_jit(const kyv_results* r);
 /* CPU backend with KYV_EVAL_ACCOUNT_BYTES: algorithmic bytes of all pairs (header fields, distinct node rows,
  * verdict, PSS mask, failure records); 0 otherwise */
 uint64_t kyv_results_alg_bytes(const kyv_results* r);

@@ -3,12 +3,15 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkyvgpu.so")
+# KYV_LIB overrides the library path (kernel-variant experiments built by scripts/build_variants.py only)
+LIB_PATH = os.environ.get("KYV_LIB") or os.path.join(HERE, "libkyvgpu.so")
 
 KYV_ABI_VERSION = 1
 BACKEND_GPU, BACKEND_CPU = 0, 1
 EVAL_NO_COPYBACK = 1
 EVAL_ACCOUNT_BYTES = 2
+EVAL_JIT_OFF = 4
+EVAL_JIT_ON = 8
 
 ST_NONE, ST_PASS, ST_FAIL, ST_SKIP, ST_ERROR, ST_FALLBACK, ST_PANIC, ST_ND = range(8)
 STATUS_NAMES = ["none", "pass", "fail", "skip", "error", "fallback", "panic", "nondeterministic"]
@@ -90,6 +93,11 @@ def lib():
     L.kyv_results_path.restype = i64
     L.kyv_results_pss_mask.argtypes = [vp, vp, u32, u32]
     L.kyv_results_pss_mask.restype = u32
+    L.kyv_results_jit.argtypes = [vp]
+    L.kyv_results_jit.restype = i32
+    L.kyv_ruleset_jit_source.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
+    L.kyv_ruleset_jit_source.restype = i64
+    L.kyv_ruleset_jit_compile.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
     L.kyv_last_error.restype = ctypes.c_char_p
     L.kyv_version.restype = ctypes.c_char_p
     _lib = L

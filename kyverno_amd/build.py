@@ -15,9 +15,9 @@ LIB = os.path.join(HERE, "libkyvgpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KYV_OFFLOAD_ARCH", "gfx950")
 
-HOST_SRCS = ["pjson.cpp", "compiler.cpp", "batch.cpp", "capi.cpp"]
+HOST_SRCS = ["pjson.cpp", "compiler.cpp", "batch.cpp", "capi.cpp", "jit.cpp"]
 HIP_SRCS = ["kyv_engine.hip"]
-HEADERS = ["kyv_layout.h", "kyv_eval.h", "kyv_pss.h", "kyv_host.h", "pjson.h", "kyv_wave.h"]
+HEADERS = ["kyv_layout.h", "kyv_eval.h", "kyv_pss.h", "kyv_host.h", "pjson.h", "kyv_wave.h", "kyv_walk.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-value", "-Wno-unused-function", "-Wno-unused-variable",
           "-Wno-unused-but-set-variable", "-I" + os.path.join(ROOT, "include")]
 
@@ -30,12 +30,12 @@ def _needs(obj, src):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def _compile(src):
+def _compile(src, obj_dir=OBJ, defines=()):
     path = os.path.join(CSRC, src)
-    obj = os.path.join(OBJ, src + ".o")
+    obj = os.path.join(obj_dir, src + ".o")
     if not _needs(obj, path):
         return obj
-    cmd = [HIPCC] + COMMON
+    cmd = [HIPCC] + COMMON + ["-D" + d for d in defines]
     if src.endswith(".hip"):
         cmd += ["--offload-arch=" + ARCH, "-x", "hip"]
     cmd += ["-c", path, "-o", obj]
@@ -45,19 +45,20 @@ def _compile(src):
     return obj
 
 
-def build(verbose=False):
-    os.makedirs(OBJ, exist_ok=True)
+def build(verbose=False, lib=LIB, defines=(), obj_dir=OBJ):
+    """Build the library; `defines`/`lib`/`obj_dir` are for kernel-variant experiments (scripts/build_variants.py)."""
+    os.makedirs(obj_dir, exist_ok=True)
     srcs = HOST_SRCS + HIP_SRCS
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
-    if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
+        objs = list(ex.map(lambda s: _compile(s, obj_dir, defines), srcs))
+    if not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread", "-L/opt/rocm/lib", "-lhiprtc", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stderr[-4000:]))
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", lib)
+    return lib
 
 
 if __name__ == "__main__":

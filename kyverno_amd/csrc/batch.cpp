@@ -103,6 +103,7 @@ struct Emitter {
       case T::Arr: {
         n.tk = N_ARR;
         n.b = (uint32_t)v.a.size();
+        n.c = NONE;  // path-column row of element 0, set by resolve_path_columns
         if (v.a.size() > 0xFFFF) magicflag = true;  // walk frames count elements in 16 bits
         out[idx] = n;
         uint32_t first = (uint32_t)out.size();
@@ -533,12 +534,108 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
     }
     derive_strings(*b, 0, T);
     order_by_kind(*b);
+    resolve_path_columns(*b, T);
     (void)seed;
     return b.release();
   } catch (std::exception& e) {
     if (err) *err = e.what();
     return nullptr;
   }
+}
+
+// Path columns (kyv_layout.h): for every resource (in kind-major order, so row space 0 rows are the kernel's
+// resource positions) follow the ruleset's path trie through the node table, recording each static lookup's
+// result; arrays at "[*]" trie positions get batch-wide element rows. Two passes: count element rows per
+// row space per chunk, then fill from the chunk's exclusive prefix.
+namespace {
+struct Resolver {
+  const Ruleset& rs;
+  Node* R;
+  uint32_t* colv;            // nullptr in the counting pass
+  const uint32_t* col_off;
+  uint32_t* next;            // next free row per row space
+  static uint32_t find(const Node* R, const Node& m, uint32_t key) {
+    uint32_t lo = m.a, hi = m.a + m.b;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) >> 1, k = node_key(R[mid]);
+      if (k == key) return mid;
+      if (k < key) lo = mid + 1; else hi = mid;
+    }
+    return NONE;
+  }
+  void go(uint32_t m, uint32_t t, uint32_t row) {
+    const Ruleset::TrieNode& T = rs.trie[t];
+    const Node mn = R[m];
+    if (node_type(mn) == N_MAP) {
+      for (auto& kv : T.kids) {
+        uint32_t x = find(R, mn, kv.first);
+        if (x == NONE) continue;  // columns are NONE-initialised
+        if (colv) colv[(size_t)col_off[rs.trie[kv.second].col] + row] = (node_type(R[x]) << COL_TYPE_SHIFT) | x;
+        go(x, kv.second, row);
+      }
+    } else if (node_type(mn) == N_ARR && T.star != NONE) {
+      uint32_t space = rs.trie[T.star].rowspace;
+      uint32_t base = next[space];
+      next[space] += mn.b;
+      if (colv) R[m].c = base;
+      for (uint32_t i = 0; i < mn.b; i++) go(mn.a + i, T.star, base + i);
+    }
+  }
+};
+}  // namespace
+
+void resolve_path_columns(Batch& b, int threads) {
+  const Ruleset& rs = *b.rs;
+  size_t n = b.hdr.size();
+  uint32_t nsp = rs.nrowspaces;
+  b.rs_rows.assign(nsp, 0);
+  b.col_off.assign(rs.ncols, 0);
+  b.colv.clear();
+  if (rs.ncols == 0 || n == 0) return;
+  int T = std::max(1, threads);
+  size_t nch = std::min(n, (size_t)T * 8);
+  std::vector<std::vector<uint32_t>> cnt(nch, std::vector<uint32_t>(nsp, 0));
+  auto eligible = [&](const ResHeader& h) { return h.nnodes < (1u << COL_TYPE_SHIFT); };
+  auto run = [&](bool fill, std::vector<std::vector<uint32_t>>& nexts) {
+    std::atomic<size_t> nx{0};
+    auto work = [&]() {
+      for (;;) {
+        size_t c = nx.fetch_add(1);
+        if (c >= nch) break;
+        size_t r0 = n * c / nch, r1 = n * (c + 1) / nch;
+        for (size_t r = r0; r < r1; r++) {
+          ResHeader& h = b.hdr[r];
+          if (!eligible(h)) continue;
+          Resolver rv{rs, b.nodes.data() + h.root, fill ? b.colv.data() : nullptr, b.col_off.data(), nexts[c].data()};
+          rv.go(0, 0, (uint32_t)r);
+        }
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back(work);
+    for (auto& t : th) t.join();
+  };
+  run(false, cnt);
+  std::vector<std::vector<uint32_t>> base(nch, std::vector<uint32_t>(nsp, 0));
+  std::vector<uint64_t> tot(nsp, 0);
+  for (size_t c = 0; c < nch; c++)
+    for (uint32_t s = 1; s < nsp; s++) {
+      if (tot[s] + cnt[c][s] > 0xFFFFFFF0ull) throw std::runtime_error("path-column row space exceeds 2^32 rows; split the batch");
+      base[c][s] = (uint32_t)tot[s];
+      tot[s] += cnt[c][s];
+    }
+  b.rs_rows[0] = (uint32_t)n;
+  for (uint32_t s = 1; s < nsp; s++) b.rs_rows[s] = (uint32_t)tot[s];
+  uint64_t total = 0;
+  for (uint32_t c = 0; c < rs.ncols; c++) {
+    b.col_off[c] = (uint32_t)total;
+    total += b.rs_rows[rs.col_rowspace[c]];
+    if (total > 0xFFFFFFF0ull) throw std::runtime_error("path columns exceed 2^32 entries; split the batch");
+  }
+  b.colv.assign(total + 1, NONE);
+  run(true, base);
+  // resources too large for column encoding: pattern pairs fall back (RF_MAGIC), so no column is read
+  for (auto& h : b.hdr) if (!eligible(h)) h.flags |= RF_MAGIC;
 }
 
 std::string format_path(const Ruleset& rs, const Batch& b, uint32_t tmpl, const uint16_t* idx, const uint32_t* key) {

@@ -9,7 +9,8 @@
 #include "kyv_host.h"
 
 namespace kyv {
-void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back);
+void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back,
+              int jit_mode);
 void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool account);
 void free_device_images(Ruleset& rs, Batch* b);
 }  // namespace kyv
@@ -74,6 +75,32 @@ int kyv_ruleset_rule_info(const kyv_ruleset* rs, uint32_t k, kyv_rule_info* out)
   return KYV_OK;
 }
 
+int64_t kyv_ruleset_jit_source(const kyv_ruleset* rs, char* buf, size_t cap, uint32_t* nrules_jit) {
+  if (!rs) return fail(KYV_EINVAL, "null argument"), -1;
+  try {
+    std::vector<uint8_t> jr;
+    std::string src = jit_source(*rs->rs, &jr);
+    if (nrules_jit) { *nrules_jit = 0; for (auto x : jr) *nrules_jit += x; }
+    if (buf && cap) { size_t n = std::min(cap - 1, src.size()); memcpy(buf, src.data(), n); buf[n] = 0; }
+    return (int64_t)src.size();
+  } catch (std::exception& e) {
+    fail(KYV_EINTERNAL, e.what());
+    return -1;
+  }
+}
+
+int kyv_ruleset_jit_compile(const kyv_ruleset* rs, double* seconds, size_t* code_bytes) {
+  if (!rs) return fail(KYV_EINVAL, "null argument");
+  try {
+    std::vector<uint8_t> jr;
+    std::vector<char> code = jit_compile(jit_source(*rs->rs, &jr), seconds);
+    if (code_bytes) *code_bytes = code.size();
+    return KYV_OK;
+  } catch (std::exception& e) {
+    return fail(KYV_EINTERNAL, e.what());
+  }
+}
+
 int kyv_ruleset_policy_info(const kyv_ruleset* rs, uint32_t p, kyv_policy_info* out) {
   if (!rs || !out || p >= rs->rs->policies.size()) return fail(KYV_ERANGE, "policy index out of range");
   const PolicyMeta& m = rs->rs->policies[p];
@@ -136,7 +163,8 @@ int kyv_eval(const kyv_ruleset* rs, const kyv_batch* b, const kyv_eval_opts* opt
       int iters = opts && opts->iterations > 0 ? opts->iterations : 1;
       bool copy = !(opts && (opts->flags & KYV_EVAL_NO_COPYBACK));
       double ms = 0;
-      eval_gpu(*rs->rs, *b->b, dev, iters, &res->r, &ms, copy);
+      int jm = !opts ? JIT_AUTO : (opts->flags & KYV_EVAL_JIT_OFF) ? JIT_OFF : (opts->flags & KYV_EVAL_JIT_ON) ? JIT_ON : JIT_AUTO;
+      eval_gpu(*rs->rs, *b->b, dev, iters, &res->r, &ms, copy, jm);
     }
     res->inv = b->b->inv;
     *out = res;
@@ -147,6 +175,8 @@ int kyv_eval(const kyv_ruleset* rs, const kyv_batch* b, const kyv_eval_opts* opt
 }
 
 void kyv_results_free(kyv_results* r) { delete r; }
+
+int kyv_results_jit(const kyv_results* r) { return r ? r->r.jit_used : 0; }
 
 int kyv_results_status(const kyv_results* r, uint8_t* out, size_t cap) {
   if (!r || !out) return fail(KYV_EINVAL, "null argument");

@@ -1097,11 +1097,90 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
       pm.nrules = (uint32_t)rs->rules.size() - pm.first_rule;
       rs->policies.push_back(pm);
     }
+    build_path_trie(*rs);
     return rs.release();
   } catch (std::exception& e) {
     if (err) *err = e.what();
     return nullptr;
   }
+}
+
+// ---------------------------------------------------------------- path trie (kyv_layout.h "Path columns")
+namespace {
+struct TrieBuilder {
+  Ruleset& rs;
+  std::vector<uint32_t> pn_trie;  // trie node a pnode was compiled against (CONFLICT: reached from two paths)
+  static constexpr uint32_t UNSET = NONE, CONFLICT = NONE - 1;
+  uint32_t child(uint32_t t, uint32_t key) {
+    for (auto& kv : rs.trie[t].kids) if (kv.first == key) return kv.second;
+    uint32_t id = (uint32_t)rs.trie.size();
+    uint32_t space = rs.trie[t].rowspace;
+    rs.trie.emplace_back();
+    rs.trie[id].rowspace = space;
+    rs.trie[id].col = rs.ncols++;
+    rs.col_rowspace.push_back(space);
+    rs.trie[t].kids.push_back({key, id});
+    return id;
+  }
+  uint32_t star(uint32_t t) {
+    if (rs.trie[t].star != NONE) return rs.trie[t].star;
+    uint32_t id = (uint32_t)rs.trie.size();
+    rs.trie.emplace_back();
+    rs.trie[id].rowspace = rs.nrowspaces++;
+    rs.trie[t].star = id;
+    return id;
+  }
+  // t == NONE: the pattern position has no static path (below a wildcard key): lookups binary-search
+  void walk(uint32_t pn, uint32_t t, int guard) {
+    if (pn == NONE || pn >= rs.pnodes.size() || guard > 4 * MAX_DEPTH) return;
+    if (pn_trie[pn] == UNSET) pn_trie[pn] = t;
+    else if (pn_trie[pn] != t) pn_trie[pn] = CONFLICT;
+    if (pn_trie[pn] == CONFLICT) t = NONE;
+    const PNode P = rs.pnodes[pn];
+    switch (P.kind) {
+      case P_MAP:
+        for (uint32_t e = 0; e < P.n; e++) {
+          uint32_t ct = (t == NONE || (rs.pentries[P.first + e].flags & EF_WILD)) ? NONE : child(t, rs.pentries[P.first + e].key);
+          PEntry& E = rs.pentries[P.first + e];
+          E.col = ct == NONE ? NONE : rs.trie[ct].col;
+          if (E.col == NONE) rs.pnodes[pn].flags |= PF_NEEDROW;
+          if (E.handler == H_STAR || E.handler == H_NEGATION || E.handler == H_EXIST_BADPAT || E.child == NONE) continue;
+          if (E.handler == H_EXISTENCE) {
+            uint32_t st = ct == NONE ? NONE : star(ct);
+            uint32_t npat = rs.pool[E.child];
+            for (uint32_t j = 0; j < npat; j++) walk(rs.pool[E.child + 1 + j], st, guard + 1);
+          } else {
+            walk(E.child, ct, guard + 1);
+          }
+        }
+        break;
+      case P_ARR_MAPS: walk(P.first, t == NONE ? NONE : star(t), guard + 1); break;
+      case P_ARR_POS: {
+        uint32_t st = t == NONE ? NONE : star(t);
+        for (uint32_t i = 0; i < P.n; i++) walk(rs.pool[P.first + i], st, guard + 1);
+        break;
+      }
+      default: break;
+    }
+  }
+};
+}  // namespace
+
+void build_path_trie(Ruleset& rs) {
+  rs.trie.assign(1, Ruleset::TrieNode{});
+  rs.ncols = 0;
+  rs.nrowspaces = 1;
+  rs.col_rowspace.clear();
+  for (auto& E : rs.pentries) E.col = NONE;
+  for (auto& P : rs.pnodes) P.flags &= (uint8_t)~PF_NEEDROW;
+  TrieBuilder tb{rs, std::vector<uint32_t>(rs.pnodes.size(), TrieBuilder::UNSET)};
+  for (auto& rd : rs.rules) {
+    if (rd.kind == RK_PATTERN) tb.walk(rd.root, 0, 0);
+    else if (rd.kind == RK_ANYPATTERN)
+      for (uint32_t a = 0; a < rd.nalts; a++) tb.walk(rs.pool[rd.root + a], 0, 0);
+  }
+  // entries of pnodes that conflicted after their first visit assigned columns: clear the whole subtree
+  // (a conflicting subtree is walked with t == NONE, which already cleared its entries' columns)
 }
 
 }  // namespace kyv

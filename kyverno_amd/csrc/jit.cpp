@@ -1,0 +1,418 @@
+// Runtime-compiled walk kernels: each ruleset's patterns are emitted as HIP source (one inlined device
+// function per pattern node) and compiled for gfx950 with hipRTC once per ruleset, then loaded per device.
+//
+// Why: the interpreted walk (kyv_wave.h) pays for generality on every step (frame management, handler
+// dispatch, 64-bit lane masks) and serialises one memory round trip per step. The generated code is the
+// per-lane recursion of eval_pattern (kyv_eval.h; pkg/engine/validate/validate.go:31-247 with
+// anchor/handlers.go, anchormap.go, error.go) unrolled for one pattern: keys, handlers, path templates and
+// leaf ids are constants, every path-column lookup of a map is issued up front (independent loads), and the
+// register footprint is what that pattern needs. The same walk-phase pieces (pair_walk, walk_chunks,
+// leaf matching) are shared with the interpreted kernel, and parity tests run both against the oracle.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <sstream>
+#include <unordered_map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kyv_host.h"
+
+namespace kyv {
+
+int pattern_depth(const Ruleset& rs, uint32_t pn, int guard);
+
+namespace {
+
+struct Gen {
+  const Ruleset& rs;
+  std::ostringstream out;
+  std::vector<uint8_t> emitted;  // pnode -> function emitted
+  bool ok = true;                // pattern compilable (else the rule stays on the interpreter)
+
+  explicit Gen(const Ruleset& r) : rs(r), emitted(r.pnodes.size(), 0) {}
+
+  static std::string u(uint32_t x) { return std::to_string(x) + "u"; }
+  static std::string i64(int64_t x) { return "(int64_t)" + std::to_string(x) + "ll"; }
+
+  // pattern.Validate(value, pattern) for one compiled leaf, as an expression-statement block that sets `okv`
+  // (and `fb`) from Val `x`: the type matrix of leaf_match with the pattern constants folded in, and the
+  // string mini-language's OR-of-AND atom groups unrolled in evaluation order.
+  std::string atom_call(const Atom& a) {
+    std::ostringstream o;
+    o << "jatom<" << (int)a.op << ", " << (int)a.flags << ", " << (int)a.glob << ">(w.v, x, " << u(a.pat) << ", "
+      << u(a.lit) << ", " << i64(a.dur) << ", " << i64(a.qlo) << ", " << i64(a.qhi) << ", &fb)";
+    return o.str();
+  }
+  std::string leaf_code(uint32_t lid) {
+    const Leaf& L = rs.leaves[lid];
+    std::ostringstream o;
+    switch (L.type) {
+      case L_NIL:
+        o << "okv = x.t == 0xFF || x.t == N_NULL || x.t == N_FALSE || (x.t == N_INT && x.i == 0) || "
+             "(x.t == N_FLOAT && x.f == 0.0) || (x.t == N_STR && x.sid == SID_EMPTY);";
+        break;
+      case L_BOOL: o << "okv = x.t == " << (L.bval ? "N_TRUE" : "N_FALSE") << ";"; break;
+      case L_FLOAT: {
+        uint64_t bits = __builtin_bit_cast(uint64_t, L.f);
+        o << "{ const double pf = __builtin_bit_cast(double, (uint64_t)" << bits << "ull);\n"
+          << "  okv = (x.t == N_INT && " << (L.fint ? "true" : "false") << " && " << i64(L.fi) << " == x.i) ||\n"
+          << "        (x.t == N_FLOAT && x.f == pf) ||\n"
+          << "        (x.t == N_STR && (gld32(w.v.str_flags + x.sid) & SF_FLOAT) && "
+             "*(const KYV_AS_GLOBAL double*)(w.v.str_f64 + x.sid) == pf); }";
+        break;
+      }
+      case L_STR: {
+        o << "{ bool done = x.t == N_STR && x.sid == " << u(L.exact) << ";\n";
+        for (uint32_t g = 0; g < L.ngroups; g++) {
+          uint32_t a0 = rs.pool[L.groups + 2 * g], na = rs.pool[L.groups + 2 * g + 1];
+          o << "  { bool all = !done;\n";
+          for (uint32_t k = 0; k < na; k++) {
+            const Atom& A = rs.atoms[a0 + k];
+            if (A.op == A_FALSE) { o << "    all = false;\n"; continue; }
+            if (A.op == A_RANGE_IN || A.op == A_RANGE_OUT) {
+              const Atom &s0 = rs.atoms[A.sub], &s1 = rs.atoms[A.sub + 1];
+              o << "    if (all) all = " << atom_call(s0) << (A.op == A_RANGE_IN ? " && " : " || ") << atom_call(s1) << ";\n";
+            } else {
+              o << "    if (all) all = " << atom_call(A) << ";\n";
+            }
+          }
+          o << "    if (all) done = true; }\n";
+        }
+        o << "  okv = done; }";
+        break;
+      }
+      case L_MAP: o << "okv = x.t == N_MAP;"; break;
+      default: o << "okv = false;";
+    }
+    return o.str();
+  }
+
+  // emit the function of pattern node `pn` (children first)
+  void node(uint32_t pn, int guard) {
+    if (pn == NONE || pn >= rs.pnodes.size() || guard > 4 * MAX_DEPTH) { ok = false; return; }
+    if (emitted[pn]) return;
+    const PNode P = rs.pnodes[pn];
+    // children first
+    switch (P.kind) {
+      case P_MAP:
+        for (uint32_t e = 0; e < P.n; e++) {
+          const PEntry& E = rs.pentries[P.first + e];
+          if (E.handler == H_STAR || E.handler == H_NEGATION || E.handler == H_EXIST_BADPAT) continue;
+          if (E.child == NONE) { ok = false; return; }
+          if (E.handler == H_EXISTENCE) {
+            uint32_t npat = rs.pool[E.child];
+            for (uint32_t j = 0; j < npat; j++) node(rs.pool[E.child + 1 + j], guard + 1);
+          } else {
+            node(E.child, guard + 1);
+          }
+        }
+        break;
+      case P_ARR_MAPS: node(P.first, guard + 1); break;
+      case P_ARR_POS:
+        for (uint32_t i = 0; i < P.n; i++) node(rs.pool[P.first + i], guard + 1);
+        break;
+      default: break;
+    }
+    if (!ok) return;
+    emitted[pn] = 1;
+    const std::string T = u(P.tmpl);
+    out << "static __device__ __forceinline__ Ret p" << pn << "(JW& w, uint32_t rn, uint32_t rt, uint32_t row) {\n";
+    switch (P.kind) {
+      case P_MAP: map(pn, P); break;
+      case P_LEAF:
+        out << "  Node n{0u, 0u, 0u, 0u};\n  if (rn != NONE) n = gnode(w.R + rn);\n";
+        out << "  bool fb = false, okv = true;\n";
+        out << "  const bool each = rn != NONE && node_type(n) == N_ARR;\n"
+               "  const uint32_t cnt = each ? n.b : 1u;\n"
+               "  for (uint32_t i = 0; i < cnt && okv; i++) {\n"
+               "    const Val x = each ? wvalue_of(w.v, w.R, n.a + i) : (rn == NONE ? wvalue_absent() : wvalue_node(w.v, n));\n"
+               "    " << leaf_code(P.first) << "\n"
+               "  }\n";
+        out << "  if (fb) { w.ost = ST_FALLBACK; return ok_ret(); }\n";
+        out << "  return okv ? ok_ret() : mkerr(EC_NONE, 0, " << T << ");\n";
+        break;
+      case P_ARR_EMPTY:
+        out << "  return mkerr(EC_NONE, 0, " << T << ");\n";
+        break;
+      case P_ARR_SCALAR: {
+        uint32_t leaf = rs.pnodes[P.first].first;
+        out << "  if (rn == NONE) return mkerr(EC_NONE, 0, " << T << ");\n";
+        out << "  const Node a = gnode(w.R + rn);\n  if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << T << ");\n";
+        out << "  bool fb = false, okv = true;\n";
+        out << "  for (uint32_t i = 0; i < a.b && okv; i++) {\n"
+               "    const Val x = wvalue_of(w.v, w.R, a.a + i);\n"
+               "    " << leaf_code(leaf) << "\n"
+               "  }\n";
+        out << "  if (fb) { w.ost = ST_FALLBACK; return ok_ret(); }\n";
+        out << "  return okv ? ok_ret() : mkerr(EC_NONE, 0, " << T << ");\n";
+        break;
+      }
+      case P_ARR_MAPS: case P_ARR_POS: {
+        out << "  if (rn == NONE) return mkerr(EC_NONE, 0, " << T << ");\n";
+        out << "  const Node a = gnode(w.R + rn);\n  if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << T << ");\n";
+        if (P.kind == P_ARR_POS) out << "  if (a.b < " << u(P.n) << ") return mkerr(EC_NONE, 0, NONE);\n";
+        out << "  uint32_t st = 0;\n";
+        auto elem = [&](const std::string& i, uint32_t child, bool setidx) {
+          if (setidx)
+            out << "    w.idx = (w.idx & ~(0xFFFFull << " << 16u * P.level << ")) | ((uint64_t)" << i << " << "
+                << 16u * P.level << ");\n";
+          out << "    { Ret r = p" << child << "(w, a.a + " << i << ", T_UNK, a.c == NONE ? NONE : a.c + " << i << ");\n"
+              << "      if (w.ost) return r;\n"
+              << "      if (r.err) { if (ret_is_skip(r)) st |= FS_SKIP | ((uint32_t)r.mask << 2); else return r; }\n"
+              << "      else st |= FS_APPLY; }\n";
+        };
+        if (P.kind == P_ARR_MAPS) {
+          out << "  for (uint32_t i = 0; i < a.b; i++) {\n";
+          elem("i", P.first, true);
+          out << "  }\n";
+        } else {
+          for (uint32_t i = 0; i < P.n; i++) {
+            out << "  {\n";
+            elem(u(i), rs.pool[P.first + i], false);
+            out << "  }\n";
+          }
+        }
+        out << "  if ((st & FS_SKIP) && !(st & FS_APPLY)) return mkerr(EC_NONE, (uint8_t)(st >> 2), " << T << ");\n";
+        out << "  return ok_ret();\n";
+        break;
+      }
+      default: ok = false;
+    }
+    out << "}\n";
+  }
+
+  // lookup expression for entry index ei (global pentries index) into c<e>/t<e>
+  void lookup(uint32_t ei, uint32_t e, const std::string& keyexpr_rowvar) {
+    const PEntry& E = rs.pentries[ei];
+    if (E.col != NONE) {
+      out << "  c" << e << " = jcol(w, " << u(ei) << ", row, &t" << e << ");\n";
+    } else {
+      std::string key = (E.flags & EF_WILD) ? "w.keys.get(" + u(E.slot) + ")" : u(E.key);
+      out << "  c" << e << " = wmap_find(w.R, " << keyexpr_rowvar << ".a, " << keyexpr_rowvar << ".b, " << key
+          << "); t" << e << " = T_UNK;\n";
+    }
+  }
+
+  void map(uint32_t pn, const PNode& P) {
+    const bool needrow = (P.flags & PF_NEEDROW) != 0;
+    const std::string T = u(P.tmpl);
+    out << "  Node m{0u, 0u, 0u, 0u};\n";
+    out << "  if (rn != NONE && " << (needrow ? "true" : "rt == T_UNK") << ") { m = gnode(w.R + rn); rt = node_type(m); }\n";
+    out << "  if (rn == NONE || rt != N_MAP) return mkerr(EC_NONE, 0, " << T << ");\n";
+    // static (column) lookups up front: independent loads, issued together
+    for (uint32_t e = 0; e < P.n; e++) {
+      out << "  uint32_t c" << e << " = NONE, t" << e << " = T_UNK;\n";
+      const PEntry& E = rs.pentries[P.first + e];
+      if (E.col != NONE) lookup(P.first + e, e, "m");
+    }
+    (void)pn;
+    // AnchorMap.CheckAnchorInResource (anchormap.go:30-44); wildcard keys use the slots as they are before
+    // this level's metadata expansion, exactly as the walk does
+    for (uint32_t e = 0; e < P.n; e++) {
+      const PEntry& E = rs.pentries[P.first + e];
+      if (E.abit == 0xFF) continue;
+      std::string B = "(1ull << " + std::to_string(E.abit) + ")";
+      out << "  w.seen |= " << B << ";\n";
+      if (E.col != NONE) {
+        out << "  if (c" << e << " != NONE) w.found |= " << B << ";\n";
+      } else {
+        std::string key = (E.flags & EF_WILD) ? "w.keys.get(" + u(E.slot) + ")" : u(E.key);
+        out << "  if (!(w.found & " << B << ") && wmap_find(w.R, m.a, m.b, " << key << ") != NONE) w.found |= " << B << ";\n";
+      }
+    }
+    if (P.flags & PF_META) {
+      out << "  { uint8_t o = expand_meta(w.v, w.v.metas[w.mbase + " << u(P.meta) << "], NodeTab{w.R}, rn, *w.hp, w.keys);\n"
+          << "    if (o != ST_NONE) { w.ost = o; return ok_ret(); } }\n";
+    }
+    for (uint32_t e = 0; e < P.n; e++) {
+      const PEntry& E = rs.pentries[P.first + e];
+      const std::string ET = u(E.tmpl);
+      const std::string c = "c" + std::to_string(e), t = "t" + std::to_string(e);
+      if (E.col == NONE) lookup(P.first + e, e, "m");
+      auto call = [&](const std::string& wrap) {
+        out << "    { Ret r = p" << E.child << "(w, " << c << ", " << t << ", row);\n"
+            << "      if (w.ost) return r;\n"
+            << "      if (r.err) { " << wrap << "return r; } }\n";
+      };
+      switch (E.handler) {
+        case H_NEGATION:
+          out << "  if (" << c << " != NONE) return mkerr(EC_NEG, PH_NEG, " << ET << ");\n";
+          break;
+        case H_EQUALITY:
+          out << "  if (" << c << " != NONE) {\n";
+          call("");
+          out << "  }\n";
+          break;
+        case H_GLOBAL:
+          out << "  if (" << c << " != NONE) {\n";
+          call("r.code = EC_GLOBAL; r.mask |= PH_GLOBAL; ");
+          out << "  }\n";
+          break;
+        case H_CONDITION:
+          out << "  if (" << c << " == NONE) return mkerr(EC_COND, PH_COND, " << ET << ");\n  {\n";
+          call("r.code = EC_COND; r.mask |= PH_COND; ");
+          out << "  }\n";
+          break;
+        case H_STAR:
+          out << "  if (" << c << " == NONE || (" << t << " != T_UNK ? " << t << " : node_type(gnode(w.R + " << c
+              << "))) == N_NULL) return mkerr(EC_NONE, 0, " << T << ");\n";
+          break;
+        case H_EXIST_BADPAT:
+          out << "  if (" << c << " != NONE) return mkerr(EC_NONE, 0, " << ET << ");\n";
+          break;
+        case H_EXISTENCE: {
+          uint32_t npat = rs.pool[E.child];
+          out << "  if (" << c << " != NONE) {\n"
+              << "    const Node a = gnode(w.R + " << c << ");\n"
+              << "    if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << ET << ");\n";
+          for (uint32_t j = 0; j < npat; j++) {
+            out << "    { bool hit = false;\n"
+                << "      for (uint32_t i = 0; i < a.b; i++) {\n"
+                << "        Ret r = p" << rs.pool[E.child + 1 + j] << "(w, a.a + i, T_UNK, a.c == NONE ? NONE : a.c + i);\n"
+                << "        if (w.ost) return r;\n"
+                << "        if (!r.err) { hit = true; break; }\n"
+                << "      }\n"
+                << "      if (!hit) return mkerr(EC_NONE, 0, " << ET << "); }\n";
+          }
+          out << "  }\n";
+          break;
+        }
+        default:  // H_DEFAULT: resourceMap[k] (absent -> nil)
+          out << "  {\n";
+          call("");
+          out << "  }\n";
+      }
+    }
+    out << "  return ok_ret();\n";
+  }
+};
+
+std::string self_dir() {
+  Dl_info info;
+  if (dladdr((void*)&self_dir, &info) && info.dli_fname) {
+    std::string p = info.dli_fname;
+    size_t s = p.rfind('/');
+    return s == std::string::npos ? std::string(".") : p.substr(0, s);
+  }
+  return ".";
+}
+
+}  // namespace
+
+// Rules whose patterns the generator covers get a bit in `jit_rules`; the source holds their node functions,
+// a root switch and the walk kernel `kyv_jit_walk`.
+std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
+  Gen g(rs);
+  jit_rules->assign(rs.rules.size(), 0);
+  std::vector<uint32_t> roots;
+  for (size_t k = 0; k < rs.rules.size(); k++) {
+    const RuleDesc& rd = rs.rules[k];
+    if (rd.kind != RK_PATTERN && rd.kind != RK_ANYPATTERN) continue;
+    std::vector<uint32_t> rr;
+    if (rd.kind == RK_PATTERN) rr.push_back(rd.root);
+    else for (uint32_t a = 0; a < rd.nalts; a++) rr.push_back(rs.pool[rd.root + a]);
+    bool ok = true;
+    for (uint32_t r : rr) if (pattern_depth(rs, r, 0) > MAX_DEPTH) ok = false;  // the walk would fall back
+    if (!ok) continue;
+    size_t mark = g.out.tellp();
+    std::vector<uint8_t> em = g.emitted;
+    g.ok = true;
+    for (uint32_t r : rr) g.node(r, 0);
+    if (!g.ok) {  // roll back this rule's functions
+      std::string s = g.out.str().substr(0, mark);
+      g.out.str("");
+      g.out.clear();
+      g.out << s;
+      g.emitted = em;
+      continue;
+    }
+    (*jit_rules)[k] = 1;
+    for (uint32_t r : rr) roots.push_back(r);
+  }
+  std::ostringstream src;
+  src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n#include \"kyv_wave.h\"\nnamespace kyv {\n";
+  src << g.out.str();
+  // one function per pattern root (inlined into the root switch)
+  for (uint32_t r : roots)
+    src << "static __device__ __forceinline__ void root" << r
+        << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, PatOut& out) {\n"
+           "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
+           "  Ret r = p" << r << "(w, 0u, T_UNK, (uint32_t)(hp - v.hdr));\n"
+           "  jfinish(w, r, out);\n"
+           "}\n";
+  src << "struct JitWalker {\n"
+         "  __device__ __forceinline__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp,\n"
+         "                                     const RuleDesc& rd, PatOut& out) {\n"
+         "    out.status = ST_NONE; out.idx = 0; out.tmpl = NONE; out.key0 = NONE; out.key1 = NONE;\n"
+         "    if (!walk) return;\n"
+         "    switch (root) {\n";
+  for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, out); break;\n";
+  src << "      default: out.status = ST_FALLBACK;\n"
+         "    }\n"
+         "  }\n"
+         "};\n"
+         "}  // namespace kyv\n"
+         "extern \"C\" __global__ void __launch_bounds__(64) kyv_jit_walk(const kyv::View* __restrict__ vp, kyv::DevOut o,\n"
+         "    const uint32_t* __restrict__ items, const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ item_cnt,\n"
+         "    const uint32_t* __restrict__ chunk_pre) {\n"
+         "  kyv::JitWalker wk;\n"
+         "  kyv::walk_chunks(*vp, o, items, item_off, item_cnt, chunk_pre, wk);\n"
+         "}\n";
+  return src.str();
+}
+
+std::vector<char> jit_compile_uncached(const std::string& src, double* seconds);
+
+// hipRTC compile of the generated source for gfx950 -> code object
+std::vector<char> jit_compile(const std::string& src, double* seconds) {
+  // process-wide cache: identical rulesets (same generated source) compile once
+  static std::mutex mu;
+  static std::unordered_map<std::string, std::vector<char>> cache;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(src);
+    if (it != cache.end()) { if (seconds) *seconds = 0; return it->second; }
+  }
+  std::vector<char> code = jit_compile_uncached(src, seconds);
+  std::lock_guard<std::mutex> lk(mu);
+  cache.emplace(src, code);
+  return code;
+}
+
+std::vector<char> jit_compile_uncached(const std::string& src, double* seconds) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::string dir = self_dir();
+  const char* env = getenv("KYV_CSRC");
+  std::string inc = "-I" + (env ? std::string(env) : dir + "/csrc");
+  std::string inc2 = "-I" + dir + "/../include";
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str()};
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "kyv_jit_walk.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    throw std::runtime_error("hiprtcCreateProgram failed");
+  hiprtcResult r = hiprtcCompileProgram(prog, 5, opts);
+  if (r != HIPRTC_SUCCESS) {
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    std::string log(ls + 1, '\0');
+    hiprtcGetProgramLog(prog, &log[0]);
+    hiprtcDestroyProgram(&prog);
+    throw std::runtime_error("hipRTC compile of the ruleset walk kernel failed: " + log.substr(0, 4000));
+  }
+  size_t cs = 0;
+  hiprtcGetCodeSize(prog, &cs);
+  std::vector<char> code(cs);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return code;
+}
+
+}  // namespace kyv

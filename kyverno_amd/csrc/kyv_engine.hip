@@ -1,14 +1,19 @@
 // HIP execution of the batched validate path on MI355X (gfx950).
 //
-// eval_kernel: one lane per resource, the rule index uniform across the wavefront, so every lane of a
-// wave walks the same compiled program over a different resource's node table (divergence only where
-// the resources differ: array trip counts, absent optional keys).  The per-lane DFS frame stack lives in
-// LDS (lane-strided, conflict-free), verdicts are written rule-major (coalesced bytes), failing-path
-// records are compacted with a wave ballot + one atomic per wave, and per-rule status counters are
-// reduced in LDS per block before one atomic per (block, rule, status).
+// Two phases per evaluation (match_eval -> pattern_eval with compaction):
+//   match_kernel  one lane per resource, rule loop uniform across the wave: kind gate, match/exclude, dispatch;
+//                 final verdicts for every pair that needs no pattern walk (incl. PodSecurity), and per-rule
+//                 work lists of the pairs that do (wave ballot + one atomic per wave and rule);
+//   scan_kernel   per-rule chunk prefix of the work lists;
+//   walk_kernel   persistent grid-stride over 64-pair chunks of ONE rule each: the wave-uniform pattern walker
+//                 (kyv_wave.h) with no idle lanes from gated / non-matching pairs.
+// Verdicts are written rule-major (coalesced bytes), failing-path records are compacted with a wave ballot +
+// one atomic per wave, per-rule status counters with ballots + one atomic per (wave, rule, status).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <mutex>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -44,6 +49,8 @@ struct DevRuleset {
   uint8_t* base = nullptr;
   size_t bytes = 0;
   size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool;
+  hipModule_t jmod = nullptr;     // runtime-compiled walk kernel (jit.cpp) loaded on this device
+  hipFunction_t jfn = nullptr;
 };
 
 struct DeviceResults {
@@ -59,10 +66,20 @@ struct DeviceResults {
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   View* view = nullptr;  // device copy of the View the kernel reads
+  // walk work lists (match_kernel -> walk_kernel): per rule a list of resource positions
+  uint32_t* items = nullptr;     // [sum of per-rule capacities]
+  uint32_t* item_off = nullptr;  // [nrules] first slot of rule k's list
+  uint32_t* item_cnt = nullptr;  // [nrules] items appended
+  uint32_t* chunk_pre = nullptr; // [nrules + 1] exclusive prefix of ceil(cnt / 64), interpreted rules
+  uint32_t* chunk_pre_jit = nullptr;  // same for the rules of the compiled walk kernel
+  uint8_t* jitf = nullptr;       // [nrules] rule walked by the compiled kernel in this evaluation
+  int jit_state = -1;            // what jitf currently holds (0 none, 1 the ruleset's jit_rules)
+  uint32_t walk_grid = 0;
 };
 
 static void free_dev_results(DeviceResults& d) {
   hipFree(d.view); hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
+  hipFree(d.items); hipFree(d.item_off); hipFree(d.item_cnt); hipFree(d.chunk_pre); hipFree(d.chunk_pre_jit); hipFree(d.jitf);
   if (d.e0) hipEventDestroy(d.e0);
   if (d.e1) hipEventDestroy(d.e1);
   if (d.stream) hipStreamDestroy(d.stream);
@@ -74,7 +91,8 @@ struct DevBatch {
   DeviceResults* out = nullptr;  // result buffers + stream, resident across evaluations
   uint8_t* base = nullptr;
   size_t bytes = 0;
-  size_t o_nodes, o_hdr, o_faux, o_soff, o_slen, o_sflags, o_sdur, o_sqty, o_sf64, o_heap, o_nsloff, o_nslkv, o_gate;
+  size_t o_nodes, o_hdr, o_faux, o_soff, o_slen, o_sflags, o_sdur, o_sqty, o_sf64, o_heap, o_nsloff, o_nslkv, o_gate,
+      o_colv, o_coloff, o_pe;
   double upload_ms = 0;
 };
 
@@ -120,6 +138,13 @@ static DevBatch* upload_batch(const Batch& b, int device) {
   d->o_nsloff = p.add(b.nsl_off);
   d->o_nslkv = p.add(b.nsl_kv);
   d->o_gate = p.add(b.gate);
+  d->o_colv = p.add(b.colv);
+  d->o_coloff = p.add(b.col_off);
+  // batch-specialised copy of the pattern entries: `col` holds the column's absolute offset into colv, so the
+  // walker reads a lookup's column without first reading the batch's column offset table
+  std::vector<PEntry> pe = b.rs->pentries;
+  for (auto& E : pe) if (E.col != NONE) E.col = b.col_off[E.col];
+  d->o_pe = p.add(pe);
   d->bytes = p.host.size();
   HIP_OK(hipMalloc(&d->base, d->bytes));
   HIP_OK(hipMemcpy(d->base, p.host.data(), d->bytes, hipMemcpyHostToDevice));
@@ -144,12 +169,16 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
     v.nsl_off = (const uint32_t*)(bbase + db->o_nsloff);
     v.nsl_kv = (const uint32_t*)(bbase + db->o_nslkv);
     v.gate = (const uint32_t*)(bbase + db->o_gate);
+    v.colv = (const uint32_t*)(bbase + db->o_colv);
+    v.col_off = (const uint32_t*)(bbase + db->o_coloff);
   } else {
     v.nodes = b.nodes.data(); v.hdr = b.hdr.data(); v.faux = b.faux.data();
     v.str_off = b.str_off.data(); v.str_len = b.str_len.data(); v.str_flags = b.str_flags.data();
     v.str_dur = b.str_dur.data(); v.str_qty = b.str_qty.data(); v.str_f64 = b.str_f64.data();
     v.heap = b.heap.data(); v.nsl_off = b.nsl_off.data(); v.nsl_kv = b.nsl_kv.data();
     v.gate = b.gate.data();
+    v.colv = b.colv.data();
+    v.col_off = b.col_off.data();
   }
   v.gate_words = b.gate_words;
   v.nres = (uint32_t)b.hdr.size();
@@ -172,78 +201,98 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
     v.reqs = rs.reqs.data(); v.pn = rs.pnodes.data(); v.pe = rs.pentries.data(); v.leaves = rs.leaves.data();
     v.atoms = rs.atoms.data(); v.metas = rs.metas.data(); v.pss = rs.pss.data(); v.pool = rs.pool.data();
   }
+  if (db) v.pe = (const PEntry*)(bbase + db->o_pe);  // device: entries with absolute column offsets
   return v;
 }
 
 // ---------------------------------------------------------------- kernels
-constexpr int WAVE = 64;
 constexpr int BLOCK = 64;        // one wave per workgroup; LDS = depth * 64 * 16 B
 constexpr int RECS_PER_PAIR = MAX_ALTS;
 
-struct DevOut {
-  uint8_t* status;         // [rule][res]
-  uint32_t* pss_fails;     // [pss rule slot][res]
-  const uint32_t* pss_slot;// rule -> pss slot or NONE
-  FailRec* recs;
-  uint32_t* nrecs;         // global record counter
-  uint32_t max_recs;
-  unsigned long long* counts;  // [rule][NSTATUS]
-  uint32_t rule_lo, rule_hi;   // rule range handled by this launch
-};
+#ifndef KYV_WPE
+#define KYV_WPE 4
+#endif
 
-// Failing-path records of one wave, appended with one atomic per emit point that has any record.
-struct WaveSink {
-  FailRec* recs;
-  uint32_t* n;
-  uint32_t max;
-  __device__ __forceinline__ void emit(bool has, const FailRec& f) {
-    unsigned long long m = __ballot(has);
-    if (!m) return;
-    const uint32_t lane = threadIdx.x & (WAVE - 1);
-    const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(n, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)leader);
-    if (has) {
-      uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-      if (at < max) recs[at] = f;
-    }
-  }
-};
-
-// One lane per resource, the rule loop uniform across the wave. `vp` points at a device-resident View so
-// that its fields are read with scalar loads instead of being copied into per-lane private memory.
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) eval_kernel(const View* __restrict__ vp, DevOut o, int depth) {
-  extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
+// Phase 1 (match_eval): one lane per resource, the rule loop uniform across the wave. Kind gate, match /
+// exclude program, dispatch; verdicts that need no pattern walk are final here (incl. PodSecurity). Pairs
+// that need the walk are appended to the rule's work list (wave ballot + one atomic per wave and rule).
+__global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ vp, DevOut o, uint32_t* __restrict__ items,
+                                                      const uint32_t* __restrict__ item_off, uint32_t* __restrict__ item_cnt) {
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
   const uint32_t r = blockIdx.x * BLOCK + lane;
   const bool active = r < v.nres;
-  WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth};
-  WaveSink sink{o.recs, o.nrecs, o.max_recs};
   const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
   for (uint32_t k = o.rule_lo; k < o.rule_hi; k++) {
     uint32_t pf = 0;
-    // kind gate: rules that cannot match this resource's kind are ST_NONE without running the match program
-    bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
-    uint8_t st = eval_pair(v, gated, r, k, wk, &pf, sink);
-    if (active) {
+    bool walk = false;
+    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+    const uint8_t st = pair_dispatch(v, gated, r, k, &pf, &walk);
+    const unsigned long long wm = __ballot(walk);
+    if (wm) {
+      const uint32_t leader = (uint32_t)__ffsll((long long)wm) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&item_cnt[k], (uint32_t)__popcll(wm));
+      base = __shfl(base, (int)leader);
+      if (walk) items[(size_t)item_off[k] + base + __popcll(wm & ((1ull << lane) - 1))] = r;
+    }
+    if (active && !walk) {
       o.status[(size_t)k * v.nres + r] = st;
-      uint32_t ps = o.pss_slot[k];
+      const uint32_t ps = o.pss_slot[k];
       if (ps != NONE) o.pss_fails[(size_t)ps * v.nres + r] = pf;
     }
-    // per-rule status counts: wave ballots -> one atomic per status present
-    for (int s = 0; s < NSTATUS; s++) {
-      unsigned long long m = __ballot(active && (st & 7) == s);
-      if (m && lane == 0) atomicAdd(&o.counts[(size_t)k * NSTATUS + s], (unsigned long long)__popcll(m));
-    }
+    count_status(o.counts, k, active && !walk, st);
   }
+}
+
+// per-rule chunk prefixes of the work lists (chunks = ceil(item_cnt / 64)), one for the interpreted walk
+// kernel and one for the compiled one (jitf[k] selects); one workgroup of 1024 threads
+__global__ void __launch_bounds__(1024) scan_kernel(const uint32_t* __restrict__ cnt, const uint8_t* __restrict__ jitf,
+                                                    uint32_t* __restrict__ pre, uint32_t* __restrict__ pre_jit, uint32_t n) {
+  __shared__ uint32_t part[2][1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t lo = t * per, hi = min(n, lo + per);
+  uint32_t s0 = 0, s1 = 0;
+  for (uint32_t k = lo; k < hi; k++) {
+    uint32_t c = (cnt[k] + WAVE - 1) / WAVE;
+    if (jitf[k]) s1 += c; else s0 += c;
+  }
+  part[0][t] = s0;
+  part[1][t] = s1;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+    uint32_t x0 = t >= off ? part[0][t - off] : 0, x1 = t >= off ? part[1][t - off] : 0;
+    __syncthreads();
+    part[0][t] += x0;
+    part[1][t] += x1;
+    __syncthreads();
+  }
+  uint32_t r0 = part[0][t] - s0, r1 = part[1][t] - s1;
+  for (uint32_t k = lo; k < hi; k++) {
+    pre[k] = r0;
+    pre_jit[k] = r1;
+    uint32_t c = (cnt[k] + WAVE - 1) / WAVE;
+    if (jitf[k]) r1 += c; else r0 += c;
+  }
+  if (t == 1023) { pre[n] = part[0][1023]; pre_jit[n] = part[1][1023]; }
+}
+
+// Phase 2 (pattern_eval): each wave takes chunks of 64 work items of ONE rule (grid-stride over all rules'
+// chunks), so every lane walks the same compiled pattern over a different resource with the wave-uniform
+// walker; verdict bytes, failing-path records (wave ballot + one atomic) and counts as in phase 1.
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_WPE)))
+walk_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restrict__ items, const uint32_t* __restrict__ item_off,
+            const uint32_t* __restrict__ item_cnt, const uint32_t* __restrict__ chunk_pre, int depth) {
+  extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
+  WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth};
+  walk_chunks(*vp, o, items, item_off, item_cnt, chunk_pre, wk);
 }
 
 // ---------------------------------------------------------------- host entry
 // Frames the walk of one pattern node can push (eval_pattern): a map frame stays while its entries are
 // walked, array frames while their elements are, an existence frame while its candidates are.
-static int pattern_depth(const Ruleset& rs, uint32_t pn, int guard) {
+int pattern_depth(const Ruleset& rs, uint32_t pn, int guard) {
   if (pn == NONE || guard > MAX_DEPTH) return MAX_DEPTH + 1;
   const PNode& P = rs.pnodes[pn];
   int d = 0;
@@ -282,7 +331,32 @@ static int ruleset_depth(const Ruleset& rs) {
 
 // GPU evaluation of every (resource, rule) pair. Device images, result buffers and the stream stay resident
 // per batch; `copy_back` false keeps the verdicts on the device (bench mode).
-void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back) {
+// Compile (once per ruleset) and load (once per device) the ruleset's walk kernel; false if unavailable.
+static std::mutex g_jit_mu;
+static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
+  if (dr->jfn) return true;
+  std::lock_guard<std::mutex> lk(g_jit_mu);
+  if (!rs.jit_tried) {
+    rs.jit_tried = true;
+    try {
+      std::string src = jit_source(rs, &rs.jit_rules);
+      bool any = false;
+      for (auto x : rs.jit_rules) any |= x != 0;
+      if (any) rs.jit_code = jit_compile(src, &rs.jit_compile_s);
+    } catch (std::exception& e) {
+      rs.jit_error = e.what();
+      rs.jit_code.clear();
+      fprintf(stderr, "[kyvgpu] runtime-compiled walk kernel unavailable, using the interpreted one: %s\n", e.what());
+    }
+  }
+  if (rs.jit_code.empty()) return false;
+  HIP_OK(hipModuleLoadData(&dr->jmod, rs.jit_code.data()));
+  HIP_OK(hipModuleGetFunction(&dr->jfn, dr->jmod, "kyv_jit_walk"));
+  return true;
+}
+
+void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back,
+              int jit_mode) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw std::runtime_error("no HIP device available (GPU backend requested)");
   if (device < 0 || device >= ndev) throw std::runtime_error("device index out of range");
@@ -323,10 +397,45 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipEventCreate(&d.e1));
     HIP_OK(hipMalloc(&d.view, sizeof(View)));
     HIP_OK(hipMemcpy(d.view, &v, sizeof(View), hipMemcpyHostToDevice));
+    // walk work-list capacity per rule: resources of the kind classes its gate admits (exact upper bound)
+    std::vector<uint64_t> cls_n(std::max<uint32_t>(b.nclass, 1), 0);
+    for (auto& h : b.hdr) cls_n[h.kclass]++;
+    std::vector<uint32_t> off(std::max<size_t>(nrules, 1), 0);
+    uint64_t cap = 0, chunks = 0;
+    for (size_t k = 0; k < nrules; k++) {
+      off[k] = (uint32_t)cap;
+      if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
+      uint64_t ck = 0;
+      for (uint32_t c = 0; c < b.nclass; c++)
+        if ((b.gate[(size_t)c * b.gate_words + k / 32] >> (k % 32)) & 1u) ck += cls_n[c];
+      cap += ck;
+      chunks += (ck + WAVE - 1) / WAVE;
+      if (cap > 0xFFFFFFF0ull) throw std::runtime_error("walk work lists exceed 2^32 items; split the batch");
+    }
+    HIP_OK(hipMalloc(&d.items, std::max<uint64_t>(cap, 1) * 4));
+    HIP_OK(hipMalloc(&d.item_off, off.size() * 4));
+    HIP_OK(hipMalloc(&d.item_cnt, off.size() * 4));
+    HIP_OK(hipMalloc(&d.chunk_pre, (nrules + 1) * 4));
+    HIP_OK(hipMalloc(&d.chunk_pre_jit, (nrules + 1) * 4));
+    HIP_OK(hipMalloc(&d.jitf, std::max<size_t>(nrules, 1)));
+    HIP_OK(hipMemcpy(d.item_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+    // persistent grid: enough waves to fill the chip several times over, never more than the chunks
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+    d.walk_grid = (uint32_t)std::min<uint64_t>(chunks, (uint64_t)cus * 64);
     db->out = dd;
   }
   DeviceResults& d = *db->out;
   hipStream_t stream = d.stream;
+  const bool use_jit = jit_mode == JIT_ON || (jit_mode == JIT_AUTO && nres >= JIT_AUTO_MIN_RESOURCES);
+  const bool jit = use_jit && ensure_jit(mrs, dr);
+  if (d.jit_state != (int)jit) {
+    std::vector<uint8_t> f(std::max<size_t>(nrules, 1), 0);
+    if (jit) for (size_t k = 0; k < nrules; k++) f[k] = rs.jit_rules[k];
+    HIP_OK(hipMemcpy(d.jitf, f.data(), f.size(), hipMemcpyHostToDevice));
+    d.jit_state = (int)jit;
+  }
   DevOut o{d.status, d.pss_fails, d.pss_slot, d.recs, d.nrecs, d.max_recs, d.counts, 0, (uint32_t)nrules};
   int depth = ruleset_depth(rs);
   size_t lds = (size_t)depth * (sizeof(UFrame) + BLOCK * sizeof(LaneFrame));
@@ -336,20 +445,45 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   for (int it = 0; it < n; it++) {
     HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
     HIP_OK(hipMemsetAsync(d.counts, 0, nrules * NSTATUS * 8, stream));
+    HIP_OK(hipMemsetAsync(d.item_cnt, 0, std::max<size_t>(1, nrules) * 4, stream));
     HIP_OK(hipEventRecord(d.e0, stream));
-    if (nres && nrules) hipLaunchKernelGGL(eval_kernel, grid, dim3(BLOCK), lds, stream, (const View*)d.view, o, depth);
-    HIP_OK(hipGetLastError());
+    if (nres && nrules) {
+      hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.items, d.item_off, d.item_cnt);
+      HIP_OK(hipGetLastError());
+      hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, d.item_cnt, d.jitf, d.chunk_pre, d.chunk_pre_jit,
+                         (uint32_t)nrules);
+      HIP_OK(hipGetLastError());
+      if (d.walk_grid) {
+        hipLaunchKernelGGL(walk_kernel, dim3(d.walk_grid), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.items,
+                           d.item_off, d.item_cnt, d.chunk_pre, depth);
+        HIP_OK(hipGetLastError());
+        if (jit) {
+          const View* vp = d.view;
+          uint32_t *it = d.items, *io = d.item_off, *ic = d.item_cnt, *pj = d.chunk_pre_jit;
+          void* args[] = {(void*)&vp, (void*)&o, (void*)&it, (void*)&io, (void*)&ic, (void*)&pj};
+          HIP_OK(hipModuleLaunchKernel(dr->jfn, d.walk_grid, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        }
+      }
+    }
     HIP_OK(hipEventRecord(d.e1, stream));
     HIP_OK(hipEventSynchronize(d.e1));
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, d.e0, d.e1));
     total_ms += ms;
   }
+#ifdef KYV_EXP_STEPS
+  {
+    unsigned long long steps = 0;
+    HIP_OK(hipMemcpyFromSymbol(&steps, HIP_SYMBOL(kyv_exp_steps), 8));
+    fprintf(stderr, "[exp] walker loop iterations (wave-level, all launches so far): %llu\n", steps);
+  }
+#endif
   if (kernel_ms_avg) *kernel_ms_avg = total_ms / n;
   if (out) {
     out->nres = (uint32_t)nres;
     out->nrules = (uint32_t)nrules;
     out->kernel_ms = total_ms / n;
+    out->jit_used = jit ? 1 : 0;
     out->h2d_ms = db->upload_ms;
     std::vector<unsigned long long> counts(nrules * NSTATUS);
     HIP_OK(hipMemcpy(counts.data(), d.counts, counts.size() * 8, hipMemcpyDeviceToHost));
@@ -446,7 +580,14 @@ void free_device_images(Ruleset& rs, Batch* b) {
       }
     b->dev.clear();
   } else {
-    for (auto* p : rs.dev) if (p) { DevRuleset* d = (DevRuleset*)p; hipSetDevice(d->device); hipFree(d->base); delete d; }
+    for (auto* p : rs.dev)
+      if (p) {
+        DevRuleset* d = (DevRuleset*)p;
+        hipSetDevice(d->device);
+        hipFree(d->base);
+        if (d->jmod) hipModuleUnload(d->jmod);
+        delete d;
+      }
     rs.dev.clear();
   }
 }

@@ -10,7 +10,9 @@
 //   metadata wildcard keys   pkg/engine/wildcards/wildcards.go:62-151
 //   PodSecurity              pkg/pss/evaluate.go:16-146 (+ pod-security-admission v0.26.1 checks)
 #pragma once
+#ifndef __HIPCC_RTC__  // hipRTC (runtime-compiled walk kernels, jit.cpp) provides the HIP runtime itself
 #include <hip/hip_runtime.h>
+#endif
 
 #include "kyv_layout.h"
 
@@ -71,6 +73,8 @@ struct View {
   const uint32_t* nsl_kv;
   const uint32_t* gate;     // [kind class][gate_words] rule bits (batch.cpp order_by_kind)
   uint32_t gate_words;
+  const uint32_t* colv;     // path columns (kyv_layout.h): colv[col_off[c] + row]
+  const uint32_t* col_off;  // (device View: pe[].col already holds col_off[col])
   // ruleset
   const RuleDesc* rules;
   uint32_t nrules;
@@ -262,6 +266,9 @@ KYV_HD bool atom_eval(const View& v, const Atom& a, const Val& x, bool* fb) {
 
 // pattern.Validate(value, pattern) (pattern.go:26-49)
 KYV_HD bool leaf_match(const View& v, const Leaf& L, const Val& x, bool* fb) {
+#ifdef KYV_EXP_LEAFTRUE
+  return true;
+#endif
   switch (L.type) {
     case L_NIL:
       switch (x.t) {

@@ -66,6 +66,22 @@ struct Ruleset {
   std::vector<PssDesc> pss;
   std::vector<uint32_t> pool;
   std::vector<std::string> templates;  // path templates: '\x01'+slot = array index, '\x02'+slot = resolved key
+  // path trie over every static lookup of every compiled pattern (kyv_layout.h "Path columns")
+  struct TrieNode {
+    uint32_t col = NONE;        // column id (key edges) 
+    uint32_t rowspace = 0;      // row space the column / this node's lookups live in
+    uint32_t star = NONE;       // "[*]" child (opens row space trie[star].rowspace)
+    std::vector<std::pair<uint32_t, uint32_t>> kids;  // (key sid, child trie node)
+  };
+  std::vector<TrieNode> trie;   // trie[0] = resource root
+  uint32_t ncols = 0, nrowspaces = 1;
+  std::vector<uint32_t> col_rowspace;
+  // runtime-compiled walk kernel (jit.cpp): generated once per ruleset, compiled on first use
+  bool jit_tried = false;
+  std::vector<uint8_t> jit_rules;   // rule k is walked by the compiled kernel
+  std::vector<char> jit_code;       // gfx950 code object
+  std::string jit_error;
+  double jit_compile_s = 0;
   // device copies (one per device, lazily uploaded)
   std::vector<void*> dev;
   ~Ruleset();
@@ -89,6 +105,8 @@ struct Batch {
   std::vector<uint32_t> inv;      // input index -> sorted position
   std::vector<uint32_t> gate;     // [kclass][gate_words] bit k: rule k can match a resource of this class
   uint32_t gate_words = 0, nclass = 0;
+  // path columns (kyv_layout.h): colv[col_off[c] + row]
+  std::vector<uint32_t> colv, col_off, rs_rows;
   std::vector<void*> dev;
   ~Batch();
 };
@@ -108,6 +126,7 @@ struct Results {
   int64_t counts[NSTATUS] = {0};
   double kernel_ms = 0, h2d_ms = 0, d2h_ms = 0;
   uint64_t alg_bytes = 0;           // CPU backend with KYV_EVAL_ACCOUNT_BYTES
+  int jit_used = 0;                 // pairs walked by the runtime-compiled kernel (1) or the interpreter only (0)
 };
 
 // compiler / flattener entry points
@@ -115,6 +134,12 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err);
 Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* nsl_json, size_t nsl_len, int threads,
                    std::string* err);
 void derive_strings(Batch& b, size_t from, int threads);
+void build_path_trie(Ruleset& rs);
+std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules);
+std::vector<char> jit_compile(const std::string& src, double* seconds);
+enum JitMode { JIT_AUTO = 0, JIT_OFF = 1, JIT_ON = 2 };
+constexpr size_t JIT_AUTO_MIN_RESOURCES = 65536;  // smaller batches are not worth a compile
+void resolve_path_columns(Batch& b, int threads);
 std::string format_path(const Ruleset& rs, const Batch& b, uint32_t tmpl, const uint16_t* idx, const uint32_t* key);
 
 }  // namespace kyv

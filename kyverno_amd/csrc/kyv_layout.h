@@ -11,7 +11,17 @@
 // columns) plus either a pattern program (pnodes/entries/leaves/atoms, traversal order fully resolved at
 // compile time, reference validate/utils.go:36-58) or a PodSecurity descriptor.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <cstdint>
+#else
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint16_t uint16_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::int64_t int64_t;
+typedef __hip_internal::size_t size_t;
+#endif
 
 namespace kyv {
 
@@ -24,7 +34,8 @@ struct Node {     // 16 bytes
   uint32_t tk;    // type (low 4 bits) | key sid << 4 (map entries) / array index << 4 (array elements)
   uint32_t a;     // MAP/ARR: first child (relative); STR: sid; INT/FLOAT: low 32 bits; BOOL: 0/1
   uint32_t b;     // MAP/ARR: child count; INT/FLOAT: high 32 bits
-  uint32_t c;     // INT: sid of decimal form; FLOAT: index into float aux table; STR: unused
+  uint32_t c;     // INT: sid of decimal form; FLOAT: index into float aux table; ARR: path-column row of
+                  // element 0 (NONE when no pattern reads inside this array); STR/MAP: unused
 };
 static_assert(sizeof(Node) == 16, "node size");
 
@@ -128,7 +139,7 @@ struct MatchBlock {
 
 // ---------------------------------------------------------------- pattern programs
 enum PKind : uint8_t { P_MAP = 0, P_ARR_MAPS = 1, P_ARR_SCALAR = 2, P_ARR_POS = 3, P_ARR_EMPTY = 4, P_LEAF = 5 };
-enum PFlag : uint8_t { PF_META = 1 };
+enum PFlag : uint8_t { PF_META = 1, PF_NEEDROW = 2 };  // PF_NEEDROW: map has an entry without a path column
 
 struct PNode {          // 16 bytes
   uint8_t kind;
@@ -144,7 +155,7 @@ enum Handler : uint8_t { H_DEFAULT = 0, H_STAR = 1, H_EQUALITY = 2, H_CONDITION 
                          H_EXISTENCE = 6, H_EXIST_BADPAT = 7 };
 enum EntryFlag : uint8_t { EF_WILD = 1 };  // key resolved at run time by metadata expansion (slot in `slot`)
 
-struct PEntry {         // 16 bytes
+struct PEntry {         // 20 bytes
   uint8_t handler;
   uint8_t flags;
   uint8_t abit;         // anchor-map bit (0xFF none)
@@ -152,7 +163,16 @@ struct PEntry {         // 16 bytes
   uint32_t key;         // sid looked up in the resource map
   uint32_t child;       // child pnode (EXISTENCE: first of n pattern maps in pool, n in `tmpl_n`)
   uint32_t tmpl;        // currentPath template (path + key + "/")
+  uint32_t col;         // path column holding this lookup's result per row of the map's row space, or NONE
 };
+
+// Path columns ("columnar JSON-path tables"). Every static key path the ruleset's patterns look up is a
+// column: for each row of its row space, the resolved node (type << COL_TYPE_SHIFT | node index relative to
+// the resource root) or NONE. Row space 0 is the resource (row = resource position in the batch); every
+// pattern array position ("[*]" in the path trie) opens a row space whose rows are the elements of all
+// resource arrays at that path, numbered batch-wide; an array node's `c` holds the row of its element 0.
+constexpr uint32_t COL_TYPE_SHIFT = 28;
+constexpr uint32_t COL_INDEX_MASK = (1u << COL_TYPE_SHIFT) - 1;
 
 enum LeafType : uint8_t { L_NIL = 0, L_BOOL = 1, L_FLOAT = 2, L_STR = 3, L_MAP = 4, L_ARR = 5 };
 struct Leaf {           // 32 bytes

@@ -8,6 +8,7 @@
 // validation.go:481-532 is modelled for the fields the checks read: a JSON type mismatch there is an error.
 #pragma once
 #include "kyv_eval.h"
+#include "kyv_walk.h"
 
 namespace kyv {
 
@@ -487,93 +488,51 @@ KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const R
 
 namespace kyv {
 
-// One (resource, rule) pair: match (+ empty OldResource retry) then dispatch (validation.go:134-183, :276-317).
-// Every lane of a wave calls this for the same rule k (`active` false for lanes past the batch end), so the
-// failing-path records can be emitted through `sink` at wave-uniform points: one emit per anyPattern
-// alternative (trip count uniform per rule), with `has` set on the lanes whose alternative failed.
-//
-// `Walker::run(v, root, walk, R, hp, rd, out)` runs one compiled pattern for the lanes with `walk` set: the host
-// instantiation is the per-lane eval_pattern (HostWalker below), the kernel's is the wave-uniform walker
-// (kyv_wave.h). It is called by every lane at the same point (the alternative loop is wave-uniform).
-struct HostWalker {
-  Stack stk;
-  KYV_HD void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp, const RuleDesc& rd,
-                  PatOut& out) {
-    out.status = ST_NONE;
-    if (walk) eval_pattern(v, root, NodeTab{R}, *hp, rd, stk, out);
-  }
-};
 
-template <class Sink, class Walker>
-KYV_HD uint8_t eval_pair(const View& v, bool active, uint32_t r, uint32_t k, Walker& wk, uint32_t* pss_fails, Sink& sink) {
+// Match + dispatch of one pair (validation.go:134-183, :276-317). Returns the verdict, or sets *walk for a
+// pattern / anyPattern pair whose verdict comes from the pattern walk (pair_walk).
+KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k, uint32_t* pss_fails, bool* walk) {
   *pss_fails = 0;
+  *walk = false;
   const RuleDesc& rd = v.rules[k];
   uint8_t st = ST_NONE;
+  if (!active) return st;
+  if (rd.match.mode == MM_NONE) return ST_FALLBACK;  // match program could not be compiled
+  const ResHeader& h = v.hdr[r];
+  NodeTab R{v.nodes + h.root};
+  LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
+  if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
+  bool nd = false;
+#ifdef KYV_EXP_NOMATCH
+  bool m = true;
+#else
+  bool m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
+  if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
+#endif
+  if (!m) return ST_NONE;
+  if (nd) return ST_ND;
+  switch (rd.kind) {
+    case RK_FALLBACK: return ST_FALLBACK;
+    case RK_PANIC: return ST_PANIC;
+    case RK_ERROR: return ST_ERROR;
+    case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
+    case RK_PATTERN: case RK_ANYPATTERN:
+      if (h.flags & RF_MAGIC) return ST_FALLBACK;
+      *walk = true;
+      return ST_NONE;
+    default: return ST_NONE;
+  }
+}
+
+// One (resource, rule) pair end to end (host backend)
+template <class Sink, class Walker>
+KYV_HD uint8_t eval_pair(const View& v, bool active, uint32_t r, uint32_t k, Walker& wk, uint32_t* pss_fails, Sink& sink) {
   bool walk = false;
-  NodeTab R{nullptr};
-  const ResHeader* hp = nullptr;
-  if (active) {
-    if (rd.match.mode == MM_NONE) {
-      st = ST_FALLBACK;  // match program could not be compiled
-    } else {
-      hp = &v.hdr[r];
-      const ResHeader& h = *hp;
-      R = NodeTab{v.nodes + h.root};
-      LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
-      if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
-      bool nd = false;
-      bool m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
-      if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
-      if (!m) st = ST_NONE;
-      else if (nd) st = ST_ND;
-      else switch (rd.kind) {
-        case RK_FALLBACK: st = ST_FALLBACK; break;
-        case RK_PANIC: st = ST_PANIC; break;
-        case RK_ERROR: st = ST_ERROR; break;
-        case RK_PSS: st = eval_pss(v, v.pss[rd.root], R, h, pss_fails); break;
-        case RK_PATTERN: case RK_ANYPATTERN:
-          if (h.flags & RF_MAGIC) st = ST_FALLBACK;
-          else walk = true;
-          break;
-        default: st = ST_NONE;
-      }
-    }
-  }
+  uint8_t st = pair_dispatch(v, active, r, k, pss_fails, &walk);
+  const RuleDesc& rd = v.rules[k];
   if (rd.kind != RK_PATTERN && rd.kind != RK_ANYPATTERN) return st;
-  uint32_t nalts = rd.kind == RK_PATTERN ? 1 : rd.nalts;  // uniform across the wave
-  uint32_t nfail = 0, nskip = 0;
-  for (uint32_t a = 0; a < nalts; a++) {
-    PatOut po;
-    wk.run(v, rd.kind == RK_PATTERN ? rd.root : v.pool[rd.root + a], walk, R.p, hp, rd, po);
-    bool rec = false;
-    if (walk) {
-      switch (po.status) {
-        case ST_PASS: st = (uint8_t)(ST_PASS | ((a < 30 ? a : 30) << 3)); walk = false; break;  // alt index for the message
-        case ST_SKIP: nskip++; break;
-        case ST_FAIL: case ST_ERROR:
-          if (rd.kind == RK_PATTERN && po.status == ST_ERROR) { st = ST_ERROR; walk = false; break; }
-          rec = true;
-          nfail++;
-          break;
-        default: st = po.status; walk = false;  // fallback / panic / nondeterministic at this point of the walk
-      }
-    }
-    FailRec fr;
-    if (rec) {
-      fr.res = r; fr.rule = k; fr.tmpl = po.status == ST_FAIL ? po.tmpl : NONE; fr.alt = (uint16_t)a; fr.nalt = 0;
-      for (int i = 0; i < MAX_IDX; i++) fr.idx[i] = (uint16_t)(po.idx >> (16 * i));
-      fr.key[0] = po.key0;
-      fr.key[1] = po.key1;
-    }
-    sink.emit(rec, fr);
-  }
-  if (walk) {
-    if (rd.kind == RK_PATTERN) st = nfail ? ST_FAIL : ST_SKIP;
-    else if (nfail) st = ST_FAIL;
-    else if (nskip) st = ST_SKIP;
-    else st = (uint8_t)(ST_PASS | (31 << 3));  // empty anyPattern list: pass with the rule message (validation.go:701)
-  }
-  return st;
+  uint8_t ws = pair_walk(v, rd, walk, r, k, wk, sink);
+  return walk ? ws : st;
 }
 
 }  // namespace kyv

@@ -12,12 +12,15 @@
 //    mask and keeps its per-lane return value until the frame pops;
 //  * the top frame lives in registers; deeper frames are spilled to LDS only on push/pop: the uniform part
 //    once per wave, the per-lane part (child range + array state) lane-strided and conflict-free;
-//  * resource node rows are read with global (not flat) loads, map keys by binary search on the key dword.
+//  * map lookups of static key paths read the batch's path columns (kyv_layout.h): one coalesced 4-byte
+//    load per lane that also carries the child's type, so most maps are entered without touching their row;
+//    dynamic keys (metadata wildcards) binary-search the key-sorted children; rows use global (not flat) loads.
 //
 // Every per-lane side effect (return value, anchor map, array indices, metadata keys) happens only for lanes
 // inside the step's mask, so each lane sees exactly the sequence of operations the per-lane walk performs.
 #pragma once
 #include "kyv_eval.h"
+#include "kyv_walk.h"
 
 namespace kyv {
 
@@ -28,11 +31,12 @@ namespace kyv {
 template <class T>
 __device__ __forceinline__ T sld(const T* p) {
   static_assert(sizeof(T) % 4 == 0, "sld: 4-byte multiple");
-  T out;
-  uint32_t* o = (uint32_t*)&out;
+  uint32_t w[sizeof(T) / 4];
   const KYV_AS_CONST uint32_t* q = (const KYV_AS_CONST uint32_t*)p;
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); i++) o[i] = q[i];
+  for (int i = 0; i < (int)(sizeof(T) / 4); i++) w[i] = q[i];
+  T out;
+  __builtin_memcpy(&out, w, sizeof(T));  // no type punning through uint32_t* (strict aliasing)
   return out;
 }
 __device__ __forceinline__ uint32_t sld32(const uint32_t* p) { return *(const KYV_AS_CONST uint32_t*)p; }
@@ -63,11 +67,33 @@ __device__ __forceinline__ uint32_t wmap_find(const Node* R, uint32_t a, uint32_
   return NONE;
 }
 
-__device__ __forceinline__ Val wvalue_of(const View& v, const Node* R, uint32_t rn) {
+constexpr uint32_t T_UNK = 0xE;  // node type not known yet (row not loaded)
+
+__device__ __forceinline__ uint32_t gld32(const uint32_t* p) { return *(const KYV_AS_GLOBAL uint32_t*)p; }
+
+// Column entry of one map-entry lookup (the device entry table holds absolute column offsets in `col`)
+__device__ __forceinline__ uint32_t wcol(const View& v, const PEntry& E, bool al, uint32_t row) {
+  return al ? gld32(v.colv + (size_t)E.col + row) : NONE;
+}
+__device__ __forceinline__ uint32_t col_decode(uint32_t enc, uint32_t* ctype) {
+  if (enc == NONE) { *ctype = T_UNK; return NONE; }
+  *ctype = enc >> COL_TYPE_SHIFT;
+  return enc & COL_INDEX_MASK;
+}
+// resourceMap[key] for one map entry: a path-column read (one coalesced 4-B load per lane, node type included)
+// when the compiler gave the entry a column, else a binary search over the map's key-sorted children
+__device__ __forceinline__ uint32_t wlookup(const View& v, const PEntry& E, bool al, const Node* R, uint32_t a, uint32_t b,
+                                            uint32_t row, const Keys& keys, uint32_t* ctype) {
+  *ctype = T_UNK;
+  if (!al) return NONE;
+  if (E.col != NONE) return col_decode(wcol(v, E, al, row), ctype);
+  uint32_t key = (E.flags & EF_WILD) ? keys.get(E.slot) : E.key;
+  return wmap_find(R, a, b, key);
+}
+
+__device__ __forceinline__ Val wvalue_node(const View& v, Node n) {
   Val x;
   x.wsid = NONE; x.nsid = NONE; x.sid = NONE; x.i = 0; x.f = 0;
-  if (rn == NONE) { x.t = 0xFF; x.nsid = SID_ZERO; return x; }
-  Node n = gnode(R + rn);
   x.t = node_type(n);
   switch (x.t) {
     case N_NULL: x.nsid = SID_ZERO; break;
@@ -77,8 +103,8 @@ __device__ __forceinline__ Val wvalue_of(const View& v, const Node* R, uint32_t 
     case N_FLOAT: {
       uint64_t bits = ((uint64_t)n.b << 32) | n.a;
       x.f = __builtin_bit_cast(double, bits);
-      x.wsid = v.faux[n.c].sid_E;
-      x.nsid = v.faux[n.c].sid_F;
+      x.wsid = gld32(&v.faux[n.c].sid_E);
+      x.nsid = gld32(&v.faux[n.c].sid_F);
       break;
     }
     case N_STR: x.sid = n.a; x.wsid = n.a; x.nsid = n.a; break;
@@ -86,11 +112,117 @@ __device__ __forceinline__ Val wvalue_of(const View& v, const Node* R, uint32_t 
   }
   return x;
 }
+__device__ __forceinline__ Val wvalue_absent() {
+  Val x;
+  x.t = 0xFF; x.wsid = NONE; x.nsid = SID_ZERO; x.sid = NONE; x.i = 0; x.f = 0;
+  return x;
+}
+__device__ __forceinline__ Val wvalue_of(const View& v, const Node* R, uint32_t rn) {
+  return rn == NONE ? wvalue_absent() : wvalue_node(v, gnode(R + rn));
+}
 
-// per-lane part of a spilled frame: child range of the map / array node + array-frame state
+// ---------------------------------------------------------------- leaves (pattern.go:26-321), wave form
+// The leaf / atom program is wave-uniform (scalar loads); only the value side is per lane. Same evaluation
+// order as leaf_match / atom_eval (kyv_eval.h): a lane evaluates atom k of group g exactly when no earlier
+// group matched and every earlier atom of group g matched, so the fallback flag is raised identically.
+__device__ __forceinline__ uint8_t gld8(const uint8_t* p) { return *(const KYV_AS_GLOBAL uint8_t*)p; }
+__device__ __forceinline__ bool wbytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) if (gld8(a + i) != gld8(b + i)) return false;
+  return true;
+}
+__device__ __forceinline__ bool wglob(const View& v, uint8_t kind, uint32_t pat, uint32_t lit, uint32_t s) {
+  switch (kind) {
+    case G_ANY: return true;
+    case G_EMPTY: return s == SID_EMPTY;
+    case G_EXACT: return s == pat;
+    case G_NONEMPTY: return gld32(v.str_len + s) > 0;
+    case G_PREFIX: case G_SUFFIX: case G_CONTAINS: {
+      const uint32_t ln = gld32(v.str_len + lit), sn = gld32(v.str_len + s);
+      if (ln > sn) return false;
+      const uint8_t* a = v.heap + gld32(v.str_off + s);
+      const uint8_t* b = v.heap + gld32(v.str_off + lit);
+      if (kind == G_PREFIX) return wbytes_eq(a, b, ln);
+      if (kind == G_SUFFIX) return wbytes_eq(a + (sn - ln), b, ln);
+      for (uint32_t i = 0; i + ln <= sn; i++) if (wbytes_eq(a + i, b, ln)) return true;
+      return false;
+    }
+    default: return glob_runes(sbytes(v, pat), v.str_len[pat], sbytes(v, s), v.str_len[s]);
+  }
+}
+__device__ __forceinline__ bool watom_simple(const View& v, const Atom& a, const Val& x, bool* fb) {
+  if ((a.flags & AF_DUR) && x.nsid != NONE && (gld32(v.str_flags + x.nsid) & SF_DUR)) {
+    int64_t d = *(const KYV_AS_GLOBAL int64_t*)(v.str_dur + x.nsid);
+    if (cmp_op(a.op, d < a.dur ? -1 : (d > a.dur ? 1 : 0))) return true;
+  }
+  if ((a.flags & AF_QTY) && x.nsid != NONE) {
+    uint32_t f = gld32(v.str_flags + x.nsid);
+    if (f & SF_QTY_BIG) { *fb = true; return false; }
+    if (f & SF_QTY) {
+      const KYV_AS_GLOBAL int64_t* q = (const KYV_AS_GLOBAL int64_t*)(v.str_qty + 2 * (size_t)x.nsid);
+      int c = cmp128(q[1], (uint64_t)q[0], a.qhi, (uint64_t)a.qlo);
+      if (cmp_op(a.op, c)) return true;
+    }
+  }
+  if ((a.op == A_EQ || a.op == A_NE) && x.wsid != NONE) {
+    bool r = wglob(v, a.glob, a.pat, a.lit, x.wsid);
+    return a.op == A_NE ? !r : r;
+  }
+  return false;
+}
+// pattern.Validate(value, pattern) for the lanes with `go`
+__device__ __forceinline__ bool wleaf_match(const View& v, const Leaf& L, bool go, const Val& x, bool* fb) {
+  switch (L.type) {
+    case L_NIL:
+      switch (x.t) {
+        case 0xFF: case N_NULL: case N_FALSE: return true;
+        case N_INT: return x.i == 0;
+        case N_FLOAT: return x.f == 0.0;
+        case N_STR: return x.sid == SID_EMPTY;
+        default: return false;
+      }
+    case L_BOOL: return (x.t == N_TRUE && L.bval) || (x.t == N_FALSE && !L.bval);
+    case L_FLOAT:
+      switch (x.t) {
+        case N_INT: return L.fint && L.fi == x.i;
+        case N_FLOAT: return x.f == L.f;
+        case N_STR: return go && (gld32(v.str_flags + x.sid) & SF_FLOAT) &&
+                           *(const KYV_AS_GLOBAL double*)(v.str_f64 + x.sid) == L.f;
+        default: return false;
+      }
+    case L_STR: {
+      bool done = x.t == N_STR && x.sid == L.exact;
+      for (uint32_t g = 0; g < L.ngroups; g++) {
+        const uint32_t a0 = sld32(v.pool + L.groups + 2 * g), na = sld32(v.pool + L.groups + 2 * g + 1);
+        bool all = go && !done;
+        for (uint32_t k = 0; k < na; k++) {
+          const Atom A = sld(v.atoms + a0 + k);
+          if (A.op == A_RANGE_IN || A.op == A_RANGE_OUT) {
+            const Atom s0 = sld(v.atoms + A.sub), s1 = sld(v.atoms + A.sub + 1);
+            if (all) {
+              bool r0 = watom_simple(v, s0, x, fb);
+              all = A.op == A_RANGE_IN ? (r0 && watom_simple(v, s1, x, fb)) : (r0 || watom_simple(v, s1, x, fb));
+            }
+          } else if (A.op == A_FALSE) {
+            all = false;
+          } else if (all) {
+            all = watom_simple(v, A, x, fb);
+          }
+        }
+        if (all) done = true;
+      }
+      return done;
+    }
+    case L_MAP: return x.t == N_MAP;
+    default: return false;
+  }
+}
+
+// per-lane part of a spilled frame: child range of the map / array node + array-frame state + column row
 struct LaneFrame {
   uint32_t a;     // first child row
   uint32_t bst;   // child count (low 16) | FrameSt bits << 16
+  uint32_t row;   // map: its row in the path-column row space; array: row of element 0
+  uint32_t pad;
 };
 // uniform part of a spilled frame
 struct UFrame {
@@ -100,6 +232,9 @@ struct UFrame {
 };
 static_assert(sizeof(UFrame) == 48, "UFrame");
 
+#ifdef KYV_EXP_STEPS
+__device__ unsigned long long kyv_exp_steps;
+#endif
 struct WaveWalker {
   LaneFrame* lf;   // LDS, [cap][64]
   UFrame* uf;      // LDS, [cap]
@@ -120,6 +255,10 @@ struct WaveWalker {
     uint64_t dead = 0;
     uint64_t emask = wballot(walk);
     if (!emask) { out.status = ST_NONE; return; }
+#ifdef KYV_EXP_NOWALK
+    out.status = walk ? ST_PASS : ST_NONE;
+    return;
+#endif
     const uint32_t meta_base = rd.meta_sites;
 
     int sp = 0;
@@ -127,12 +266,14 @@ struct WaveWalker {
     uint32_t t_kind = 0, t_pn = 0, t_i = 0, t_j = 0;
     uint64_t t_alive = 0, t_cmask = 0, t_search = 0;
     // top frame (per lane)
-    uint32_t t_a = 0, t_b = 0, t_st = 0;
+    uint32_t t_a = 0, t_b = 0, t_st = 0, t_row = 0;
 
     int action = 0;
     uint32_t epn = root, ern = 0;
+    uint32_t etype = T_UNK;        // per lane: type of the node being entered, when a column supplied it
+    uint32_t erow = hp ? hp - v.hdr : 0;  // per lane: column row of the node being entered (root: the resource)
 
-#define KYV_PUSH(KIND, PN, ALIVE, A, B)                                                     \
+#define KYV_PUSH(KIND, PN, ALIVE, A, B, ROW)                                                   \
   do {                                                                                      \
     if (sp > 0) {                                                                           \
       if (lane == 0) {                                                                      \
@@ -141,11 +282,11 @@ struct WaveWalker {
         u.alive = t_alive; u.cmask = t_cmask; u.search = t_search;                          \
       }                                                                                     \
       LaneFrame& l = lf[(uint32_t)(sp - 1) * 64u + lane];                                   \
-      l.a = t_a; l.bst = (t_b & 0xFFFFu) | (t_st << 16);                                   \
+      l.a = t_a; l.bst = (t_b & 0xFFFFu) | (t_st << 16); l.row = t_row;                  \
     }                                                                                       \
     t_kind = (KIND); t_pn = (PN); t_i = 0; t_j = 0;                                         \
     t_alive = (ALIVE); t_cmask = 0; t_search = (ALIVE);                                     \
-    t_a = (A); t_b = (B); t_st = 0;                                                         \
+    t_a = (A); t_b = (B); t_st = 0; t_row = (ROW);                                          \
     sp++;                                                                                   \
   } while (0)
 
@@ -157,18 +298,29 @@ struct WaveWalker {
       t_kind = uni(u.kind); t_pn = uni(u.pn); t_i = uni(u.i); t_j = uni(u.j);               \
       t_alive = uni64(u.alive); t_cmask = uni64(u.cmask); t_search = uni64(u.search);       \
       LaneFrame l = lf[(uint32_t)(sp - 1) * 64u + lane];                                    \
-      t_a = l.a; t_b = l.bst & 0xFFFFu; t_st = l.bst >> 16;                                 \
+      t_a = l.a; t_b = l.bst & 0xFFFFu; t_st = l.bst >> 16; t_row = l.row;                  \
     }                                                                                       \
   } while (0)
 
+#ifdef KYV_EXP_STEPS
+    uint32_t nsteps = 0;
+#endif
     for (;;) {
+#ifdef KYV_EXP_STEPS
+      nsteps++;
+#endif
       if (action == 0) {
         // ---------------------------------------------------------------- enter epn for lanes in emask
         const PNode P = sld(v.pn + epn);
         const bool in = (emask & lbit) != 0;
         uint32_t rt = 0xFF;
         Node rnode{0, 0, 0, 0};
-        if (in && ern != NONE) { rnode = gnode(R + ern); rt = node_type(rnode); }
+        // maps whose entries all have path columns never need their own row (type came with the column)
+        const bool needrow = P.kind != P_MAP || (P.flags & PF_NEEDROW);
+        if (in && ern != NONE) {
+          if (needrow || etype == T_UNK) { rnode = gnode(R + ern); rt = node_type(rnode); }
+          else rt = etype;
+        }
         if (P.kind == P_MAP) {
           uint64_t bad = wballot(in && rt != N_MAP);
           if (bad & lbit) ret = mkerr(EC_NONE, 0, P.tmpl);
@@ -177,13 +329,13 @@ struct WaveWalker {
             // AnchorMap.CheckAnchorInResource (anchormap.go:30-44)
             for (uint32_t e = 0; e < P.n; e++) {
               const PEntry E = sld(v.pe + P.first + e);
-              if (E.abit != 0xFF && (go & lbit)) {
-                uint64_t b = 1ull << E.abit;
-                seen |= b;
-                if (!(found & b)) {
-                  uint32_t key = (E.flags & EF_WILD) ? keys.get(E.slot) : E.key;
-                  if (wmap_find(R, rnode.a, rnode.b, key) != NONE) found |= b;
-                }
+              if (E.abit != 0xFF) {
+                const uint64_t b = 1ull << E.abit;
+                const bool chk = (go & lbit) && !(found & b);
+                uint32_t ct, c;
+                if (go & lbit) seen |= b;
+                c = wlookup(v, E, chk, R, rnode.a, rnode.b, erow, keys, &ct);
+                if (c != NONE) found |= b;
               }
             }
             if (P.flags & PF_META) {
@@ -201,7 +353,7 @@ struct WaveWalker {
             }
           }
           if (go) {
-            KYV_PUSH(F_MAP, epn, go, rnode.a, rnode.b);
+            KYV_PUSH(F_MAP, epn, go, rnode.a, rnode.b, erow);
             action = 1;
           } else {
             action = 2;
@@ -223,7 +375,7 @@ struct WaveWalker {
           const bool each = rt == N_ARR;
           const uint32_t cnt = go ? (each ? rnode.b : 1u) : 0u;
           bool fb = false, okv = true;
-          for (uint32_t i = 0; i < cnt && okv; i++) okv = leaf_match(v, L, wvalue_of(v, R, each ? rnode.a + i : ern), &fb);
+          for (uint32_t i = 0; i < cnt && okv; i++) okv = wleaf_match(v, L, true, wvalue_of(v, R, each ? rnode.a + i : ern), &fb);
           uint64_t d = wballot(go && fb);
           if (d & lbit) ost = ST_FALLBACK;
           dead |= d;
@@ -246,7 +398,7 @@ struct WaveWalker {
           go = 0;
         }
         if (go) {
-          KYV_PUSH(P.kind == P_ARR_MAPS ? F_AOM : F_POS, epn, go, rnode.a, rnode.b);
+          KYV_PUSH(P.kind == P_ARR_MAPS ? F_AOM : F_POS, epn, go, rnode.a, rnode.b, rnode.c);
           action = 1;
         } else {
           action = 2;
@@ -268,11 +420,8 @@ struct WaveWalker {
           const PEntry E = sld(v.pe + P.first + t_i);
           t_i++;
           const bool al = (alive & lbit) != 0;
-          uint32_t c = NONE;
-          if (al) {
-            uint32_t key = (E.flags & EF_WILD) ? keys.get(E.slot) : E.key;
-            c = wmap_find(R, t_a, t_b, key);
-          }
+          uint32_t ct, c;
+          c = wlookup(v, E, al, R, t_a, t_b, t_row, keys, &ct);
           t_alive = alive;
           switch (E.handler) {
             case H_NEGATION: {
@@ -283,7 +432,7 @@ struct WaveWalker {
             }
             case H_EQUALITY: case H_GLOBAL: {
               uint64_t ent = wballot(al && c != NONE);
-              if (ent) { t_cmask = ent; emask = ent; epn = E.child; ern = c; action = 0; }
+              if (ent) { t_cmask = ent; emask = ent; epn = E.child; ern = c; etype = ct; erow = t_row; action = 0; }
               continue;
             }
             case H_CONDITION: {
@@ -291,12 +440,12 @@ struct WaveWalker {
               uint64_t absent = alive & ~pres;
               if (absent & lbit) ret = mkerr(EC_COND, PH_COND, E.tmpl);
               t_alive &= ~absent;
-              if (pres) { t_cmask = pres; emask = pres; epn = E.child; ern = c; action = 0; }
+              if (pres) { t_cmask = pres; emask = pres; epn = E.child; ern = c; etype = ct; erow = t_row; action = 0; }
               continue;
             }
             case H_STAR: {
               bool isnull = false;
-              if (al && c != NONE) isnull = node_type(gnode(R + c)) == N_NULL;
+              if (al && c != NONE) isnull = (ct != T_UNK ? ct : node_type(gnode(R + c))) == N_NULL;
               uint64_t badl = wballot(al && (c == NONE || isnull));
               if (badl & lbit) ret = mkerr(EC_NONE, 0, P.tmpl);  // dh.path: the parent path
               t_alive &= ~badl;
@@ -318,12 +467,12 @@ struct WaveWalker {
                   continue;
                 }
                 t_cmask = ex;
-                KYV_PUSH(F_EXIST, P.first + t_i - 1, ex, cn.a, cn.b);
+                KYV_PUSH(F_EXIST, P.first + t_i - 1, ex, cn.a, cn.b, cn.c);
               }
               continue;
             }
             default: {  // H_DEFAULT: recurse on resourceMap[k] (absent -> nil)
-              t_cmask = alive; emask = alive; epn = E.child; ern = c; action = 0;
+              t_cmask = alive; emask = alive; epn = E.child; ern = c; etype = ct; erow = t_row; action = 0;
               continue;
             }
           }
@@ -348,6 +497,8 @@ struct WaveWalker {
               out.idx = (out.idx & ~(0xFFFFull << sh)) | ((uint64_t)t_i << sh);
             }
             ern = t_a + t_i;
+            erow = t_row == NONE ? NONE : t_row + t_i;
+            etype = T_UNK;
           }
           epn = t_kind == F_AOM ? P.first : sld32(v.pool + P.first + t_i);
           t_i++;
@@ -381,7 +532,11 @@ struct WaveWalker {
             continue;
           }
           epn = sld32(v.pool + E.child + 1 + t_j);
-          if (search & lbit) ern = t_a + t_i;
+          if (search & lbit) {
+            ern = t_a + t_i;
+            erow = t_row == NONE ? NONE : t_row + t_i;
+            etype = T_UNK;
+          }
           t_i++;
           t_search = search;
           t_cmask = search;
@@ -421,6 +576,9 @@ struct WaveWalker {
     }
 #undef KYV_PUSH
 #undef KYV_POP
+#ifdef KYV_EXP_STEPS
+    if (lane == 0) atomicAdd(&kyv_exp_steps, (unsigned long long)nsteps);
+#endif
 
     out.key0 = keys.k0;
     out.key1 = keys.k1;
@@ -434,5 +592,133 @@ struct WaveWalker {
     out.status = ret.tmpl == NONE ? ST_ERROR : ST_FAIL;
   }
 };
+
+// ---------------------------------------------------------------- runtime-compiled walkers (jit.cpp)
+// Per-lane state of one compiled pattern walk. The generated code is the per-lane recursion of eval_pattern
+// (kyv_eval.h) unrolled over one pattern: one inlined function per pattern node, arrays as loops, errors as
+// return values; `ost` != ST_NONE ends the walk with that status (fallback / panic / nondeterministic).
+struct JW {
+  const View& v;
+  const Node* R;
+  const ResHeader* hp;
+  uint64_t seen, found;  // AnchorMap (anchormap.go)
+  Keys keys;             // resolved metadata wildcard keys (wildcards.go)
+  uint64_t idx;          // array indices of the failing path
+  uint32_t mbase;        // rule's first metadata-expansion site
+  uint8_t ost;
+};
+// one simple comparison with the atom's operator, flags and glob class as template constants (the generated
+// leaf code instantiates exactly the branches watom_simple would take for that atom)
+template <uint8_t OP, uint8_t FLAGS, uint8_t GLOB>
+__device__ __forceinline__ bool jatom(const View& v, const Val& x, uint32_t pat, uint32_t lit, int64_t dur, int64_t qlo,
+                                      int64_t qhi, bool* fb) {
+  if ((FLAGS & AF_DUR) && x.nsid != NONE && (gld32(v.str_flags + x.nsid) & SF_DUR)) {
+    int64_t d = *(const KYV_AS_GLOBAL int64_t*)(v.str_dur + x.nsid);
+    if (cmp_op(OP, d < dur ? -1 : (d > dur ? 1 : 0))) return true;
+  }
+  if ((FLAGS & AF_QTY) && x.nsid != NONE) {
+    uint32_t f = gld32(v.str_flags + x.nsid);
+    if (f & SF_QTY_BIG) { *fb = true; return false; }
+    if (f & SF_QTY) {
+      const KYV_AS_GLOBAL int64_t* q = (const KYV_AS_GLOBAL int64_t*)(v.str_qty + 2 * (size_t)x.nsid);
+      if (cmp_op(OP, cmp128(q[1], (uint64_t)q[0], qhi, (uint64_t)qlo))) return true;
+    }
+  }
+  if ((OP == A_EQ || OP == A_NE) && x.wsid != NONE) {
+    bool r = wglob(v, GLOB, pat, lit, x.wsid);
+    return OP == A_NE ? !r : r;
+  }
+  return false;
+}
+// lookup through a path column: the device entry table holds the column's absolute offset
+__device__ __forceinline__ uint32_t jcol(const JW& w, uint32_t e, uint32_t row, uint32_t* ct) {
+  const uint32_t off = sld32(&w.v.pe[e].col);
+  return col_decode(row == NONE ? NONE : gld32(w.v.colv + (size_t)off + row), ct);
+}
+// MatchPattern's classification (validate.go:31-56), as at the end of eval_pattern
+__device__ __forceinline__ void jfinish(const JW& w, const Ret& ret, PatOut& out) {
+  out.key0 = w.keys.k0;
+  out.key1 = w.keys.k1;
+  out.idx = w.idx;
+  out.tmpl = NONE;
+  if (w.ost != ST_NONE) { out.status = w.ost; return; }
+  if (!ret.err) { out.status = ST_PASS; return; }
+  if (ret_is_skip(ret)) { out.status = ST_SKIP; return; }
+  if (ret_is_neg(ret)) { out.status = ST_FAIL; out.tmpl = ret.tmpl; return; }
+  if (w.seen & ~w.found) { out.status = ST_ERROR; return; }
+  out.tmpl = ret.tmpl;
+  out.status = ret.tmpl == NONE ? ST_ERROR : ST_FAIL;
+}
+
+// ---------------------------------------------------------------- walk-phase kernel pieces (shared by the
+// interpreted walk_kernel and the runtime-compiled per-ruleset kernels of jit.cpp)
+constexpr int WAVE = 64;
+struct DevOut {
+  uint8_t* status;         // [rule][res]
+  uint32_t* pss_fails;     // [pss rule slot][res]
+  const uint32_t* pss_slot;// rule -> pss slot or NONE
+  FailRec* recs;
+  uint32_t* nrecs;         // global record counter
+  uint32_t max_recs;
+  unsigned long long* counts;  // [rule][NSTATUS]
+  uint32_t rule_lo, rule_hi;   // rule range handled by this launch
+};
+
+// Failing-path records of one wave, appended with one atomic per emit point that has any record.
+struct WaveSink {
+  FailRec* recs;
+  uint32_t* n;
+  uint32_t max;
+  __device__ __forceinline__ void emit(bool has, const FailRec& f) {
+    unsigned long long m = __ballot(has);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & (WAVE - 1);
+    const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(n, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (has) {
+      uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+      if (at < max) recs[at] = f;
+    }
+  }
+};
+
+// per-rule status counts: wave ballots -> one atomic per status present
+__device__ __forceinline__ void count_status(unsigned long long* counts, uint32_t k, bool active, uint8_t st) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  for (int s = 0; s < NSTATUS; s++) {
+    unsigned long long m = __ballot(active && (st & 7) == s);
+    if (m && lane == 0) atomicAdd(&counts[(size_t)k * NSTATUS + s], (unsigned long long)__popcll(m));
+  }
+}
+
+
+// Grid-stride over 64-pair chunks of the per-rule work lists: rule k owns chunks [chunk_pre[k], chunk_pre[k+1]),
+// so every wave walks ONE rule over 64 resources; verdict bytes, records and counts as in match_kernel.
+template <class Walker>
+__device__ __forceinline__ void walk_chunks(const View& v, DevOut o, const uint32_t* __restrict__ items,
+                                            const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ item_cnt,
+                                            const uint32_t* __restrict__ chunk_pre, Walker& wk) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint32_t nr = v.nrules;
+  const uint32_t total = sld32(chunk_pre + nr);
+  WaveSink sink{o.recs, o.nrecs, o.max_recs};
+  for (uint32_t c = blockIdx.x; c < total; c += gridDim.x) {
+    uint32_t lo = 0, hi = nr;  // rule k: chunk_pre[k] <= c < chunk_pre[k + 1]
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (sld32(chunk_pre + mid) <= c) lo = mid; else hi = mid;
+    }
+    const uint32_t k = lo;
+    const uint32_t i = (c - sld32(chunk_pre + k)) * WAVE + lane;
+    const bool active = i < sld32(item_cnt + k);
+    const uint32_t r = active ? items[(size_t)sld32(item_off + k) + i] : 0u;
+    const RuleDesc rd = sld(v.rules + k);
+    const uint8_t st = pair_walk(v, rd, active, r, k, wk, sink);
+    if (active) o.status[(size_t)k * v.nres + r] = st;
+    count_status(o.counts, k, active, st);
+  }
+}
 
 }  // namespace kyv

@@ -49,6 +49,21 @@ class Ruleset:
             self.policies.append({"name": pi.name.decode(), "namespace": pi.namespace_.decode(), "first_rule": pi.first_rule,
                                   "nrules": pi.nrules, "apply_one": bool(pi.apply_one), "scored_false": bool(pi.scored_false)})
 
+    def jit_source(self):
+        """(generated HIP source of the ruleset's walk kernel, number of rules it covers)"""
+        L = K.lib()
+        n = ctypes.c_uint32()
+        size = L.kyv_ruleset_jit_source(self.h, None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(size + 1)
+        L.kyv_ruleset_jit_source(self.h, buf, size + 1, ctypes.byref(n))
+        return buf.value.decode(), n.value
+
+    def jit_compile(self):
+        """hipRTC-compile the walk kernel for gfx950 (no GPU needed) -> (seconds, code-object bytes)"""
+        secs, size = ctypes.c_double(), ctypes.c_size_t()
+        K.check(K.lib().kyv_ruleset_jit_compile(self.h, ctypes.byref(secs), ctypes.byref(size)))
+        return secs.value, size.value
+
     def __del__(self):
         if getattr(self, "h", None):
             K.lib().kyv_ruleset_free(self.h)
@@ -86,6 +101,7 @@ class Results:
         self.counts = {K.STATUS_NAMES[s]: L.kyv_results_count(h, s) for s in range(8)}
         self.kernel_ms = L.kyv_results_kernel_ms(h)
         self.alg_bytes = L.kyv_results_alg_bytes(h)
+        self.jit = bool(L.kyv_results_jit(h))
         self.status = None
         if copied:
             nr, nres = len(ruleset.rules), batch.n
@@ -119,10 +135,14 @@ class Results:
             self.h = None
 
 
-def evaluate(ruleset, batch, backend="gpu", device=0, iterations=1, threads=0, copy_back=True, account_bytes=False):
-    """Evaluate every (resource, rule) pair. backend="gpu" is the product path; "cpu" must be explicit."""
+def evaluate(ruleset, batch, backend="gpu", device=0, iterations=1, threads=0, copy_back=True, account_bytes=False,
+             jit=None):
+    """Evaluate every (resource, rule) pair. backend="gpu" is the product path; "cpu" must be explicit.
+    jit: None = library default (runtime-compiled walk kernel for batches >= 65536 resources), True / False force."""
     L = K.lib()
     flags = (0 if copy_back else K.EVAL_NO_COPYBACK) | (K.EVAL_ACCOUNT_BYTES if account_bytes else 0)
+    if jit is not None:
+        flags |= K.EVAL_JIT_ON if jit else K.EVAL_JIT_OFF
     opts = K.EvalOpts(K.KYV_ABI_VERSION, K.BACKEND_GPU if backend == "gpu" else K.BACKEND_CPU, device, iterations,
                       threads, flags)
     h = ctypes.c_void_p()

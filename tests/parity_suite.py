@@ -49,9 +49,9 @@ def run_pss_goldens(backend):
     return n
 
 
-def run_synthetic(backend, policies, n, seed, kind="mixed", edge=True):
+def run_synthetic(backend, policies, n, seed, kind="mixed", edge=True, jit=None):
     from kyverno_amd import synth
     docs, nsl = (synth.mixed if kind == "mixed" else synth.pods)(n, seed=seed, edge=edge)
-    st, res = PU.compare(policies, docs, nsl, backend=backend)
+    st, res = PU.compare(policies, docs, nsl, backend=backend, jit=jit)
     assert_clean("synthetic/%s/%d" % (kind, seed), st)
     return st, res

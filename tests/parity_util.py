@@ -24,11 +24,11 @@ def oracle_pairs(policies, resources, ns_labels):
     return out
 
 
-def compare(policies, resources, ns_labels=None, backend="gpu", check_messages=True, max_report=20):
+def compare(policies, resources, ns_labels=None, backend="gpu", check_messages=True, max_report=20, jit=None):
     """Returns a stats dict; raises AssertionError on verdict/path/message mismatches."""
     rs = E.Ruleset(policies)
     b = E.Batch(rs, resources, ns_labels)
-    res = E.evaluate(rs, b, backend=backend)
+    res = E.evaluate(rs, b, backend=backend, **({} if backend != "gpu" else {"jit": jit}))
     ora = oracle_pairs(policies, resources, ns_labels or {})
     st = res.status
     stats = {"pairs": 0, "matched": 0, "compared": 0, "fallback": 0, "nd": 0, "messages": 0, "unsupported": 0}

@@ -88,3 +88,11 @@ def test_empty_and_tiny_batches_gpu():
         assert b.n == len(docs)
         if b.n:
             assert np.array_equal(g.raw, c.raw)
+
+
+def test_c3_synthetic_gpu_jit():
+    """Runtime-compiled walk kernel (forced on a small batch) against the oracle: bit-exact verdicts, paths,
+    messages on the C3 corpus with edge cases."""
+    st, res = S.run_synthetic("gpu", cases.best_practices() + cases.chart_restricted(), 3000, seed=41, jit=True)
+    assert res.jit
+    assert st["compared"] > 50000
