@@ -50,7 +50,8 @@ EXPORTS = [
     "kyv_ruleset_rule_info", "kyv_ruleset_policy_info", "kyv_batch_build", "kyv_batch_free",
     "kyv_batch_num_resources", "kyv_batch_stats_get", "kyv_eval", "kyv_results_free", "kyv_results_status",
     "kyv_results_count", "kyv_results_kernel_ms", "kyv_results_alg_bytes", "kyv_results_message", "kyv_results_path",
-    "kyv_results_pss_mask", "kyv_last_error", "kyv_version",
+    "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
+    "kyv_ruleset_jit_compile",
 ]
 
 _lib = None

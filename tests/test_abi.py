@@ -65,3 +65,17 @@ def test_batch_for_other_ruleset_rejected():
     batch = E.Batch(a, [{"kind": "Pod", "metadata": {"name": "x"}}])
     with pytest.raises(K.KyvError):
         E.evaluate(b, batch, backend="cpu")
+
+
+def test_jit_walk_kernel_compiles_for_gfx950():
+    """The runtime-compiled walk kernel of a ruleset: generated source covers the pattern rules and hipRTC
+    compiles it for gfx950 without a GPU (the GPU tests then check its verdicts against the oracle)."""
+    import cases
+    from kyverno_amd import engine as E
+    rs = E.Ruleset(cases.best_practices() + cases.quirk_policies())
+    src, n = rs.jit_source()
+    npat = sum(1 for r in rs.rules if r["kind"] in ("pattern", "anyPattern"))
+    assert n > 0 and n <= npat
+    assert "kyv_jit_walk" in src
+    secs, size = rs.jit_compile()
+    assert size > 1000
