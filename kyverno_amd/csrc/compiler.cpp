@@ -1006,6 +1006,8 @@ std::string fallback_reason(const Value& r) {  // validator.validate dispatch (v
 
 }  // namespace
 
+void mark_gate_exact(Ruleset& rs);
+
 Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
   auto rs = std::make_unique<Ruleset>();
   try {
@@ -1098,6 +1100,7 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
       rs->policies.push_back(pm);
     }
     build_path_trie(*rs);
+    mark_gate_exact(*rs);
     return rs.release();
   } catch (std::exception& e) {
     if (err) *err = e.what();
@@ -1165,6 +1168,31 @@ struct TrieBuilder {
   }
 };
 }  // namespace
+
+// RD_GATE_EXACT: the rule's match block is decided by the resource kind alone (every filter is a plain kinds
+// list without group/version, no exclude, no empty-OldResource retry), so the batch's per-kind-class rule gate
+// (batch.cpp rule_gate) equals MatchesResourceDescription (pkg/engine/utils.go:185-256) for it.
+void mark_gate_exact(Ruleset& rs) {
+  for (auto& rd : rs.rules) {
+    rd.flags &= (uint8_t)~RD_GATE_EXACT;
+    if (rd.empty_may_match || rd.exclude.mode != MM_NONE) continue;
+    const MatchBlock& m = rd.match;
+    if (m.mode == MM_NONE || m.nfilters == 0) continue;
+    if (m.mode != MM_ANY && m.nfilters != 1) continue;
+    bool ok = true;
+    for (uint32_t i = 0; i < m.nfilters && ok; i++) {
+      const Filter& f = rs.filters[m.filters + i];
+      if (f.nkinds == 0 || f.name != NONE || f.nnames || f.nnss || f.nann ||
+          (f.flags & (FF_HAS_SEL | FF_HAS_NSSEL | FF_ZERO_RD)))
+        ok = false;
+      for (uint32_t j = 0; j < f.nkinds && ok; j++) {
+        const KindDesc& k = rs.kinds[f.kinds + j];
+        if (k.kind != NONE && k.gv_mode != 0) ok = false;
+      }
+    }
+    if (ok) rd.flags |= RD_GATE_EXACT;
+  }
+}
 
 void build_path_trie(Ruleset& rs) {
   rs.trie.assign(1, Ruleset::TrieNode{});

@@ -360,11 +360,12 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
          "  }\n"
          "};\n"
          "}  // namespace kyv\n"
-         "extern \"C\" __global__ void __launch_bounds__(64) kyv_jit_walk(const kyv::View* __restrict__ vp, kyv::DevOut o,\n"
+         "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n"
+         "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE))) kyv_jit_walk(const kyv::View* __restrict__ vp, kyv::DevOut o,\n"
          "    const uint32_t* __restrict__ items, const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ item_cnt,\n"
-         "    const uint32_t* __restrict__ chunk_pre) {\n"
+         "    kyv::ChunkMap cm) {\n"
          "  kyv::JitWalker wk;\n"
-         "  kyv::walk_chunks(*vp, o, items, item_off, item_cnt, chunk_pre, wk);\n"
+         "  kyv::walk_chunks(*vp, o, items, item_off, item_cnt, cm, wk);\n"
          "}\n";
   return src.str();
 }
@@ -393,11 +394,12 @@ std::vector<char> jit_compile_uncached(const std::string& src, double* seconds) 
   const char* env = getenv("KYV_CSRC");
   std::string inc = "-I" + (env ? std::string(env) : dir + "/csrc");
   std::string inc2 = "-I" + dir + "/../include";
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str()};
+  std::string wpe = std::string("-DKYV_JIT_WPE=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4");
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str(), wpe.c_str()};
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "kyv_jit_walk.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     throw std::runtime_error("hiprtcCreateProgram failed");
-  hiprtcResult r = hiprtcCompileProgram(prog, 5, opts);
+  hiprtcResult r = hiprtcCompileProgram(prog, 6, opts);
   if (r != HIPRTC_SUCCESS) {
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);

@@ -4,14 +4,15 @@
 //   match_kernel  one lane per resource, rule loop uniform across the wave: kind gate, match/exclude, dispatch;
 //                 final verdicts for every pair that needs no pattern walk (incl. PodSecurity), and per-rule
 //                 work lists of the pairs that do (wave ballot + one atomic per wave and rule);
-//   scan_kernel   per-rule chunk prefix of the work lists;
 //   walk_kernel   persistent grid-stride over 64-pair chunks of ONE rule each: the wave-uniform pattern walker
 //                 (kyv_wave.h) with no idle lanes from gated / non-matching pairs.
 // Verdicts are written rule-major (coalesced bytes), failing-path records are compacted with a wave ballot +
 // one atomic per wave, per-rule status counters with ballots + one atomic per (wave, rule, status).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <mutex>
 #include <cstdio>
 #include <cstring>
@@ -70,16 +71,17 @@ struct DeviceResults {
   uint32_t* items = nullptr;     // [sum of per-rule capacities]
   uint32_t* item_off = nullptr;  // [nrules] first slot of rule k's list
   uint32_t* item_cnt = nullptr;  // [nrules] items appended
-  uint32_t* chunk_pre = nullptr; // [nrules + 1] exclusive prefix of ceil(cnt / 64), interpreted rules
-  uint32_t* chunk_pre_jit = nullptr;  // same for the rules of the compiled walk kernel
-  uint8_t* jitf = nullptr;       // [nrules] rule walked by the compiled kernel in this evaluation
-  int jit_state = -1;            // what jitf currently holds (0 none, 1 the ruleset's jit_rules)
-  uint32_t walk_grid = 0;
+  std::vector<uint64_t> cap;     // [nrules] work-list capacity (resources of the kind classes the gate admits)
+  uint32_t* sched = nullptr;     // chunk schedules of the two walk kernels (ChunkMap arrays)
+  ChunkMap cm[2] = {};           // [0] interpreted walk kernel, [1] runtime-compiled one
+  uint32_t grid[2] = {0, 0};
+  int jit_state = -1;            // what the schedules were laid out for (0 interpreter only, 1 with the jit kernel)
+  int cus = 256;
 };
 
 static void free_dev_results(DeviceResults& d) {
   hipFree(d.view); hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
-  hipFree(d.items); hipFree(d.item_off); hipFree(d.item_cnt); hipFree(d.chunk_pre); hipFree(d.chunk_pre_jit); hipFree(d.jitf);
+  hipFree(d.items); hipFree(d.item_off); hipFree(d.item_cnt); hipFree(d.sched);
   if (d.e0) hipEventDestroy(d.e0);
   if (d.e1) hipEventDestroy(d.e1);
   if (d.stream) hipStreamDestroy(d.stream);
@@ -224,9 +226,10 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
   const bool active = r < v.nres;
   const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
   for (uint32_t k = o.rule_lo; k < o.rule_hi; k++) {
+    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+    if (!__ballot(gated)) continue;  // status bytes are pre-set to ST_NONE, PSS masks to 0
     uint32_t pf = 0;
     bool walk = false;
-    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
     const uint8_t st = pair_dispatch(v, gated, r, k, &pf, &walk);
     const unsigned long long wm = __ballot(walk);
     if (wm) {
@@ -236,46 +239,13 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
       base = __shfl(base, (int)leader);
       if (walk) items[(size_t)item_off[k] + base + __popcll(wm & ((1ull << lane) - 1))] = r;
     }
-    if (active && !walk) {
+    if (gated && !walk && st != ST_NONE) {
       o.status[(size_t)k * v.nres + r] = st;
       const uint32_t ps = o.pss_slot[k];
-      if (ps != NONE) o.pss_fails[(size_t)ps * v.nres + r] = pf;
+      if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
     }
-    count_status(o.counts, k, active && !walk, st);
+    count_status(o.counts, k, gated && !walk, st);
   }
-}
-
-// per-rule chunk prefixes of the work lists (chunks = ceil(item_cnt / 64)), one for the interpreted walk
-// kernel and one for the compiled one (jitf[k] selects); one workgroup of 1024 threads
-__global__ void __launch_bounds__(1024) scan_kernel(const uint32_t* __restrict__ cnt, const uint8_t* __restrict__ jitf,
-                                                    uint32_t* __restrict__ pre, uint32_t* __restrict__ pre_jit, uint32_t n) {
-  __shared__ uint32_t part[2][1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = (n + 1023) / 1024;
-  const uint32_t lo = t * per, hi = min(n, lo + per);
-  uint32_t s0 = 0, s1 = 0;
-  for (uint32_t k = lo; k < hi; k++) {
-    uint32_t c = (cnt[k] + WAVE - 1) / WAVE;
-    if (jitf[k]) s1 += c; else s0 += c;
-  }
-  part[0][t] = s0;
-  part[1][t] = s1;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
-    uint32_t x0 = t >= off ? part[0][t - off] : 0, x1 = t >= off ? part[1][t - off] : 0;
-    __syncthreads();
-    part[0][t] += x0;
-    part[1][t] += x1;
-    __syncthreads();
-  }
-  uint32_t r0 = part[0][t] - s0, r1 = part[1][t] - s1;
-  for (uint32_t k = lo; k < hi; k++) {
-    pre[k] = r0;
-    pre_jit[k] = r1;
-    uint32_t c = (cnt[k] + WAVE - 1) / WAVE;
-    if (jitf[k]) r1 += c; else r0 += c;
-  }
-  if (t == 1023) { pre[n] = part[0][1023]; pre_jit[n] = part[1][1023]; }
 }
 
 // Phase 2 (pattern_eval): each wave takes chunks of 64 work items of ONE rule (grid-stride over all rules'
@@ -283,10 +253,10 @@ __global__ void __launch_bounds__(1024) scan_kernel(const uint32_t* __restrict__
 // walker; verdict bytes, failing-path records (wave ballot + one atomic) and counts as in phase 1.
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_WPE)))
 walk_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restrict__ items, const uint32_t* __restrict__ item_off,
-            const uint32_t* __restrict__ item_cnt, const uint32_t* __restrict__ chunk_pre, int depth) {
+            const uint32_t* __restrict__ item_cnt, ChunkMap cm, int depth) {
   extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
   WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth};
-  walk_chunks(*vp, o, items, item_off, item_cnt, chunk_pre, wk);
+  walk_chunks(*vp, o, items, item_off, item_cnt, cm, wk);
 }
 
 // ---------------------------------------------------------------- host entry
@@ -402,6 +372,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     for (auto& h : b.hdr) cls_n[h.kclass]++;
     std::vector<uint32_t> off(std::max<size_t>(nrules, 1), 0);
     uint64_t cap = 0, chunks = 0;
+    d.cap.assign(nrules, 0);
     for (size_t k = 0; k < nrules; k++) {
       off[k] = (uint32_t)cap;
       if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
@@ -409,31 +380,64 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       for (uint32_t c = 0; c < b.nclass; c++)
         if ((b.gate[(size_t)c * b.gate_words + k / 32] >> (k % 32)) & 1u) ck += cls_n[c];
       cap += ck;
+      d.cap[k] = ck;
       chunks += (ck + WAVE - 1) / WAVE;
       if (cap > 0xFFFFFFF0ull) throw std::runtime_error("walk work lists exceed 2^32 items; split the batch");
     }
     HIP_OK(hipMalloc(&d.items, std::max<uint64_t>(cap, 1) * 4));
     HIP_OK(hipMalloc(&d.item_off, off.size() * 4));
     HIP_OK(hipMalloc(&d.item_cnt, off.size() * 4));
-    HIP_OK(hipMalloc(&d.chunk_pre, (nrules + 1) * 4));
-    HIP_OK(hipMalloc(&d.chunk_pre_jit, (nrules + 1) * 4));
-    HIP_OK(hipMalloc(&d.jitf, std::max<size_t>(nrules, 1)));
     HIP_OK(hipMemcpy(d.item_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
     // persistent grid: enough waves to fill the chip several times over, never more than the chunks
     int cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-    d.walk_grid = (uint32_t)std::min<uint64_t>(chunks, (uint64_t)cus * 64);
+    d.cus = cus;
+    (void)chunks;
     db->out = dd;
   }
   DeviceResults& d = *db->out;
   hipStream_t stream = d.stream;
   const bool use_jit = jit_mode == JIT_ON || (jit_mode == JIT_AUTO && nres >= JIT_AUTO_MIN_RESOURCES);
   const bool jit = use_jit && ensure_jit(mrs, dr);
-  if (d.jit_state != (int)jit) {
-    std::vector<uint8_t> f(std::max<size_t>(nrules, 1), 0);
-    if (jit) for (size_t k = 0; k < nrules; k++) f[k] = rs.jit_rules[k];
-    HIP_OK(hipMemcpy(d.jitf, f.data(), f.size(), hipMemcpyHostToDevice));
+  if (d.jit_state != (int)jit) {  // lay out the two walk schedules (see ChunkMap)
+    const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)atoi(getenv("KYV_WIN")) : 1u;  // rules per window (experiments)
+    std::vector<uint32_t> buf;
+    size_t offs[2][4];
+    uint32_t nwin[2];
+    for (int cls = 0; cls < 2; cls++) {
+      std::vector<uint32_t> rl;
+      for (size_t k = 0; k < nrules; k++) {
+        if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
+        bool kj = jit && rs.jit_rules[k];
+        if ((int)kj == cls && d.cap[k] > 0) rl.push_back((uint32_t)k);
+      }
+      std::stable_sort(rl.begin(), rl.end(), [&](uint32_t a, uint32_t b2) { return d.cap[a] > d.cap[b2]; });
+      std::vector<uint32_t> pre{0}, first, cnt;
+      uint64_t slots = 0;
+      for (size_t i = 0; i < rl.size(); i += WIN) {
+        uint32_t n = (uint32_t)std::min<size_t>(WIN, rl.size() - i);
+        uint64_t maxc = 0;
+        for (size_t t = i; t < i + n; t++) maxc = std::max<uint64_t>(maxc, (d.cap[rl[t]] + WAVE - 1) / WAVE);
+        slots += maxc * n;
+        if (slots > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
+        pre.push_back((uint32_t)slots);
+        first.push_back((uint32_t)i);
+        cnt.push_back(n);
+      }
+      nwin[cls] = (uint32_t)first.size();
+      offs[cls][0] = buf.size(); buf.insert(buf.end(), pre.begin(), pre.end());
+      offs[cls][1] = buf.size(); buf.insert(buf.end(), first.begin(), first.end()); buf.push_back(0);
+      offs[cls][2] = buf.size(); buf.insert(buf.end(), cnt.begin(), cnt.end()); buf.push_back(0);
+      offs[cls][3] = buf.size(); buf.insert(buf.end(), rl.begin(), rl.end()); buf.push_back(0);
+      d.grid[cls] = (uint32_t)std::min<uint64_t>(slots, (uint64_t)d.cus * 64);
+    }
+    hipFree(d.sched);
+    HIP_OK(hipMalloc(&d.sched, buf.size() * 4));
+    HIP_OK(hipMemcpy(d.sched, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
+    for (int cls = 0; cls < 2; cls++)
+      d.cm[cls] = ChunkMap{d.sched + offs[cls][0], d.sched + offs[cls][1], d.sched + offs[cls][2], d.sched + offs[cls][3],
+                           nwin[cls]};
     d.jit_state = (int)jit;
   }
   DevOut o{d.status, d.pss_fails, d.pss_slot, d.recs, d.nrecs, d.max_recs, d.counts, 0, (uint32_t)nrules};
@@ -443,26 +447,26 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   double total_ms = 0;
   int n = std::max(1, iters);
   for (int it = 0; it < n; it++) {
+    HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
     HIP_OK(hipMemsetAsync(d.counts, 0, nrules * NSTATUS * 8, stream));
     HIP_OK(hipMemsetAsync(d.item_cnt, 0, std::max<size_t>(1, nrules) * 4, stream));
-    HIP_OK(hipEventRecord(d.e0, stream));
+    HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
+    if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     if (nres && nrules) {
       hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.items, d.item_off, d.item_cnt);
       HIP_OK(hipGetLastError());
-      hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, d.item_cnt, d.jitf, d.chunk_pre, d.chunk_pre_jit,
-                         (uint32_t)nrules);
-      HIP_OK(hipGetLastError());
-      if (d.walk_grid) {
-        hipLaunchKernelGGL(walk_kernel, dim3(d.walk_grid), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.items,
-                           d.item_off, d.item_cnt, d.chunk_pre, depth);
+      if (d.grid[0]) {
+        hipLaunchKernelGGL(walk_kernel, dim3(d.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.items,
+                           d.item_off, d.item_cnt, d.cm[0], depth);
         HIP_OK(hipGetLastError());
-        if (jit) {
-          const View* vp = d.view;
-          uint32_t *it = d.items, *io = d.item_off, *ic = d.item_cnt, *pj = d.chunk_pre_jit;
-          void* args[] = {(void*)&vp, (void*)&o, (void*)&it, (void*)&io, (void*)&ic, (void*)&pj};
-          HIP_OK(hipModuleLaunchKernel(dr->jfn, d.walk_grid, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
-        }
+      }
+      if (jit && d.grid[1]) {
+        const View* vp = d.view;
+        uint32_t *it = d.items, *io = d.item_off, *ic = d.item_cnt;
+        ChunkMap cmj = d.cm[1];
+        void* args[] = {(void*)&vp, (void*)&o, (void*)&it, (void*)&io, (void*)&ic, (void*)&cmj};
+        HIP_OK(hipModuleLaunchKernel(dr->jfn, d.grid[1], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
     }
     HIP_OK(hipEventRecord(d.e1, stream));
@@ -490,6 +494,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     for (int s = 0; s < NSTATUS; s++) out->counts[s] = 0;
     for (size_t k = 0; k < nrules; k++)
       for (int s = 0; s < NSTATUS; s++) out->counts[s] += (int64_t)counts[k * NSTATUS + s];
+    // ST_NONE pairs are not counted on the device
+    int64_t counted = 0;
+    for (int s = 0; s < NSTATUS; s++) if (s != ST_NONE) counted += out->counts[s];
+    out->counts[ST_NONE] = (int64_t)(nres * nrules) - counted;
     if (copy_back) {
       auto t0 = std::chrono::steady_clock::now();
       out->status.resize(nres * nrules);

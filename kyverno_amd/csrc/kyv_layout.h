@@ -280,11 +280,13 @@ struct PssDesc {
 enum RuleKind : uint8_t { RK_NONE = 0, RK_PATTERN = 1, RK_ANYPATTERN = 2, RK_PSS = 3, RK_FALLBACK = 4, RK_PANIC = 5,
                           RK_ERROR = 6 };
 
+enum RuleFlag : uint8_t { RD_GATE_EXACT = 1 };  // match == the batch's kind gate (kinds-only filters, no exclude)
+
 struct RuleDesc {
   uint8_t kind;
   uint8_t uses_meta;     // pattern contains metadata-expansion sites
   uint8_t nslots;
-  uint8_t pad;
+  uint8_t flags;         // RuleFlag
   uint32_t policy;       // policy index
   MatchBlock match, exclude;
   uint32_t empty_may_match;  // evaluate the empty-OldResource retry (validation.go:606)

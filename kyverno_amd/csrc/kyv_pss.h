@@ -503,12 +503,11 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
   LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
   if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
   bool nd = false;
-#ifdef KYV_EXP_NOMATCH
-  bool m = true;
-#else
-  bool m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
-  if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
-#endif
+  bool m = true;  // RD_GATE_EXACT: `active` (the kind gate) already decided the match
+  if (!(rd.flags & RD_GATE_EXACT)) {
+    m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
+    if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
+  }
   if (!m) return ST_NONE;
   if (nd) return ST_ND;
   switch (rd.kind) {

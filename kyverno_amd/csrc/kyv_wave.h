@@ -686,33 +686,54 @@ struct WaveSink {
 
 // per-rule status counts: wave ballots -> one atomic per status present
 __device__ __forceinline__ void count_status(unsigned long long* counts, uint32_t k, bool active, uint8_t st) {
+  // ST_NONE is not counted (the host derives it); one ballot per status value present in the wave
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  for (int s = 0; s < NSTATUS; s++) {
-    unsigned long long m = __ballot(active && (st & 7) == s);
-    if (m && lane == 0) atomicAdd(&counts[(size_t)k * NSTATUS + s], (unsigned long long)__popcll(m));
+  const uint32_t s = st & 7u;
+  unsigned long long m = __ballot(active && s != ST_NONE);
+  while (m) {
+    const uint32_t sv = __shfl(s, (int)__ffsll((long long)m) - 1);
+    const unsigned long long ms = __ballot(active && s == sv);
+    if (lane == 0) atomicAdd(&counts[(size_t)k * NSTATUS + sv], (unsigned long long)__popcll(ms));
+    m &= ~ms;
   }
 }
 
 
-// Grid-stride over 64-pair chunks of the per-rule work lists: rule k owns chunks [chunk_pre[k], chunk_pre[k+1]),
-// so every wave walks ONE rule over 64 resources; verdict bytes, records and counts as in match_kernel.
+// Chunk schedule of a walk kernel: the rules it walks, in windows of a few rules; a window's slots run
+// resource-chunk-major (slot = chunk j of rule (slot % n)), so the waves resident at one time walk the same
+// resources under the few rules of one window: node rows are reused from L2/MALL across those rules while the
+// window's code stays in the instruction cache. Laid out on the host from the per-rule capacities (kind gate);
+// slots past a rule's actual work-list length are skipped.
+struct ChunkMap {
+  const uint32_t* pre;    // [nwin + 1] first slot of each window
+  const uint32_t* first;  // [nwin] first entry of the window in `rules`
+  const uint32_t* cnt;    // [nwin] rules in the window
+  const uint32_t* rules;  // rule ids
+  uint32_t nwin;
+};
+
+// Grid-stride over the schedule; every wave walks ONE rule over 64 resources of that rule's work list;
+// verdict bytes, records and counts as in match_kernel.
 template <class Walker>
 __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, const uint32_t* __restrict__ items,
                                             const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ item_cnt,
-                                            const uint32_t* __restrict__ chunk_pre, Walker& wk) {
+                                            ChunkMap cm, Walker& wk) {
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const uint32_t nr = v.nrules;
-  const uint32_t total = sld32(chunk_pre + nr);
+  const uint32_t total = sld32(cm.pre + cm.nwin);
   WaveSink sink{o.recs, o.nrecs, o.max_recs};
   for (uint32_t c = blockIdx.x; c < total; c += gridDim.x) {
-    uint32_t lo = 0, hi = nr;  // rule k: chunk_pre[k] <= c < chunk_pre[k + 1]
+    uint32_t lo = 0, hi = cm.nwin;  // window w: pre[w] <= c < pre[w + 1]
     while (hi - lo > 1) {
       uint32_t mid = (lo + hi) >> 1;
-      if (sld32(chunk_pre + mid) <= c) lo = mid; else hi = mid;
+      if (sld32(cm.pre + mid) <= c) lo = mid; else hi = mid;
     }
-    const uint32_t k = lo;
-    const uint32_t i = (c - sld32(chunk_pre + k)) * WAVE + lane;
-    const bool active = i < sld32(item_cnt + k);
+    const uint32_t local = c - sld32(cm.pre + lo), nw = sld32(cm.cnt + lo);
+    const uint32_t j = local / nw;
+    const uint32_t k = sld32(cm.rules + sld32(cm.first + lo) + local % nw);
+    const uint32_t n = sld32(item_cnt + k);
+    if (j * WAVE >= n) continue;  // past this rule's work list
+    const uint32_t i = j * WAVE + lane;
+    const bool active = i < n;
     const uint32_t r = active ? items[(size_t)sld32(item_off + k) + i] : 0u;
     const RuleDesc rd = sld(v.rules + k);
     const uint8_t st = pair_walk(v, rd, active, r, k, wk, sink);
