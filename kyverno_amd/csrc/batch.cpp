@@ -171,6 +171,7 @@ void flatten_one(Chunk& ch, const Value& doc) {
   h.labels = h.ann = NONE;
   h.nsl = NONE;
   h.flags = em.magicflag ? RF_MAGIC : 0;
+  if (doc.t == T::Obj) h.flags |= RF_ROOT_MAP;
   const Value* meta = nested(doc, {"metadata"});
   if (meta && meta->t == T::Obj) {
     uint32_t mnode = NONE;

@@ -37,7 +37,74 @@ struct Gen {
   std::vector<uint8_t> emitted;  // pnode -> function emitted
   bool ok = true;                // pattern compilable (else the rule stays on the interpreter)
 
-  explicit Gen(const Ruleset& r) : rs(r), emitted(r.pnodes.size(), 0) {}
+  // Column scopes: the pattern root and every array-element pattern open a scope (one row of one row space);
+  // every column lookup of the maps inside a scope (not crossing into array elements) is loaded up front by
+  // the scope's caller into `pc[]`, so a scope costs one round of independent loads however deep its maps nest.
+  std::vector<int> slot;                         // pentry -> index in its scope's pc[], -1 none
+  std::vector<std::vector<uint32_t>> scope_of;   // scope-root pnode -> its column entries (pentry ids)
+  std::vector<uint8_t> scoped;                   // pnode -> scope collected
+
+  explicit Gen(const Ruleset& r)
+      : rs(r), emitted(r.pnodes.size(), 0), slot(r.pentries.size(), -1), scope_of(r.pnodes.size()), scoped(r.pnodes.size(), 0) {}
+
+  void collect(uint32_t pn, std::vector<uint32_t>& list, int guard) {
+    if (pn == NONE || pn >= rs.pnodes.size() || guard > 4 * MAX_DEPTH) return;
+    const PNode& P = rs.pnodes[pn];
+    if (P.kind != P_MAP) return;
+    for (uint32_t e = 0; e < P.n; e++) {
+      const uint32_t ei = P.first + e;
+      const PEntry& E = rs.pentries[ei];
+      if (E.col != NONE) {
+        if (slot[ei] >= 0) { ok = false; continue; }  // entry reached from two scopes: leave the rule interpreted
+        slot[ei] = (int)list.size();
+        list.push_back(ei);
+      }
+      if (E.handler == H_STAR || E.handler == H_NEGATION || E.handler == H_EXIST_BADPAT || E.handler == H_EXISTENCE ||
+          E.child == NONE)
+        continue;
+      collect(E.child, list, guard + 1);  // child maps share the scope; arrays open new ones
+    }
+  }
+  void scope(uint32_t root) {
+    if (root == NONE || root >= rs.pnodes.size() || scoped[root]) return;
+    scoped[root] = 1;
+    collect(root, scope_of[root], 0);
+  }
+  // open the scopes of every array-element pattern below pn
+  void scopes_below(uint32_t pn, int guard) {
+    if (pn == NONE || pn >= rs.pnodes.size() || guard > 4 * MAX_DEPTH) return;
+    const PNode& P = rs.pnodes[pn];
+    switch (P.kind) {
+      case P_MAP:
+        for (uint32_t e = 0; e < P.n; e++) {
+          const PEntry& E = rs.pentries[P.first + e];
+          if (E.handler == H_STAR || E.handler == H_NEGATION || E.handler == H_EXIST_BADPAT || E.child == NONE) continue;
+          if (E.handler == H_EXISTENCE) {
+            for (uint32_t j = 0; j < rs.pool[E.child]; j++) {
+              scope(rs.pool[E.child + 1 + j]);
+              scopes_below(rs.pool[E.child + 1 + j], guard + 1);
+            }
+          } else {
+            scopes_below(E.child, guard + 1);
+          }
+        }
+        break;
+      case P_ARR_MAPS: scope(P.first); scopes_below(P.first, guard + 1); break;
+      case P_ARR_POS:
+        for (uint32_t i = 0; i < P.n; i++) { scope(rs.pool[P.first + i]); scopes_below(rs.pool[P.first + i], guard + 1); }
+        break;
+      default: break;
+    }
+  }
+  // preload of scope `root`'s columns at row expression `rowx` into array `name`
+  std::string preload(uint32_t root, const std::string& name, const std::string& rowx) {
+    scope(root);
+    const auto& L = scope_of[root];
+    std::ostringstream o;
+    o << "uint32_t " << name << "[" << std::max<size_t>(1, L.size()) << "];";
+    for (size_t i = 0; i < L.size(); i++) o << " " << name << "[" << i << "] = jraw(w, " << u(L[i]) << ", " << rowx << ");";
+    return o.str();
+  }
 
   static std::string u(uint32_t x) { return std::to_string(x) + "u"; }
   static std::string i64(int64_t x) { return "(int64_t)" + std::to_string(x) + "ll"; }
@@ -124,7 +191,8 @@ struct Gen {
     if (!ok) return;
     emitted[pn] = 1;
     const std::string T = u(P.tmpl);
-    out << "static __device__ __forceinline__ Ret p" << pn << "(JW& w, uint32_t rn, uint32_t rt, uint32_t row) {\n";
+    out << "static __device__ __forceinline__ Ret p" << pn
+        << "(JW& w, uint32_t rn, uint32_t rt, uint32_t row, const uint32_t* pc) {\n";
     switch (P.kind) {
       case P_MAP: map(pn, P); break;
       case P_LEAF:
@@ -164,7 +232,9 @@ struct Gen {
           if (setidx)
             out << "    w.idx = (w.idx & ~(0xFFFFull << " << 16u * P.level << ")) | ((uint64_t)" << i << " << "
                 << 16u * P.level << ");\n";
-          out << "    { Ret r = p" << child << "(w, a.a + " << i << ", T_UNK, a.c == NONE ? NONE : a.c + " << i << ");\n"
+          out << "    { const uint32_t er = a.c == NONE ? NONE : a.c + " << i << ";\n"
+              << "      " << preload(child, "pe", "er") << "\n"
+              << "      Ret r = p" << child << "(w, a.a + " << i << ", T_UNK, er, pe);\n"
               << "      if (w.ost) return r;\n"
               << "      if (r.err) { if (ret_is_skip(r)) st |= FS_SKIP | ((uint32_t)r.mask << 2); else return r; }\n"
               << "      else st |= FS_APPLY; }\n";
@@ -193,7 +263,8 @@ struct Gen {
   void lookup(uint32_t ei, uint32_t e, const std::string& keyexpr_rowvar) {
     const PEntry& E = rs.pentries[ei];
     if (E.col != NONE) {
-      out << "  c" << e << " = jcol(w, " << u(ei) << ", row, &t" << e << ");\n";
+      if (slot[ei] < 0) { ok = false; return; }  // every column entry belongs to a collected scope
+      out << "  c" << e << " = col_decode(pc[" << slot[ei] << "], &t" << e << ");\n";
     } else {
       std::string key = (E.flags & EF_WILD) ? "w.keys.get(" + u(E.slot) + ")" : u(E.key);
       out << "  c" << e << " = wmap_find(w.R, " << keyexpr_rowvar << ".a, " << keyexpr_rowvar << ".b, " << key
@@ -238,7 +309,7 @@ struct Gen {
       const std::string c = "c" + std::to_string(e), t = "t" + std::to_string(e);
       if (E.col == NONE) lookup(P.first + e, e, "m");
       auto call = [&](const std::string& wrap) {
-        out << "    { Ret r = p" << E.child << "(w, " << c << ", " << t << ", row);\n"
+        out << "    { Ret r = p" << E.child << "(w, " << c << ", " << t << ", row, pc);\n"
             << "      if (w.ost) return r;\n"
             << "      if (r.err) { " << wrap << "return r; } }\n";
       };
@@ -276,7 +347,9 @@ struct Gen {
           for (uint32_t j = 0; j < npat; j++) {
             out << "    { bool hit = false;\n"
                 << "      for (uint32_t i = 0; i < a.b; i++) {\n"
-                << "        Ret r = p" << rs.pool[E.child + 1 + j] << "(w, a.a + i, T_UNK, a.c == NONE ? NONE : a.c + i);\n"
+                << "        const uint32_t er = a.c == NONE ? NONE : a.c + i;\n"
+                << "        " << preload(rs.pool[E.child + 1 + j], "pe", "er") << "\n"
+                << "        Ret r = p" << rs.pool[E.child + 1 + j] << "(w, a.a + i, T_UNK, er, pe);\n"
                 << "        if (w.ost) return r;\n"
                 << "        if (!r.err) { hit = true; break; }\n"
                 << "      }\n"
@@ -325,6 +398,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
     size_t mark = g.out.tellp();
     std::vector<uint8_t> em = g.emitted;
     g.ok = true;
+    for (uint32_t r : rr) { g.scope(r); g.scopes_below(r, 0); }
     for (uint32_t r : rr) g.node(r, 0);
     if (!g.ok) {  // roll back this rule's functions
       std::string s = g.out.str().substr(0, mark);
@@ -345,7 +419,9 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
     src << "static __device__ __forceinline__ void root" << r
         << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, PatOut& out) {\n"
            "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
-           "  Ret r = p" << r << "(w, 0u, T_UNK, (uint32_t)(hp - v.hdr));\n"
+           "  const uint32_t row = (uint32_t)(hp - v.hdr);\n"
+           "  " << g.preload(r, "pc", "row") << "\n"
+           "  Ret r = p" << r << "(w, 0u, (hp->flags & RF_ROOT_MAP) ? (uint32_t)N_MAP : T_UNK, row, pc);\n"
            "  jfinish(w, r, out);\n"
            "}\n";
   src << "struct JitWalker {\n"
@@ -362,10 +438,9 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
          "}  // namespace kyv\n"
          "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n"
          "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE))) kyv_jit_walk(const kyv::View* __restrict__ vp, kyv::DevOut o,\n"
-         "    const uint32_t* __restrict__ items, const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ item_cnt,\n"
-         "    kyv::ChunkMap cm) {\n"
+         "    kyv::WorkLists wl, kyv::ChunkMap cm) {\n"
          "  kyv::JitWalker wk;\n"
-         "  kyv::walk_chunks(*vp, o, items, item_off, item_cnt, cm, wk);\n"
+         "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"
          "}\n";
   return src.str();
 }

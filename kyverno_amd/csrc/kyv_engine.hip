@@ -68,9 +68,7 @@ struct DeviceResults {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   View* view = nullptr;  // device copy of the View the kernel reads
   // walk work lists (match_kernel -> walk_kernel): per rule a list of resource positions
-  uint32_t* items = nullptr;     // [sum of per-rule capacities]
-  uint32_t* item_off = nullptr;  // [nrules] first slot of rule k's list
-  uint32_t* item_cnt = nullptr;  // [nrules] items appended
+  WorkLists wl{};                // walk work lists (kyv_wave.h)
   std::vector<uint64_t> cap;     // [nrules] work-list capacity (resources of the kind classes the gate admits)
   uint32_t* sched = nullptr;     // chunk schedules of the two walk kernels (ChunkMap arrays)
   ChunkMap cm[2] = {};           // [0] interpreted walk kernel, [1] runtime-compiled one
@@ -81,7 +79,7 @@ struct DeviceResults {
 
 static void free_dev_results(DeviceResults& d) {
   hipFree(d.view); hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
-  hipFree(d.items); hipFree(d.item_off); hipFree(d.item_cnt); hipFree(d.sched);
+  hipFree(d.wl.items); hipFree(d.wl.cnt); hipFree(d.sched);
   if (d.e0) hipEventDestroy(d.e0);
   if (d.e1) hipEventDestroy(d.e1);
   if (d.stream) hipStreamDestroy(d.stream);
@@ -218,8 +216,7 @@ constexpr int RECS_PER_PAIR = MAX_ALTS;
 // Phase 1 (match_eval): one lane per resource, the rule loop uniform across the wave. Kind gate, match /
 // exclude program, dispatch; verdicts that need no pattern walk are final here (incl. PodSecurity). Pairs
 // that need the walk are appended to the rule's work list (wave ballot + one atomic per wave and rule).
-__global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ vp, DevOut o, uint32_t* __restrict__ items,
-                                                      const uint32_t* __restrict__ item_off, uint32_t* __restrict__ item_cnt) {
+__global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl) {
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
   const uint32_t r = blockIdx.x * BLOCK + lane;
@@ -232,12 +229,11 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
     bool walk = false;
     const uint8_t st = pair_dispatch(v, gated, r, k, &pf, &walk);
     const unsigned long long wm = __ballot(walk);
-    if (wm) {
-      const uint32_t leader = (uint32_t)__ffsll((long long)wm) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(&item_cnt[k], (uint32_t)__popcll(wm));
-      base = __shfl(base, (int)leader);
-      if (walk) items[(size_t)item_off[k] + base + __popcll(wm & ((1ull << lane) - 1))] = r;
+    const RuleDesc& rdk = v.rules[k];
+    if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {  // this wave's work list for rule k
+      const size_t list = (size_t)k * wl.nwaves + blockIdx.x;
+      if (walk) wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] = r;
+      if (lane == 0) wl.cnt[list] = (uint8_t)__popcll(wm);
     }
     if (gated && !walk && st != ST_NONE) {
       o.status[(size_t)k * v.nres + r] = st;
@@ -252,11 +248,10 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
 // chunks), so every lane walks the same compiled pattern over a different resource with the wave-uniform
 // walker; verdict bytes, failing-path records (wave ballot + one atomic) and counts as in phase 1.
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_WPE)))
-walk_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restrict__ items, const uint32_t* __restrict__ item_off,
-            const uint32_t* __restrict__ item_cnt, ChunkMap cm, int depth) {
+walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, ChunkMap cm, int depth) {
   extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
   WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth};
-  walk_chunks(*vp, o, items, item_off, item_cnt, cm, wk);
+  walk_chunks(*vp, o, wl, cm, wk);
 }
 
 // ---------------------------------------------------------------- host entry
@@ -367,33 +362,15 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipEventCreate(&d.e1));
     HIP_OK(hipMalloc(&d.view, sizeof(View)));
     HIP_OK(hipMemcpy(d.view, &v, sizeof(View), hipMemcpyHostToDevice));
-    // walk work-list capacity per rule: resources of the kind classes its gate admits (exact upper bound)
-    std::vector<uint64_t> cls_n(std::max<uint32_t>(b.nclass, 1), 0);
-    for (auto& h : b.hdr) cls_n[h.kclass]++;
-    std::vector<uint32_t> off(std::max<size_t>(nrules, 1), 0);
-    uint64_t cap = 0, chunks = 0;
-    d.cap.assign(nrules, 0);
-    for (size_t k = 0; k < nrules; k++) {
-      off[k] = (uint32_t)cap;
-      if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
-      uint64_t ck = 0;
-      for (uint32_t c = 0; c < b.nclass; c++)
-        if ((b.gate[(size_t)c * b.gate_words + k / 32] >> (k % 32)) & 1u) ck += cls_n[c];
-      cap += ck;
-      d.cap[k] = ck;
-      chunks += (ck + WAVE - 1) / WAVE;
-      if (cap > 0xFFFFFFF0ull) throw std::runtime_error("walk work lists exceed 2^32 items; split the batch");
-    }
-    HIP_OK(hipMalloc(&d.items, std::max<uint64_t>(cap, 1) * 4));
-    HIP_OK(hipMalloc(&d.item_off, off.size() * 4));
-    HIP_OK(hipMalloc(&d.item_cnt, off.size() * 4));
-    HIP_OK(hipMemcpy(d.item_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+    // walk work lists: one 64-slot list per (rule, match wave)
+    d.wl.nwaves = (uint32_t)((nres + WAVE - 1) / WAVE);
+    HIP_OK(hipMalloc(&d.wl.items, std::max<size_t>(1, nrules * (size_t)d.wl.nwaves * WAVE) * 4));
+    HIP_OK(hipMalloc(&d.wl.cnt, std::max<size_t>(4, nrules * (size_t)d.wl.nwaves + 4)));
     // persistent grid: enough waves to fill the chip several times over, never more than the chunks
     int cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
     d.cus = cus;
-    (void)chunks;
     db->out = dd;
   }
   DeviceResults& d = *db->out;
@@ -401,35 +378,48 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   const bool use_jit = jit_mode == JIT_ON || (jit_mode == JIT_AUTO && nres >= JIT_AUTO_MIN_RESOURCES);
   const bool jit = use_jit && ensure_jit(mrs, dr);
   if (d.jit_state != (int)jit) {  // lay out the two walk schedules (see ChunkMap)
-    const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)atoi(getenv("KYV_WIN")) : 1u;  // rules per window (experiments)
+    const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)std::max(1, atoi(getenv("KYV_WIN"))) : 1u;  // rules per window (1: best measured)
+    const uint32_t nw = d.wl.nwaves, gw = b.gate_words;
+    // gated rule set of every match wave (union over the kind classes of its lanes), as runs of equal sets
+    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> runs;  // (first wave, gate words)
+    for (uint32_t w = 0; w < nw; w++) {
+      std::vector<uint32_t> g(gw, 0);
+      for (size_t r = (size_t)w * WAVE; r < std::min(nres, (size_t)(w + 1) * WAVE); r++)
+        for (uint32_t i = 0; i < gw; i++) g[i] |= b.gate[(size_t)b.hdr[r].kclass * gw + i];
+      if (runs.empty() || runs.back().second != g) runs.push_back({w, g});
+    }
     std::vector<uint32_t> buf;
-    size_t offs[2][4];
-    uint32_t nwin[2];
+    size_t offs[2][5];
+    uint32_t nseg[2];
     for (int cls = 0; cls < 2; cls++) {
-      std::vector<uint32_t> rl;
-      for (size_t k = 0; k < nrules; k++) {
-        if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
-        bool kj = jit && rs.jit_rules[k];
-        if ((int)kj == cls && d.cap[k] > 0) rl.push_back((uint32_t)k);
-      }
-      std::stable_sort(rl.begin(), rl.end(), [&](uint32_t a, uint32_t b2) { return d.cap[a] > d.cap[b2]; });
-      std::vector<uint32_t> pre{0}, first, cnt;
+      std::vector<uint32_t> pre{0}, w0, first, cnt, rl;
       uint64_t slots = 0;
-      for (size_t i = 0; i < rl.size(); i += WIN) {
-        uint32_t n = (uint32_t)std::min<size_t>(WIN, rl.size() - i);
-        uint64_t maxc = 0;
-        for (size_t t = i; t < i + n; t++) maxc = std::max<uint64_t>(maxc, (d.cap[rl[t]] + WAVE - 1) / WAVE);
-        slots += maxc * n;
-        if (slots > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
-        pre.push_back((uint32_t)slots);
-        first.push_back((uint32_t)i);
-        cnt.push_back(n);
+      for (size_t ri = 0; ri < runs.size(); ri++) {
+        const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
+        std::vector<uint32_t> ks;
+        for (size_t k = 0; k < nrules; k++) {
+          if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
+          if (!((runs[ri].second[k / 32] >> (k % 32)) & 1u)) continue;
+          if ((int)(jit && rs.jit_rules[k]) != cls) continue;
+          ks.push_back((uint32_t)k);
+        }
+        for (size_t i = 0; i < ks.size(); i += WIN) {
+          uint32_t n = (uint32_t)std::min<size_t>(WIN, ks.size() - i);
+          w0.push_back(wb);
+          first.push_back((uint32_t)rl.size());
+          cnt.push_back(n);
+          rl.insert(rl.end(), ks.begin() + i, ks.begin() + i + n);
+          slots += (uint64_t)(we - wb) * n;
+          if (slots > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
+          pre.push_back((uint32_t)slots);
+        }
       }
-      nwin[cls] = (uint32_t)first.size();
+      nseg[cls] = (uint32_t)w0.size();
       offs[cls][0] = buf.size(); buf.insert(buf.end(), pre.begin(), pre.end());
-      offs[cls][1] = buf.size(); buf.insert(buf.end(), first.begin(), first.end()); buf.push_back(0);
-      offs[cls][2] = buf.size(); buf.insert(buf.end(), cnt.begin(), cnt.end()); buf.push_back(0);
-      offs[cls][3] = buf.size(); buf.insert(buf.end(), rl.begin(), rl.end()); buf.push_back(0);
+      offs[cls][1] = buf.size(); buf.insert(buf.end(), w0.begin(), w0.end()); buf.push_back(0);
+      offs[cls][2] = buf.size(); buf.insert(buf.end(), first.begin(), first.end()); buf.push_back(0);
+      offs[cls][3] = buf.size(); buf.insert(buf.end(), cnt.begin(), cnt.end()); buf.push_back(0);
+      offs[cls][4] = buf.size(); buf.insert(buf.end(), rl.begin(), rl.end()); buf.push_back(0);
       d.grid[cls] = (uint32_t)std::min<uint64_t>(slots, (uint64_t)d.cus * 64);
     }
     hipFree(d.sched);
@@ -437,7 +427,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMemcpy(d.sched, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
     for (int cls = 0; cls < 2; cls++)
       d.cm[cls] = ChunkMap{d.sched + offs[cls][0], d.sched + offs[cls][1], d.sched + offs[cls][2], d.sched + offs[cls][3],
-                           nwin[cls]};
+                           d.sched + offs[cls][4], nseg[cls]};
     d.jit_state = (int)jit;
   }
   DevOut o{d.status, d.pss_fails, d.pss_slot, d.recs, d.nrecs, d.max_recs, d.counts, 0, (uint32_t)nrules};
@@ -450,22 +440,21 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
     HIP_OK(hipMemsetAsync(d.counts, 0, nrules * NSTATUS * 8, stream));
-    HIP_OK(hipMemsetAsync(d.item_cnt, 0, std::max<size_t>(1, nrules) * 4, stream));
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     if (nres && nrules) {
-      hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.items, d.item_off, d.item_cnt);
+      hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl);
       HIP_OK(hipGetLastError());
       if (d.grid[0]) {
-        hipLaunchKernelGGL(walk_kernel, dim3(d.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.items,
-                           d.item_off, d.item_cnt, d.cm[0], depth);
+        hipLaunchKernelGGL(walk_kernel, dim3(d.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, d.cm[0],
+                           depth);
         HIP_OK(hipGetLastError());
       }
       if (jit && d.grid[1]) {
         const View* vp = d.view;
-        uint32_t *it = d.items, *io = d.item_off, *ic = d.item_cnt;
+        WorkLists wl = d.wl;
         ChunkMap cmj = d.cm[1];
-        void* args[] = {(void*)&vp, (void*)&o, (void*)&it, (void*)&io, (void*)&ic, (void*)&cmj};
+        void* args[] = {(void*)&vp, (void*)&o, (void*)&wl, (void*)&cmj};
         HIP_OK(hipModuleLaunchKernel(dr->jfn, d.grid[1], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
     }

@@ -69,6 +69,7 @@ enum ResFlag : uint32_t {
   RF_ANCHORISH = 1u << 1,   // some key under metadata parses as an anchor -> metadata expansion falls back
   RF_EMPTY = 1u << 2,
   RF_TOO_DEEP = 1u << 3,
+  RF_ROOT_MAP = 1u << 4,    // the resource document is a JSON object (walks skip the root row's type check load)
 };
 
 struct ResHeader {          // 64 bytes, one per resource (unstructured accessors, host-computed)

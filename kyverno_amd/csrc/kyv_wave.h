@@ -635,6 +635,11 @@ __device__ __forceinline__ uint32_t jcol(const JW& w, uint32_t e, uint32_t row, 
   const uint32_t off = sld32(&w.v.pe[e].col);
   return col_decode(row == NONE ? NONE : gld32(w.v.colv + (size_t)off + row), ct);
 }
+// raw column entry of a lookup (speculative preload of a column scope; NONE rows give NONE)
+__device__ __forceinline__ uint32_t jraw(const JW& w, uint32_t e, uint32_t row) {
+  const uint32_t off = sld32(&w.v.pe[e].col);
+  return row == NONE ? NONE : gld32(w.v.colv + (size_t)off + row);
+}
 // MatchPattern's classification (validate.go:31-56), as at the end of eval_pattern
 __device__ __forceinline__ void jfinish(const JW& w, const Ret& ret, PatOut& out) {
   out.key0 = w.keys.k0;
@@ -699,42 +704,54 @@ __device__ __forceinline__ void count_status(unsigned long long* counts, uint32_
 }
 
 
-// Chunk schedule of a walk kernel: the rules it walks, in windows of a few rules; a window's slots run
-// resource-chunk-major (slot = chunk j of rule (slot % n)), so the waves resident at one time walk the same
-// resources under the few rules of one window: node rows are reused from L2/MALL across those rules while the
-// window's code stays in the instruction cache. Laid out on the host from the per-rule capacities (kind gate);
-// slots past a rule's actual work-list length are skipped.
+// Walk work lists, written by match_kernel without atomics: for rule k and match wave w (64 consecutive
+// resources of the kind-major batch), cnt[k][w] pairs need the walk and items[k][w][0..cnt) are their resource
+// positions (compacted with a ballot prefix).
+struct WorkLists {
+  uint32_t* items;   // [nrules][nwaves][64]
+  uint8_t* cnt;      // [nrules][nwaves]
+  uint32_t nwaves;
+};
+__device__ __forceinline__ uint32_t sld8(const uint8_t* p) {  // scalar load of one byte (uniform address)
+  const size_t a = (size_t)p;
+  return (sld32((const uint32_t*)(a & ~(size_t)3)) >> (8 * (a & 3))) & 0xFFu;
+}
+
+// Chunk schedule of a walk kernel, laid out on the host: segments of (run of match waves with the same gated
+// rule set) x (window of a few of those rules); a segment's slots run wave-major with the window's rules
+// fastest, so the waves resident at one time walk the same 64 resources under the few rules of one window:
+// node rows and columns are reused from L2 across those rules, and the window's code stays in the
+// instruction cache. Chunks whose work list is empty (no pair matched) are skipped.
 struct ChunkMap {
-  const uint32_t* pre;    // [nwin + 1] first slot of each window
-  const uint32_t* first;  // [nwin] first entry of the window in `rules`
-  const uint32_t* cnt;    // [nwin] rules in the window
+  const uint32_t* pre;    // [nseg + 1] first slot of each segment
+  const uint32_t* w0;     // [nseg] first match wave of the segment
+  const uint32_t* first;  // [nseg] first entry of the segment's rules in `rules`
+  const uint32_t* cnt;    // [nseg] rules in the segment
   const uint32_t* rules;  // rule ids
-  uint32_t nwin;
+  uint32_t nseg;
 };
 
-// Grid-stride over the schedule; every wave walks ONE rule over 64 resources of that rule's work list;
+// Grid-stride over the schedule; every wave walks ONE rule over the (up to 64) resources of one work list;
 // verdict bytes, records and counts as in match_kernel.
 template <class Walker>
-__device__ __forceinline__ void walk_chunks(const View& v, DevOut o, const uint32_t* __restrict__ items,
-                                            const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ item_cnt,
-                                            ChunkMap cm, Walker& wk) {
+__device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists wl, ChunkMap cm, Walker& wk) {
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const uint32_t total = sld32(cm.pre + cm.nwin);
+  const uint32_t total = sld32(cm.pre + cm.nseg);
   WaveSink sink{o.recs, o.nrecs, o.max_recs};
   for (uint32_t c = blockIdx.x; c < total; c += gridDim.x) {
-    uint32_t lo = 0, hi = cm.nwin;  // window w: pre[w] <= c < pre[w + 1]
+    uint32_t lo = 0, hi = cm.nseg;  // segment: pre[seg] <= c < pre[seg + 1]
     while (hi - lo > 1) {
       uint32_t mid = (lo + hi) >> 1;
       if (sld32(cm.pre + mid) <= c) lo = mid; else hi = mid;
     }
     const uint32_t local = c - sld32(cm.pre + lo), nw = sld32(cm.cnt + lo);
-    const uint32_t j = local / nw;
+    const uint32_t w = sld32(cm.w0 + lo) + local / nw;
     const uint32_t k = sld32(cm.rules + sld32(cm.first + lo) + local % nw);
-    const uint32_t n = sld32(item_cnt + k);
-    if (j * WAVE >= n) continue;  // past this rule's work list
-    const uint32_t i = j * WAVE + lane;
-    const bool active = i < n;
-    const uint32_t r = active ? items[(size_t)sld32(item_off + k) + i] : 0u;
+    const size_t list = (size_t)k * wl.nwaves + w;
+    const uint32_t n = sld8(wl.cnt + list);
+    if (!n) continue;
+    const bool active = lane < n;
+    const uint32_t r = active ? wl.items[list * WAVE + lane] : 0u;
     const RuleDesc rd = sld(v.rules + k);
     const uint8_t st = pair_walk(v, rd, active, r, k, wk, sink);
     if (active) o.status[(size_t)k * v.nres + r] = st;
