@@ -5,6 +5,8 @@
 // string), GetLabels/GetAnnotations (NestedStringMap -> nil unless a map of strings), GroupVersionKind
 // (ParseGroupVersion; more than one '/' -> empty GVK).
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <thread>
 
@@ -552,9 +554,12 @@ namespace {
 struct Resolver {
   const Ruleset& rs;
   Node* R;
-  uint32_t* colv;            // nullptr in the counting pass
+  uint64_t* colv;            // nullptr in the counting pass
   const uint32_t* col_off;
   uint32_t* next;            // next free row per row space
+  uint64_t entry(uint32_t x) const {
+    return ((uint64_t)R[x].a << 32) | ((uint64_t)node_type(R[x]) << COL_TYPE_SHIFT) | x;
+  }
   static uint32_t find(const Node* R, const Node& m, uint32_t key) {
     uint32_t lo = m.a, hi = m.a + m.b;
     while (lo < hi) {
@@ -571,14 +576,18 @@ struct Resolver {
       for (auto& kv : T.kids) {
         uint32_t x = find(R, mn, kv.first);
         if (x == NONE) continue;  // columns are NONE-initialised
-        if (colv) colv[(size_t)col_off[rs.trie[kv.second].col] + row] = (node_type(R[x]) << COL_TYPE_SHIFT) | x;
+        if (colv) colv[(size_t)col_off[rs.trie[kv.second].col] + row] = entry(x);
         go(x, kv.second, row);
       }
     } else if (node_type(mn) == N_ARR && T.star != NONE) {
       uint32_t space = rs.trie[T.star].rowspace;
       uint32_t base = next[space];
       next[space] += mn.b;
-      if (colv) R[m].c = base;
+      if (colv) {
+        R[m].c = base;
+        const size_t self = col_off[rs.trie[T.star].col];
+        for (uint32_t i = 0; i < mn.b; i++) colv[self + base + i] = entry(mn.a + i);
+      }
       for (uint32_t i = 0; i < mn.b; i++) go(mn.a + i, T.star, base + i);
     }
   }
@@ -633,7 +642,13 @@ void resolve_path_columns(Batch& b, int threads) {
     total += b.rs_rows[rs.col_rowspace[c]];
     if (total > 0xFFFFFFF0ull) throw std::runtime_error("path columns exceed 2^32 entries; split the batch");
   }
-  b.colv.assign(total + 1, NONE);
+  b.colv.assign(total + 1, (uint64_t)NONE);
+  if (getenv("KYV_DEBUG_STATS")) {
+    fprintf(stderr, "[kyvgpu] path columns: %u columns, %u row spaces, %llu entries (rows:", rs.ncols, nsp,
+            (unsigned long long)total);
+    for (uint32_t sp = 0; sp < nsp; sp++) fprintf(stderr, " %u", b.rs_rows[sp]);
+    fprintf(stderr, ")\n");
+  }
   run(true, base);
   // resources too large for column encoding: pattern pairs fall back (RF_MAGIC), so no column is read
   for (auto& h : b.hdr) if (!eligible(h)) h.flags |= RF_MAGIC;

@@ -1130,6 +1130,8 @@ struct TrieBuilder {
     uint32_t id = (uint32_t)rs.trie.size();
     rs.trie.emplace_back();
     rs.trie[id].rowspace = rs.nrowspaces++;
+    rs.trie[id].col = rs.ncols++;  // self column of the elements
+    rs.col_rowspace.push_back(rs.trie[id].rowspace);
     rs.trie[t].star = id;
     return id;
   }
@@ -1150,6 +1152,7 @@ struct TrieBuilder {
           if (E.handler == H_STAR || E.handler == H_NEGATION || E.handler == H_EXIST_BADPAT || E.child == NONE) continue;
           if (E.handler == H_EXISTENCE) {
             uint32_t st = ct == NONE ? NONE : star(ct);
+            rs.pe_self[P.first + e] = st == NONE ? NONE : rs.trie[st].col;
             uint32_t npat = rs.pool[E.child];
             for (uint32_t j = 0; j < npat; j++) walk(rs.pool[E.child + 1 + j], st, guard + 1);
           } else {
@@ -1157,9 +1160,20 @@ struct TrieBuilder {
           }
         }
         break;
-      case P_ARR_MAPS: walk(P.first, t == NONE ? NONE : star(t), guard + 1); break;
+      case P_ARR_MAPS: {
+        uint32_t st = t == NONE ? NONE : star(t);
+        rs.pn_self[pn] = st == NONE ? NONE : rs.trie[st].col;
+        walk(P.first, st, guard + 1);
+        break;
+      }
+      case P_ARR_SCALAR: {  // element values through the self column
+        uint32_t st = t == NONE ? NONE : star(t);
+        rs.pn_self[pn] = st == NONE ? NONE : rs.trie[st].col;
+        break;
+      }
       case P_ARR_POS: {
         uint32_t st = t == NONE ? NONE : star(t);
+        rs.pn_self[pn] = st == NONE ? NONE : rs.trie[st].col;
         for (uint32_t i = 0; i < P.n; i++) walk(rs.pool[P.first + i], st, guard + 1);
         break;
       }
@@ -1201,6 +1215,8 @@ void build_path_trie(Ruleset& rs) {
   rs.col_rowspace.clear();
   for (auto& E : rs.pentries) E.col = NONE;
   for (auto& P : rs.pnodes) P.flags &= (uint8_t)~PF_NEEDROW;
+  rs.pn_self.assign(rs.pnodes.size(), NONE);
+  rs.pe_self.assign(rs.pentries.size(), NONE);
   TrieBuilder tb{rs, std::vector<uint32_t>(rs.pnodes.size(), TrieBuilder::UNSET)};
   for (auto& rd : rs.rules) {
     if (rd.kind == RK_PATTERN) tb.walk(rd.root, 0, 0);

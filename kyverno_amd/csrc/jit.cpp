@@ -101,7 +101,7 @@ struct Gen {
     scope(root);
     const auto& L = scope_of[root];
     std::ostringstream o;
-    o << "uint32_t " << name << "[" << std::max<size_t>(1, L.size()) << "];";
+    o << "uint64_t " << name << "[" << std::max<size_t>(1, L.size()) << "];";
     for (size_t i = 0; i < L.size(); i++) o << " " << name << "[" << i << "] = jraw(w, " << u(L[i]) << ", " << rowx << ");";
     return o.str();
   }
@@ -192,16 +192,19 @@ struct Gen {
     emitted[pn] = 1;
     const std::string T = u(P.tmpl);
     out << "static __device__ __forceinline__ Ret p" << pn
-        << "(JW& w, uint32_t rn, uint32_t rt, uint32_t row, const uint32_t* pc) {\n";
+        << "(JW& w, uint32_t rn, uint32_t rt, uint32_t ra, uint32_t row, const uint64_t* pc) {\n";
     switch (P.kind) {
       case P_MAP: map(pn, P); break;
       case P_LEAF:
-        out << "  Node n{0u, 0u, 0u, 0u};\n  if (rn != NONE) n = gnode(w.R + rn);\n";
+        // a string / boolean / null whose type and `a` came with the column needs no row read
+        out << "  const bool known = rt == N_STR || rt == N_TRUE || rt == N_FALSE || rt == N_NULL;\n"
+               "  Node n{0u, 0u, 0u, 0u};\n  if (rn != NONE && !known) n = gnode(w.R + rn);\n";
         out << "  bool fb = false, okv = true;\n";
-        out << "  const bool each = rn != NONE && node_type(n) == N_ARR;\n"
+        out << "  const bool each = rn != NONE && !known && node_type(n) == N_ARR;\n"
                "  const uint32_t cnt = each ? n.b : 1u;\n"
                "  for (uint32_t i = 0; i < cnt && okv; i++) {\n"
-               "    const Val x = each ? wvalue_of(w.v, w.R, n.a + i) : (rn == NONE ? wvalue_absent() : wvalue_node(w.v, n));\n"
+               "    const Val x = each ? wvalue_of(w.v, w.R, n.a + i)\n"
+               "                       : (rn == NONE ? wvalue_absent() : known ? jvalue(w, rn, rt, ra) : wvalue_node(w.v, n));\n"
                "    " << leaf_code(P.first) << "\n"
                "  }\n";
         out << "  if (fb) { w.ost = ST_FALLBACK; return ok_ret(); }\n";
@@ -215,8 +218,14 @@ struct Gen {
         out << "  if (rn == NONE) return mkerr(EC_NONE, 0, " << T << ");\n";
         out << "  const Node a = gnode(w.R + rn);\n  if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << T << ");\n";
         out << "  bool fb = false, okv = true;\n";
-        out << "  for (uint32_t i = 0; i < a.b && okv; i++) {\n"
-               "    const Val x = wvalue_of(w.v, w.R, a.a + i);\n"
+        const uint32_t self = rs.pn_self[pn];
+        out << "  for (uint32_t i = 0; i < a.b && okv; i++) {\n";
+        if (self != NONE)
+          out << "    uint32_t et, ea; const uint32_t ei = jdec(jself(w, " << u(self) << ", a.c == NONE ? NONE : a.c + i), &et, &ea);\n"
+                 "    const Val x = ei == NONE ? wvalue_of(w.v, w.R, a.a + i) : jvalue(w, ei, et, ea);\n";
+        else
+          out << "    const Val x = wvalue_of(w.v, w.R, a.a + i);\n";
+        out << ""
                "    " << leaf_code(leaf) << "\n"
                "  }\n";
         out << "  if (fb) { w.ost = ST_FALLBACK; return ok_ret(); }\n";
@@ -232,9 +241,14 @@ struct Gen {
           if (setidx)
             out << "    w.idx = (w.idx & ~(0xFFFFull << " << 16u * P.level << ")) | ((uint64_t)" << i << " << "
                 << 16u * P.level << ");\n";
+          const uint32_t self = rs.pn_self[pn];
           out << "    { const uint32_t er = a.c == NONE ? NONE : a.c + " << i << ";\n"
-              << "      " << preload(child, "pe", "er") << "\n"
-              << "      Ret r = p" << child << "(w, a.a + " << i << ", T_UNK, er, pe);\n"
+              << "      " << preload(child, "pe", "er") << "\n";
+          if (self != NONE)
+            out << "      uint32_t et, ea; jdec(jself(w, " << u(self) << ", er), &et, &ea);\n";
+          else
+            out << "      const uint32_t et = T_UNK, ea = 0u;\n";
+          out << "      Ret r = p" << child << "(w, a.a + " << i << ", et, ea, er, pe);\n"
               << "      if (w.ost) return r;\n"
               << "      if (r.err) { if (ret_is_skip(r)) st |= FS_SKIP | ((uint32_t)r.mask << 2); else return r; }\n"
               << "      else st |= FS_APPLY; }\n";
@@ -264,11 +278,11 @@ struct Gen {
     const PEntry& E = rs.pentries[ei];
     if (E.col != NONE) {
       if (slot[ei] < 0) { ok = false; return; }  // every column entry belongs to a collected scope
-      out << "  c" << e << " = col_decode(pc[" << slot[ei] << "], &t" << e << ");\n";
+      out << "  c" << e << " = jdec(pc[" << slot[ei] << "], &t" << e << ", &a" << e << ");\n";
     } else {
       std::string key = (E.flags & EF_WILD) ? "w.keys.get(" + u(E.slot) + ")" : u(E.key);
       out << "  c" << e << " = wmap_find(w.R, " << keyexpr_rowvar << ".a, " << keyexpr_rowvar << ".b, " << key
-          << "); t" << e << " = T_UNK;\n";
+          << "); t" << e << " = T_UNK; a" << e << " = 0u;\n";
     }
   }
 
@@ -280,7 +294,7 @@ struct Gen {
     out << "  if (rn == NONE || rt != N_MAP) return mkerr(EC_NONE, 0, " << T << ");\n";
     // static (column) lookups up front: independent loads, issued together
     for (uint32_t e = 0; e < P.n; e++) {
-      out << "  uint32_t c" << e << " = NONE, t" << e << " = T_UNK;\n";
+      out << "  uint32_t c" << e << " = NONE, t" << e << " = T_UNK, a" << e << " = 0u;\n";
       const PEntry& E = rs.pentries[P.first + e];
       if (E.col != NONE) lookup(P.first + e, e, "m");
     }
@@ -309,7 +323,7 @@ struct Gen {
       const std::string c = "c" + std::to_string(e), t = "t" + std::to_string(e);
       if (E.col == NONE) lookup(P.first + e, e, "m");
       auto call = [&](const std::string& wrap) {
-        out << "    { Ret r = p" << E.child << "(w, " << c << ", " << t << ", row, pc);\n"
+        out << "    { Ret r = p" << E.child << "(w, " << c << ", " << t << ", a" << e << ", row, pc);\n"
             << "      if (w.ost) return r;\n"
             << "      if (r.err) { " << wrap << "return r; } }\n";
       };
@@ -349,7 +363,10 @@ struct Gen {
                 << "      for (uint32_t i = 0; i < a.b; i++) {\n"
                 << "        const uint32_t er = a.c == NONE ? NONE : a.c + i;\n"
                 << "        " << preload(rs.pool[E.child + 1 + j], "pe", "er") << "\n"
-                << "        Ret r = p" << rs.pool[E.child + 1 + j] << "(w, a.a + i, T_UNK, er, pe);\n"
+                << "        uint32_t et = T_UNK, ea = 0u;\n"
+                << (rs.pe_self[P.first + e] != NONE ? "        jdec(jself(w, " + u(rs.pe_self[P.first + e]) + ", er), &et, &ea);\n"
+                                                      : std::string())
+                << "        Ret r = p" << rs.pool[E.child + 1 + j] << "(w, a.a + i, et, ea, er, pe);\n"
                 << "        if (w.ost) return r;\n"
                 << "        if (!r.err) { hit = true; break; }\n"
                 << "      }\n"
@@ -421,7 +438,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
            "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
            "  const uint32_t row = (uint32_t)(hp - v.hdr);\n"
            "  " << g.preload(r, "pc", "row") << "\n"
-           "  Ret r = p" << r << "(w, 0u, (hp->flags & RF_ROOT_MAP) ? (uint32_t)N_MAP : T_UNK, row, pc);\n"
+           "  Ret r = p" << r << "(w, 0u, (hp->flags & RF_ROOT_MAP) ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
            "  jfinish(w, r, out);\n"
            "}\n";
   src << "struct JitWalker {\n"
@@ -470,11 +487,12 @@ std::vector<char> jit_compile_uncached(const std::string& src, double* seconds) 
   std::string inc = "-I" + (env ? std::string(env) : dir + "/csrc");
   std::string inc2 = "-I" + dir + "/../include";
   std::string wpe = std::string("-DKYV_JIT_WPE=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4");
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str(), wpe.c_str()};
+  std::string extra = getenv("KYV_JIT_DEFS") ? getenv("KYV_JIT_DEFS") : "-DKYV_JIT_NOEXTRA";  // experiments only
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str(), wpe.c_str(), extra.c_str()};
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "kyv_jit_walk.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     throw std::runtime_error("hiprtcCreateProgram failed");
-  hiprtcResult r = hiprtcCompileProgram(prog, 6, opts);
+  hiprtcResult r = hiprtcCompileProgram(prog, 7, opts);
   if (r != HIPRTC_SUCCESS) {
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);

@@ -60,6 +60,9 @@ struct DeviceResults {
   uint32_t* pss_slot = nullptr;
   FailRec* recs = nullptr;
   uint32_t* nrecs = nullptr;
+  FailRec* stage = nullptr;      // per-chunk staging of failing-path records (DevOut)
+  uint32_t* rbase = nullptr;
+  uint16_t* rcnt = nullptr;
   unsigned long long* counts = nullptr;
   uint32_t max_recs = 0;
   uint32_t npss = 0;
@@ -79,6 +82,7 @@ struct DeviceResults {
 
 static void free_dev_results(DeviceResults& d) {
   hipFree(d.view); hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
+  hipFree(d.stage); hipFree(d.rbase); hipFree(d.rcnt);
   hipFree(d.wl.items); hipFree(d.wl.cnt); hipFree(d.sched);
   if (d.e0) hipEventDestroy(d.e0);
   if (d.e1) hipEventDestroy(d.e1);
@@ -169,7 +173,7 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
     v.nsl_off = (const uint32_t*)(bbase + db->o_nsloff);
     v.nsl_kv = (const uint32_t*)(bbase + db->o_nslkv);
     v.gate = (const uint32_t*)(bbase + db->o_gate);
-    v.colv = (const uint32_t*)(bbase + db->o_colv);
+    v.colv = (const uint64_t*)(bbase + db->o_colv);
     v.col_off = (const uint32_t*)(bbase + db->o_coloff);
   } else {
     v.nodes = b.nodes.data(); v.hdr = b.hdr.data(); v.faux = b.faux.data();
@@ -252,6 +256,37 @@ walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, ChunkMap cm, in
   extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
   WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth};
   walk_chunks(*vp, o, wl, cm, wk);
+}
+
+// Gather the staged failing-path records of every walk chunk into one dense list: one thread per chunk, one
+// atomic per wave (its chunks' total) for the output position.
+__global__ void __launch_bounds__(256) compact_kernel(const FailRec* __restrict__ stage, const uint32_t* __restrict__ rbase,
+                                                      const uint16_t* __restrict__ rcnt, uint32_t nwaves, uint32_t nrules,
+                                                      uint32_t rule_lo, FailRec* __restrict__ out, uint32_t* __restrict__ nout,
+                                                      uint32_t max_out, const RuleDesc* __restrict__ rules) {
+  const size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const bool in = c < (size_t)nrules * nwaves;
+  const uint32_t n = in ? rcnt[c] : 0u;
+  // wave-exclusive prefix of n
+  uint32_t pre = n;
+  for (int off = 1; off < WAVE; off <<= 1) {
+    uint32_t y = __shfl_up(pre, off);
+    if ((int)lane >= off) pre += y;
+  }
+  const uint32_t tot = __shfl(pre, WAVE - 1);
+  if (!tot) return;
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(nout, tot);
+  base = __shfl(base, 0);
+  if (!n) return;
+  const uint32_t k = (uint32_t)(c / nwaves), w = (uint32_t)(c % nwaves);
+  const RuleDesc& rd = rules[k];
+  const uint32_t alts = rd.kind == RK_PATTERN ? 1u : min(rd.nalts, (uint32_t)MAX_ALTS);
+  const FailRec* src = stage + rbase[k] + (size_t)w * WAVE * alts;
+  const uint32_t at = base + pre - n;
+  for (uint32_t i = 0; i < n && at + i < max_out; i++) out[at + i] = src[i];
+  (void)rule_lo;
 }
 
 // ---------------------------------------------------------------- host entry
@@ -355,6 +390,22 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMalloc(&d.pss_slot, std::max<size_t>(4, nrules * 4)));
     HIP_OK(hipMalloc(&d.recs, (size_t)d.max_recs * sizeof(FailRec)));
     HIP_OK(hipMalloc(&d.nrecs, 4));
+    {  // staging: chunk (k, w) owns 64 * alts(k) slots
+      const size_t nwv = (nres + WAVE - 1) / WAVE;
+      std::vector<uint32_t> rb(std::max<size_t>(nrules, 1), 0);
+      size_t tot = 0;
+      for (size_t k = 0; k < nrules; k++) {
+        rb[k] = (uint32_t)tot;
+        const RuleDesc& rd = rs.rules[k];
+        size_t alts = rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, MAX_ALTS) : 0;
+        tot += alts * nwv * WAVE;
+        if (tot > 0xFFFFFFF0ull) throw std::runtime_error("batch too large for one failure-record staging buffer");
+      }
+      HIP_OK(hipMalloc(&d.stage, std::max<size_t>(tot, 1) * sizeof(FailRec)));
+      HIP_OK(hipMalloc(&d.rbase, rb.size() * 4));
+      HIP_OK(hipMemcpy(d.rbase, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
+      HIP_OK(hipMalloc(&d.rcnt, std::max<size_t>(nrules * nwv, 1) * 2));
+    }
     HIP_OK(hipMalloc(&d.counts, std::max<size_t>(8, nrules * NSTATUS * 8)));
     HIP_OK(hipMemcpy(d.pss_slot, pss_slot.data(), nrules * 4, hipMemcpyHostToDevice));
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
@@ -430,7 +481,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
                            d.sched + offs[cls][4], nseg[cls]};
     d.jit_state = (int)jit;
   }
-  DevOut o{d.status, d.pss_fails, d.pss_slot, d.recs, d.nrecs, d.max_recs, d.counts, 0, (uint32_t)nrules};
+  DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, d.rbase, d.rcnt, d.counts, 0, (uint32_t)nrules};
   int depth = ruleset_depth(rs);
   size_t lds = (size_t)depth * (sizeof(UFrame) + BLOCK * sizeof(LaneFrame));
   dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
@@ -439,6 +490,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   for (int it = 0; it < n; it++) {
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
+    HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nrules * (size_t)d.wl.nwaves, 1) * 2, stream));
     HIP_OK(hipMemsetAsync(d.counts, 0, nrules * NSTATUS * 8, stream));
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
@@ -457,6 +509,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         void* args[] = {(void*)&vp, (void*)&o, (void*)&wl, (void*)&cmj};
         HIP_OK(hipModuleLaunchKernel(dr->jfn, d.grid[1], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
+      const size_t nchunks = nrules * (size_t)d.wl.nwaves;
+      hipLaunchKernelGGL(compact_kernel, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, stream, d.stage, d.rbase, d.rcnt,
+                         d.wl.nwaves, (uint32_t)nrules, o.rule_lo, d.recs, d.nrecs, d.max_recs, (const RuleDesc*)(dr->base + dr->o_rules));
+      HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(d.e1, stream));
     HIP_OK(hipEventSynchronize(d.e1));

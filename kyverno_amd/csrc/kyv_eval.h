@@ -73,7 +73,7 @@ struct View {
   const uint32_t* nsl_kv;
   const uint32_t* gate;     // [kind class][gate_words] rule bits (batch.cpp order_by_kind)
   uint32_t gate_words;
-  const uint32_t* colv;     // path columns (kyv_layout.h): colv[col_off[c] + row]
+  const uint64_t* colv;     // path columns (kyv_layout.h): colv[col_off[c] + row]
   const uint32_t* col_off;  // (device View: pe[].col already holds col_off[col])
   // ruleset
   const RuleDesc* rules;

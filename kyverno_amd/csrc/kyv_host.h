@@ -68,7 +68,7 @@ struct Ruleset {
   std::vector<std::string> templates;  // path templates: '\x01'+slot = array index, '\x02'+slot = resolved key
   // path trie over every static lookup of every compiled pattern (kyv_layout.h "Path columns")
   struct TrieNode {
-    uint32_t col = NONE;        // column id (key edges) 
+    uint32_t col = NONE;        // column id (key edges; "[*]" nodes: the elements' self column)
     uint32_t rowspace = 0;      // row space the column / this node's lookups live in
     uint32_t star = NONE;       // "[*]" child (opens row space trie[star].rowspace)
     std::vector<std::pair<uint32_t, uint32_t>> kids;  // (key sid, child trie node)
@@ -76,6 +76,8 @@ struct Ruleset {
   std::vector<TrieNode> trie;   // trie[0] = resource root
   uint32_t ncols = 0, nrowspaces = 1;
   std::vector<uint32_t> col_rowspace;
+  std::vector<uint32_t> pn_self;  // array pnode -> self column of its elements (NONE: none)
+  std::vector<uint32_t> pe_self;  // existence entry -> self column of the candidate elements
   // runtime-compiled walk kernel (jit.cpp): generated once per ruleset, compiled on first use
   bool jit_tried = false;
   std::vector<uint8_t> jit_rules;   // rule k is walked by the compiled kernel
@@ -106,7 +108,8 @@ struct Batch {
   std::vector<uint32_t> gate;     // [kclass][gate_words] bit k: rule k can match a resource of this class
   uint32_t gate_words = 0, nclass = 0;
   // path columns (kyv_layout.h): colv[col_off[c] + row]
-  std::vector<uint32_t> colv, col_off, rs_rows;
+  std::vector<uint64_t> colv;
+  std::vector<uint32_t> col_off, rs_rows;
   std::vector<void*> dev;
   ~Batch();
 };

@@ -168,10 +168,11 @@ struct PEntry {         // 20 bytes
 };
 
 // Path columns ("columnar JSON-path tables"). Every static key path the ruleset's patterns look up is a
-// column: for each row of its row space, the resolved node (type << COL_TYPE_SHIFT | node index relative to
-// the resource root) or NONE. Row space 0 is the resource (row = resource position in the batch); every
-// pattern array position ("[*]" in the path trie) opens a row space whose rows are the elements of all
-// resource arrays at that path, numbered batch-wide; an array node's `c` holds the row of its element 0.
+// column: for each row of its row space, an 8-byte entry: low word = the resolved node (type << COL_TYPE_SHIFT |
+// node index relative to the resource root) or NONE, high word = the node's `a` (string id, first child, ...).
+// Row space 0 is the resource (row = resource position in the batch); every pattern array position ("[*]" in
+// the path trie) opens a row space whose rows are the elements of all resource arrays at that path, numbered
+// batch-wide, with a "self" column holding each element; an array node's `c` holds the row of its element 0.
 constexpr uint32_t COL_TYPE_SHIFT = 28;
 constexpr uint32_t COL_INDEX_MASK = (1u << COL_TYPE_SHIFT) - 1;
 

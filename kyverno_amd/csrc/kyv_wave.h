@@ -73,7 +73,7 @@ __device__ __forceinline__ uint32_t gld32(const uint32_t* p) { return *(const KY
 
 // Column entry of one map-entry lookup (the device entry table holds absolute column offsets in `col`)
 __device__ __forceinline__ uint32_t wcol(const View& v, const PEntry& E, bool al, uint32_t row) {
-  return al ? gld32(v.colv + (size_t)E.col + row) : NONE;
+  return al ? gld32((const uint32_t*)(v.colv + (size_t)E.col + row)) : NONE;
 }
 __device__ __forceinline__ uint32_t col_decode(uint32_t enc, uint32_t* ctype) {
   if (enc == NONE) { *ctype = T_UNK; return NONE; }
@@ -630,15 +630,38 @@ __device__ __forceinline__ bool jatom(const View& v, const Val& x, uint32_t pat,
   }
   return false;
 }
-// lookup through a path column: the device entry table holds the column's absolute offset
-__device__ __forceinline__ uint32_t jcol(const JW& w, uint32_t e, uint32_t row, uint32_t* ct) {
+constexpr uint64_t COL_NONE = 0xFFFFFFFFull;
+// raw 8-byte column entry of a lookup (speculative preload of a column scope; NONE rows give COL_NONE); the
+// device entry table holds the column's absolute offset in `col`
+__device__ __forceinline__ uint64_t jraw(const JW& w, uint32_t e, uint32_t row) {
   const uint32_t off = sld32(&w.v.pe[e].col);
-  return col_decode(row == NONE ? NONE : gld32(w.v.colv + (size_t)off + row), ct);
+  return row == NONE ? COL_NONE : *(const KYV_AS_GLOBAL uint64_t*)(w.v.colv + (size_t)off + row);
 }
-// raw column entry of a lookup (speculative preload of a column scope; NONE rows give NONE)
-__device__ __forceinline__ uint32_t jraw(const JW& w, uint32_t e, uint32_t row) {
-  const uint32_t off = sld32(&w.v.pe[e].col);
-  return row == NONE ? NONE : gld32(w.v.colv + (size_t)off + row);
+// self column (array elements) by column id
+__device__ __forceinline__ uint64_t jself(const JW& w, uint32_t col, uint32_t row) {
+  const uint32_t off = sld32(w.v.col_off + col);
+  return row == NONE ? COL_NONE : *(const KYV_AS_GLOBAL uint64_t*)(w.v.colv + (size_t)off + row);
+}
+// entry -> node index (NONE absent), type (T_UNK absent) and the node's `a`
+__device__ __forceinline__ uint32_t jdec(uint64_t x, uint32_t* t, uint32_t* a) {
+  const uint32_t lo = (uint32_t)x;
+  *a = (uint32_t)(x >> 32);
+  if (lo == NONE) { *t = T_UNK; return NONE; }
+  *t = lo >> COL_TYPE_SHIFT;
+  return lo & COL_INDEX_MASK;
+}
+// value of a node known by (index, type, a): strings, booleans and null need no row read
+__device__ __forceinline__ Val jvalue(const JW& w, uint32_t idx, uint32_t t, uint32_t a) {
+  if (idx == NONE) return wvalue_absent();
+  Val x;
+  x.wsid = NONE; x.nsid = NONE; x.sid = NONE; x.i = 0; x.f = 0;
+  switch (t) {
+    case N_STR: x.t = N_STR; x.sid = a; x.wsid = a; x.nsid = a; return x;
+    case N_TRUE: x.t = N_TRUE; x.wsid = SID_TRUE; return x;
+    case N_FALSE: x.t = N_FALSE; x.wsid = SID_FALSE; return x;
+    case N_NULL: x.t = N_NULL; x.nsid = SID_ZERO; return x;
+    default: return wvalue_node(w.v, gnode(w.R + idx));
+  }
 }
 // MatchPattern's classification (validate.go:31-56), as at the end of eval_pattern
 __device__ __forceinline__ void jfinish(const JW& w, const Ret& ret, PatOut& out) {
@@ -662,36 +685,36 @@ struct DevOut {
   uint8_t* status;         // [rule][res]
   uint32_t* pss_fails;     // [pss rule slot][res]
   const uint32_t* pss_slot;// rule -> pss slot or NONE
-  FailRec* recs;
-  uint32_t* nrecs;         // global record counter
-  uint32_t max_recs;
+  FailRec* stage;          // failing-path records, staged per walk chunk: chunk (k, w) owns 64 * alts(k) slots
+  const uint32_t* rbase;   // [nrules] first staging slot of rule k (its chunks follow, wave-major)
+  uint16_t* rcnt;          // [nrules][nwaves] records staged by chunk (k, w)
   unsigned long long* counts;  // [rule][NSTATUS]
   uint32_t rule_lo, rule_hi;   // rule range handled by this launch
 };
 
-// Failing-path records of one wave, appended with one atomic per emit point that has any record.
+// Failing-path records of one walk chunk, packed with wave ballots into the chunk's own staging slots (no
+// atomics, no waiting); compact_kernel gathers the chunks' records afterwards.
 struct WaveSink {
   FailRec* recs;
-  uint32_t* n;
-  uint32_t max;
+  uint32_t n;  // wave-uniform
   __device__ __forceinline__ void emit(bool has, const FailRec& f) {
+#ifdef KYV_EXP_NOSINK
+    return;
+#endif
     unsigned long long m = __ballot(has);
     if (!m) return;
     const uint32_t lane = threadIdx.x & (WAVE - 1);
-    const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(n, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)leader);
-    if (has) {
-      uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-      if (at < max) recs[at] = f;
-    }
+    if (has) recs[n + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = f;
+    n += (uint32_t)__popcll(m);
   }
 };
 
 // per-rule status counts: wave ballots -> one atomic per status present
 __device__ __forceinline__ void count_status(unsigned long long* counts, uint32_t k, bool active, uint8_t st) {
   // ST_NONE is not counted (the host derives it); one ballot per status value present in the wave
+#ifdef KYV_EXP_NOCOUNT
+  return;
+#endif
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint32_t s = st & 7u;
   unsigned long long m = __ballot(active && s != ST_NONE);
@@ -737,7 +760,6 @@ template <class Walker>
 __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists wl, ChunkMap cm, Walker& wk) {
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint32_t total = sld32(cm.pre + cm.nseg);
-  WaveSink sink{o.recs, o.nrecs, o.max_recs};
   for (uint32_t c = blockIdx.x; c < total; c += gridDim.x) {
     uint32_t lo = 0, hi = cm.nseg;  // segment: pre[seg] <= c < pre[seg + 1]
     while (hi - lo > 1) {
@@ -753,8 +775,11 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
     const bool active = lane < n;
     const uint32_t r = active ? wl.items[list * WAVE + lane] : 0u;
     const RuleDesc rd = sld(v.rules + k);
+    const uint32_t alts = rd.kind == RK_PATTERN ? 1u : min(rd.nalts, (uint32_t)MAX_ALTS);
+    WaveSink sink{o.stage + sld32(o.rbase + k) + (size_t)w * WAVE * alts, 0u};
     const uint8_t st = pair_walk(v, rd, active, r, k, wk, sink);
     if (active) o.status[(size_t)k * v.nres + r] = st;
+    if (sink.n && lane == 0) o.rcnt[list] = (uint16_t)sink.n;
     count_status(o.counts, k, active, st);
   }
 }
