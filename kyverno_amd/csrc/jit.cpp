@@ -434,20 +434,21 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
   // one function per pattern root (inlined into the root switch)
   for (uint32_t r : roots)
     src << "static __device__ __forceinline__ void root" << r
-        << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, PatOut& out) {\n"
+        << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, bool rootmap, PatOut& out) {\n"
            "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
            "  const uint32_t row = (uint32_t)(hp - v.hdr);\n"
            "  " << g.preload(r, "pc", "row") << "\n"
-           "  Ret r = p" << r << "(w, 0u, (hp->flags & RF_ROOT_MAP) ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
+           "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
            "  jfinish(w, r, out);\n"
            "}\n";
   src << "struct JitWalker {\n"
+         "  bool rootmap;\n"
          "  __device__ __forceinline__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp,\n"
          "                                     const RuleDesc& rd, PatOut& out) {\n"
          "    out.status = ST_NONE; out.idx = 0; out.tmpl = NONE; out.key0 = NONE; out.key1 = NONE;\n"
          "    if (!walk) return;\n"
          "    switch (root) {\n";
-  for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, out); break;\n";
+  for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, rootmap, out); break;\n";
   src << "      default: out.status = ST_FALLBACK;\n"
          "    }\n"
          "  }\n"
@@ -456,7 +457,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
          "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n"
          "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE))) kyv_jit_walk(const kyv::View* __restrict__ vp, kyv::DevOut o,\n"
          "    kyv::WorkLists wl, kyv::ChunkMap cm) {\n"
-         "  kyv::JitWalker wk;\n"
+         "  kyv::JitWalker wk{false};\n"
          "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"
          "}\n";
   return src.str();

@@ -63,6 +63,7 @@ struct DeviceResults {
   FailRec* stage = nullptr;      // per-chunk staging of failing-path records (DevOut)
   uint32_t* rbase = nullptr;
   uint16_t* rcnt = nullptr;
+  uint32_t* tsum = nullptr;      // compaction tile sums / offsets
   unsigned long long* counts = nullptr;
   uint32_t max_recs = 0;
   uint32_t npss = 0;
@@ -73,7 +74,7 @@ struct DeviceResults {
   // walk work lists (match_kernel -> walk_kernel): per rule a list of resource positions
   WorkLists wl{};                // walk work lists (kyv_wave.h)
   std::vector<uint64_t> cap;     // [nrules] work-list capacity (resources of the kind classes the gate admits)
-  uint32_t* sched = nullptr;     // chunk schedules of the two walk kernels (ChunkMap arrays)
+  uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   ChunkMap cm[2] = {};           // [0] interpreted walk kernel, [1] runtime-compiled one
   uint32_t grid[2] = {0, 0};
   int jit_state = -1;            // what the schedules were laid out for (0 interpreter only, 1 with the jit kernel)
@@ -82,7 +83,7 @@ struct DeviceResults {
 
 static void free_dev_results(DeviceResults& d) {
   hipFree(d.view); hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
-  hipFree(d.stage); hipFree(d.rbase); hipFree(d.rcnt);
+  hipFree(d.stage); hipFree(d.rbase); hipFree(d.rcnt); hipFree(d.tsum);
   hipFree(d.wl.items); hipFree(d.wl.cnt); hipFree(d.sched);
   if (d.e0) hipEventDestroy(d.e0);
   if (d.e1) hipEventDestroy(d.e1);
@@ -236,7 +237,11 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
     const RuleDesc& rdk = v.rules[k];
     if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {  // this wave's work list for rule k
       const size_t list = (size_t)k * wl.nwaves + blockIdx.x;
-      if (walk) wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] = r;
+      if (walk) {
+        const ResHeader& h = v.hdr[r];
+        wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
+            make_uint2(r | ((h.flags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), h.root);
+      }
       if (lane == 0) wl.cnt[list] = (uint8_t)__popcll(wm);
     }
     if (gated && !walk && st != ST_NONE) {
@@ -254,39 +259,69 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_WPE)))
 walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, ChunkMap cm, int depth) {
   extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
-  WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth};
+  WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth, false};
   walk_chunks(*vp, o, wl, cm, wk);
 }
 
-// Gather the staged failing-path records of every walk chunk into one dense list: one thread per chunk, one
-// atomic per wave (its chunks' total) for the output position.
-__global__ void __launch_bounds__(256) compact_kernel(const FailRec* __restrict__ stage, const uint32_t* __restrict__ rbase,
-                                                      const uint16_t* __restrict__ rcnt, uint32_t nwaves, uint32_t nrules,
-                                                      uint32_t rule_lo, FailRec* __restrict__ out, uint32_t* __restrict__ nout,
-                                                      uint32_t max_out, const RuleDesc* __restrict__ rules) {
-  const size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const bool in = c < (size_t)nrules * nwaves;
-  const uint32_t n = in ? rcnt[c] : 0u;
-  // wave-exclusive prefix of n
-  uint32_t pre = n;
+// Gather the staged failing-path records of every walk chunk into one dense list, without atomics:
+//   compact_sum_kernel   one wave per 64 consecutive chunks: the tile's record total;
+//   compact_scan_kernel  exclusive prefix over the tiles (one workgroup) and the grand total;
+//   compact_copy_kernel  one wave per tile: wave prefix of the chunks' counts, then the wave copies each
+//                        non-empty chunk's records cooperatively (lane i moves record i).
+__device__ __forceinline__ const FailRec* chunk_stage(const FailRec* stage, const uint32_t* rbase, const RuleDesc* rules,
+                                                      uint32_t nwaves, size_t c) {
+  const uint32_t k = (uint32_t)(c / nwaves), w = (uint32_t)(c % nwaves);
+  const uint32_t alts = rules[k].kind == RK_PATTERN ? 1u : min(rules[k].nalts, (uint32_t)MAX_ALTS);
+  return stage + rbase[k] + (size_t)w * WAVE * alts;
+}
+__global__ void __launch_bounds__(WAVE) compact_sum_kernel(const uint16_t* __restrict__ rcnt, size_t total,
+                                                           uint32_t* __restrict__ tsum) {
+  const size_t c = (size_t)blockIdx.x * WAVE + threadIdx.x;
+  uint32_t n = c < total ? rcnt[c] : 0u;
+  for (int off = WAVE / 2; off > 0; off >>= 1) n += __shfl_xor(n, off);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = n;
+}
+__global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict__ tsum, uint32_t ntiles,
+                                                            uint32_t* __restrict__ nout) {
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x, per = (ntiles + 1023) / 1024;
+  const uint32_t lo = t * per, hi = min(ntiles, lo + per);
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; i++) sum += tsum[i];
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t y = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += y;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (uint32_t i = lo; i < hi; i++) { uint32_t x = tsum[i]; tsum[i] = run; run += x; }
+  if (t == 1023) *nout = part[1023];
+}
+__global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __restrict__ stage, const uint32_t* __restrict__ rbase,
+                                                            const uint16_t* __restrict__ rcnt, const RuleDesc* __restrict__ rules,
+                                                            uint32_t nwaves, size_t total, const uint32_t* __restrict__ tbase,
+                                                            FailRec* __restrict__ out, uint32_t max_out) {
+  const uint32_t lane = threadIdx.x;
+  const size_t c = (size_t)blockIdx.x * WAVE + lane;
+  const uint32_t n = c < total ? rcnt[c] : 0u;
+  uint32_t pre = n;  // inclusive wave prefix
   for (int off = 1; off < WAVE; off <<= 1) {
     uint32_t y = __shfl_up(pre, off);
     if ((int)lane >= off) pre += y;
   }
-  const uint32_t tot = __shfl(pre, WAVE - 1);
-  if (!tot) return;
-  uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(nout, tot);
-  base = __shfl(base, 0);
-  if (!n) return;
-  const uint32_t k = (uint32_t)(c / nwaves), w = (uint32_t)(c % nwaves);
-  const RuleDesc& rd = rules[k];
-  const uint32_t alts = rd.kind == RK_PATTERN ? 1u : min(rd.nalts, (uint32_t)MAX_ALTS);
-  const FailRec* src = stage + rbase[k] + (size_t)w * WAVE * alts;
-  const uint32_t at = base + pre - n;
-  for (uint32_t i = 0; i < n && at + i < max_out; i++) out[at + i] = src[i];
-  (void)rule_lo;
+  const uint32_t base = tbase[blockIdx.x];
+  unsigned long long m = __ballot(n != 0);
+  while (m) {
+    const int j = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const uint32_t nj = __shfl(n, j), at = base + __shfl(pre, j) - nj;
+    const FailRec* src = chunk_stage(stage, rbase, rules, nwaves, (size_t)blockIdx.x * WAVE + j);
+    for (uint32_t i = lane; i < nj; i += WAVE)
+      if (at + i < max_out) out[at + i] = src[i];
+  }
 }
 
 // ---------------------------------------------------------------- host entry
@@ -405,6 +440,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipMalloc(&d.rbase, rb.size() * 4));
       HIP_OK(hipMemcpy(d.rbase, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
       HIP_OK(hipMalloc(&d.rcnt, std::max<size_t>(nrules * nwv, 1) * 2));
+      HIP_OK(hipMalloc(&d.tsum, std::max<size_t>((nrules * nwv + WAVE - 1) / WAVE, 1) * 4));
     }
     HIP_OK(hipMalloc(&d.counts, std::max<size_t>(8, nrules * NSTATUS * 8)));
     HIP_OK(hipMemcpy(d.pss_slot, pss_slot.data(), nrules * 4, hipMemcpyHostToDevice));
@@ -415,7 +451,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMemcpy(d.view, &v, sizeof(View), hipMemcpyHostToDevice));
     // walk work lists: one 64-slot list per (rule, match wave)
     d.wl.nwaves = (uint32_t)((nres + WAVE - 1) / WAVE);
-    HIP_OK(hipMalloc(&d.wl.items, std::max<size_t>(1, nrules * (size_t)d.wl.nwaves * WAVE) * 4));
+    HIP_OK(hipMalloc(&d.wl.items, std::max<size_t>(1, nrules * (size_t)d.wl.nwaves * WAVE) * sizeof(uint2)));
     HIP_OK(hipMalloc(&d.wl.cnt, std::max<size_t>(4, nrules * (size_t)d.wl.nwaves + 4)));
     // persistent grid: enough waves to fill the chip several times over, never more than the chunks
     int cus = 256;
@@ -439,12 +475,8 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         for (uint32_t i = 0; i < gw; i++) g[i] |= b.gate[(size_t)b.hdr[r].kclass * gw + i];
       if (runs.empty() || runs.back().second != g) runs.push_back({w, g});
     }
-    std::vector<uint32_t> buf;
-    size_t offs[2][5];
-    uint32_t nseg[2];
+    std::vector<uint2> slots[2];
     for (int cls = 0; cls < 2; cls++) {
-      std::vector<uint32_t> pre{0}, w0, first, cnt, rl;
-      uint64_t slots = 0;
       for (size_t ri = 0; ri < runs.size(); ri++) {
         const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
         std::vector<uint32_t> ks;
@@ -455,30 +487,21 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
           ks.push_back((uint32_t)k);
         }
         for (size_t i = 0; i < ks.size(); i += WIN) {
-          uint32_t n = (uint32_t)std::min<size_t>(WIN, ks.size() - i);
-          w0.push_back(wb);
-          first.push_back((uint32_t)rl.size());
-          cnt.push_back(n);
-          rl.insert(rl.end(), ks.begin() + i, ks.begin() + i + n);
-          slots += (uint64_t)(we - wb) * n;
-          if (slots > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
-          pre.push_back((uint32_t)slots);
+          const size_t n = std::min<size_t>(WIN, ks.size() - i);
+          for (uint32_t w = wb; w < we; w++)
+            for (size_t t = i; t < i + n; t++) slots[cls].push_back(make_uint2(ks[t], w));
         }
       }
-      nseg[cls] = (uint32_t)w0.size();
-      offs[cls][0] = buf.size(); buf.insert(buf.end(), pre.begin(), pre.end());
-      offs[cls][1] = buf.size(); buf.insert(buf.end(), w0.begin(), w0.end()); buf.push_back(0);
-      offs[cls][2] = buf.size(); buf.insert(buf.end(), first.begin(), first.end()); buf.push_back(0);
-      offs[cls][3] = buf.size(); buf.insert(buf.end(), cnt.begin(), cnt.end()); buf.push_back(0);
-      offs[cls][4] = buf.size(); buf.insert(buf.end(), rl.begin(), rl.end()); buf.push_back(0);
-      d.grid[cls] = (uint32_t)std::min<uint64_t>(slots, (uint64_t)d.cus * 64);
+      if (slots[cls].size() > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
+      d.grid[cls] = (uint32_t)std::min<size_t>(slots[cls].size(), (size_t)d.cus * 64);
     }
     hipFree(d.sched);
-    HIP_OK(hipMalloc(&d.sched, buf.size() * 4));
-    HIP_OK(hipMemcpy(d.sched, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
-    for (int cls = 0; cls < 2; cls++)
-      d.cm[cls] = ChunkMap{d.sched + offs[cls][0], d.sched + offs[cls][1], d.sched + offs[cls][2], d.sched + offs[cls][3],
-                           d.sched + offs[cls][4], nseg[cls]};
+    const size_t n0 = slots[0].size(), n1 = slots[1].size();
+    HIP_OK(hipMalloc(&d.sched, std::max<size_t>(1, n0 + n1) * sizeof(uint2)));
+    if (n0) HIP_OK(hipMemcpy(d.sched, slots[0].data(), n0 * sizeof(uint2), hipMemcpyHostToDevice));
+    if (n1) HIP_OK(hipMemcpy(d.sched + n0, slots[1].data(), n1 * sizeof(uint2), hipMemcpyHostToDevice));
+    d.cm[0] = ChunkMap{d.sched, (uint32_t)n0};
+    d.cm[1] = ChunkMap{d.sched + n0, (uint32_t)n1};
     d.jit_state = (int)jit;
   }
   DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, d.rbase, d.rcnt, d.counts, 0, (uint32_t)nrules};
@@ -510,8 +533,12 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         HIP_OK(hipModuleLaunchKernel(dr->jfn, d.grid[1], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
       const size_t nchunks = nrules * (size_t)d.wl.nwaves;
-      hipLaunchKernelGGL(compact_kernel, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, stream, d.stage, d.rbase, d.rcnt,
-                         d.wl.nwaves, (uint32_t)nrules, o.rule_lo, d.recs, d.nrecs, d.max_recs, (const RuleDesc*)(dr->base + dr->o_rules));
+      const uint32_t ntiles = (uint32_t)((nchunks + WAVE - 1) / WAVE);
+      const RuleDesc* drules = (const RuleDesc*)(dr->base + dr->o_rules);
+      hipLaunchKernelGGL(compact_sum_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.rcnt, nchunks, d.tsum);
+      hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, d.tsum, ntiles, d.nrecs);
+      hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, d.rbase, d.rcnt, drules,
+                         d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs);
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(d.e1, stream));

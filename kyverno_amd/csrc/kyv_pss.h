@@ -530,7 +530,7 @@ KYV_HD uint8_t eval_pair(const View& v, bool active, uint32_t r, uint32_t k, Wal
   uint8_t st = pair_dispatch(v, active, r, k, pss_fails, &walk);
   const RuleDesc& rd = v.rules[k];
   if (rd.kind != RK_PATTERN && rd.kind != RK_ANYPATTERN) return st;
-  uint8_t ws = pair_walk(v, rd, walk, r, k, wk, sink);
+  uint8_t ws = pair_walk(v, rd, walk, r, k, walk ? v.nodes + v.hdr[r].root : nullptr, wk, sink);
   return walk ? ws : st;
 }
 

@@ -24,10 +24,10 @@ struct HostWalker {
 };
 
 template <class Sink, class Walker>
-KYV_HD uint8_t pair_walk(const View& v, const RuleDesc& rd, bool walk, uint32_t r, uint32_t k, Walker& wk, Sink& sink) {
+KYV_HD uint8_t pair_walk(const View& v, const RuleDesc& rd, bool walk, uint32_t r, uint32_t k, const Node* R, Walker& wk,
+                         Sink& sink) {
   uint8_t st = ST_NONE;
-  const ResHeader* hp = walk ? &v.hdr[r] : nullptr;
-  const Node* R = walk ? v.nodes + hp->root : nullptr;
+  const ResHeader* hp = walk ? v.hdr + r : nullptr;  // address only; walkers read it for metadata expansion
   const uint32_t nalts = rd.kind == RK_PATTERN ? 1 : rd.nalts;  // uniform across the wave
   uint32_t nfail = 0, nskip = 0;
   for (uint32_t a = 0; a < nalts; a++) {

@@ -239,6 +239,7 @@ struct WaveWalker {
   LaneFrame* lf;   // LDS, [cap][64]
   UFrame* uf;      // LDS, [cap]
   int cap;
+  bool rootmap;    // per lane (unused by the interpreter)
 
   __device__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp, const RuleDesc& rd,
                       PatOut& out) {
@@ -730,8 +731,9 @@ __device__ __forceinline__ void count_status(unsigned long long* counts, uint32_
 // Walk work lists, written by match_kernel without atomics: for rule k and match wave w (64 consecutive
 // resources of the kind-major batch), cnt[k][w] pairs need the walk and items[k][w][0..cnt) are their resource
 // positions (compacted with a ballot prefix).
+constexpr uint32_t ITEM_ROOT_MAP = 1u << 31;  // items[].x: resource position | root-is-a-map flag
 struct WorkLists {
-  uint32_t* items;   // [nrules][nwaves][64]
+  uint2* items;      // [nrules][nwaves][64]: (resource position | ITEM_ROOT_MAP, node offset of its root)
   uint8_t* cnt;      // [nrules][nwaves]
   uint32_t nwaves;
 };
@@ -740,18 +742,12 @@ __device__ __forceinline__ uint32_t sld8(const uint8_t* p) {  // scalar load of 
   return (sld32((const uint32_t*)(a & ~(size_t)3)) >> (8 * (a & 3))) & 0xFFu;
 }
 
-// Chunk schedule of a walk kernel, laid out on the host: segments of (run of match waves with the same gated
-// rule set) x (window of a few of those rules); a segment's slots run wave-major with the window's rules
-// fastest, so the waves resident at one time walk the same 64 resources under the few rules of one window:
-// node rows and columns are reused from L2 across those rules, and the window's code stays in the
-// instruction cache. Chunks whose work list is empty (no pair matched) are skipped.
+// Chunk schedule of a walk kernel, laid out on the host as one (rule, match wave) pair per slot: runs of match
+// waves with the same gated rule set, each run wave-major with its rules in windows of a few rules. Slots whose
+// work list is empty (no pair matched) are skipped.
 struct ChunkMap {
-  const uint32_t* pre;    // [nseg + 1] first slot of each segment
-  const uint32_t* w0;     // [nseg] first match wave of the segment
-  const uint32_t* first;  // [nseg] first entry of the segment's rules in `rules`
-  const uint32_t* cnt;    // [nseg] rules in the segment
-  const uint32_t* rules;  // rule ids
-  uint32_t nseg;
+  const uint2* slots;  // [total] (rule, match wave)
+  uint32_t total;
 };
 
 // Grid-stride over the schedule; every wave walks ONE rule over the (up to 64) resources of one work list;
@@ -759,25 +755,21 @@ struct ChunkMap {
 template <class Walker>
 __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists wl, ChunkMap cm, Walker& wk) {
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const uint32_t total = sld32(cm.pre + cm.nseg);
-  for (uint32_t c = blockIdx.x; c < total; c += gridDim.x) {
-    uint32_t lo = 0, hi = cm.nseg;  // segment: pre[seg] <= c < pre[seg + 1]
-    while (hi - lo > 1) {
-      uint32_t mid = (lo + hi) >> 1;
-      if (sld32(cm.pre + mid) <= c) lo = mid; else hi = mid;
-    }
-    const uint32_t local = c - sld32(cm.pre + lo), nw = sld32(cm.cnt + lo);
-    const uint32_t w = sld32(cm.w0 + lo) + local / nw;
-    const uint32_t k = sld32(cm.rules + sld32(cm.first + lo) + local % nw);
+  for (uint32_t c = blockIdx.x; c < cm.total; c += gridDim.x) {
+    const uint2 kw = sld(cm.slots + c);
+    const uint32_t k = kw.x, w = kw.y;
     const size_t list = (size_t)k * wl.nwaves + w;
     const uint32_t n = sld8(wl.cnt + list);
     if (!n) continue;
     const bool active = lane < n;
-    const uint32_t r = active ? wl.items[list * WAVE + lane] : 0u;
+    uint2 it = make_uint2(0u, 0u);
+    if (active) it = wl.items[list * WAVE + lane];
+    const uint32_t r = it.x & ~ITEM_ROOT_MAP;
+    wk.rootmap = (it.x & ITEM_ROOT_MAP) != 0;
     const RuleDesc rd = sld(v.rules + k);
     const uint32_t alts = rd.kind == RK_PATTERN ? 1u : min(rd.nalts, (uint32_t)MAX_ALTS);
     WaveSink sink{o.stage + sld32(o.rbase + k) + (size_t)w * WAVE * alts, 0u};
-    const uint8_t st = pair_walk(v, rd, active, r, k, wk, sink);
+    const uint8_t st = pair_walk(v, rd, active, r, k, v.nodes + it.y, wk, sink);
     if (active) o.status[(size_t)k * v.nres + r] = st;
     if (sink.n && lane == 0) o.rcnt[list] = (uint16_t)sink.n;
     count_status(o.counts, k, active, st);
