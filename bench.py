@@ -204,7 +204,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": "profiles/%s_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, bytes "
                                            "per launch)" % pmc_tag if traffic else None,
-                         "bytes_per_eval": bytes_per_eval, "kernel": "eval_kernel", "kernel_ms": kernel_ms,
+                         "bytes_per_eval": bytes_per_eval,
+                         "kernel": "one evaluation: match_kernel + walk kernels (kyv_jit_walk) + record compaction",
+                         "kernel_ms": kernel_ms,
                          "kernel_ms_max_rank": kernel_ms_max},
             "cpu_baseline": cpu,
             "verdicts": {k: v for k, v in counts.items()},

@@ -18,7 +18,11 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "eval_kernel"
+EVAL = ("kyv", "kyv_jit_walk")  # kernels of one evaluation: kyv::match_kernel, walk kernels, compaction
+
+
+def is_eval(name):
+    return name.startswith("kyv::") or name.startswith("kyv_jit")
 
 
 def main(tag):
@@ -26,19 +30,20 @@ def main(tag):
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, tag + "_kernel_stats.csv"))
-    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
-    krow = [r for r in stats if KERNEL in r["Name"]][0]
-    counters = {}
+    stats = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))) if is_eval(r["Name"])]
+    per_kernel = {r["Name"].split("(")[0]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])} for r in stats}
+    counters = {}  # kernel -> counter -> values
     rows_out = []
     for p in sorted(os.listdir(src)):
         f = os.path.join(src, p, "run_counter_collection.csv")
         if not p.startswith("pmc_") or not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            if KERNEL not in r["Kernel_Name"]:
+            if not is_eval(r["Kernel_Name"]):
                 continue
-            counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-            rows_out.append({"pass": p, "dispatch": r["Dispatch_Id"], "counter": r["Counter_Name"],
+            kn = r["Kernel_Name"].split("(")[0]
+            counters.setdefault(kn, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            rows_out.append({"pass": p, "dispatch": r["Dispatch_Id"], "kernel": kn, "counter": r["Counter_Name"],
                              "value": r["Counter_Value"], "grid": r["Grid_Size"], "wg": r["Workgroup_Size"],
                              "lds": r["LDS_Block_Size"], "vgpr": r["VGPR_Count"], "sgpr": r["SGPR_Count"],
                              "ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
@@ -46,30 +51,32 @@ def main(tag):
         w = csv.DictWriter(fh, fieldnames=list(rows_out[0].keys()) if rows_out else ["pass"])
         w.writeheader()
         w.writerows(rows_out)
-    avg = {k: sum(v) / len(v) for k, v in counters.items()}
-    fetch = avg.get("FETCH_SIZE", 0.0) * 1024
-    write = avg.get("WRITE_SIZE", 0.0) * 1024
+    avg = {kn: {c: sum(v) / len(v) for c, v in cs.items()} for kn, cs in counters.items()}
+    fetch = sum(a.get("FETCH_SIZE", 0.0) for a in avg.values()) * 1024
+    write = sum(a.get("WRITE_SIZE", 0.0) for a in avg.values()) * 1024
+    eval_ns = sum(k["avg_ns"] for k in per_kernel.values())
+    dom = max(per_kernel.items(), key=lambda kv: kv[1]["avg_ns"])[0] if per_kernel else None
     out = {
         "tag": tag,
-        "kernel": krow["Name"],
-        "launches": int(krow["Calls"]),
-        "avg_ns": float(krow["AverageNs"]),
+        "kernels": per_kernel,
+        "eval_avg_ns": eval_ns,
+        "dominant_kernel": dom,
         "counters_avg_per_launch": avg,
         "fetch_bytes_raw": fetch,
         "write_bytes_raw": write,
-        "traffic_bytes_raw": fetch + write,
         "traffic_bytes": fetch + write,
         "traffic_bytes_x2read": 2 * fetch + write,
-        "traffic_note": "memory-side bytes per launch from TCC_EA (FETCH_SIZE + WRITE_SIZE, KiB x 1024); "
-                        "traffic_bytes_x2read applies the guide's x2 wide-stream read correction (upper estimate)",
+        "traffic_note": "memory-side bytes of one evaluation (all its kernels) from TCC_EA (FETCH_SIZE + WRITE_SIZE, "
+                        "KiB x 1024); traffic_bytes_x2read applies the guide's x2 wide-stream read correction",
     }
-    if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
-        out["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
-    if "SQ_WAVE_CYCLES" in avg:
-        out["wait_frac"] = avg.get("SQ_WAIT_ANY", 0) / avg["SQ_WAVE_CYCLES"]
-        out["active_frac"] = avg.get("SQ_ACTIVE_INST_ANY", 0) / avg["SQ_WAVE_CYCLES"]
-        if "GRBM_GUI_ACTIVE" in avg:
-            out["clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / (out["avg_ns"])
+    if dom and dom in avg:
+        d = avg[dom]
+        if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
+            out["dominant_l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
+        if "SQ_WAVE_CYCLES" in d:
+            out["dominant_wait_frac"] = d.get("SQ_WAIT_ANY", 0) / d["SQ_WAVE_CYCLES"]
+            if "GRBM_GUI_ACTIVE" in d:
+                out["clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8 / per_kernel[dom]["avg_ns"]
     log = os.path.join(src, "bench_trace.log")
     if os.path.exists(log):
         for line in open(log):
