@@ -585,6 +585,7 @@ struct Resolver {
       next[space] += mn.b;
       if (colv) {
         R[m].c = base;
+        colv[(size_t)col_off[T.lencol] + row] = (uint64_t)mn.b | ((uint64_t)base << 32);
         const size_t self = col_off[rs.trie[T.star].col];
         for (uint32_t i = 0; i < mn.b; i++) colv[self + base + i] = entry(mn.a + i);
       }

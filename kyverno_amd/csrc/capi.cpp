@@ -80,7 +80,7 @@ int64_t kyv_ruleset_jit_source(const kyv_ruleset* rs, char* buf, size_t cap, uin
   try {
     std::vector<uint8_t> jr;
     std::string src = jit_source(*rs->rs, &jr);
-    if (nrules_jit) { *nrules_jit = 0; for (auto x : jr) *nrules_jit += x; }
+    if (nrules_jit) { *nrules_jit = 0; for (auto x : jr) *nrules_jit += x ? 1 : 0; }
     if (buf && cap) { size_t n = std::min(cap - 1, src.size()); memcpy(buf, src.data(), n); buf[n] = 0; }
     return (int64_t)src.size();
   } catch (std::exception& e) {

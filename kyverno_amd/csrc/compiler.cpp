@@ -1133,6 +1133,8 @@ struct TrieBuilder {
     rs.trie[id].col = rs.ncols++;  // self column of the elements
     rs.col_rowspace.push_back(rs.trie[id].rowspace);
     rs.trie[t].star = id;
+    rs.trie[t].lencol = rs.ncols++;  // (count, element-0 row) of the arrays at t
+    rs.col_rowspace.push_back(rs.trie[t].rowspace);
     return id;
   }
   // t == NONE: the pattern position has no static path (below a wildcard key): lookups binary-search
@@ -1153,6 +1155,7 @@ struct TrieBuilder {
           if (E.handler == H_EXISTENCE) {
             uint32_t st = ct == NONE ? NONE : star(ct);
             rs.pe_self[P.first + e] = st == NONE ? NONE : rs.trie[st].col;
+            rs.pe_len[P.first + e] = st == NONE ? NONE : rs.trie[ct].lencol;
             uint32_t npat = rs.pool[E.child];
             for (uint32_t j = 0; j < npat; j++) walk(rs.pool[E.child + 1 + j], st, guard + 1);
           } else {
@@ -1163,17 +1166,20 @@ struct TrieBuilder {
       case P_ARR_MAPS: {
         uint32_t st = t == NONE ? NONE : star(t);
         rs.pn_self[pn] = st == NONE ? NONE : rs.trie[st].col;
+        rs.pn_len[pn] = st == NONE ? NONE : rs.trie[t].lencol;
         walk(P.first, st, guard + 1);
         break;
       }
       case P_ARR_SCALAR: {  // element values through the self column
         uint32_t st = t == NONE ? NONE : star(t);
         rs.pn_self[pn] = st == NONE ? NONE : rs.trie[st].col;
+        rs.pn_len[pn] = st == NONE ? NONE : rs.trie[t].lencol;
         break;
       }
       case P_ARR_POS: {
         uint32_t st = t == NONE ? NONE : star(t);
         rs.pn_self[pn] = st == NONE ? NONE : rs.trie[st].col;
+        rs.pn_len[pn] = st == NONE ? NONE : rs.trie[t].lencol;
         for (uint32_t i = 0; i < P.n; i++) walk(rs.pool[P.first + i], st, guard + 1);
         break;
       }
@@ -1217,6 +1223,8 @@ void build_path_trie(Ruleset& rs) {
   for (auto& P : rs.pnodes) P.flags &= (uint8_t)~PF_NEEDROW;
   rs.pn_self.assign(rs.pnodes.size(), NONE);
   rs.pe_self.assign(rs.pentries.size(), NONE);
+  rs.pn_len.assign(rs.pnodes.size(), NONE);
+  rs.pe_len.assign(rs.pentries.size(), NONE);
   TrieBuilder tb{rs, std::vector<uint32_t>(rs.pnodes.size(), TrieBuilder::UNSET)};
   for (auto& rd : rs.rules) {
     if (rd.kind == RK_PATTERN) tb.walk(rd.root, 0, 0);

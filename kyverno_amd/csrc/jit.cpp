@@ -36,28 +36,46 @@ struct Gen {
   std::ostringstream out;
   std::vector<uint8_t> emitted;  // pnode -> function emitted
   bool ok = true;                // pattern compilable (else the rule stays on the interpreter)
+  const bool use_len = getenv("KYV_JIT_LEN") && atoi(getenv("KYV_JIT_LEN")) != 0;  // array lengths via columns (measured slower: off)
 
   // Column scopes: the pattern root and every array-element pattern open a scope (one row of one row space);
   // every column lookup of the maps inside a scope (not crossing into array elements) is loaded up front by
   // the scope's caller into `pc[]`, so a scope costs one round of independent loads however deep its maps nest.
-  std::vector<int> slot;                         // pentry -> index in its scope's pc[], -1 none
-  std::vector<std::vector<uint32_t>> scope_of;   // scope-root pnode -> its column entries (pentry ids)
+  std::vector<int> slot;                         // pentry -> index of its column in its scope's pc[], -1 none
+  std::vector<int> slot_alen;                    // array pnode -> index of its length column in pc[], -1 none
+  std::vector<int> slot_elen;                    // existence entry -> index of the candidates' length column
+  std::vector<std::vector<uint32_t>> scope_of;   // scope-root pnode -> its column ids, in pc[] order
   std::vector<uint8_t> scoped;                   // pnode -> scope collected
 
   explicit Gen(const Ruleset& r)
-      : rs(r), emitted(r.pnodes.size(), 0), slot(r.pentries.size(), -1), scope_of(r.pnodes.size()), scoped(r.pnodes.size(), 0) {}
+      : rs(r), emitted(r.pnodes.size(), 0), slot(r.pentries.size(), -1), slot_alen(r.pnodes.size(), -1),
+        slot_elen(r.pentries.size(), -1), scope_of(r.pnodes.size()), scoped(r.pnodes.size(), 0) {}
 
+  int add(std::vector<uint32_t>& list, uint32_t col) {
+    list.push_back(col);
+    return (int)list.size() - 1;
+  }
   void collect(uint32_t pn, std::vector<uint32_t>& list, int guard) {
     if (pn == NONE || pn >= rs.pnodes.size() || guard > 4 * MAX_DEPTH) return;
     const PNode& P = rs.pnodes[pn];
+    if (P.kind == P_ARR_MAPS || P.kind == P_ARR_POS || P.kind == P_ARR_SCALAR) {  // the array's own length entry
+      if (rs.pn_len[pn] != NONE && use_len) {
+        if (slot_alen[pn] >= 0) { ok = false; return; }
+        slot_alen[pn] = add(list, rs.pn_len[pn]);
+      }
+      return;  // its elements open their own scopes
+    }
     if (P.kind != P_MAP) return;
     for (uint32_t e = 0; e < P.n; e++) {
       const uint32_t ei = P.first + e;
       const PEntry& E = rs.pentries[ei];
       if (E.col != NONE) {
         if (slot[ei] >= 0) { ok = false; continue; }  // entry reached from two scopes: leave the rule interpreted
-        slot[ei] = (int)list.size();
-        list.push_back(ei);
+        slot[ei] = add(list, E.col);
+      }
+      if (E.handler == H_EXISTENCE && rs.pe_len[ei] != NONE && use_len) {
+        if (slot_elen[ei] >= 0) { ok = false; continue; }
+        slot_elen[ei] = add(list, rs.pe_len[ei]);
       }
       if (E.handler == H_STAR || E.handler == H_NEGATION || E.handler == H_EXIST_BADPAT || E.handler == H_EXISTENCE ||
           E.child == NONE)
@@ -102,7 +120,7 @@ struct Gen {
     const auto& L = scope_of[root];
     std::ostringstream o;
     o << "uint64_t " << name << "[" << std::max<size_t>(1, L.size()) << "];";
-    for (size_t i = 0; i < L.size(); i++) o << " " << name << "[" << i << "] = jraw(w, " << u(L[i]) << ", " << rowx << ");";
+    for (size_t i = 0; i < L.size(); i++) o << " " << name << "[" << i << "] = jself(w, " << u(L[i]) << ", " << rowx << ");";
     return o.str();
   }
 
@@ -215,46 +233,44 @@ struct Gen {
         break;
       case P_ARR_SCALAR: {
         uint32_t leaf = rs.pnodes[P.first].first;
-        out << "  if (rn == NONE) return mkerr(EC_NONE, 0, " << T << ");\n";
-        out << "  const Node a = gnode(w.R + rn);\n  if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << T << ");\n";
+        array_head(pn, T);
         out << "  bool fb = false, okv = true;\n";
         const uint32_t self = rs.pn_self[pn];
-        out << "  for (uint32_t i = 0; i < a.b && okv; i++) {\n";
+        out << "  for (uint32_t i = 0; i < cnt && okv; i++) {\n";
         if (self != NONE)
-          out << "    uint32_t et, ea; const uint32_t ei = jdec(jself(w, " << u(self) << ", a.c == NONE ? NONE : a.c + i), &et, &ea);\n"
-                 "    const Val x = ei == NONE ? wvalue_of(w.v, w.R, a.a + i) : jvalue(w, ei, et, ea);\n";
+          out << "    uint32_t et, ea; const uint32_t ei = jdec(jself(w, " << u(self) << ", eb == NONE ? NONE : eb + i), &et, &ea);\n"
+                 "    const Val x = ei == NONE ? wvalue_of(w.v, w.R, aa + i) : jvalue(w, ei, et, ea);\n";
         else
-          out << "    const Val x = wvalue_of(w.v, w.R, a.a + i);\n";
-        out << ""
-               "    " << leaf_code(leaf) << "\n"
+          out << "    const Val x = wvalue_of(w.v, w.R, aa + i);\n";
+        out << "    " << leaf_code(leaf) << "\n"
                "  }\n";
         out << "  if (fb) { w.ost = ST_FALLBACK; return ok_ret(); }\n";
         out << "  return okv ? ok_ret() : mkerr(EC_NONE, 0, " << T << ");\n";
         break;
       }
       case P_ARR_MAPS: case P_ARR_POS: {
-        out << "  if (rn == NONE) return mkerr(EC_NONE, 0, " << T << ");\n";
-        out << "  const Node a = gnode(w.R + rn);\n  if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << T << ");\n";
-        if (P.kind == P_ARR_POS) out << "  if (a.b < " << u(P.n) << ") return mkerr(EC_NONE, 0, NONE);\n";
+        array_head(pn, T);
+        if (P.kind == P_ARR_POS) out << "  if (cnt < " << u(P.n) << ") return mkerr(EC_NONE, 0, NONE);\n";
         out << "  uint32_t st = 0;\n";
+        const uint32_t self = rs.pn_self[pn];
         auto elem = [&](const std::string& i, uint32_t child, bool setidx) {
           if (setidx)
             out << "    w.idx = (w.idx & ~(0xFFFFull << " << 16u * P.level << ")) | ((uint64_t)" << i << " << "
                 << 16u * P.level << ");\n";
-          const uint32_t self = rs.pn_self[pn];
-          out << "    { const uint32_t er = a.c == NONE ? NONE : a.c + " << i << ";\n"
+          out << "    { const uint32_t er = eb == NONE ? NONE : eb + " << i << ";\n"
               << "      " << preload(child, "pe", "er") << "\n";
           if (self != NONE)
-            out << "      uint32_t et, ea; jdec(jself(w, " << u(self) << ", er), &et, &ea);\n";
+            out << "      uint32_t et, ea; uint32_t ei = jdec(jself(w, " << u(self) << ", er), &et, &ea);\n"
+                   "      if (ei == NONE) { ei = aa + " << i << "; et = T_UNK; }\n";
           else
-            out << "      const uint32_t et = T_UNK, ea = 0u;\n";
-          out << "      Ret r = p" << child << "(w, a.a + " << i << ", et, ea, er, pe);\n"
+            out << "      const uint32_t ei = aa + " << i << ", et = T_UNK, ea = 0u;\n";
+          out << "      Ret r = p" << child << "(w, ei, et, ea, er, pe);\n"
               << "      if (w.ost) return r;\n"
               << "      if (r.err) { if (ret_is_skip(r)) st |= FS_SKIP | ((uint32_t)r.mask << 2); else return r; }\n"
               << "      else st |= FS_APPLY; }\n";
         };
         if (P.kind == P_ARR_MAPS) {
-          out << "  for (uint32_t i = 0; i < a.b; i++) {\n";
+          out << "  for (uint32_t i = 0; i < cnt; i++) {\n";
           elem("i", P.first, true);
           out << "  }\n";
         } else {
@@ -271,6 +287,20 @@ struct Gen {
       default: ok = false;
     }
     out << "}\n";
+  }
+
+  // an array node's element count `cnt`, element-0 column row `eb` and first element row `aa`: from the
+  // preloaded length column when the array came through a column (no row read), else from its row
+  void array_head(uint32_t pn, const std::string& T) {
+    out << "  if (rn == NONE) return mkerr(EC_NONE, 0, " << T << ");\n";
+    out << "  uint32_t cnt, eb, aa = NONE;\n";
+    if (slot_alen[pn] >= 0)
+      out << "  if (rt == N_ARR && (uint32_t)(pc[" << slot_alen[pn] << "] >> 32) != NONE) {\n"
+             "    cnt = (uint32_t)pc[" << slot_alen[pn] << "]; eb = (uint32_t)(pc[" << slot_alen[pn] << "] >> 32);\n"
+             "  } else\n";
+    out << "  { const Node a = gnode(w.R + rn);\n"
+           "    if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << T << ");\n"
+           "    cnt = a.b; eb = a.c; aa = a.a; }\n";
   }
 
   // lookup expression for entry index ei (global pentries index) into c<e>/t<e>
@@ -356,17 +386,25 @@ struct Gen {
         case H_EXISTENCE: {
           uint32_t npat = rs.pool[E.child];
           out << "  if (" << c << " != NONE) {\n"
-              << "    const Node a = gnode(w.R + " << c << ");\n"
-              << "    if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << ET << ");\n";
+              << "    uint32_t cnt, eb, aa = NONE;\n";
+          if (slot_elen[P.first + e] >= 0)
+            out << "    if (" << t << " == N_ARR && (uint32_t)(pc[" << slot_elen[P.first + e] << "] >> 32) != NONE) {\n"
+                << "      cnt = (uint32_t)pc[" << slot_elen[P.first + e] << "]; eb = (uint32_t)(pc[" << slot_elen[P.first + e]
+                << "] >> 32);\n"
+                << "    } else\n";
+          out << "    { const Node a = gnode(w.R + " << c << ");\n"
+              << "      if (node_type(a) != N_ARR) return mkerr(EC_NONE, 0, " << ET << ");\n"
+              << "      cnt = a.b; eb = a.c; aa = a.a; }\n";
           for (uint32_t j = 0; j < npat; j++) {
             out << "    { bool hit = false;\n"
-                << "      for (uint32_t i = 0; i < a.b; i++) {\n"
-                << "        const uint32_t er = a.c == NONE ? NONE : a.c + i;\n"
+                << "      for (uint32_t i = 0; i < cnt; i++) {\n"
+                << "        const uint32_t er = eb == NONE ? NONE : eb + i;\n"
                 << "        " << preload(rs.pool[E.child + 1 + j], "pe", "er") << "\n"
-                << "        uint32_t et = T_UNK, ea = 0u;\n"
-                << (rs.pe_self[P.first + e] != NONE ? "        jdec(jself(w, " + u(rs.pe_self[P.first + e]) + ", er), &et, &ea);\n"
+                << "        uint32_t et = T_UNK, ea = 0u, ei = NONE;\n"
+                << (rs.pe_self[P.first + e] != NONE ? "        ei = jdec(jself(w, " + u(rs.pe_self[P.first + e]) + ", er), &et, &ea);\n"
                                                       : std::string())
-                << "        Ret r = p" << rs.pool[E.child + 1 + j] << "(w, a.a + i, et, ea, er, pe);\n"
+                << "        if (ei == NONE) { ei = aa + i; et = T_UNK; }\n"
+                << "        Ret r = p" << rs.pool[E.child + 1 + j] << "(w, ei, et, ea, er, pe);\n"
                 << "        if (w.ost) return r;\n"
                 << "        if (!r.err) { hit = true; break; }\n"
                 << "      }\n"
@@ -402,7 +440,7 @@ std::string self_dir() {
 std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
   Gen g(rs);
   jit_rules->assign(rs.rules.size(), 0);
-  std::vector<uint32_t> roots;
+  std::vector<std::pair<uint32_t, std::vector<uint32_t>>> rule_roots;  // covered rule -> its pattern roots
   for (size_t k = 0; k < rs.rules.size(); k++) {
     const RuleDesc& rd = rs.rules[k];
     if (rd.kind != RK_PATTERN && rd.kind != RK_ANYPATTERN) continue;
@@ -426,40 +464,53 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
       continue;
     }
     (*jit_rules)[k] = 1;
-    for (uint32_t r : rr) roots.push_back(r);
+    rule_roots.push_back({(uint32_t)k, rr});
   }
   std::ostringstream src;
   src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n#include \"kyv_wave.h\"\nnamespace kyv {\n";
   src << g.out.str();
-  // one function per pattern root (inlined into the root switch)
-  for (uint32_t r : roots)
-    src << "static __device__ __forceinline__ void root" << r
-        << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, bool rootmap, PatOut& out) {\n"
-           "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
-           "  const uint32_t row = (uint32_t)(hp - v.hdr);\n"
-           "  " << g.preload(r, "pc", "row") << "\n"
-           "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
-           "  jfinish(w, r, out);\n"
+  // Rules are split into groups of a few, one kernel per group (kyv_jit_walk_<g>): the compiler allocates
+  // registers per group instead of for the worst pattern of the whole ruleset, and a group's code stays in
+  // the instruction cache. jit_rules[k] = group + 1.
+  const size_t per = getenv("KYV_JIT_GROUP") ? (size_t)std::max(1, atoi(getenv("KYV_JIT_GROUP"))) : (size_t)1000000;
+  const size_t ngroups = std::min<size_t>(250, (rule_roots.size() + per - 1) / per);
+  for (size_t gi = 0; gi < ngroups; gi++) {
+    const size_t lo = rule_roots.size() * gi / ngroups, hi = rule_roots.size() * (gi + 1) / ngroups;
+    std::vector<uint32_t> roots;
+    for (size_t i = lo; i < hi; i++) {
+      (*jit_rules)[rule_roots[i].first] = (uint8_t)(gi + 1);
+      for (uint32_t r : rule_roots[i].second) roots.push_back(r);
+    }
+    for (uint32_t r : roots)
+      src << "static __device__ __forceinline__ void root" << r
+          << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, bool rootmap, PatOut& out) {\n"
+             "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
+             "  const uint32_t row = (uint32_t)(hp - v.hdr);\n"
+             "  " << g.preload(r, "pc", "row") << "\n"
+             "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
+             "  jfinish(w, r, out);\n"
+             "}\n";
+    src << "struct JitWalker" << gi << " {\n"
+           "  bool rootmap;\n"
+           "  __device__ __forceinline__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp,\n"
+           "                                     const RuleDesc& rd, PatOut& out) {\n"
+           "    out.status = ST_NONE; out.idx = 0; out.tmpl = NONE; out.key0 = NONE; out.key1 = NONE;\n"
+           "    if (!walk) return;\n"
+           "    switch (root) {\n";
+    for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, rootmap, out); break;\n";
+    src << "      default: out.status = ST_FALLBACK;\n"
+           "    }\n"
+           "  }\n"
+           "};\n";
+  }
+  src << "}  // namespace kyv\n"
+         "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 5\n#endif\n";
+  for (size_t gi = 0; gi < ngroups; gi++)
+    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE)))\n"
+           "kyv_jit_walk_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, kyv::WorkLists wl, kyv::ChunkMap cm) {\n"
+           "  kyv::JitWalker" << gi << " wk{false};\n"
+           "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"
            "}\n";
-  src << "struct JitWalker {\n"
-         "  bool rootmap;\n"
-         "  __device__ __forceinline__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp,\n"
-         "                                     const RuleDesc& rd, PatOut& out) {\n"
-         "    out.status = ST_NONE; out.idx = 0; out.tmpl = NONE; out.key0 = NONE; out.key1 = NONE;\n"
-         "    if (!walk) return;\n"
-         "    switch (root) {\n";
-  for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, rootmap, out); break;\n";
-  src << "      default: out.status = ST_FALLBACK;\n"
-         "    }\n"
-         "  }\n"
-         "};\n"
-         "}  // namespace kyv\n"
-         "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n"
-         "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE))) kyv_jit_walk(const kyv::View* __restrict__ vp, kyv::DevOut o,\n"
-         "    kyv::WorkLists wl, kyv::ChunkMap cm) {\n"
-         "  kyv::JitWalker wk{false};\n"
-         "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"
-         "}\n";
   return src.str();
 }
 
@@ -487,7 +538,7 @@ std::vector<char> jit_compile_uncached(const std::string& src, double* seconds) 
   const char* env = getenv("KYV_CSRC");
   std::string inc = "-I" + (env ? std::string(env) : dir + "/csrc");
   std::string inc2 = "-I" + dir + "/../include";
-  std::string wpe = std::string("-DKYV_JIT_WPE=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4");
+  std::string wpe = std::string("-DKYV_JIT_WPE=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "5");
   std::string extra = getenv("KYV_JIT_DEFS") ? getenv("KYV_JIT_DEFS") : "-DKYV_JIT_NOEXTRA";  // experiments only
   const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str(), wpe.c_str(), extra.c_str()};
   hiprtcProgram prog;

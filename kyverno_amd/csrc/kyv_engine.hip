@@ -50,8 +50,8 @@ struct DevRuleset {
   uint8_t* base = nullptr;
   size_t bytes = 0;
   size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool;
-  hipModule_t jmod = nullptr;     // runtime-compiled walk kernel (jit.cpp) loaded on this device
-  hipFunction_t jfn = nullptr;
+  hipModule_t jmod = nullptr;     // runtime-compiled walk kernels (jit.cpp) loaded on this device
+  std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
 };
 
 struct DeviceResults {
@@ -75,8 +75,8 @@ struct DeviceResults {
   WorkLists wl{};                // walk work lists (kyv_wave.h)
   std::vector<uint64_t> cap;     // [nrules] work-list capacity (resources of the kind classes the gate admits)
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
-  ChunkMap cm[2] = {};           // [0] interpreted walk kernel, [1] runtime-compiled one
-  uint32_t grid[2] = {0, 0};
+  std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
+  std::vector<uint32_t> grid;
   int jit_state = -1;            // what the schedules were laid out for (0 interpreter only, 1 with the jit kernel)
   int cus = 256;
 };
@@ -369,7 +369,7 @@ static int ruleset_depth(const Ruleset& rs) {
 // Compile (once per ruleset) and load (once per device) the ruleset's walk kernel; false if unavailable.
 static std::mutex g_jit_mu;
 static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
-  if (dr->jfn) return true;
+  if (!dr->jfns.empty()) return true;
   std::lock_guard<std::mutex> lk(g_jit_mu);
   if (!rs.jit_tried) {
     rs.jit_tried = true;
@@ -386,7 +386,11 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   }
   if (rs.jit_code.empty()) return false;
   HIP_OK(hipModuleLoadData(&dr->jmod, rs.jit_code.data()));
-  HIP_OK(hipModuleGetFunction(&dr->jfn, dr->jmod, "kyv_jit_walk"));
+  uint32_t ng = 0;
+  for (auto x : rs.jit_rules) ng = std::max<uint32_t>(ng, x);
+  dr->jfns.resize(ng);
+  for (uint32_t g = 0; g < ng; g++)
+    HIP_OK(hipModuleGetFunction(&dr->jfns[g], dr->jmod, ("kyv_jit_walk_" + std::to_string(g)).c_str()));
   return true;
 }
 
@@ -475,33 +479,40 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         for (uint32_t i = 0; i < gw; i++) g[i] |= b.gate[(size_t)b.hdr[r].kclass * gw + i];
       if (runs.empty() || runs.back().second != g) runs.push_back({w, g});
     }
-    std::vector<uint2> slots[2];
-    for (int cls = 0; cls < 2; cls++) {
-      for (size_t ri = 0; ri < runs.size(); ri++) {
-        const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
-        std::vector<uint32_t> ks;
-        for (size_t k = 0; k < nrules; k++) {
-          if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
-          if (!((runs[ri].second[k / 32] >> (k % 32)) & 1u)) continue;
-          if ((int)(jit && rs.jit_rules[k]) != cls) continue;
-          ks.push_back((uint32_t)k);
-        }
-        for (size_t i = 0; i < ks.size(); i += WIN) {
-          const size_t n = std::min<size_t>(WIN, ks.size() - i);
-          for (uint32_t w = wb; w < we; w++)
-            for (size_t t = i; t < i + n; t++) slots[cls].push_back(make_uint2(ks[t], w));
-        }
+    const uint32_t ncls = 1 + (jit ? (uint32_t)dr->jfns.size() : 0u);  // 0: interpreter, 1 + g: compiled group g
+    std::vector<std::vector<uint2>> slots(ncls);
+    for (size_t ri = 0; ri < runs.size(); ri++) {
+      const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
+      std::vector<std::vector<uint32_t>> ks(ncls);
+      for (size_t k = 0; k < nrules; k++) {
+        if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
+        if (!((runs[ri].second[k / 32] >> (k % 32)) & 1u)) continue;
+        ks[jit ? rs.jit_rules[k] : 0].push_back((uint32_t)k);
       }
+      for (uint32_t cls = 0; cls < ncls; cls++)
+        for (size_t i = 0; i < ks[cls].size(); i += WIN) {
+          const size_t n = std::min<size_t>(WIN, ks[cls].size() - i);
+          for (uint32_t w = wb; w < we; w++)
+            for (size_t t = i; t < i + n; t++) slots[cls].push_back(make_uint2(ks[cls][t], w));
+        }
+    }
+    size_t tot = 0;
+    d.grid.assign(ncls, 0);
+    for (uint32_t cls = 0; cls < ncls; cls++) {
       if (slots[cls].size() > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
       d.grid[cls] = (uint32_t)std::min<size_t>(slots[cls].size(), (size_t)d.cus * 64);
+      tot += slots[cls].size();
     }
     hipFree(d.sched);
-    const size_t n0 = slots[0].size(), n1 = slots[1].size();
-    HIP_OK(hipMalloc(&d.sched, std::max<size_t>(1, n0 + n1) * sizeof(uint2)));
-    if (n0) HIP_OK(hipMemcpy(d.sched, slots[0].data(), n0 * sizeof(uint2), hipMemcpyHostToDevice));
-    if (n1) HIP_OK(hipMemcpy(d.sched + n0, slots[1].data(), n1 * sizeof(uint2), hipMemcpyHostToDevice));
-    d.cm[0] = ChunkMap{d.sched, (uint32_t)n0};
-    d.cm[1] = ChunkMap{d.sched + n0, (uint32_t)n1};
+    HIP_OK(hipMalloc(&d.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
+    d.cm.assign(ncls, ChunkMap{nullptr, 0});
+    size_t at = 0;
+    for (uint32_t cls = 0; cls < ncls; cls++) {
+      if (!slots[cls].empty())
+        HIP_OK(hipMemcpy(d.sched + at, slots[cls].data(), slots[cls].size() * sizeof(uint2), hipMemcpyHostToDevice));
+      d.cm[cls] = ChunkMap{d.sched + at, (uint32_t)slots[cls].size()};
+      at += slots[cls].size();
+    }
     d.jit_state = (int)jit;
   }
   DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, d.rbase, d.rcnt, d.counts, 0, (uint32_t)nrules};
@@ -525,12 +536,13 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
                            depth);
         HIP_OK(hipGetLastError());
       }
-      if (jit && d.grid[1]) {
+      for (size_t cls = 1; cls < d.cm.size(); cls++) {
+        if (!d.grid[cls]) continue;
         const View* vp = d.view;
         WorkLists wl = d.wl;
-        ChunkMap cmj = d.cm[1];
+        ChunkMap cmj = d.cm[cls];
         void* args[] = {(void*)&vp, (void*)&o, (void*)&wl, (void*)&cmj};
-        HIP_OK(hipModuleLaunchKernel(dr->jfn, d.grid[1], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        HIP_OK(hipModuleLaunchKernel(dr->jfns[cls - 1], d.grid[cls], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
       const size_t nchunks = nrules * (size_t)d.wl.nwaves;
       const uint32_t ntiles = (uint32_t)((nchunks + WAVE - 1) / WAVE);

@@ -71,6 +71,8 @@ struct Ruleset {
     uint32_t col = NONE;        // column id (key edges; "[*]" nodes: the elements' self column)
     uint32_t rowspace = 0;      // row space the column / this node's lookups live in
     uint32_t star = NONE;       // "[*]" child (opens row space trie[star].rowspace)
+    uint32_t lencol = NONE;     // with a "[*]" child: column (this node's row space) of the array's (count, row of
+                                // element 0) as (low, high) words
     std::vector<std::pair<uint32_t, uint32_t>> kids;  // (key sid, child trie node)
   };
   std::vector<TrieNode> trie;   // trie[0] = resource root
@@ -78,6 +80,8 @@ struct Ruleset {
   std::vector<uint32_t> col_rowspace;
   std::vector<uint32_t> pn_self;  // array pnode -> self column of its elements (NONE: none)
   std::vector<uint32_t> pe_self;  // existence entry -> self column of the candidate elements
+  std::vector<uint32_t> pn_len;   // array pnode -> its length column (TrieNode::lencol) or NONE
+  std::vector<uint32_t> pe_len;   // existence entry -> length column of the candidate array
   // runtime-compiled walk kernel (jit.cpp): generated once per ruleset, compiled on first use
   bool jit_tried = false;
   std::vector<uint8_t> jit_rules;   // rule k is walked by the compiled kernel
