@@ -55,3 +55,29 @@ def run_synthetic(backend, policies, n, seed, kind="mixed", edge=True, jit=None)
     st, res = PU.compare(policies, docs, nsl, backend=backend, jit=jit)
     assert_clean("synthetic/%s/%d" % (kind, seed), st)
     return st, res
+
+
+def run_merged(backend, groups, name, jit=None):
+    """All (policies, resources) groups of a golden corpus as ONE ruleset over ONE batch (policy names prefixed
+    per group so they stay distinct): every policy meets every resource, and a runtime-compiled walk kernel is
+    compiled once for the whole corpus."""
+    import copy
+    pols, res = [], []
+    for gi, (ps, rs_) in enumerate(groups):
+        for p in ps:
+            q = copy.deepcopy(p)
+            q.setdefault("metadata", {})["name"] = "g%d-%s" % (gi, q.get("metadata", {}).get("name", ""))
+            pols.append(q)
+        res.extend(rs_)
+    st, r = PU.compare(pols, res, None, backend=backend, jit=jit)
+    assert_clean(name, st)
+    return st, r
+
+
+def golden_groups():
+    """engine + cli + walk golden corpora as (policies, resources) groups"""
+    groups = [(p, r) for p, r in cases.engine_cases()]
+    groups += [(p, r) for _, p, r in cases.cli_cases()]
+    wp, wr = cases.walk_policy_cases()
+    groups += [([wp[i]], [wr[i]]) for i in range(len(wp))]
+    return groups

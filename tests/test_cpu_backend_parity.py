@@ -30,3 +30,9 @@ def test_c3_synthetic_edge():
 def test_quirk_policies():
     st, _ = S.run_synthetic("cpu", cases.quirk_policies(), 400, seed=22)
     assert st["compared"] > 2000
+
+
+def test_goldens_merged_cpu():
+    """the merged golden corpus (every golden policy x every golden resource) on the host instantiation"""
+    st, _ = S.run_merged("cpu", S.golden_groups(), "goldens-merged/cpu")
+    assert st["compared"] > 1000

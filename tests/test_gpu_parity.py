@@ -96,3 +96,17 @@ def test_c3_synthetic_gpu_jit():
     st, res = S.run_synthetic("gpu", cases.best_practices() + cases.chart_restricted(), 3000, seed=41, jit=True)
     assert res.jit
     assert st["compared"] > 50000
+
+
+def test_goldens_merged_gpu_jit():
+    """Every engine / CLI / validate-walk golden policy against every golden resource, with the pattern walk in
+    the runtime-compiled kernel (forced), bit-exact against the oracle."""
+    st, res = S.run_merged("gpu", S.golden_groups(), "goldens-merged/jit", jit=True)
+    assert res.jit
+    assert st["compared"] > 1000
+
+
+def test_goldens_merged_gpu_interpreter():
+    st, res = S.run_merged("gpu", S.golden_groups(), "goldens-merged/interp", jit=False)
+    assert not res.jit
+    assert st["compared"] > 1000
