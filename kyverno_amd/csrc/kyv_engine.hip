@@ -73,6 +73,8 @@ struct DeviceResults {
   View* view = nullptr;  // device copy of the View the kernel reads
   // walk work lists (match_kernel -> walk_kernel): per rule a list of resource positions
   WorkLists wl{};                // walk work lists (kyv_wave.h)
+  uint32_t* mrules = nullptr;    // rules match_kernel evaluates: all but the direct-walk ones (pattern + RD_GATE_EXACT)
+  uint32_t nm = 0;
   std::vector<uint64_t> cap;     // [nrules] work-list capacity (resources of the kind classes the gate admits)
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
@@ -84,7 +86,7 @@ struct DeviceResults {
 static void free_dev_results(DeviceResults& d) {
   hipFree(d.view); hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
   hipFree(d.stage); hipFree(d.rbase); hipFree(d.rcnt); hipFree(d.tsum);
-  hipFree(d.wl.items); hipFree(d.wl.cnt); hipFree(d.sched);
+  hipFree(d.wl.items); hipFree(d.wl.cnt); hipFree(d.sched); hipFree(d.mrules);
   if (d.e0) hipEventDestroy(d.e0);
   if (d.e1) hipEventDestroy(d.e1);
   if (d.stream) hipStreamDestroy(d.stream);
@@ -221,13 +223,15 @@ constexpr int RECS_PER_PAIR = MAX_ALTS;
 // Phase 1 (match_eval): one lane per resource, the rule loop uniform across the wave. Kind gate, match /
 // exclude program, dispatch; verdicts that need no pattern walk are final here (incl. PodSecurity). Pairs
 // that need the walk are appended to the rule's work list (wave ballot + one atomic per wave and rule).
-__global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl) {
+__global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl,
+                                                      const uint32_t* __restrict__ mrules, uint32_t nm) {
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
   const uint32_t r = blockIdx.x * BLOCK + lane;
   const bool active = r < v.nres;
   const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
-  for (uint32_t k = o.rule_lo; k < o.rule_hi; k++) {
+  for (uint32_t mi = 0; mi < nm; mi++) {  // rules that need this phase (direct-walk rules are decided in the walk)
+    const uint32_t k = mrules[mi];
     const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
     if (!__ballot(gated)) continue;  // status bytes are pre-set to ST_NONE, PSS masks to 0
     uint32_t pf = 0;
@@ -455,6 +459,17 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMemcpy(d.view, &v, sizeof(View), hipMemcpyHostToDevice));
     // walk work lists: one 64-slot list per (rule, match wave)
     d.wl.nwaves = (uint32_t)((nres + WAVE - 1) / WAVE);
+    {
+      std::vector<uint32_t> ml;
+      for (size_t k = 0; k < nrules; k++) {
+        const RuleDesc& rd = rs.rules[k];
+        const bool direct = (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) && (rd.flags & RD_GATE_EXACT);
+        if (!direct) ml.push_back((uint32_t)k);
+      }
+      d.nm = (uint32_t)ml.size();
+      HIP_OK(hipMalloc(&d.mrules, std::max<size_t>(1, ml.size()) * 4));
+      if (!ml.empty()) HIP_OK(hipMemcpy(d.mrules, ml.data(), ml.size() * 4, hipMemcpyHostToDevice));
+    }
     HIP_OK(hipMalloc(&d.wl.items, std::max<size_t>(1, nrules * (size_t)d.wl.nwaves * WAVE) * sizeof(uint2)));
     HIP_OK(hipMalloc(&d.wl.cnt, std::max<size_t>(4, nrules * (size_t)d.wl.nwaves + 4)));
     // persistent grid: enough waves to fill the chip several times over, never more than the chunks
@@ -529,7 +544,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     if (nres && nrules) {
-      hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl);
+      if (d.nm) hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, d.mrules, d.nm);
       HIP_OK(hipGetLastError());
       if (d.grid[0]) {
         hipLaunchKernelGGL(walk_kernel, dim3(d.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, d.cm[0],

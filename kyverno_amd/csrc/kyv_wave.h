@@ -759,19 +759,39 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
     const uint2 kw = sld(cm.slots + c);
     const uint32_t k = kw.x, w = kw.y;
     const size_t list = (size_t)k * wl.nwaves + w;
-    const uint32_t n = sld8(wl.cnt + list);
-    if (!n) continue;
-    const bool active = lane < n;
-    uint2 it = make_uint2(0u, 0u);
-    if (active) it = wl.items[list * WAVE + lane];
-    const uint32_t r = it.x & ~ITEM_ROOT_MAP;
-    wk.rootmap = (it.x & ITEM_ROOT_MAP) != 0;
     const RuleDesc rd = sld(v.rules + k);
+    bool active;
+    uint32_t r;
+    uint2 it = make_uint2(0u, 0u);
+    bool magic = false;
+    if (rd.flags & RD_GATE_EXACT) {
+      // match == kind gate: the chunk's pairs are the gated lanes of match wave w, read straight from the headers
+      r = w * WAVE + lane;
+      bool gated = false;
+      if (r < v.nres) {
+        const ResHeader* h = v.hdr + r;
+        const uint32_t cls = gld32(&h->kclass), fl = gld32(&h->flags);
+        gated = (gld32(v.gate + (size_t)cls * v.gate_words + (k >> 5)) >> (k & 31)) & 1u;
+        magic = gated && (fl & RF_MAGIC);  // pattern pairs on such resources go to the CPU engine (pair_dispatch)
+        it = make_uint2(r | ((fl & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), gld32(&h->root));
+      }
+      active = gated && !magic;
+      if (!__ballot(gated)) continue;
+    } else {
+      const uint32_t n = sld8(wl.cnt + list);
+      if (!n) continue;
+      active = lane < n;
+      if (active) it = wl.items[list * WAVE + lane];
+      r = it.x & ~ITEM_ROOT_MAP;
+    }
+    wk.rootmap = (it.x & ITEM_ROOT_MAP) != 0;
     const uint32_t alts = rd.kind == RK_PATTERN ? 1u : min(rd.nalts, (uint32_t)MAX_ALTS);
     WaveSink sink{o.stage + sld32(o.rbase + k) + (size_t)w * WAVE * alts, 0u};
-    const uint8_t st = pair_walk(v, rd, active, r, k, v.nodes + it.y, wk, sink);
-    if (active) o.status[(size_t)k * v.nres + r] = st;
+    uint8_t st = pair_walk(v, rd, active, r, k, v.nodes + it.y, wk, sink);
+    if (magic) st = ST_FALLBACK;
+    if (active || magic) o.status[(size_t)k * v.nres + r] = st;
     if (sink.n && lane == 0) o.rcnt[list] = (uint16_t)sink.n;
+    active = active || magic;
     count_status(o.counts, k, active, st);
   }
 }
