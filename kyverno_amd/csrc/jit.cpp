@@ -496,6 +496,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
            "                                     const RuleDesc& rd, PatOut& out) {\n"
            "    out.status = ST_NONE; out.idx = 0; out.tmpl = NONE; out.key0 = NONE; out.key1 = NONE;\n"
            "    if (!walk) return;\n"
+           "#ifdef KYV_EXP_JIT_EMPTY\n    out.status = ST_PASS; return;\n#endif\n"
            "    switch (root) {\n";
     for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, rootmap, out); break;\n";
     src << "      default: out.status = ST_FALLBACK;\n"

@@ -6,8 +6,8 @@
 //                 work lists of the pairs that do (wave ballot + one atomic per wave and rule);
 //   walk_kernel   persistent grid-stride over 64-pair chunks of ONE rule each: the wave-uniform pattern walker
 //                 (kyv_wave.h) with no idle lanes from gated / non-matching pairs.
-// Verdicts are written rule-major (coalesced bytes), failing-path records are compacted with a wave ballot +
-// one atomic per wave, per-rule status counters with ballots + one atomic per (wave, rule, status).
+// Verdicts are written rule-major (coalesced bytes); failing-path records are staged per walk chunk and compacted
+// without atomics (compact_*_kernel); verdict totals are one histogram pass over the status bytes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -253,13 +253,12 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
       const uint32_t ps = o.pss_slot[k];
       if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
     }
-    count_status(o.counts, k, gated && !walk, st);
   }
 }
 
 // Phase 2 (pattern_eval): each wave takes chunks of 64 work items of ONE rule (grid-stride over all rules'
 // chunks), so every lane walks the same compiled pattern over a different resource with the wave-uniform
-// walker; verdict bytes, failing-path records (wave ballot + one atomic) and counts as in phase 1.
+// walker; verdict bytes as in phase 1, failing-path records staged in the chunk's own slots.
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_WPE)))
 walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, ChunkMap cm, int depth) {
   extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
@@ -325,6 +324,48 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
     const FailRec* src = chunk_stage(stage, rbase, rules, nwaves, (size_t)blockIdx.x * WAVE + j);
     for (uint32_t i = lane; i < nj; i += WAVE)
       if (at + i < max_out) out[at + i] = src[i];
+  }
+}
+
+// Verdict totals: one histogram pass over the [rule][res] status bytes after both phases (the verdict bytes are
+// complete there: ST_NONE preset, every decided pair written once). Statuses are 0..7, so a 32-bit word holds four
+// 3-bit values and the bytes equal to s are the zero bytes of word ^ (s * 0x01010101). Per thread u32 tallies,
+// block reduction in LDS, one atomic per block and status (a few hundred blocks: no hot-address queue).
+constexpr int HIST_BLOCK = 256;
+__device__ __forceinline__ uint32_t bytes_eq(uint32_t w, uint32_t s) {
+  const uint32_t x = w ^ (s * 0x01010101u);
+  return 4u - (uint32_t)__popc((x | (x >> 1) | (x >> 2)) & 0x01010101u);
+}
+__global__ void __launch_bounds__(HIST_BLOCK) status_hist_kernel(const uint8_t* __restrict__ status, size_t n,
+                                                                 unsigned long long* __restrict__ counts) {
+  __shared__ uint32_t part[HIST_BLOCK / WAVE][NSTATUS];
+  uint32_t c[NSTATUS] = {0};
+  const size_t nv = n / 16, stride = (size_t)gridDim.x * HIST_BLOCK;
+  const kyv_u32x4* s4 = (const kyv_u32x4*)status;
+  for (size_t i = (size_t)blockIdx.x * HIST_BLOCK + threadIdx.x; i < nv; i += stride) {
+    const kyv_u32x4 q = __builtin_nontemporal_load(s4 + i);
+#pragma unroll
+    for (uint32_t s = 1; s < NSTATUS; s++) c[s] += bytes_eq(q.x, s) + bytes_eq(q.y, s) + bytes_eq(q.z, s) + bytes_eq(q.w, s);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n % 16) {  // tail bytes
+    const uint32_t b = status[nv * 16 + threadIdx.x] & 7u;
+#pragma unroll
+    for (uint32_t s = 1; s < NSTATUS; s++) c[s] += b == s;
+  }
+#pragma unroll
+  for (uint32_t s = 1; s < NSTATUS; s++) {
+    uint32_t x = c[s];
+    for (int off = WAVE / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    c[s] = x;
+  }
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+  if (lane == 0)
+    for (uint32_t s = 1; s < NSTATUS; s++) part[wv][s] = c[s];
+  __syncthreads();
+  if (threadIdx.x > 0 && threadIdx.x < NSTATUS) {
+    uint32_t t = 0;
+    for (int j = 0; j < HIST_BLOCK / WAVE; j++) t += part[j][threadIdx.x];
+    if (t) atomicAdd(&counts[threadIdx.x], (unsigned long long)t);
   }
 }
 
@@ -450,7 +491,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipMalloc(&d.rcnt, std::max<size_t>(nrules * nwv, 1) * 2));
       HIP_OK(hipMalloc(&d.tsum, std::max<size_t>((nrules * nwv + WAVE - 1) / WAVE, 1) * 4));
     }
-    HIP_OK(hipMalloc(&d.counts, std::max<size_t>(8, nrules * NSTATUS * 8)));
+    HIP_OK(hipMalloc(&d.counts, NSTATUS * 8));
     HIP_OK(hipMemcpy(d.pss_slot, pss_slot.data(), nrules * 4, hipMemcpyHostToDevice));
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.e0));
@@ -530,7 +571,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     }
     d.jit_state = (int)jit;
   }
-  DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, d.rbase, d.rcnt, d.counts, 0, (uint32_t)nrules};
+  DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, d.rbase, d.rcnt, 0, (uint32_t)nrules};
   int depth = ruleset_depth(rs);
   size_t lds = (size_t)depth * (sizeof(UFrame) + BLOCK * sizeof(LaneFrame));
   dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
@@ -540,7 +581,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
     HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nrules * (size_t)d.wl.nwaves, 1) * 2, stream));
-    HIP_OK(hipMemsetAsync(d.counts, 0, nrules * NSTATUS * 8, stream));
+    HIP_OK(hipMemsetAsync(d.counts, 0, NSTATUS * 8, stream));
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     if (nres && nrules) {
@@ -566,6 +607,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, d.tsum, ntiles, d.nrecs);
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, d.rbase, d.rcnt, drules,
                          d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs);
+      const size_t nst = nres * nrules;
+      const uint32_t hgrid = (uint32_t)std::max<size_t>(1, std::min<size_t>((size_t)d.cus * 2, (nst / 16 + HIST_BLOCK - 1) / HIST_BLOCK));
+      hipLaunchKernelGGL(status_hist_kernel, dim3(hgrid), dim3(HIST_BLOCK), 0, stream, d.status, nst, d.counts);
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(d.e1, stream));
@@ -588,14 +632,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     out->kernel_ms = total_ms / n;
     out->jit_used = jit ? 1 : 0;
     out->h2d_ms = db->upload_ms;
-    std::vector<unsigned long long> counts(nrules * NSTATUS);
-    HIP_OK(hipMemcpy(counts.data(), d.counts, counts.size() * 8, hipMemcpyDeviceToHost));
-    for (int s = 0; s < NSTATUS; s++) out->counts[s] = 0;
-    for (size_t k = 0; k < nrules; k++)
-      for (int s = 0; s < NSTATUS; s++) out->counts[s] += (int64_t)counts[k * NSTATUS + s];
-    // ST_NONE pairs are not counted on the device
+    unsigned long long counts[NSTATUS];
+    HIP_OK(hipMemcpy(counts, d.counts, sizeof(counts), hipMemcpyDeviceToHost));
+    // ST_NONE pairs are not tallied on the device
     int64_t counted = 0;
-    for (int s = 0; s < NSTATUS; s++) if (s != ST_NONE) counted += out->counts[s];
+    for (int s = 0; s < NSTATUS; s++) out->counts[s] = s == ST_NONE ? 0 : (int64_t)counts[s], counted += out->counts[s];
     out->counts[ST_NONE] = (int64_t)(nres * nrules) - counted;
     if (copy_back) {
       auto t0 = std::chrono::steady_clock::now();

@@ -689,7 +689,6 @@ struct DevOut {
   FailRec* stage;          // failing-path records, staged per walk chunk: chunk (k, w) owns 64 * alts(k) slots
   const uint32_t* rbase;   // [nrules] first staging slot of rule k (its chunks follow, wave-major)
   uint16_t* rcnt;          // [nrules][nwaves] records staged by chunk (k, w)
-  unsigned long long* counts;  // [rule][NSTATUS]
   uint32_t rule_lo, rule_hi;   // rule range handled by this launch
 };
 
@@ -709,24 +708,6 @@ struct WaveSink {
     n += (uint32_t)__popcll(m);
   }
 };
-
-// per-rule status counts: wave ballots -> one atomic per status present
-__device__ __forceinline__ void count_status(unsigned long long* counts, uint32_t k, bool active, uint8_t st) {
-  // ST_NONE is not counted (the host derives it); one ballot per status value present in the wave
-#ifdef KYV_EXP_NOCOUNT
-  return;
-#endif
-  const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const uint32_t s = st & 7u;
-  unsigned long long m = __ballot(active && s != ST_NONE);
-  while (m) {
-    const uint32_t sv = __shfl(s, (int)__ffsll((long long)m) - 1);
-    const unsigned long long ms = __ballot(active && s == sv);
-    if (lane == 0) atomicAdd(&counts[(size_t)k * NSTATUS + sv], (unsigned long long)__popcll(ms));
-    m &= ~ms;
-  }
-}
-
 
 // Walk work lists, written by match_kernel without atomics: for rule k and match wave w (64 consecutive
 // resources of the kind-major batch), cnt[k][w] pairs need the walk and items[k][w][0..cnt) are their resource
@@ -751,7 +732,7 @@ struct ChunkMap {
 };
 
 // Grid-stride over the schedule; every wave walks ONE rule over the (up to 64) resources of one work list;
-// verdict bytes, records and counts as in match_kernel.
+// verdict bytes and records as in match_kernel (the status counts are one histogram pass afterwards).
 template <class Walker>
 __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists wl, ChunkMap cm, Walker& wk) {
   const uint32_t lane = threadIdx.x & (WAVE - 1);
@@ -791,8 +772,6 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
     if (magic) st = ST_FALLBACK;
     if (active || magic) o.status[(size_t)k * v.nres + r] = st;
     if (sink.n && lane == 0) o.rcnt[list] = (uint16_t)sink.n;
-    active = active || magic;
-    count_status(o.counts, k, active, st);
   }
 }
 
