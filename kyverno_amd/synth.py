@@ -319,3 +319,53 @@ def cached_corpus(n, kind="mixed", seed=SEED, edge=False, cache_dir=None):
     with open(base + ".nsl.json", "w") as f:
         json.dump(nsl, f)
     return data, nsl
+
+
+def c4_policies(n=10000, seed=SEED):
+    """BASELINE configs[3]: n generated ClusterPolicies, one validate rule each, with
+    wildcard-heavy match (kinds incl. group/version and `*`, names, namespaces, matchLabels / matchExpressions
+    selectors, annotations, namespaceSelector) and exclude blocks; simple metadata patterns. Kinds naming Pod
+    or Deployment get autogen rules, so the compiled rule count is ~2-3x n."""
+    r = random.Random(seed ^ 0xC4)
+    kinds = [["Pod"], ["Deployment"], ["apps/v1/Deployment"], ["*"], ["ConfigMap"], ["Pod", "Service"],
+             ["v1/Pod"], ["apps/*/StatefulSet"], ["Job", "CronJob"], ["Namespace"]]
+    names = ["pod-*", "*-00001*", "deployment-??0*", "*", "pod-000?1*", "configmap-*"]
+    nss = ["ns-?0*", "ns-00*", "ns-01??", "ns-*1", "team-*"]
+    patterns = [{"metadata": {"labels": {"owner": "?*"}}}, {"metadata": {"labels": {"app": "app-*"}}},
+                {"metadata": {"name": "!*-x"}}, {"metadata": {"=(annotations)": {"=(example.com/a0)": "value-?*"}}},
+                {"metadata": {"labels": {"tier": "frontend | backend"}}}]
+    out = []
+    for i in range(n):
+        res = {"kinds": list(r.choice(kinds))}
+        u = r.random()
+        if u < 0.3:
+            res["names"] = [r.choice(names)] + ([r.choice(names)] if r.random() < 0.3 else [])
+        elif u < 0.4:
+            res["name"] = r.choice(names)
+        if r.random() < 0.4:
+            res["namespaces"] = [r.choice(nss)]
+        v = r.random()
+        if v < 0.25:
+            res["selector"] = {"matchLabels": {"tier": r.choice(["fr*", "back?nd", "data", "*"])}}
+        elif v < 0.35:
+            res["selector"] = {"matchExpressions": [{"key": "app", "operator": r.choice(["In", "NotIn"]),
+                                                     "values": ["app-%d" % r.randint(0, 300) for _ in range(3)]},
+                                                    {"key": "owner", "operator": r.choice(["Exists", "DoesNotExist"])}]}
+        elif v < 0.42:
+            res["namespaceSelector"] = {"matchLabels": {"env": r.choice(["prod", "dev"])}}
+        if r.random() < 0.15:
+            res["annotations"] = {"example.com/a%d" % r.randint(0, 2): "value-%d*" % r.randint(0, 9)}
+        match = {"any": [{"resources": res}]}
+        if r.random() < 0.2:
+            match["any"].append({"resources": {"kinds": ["Service"], "names": ["service-*"]}})
+        rule = {"name": "r%05d" % i, "match": match,
+                "validate": {"message": "generated rule %d" % i, "pattern": r.choice(patterns)}}
+        w = r.random()
+        if w < 0.25:
+            rule["exclude"] = {"any": [{"resources": {"namespaces": [r.choice(nss)]}}]}
+        elif w < 0.35:
+            rule["exclude"] = {"any": [{"resources": {"annotations": {"example.com/a1": "value-?0*"}}}]}
+        out.append({"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy",
+                    "metadata": {"name": "c4-%05d" % i},
+                    "spec": {"validationFailureAction": "Audit", "background": True, "rules": [rule]}})
+    return out

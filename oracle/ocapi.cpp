@@ -280,6 +280,80 @@ long long oracle_validate_batch(const char* policies_json, const char* resources
   return (long long)rs.size() * (long long)nrules;
 }
 
+// Per-pair verdict matrix for parity at sizes where one oracle_validate call per resource is too slow (C4:
+// thousands of policies). Same semantics as oracle_validate (validate_policy, autogen computed once per policy
+// instead of per call). out[rule * nres + res] for the policies' validate rules in order: 0 not matched / no
+// response, 1 pass, 2 fail, 3 skip, 4 error, 5 panic, 6 unsupported (CPU fallback), 7 nondeterministic.
+// Returns the rule names as a JSON array [[policy, rule], ...] (free with oracle_free), or null on error.
+extern "C" char* oracle_validate_matrix(const char* policies_json, const char* resources_json, const char* nslabels_json,
+                                        int nthreads, unsigned char* out, long long out_len) {
+  try {
+    VP pols = oj::parse(policies_json, true);
+    VP res = oj::parse(resources_json, false);
+    VP nsl = nslabels_json && *nslabels_json ? oj::parse(nslabels_json, false) : nullptr;
+    std::map<std::string, std::map<std::string, std::string>> nsLabels;
+    if (nsl && nsl->t == T::Obj) for (auto& kv : nsl->o) nsLabels[kv.first] = labels_of(kv.second);
+    static const std::map<std::string, std::string> kNoLabels;
+    std::vector<VP> list;
+    if (pols->t == T::Arr) list = pols->a; else list.push_back(pols);
+    struct Pol { VP policy; std::vector<VP> rules; size_t first; std::map<std::string, size_t> idx; };
+    std::vector<Pol> plist;
+    auto names = Value::arr();
+    size_t nrules = 0;
+    for (auto& p : list) {
+      if (!p || p->t != T::Obj) continue;
+      std::string kind = oj::get_str(p, "kind");
+      if (kind != "ClusterPolicy" && kind != "Policy") continue;
+      Pol x{p, compute_rules(p), nrules, {}};
+      std::string pname = nested_string(p, {"metadata", "name"});
+      for (auto& r : x.rules) {
+        VP v = r->get("validate");
+        if (!((v && v->t == T::Obj && !v->o.empty()) || has_nonempty(r, "verifyImages"))) continue;
+        std::string rn = oj::get_str(r, "name");
+        x.idx[rn] = nrules++;
+        auto pr = Value::arr();
+        pr->a.push_back(Value::str(pname));
+        pr->a.push_back(Value::str(rn));
+        names->a.push_back(pr);
+      }
+      plist.push_back(std::move(x));
+    }
+    if (res->t != T::Arr) return nullptr;
+    size_t n = res->a.size();
+    if ((long long)(nrules * n) > out_len) return nullptr;
+    std::fill(out, out + nrules * n, (unsigned char)0);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      while (true) {
+        size_t i = next.fetch_add(16);
+        if (i >= n) break;
+        for (size_t k = i; k < std::min(n, i + 16); k++) {
+          const VP& r = res->a[k];
+          auto it = nsLabels.find(nested_string(r, {"metadata", "namespace"}));
+          const auto& labels = it == nsLabels.end() ? kNoLabels : it->second;
+          for (auto& pol : plist) {
+            PolicyResult pr = validate_policy_rules(pol.policy, pol.rules, r, labels);
+            for (auto& rr : pr.rules) {
+              auto f = pol.idx.find(rr.name);
+              if (f == pol.idx.end()) continue;
+              unsigned char c = rr.status == "pass" ? 1 : rr.status == "fail" ? 2 : rr.status == "skip" ? 3
+                              : rr.status == "error" ? 4 : rr.status == "panic" ? 5 : 6;
+              if (rr.nondeterministic && c != 6) c = 7;
+              out[f->second * n + k] = c;
+            }
+          }
+        }
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    return dup(oj::dump(names));
+  } catch (std::exception&) {
+    return nullptr;
+  }
+}
+
 extern "C" {
 int oracle_leaf(const char* fn, const char* value_json, int value_float, const char* pattern_json, const char* op) {
   try {

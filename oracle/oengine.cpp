@@ -774,6 +774,12 @@ static bool rule_has_validate(const VP& rule) {
 
 // Validate (validation.go:39-183) for one policy and one resource
 PolicyResult validate_policy(const VP& policy, const VP& resource, const std::map<std::string, std::string>& nsLabels) {
+  return validate_policy_rules(policy, compute_rules(policy), resource, nsLabels);
+}
+
+// validate_policy with the policy's computed rules (autogen.ComputeRules) prepared by the caller
+PolicyResult validate_policy_rules(const VP& policy, const std::vector<VP>& rules, const VP& resource,
+                                   const std::map<std::string, std::string>& nsLabels) {
   PolicyResult pr;
   pr.name = nested_string(policy, {"metadata", "name"});
   std::string kind = oj::get_str(policy, "kind");
@@ -785,7 +791,7 @@ PolicyResult validate_policy(const VP& policy, const VP& resource, const std::ma
   VP spec = policy->get("spec");
   bool applyOne = oj::get_str(spec, "applyRules") == "One";
   int applied = 0;
-  for (auto& rule : compute_rules(policy)) {
+  for (auto& rule : rules) {
     if (!rule_has_validate(rule) && !has_nonempty(rule, "verifyImages")) continue;
     bool nd = false;
     bool m = matches_resource_description(rule, resource, nsLabels, &nd);

@@ -34,6 +34,8 @@ RuleResult validate_rule(const oj::VP& rule, const oj::VP& resource);
 std::string nested_string(const oj::VP& obj, std::initializer_list<const char*> path);
 bool has_nonempty(const oj::VP& o, const char* k);
 PolicyResult validate_policy(const oj::VP& policy, const oj::VP& resource, const std::map<std::string, std::string>& nsLabels);
+PolicyResult validate_policy_rules(const oj::VP& policy, const std::vector<oj::VP>& rules, const oj::VP& resource,
+                                   const std::map<std::string, std::string>& nsLabels);
 std::string rule_unsupported_reason(const oj::VP& rule);
 void get_kind_from_gvk(const std::string& str, std::string& gv, std::string& kind);
 

@@ -27,6 +27,9 @@ def lib():
             build()
         L = ctypes.CDLL(_LIB)
         L.oracle_free.argtypes = [ctypes.c_void_p]
+        L.oracle_validate_matrix.restype = ctypes.c_void_p
+        L.oracle_validate_matrix.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.c_longlong]
         for name in ("oracle_match_pattern", "oracle_pss", "oracle_validate", "oracle_compute_rules"):
             getattr(L, name).restype = ctypes.c_void_p
         L.oracle_format_float.restype = ctypes.c_void_p
@@ -115,3 +118,21 @@ def validate_batch(policies, resources, ns_labels=None, threads=1):
     n = lib().oracle_validate_batch(_s(policies), _s(resources), _s(ns_labels) if ns_labels else b"",
                                     threads, counts, ctypes.byref(secs))
     return n, list(counts), secs.value
+
+
+MATRIX_STATUS = ("none", "pass", "fail", "skip", "error", "panic", "unsupported", "nondeterministic")
+
+
+def validate_matrix(policies, resources, ns_labels=None, threads=8):
+    """-> (names [(policy, rule)], uint8 array [rule, resource] of MATRIX_STATUS codes)"""
+    import numpy as np
+    pj, rj = _s(policies), _s(resources)
+    # upper bound on rules: computed rules <= 3 per rule of the input (autogen)
+    cap = 3 * sum(len((p.get("spec") or {}).get("rules") or []) for p in policies) + 1
+    out = np.zeros(cap * max(1, len(resources)), dtype=np.uint8)
+    ptr = lib().oracle_validate_matrix(pj, rj, _s(ns_labels) if ns_labels else b"", threads,
+                                       out.ctypes.data, out.size)
+    if not ptr:
+        raise ValueError("oracle_validate_matrix failed")
+    names = [tuple(x) for x in json.loads(_take(ptr))]
+    return names, out[: len(names) * len(resources)].reshape(len(names), len(resources))

@@ -81,3 +81,15 @@ def golden_groups():
     wp, wr = cases.walk_policy_cases()
     groups += [([wp[i]], [wr[i]]) for i in range(len(wp))]
     return groups
+
+
+def run_c4(backend, npol, nres, seed=11, jit=None):
+    """BASELINE configs[3] (C4): generated wildcard-heavy match/exclude policies over mixed resources,
+    status parity on every pair against the oracle's verdict matrix."""
+    from kyverno_amd import synth
+    pols = synth.c4_policies(npol)
+    docs, nsl = synth.mixed(nres, seed=seed, edge=True)
+    st, res = PU.compare_matrix(pols, docs, nsl, backend=backend, jit=jit)
+    assert_clean("c4/%dx%d" % (npol, nres), st)
+    assert st["matched"] > 0
+    return st, res

@@ -75,3 +75,37 @@ def compare(policies, resources, ns_labels=None, backend="gpu", check_messages=T
     stats["nbad"] = len(bad)
     stats["counts"] = res.counts
     return stats, res
+
+
+# oracle matrix code -> device status
+_MATRIX_TO_DEVICE = {0: K.ST_NONE, 1: K.ST_PASS, 2: K.ST_FAIL, 3: K.ST_SKIP, 4: K.ST_ERROR, 5: K.ST_PANIC,
+                     6: K.ST_FALLBACK, 7: K.ST_ND}
+
+
+def compare_matrix(policies, resources, ns_labels=None, backend="gpu", jit=None, threads=8):
+    """Status-level parity for large rulesets (C4): every (resource, rule) verdict of the device vs the oracle's
+    verdict matrix (oracle.validate_matrix). Nondeterministic pairs (either side) are excluded from the count.
+    Returns (stats, results); stats["nbad"] counts mismatching pairs."""
+    import numpy as np
+    rs = E.Ruleset(policies)
+    b = E.Batch(rs, resources, ns_labels)
+    res = E.evaluate(rs, b, backend=backend, **({} if backend != "gpu" else {"jit": jit}))
+    names, m = O.validate_matrix(policies, resources, ns_labels, threads=threads)
+    row = {nm: i for i, nm in enumerate(names)}
+    lut = np.array([_MATRIX_TO_DEVICE[i] for i in range(8)], dtype=np.uint8)
+    st = np.asarray(res.status)
+    bad, compared, nd, matched = [], 0, 0, 0
+    for k, rule in enumerate(rs.rules):
+        key = (rs.policies[rule["policy"]]["name"], rule["name"])
+        want = lut[m[row[key]]] if key in row else np.zeros(len(resources), np.uint8)
+        got = st[k, : len(resources)]
+        ndm = (want == K.ST_ND) | (got == K.ST_ND)
+        nd += int(ndm.sum())
+        diff = np.nonzero((want != got) & ~ndm)[0]
+        matched += int((got != K.ST_NONE).sum())
+        compared += len(resources) - int(ndm.sum())
+        for ri in diff[:3]:
+            bad.append((key, int(ri), K.STATUS_NAMES[got[ri]], K.STATUS_NAMES[want[ri]]))
+    stats = {"pairs": len(rs.rules) * len(resources), "compared": compared, "matched": matched, "nd": nd,
+             "nbad": len(bad), "bad": bad[:20], "rules": len(rs.rules)}
+    return stats, res

@@ -36,3 +36,9 @@ def test_goldens_merged_cpu():
     """the merged golden corpus (every golden policy x every golden resource) on the host instantiation"""
     st, _ = S.run_merged("cpu", S.golden_groups(), "goldens-merged/cpu")
     assert st["compared"] > 1000
+
+
+def test_c4_policycache_stress_cpu():
+    """configs[3] shape at reduced size: 1,000 generated wildcard-heavy policies x 300 mixed resources"""
+    st, _ = S.run_c4("cpu", 1000, 300)
+    assert st["compared"] > 300000

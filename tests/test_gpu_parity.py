@@ -110,3 +110,10 @@ def test_goldens_merged_gpu_interpreter():
     st, res = S.run_merged("gpu", S.golden_groups(), "goldens-merged/interp", jit=False)
     assert not res.jit
     assert st["compared"] > 1000
+
+
+def test_c4_policycache_stress_gpu():
+    """configs[3]: the full 10,000 generated policies (match/exclude stress) over 2,000 mixed resources,
+    every pair's status against the oracle's verdict matrix"""
+    st, res = S.run_c4("gpu", 10000, 2000)
+    assert st["rules"] >= 10000 and st["compared"] > 2e7
