@@ -4,6 +4,7 @@
 #include <cstring>
 
 #include "goutil.h"
+#include "ocond.h"
 #include "oengine.h"
 #include "ojson.h"
 #include "opss.h"
@@ -351,6 +352,22 @@ extern "C" char* oracle_validate_matrix(const char* policies_json, const char* r
     return dup(oj::dump(names));
   } catch (std::exception&) {
     return nullptr;
+  }
+}
+
+// One condition as pkg/engine/variables/evaluate_test.go TestEvaluate drives it: key/value are the raw JSON of
+// Condition.RawKey / RawValue (decoded by GetKey/GetValue). Returns 1 true, 0 false, 2 reference panic, -1 bad input.
+extern "C" int oracle_condition(const char* key_json, const char* op, const char* value_json) {
+  try {
+    VP k = key_json && *key_json ? oj::parse(key_json, false) : nullptr;
+    VP v = value_json && *value_json ? oj::parse(value_json, false) : nullptr;
+    if (k && k->t == T::Null) k = nullptr;
+    if (v && v->t == T::Null) v = nullptr;
+    return evaluate_condition(k, op, v) ? 1 : 0;
+  } catch (RefPanic&) {
+    return 2;
+  } catch (...) {
+    return -1;
   }
 }
 

@@ -14,6 +14,7 @@
 #include <set>
 
 #include "goutil.h"
+#include "ocond.h"
 #include "opss.h"
 #include "ovalidate.h"
 
@@ -619,10 +620,13 @@ static bool contains_vars(const VP& v) {
 std::string rule_unsupported_reason(const VP& rule) {
   VP val = rule->get("validate");
   if (has_nonempty(rule, "context")) return "context";
-  if (!isnil(rule->get("preconditions"))) return "preconditions";
+  if (!isnil(rule->get("preconditions")) && !conditions_supported(rule->get("preconditions"))) return "preconditions";
   if (has_nonempty(rule, "verifyImages")) return "verifyImages";
   if (!val) return "";
-  if (!isnil(val->get("deny"))) return "deny";
+  if (!isnil(val->get("deny"))) {
+    VP d = val->get("deny");
+    if (d->t != T::Obj || !conditions_supported(d->get("conditions"))) return "deny";
+  }
   if (contains_vars(val->get("pattern")) || contains_vars(val->get("anyPattern"))) return "variables";
   if (isnil(val->get("pattern")) && isnil(val->get("anyPattern")) && isnil(val->get("podSecurity")) && has_nonempty(val, "foreach"))
     return "foreach";
@@ -649,6 +653,39 @@ static RuleResult validate_rule_body(const VP& rule, const VP& resource) {
   VP val = rule->get("validate");
   std::string msg = oj::get_str(val, "message");
   try {
+    VP pre = rule->get("preconditions");
+    if (!isnil(pre)) {  // checkPreconditions (validation.go:281-288, utils.go:328-341)
+      CondResult c = eval_conditions(pre, resource);
+      if (c.r == CondOutcome::Unsupported) { out.status = "unsupported"; out.message = "preconditions"; return out; }
+      if (c.r == CondOutcome::Error) {
+        out.status = "error";
+        out.message = "failed to evaluate preconditions: failed to substitute variables in preconditions: " + c.err;
+        out.message_unpinned = c.err_unpinned;
+        return out;
+      }
+      if (c.r != CondOutcome::True) { out.status = "skip"; out.message = "preconditions not met"; return out; }
+    }
+    if (!isnil(val->get("deny"))) {  // validateDeny (validation.go:437-479)
+      CondResult c = eval_conditions(val->get("deny")->get("conditions"), resource);
+      if (c.r == CondOutcome::Unsupported) { out.status = "unsupported"; out.message = "deny"; return out; }
+      if (c.r == CondOutcome::Error) {
+        out.status = "error";
+        out.message = "failed to substitute variables in deny conditions: " + c.err;
+        out.message_unpinned = c.err_unpinned;
+        return out;
+      }
+      if (c.r == CondOutcome::True) {
+        out.status = "fail";
+        bool unp = false;
+        out.message = msg.empty() ? "validation error: rule " + out.name + " failed" : render_message(msg, resource, &unp);
+        out.message_unpinned = unp;
+        out.deny_message = true;
+      } else {
+        out.status = "pass";
+        out.message = "validation rule '" + out.name + "' passed.";
+      }
+      return out;
+    }
     if (!isnil(val->get("pattern"))) {  // validatePatterns single pattern (validation.go:619-641)
       EvalFlags fl;
       PatternResult pr = match_pattern(resource, val->get("pattern"), fl);
@@ -763,7 +800,8 @@ RuleResult validate_rule(const VP& rule, const VP& resource) {
   // Variables in validate.message change only the message text (validation.go:469, :731), never the verdict:
   // the verdict stays pinned, the rendered text is left to the JMESPath substitution on the host.
   std::string msg = oj::get_str(rule->get("validate"), "message");
-  if (msg.find("{{") != std::string::npos || msg.find("$(") != std::string::npos) out.message_unpinned = true;
+  if (!out.deny_message && (msg.find("{{") != std::string::npos || msg.find("$(") != std::string::npos))
+    out.message_unpinned = true;
   return out;
 }
 

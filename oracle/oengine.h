@@ -18,6 +18,7 @@ struct RuleResult {
   std::vector<PSSResult> pss_checks;
   bool nondeterministic = false;  // verdict depends on Go map order in the reference
   bool message_unpinned = false;  // message text order/content not pinned (PSS excludes / decode errors)
+  bool deny_message = false;      // deny failure message rendered by render_message (variables resolved)
 };
 
 struct PolicyResult {

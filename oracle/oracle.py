@@ -74,6 +74,14 @@ def quantity_cmp(a, b):
     return lib().oracle_quantity_cmp(_s(a), _s(b))
 
 
+def condition(key_json, op, value_json):
+    """evaluate_test.go semantics: raw JSON key/value -> True/False, or "panic" """
+    r = lib().oracle_condition(_s(key_json), op.encode(), _s(value_json))
+    if r < 0:
+        raise ValueError("bad input")
+    return "panic" if r == 2 else bool(r)
+
+
 def duration(s):
     v = ctypes.c_longlong(0)
     ok = lib().oracle_duration(_s(s), ctypes.byref(v))

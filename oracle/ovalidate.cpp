@@ -672,3 +672,8 @@ RawWalk validate_entry(const std::string& entry, const VP& res, const VP& pat0, 
 }
 
 }  // namespace orc
+
+namespace orc {
+// operator.GetOperatorFromStringPattern(p) == operator.InRange (pkg/engine/operator/operator.go:35-61)
+bool is_in_range_pattern(const std::string& p) { return get_operator(p) == Op::InRange; }
+}  // namespace orc

@@ -52,3 +52,7 @@ struct RawWalk {
 bool leaf_fn(const std::string& fn, const oj::VP& v, const oj::VP& p, const std::string& op);
 RawWalk validate_entry(const std::string& entry, const oj::VP& res, const oj::VP& pat, EvalFlags& fl);
 }  // namespace orc
+
+namespace orc {
+bool is_in_range_pattern(const std::string& p);
+}  // namespace orc

@@ -12,6 +12,7 @@ executed or imported) and writes small JSON fixtures next to this script:
   cli.json           test/cli/test/*/kyverno-test.yaml + inputs   (CLI `kyverno test` results)
   best_practices.json test/best_practices/*.yaml                  (C1 / C3 policy set)
   chart_restricted.json charts/kyverno-policies/templates/**      (hand-rendered PSS restricted profile)
+  conditions.json    pkg/engine/variables/evaluate_test.go        (condition operators: key, operator, value -> bool)
 
 Usage: python tests/golden/extract.py [/root/reference]
 """
@@ -166,6 +167,8 @@ def extract_engine():
     recs = []
     for fname, body in functions(src):
         raws = dict(re.findall(r"(\w+) := \[\]byte\(`(.*?)`\)", body, re.S))
+        if "policyRaw" in raws and "resourceRaw" in raws and "rawPolicy" not in raws:  # deny-condition tests
+            raws["rawPolicy"], raws["rawResource"] = raws["policyRaw"], raws["resourceRaw"]
         if "rawPolicy" in raws and "rawResource" in raws and "testCases" not in body:
             m = re.search(r"msgs := \[\]string\{(.*?)\}\n", body, re.S)
             msgs = [go_unquote(x) for x in re.findall(r'"(?:[^"\\]|\\.)*"', m.group(1))] if m else None
@@ -178,6 +181,14 @@ def extract_engine():
                 continue
             recs.append({"test": fname, "policy": raws["rawPolicy"], "resource": raws["rawResource"],
                          "msgs": msgs, "successful": succ})
+        elif "expectedResults" in body and "expectedMessages" in body:  # Test_Flux_Kustomization_PathNotPresent
+            for m in re.finditer(r'name:\s*"([^"]*)",\s*policyRaw:\s*\[\]byte\(`(.*?)`\),.*?resourceRaw:\s*\[\]byte\(`(.*?)`\),'
+                                 r'\s*expectedResults:\s*\[\]engineapi\.RuleStatus\{(.*?)\},\s*expectedMessages:\s*\[\]string\{(.*?)\},\n',
+                                 body, re.S):
+                sts = [x.replace("RuleStatus", "").lower() for x in re.findall(r"engineapi\.(\w+)", m.group(4))]
+                msgs = [go_unquote(x) for x in re.findall(r'"(?:[^"\\]|\\.)*"', m.group(5))]
+                recs.append({"test": f"{fname}/{m.group(1)}", "policy": m.group(2), "resource": m.group(3),
+                             "msgs": msgs, "statuses": sts})
         elif "testCases" in body and "expectedFailed" in body:
             pol = raws.get("rawPolicy")
             for m in re.finditer(r'description:\s*"([^"]*)",\s*rawPolicy:\s*(\w+),\s*rawResource:\s*\[\]byte\(`(.*?)`\),\s*expected(\w+):\s*true', body, re.S):
@@ -329,6 +340,94 @@ def extract_chart():
     write("chart_restricted.json", recs)
 
 
+# ---------------------------------------------------------------- condition operators
+class _GoLit:
+    """Tiny parser for the Go composite literals used as condition keys/values in evaluate_test.go:
+    strings, ints, floats, int64(..), bools, nil, []interface{}{...}, []string{...}, map[string]interface{}{k: v}."""
+
+    def __init__(self, s):
+        self.s, self.i = s, 0
+
+    def ws(self):
+        while self.i < len(self.s) and self.s[self.i] in " \t\n,":
+            self.i += 1
+
+    def parse(self):
+        self.ws()
+        s, i = self.s, self.i
+        if s[i] == '"':
+            m = re.match(r'"(?:[^"\\]|\\.)*"', s[i:])
+            self.i += m.end()
+            return ("str", go_unquote(m.group(0)))
+        if s.startswith("[]", i):
+            self.i += re.match(r"\[\](?:interface\{\}|[\w.\[\]]+)\{", s[i:]).end()
+            items = []
+            while True:
+                self.ws()
+                if s[self.i] == "}":
+                    self.i += 1
+                    return ("arr", items)
+                items.append(self.parse())
+        if s.startswith("map[", i):
+            self.i += re.match(r"map\[\w+\](?:interface\{\}|\w+)\{", s[i:]).end()
+            items = []
+            while True:
+                self.ws()
+                if s[self.i] == "}":
+                    self.i += 1
+                    return ("map", items)
+                k = self.parse()
+                self.ws()
+                assert s[self.i] == ":"
+                self.i += 1
+                items.append((k[1], self.parse()))
+        m = re.match(r"(int64|float64|int)\(([^()]*)\)", s[i:])
+        if m:
+            self.i += m.end()
+            return ("num", m.group(2).strip(), m.group(1) == "float64")
+        m = re.match(r"true|false|nil", s[i:])
+        if m:
+            self.i += m.end()
+            return ("lit", m.group(0))
+        m = re.match(r"-?[0-9][0-9.eE+-]*", s[i:])
+        self.i += m.end()
+        return ("num", m.group(0), "." in m.group(0) or "e" in m.group(0).lower())
+
+
+def _go_marshal(v):
+    """json.Marshal of the decoded Go value (encoding/json: float64 integral values print without fraction)."""
+    t = v[0]
+    if t == "str":
+        return json.dumps(v[1])
+    if t == "lit":
+        return "null" if v[1] == "nil" else v[1]
+    if t == "num":
+        if v[2]:
+            f = float(v[1])
+            return str(int(f)) if f == int(f) and abs(f) < 1e21 else repr(f)
+        return str(int(v[1]))
+    if t == "arr":
+        return "[" + ",".join(_go_marshal(x) for x in v[1]) + "]"
+    return "{" + ",".join(json.dumps(k) + ":" + _go_marshal(x) for k, x in sorted(v[1])) + "}"
+
+
+def extract_conditions():
+    src = read("pkg/engine/variables/evaluate_test.go")
+    body = dict(functions(src))["TestEvaluate"]
+    recs = []
+    pat = re.compile(r'\{kyverno\.Condition\{RawKey: kyverno\.ToJSON\((.*?)\), Operator: kyverno\.ConditionOperators\["(\w+)"\], '
+                     r'RawValue: kyverno\.ToJSON\((.*?)\)\}, (true|false)\},\s*$')
+    for ln, line in enumerate(body.splitlines()):
+        m = pat.search(line.strip())
+        if not m:
+            continue
+        key, op, val, want = m.groups()
+        recs.append({"key": _go_marshal(_GoLit(key).parse()), "operator": op,
+                     "value": _go_marshal(_GoLit(val).parse()), "result": want == "true",
+                     "src": "pkg/engine/variables/evaluate_test.go TestEvaluate #%d" % len(recs)})
+    write("conditions.json", recs)
+
+
 if __name__ == "__main__":
     extract_wildcard()
     extract_pattern_leaf()
@@ -338,3 +437,4 @@ if __name__ == "__main__":
     extract_cli()
     extract_best_practices()
     extract_chart()
+    extract_conditions()

@@ -67,6 +67,8 @@ def test_engine_golden(golden):
         if r.get("msgs") is not None:
             for i, x in enumerate(rules):
                 assert x["message"] == r["msgs"][i], r["test"]
+        if r.get("statuses") is not None:
+            assert sts == r["statuses"], r["test"]
         if r.get("successful") is not None:
             assert (not any(s in ("fail", "error") for s in sts)) == r["successful"], r["test"]
         e = r.get("expect")
@@ -136,3 +138,11 @@ def test_cli_golden(golden):
         assert st == res["result"], (dname, res)
         n += 1
     assert n >= 20
+
+
+def test_conditions_golden(golden):
+    """pkg/engine/variables/evaluate_test.go TestEvaluate: every (key, operator, value) -> bool case"""
+    recs = golden("conditions.json")
+    assert len(recs) >= 330
+    for r in recs:
+        assert O.condition(r["key"], r["operator"], r["value"]) == r["result"], r
