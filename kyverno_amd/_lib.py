@@ -15,7 +15,7 @@ EVAL_JIT_ON = 8
 
 ST_NONE, ST_PASS, ST_FAIL, ST_SKIP, ST_ERROR, ST_FALLBACK, ST_PANIC, ST_ND = range(8)
 STATUS_NAMES = ["none", "pass", "fail", "skip", "error", "fallback", "panic", "nondeterministic"]
-RULE_KINDS = {1: "pattern", 2: "anyPattern", 3: "podSecurity", 4: "fallback", 5: "panic", 6: "error"}
+RULE_KINDS = {1: "pattern", 2: "anyPattern", 3: "podSecurity", 4: "fallback", 5: "panic", 6: "error", 7: "deny"}
 
 
 class CompileOpts(ctypes.Structure):

@@ -266,6 +266,22 @@ void derive_strings(Batch& b, size_t from, int threads) {
         else { b.str_qty[2 * s] = 0; b.str_qty[2 * s + 1] = 0; if (q == 2) f |= SF_QTY_BIG; }
         double fv;
         if (pj::go_parse_float(x, &fv)) { f |= SF_FLOAT; b.str_f64[s] = fv; } else b.str_f64[s] = 0;
+        {  // strconv.ParseInt(x, 10, 64): optional sign, decimal digits, int64 range
+          size_t i0 = (!x.empty() && (x[0] == '+' || x[0] == '-')) ? 1 : 0;
+          bool digits = x.size() > i0;
+          for (size_t i = i0; i < x.size() && digits; i++) digits = x[i] >= '0' && x[i] <= '9';
+          if (digits) {
+            unsigned __int128 m = 0;
+            bool ovf = false;
+            for (size_t i = i0; i < x.size() && !ovf; i++) { m = m * 10 + (unsigned)(x[i] - '0'); ovf = m > ((unsigned __int128)1 << 63); }
+            bool neg = i0 && x[0] == '-';
+            if (!ovf && (neg || m < ((unsigned __int128)1 << 63))) {
+              f |= SF_INT;
+              if (m > ((unsigned __int128)1 << 53)) f |= SF_INT_BIG;
+            }
+          }
+          if (!x.empty() && x[0] >= '0' && x[0] <= '9' && std::count(x.begin(), x.end(), '.') >= 2) f |= SF_SEMVERISH;
+        }
         // label key / value validity (apimachinery validation.IsQualifiedName / IsValidLabelValue)
         auto qn = [](const std::string& nm) {
           if (nm.empty() || nm.size() > 63) return false;

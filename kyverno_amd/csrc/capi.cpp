@@ -218,6 +218,83 @@ static int64_t put(const std::string& s, char* buf, size_t cap) {
   return (int64_t)s.size();
 }
 
+// request.object path on the host copy of a resource (kyverno/go-jmespath semantics, kyv_cond.h cv_operand):
+// returns false with *miss on a key missing from a map; *node = NONE for null
+static bool host_resolve(const Batch& b, uint32_t res, const std::vector<uint32_t>& segs, uint32_t* node, uint32_t* miss) {
+  const Node* R = b.nodes.data() + b.hdr[res].root;
+  uint32_t cur = 0;
+  for (uint32_t s = 0; s < segs.size(); s++) {
+    const Node& n = R[cur];
+    if (node_type(n) != N_MAP) { *node = NONE; return true; }
+    uint32_t hit = NONE;
+    for (uint32_t j = n.a; j < n.a + n.b; j++) if (node_key(R[j]) == segs[s]) { hit = j; break; }
+    if (hit == NONE) { *miss = s; return false; }
+    cur = hit;
+  }
+  *node = node_type(R[cur]) == N_NULL ? NONE : cur;
+  return true;
+}
+
+// vars.go:395-399 error text of the first unresolved reference of a condition program
+static bool cond_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t prog, std::string* out) {
+  const CondProg& p = rs.cprogs[prog];
+  uint32_t nany = p.nany == NONE ? 0 : p.nany;
+  for (int blk = 0; blk < 2; blk++) {
+    uint32_t c0 = blk ? p.all0 : p.any0, n = blk ? p.nall : nany;
+    for (uint32_t i = 0; i < n; i++) {
+      const Cond& c = rs.conds[c0 + i];
+      const CondText& ct = rs.cond_text[c0 + i];
+      for (int side = 0; side < 2; side++) {
+        const CondOperand& o = side ? c.value : c.key;
+        if (o.kind != OK_PATH) continue;
+        std::vector<uint32_t> segs(rs.pool.begin() + o.a, rs.pool.begin() + o.a + o.nseg);
+        uint32_t node, miss;
+        if (!host_resolve(b, res, segs, &node, &miss)) {
+          *out = "failed to resolve " + ct.var[side] + " at path " + ct.path[side] +
+                 ": JMESPath query failed: Unknown key \"" + ct.segs[side][miss] + "\" in path";
+          return true;
+        }
+      }
+    }
+  }
+  return false;
+}
+
+// getDenyMessage (validation.go:466-479) with the message's request.object references resolved; -1: not renderable
+static int64_t deny_message(const RuleMeta& m, const Batch& b, uint32_t res, char* buf, size_t cap) {
+  if (m.message.empty()) return put("validation error: rule " + m.name + " failed", buf, cap);
+  if (m.msg_parts.empty()) return put(m.message, buf, cap);
+  const Node* R = b.nodes.data() + b.hdr[res].root;
+  std::string out;
+  for (auto& part : m.msg_parts) {
+    if (!part.var) { out += part.text; continue; }
+    uint32_t node, miss;
+    if (!host_resolve(b, res, part.segs, &node, &miss)) return put(m.message, buf, cap);  // substitution error
+    std::string sub;
+    uint32_t t = node == NONE ? N_NULL : node_type(R[node]);
+    if (m.msg_whole_var)
+      return put(t == N_STR ? b.dict.strs[R[node].a] : "the produced message didn't resolve to a string, check your policy definition.", buf, cap);
+    switch (t) {
+      case N_STR: sub = b.dict.strs[R[node].a]; break;
+      case N_NULL: sub = "null"; break;
+      case N_TRUE: sub = "true"; break;
+      case N_FALSE: sub = "false"; break;
+      case N_INT: sub = pj::go_fmt_json((double)(int64_t)(((uint64_t)R[node].b << 32) | R[node].a)); break;
+      case N_FLOAT: {
+        uint64_t bits = ((uint64_t)R[node].b << 32) | R[node].a;
+        double f;
+        memcpy(&f, &bits, 8);
+        sub = pj::go_fmt_json(f);
+        break;
+      }
+      default: return -1;  // json.Marshal of a map / array
+    }
+    if (sub.find("{{") != std::string::npos) return -1;  // nested variables are substituted again
+    out += sub;
+  }
+  return put(out, buf, cap);
+}
+
 // validation.go:722-758 (buildErrorMessage / buildAnyPatternErrorMessage) and :640/:665 pass messages
 int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res, uint32_t rule,
                             char* buf, size_t cap) {
@@ -230,6 +307,21 @@ int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const
   uint8_t st = sb & 7, alt = sb >> 3;
   const RuleMeta& m = rs.meta[rule];
   const RuleDesc& d = rs.rules[rule];
+  if (sb >> 3 == (ST_MARK_PRE >> 3) && d.pre != NONE) {  // checkPreconditions outcome (validation.go:281-288)
+    if (st == ST_SKIP) return put("preconditions not met", buf, cap);
+    std::string e;
+    if (st == ST_ERROR && cond_error_text(rs, b, res, d.pre, &e))
+      return put("failed to evaluate preconditions: failed to substitute variables in preconditions: " + e, buf, cap);
+    return -1;
+  }
+  if (d.kind == RK_DENY) {  // validateDeny (validation.go:437-479)
+    if (st == ST_PASS) return put("validation rule '" + m.name + "' passed.", buf, cap);
+    if (st == ST_FAIL) return m.message_vars ? -1 : deny_message(m, b, res, buf, cap);
+    std::string e;
+    if (st == ST_ERROR && cond_error_text(rs, b, res, d.root, &e))
+      return put("failed to substitute variables in deny conditions: " + e, buf, cap);
+    return -1;
+  }
   if (m.message_vars && st == ST_FAIL) return -1;  // message needs variable substitution (CPU engine)
   std::string msg;
   if (d.kind == RK_PSS) {

@@ -980,6 +980,249 @@ uint32_t compile_pss(Cx& c, const Value& ps) {
   return (uint32_t)c.rs.pss.size() - 1;
 }
 
+// ---------------------------------------------------------------- conditions (deny / preconditions)
+// `{{ request.object(.seg)* }}` with segments that are JMESPath identifiers or quoted identifiers (no escapes):
+// the reference subset the device evaluates (vars.go:352-431 with DefaultVariableResolver)
+bool object_var(const std::string& s, std::vector<std::string>& segs, std::string* text) {
+  if (s.size() < 4 || s.compare(0, 2, "{{") != 0 || s.compare(s.size() - 2, 2, "}}") != 0) return false;
+  std::string inner = s.substr(2, s.size() - 4);
+  if (inner.find('{') != std::string::npos || inner.find('}') != std::string::npos) return false;
+  inner = pj::go_trim_space(inner);
+  const std::string pre = "request.object";
+  if (inner.compare(0, pre.size(), pre) != 0) return false;
+  auto ident = [](char ch, bool first) { return isalpha((unsigned char)ch) || ch == '_' || (!first && isdigit((unsigned char)ch)); };
+  size_t i = pre.size();
+  if (i < inner.size() && ident(inner[i], false)) return false;
+  segs.clear();
+  while (i < inner.size()) {
+    if (inner[i] != '.' || ++i >= inner.size()) return false;
+    if (inner[i] == '"') {
+      size_t j = i + 1;
+      while (j < inner.size() && inner[j] != '"') { if (inner[j] == '\\') return false; j++; }
+      if (j >= inner.size() || j == i + 1) return false;
+      segs.push_back(inner.substr(i + 1, j - i - 1));
+      i = j + 1;
+    } else if (ident(inner[i], true)) {
+      size_t j = i;
+      while (j < inner.size() && ident(inner[j], false)) j++;
+      segs.push_back(inner.substr(i, j - i));
+      i = j;
+    } else {
+      return false;
+    }
+  }
+  if (text) *text = inner;
+  return true;
+}
+bool var_syntax(const std::string& s) { return s.find("{{") != std::string::npos || s.find("$(") != std::string::npos; }
+bool var_anywhere(const Value& v) {
+  if (v.t == T::Str) return var_syntax(v.s);
+  for (auto& e : v.a) if (var_anywhere(e)) return true;
+  for (auto& kv : v.o) if (var_syntax(kv.first) || var_anywhere(kv.second)) return true;
+  return false;
+}
+// operator.GetOperatorFromStringPattern(s) == InRange (pkg/engine/operator/operator.go:35-61)
+bool in_range_pattern(const std::string& s) {
+  if (s.size() < 2) return false;
+  if (s[0] == '>' || s[0] == '<' || s[0] == '!') return false;
+  std::string l, r;
+  if (range_split(s, "!-", l, r)) return false;
+  return range_split(s, "-", l, r);
+}
+
+// literal JSON value -> cnodes (after the Condition.GetKey round trip: json.Marshal + util/json decode)
+uint32_t emit_cnode(Cx& c, const Value& v) {
+  Node n{};
+  switch (v.t) {
+    case T::Null: n.tk = N_NULL; break;
+    case T::Bool: n.tk = v.b ? N_TRUE : N_FALSE; n.a = v.b; break;
+    case T::Int: n.tk = N_INT; n.a = (uint32_t)(uint64_t)v.i; n.b = (uint32_t)((uint64_t)v.i >> 32);
+      n.c = c.sid(std::to_string(v.i)); break;
+    case T::Float: {
+      uint64_t bits;
+      memcpy(&bits, &v.f, 8);
+      n.tk = N_FLOAT; n.a = (uint32_t)bits; n.b = (uint32_t)(bits >> 32); n.c = c.sid(pj::go_fmt_g(v.f));
+      break;
+    }
+    case T::Str: n.tk = N_STR; n.a = c.sid(v.s); break;
+    case T::Arr: {
+      uint32_t at = (uint32_t)c.rs.cnodes.size();
+      n.tk = N_ARR; n.a = at + 1; n.b = (uint32_t)v.a.size();
+      c.rs.cnodes.push_back(n);
+      for (auto& e : v.a) {
+        if (e.t == T::Arr || e.t == T::Obj) throw Fallback{"conditions: nested literal"};
+        emit_cnode(c, e);
+      }
+      return at;
+    }
+    default: throw Fallback{"conditions: map literal"};
+  }
+  c.rs.cnodes.push_back(n);
+  return (uint32_t)c.rs.cnodes.size() - 1;
+}
+
+CondOperand compile_operand(Cx& c, const Value* v, CondText& ct, int side, const std::string& path) {
+  CondOperand o{};
+  o.kind = OK_NIL;
+  ct.path[side] = path;
+  if (!v || v->t == T::Null) return o;
+  if (v->t == T::Str && var_syntax(v->s)) {
+    std::vector<std::string> segs;
+    if (!object_var(v->s, segs, &ct.var[side])) throw Fallback{"conditions: variables beyond request.object paths"};
+    o.kind = OK_PATH;
+    o.nseg = (uint16_t)segs.size();
+    o.a = (uint32_t)c.rs.pool.size();
+    for (auto& sg : segs) c.rs.pool.push_back(c.sid(sg));
+    ct.segs[side] = segs;
+    return o;
+  }
+  if (var_anywhere(*v)) throw Fallback{"conditions: variables inside a literal"};
+  Value lit = pj::parse(pj::dump(*v), false);
+  if (lit.t == T::Null) return o;
+  o.kind = OK_LIT;
+  o.a = emit_cnode(c, lit);
+  if (lit.t == T::Str) {
+    const std::string& s = lit.s;
+    if (in_range_pattern(s)) o.sv |= SV_RANGE;
+    try {
+      Value j = pj::parse(s, true);
+      o.sv |= SV_JSON;
+      bool ok = j.t == T::Null || j.t == T::Arr;
+      if (j.t == T::Arr) for (auto& e : j.a) if (e.t != T::Str && e.t != T::Null) ok = false;
+      if (ok) {
+        o.sv |= SV_LIST;
+        o.list = (uint32_t)c.rs.pool.size();
+        o.nlist = (uint32_t)j.a.size();
+        for (auto& e : j.a) c.rs.pool.push_back(c.sid(e.t == T::Str ? e.s : ""));
+      }
+    } catch (pj::Error&) {
+    }
+  }
+  return o;
+}
+
+// operator name -> CondOp (operator.go:27-75: handler chosen case-insensitively; numeric compareByCondition
+// matches the exact operator name, so other spellings of the numeric operators are always false)
+uint8_t cond_op(const std::string& op) {
+  std::string l = op;
+  for (auto& ch : l) ch = (char)tolower((unsigned char)ch);
+  if (l.compare(0, 8, "duration") == 0 && (l == "durationgreaterthanorequals" || l == "durationgreaterthan" ||
+                                           l == "durationlessthanorequals" || l == "durationlessthan"))
+    throw Fallback{"conditions: Duration* operator"};
+  if (l == "equal" || l == "equals") return CO_EQ;
+  if (l == "notequal" || l == "notequals") return CO_NE;
+  if (l == "in") return CO_IN;
+  if (l == "notin") return CO_NOTIN;
+  if (l == "anyin") return CO_ANYIN;
+  if (l == "allin") return CO_ALLIN;
+  if (l == "anynotin") return CO_ANYNOTIN;
+  if (l == "allnotin") return CO_ALLNOTIN;
+  if (op == "GreaterThan") return CO_GT;
+  if (op == "GreaterThanOrEquals") return CO_GE;
+  if (op == "LessThan") return CO_LT;
+  if (op == "LessThanOrEquals") return CO_LE;
+  return CO_FALSE;
+}
+bool valid_op_exact(const std::string& op) {  // kyvernov1.ConditionOperators (common_types.go:225-244)
+  static const char* ops[] = {"Equal", "Equals", "NotEqual", "NotEquals", "In", "AnyIn", "AllIn", "NotIn", "AnyNotIn",
+                              "AllNotIn", "GreaterThanOrEquals", "GreaterThan", "LessThanOrEquals", "LessThan",
+                              "DurationGreaterThanOrEquals", "DurationGreaterThan", "DurationLessThanOrEquals",
+                              "DurationLessThan"};
+  for (auto o : ops) if (op == o) return true;
+  return false;
+}
+
+uint32_t compile_cond(Cx& c, const Value& e, const std::string& path, bool old_list) {
+  if (e.t != T::Obj) throw Fallback{"conditions: malformed condition"};
+  for (auto& kv : e.o)
+    if (kv.first != "key" && kv.first != "operator" && kv.first != "value" && kv.first != "message")
+      throw Fallback{"conditions: unknown condition field"};
+  const Value* op = e.get("operator");
+  if (op && op->t != T::Str && op->t != T::Null) throw Fallback{"conditions: malformed operator"};
+  std::string ops = op && op->t == T::Str ? op->s : "";
+  if (old_list && !valid_op_exact(ops)) throw Fallback{"conditions: invalid condition operator"};
+  Cond cd{};
+  cd.op = cond_op(ops);
+  cd.leaf = cd.leaf_neg = NONE;
+  CondText ct;
+  cd.key = compile_operand(c, e.get("key"), ct, 0, path + "/key");
+  cd.value = compile_operand(c, e.get("value"), ct, 1, path + "/value");
+  if (cd.value.sv & SV_RANGE) {
+    const std::string& s = c.rs.dict.strs[c.rs.cnodes[cd.value.a].a];
+    cd.leaf = compile_leaf(c, Value::S(s));
+    std::string s2 = s;
+    size_t i = s2.find('-');
+    if (i != std::string::npos) s2.replace(i, 1, "!-");
+    cd.leaf_neg = compile_leaf(c, Value::S(s2));
+  }
+  c.rs.conds.push_back(cd);
+  c.rs.cond_text.push_back(ct);
+  return (uint32_t)c.rs.conds.size() - 1;
+}
+
+// rule.preconditions / validate.deny.conditions -> CondProg (utils/utils.go:52 TransformConditions,
+// pkg/utils/api/json.go:30-85); shapes outside the device subset throw Fallback
+uint32_t compile_conds(Cx& c, const Value* doc) {
+  CondProg p{};
+  p.nany = NONE;
+  std::vector<Cond> blk;
+  auto block = [&](const Value& list, const std::string& base, bool old_list, uint32_t* first, uint32_t* n) {
+    std::vector<uint32_t> ids;
+    for (size_t i = 0; i < list.a.size(); i++) ids.push_back(compile_cond(c, list.a[i], base + "/" + std::to_string(i), old_list));
+    *first = ids.empty() ? (uint32_t)c.rs.conds.size() : ids[0];
+    *n = (uint32_t)ids.size();
+  };
+  if (!doc || doc->t == T::Null) {
+    p.all0 = 0; p.nall = 0;
+  } else if (doc->t == T::Arr) {
+    block(*doc, "", true, &p.all0, &p.nall);
+  } else if (doc->t == T::Obj) {
+    for (auto& kv : doc->o) if (kv.first != "any" && kv.first != "all") throw Fallback{"conditions: unknown field"};
+    const Value* any = doc->get("any");
+    const Value* all = doc->get("all");
+    if (any && any->t != T::Null) {
+      if (any->t != T::Arr) throw Fallback{"conditions: malformed any"};
+      block(*any, "/any", false, &p.any0, &p.nany);
+    }
+    if (all && all->t != T::Null) {
+      if (all->t != T::Arr) throw Fallback{"conditions: malformed all"};
+      block(*all, "/all", false, &p.all0, &p.nall);
+    }
+  } else {
+    throw Fallback{"conditions: malformed"};
+  }
+  c.rs.cprogs.push_back(p);
+  return (uint32_t)c.rs.cprogs.size() - 1;
+}
+
+// deny message with `{{ request.object... }}` references -> parts (false: other variables, escapes, references)
+bool compile_message(Cx& c, const std::string& msg, RuleMeta& rm) {
+  rm.msg_parts.clear();
+  rm.msg_whole_var = false;
+  if (!var_syntax(msg)) return true;
+  if (msg.find("$(") != std::string::npos || msg.find("\\{{") != std::string::npos) return false;
+  std::vector<std::string> segs;
+  auto add_var = [&](const std::vector<std::string>& sg) {
+    RuleMeta::MsgPart mp;
+    mp.var = true;
+    for (auto& x : sg) mp.segs.push_back(c.sid(x));
+    rm.msg_parts.push_back(mp);
+  };
+  if (object_var(msg, segs, nullptr)) { rm.msg_whole_var = true; add_var(segs); return true; }
+  size_t i = 0;
+  while (i < msg.size()) {
+    size_t a = msg.find("{{", i);
+    if (a == std::string::npos) { rm.msg_parts.push_back({msg.substr(i), {}, false}); break; }
+    size_t b = msg.find("}}", a + 2);
+    if (b == std::string::npos) return false;
+    if (!object_var(msg.substr(a, b + 2 - a), segs, nullptr)) return false;
+    if (a > i) rm.msg_parts.push_back({msg.substr(i, a - i), {}, false});
+    add_var(segs);
+    i = b + 2;
+  }
+  return true;
+}
+
 // ---------------------------------------------------------------- rule classification
 bool contains_vars(const Value& v) {
   auto hit = [](const std::string& s) { return s.find("{{") != std::string::npos || s.find("$(") != std::string::npos; };
@@ -992,10 +1235,9 @@ bool contains_vars(const Value& v) {
 std::string fallback_reason(const Value& r) {  // validator.validate dispatch (validation.go:276-317)
   const Value* val = r.get("validate");
   if (nonempty(r.get("context"))) return "context";
-  if (!nil(r.get("preconditions"))) return "preconditions";
   if (nonempty(r.get("verifyImages"))) return "verifyImages";
   if (!val) return "";
-  if (!nil(val->get("deny"))) return "deny";
+  if (!nil(val->get("deny"))) return val->get("deny")->t == T::Obj ? "" : "deny";
   if ((val->get("pattern") && contains_vars(*val->get("pattern"))) || (val->get("anyPattern") && contains_vars(*val->get("anyPattern"))))
     return "variables";
   if (nil(val->get("pattern")) && nil(val->get("anyPattern")) && nil(val->get("podSecurity")) && nonempty(val->get("foreach")))
@@ -1036,6 +1278,7 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
         bool hasValidate = val && val->t == T::Obj && !val->o.empty();
         if (!hasValidate && !nonempty(r.get("verifyImages"))) continue;  // no response (validation.go:144-149)
         RuleDesc rd{};
+        rd.pre = NONE;
         RuleMeta rm;
         rm.name = r.str_or("name");
         rm.message = val ? val->str_or("message") : "";
@@ -1043,7 +1286,8 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
         rm.message_vars = rm.message.find("{{") != std::string::npos || rm.message.find("$(") != std::string::npos;
         rd.policy = pidx;
         size_t mark_p = rs->pnodes.size(), mark_e = rs->pentries.size(), mark_l = rs->leaves.size(),
-               mark_a = rs->atoms.size(), mark_pool = rs->pool.size(), mark_t = rs->templates.size();
+               mark_a = rs->atoms.size(), mark_pool = rs->pool.size(), mark_t = rs->templates.size(),
+               mark_cn = rs->cnodes.size(), mark_cd = rs->conds.size(), mark_cp = rs->cprogs.size();
         try {
           bool em = false;
           rd.match = compile_block(c, r.get("match"), true, &em);
@@ -1052,9 +1296,15 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
           std::string why = fallback_reason(r);
           c.nslots = 0;
           c.sites.clear();
+          rd.pre = NONE;
+          if (why.empty() && !nil(r.get("preconditions"))) rd.pre = compile_conds(c, r.get("preconditions"));
           if (!why.empty()) {
             rd.kind = RK_FALLBACK;
             rm.reason = why;
+          } else if (val && !nil(val->get("deny"))) {  // deny wins over pattern (validation.go:290-292)
+            rd.kind = RK_DENY;
+            rd.root = compile_conds(c, val->get("deny")->get("conditions"));
+            rm.message_vars = !compile_message(c, rm.message, rm);
           } else if (val && !nil(val->get("pattern"))) {
             rd.kind = RK_PATTERN;
             rd.root = compile_pattern_root(c, *val->get("pattern"));
@@ -1088,9 +1338,12 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
         } catch (Fallback& f) {
           rs->pnodes.resize(mark_p); rs->pentries.resize(mark_e); rs->leaves.resize(mark_l);
           rs->atoms.resize(mark_a); rs->templates.resize(mark_t);
+          rs->cnodes.resize(mark_cn); rs->conds.resize(mark_cd); rs->cond_text.resize(mark_cd); rs->cprogs.resize(mark_cp);
           (void)mark_pool;
           rd.kind = RK_FALLBACK;
+          rd.pre = NONE;
           rm.reason = f.why;
+          rm.msg_parts.clear();
         }
         rm.kind = rd.kind;
         rs->rules.push_back(rd);
@@ -1195,7 +1448,7 @@ struct TrieBuilder {
 void mark_gate_exact(Ruleset& rs) {
   for (auto& rd : rs.rules) {
     rd.flags &= (uint8_t)~RD_GATE_EXACT;
-    if (rd.empty_may_match || rd.exclude.mode != MM_NONE) continue;
+    if (rd.empty_may_match || rd.exclude.mode != MM_NONE || rd.pre != NONE) continue;
     const MatchBlock& m = rd.match;
     if (m.mode == MM_NONE || m.nfilters == 0) continue;
     if (m.mode != MM_ANY && m.nfilters != 1) continue;

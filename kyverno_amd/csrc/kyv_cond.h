@@ -1,0 +1,490 @@
+// Conditions of validate.deny and rule preconditions for one (resource, rule) pair, __host__ __device__.
+//
+// Reference (paths relative to /root/reference):
+//   pkg/engine/variables/evaluate.go:11-83           Evaluate, any/all blocks, old-style list
+//   pkg/engine/variables/operator/*.go               operator handlers (equal, notequal, in, notin, anyin, allin,
+//                                                    anynotin, allnotin, numeric)
+//   pkg/engine/variables/vars.go:352-431             `{{ request.object... }}` substitution; a key missing from a map
+//                                                    is a NotFoundError from the kyverno/go-jmespath fork
+//   api/kyverno/v1/common_types.go:185-199           Condition.GetKey/GetValue: the substituted document goes
+//                                                    through json.Marshal + apimachinery util/json (integral -> int64)
+//
+// Values are typed as the operator handlers see them (after that round trip). Where the device cannot
+// reproduce the reference bit for bit (fmt.Sprint of a float that is not in the dictionary, a resource-side
+// string the handler would JSON-decode, semver operands, quantities beyond int128 nano units, composite
+// elements) the pair returns ST_FALLBACK and the CPU engine decides it.
+#pragma once
+#include "kyv_eval.h"
+
+namespace kyv {
+
+enum CondRes : uint8_t { CR_FALSE = 0, CR_TRUE = 1, CR_FB = 2, CR_PANIC = 3 };
+enum CType : uint8_t { CT_NIL = 0, CT_BOOL = 1, CT_INT = 2, CT_FLOAT = 3, CT_STR = 4, CT_ARR = 5, CT_MAP = 6 };
+
+struct CV {
+  uint8_t t;       // CType
+  uint8_t res;     // 1: resource node table, 0: ruleset literal (cnodes)
+  uint8_t b;       // CT_BOOL
+  uint8_t pad;
+  uint32_t sid;    // CT_STR: the string; else fmt.Sprint form (NONE when not in the dictionary)
+  uint32_t node;   // CT_ARR / CT_MAP: node index (relative to the resource root / absolute in cnodes)
+  uint32_t n;      // CT_ARR: element count
+  int64_t i;
+  double f;
+};
+
+constexpr double TWO63 = 9223372036854775808.0;
+
+KYV_HD int64_t go_f2i(double f) {  // int64(float64) as amd64 does it (out of range -> min int64)
+  if (!(f >= -TWO63 && f < TWO63)) return INT64_MIN;
+  return (int64_t)f;
+}
+
+KYV_HD CV cv_node(const Node& n, bool res) {
+  CV x;
+  x.t = CT_NIL; x.res = res ? 1 : 0; x.b = 0; x.pad = 0; x.sid = KSID(NIL_STR); x.node = NONE; x.n = 0; x.i = 0; x.f = 0;
+  switch (node_type(n)) {
+    case N_NULL: break;
+    case N_FALSE: x.t = CT_BOOL; x.sid = SID_FALSE; break;
+    case N_TRUE: x.t = CT_BOOL; x.b = 1; x.sid = SID_TRUE; break;
+    case N_INT: {
+      int64_t i = (int64_t)(((uint64_t)n.b << 32) | n.a);
+      x.t = CT_INT; x.i = i; x.sid = n.c;
+      if (res) {  // JSON context decode (float64) then the util/json round trip
+        double d = (double)i;
+        if (d >= TWO63) { x.t = CT_FLOAT; x.f = d; x.sid = NONE; }
+        else { x.i = (int64_t)d; if (x.i != i) x.sid = NONE; }
+      }
+      break;
+    }
+    case N_FLOAT: {
+      double f = __builtin_bit_cast(double, ((uint64_t)n.b << 32) | n.a);
+      x.t = CT_FLOAT; x.f = f; x.sid = res ? NONE : n.c;
+      if (res && f == __builtin_trunc(f) && f > -1e21 && f < 1e21 && f >= -TWO63 && f < TWO63) {
+        x.t = CT_INT; x.i = (int64_t)f;  // integral: json "%f"-style digits decode as int64
+      }
+      break;
+    }
+    case N_STR: x.t = CT_STR; x.sid = n.a; break;
+    case N_ARR: x.t = CT_ARR; x.node = NONE; x.n = n.b; x.sid = NONE; break;
+    case N_MAP: x.t = CT_MAP; x.sid = NONE; break;
+    default: break;
+  }
+  return x;
+}
+
+// element j of an array operand
+KYV_HD CV cv_elem(const View& v, NodeTab R, const CV& arr, uint32_t j) {
+  if (arr.res) {
+    const Node& a = R[arr.node];
+    return cv_node(R[a.a + j], true);
+  }
+  const Node& a = v.cnodes[arr.node];
+  return cv_node(v.cnodes[a.a + j], false);
+}
+
+// operand value; returns false on a NotFoundError (*miss = failing segment)
+KYV_HD bool cv_operand(const View& v, NodeTab R, const CondOperand& o, CV* out, uint32_t* miss) {
+  if (o.kind == OK_LIT) {
+    *out = cv_node(v.cnodes[o.a], false);
+    if (out->t == CT_ARR) out->node = o.a;
+    return true;
+  }
+  Node nil{N_NULL, 0, 0, 0};
+  if (o.kind != OK_PATH) { *out = cv_node(nil, false); return true; }
+  uint32_t cur = 0;  // request.object = the resource root
+  for (uint32_t s = 0; s < o.nseg; s++) {
+    const Node& n = R[cur];
+    if (node_type(n) != N_MAP) { *out = cv_node(nil, true); return true; }  // field of a non-map: null
+    uint32_t nx = map_find(R, cur, v.pool[o.a + s]);
+    if (nx == NONE) { *miss = s; return false; }
+    cur = nx;
+  }
+  *out = cv_node(R[cur], true);
+  if (out->t == CT_ARR) out->node = cur;
+  return true;
+}
+
+KYV_HD uint32_t sflags(const View& v, uint32_t sid) { return v.str_flags[sid]; }
+
+// operator.parseDuration (operator.go:94-138): 1 both durations (seconds), 0 not durations
+KYV_HD int dur_side(const View& v, const CV& x, int64_t* d, bool* have) {
+  *have = false;
+  if (x.t == CT_STR && x.sid != SID_ZERO && (sflags(v, x.sid) & SF_DUR)) { *d = v.str_dur[x.sid]; *have = true; }
+  return 0;
+}
+KYV_HD bool num_secs(const CV& x, int64_t* d) {
+  if (x.t == CT_INT) { *d = (int64_t)((uint64_t)x.i * 1000000000ull); return true; }
+  if (x.t == CT_FLOAT) { *d = (int64_t)((uint64_t)go_f2i(x.f) * 1000000000ull); return true; }
+  return false;
+}
+KYV_HD double dur_seconds(int64_t d) {  // time.Duration.Seconds
+  int64_t sec = d / 1000000000LL, nsec = d % 1000000000LL;
+  return (double)sec + (double)nsec / 1e9;
+}
+KYV_HD bool parse_duration2(const View& v, const CV& k, const CV& x, double* ks, double* vs) {
+  int64_t kd = 0, vd = 0;
+  bool hk, hv;
+  dur_side(v, k, &kd, &hk);
+  dur_side(v, x, &vd, &hv);
+  if (!hk && !hv) return false;
+  if (!hk && !num_secs(k, &kd)) return false;
+  if (!hv && !num_secs(x, &vd)) return false;
+  *ks = dur_seconds(kd);
+  *vs = dur_seconds(vd);
+  return true;
+}
+
+KYV_HD bool qty_ok(const View& v, uint32_t sid) { return (sflags(v, sid) & (SF_QTY | SF_QTY_BIG)) != 0; }
+// Quantity.Cmp; CR_FB when either side is beyond int128 nano units
+KYV_HD int qty_cmp(const View& v, uint32_t a, uint32_t b, bool* fb) {
+  if ((sflags(v, a) | sflags(v, b)) & SF_QTY_BIG) { *fb = true; return 0; }
+  return cmp128(v.str_qty[2 * a + 1], (uint64_t)v.str_qty[2 * a], v.str_qty[2 * b + 1], (uint64_t)v.str_qty[2 * b]);
+}
+// strconv.ParseInt(s, 10, 64): 1 ok (*out), 0 error, 2 ok but not exact in the dictionary's float column
+KYV_HD int parse_int_sid(const View& v, uint32_t sid, int64_t* out) {
+  uint32_t f = sflags(v, sid);
+  if (!(f & SF_INT)) return 0;
+  if (f & SF_INT_BIG) return 2;
+  *out = (int64_t)v.str_f64[sid];
+  return 1;
+}
+
+// ---------------------------------------------------------------- Equal / NotEqual (equal.go, notequal.go)
+KYV_HD int deep_equal_arr(const View& v, NodeTab R, const CV& a, const CV& b) {
+  if (a.n != b.n) return CR_FALSE;
+  for (uint32_t j = 0; j < a.n; j++) {
+    CV x = cv_elem(v, R, a, j), y = cv_elem(v, R, b, j);
+    if (x.t == CT_ARR || x.t == CT_MAP || y.t == CT_ARR || y.t == CT_MAP) return CR_FB;
+    if (x.t != y.t) return CR_FALSE;
+    bool eq = true;
+    switch (x.t) {
+      case CT_BOOL: eq = x.b == y.b; break;
+      case CT_INT: eq = x.i == y.i; break;
+      case CT_FLOAT: eq = x.f == y.f; break;
+      case CT_STR: eq = x.sid == y.sid; break;
+      default: break;
+    }
+    if (!eq) return CR_FALSE;
+  }
+  return CR_TRUE;
+}
+
+KYV_HD int op_equal(const View& v, NodeTab R, const CV& k, const CV& x, bool neg) {
+  auto ret = [&](bool b) { return (int)((b != neg) ? CR_TRUE : CR_FALSE); };
+  switch (k.t) {
+    case CT_BOOL:
+      if (x.t != CT_BOOL) return neg ? CR_TRUE : CR_FALSE;
+      return ret(x.b == k.b);
+    case CT_INT:
+      switch (x.t) {
+        case CT_INT: return ret(x.i == k.i);
+        case CT_FLOAT: return x.f == __builtin_trunc(x.f) ? ret(go_f2i(x.f) == k.i) : CR_FALSE;
+        case CT_STR: {
+          int64_t y;
+          int p = parse_int_sid(v, x.sid, &y);
+          if (p == 2) return CR_FB;
+          return p ? ret(y == k.i) : (neg ? CR_TRUE : CR_FALSE);
+        }
+        default: return neg ? CR_TRUE : CR_FALSE;
+      }
+    case CT_FLOAT:
+      switch (x.t) {
+        case CT_INT: return k.f == __builtin_trunc(k.f) ? ret(go_f2i(k.f) == x.i) : (neg ? CR_TRUE : CR_FALSE);
+        case CT_FLOAT: return ret(x.f == k.f);
+        case CT_STR:
+          if (sflags(v, x.sid) & SF_FLOAT) return ret(v.str_f64[x.sid] == k.f);
+          return neg ? CR_TRUE : CR_FALSE;
+        default: return neg ? CR_TRUE : CR_FALSE;
+      }
+    case CT_STR: {
+      double ks, vs;
+      if (parse_duration2(v, k, x, &ks, &vs)) return ret(ks == vs);
+      if (qty_ok(v, k.sid) && x.t == CT_STR) {
+        if (neg && x.sid == SID_EMPTY) return glob_sid(v, x.sid, k.sid) ? CR_FALSE : CR_TRUE;
+        if (!qty_ok(v, x.sid)) return CR_FALSE;
+        bool fb = false;
+        int c = qty_cmp(v, k.sid, x.sid, &fb);
+        if (fb) return CR_FB;
+        return ret(c == 0);
+      }
+      if (x.t == CT_STR) return ret(glob_sid(v, x.sid, k.sid));
+      return neg ? CR_TRUE : CR_FALSE;
+    }
+    case CT_ARR:
+      if (x.t != CT_ARR) return neg ? CR_TRUE : CR_FALSE;
+      {
+        int r = deep_equal_arr(v, R, k, x);
+        return r == CR_FB ? CR_FB : ret(r == CR_TRUE);
+      }
+    case CT_MAP:
+      if (x.t != CT_MAP) return neg ? CR_TRUE : CR_FALSE;
+      return CR_FB;
+    default: return CR_FALSE;  // nil key: no handler branch
+  }
+}
+
+// ---------------------------------------------------------------- In / NotIn (in.go, notin.go)
+KYV_HD bool wild2(const View& v, uint32_t a, uint32_t b) { return glob_sid(v, a, b) || glob_sid(v, b, a); }
+
+// fmt.Sprint form of a scalar key / element; NONE -> the device cannot render it
+KYV_HD uint32_t sprint_sid(const CV& x) {
+  if (x.t == CT_ARR || x.t == CT_MAP) return NONE;
+  return x.sid;
+}
+
+// key string vs value: keyExistsInArray (in.go:52-86) when in_list; anyKeyExistsInArray (anyin.go:51-96) otherwise.
+// returns CR_TRUE/CR_FALSE for exists, CR_FB, or 4 = invalidType
+constexpr int CR_INVALID = 4;
+KYV_HD int key_exists(const View& v, NodeTab R, uint32_t ks, const CV& x, const Cond& c, bool in_list) {
+  if (x.t == CT_ARR) {
+    for (uint32_t j = 0; j < x.n; j++) {
+      uint32_t es = sprint_sid(cv_elem(v, R, x, j));
+      if (es == NONE) return CR_FB;
+      if (wild2(v, es, ks)) return CR_TRUE;
+    }
+    return CR_FALSE;
+  }
+  if (x.t != CT_STR) return CR_INVALID;
+  if (glob_sid(v, x.sid, ks)) return CR_TRUE;
+  if (x.res) return CR_FB;  // resource-side string the handler would JSON-decode
+  const CondOperand& o = c.value;
+  if (!in_list) {
+    if (o.sv & SV_RANGE) {
+      Val y;
+      y.t = N_STR; y.sid = y.wsid = y.nsid = ks; y.i = 0; y.f = 0;
+      bool fb = false;
+      bool r = leaf_match(v, v.leaves[c.leaf], y, &fb);
+      if (fb) return CR_FB;
+      return r ? CR_TRUE : CR_FALSE;
+    }
+    if (!(o.sv & SV_JSON)) return ks == x.sid ? CR_TRUE : CR_FALSE;  // arr = [value]
+  }
+  if (!(o.sv & SV_LIST)) return CR_INVALID;
+  for (uint32_t j = 0; j < o.nlist; j++) if (v.pool[o.list + j] == ks) return CR_TRUE;
+  return CR_FALSE;
+}
+
+constexpr uint32_t MAX_CKEYS = 16;
+
+// key list: element sids (fmt.Sprint, or v.(string) for In/NotIn which panics on non-strings)
+KYV_HD int key_list(const View& v, NodeTab R, const CV& k, bool strict, uint32_t* ks, uint32_t* n) {
+  if (k.n > MAX_CKEYS) return CR_FB;
+  *n = k.n;
+  for (uint32_t j = 0; j < k.n; j++) {
+    CV e = cv_elem(v, R, k, j);
+    if (strict && e.t != CT_STR) return CR_PANIC;
+    ks[j] = sprint_sid(e);
+    if (ks[j] == NONE) return CR_FB;
+  }
+  return CR_TRUE;
+}
+
+KYV_HD int op_in(const View& v, NodeTab R, const Cond& c, const CV& k, const CV& x, bool notin) {
+  if (k.t == CT_STR || k.t == CT_INT || k.t == CT_FLOAT) {
+    uint32_t ks = sprint_sid(k);
+    if (ks == NONE) return CR_FB;
+    int e = key_exists(v, R, ks, x, c, true);
+    if (e == CR_FB) return CR_FB;
+    if (e == CR_INVALID) return CR_FALSE;
+    return (e == CR_TRUE) != notin ? CR_TRUE : CR_FALSE;
+  }
+  if (k.t != CT_ARR) return CR_FALSE;
+  uint32_t ks[MAX_CKEYS], n = 0;
+  int kr = key_list(v, R, k, true, ks, &n);
+  if (kr != CR_TRUE) return kr;
+  // setExistsInArray (in.go:104-143)
+  auto found = [&](uint32_t s, const CV* arr, const CondOperand* lst) {
+    if (arr) {
+      for (uint32_t j = 0; j < arr->n; j++) if (cv_elem(v, R, *arr, j).sid == s) return true;
+      return false;
+    }
+    for (uint32_t j = 0; j < lst->nlist; j++) if (v.pool[lst->list + j] == s) return true;
+    return false;
+  };
+  const CV* arr = nullptr;
+  if (x.t == CT_ARR) {
+    for (uint32_t j = 0; j < x.n; j++) if (cv_elem(v, R, x, j).t != CT_STR) return CR_FALSE;  // invalidType
+    arr = &x;
+  } else if (x.t == CT_STR) {
+    if (n == 1 && ks[0] == x.sid) return CR_TRUE;
+    if (x.res) return CR_FB;
+    if (!(c.value.sv & SV_LIST)) return CR_FALSE;
+  } else {
+    return CR_FALSE;
+  }
+  bool all_in = true;
+  for (uint32_t i = 0; i < n; i++) if (!found(ks[i], arr, &c.value)) { all_in = false; break; }
+  return (notin ? !all_in : all_in) ? CR_TRUE : CR_FALSE;
+}
+
+// ---------------------------------------------------------------- AnyIn / AllIn / AnyNotIn / AllNotIn
+KYV_HD int op_any_all(const View& v, NodeTab R, const Cond& c, const CV& k, const CV& x, bool all, bool neg) {
+  if (k.t == CT_STR || k.t == CT_INT || k.t == CT_FLOAT) {
+    uint32_t ks = sprint_sid(k);
+    if (ks == NONE) return CR_FB;
+    int e = key_exists(v, R, ks, x, c, false);
+    if (e == CR_FB) return CR_FB;
+    if (e == CR_INVALID) return CR_FALSE;
+    return (e == CR_TRUE) != neg ? CR_TRUE : CR_FALSE;
+  }
+  if (k.t != CT_ARR) return CR_FALSE;
+  uint32_t ks[MAX_CKEYS], n = 0;
+  int kr = key_list(v, R, k, false, ks, &n);
+  if (kr != CR_TRUE) return kr;
+  // anySetExistsInArray / allSetExistsInArray (anyin.go:115-180, allin.go:115-180)
+  uint32_t matched = 0;
+  if (x.t == CT_ARR) {
+    for (uint32_t i = 0; i < n; i++)
+      for (uint32_t j = 0; j < x.n; j++) {
+        uint32_t es = sprint_sid(cv_elem(v, R, x, j));
+        if (es == NONE) return CR_FB;
+        if (wild2(v, ks[i], es)) { matched++; break; }
+      }
+  } else if (x.t == CT_STR) {
+    if (n == 1 && ks[0] == x.sid) return neg ? CR_FALSE : CR_TRUE;
+    if (x.res) return CR_FB;
+    const CondOperand& o = c.value;
+    if (o.sv & SV_RANGE) {
+      uint32_t hits = 0;
+      for (uint32_t i = 0; i < n; i++) {
+        Val y;
+        y.t = N_STR; y.sid = y.wsid = y.nsid = ks[i]; y.i = 0; y.f = 0;
+        bool fb = false;
+        bool r = leaf_match(v, v.leaves[(!all && neg) ? c.leaf_neg : c.leaf], y, &fb);
+        if (fb) return CR_FB;
+        hits += r ? 1u : 0u;
+      }
+      if (!all) return hits > 0 ? CR_TRUE : CR_FALSE;       // AnyIn; AnyNotIn (on the "!-" pattern)
+      if (neg) return hits == 0 ? CR_TRUE : CR_FALSE;       // AllNotIn
+      return hits == n ? CR_TRUE : CR_FALSE;                // AllIn
+    }
+    if (o.sv & SV_JSON) {
+      if (!(o.sv & SV_LIST)) return CR_FALSE;  // invalidType
+      for (uint32_t i = 0; i < n; i++)
+        for (uint32_t j = 0; j < o.nlist; j++)
+          if (wild2(v, ks[i], v.pool[o.list + j])) { matched++; break; }
+    } else {
+      for (uint32_t i = 0; i < n; i++) if (wild2(v, ks[i], x.sid)) matched++;
+    }
+  } else {
+    return CR_FALSE;
+  }
+  bool r;
+  if (!all) r = neg ? matched < n : matched > 0;
+  else r = neg ? matched == 0 : matched == n;
+  return r ? CR_TRUE : CR_FALSE;
+}
+
+// ---------------------------------------------------------------- numeric (numeric.go)
+KYV_HD bool cmp_by(uint8_t op, double a, double b) {
+  switch (op) {
+    case CO_GT: return a > b;
+    case CO_GE: return a >= b;
+    case CO_LT: return a < b;
+    case CO_LE: return a <= b;
+    default: return false;
+  }
+}
+KYV_HD int num_float(const View& v, uint8_t op, double kf, const CV& kcv, const CV& x) {
+  switch (x.t) {
+    case CT_INT: return cmp_by(op, kf, (double)x.i) ? CR_TRUE : CR_FALSE;
+    case CT_FLOAT: return cmp_by(op, kf, x.f) ? CR_TRUE : CR_FALSE;
+    case CT_STR: {
+      double ks, vs;
+      if (parse_duration2(v, kcv, x, &ks, &vs)) return cmp_by(op, ks, vs) ? CR_TRUE : CR_FALSE;
+      if (sflags(v, x.sid) & SF_FLOAT) return cmp_by(op, kf, v.str_f64[x.sid]) ? CR_TRUE : CR_FALSE;
+      return CR_FALSE;  // ParseInt cannot succeed where ParseFloat failed
+    }
+    default: return CR_FALSE;
+  }
+}
+KYV_HD int op_numeric(const View& v, const CV& k, const CV& x, uint8_t op) {
+  switch (k.t) {
+    case CT_INT: return num_float(v, op, (double)k.i, k, x);
+    case CT_FLOAT: return num_float(v, op, k.f, k, x);
+    case CT_STR: {
+      double ks, vs;
+      if (parse_duration2(v, k, x, &ks, &vs)) return cmp_by(op, ks, vs) ? CR_TRUE : CR_FALSE;
+      if (x.t == CT_STR && qty_ok(v, k.sid) && qty_ok(v, x.sid)) {
+        bool fb = false;
+        int c = qty_cmp(v, k.sid, x.sid, &fb);
+        if (fb) return CR_FB;
+        return cmp_by(op, (double)c, 0.0) ? CR_TRUE : CR_FALSE;
+      }
+      if (sflags(v, k.sid) & SF_FLOAT) {
+        CV kf = k;
+        kf.t = CT_FLOAT;
+        kf.f = v.str_f64[k.sid];
+        return num_float(v, op, kf.f, kf, x);
+      }
+      if (sflags(v, k.sid) & SF_SEMVERISH) return CR_FB;  // blang/semver comparison: CPU engine
+      return CR_FALSE;
+    }
+    default: return CR_FALSE;
+  }
+}
+
+KYV_HD int eval_cond(const View& v, NodeTab R, const Cond& c, const CV& k, const CV& x) {
+  switch (c.op) {
+    case CO_EQ: return op_equal(v, R, k, x, false);
+    case CO_NE: return op_equal(v, R, k, x, true);
+    case CO_IN: return op_in(v, R, c, k, x, false);
+    case CO_NOTIN: return op_in(v, R, c, k, x, true);
+    case CO_ANYIN: return op_any_all(v, R, c, k, x, false, false);
+    case CO_ALLIN: return op_any_all(v, R, c, k, x, true, false);
+    case CO_ANYNOTIN: return op_any_all(v, R, c, k, x, false, true);
+    case CO_ALLNOTIN: return op_any_all(v, R, c, k, x, true, true);
+    case CO_GT: case CO_GE: case CO_LT: case CO_LE: return op_numeric(v, k, x, c.op);
+    default: return CR_FALSE;
+  }
+}
+
+// Whole program: substitution first (every reference of the document, vars.go:352-431: any NotFoundError ->
+// error), then any/all evaluation (evaluate.go:42-69). Returns CR_TRUE / CR_FALSE / CR_FB / CR_PANIC, or
+// CP_ERROR with *err_cond / *err_side / *err_seg naming the first unresolved reference (for the host message).
+constexpr int CP_ERROR = 5;
+KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond, uint32_t* err_side, uint32_t* err_seg) {
+  const CondProg& p = v.cprogs[prog];
+  const uint32_t nany = p.nany == NONE ? 0u : p.nany;
+  for (uint32_t blk = 0; blk < 2; blk++) {
+    uint32_t c0 = blk ? p.all0 : p.any0, n = blk ? p.nall : nany;
+    for (uint32_t i = 0; i < n; i++) {
+      const Cond& c = v.conds[c0 + i];
+      CV tmp;
+      uint32_t miss = 0;
+      for (uint32_t side = 0; side < 2; side++) {
+        const CondOperand& o = side ? c.value : c.key;
+        if (o.kind == OK_PATH && !cv_operand(v, R, o, &tmp, &miss)) {
+          *err_cond = c0 + i; *err_side = side; *err_seg = miss;
+          return CP_ERROR;
+        }
+      }
+    }
+  }
+  auto one = [&](uint32_t ci) -> int {
+    const Cond& c = v.conds[ci];
+    CV k, x;
+    uint32_t miss;
+    cv_operand(v, R, c.key, &k, &miss);
+    cv_operand(v, R, c.value, &x, &miss);
+    return eval_cond(v, R, c, k, x);
+  };
+  if (p.nany != NONE) {
+    bool any = false;
+    for (uint32_t i = 0; i < p.nany; i++) {
+      int r = one(p.any0 + i);
+      if (r == CR_FB || r == CR_PANIC) return r;
+      if (r == CR_TRUE) { any = true; break; }
+    }
+    if (!any) return CR_FALSE;
+  }
+  for (uint32_t i = 0; i < p.nall; i++) {
+    int r = one(p.all0 + i);
+    if (r == CR_FB || r == CR_PANIC) return r;
+    if (r == CR_FALSE) return CR_FALSE;
+  }
+  return CR_TRUE;
+}
+
+}  // namespace kyv

@@ -49,7 +49,7 @@ struct DevRuleset {
   int device = -1;
   uint8_t* base = nullptr;
   size_t bytes = 0;
-  size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool;
+  size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool, o_cnodes, o_conds, o_cprogs;
   hipModule_t jmod = nullptr;     // runtime-compiled walk kernels (jit.cpp) loaded on this device
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
 };
@@ -120,6 +120,9 @@ static DevRuleset* upload_ruleset(const Ruleset& rs, int device) {
   d->o_metas = p.add(rs.metas);
   d->o_pss = p.add(rs.pss);
   d->o_pool = p.add(rs.pool);
+  d->o_cnodes = p.add(rs.cnodes);
+  d->o_conds = p.add(rs.conds);
+  d->o_cprogs = p.add(rs.cprogs);
   d->bytes = p.host.size();
   HIP_OK(hipMalloc(&d->base, d->bytes));
   HIP_OK(hipMemcpy(d->base, p.host.data(), d->bytes, hipMemcpyHostToDevice));
@@ -203,10 +206,14 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
     v.metas = (const MetaSite*)(rbase + dr->o_metas);
     v.pss = (const PssDesc*)(rbase + dr->o_pss);
     v.pool = (const uint32_t*)(rbase + dr->o_pool);
+    v.cnodes = (const Node*)(rbase + dr->o_cnodes);
+    v.conds = (const Cond*)(rbase + dr->o_conds);
+    v.cprogs = (const CondProg*)(rbase + dr->o_cprogs);
   } else {
     v.rules = rs.rules.data(); v.filters = rs.filters.data(); v.kinds = rs.kinds.data(); v.sels = rs.sels.data();
     v.reqs = rs.reqs.data(); v.pn = rs.pnodes.data(); v.pe = rs.pentries.data(); v.leaves = rs.leaves.data();
     v.atoms = rs.atoms.data(); v.metas = rs.metas.data(); v.pss = rs.pss.data(); v.pool = rs.pool.data();
+    v.cnodes = rs.cnodes.data(); v.conds = rs.conds.data(); v.cprogs = rs.cprogs.data();
   }
   if (db) v.pe = (const PEntry*)(bbase + db->o_pe);  // device: entries with absolute column offsets
   return v;

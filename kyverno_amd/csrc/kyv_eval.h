@@ -89,6 +89,9 @@ struct View {
   const MetaSite* metas;
   const PssDesc* pss;
   const uint32_t* pool;
+  const Node* cnodes;       // condition literals
+  const Cond* conds;
+  const CondProg* cprogs;
 };
 
 // ---------------------------------------------------------------- strings

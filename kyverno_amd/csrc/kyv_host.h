@@ -38,6 +38,18 @@ struct RuleMeta {
   std::string reason;         // RK_FALLBACK / RK_PANIC / RK_ERROR reason
   bool message_vars = false;  // message needs variable substitution (CPU)
   std::string pss_level, pss_version;
+  // deny failure message (getDenyMessage, validation.go:466-479): literal text and `{{ request.object... }}`
+  // references (key sids); msg_whole_var: the message is exactly one reference
+  struct MsgPart { std::string text; std::vector<uint32_t> segs; bool var = false; };
+  std::vector<MsgPart> msg_parts;
+  bool msg_whole_var = false;
+};
+
+// host-side text of a condition's references, for error messages (vars.go:395-399)
+struct CondText {
+  std::string var[2];   // key / value: variable text (replaceBracesAndTrimSpaces)
+  std::string path[2];  // JSON pointer of the operand in the conditions document (data.Path)
+  std::vector<std::string> segs[2];
 };
 
 struct PolicyMeta {
@@ -65,6 +77,10 @@ struct Ruleset {
   std::vector<MetaSite> metas;
   std::vector<PssDesc> pss;
   std::vector<uint32_t> pool;
+  std::vector<Node> cnodes;     // condition literals
+  std::vector<Cond> conds;
+  std::vector<CondProg> cprogs;
+  std::vector<CondText> cond_text;
   std::vector<std::string> templates;  // path templates: '\x01'+slot = array index, '\x02'+slot = resolved key
   // path trie over every static lookup of every compiled pattern (kyv_layout.h "Path columns")
   struct TrieNode {

@@ -57,6 +57,9 @@ enum StrFlag : uint32_t {
   SF_LKEY = 1u << 5,       // valid label key (IsQualifiedName)
   SF_LVAL = 1u << 6,       // valid label value
   SF_MAGIC = 1u << 7,      // contains an anchor-error phrase (error.go:20-26)
+  SF_INT = 1u << 8,        // strconv.ParseInt(s, 10, 64) ok (value = str_f64 when not SF_INT_BIG)
+  SF_INT_BIG = 1u << 9,    // ... but |value| > 2^53 (not exact in str_f64) -> condition pairs fall back
+  SF_SEMVERISH = 1u << 10, // could parse as blang/semver (digit first, two dots) -> numeric conditions fall back
 };
 
 // fixed dictionary ids (seeded first in every batch)
@@ -243,7 +246,7 @@ struct MetaSite {       // metadata-expansion site (wildcards.go:62-83)
   X(CAP_SYS_CHROOT, "SYS_CHROOT") X(SYSCTL_SHM, "kernel.shm_rmid_forced")                                    \
   X(SYSCTL_PORTRANGE, "net.ipv4.ip_local_port_range") X(SYSCTL_SYNCOOKIES, "net.ipv4.tcp_syncookies")        \
   X(SYSCTL_PINGRANGE, "net.ipv4.ping_group_range") X(SYSCTL_UNPRIV, "net.ipv4.ip_unprivileged_port_start")   \
-  X(FAKE, "fake")
+  X(FAKE, "fake") X(NIL_STR, "<nil>")
 
 enum WellKnown : uint32_t {
 #define KYV_WK_ENUM(id, s) K_##id,
@@ -280,7 +283,37 @@ struct PssDesc {
 
 // ---------------------------------------------------------------- rules
 enum RuleKind : uint8_t { RK_NONE = 0, RK_PATTERN = 1, RK_ANYPATTERN = 2, RK_PSS = 3, RK_FALLBACK = 4, RK_PANIC = 5,
-                          RK_ERROR = 6 };
+                          RK_ERROR = 6, RK_DENY = 7 };
+
+// ---------------------------------------------------------------- conditions (validate.deny, rule preconditions)
+// A condition program is the any/all form of pkg/engine/variables/evaluate.go:42-69 (the old list form is an `all`
+// block without `any`). Operands are literals (ruleset node table `cnodes`, already put through the
+// Condition.GetKey json round trip) or `{{ request.object.<path> }}` references resolved per resource.
+enum CondOp : uint8_t { CO_EQ = 0, CO_NE = 1, CO_IN = 2, CO_NOTIN = 3, CO_ANYIN = 4, CO_ALLIN = 5, CO_ANYNOTIN = 6,
+                        CO_ALLNOTIN = 7, CO_GT = 8, CO_GE = 9, CO_LT = 10, CO_LE = 11, CO_FALSE = 12 };
+enum OperandKind : uint8_t { OK_NIL = 0, OK_LIT = 1, OK_PATH = 2 };
+enum StrValFlag : uint8_t { SV_LIST = 1, SV_JSON = 2, SV_RANGE = 4 };  // literal string value: json []string ok,
+                                                                        // json.Valid, InRange operator pattern
+struct CondOperand {     // 16 bytes
+  uint8_t kind;          // OperandKind
+  uint8_t sv;            // StrValFlag (literal strings)
+  uint16_t nseg;         // OK_PATH: path segments
+  uint32_t a;            // OK_LIT: cnodes index; OK_PATH: pool offset of the segments' key sids
+  uint32_t list, nlist;  // SV_LIST: pool offset / count of the []string element sids
+};
+struct Cond {            // 48 bytes
+  uint8_t op;            // CondOp
+  uint8_t pad[3];
+  uint32_t leaf;         // SV_RANGE value: pattern leaf of the value string (handleRange, anyin.go:98-104)
+  uint32_t leaf_neg;     // ... and of its first "-" replaced by "!-" (AnyNotIn, anyin.go:143-152)
+  uint32_t pad2;
+  CondOperand key, value;
+};
+struct CondProg {        // 16 bytes
+  uint32_t any0, nany;   // nany == NONE: no `any` block
+  uint32_t all0, nall;
+};
+static_assert(sizeof(Cond) == 48, "cond size");
 
 enum RuleFlag : uint8_t { RD_GATE_EXACT = 1 };  // match == the batch's kind gate (kinds-only filters, no exclude)
 
@@ -295,12 +328,17 @@ struct RuleDesc {
   uint32_t root;         // RK_PATTERN: root pnode; RK_ANYPATTERN: first of nalts root ids in pool; RK_PSS: PssDesc
   uint32_t nalts;
   uint32_t meta_sites, nmeta;
+  uint32_t pre;          // precondition program (CondProg index) or NONE; RK_DENY: `root` is the deny program
+  uint32_t pad;
 };
 
 // ---------------------------------------------------------------- results
 enum Status : uint8_t { ST_NONE = 0, ST_PASS = 1, ST_FAIL = 2, ST_SKIP = 3, ST_ERROR = 4, ST_FALLBACK = 5, ST_PANIC = 6,
                         ST_ND = 7 };
 constexpr int NSTATUS = 8;
+// high 5 bits of a status byte: the passing anyPattern alternative (ST_PASS), or ST_MARK_PRE on a skip / error that
+// came from the rule's preconditions ("preconditions not met", validation.go:286-288)
+constexpr uint8_t ST_MARK_PRE = 30u << 3;
 
 constexpr int MAX_IDX = 4;
 constexpr int MAX_SLOTS = 2;

@@ -7,6 +7,7 @@
 // bitmask over (check, version) slots in DefaultChecks() registration order.  The typed decode of
 // validation.go:481-532 is modelled for the fields the checks read: a JSON type mismatch there is an error.
 #pragma once
+#include "kyv_cond.h"
 #include "kyv_eval.h"
 #include "kyv_walk.h"
 
@@ -510,10 +511,25 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
   }
   if (!m) return ST_NONE;
   if (nd) return ST_ND;
+  if (rd.kind == RK_FALLBACK) return ST_FALLBACK;
+  uint32_t ec, es, eg;
+  if (rd.pre != NONE) {  // checkPreconditions (validation.go:281-288)
+    int c = eval_prog(v, R, rd.pre, &ec, &es, &eg);
+    if (c == CR_FB) return ST_FALLBACK;
+    if (c == CR_PANIC) return ST_PANIC;
+    if (c == CP_ERROR) return ST_ERROR | ST_MARK_PRE;
+    if (c == CR_FALSE) return ST_SKIP | ST_MARK_PRE;
+  }
   switch (rd.kind) {
-    case RK_FALLBACK: return ST_FALLBACK;
     case RK_PANIC: return ST_PANIC;
     case RK_ERROR: return ST_ERROR;
+    case RK_DENY: {  // validateDeny (validation.go:437-464)
+      int c = eval_prog(v, R, rd.root, &ec, &es, &eg);
+      if (c == CR_FB) return ST_FALLBACK;
+      if (c == CR_PANIC) return ST_PANIC;
+      if (c == CP_ERROR) return ST_ERROR;
+      return c == CR_TRUE ? ST_FAIL : ST_PASS;
+    }
     case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
     case RK_PATTERN: case RK_ANYPATTERN:
       if (h.flags & RF_MAGIC) return ST_FALLBACK;

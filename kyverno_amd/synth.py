@@ -369,3 +369,74 @@ def c4_policies(n=10000, seed=SEED):
                     "metadata": {"name": "c4-%05d" % i},
                     "spec": {"validationFailureAction": "Audit", "background": True, "rules": [rule]}})
     return out
+
+
+def c5_policies(n=50, seed=SEED):
+    """BASELINE configs[4]: n policies whose rules use preconditions / deny conditions with
+    variables. About 60% use only `{{ request.object.<path> }}` operands with the condition operators (the
+    device-compilable subset: Equals / NotEquals / In / AnyIn / AllIn / NotIn / AnyNotIn / AllNotIn / numeric,
+    old-list and any/all forms, literal ranges, JSON-string lists, quantities, durations, message variables);
+    the rest use JMESPath projections, functions, `||` defaults or other context variables (CPU fallback)."""
+    r = random.Random(seed ^ 0xC5)
+    pod = {"any": [{"resources": {"kinds": ["Pod"]}}]}
+    wl = {"any": [{"resources": {"kinds": ["Deployment", "StatefulSet"]}}]}
+    svc = {"any": [{"resources": {"kinds": ["Service"]}}]}
+    allk = {"any": [{"resources": {"kinds": ["Pod", "Deployment", "ConfigMap", "Service"]}}]}
+
+    def c(k, op, v):
+        return {"key": k, "operator": op, "value": v}
+
+    o = "{{request.object.%s}}"
+    gpu = [
+        lambda: ("deny", pod, {"any": [c(o % "metadata.labels.tier", "Equals", r.choice(["data", "front*"]))]}, None,
+                 "tier not allowed"),
+        lambda: ("deny", allk, {"all": [c("{{ request.object.metadata.namespace }}", "AnyIn", ["ns-00*", "ns-01?0"]),
+                                        c(o % "metadata.labels.app", "NotEquals", "app-1*")]}, None,
+                 "{{request.object.metadata.name}} in {{request.object.metadata.namespace}} is not allowed"),
+        lambda: ("pattern", pod, None, {"all": [c(o % "metadata.labels.tier", "In", ["frontend", "backend"])]},
+                 "owner label required"),
+        lambda: ("deny", wl, [c(o % "spec.replicas", r.choice(["GreaterThan", "LessThanOrEquals"]), r.choice([3, "2", 1.5]))],
+                 None, ""),
+        lambda: ("deny", pod, {"all": [c("1Gi", "GreaterThanOrEquals", "1024Mi"), c("1h", "GreaterThan", "30m"),
+                                       c(o % "metadata.labels.owner", "Equals", "team-1?")]}, None, "owner team-1x"),
+        lambda: ("deny", pod, [c(o % "spec.serviceAccountName", "Equals", "sa-" + str(r.randint(0, 9)))], None,
+                 "service account {{request.object.spec.serviceAccountName}} is reserved"),
+        lambda: ("pss", pod, None, {"any": [c(o % "metadata.namespace", "AnyNotIn", ["ns-000*"])]}, ""),
+        lambda: ("deny", pod, {"any": [c(o % "spec.securityContext.supplementalGroups", r.choice(["AnyIn", "AllNotIn"]), [0])]},
+                 None, "group 0"),
+        lambda: ("deny", wl, {"all": [c(o % "spec.replicas", r.choice(["AnyIn", "AnyNotIn", "AllIn"]), "2-4")]}, None,
+                 "replicas range"),
+        lambda: ("deny", pod, {"any": [c(o % "metadata.labels.tier", "AnyIn", '["frontend","data"]')]}, None, "tier list"),
+        lambda: ("deny", pod, {"any": [c(o % "spec.securityContext.fsGroup", r.choice(["Equals", "NotEquals"]), "2000")]},
+                 None, "fsGroup"),
+        lambda: ("deny", pod, {"any": [c(o % "spec.hostNetwork", "Equals", True)]}, None, "hostNetwork"),
+        lambda: ("deny", allk, {"any": [c(o % "kind", "equals", "ConfigMap"),
+                                        c(o % 'metadata.annotations."example.com/a0"', "In", ["value-1*", "value-2"])]},
+                 None, "annotated"),
+        lambda: ("pattern", pod, None, [c(o % "metadata.namespace", "NotIn", ["ns-0001", "ns-0002"])],
+                 "tier label required"),
+        lambda: ("deny", svc, {"any": [c(o % "spec.type", "Equals", "LoadBalancer")]}, None, "no load balancers"),
+    ]
+    cpu = [
+        lambda: ("deny", pod, {"any": [c("{{ request.object.spec.containers[].image }}", "AnyIn", ["*:latest"])]}, None,
+                 "latest"),
+        lambda: ("deny", pod, {"any": [c("{{ length(request.object.spec.containers) }}", "GreaterThan", 2)]}, None, "many"),
+        lambda: ("deny", pod, {"any": [c("{{ request.object.metadata.labels.app || '' }}", "Equals", "")]}, None, "app"),
+        lambda: ("pattern", pod, None, {"any": [c("{{ request.operation }}", "Equals", "CREATE")]}, "owner"),
+    ]
+    out = []
+    for i in range(n):
+        t = (gpu[i % len(gpu)] if r.random() < 0.6 else cpu[i % len(cpu)])()
+        kind, match, cond, pre, msg = t
+        rule = {"name": "c5-r%03d" % i, "match": match}
+        if pre is not None:
+            rule["preconditions"] = pre
+        if kind == "deny":
+            rule["validate"] = {"message": msg, "deny": {"conditions": cond}} if msg else {"deny": {"conditions": cond}}
+        elif kind == "pattern":
+            rule["validate"] = {"message": msg, "pattern": {"metadata": {"labels": {"owner": "?*"}}}}
+        else:
+            rule["validate"] = {"podSecurity": {"level": "baseline", "version": "latest"}}
+        out.append({"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "c5-%03d" % i},
+                    "spec": {"validationFailureAction": "Audit", "background": True, "rules": [rule]}})
+    return out

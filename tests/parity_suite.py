@@ -93,3 +93,31 @@ def run_c4(backend, npol, nres, seed=11, jit=None):
     assert_clean("c4/%dx%d" % (npol, nres), st)
     assert st["matched"] > 0
     return st, res
+
+
+def run_condition_goldens(backend):
+    """pkg/engine/variables/evaluate_test.go TestEvaluate through the device evaluator: every golden condition
+    becomes a deny rule over one Pod (deny true -> fail, false -> pass); the verdict must equal the golden result
+    (and the oracle). Map literals are compiled to CPU fallback and are skipped."""
+    import json
+    from kyverno_amd import _lib as K
+    recs = cases.load("conditions.json")
+    pols = []
+    for i, r in enumerate(recs):
+        cond = {"key": json.loads(r["key"]), "operator": r["operator"], "value": json.loads(r["value"])}
+        pols.append({"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "cond-%03d" % i, "annotations": {"pod-policies.kyverno.io/autogen-controllers": "none"}},
+                     "spec": {"rules": [{"name": "c", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                                         "validate": {"deny": {"conditions": {"all": [cond]}}}}]}})
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "default"},
+           "spec": {"containers": [{"name": "c", "image": "nginx"}]}}
+    st, res = PU.compare(pols, [pod], None, backend=backend)
+    assert_clean("conditions", st)
+    n = 0
+    for k, rule in enumerate(res.ruleset.rules):
+        s = int(res.status[k, 0])
+        if s == K.ST_FALLBACK:
+            continue
+        i = int(res.ruleset.policies[rule["policy"]]["name"].split("-")[1])
+        assert s == (K.ST_FAIL if recs[i]["result"] else K.ST_PASS), (recs[i], K.STATUS_NAMES[s])
+        n += 1
+    return n

@@ -42,3 +42,14 @@ def test_c4_policycache_stress_cpu():
     """configs[3] shape at reduced size: 1,000 generated wildcard-heavy policies x 300 mixed resources"""
     st, _ = S.run_c4("cpu", 1000, 300)
     assert st["compared"] > 300000
+
+
+def test_condition_goldens_cpu():
+    assert S.run_condition_goldens("cpu") >= 300
+
+
+def test_c5_conditions_cpu():
+    """configs[4]: deny / preconditions with request.object variables (GPU subset) + counted CPU fallback"""
+    from kyverno_amd import synth
+    st, _ = S.run_synthetic("cpu", synth.c5_policies(50), 500, seed=12)
+    assert st["compared"] > 5000 and st["fallback"] > 0

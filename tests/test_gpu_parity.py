@@ -117,3 +117,12 @@ def test_c4_policycache_stress_gpu():
     every pair's status against the oracle's verdict matrix"""
     st, res = S.run_c4("gpu", 10000, 2000)
     assert st["rules"] >= 10000 and st["compared"] > 2e7
+
+
+def test_condition_goldens_gpu():
+    assert S.run_condition_goldens("gpu") >= 300
+
+
+def test_c5_conditions_gpu():
+    st, _ = S.run_synthetic("gpu", synth.c5_policies(50), 4000, seed=34)
+    assert st["compared"] > 40000 and st["fallback"] > 0
