@@ -170,7 +170,11 @@ def main():
     dt_max = all_max(pg, dt)
     kernel_ms = kms / max(1, args.steps)
     kernel_ms_max = all_max(pg, kernel_ms)
-    total_pairs = all_sum(pg, pairs)
+    # pairs the device decided: every (resource, compiled rule) pair except those it hands to the CPU engine
+    # (ST_FALLBACK: rules / pairs outside the GPU subset, counted separately, not in `value`)
+    fb_pairs = int(counts.get("fallback", 0))
+    total_pairs = all_sum(pg, pairs - fb_pairs)
+    total_fb = all_sum(pg, fb_pairs)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -184,6 +188,7 @@ def main():
                               "C2: podSecurity restricted/latest (%d compiled rules) over %d pods per GPU" %
                               (nrules, batch.n),
                   "resources_per_gpu": batch.n, "compiled_rules": nrules, "pairs_per_step": int(total_pairs),
+                  "cpu_fallback_pairs_per_step": int(total_fb),
                   "parallelism": "shard%d" % world}
         traffic, pmc_tag = pmc_traffic(config)
         line = {

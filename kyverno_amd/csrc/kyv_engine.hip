@@ -532,7 +532,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   const bool use_jit = jit_mode == JIT_ON || (jit_mode == JIT_AUTO && nres >= JIT_AUTO_MIN_RESOURCES);
   const bool jit = use_jit && ensure_jit(mrs, dr);
   if (d.jit_state != (int)jit) {  // lay out the two walk schedules (see ChunkMap)
-    const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)std::max(1, atoi(getenv("KYV_WIN"))) : 1u;  // rules per window (1: best measured)
+    // rules per window: all of a wave's rules back to back (wave-major) measured best together with the XCD
+    // placement below (C3 walk 3.94 ms rule-major -> 3.47 ms; windows of 2-8 rules were slower than either)
+    const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)std::max(1, atoi(getenv("KYV_WIN"))) : 0xFFFFu;
     const uint32_t nw = d.wl.nwaves, gw = b.gate_words;
     // gated rule set of every match wave (union over the kind classes of its lanes), as runs of equal sets
     std::vector<std::pair<uint32_t, std::vector<uint32_t>>> runs;  // (first wave, gate words)
@@ -561,10 +563,41 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     }
     size_t tot = 0;
     d.grid.assign(ncls, 0);
+    const bool xcd = !getenv("KYV_XCD") || atoi(getenv("KYV_XCD")) != 0;
     for (uint32_t cls = 0; cls < ncls; cls++) {
       if (slots[cls].size() > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
       d.grid[cls] = (uint32_t)std::min<size_t>(slots[cls].size(), (size_t)d.cus * 64);
       tot += slots[cls].size();
+      // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs (block b and b + 8 share one L2),
+      // and the grid-stride loop hands position p to block p % G. The chunks of one match wave (the same 64
+      // resources under its rules) are kept on ONE XCD, so its L2 serves the resources' rows to every rule; whole
+      // waves go to the XCD with the least work so far (balance), in schedule order.
+      const size_t T = slots[cls].size(), G = d.grid[cls];
+      if (xcd && G >= 8 && T > G) {
+        std::vector<std::vector<uint32_t>> pos(8);
+        for (size_t q = 0; q < T; q++) pos[(q % G) % 8].push_back((uint32_t)q);
+        std::vector<uint2> out(T);
+        size_t fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (size_t i = 0; i < T;) {
+          size_t j = i;
+          while (j < T && slots[cls][j].y == slots[cls][i].y) j++;  // one wave's chunks
+          int best = -1;
+          double br = 2.0;
+          for (int x = 0; x < 8; x++) {
+            if (fill[x] >= pos[x].size()) continue;
+            double r = (double)fill[x] / (double)pos[x].size();
+            if (r < br) { br = r; best = x; }
+          }
+          for (size_t t = i; t < j; t++) {
+            int x = best;
+            if (fill[x] >= pos[x].size())  // XCD full: next XCD with room
+              for (int y = 0; y < 8; y++) if (fill[y] < pos[y].size()) { x = y; break; }
+            out[pos[x][fill[x]++]] = slots[cls][t];
+          }
+          i = j;
+        }
+        slots[cls].swap(out);
+      }
     }
     hipFree(d.sched);
     HIP_OK(hipMalloc(&d.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
