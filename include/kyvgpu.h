@@ -138,6 +138,9 @@ void kyv_results_free(kyv_results* r);
  * alternative that passed (31 = none) */
 int kyv_results_status(const kyv_results* r, uint8_t* out, size_t cap);
 int64_t kyv_results_count(const kyv_results* r, int status);
+/* per-rule verdict totals, out[rule * 8 + status] (KYV_ST_*), for report summaries: replaces the per-result tally of
+ * CalculateSummary (pkg/utils/report/results.go:38-54) over a background-scan batch; returns KYV_OK */
+int kyv_results_rule_counts(const kyv_results* r, int64_t* out, size_t cap);
 double kyv_results_kernel_ms(const kyv_results* r);
 /* 1 when the runtime-compiled walk kernel evaluated this result's pattern rules, 0 for the interpreter */
 int kyv_results_jit(const kyv_results* r);

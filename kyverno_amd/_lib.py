@@ -51,7 +51,7 @@ EXPORTS = [
     "kyv_batch_num_resources", "kyv_batch_stats_get", "kyv_eval", "kyv_results_free", "kyv_results_status",
     "kyv_results_count", "kyv_results_kernel_ms", "kyv_results_alg_bytes", "kyv_results_message", "kyv_results_path",
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
-    "kyv_ruleset_jit_compile",
+    "kyv_ruleset_jit_compile", "kyv_results_rule_counts",
 ]
 
 _lib = None
@@ -82,6 +82,8 @@ def lib():
     L.kyv_eval.argtypes = [vp, vp, ctypes.POINTER(EvalOpts), ctypes.POINTER(vp)]
     L.kyv_results_free.argtypes = [vp]
     L.kyv_results_status.argtypes = [vp, ctypes.c_void_p, sz]
+    L.kyv_results_rule_counts.argtypes = [vp, vp, ctypes.c_size_t]
+    L.kyv_results_rule_counts.restype = i32
     L.kyv_results_count.argtypes = [vp, i32]
     L.kyv_results_count.restype = i64
     L.kyv_results_kernel_ms.argtypes = [vp]

@@ -195,6 +195,13 @@ int64_t kyv_results_count(const kyv_results* r, int s) {
   return r->r.counts[s];
 }
 
+int kyv_results_rule_counts(const kyv_results* r, int64_t* out, size_t cap) {
+  if (!r || !out) return fail(KYV_EINVAL, "null argument");
+  if (cap < r->r.rule_counts.size()) return fail(KYV_ERANGE, "buffer too small");
+  std::copy(r->r.rule_counts.begin(), r->r.rule_counts.end(), out);
+  return KYV_OK;
+}
+
 double kyv_results_kernel_ms(const kyv_results* r) { return r ? r->r.kernel_ms : 0; }
 
 uint64_t kyv_results_alg_bytes(const kyv_results* r) { return r ? r->r.alg_bytes : 0; }

@@ -343,19 +343,25 @@ __device__ __forceinline__ uint32_t bytes_eq(uint32_t w, uint32_t s) {
   const uint32_t x = w ^ (s * 0x01010101u);
   return 4u - (uint32_t)__popc((x | (x >> 1) | (x >> 2)) & 0x01010101u);
 }
-__global__ void __launch_bounds__(HIST_BLOCK) status_hist_kernel(const uint8_t* __restrict__ status, size_t n,
+__global__ void __launch_bounds__(HIST_BLOCK) status_hist_kernel(const uint8_t* __restrict__ status, size_t nres,
                                                                  unsigned long long* __restrict__ counts) {
+  // blockIdx.y = rule: its verdict row is status[k * nres, (k + 1) * nres); per-rule totals feed the report
+  // summaries (CalculateSummary, pkg/utils/report/results.go:38-54), their sum the evaluation's verdict counts
   __shared__ uint32_t part[HIST_BLOCK / WAVE][NSTATUS];
   uint32_t c[NSTATUS] = {0};
-  const size_t nv = n / 16, stride = (size_t)gridDim.x * HIST_BLOCK;
-  const kyv_u32x4* s4 = (const kyv_u32x4*)status;
+  const uint8_t* row = status + (size_t)blockIdx.y * nres;
+  size_t head = (16 - ((size_t)row & 15)) & 15;
+  if (head > nres) head = nres;
+  const size_t nv = (nres - head) / 16, tail0 = head + nv * 16, stride = (size_t)gridDim.x * HIST_BLOCK;
+  const kyv_u32x4* s4 = (const kyv_u32x4*)(row + head);
   for (size_t i = (size_t)blockIdx.x * HIST_BLOCK + threadIdx.x; i < nv; i += stride) {
     const kyv_u32x4 q = __builtin_nontemporal_load(s4 + i);
 #pragma unroll
     for (uint32_t s = 1; s < NSTATUS; s++) c[s] += bytes_eq(q.x, s) + bytes_eq(q.y, s) + bytes_eq(q.z, s) + bytes_eq(q.w, s);
   }
-  if (blockIdx.x == 0 && threadIdx.x < n % 16) {  // tail bytes
-    const uint32_t b = status[nv * 16 + threadIdx.x] & 7u;
+  if (blockIdx.x == 0 && threadIdx.x < head + (nres - tail0)) {  // unaligned head / tail bytes (< 32)
+    const size_t at = threadIdx.x < head ? threadIdx.x : tail0 + (threadIdx.x - head);
+    const uint32_t b = row[at] & 7u;
 #pragma unroll
     for (uint32_t s = 1; s < NSTATUS; s++) c[s] += b == s;
   }
@@ -372,7 +378,7 @@ __global__ void __launch_bounds__(HIST_BLOCK) status_hist_kernel(const uint8_t* 
   if (threadIdx.x > 0 && threadIdx.x < NSTATUS) {
     uint32_t t = 0;
     for (int j = 0; j < HIST_BLOCK / WAVE; j++) t += part[j][threadIdx.x];
-    if (t) atomicAdd(&counts[threadIdx.x], (unsigned long long)t);
+    if (t) atomicAdd(&counts[(size_t)blockIdx.y * NSTATUS + threadIdx.x], (unsigned long long)t);
   }
 }
 
@@ -498,7 +504,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipMalloc(&d.rcnt, std::max<size_t>(nrules * nwv, 1) * 2));
       HIP_OK(hipMalloc(&d.tsum, std::max<size_t>((nrules * nwv + WAVE - 1) / WAVE, 1) * 4));
     }
-    HIP_OK(hipMalloc(&d.counts, NSTATUS * 8));
+    HIP_OK(hipMalloc(&d.counts, std::max<size_t>(1, nrules) * NSTATUS * 8));
     HIP_OK(hipMemcpy(d.pss_slot, pss_slot.data(), nrules * 4, hipMemcpyHostToDevice));
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.e0));
@@ -621,7 +627,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
     HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nrules * (size_t)d.wl.nwaves, 1) * 2, stream));
-    HIP_OK(hipMemsetAsync(d.counts, 0, NSTATUS * 8, stream));
+    HIP_OK(hipMemsetAsync(d.counts, 0, std::max<size_t>(1, nrules) * NSTATUS * 8, stream));
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     if (nres && nrules) {
@@ -647,9 +653,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, d.tsum, ntiles, d.nrecs);
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, d.rbase, d.rcnt, drules,
                          d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs);
-      const size_t nst = nres * nrules;
-      const uint32_t hgrid = (uint32_t)std::max<size_t>(1, std::min<size_t>((size_t)d.cus * 2, (nst / 16 + HIST_BLOCK - 1) / HIST_BLOCK));
-      hipLaunchKernelGGL(status_hist_kernel, dim3(hgrid), dim3(HIST_BLOCK), 0, stream, d.status, nst, d.counts);
+      const uint32_t hgrid = (uint32_t)std::max<size_t>(
+          1, std::min<size_t>(((size_t)d.cus * 2 + nrules - 1) / std::max<size_t>(1, nrules), (nres / 16 + HIST_BLOCK - 1) / HIST_BLOCK));
+      if (nrules) hipLaunchKernelGGL(status_hist_kernel, dim3(hgrid, (uint32_t)nrules), dim3(HIST_BLOCK), 0, stream, d.status, nres, d.counts);
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(d.e1, stream));
@@ -672,12 +678,21 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     out->kernel_ms = total_ms / n;
     out->jit_used = jit ? 1 : 0;
     out->h2d_ms = db->upload_ms;
-    unsigned long long counts[NSTATUS];
-    HIP_OK(hipMemcpy(counts, d.counts, sizeof(counts), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> rc(nrules * NSTATUS);
+    if (nrules) HIP_OK(hipMemcpy(rc.data(), d.counts, rc.size() * 8, hipMemcpyDeviceToHost));
     // ST_NONE pairs are not tallied on the device
-    int64_t counted = 0;
-    for (int s = 0; s < NSTATUS; s++) out->counts[s] = s == ST_NONE ? 0 : (int64_t)counts[s], counted += out->counts[s];
-    out->counts[ST_NONE] = (int64_t)(nres * nrules) - counted;
+    out->rule_counts.assign(nrules * NSTATUS, 0);
+    for (int s = 0; s < NSTATUS; s++) out->counts[s] = 0;
+    for (size_t k = 0; k < nrules; k++) {
+      int64_t counted = 0;
+      for (int s = 1; s < NSTATUS; s++) {
+        out->rule_counts[k * NSTATUS + s] = (int64_t)rc[k * NSTATUS + s];
+        counted += (int64_t)rc[k * NSTATUS + s];
+        out->counts[s] += (int64_t)rc[k * NSTATUS + s];
+      }
+      out->rule_counts[k * NSTATUS + ST_NONE] = (int64_t)nres - counted;
+      out->counts[ST_NONE] += (int64_t)nres - counted;
+    }
     if (copy_back) {
       auto t0 = std::chrono::steady_clock::now();
       out->status.resize(nres * nrules);
@@ -751,7 +766,11 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
   out->fails.clear();
   for (auto& v2 : recs) out->fails.insert(out->fails.end(), v2.begin(), v2.end());
   for (int s = 0; s < NSTATUS; s++) out->counts[s] = 0;
-  for (uint8_t s : out->status) out->counts[s & 7]++;
+  out->rule_counts.assign(nrules * NSTATUS, 0);
+  for (size_t k = 0; k < nrules; k++)
+    for (size_t r = 0; r < nres; r++) out->rule_counts[k * NSTATUS + (out->status[k * nres + r] & 7)]++;
+  for (size_t k = 0; k < nrules; k++)
+    for (int s = 0; s < NSTATUS; s++) out->counts[s] += out->rule_counts[k * NSTATUS + s];
   out->alg_bytes = 0;
   for (auto x : bytes) out->alg_bytes += x;
 }

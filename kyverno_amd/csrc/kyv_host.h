@@ -147,6 +147,7 @@ struct Results {
   std::vector<uint32_t> pss_fails;  // [rule][res] for PSS rules (empty otherwise)
   std::vector<FailRec> fails;
   int64_t counts[NSTATUS] = {0};
+  std::vector<int64_t> rule_counts;  // [rule][status] (report summaries)
   double kernel_ms = 0, h2d_ms = 0, d2h_ms = 0;
   uint64_t alg_bytes = 0;           // CPU backend with KYV_EVAL_ACCOUNT_BYTES
   int jit_used = 0;                 // pairs walked by the runtime-compiled kernel (1) or the interpreter only (0)

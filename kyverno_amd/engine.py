@@ -102,6 +102,10 @@ class Results:
         self.kernel_ms = L.kyv_results_kernel_ms(h)
         self.alg_bytes = L.kyv_results_alg_bytes(h)
         self.jit = bool(L.kyv_results_jit(h))
+        rc = np.zeros(len(ruleset.rules) * 8, dtype=np.int64)
+        if rc.size:
+            K.check(L.kyv_results_rule_counts(h, rc.ctypes.data, rc.size))
+        self.rule_counts = rc.reshape(len(ruleset.rules), 8)  # [rule][status] verdict totals
         self.status = None
         if copied:
             nr, nres = len(ruleset.rules), batch.n

@@ -1,0 +1,152 @@
+"""Batched background scan: report results and summaries for a batch of resources.
+
+The reference reconciles one resource at a time (pkg/controllers/report/background/controller.go:250-361): for
+each background policy `scanner.ScanResource` builds a JSON context and calls `engine.Validate`
+(pkg/controllers/report/utils/scanner.go:60-110); every EngineResponse becomes report rows
+(`EngineResponseToReportResults`, pkg/utils/report/results.go:84-124) and the report carries `CalculateSummary`
+(results.go:38-54). Here a whole batch goes through one `kyv_eval`; the per-policy summary is assembled from the
+device's per-rule verdict totals (`kyv_results_rule_counts`), so rows are only materialised on request.
+
+Multi-GPU: each rank scans its own shard; `reduce_summary` sums the per-policy summaries over the process group
+(RCCL with the "nccl" backend, gloo on CPU) - the only collective of the path.
+
+Pairs outside the device subset (KYV_ST_FALLBACK, PANIC, ND) are listed by `fallback_pairs()`: the Go shim
+evaluates exactly those with the reference engine; they are counted as `cpu_fallback`, not in pass/fail/....
+"""
+import numpy as np
+
+from . import _lib as K
+from . import engine as E
+
+SUMMARY_FIELDS = ("pass", "fail", "warn", "error", "skip", "cpu_fallback")
+
+
+def policy_key(pol):
+    """cache.MetaNamespaceKeyFunc: "<namespace>/<name>" for namespaced policies, "<name>" otherwise"""
+    md = pol.get("metadata") or {}
+    ns = md.get("namespace") or ""
+    return ns + "/" + md.get("name", "") if ns else md.get("name", "")
+
+
+class BackgroundScan:
+    """Background scan over batches: policies compiled once (background: false policies are not scanned)."""
+
+    def __init__(self, policies, backend="gpu", device=0):
+        self.policies = [p for p in policies if isinstance(p, dict) and p.get("kind") in ("ClusterPolicy", "Policy")
+                         and (p.get("spec") or {}).get("background", True) is not False]
+        self.ruleset = E.Ruleset(self.policies)
+        self.backend, self.device = backend, device
+        self.meta = []
+        by_name = {(p.get("metadata") or {}).get("name"): p for p in self.policies}
+        for pm in self.ruleset.policies:
+            pol = by_name.get(pm["name"]) or {}
+            ann = (pol.get("metadata") or {}).get("annotations") or {}
+            sev = ann.get("policies.kyverno.io/severity", "")
+            self.meta.append({
+                "key": policy_key(pol) if pol else pm["name"],
+                "scored": ann.get("policies.kyverno.io/scored") != "false",
+                "category": ann.get("policies.kyverno.io/category", ""),
+                "severity": sev if sev in ("high", "medium", "low") else "",
+                "apply_one": pm["apply_one"], "first_rule": pm["first_rule"], "nrules": pm["nrules"],
+            })
+
+    def scan(self, resources, ns_labels=None):
+        batch = E.Batch(self.ruleset, resources, ns_labels)
+        res = E.evaluate(self.ruleset, batch, backend=self.backend, device=self.device)
+        return ScanReport(self, batch, res)
+
+
+class ScanReport:
+    def __init__(self, scan, batch, res):
+        self.scan, self.batch, self.res = scan, batch, res
+
+    def summary_matrix(self):
+        """int64 [policies, 6]: SUMMARY_FIELDS per policy over the batch (CalculateSummary of its report rows)."""
+        out = np.zeros((len(self.scan.meta), len(SUMMARY_FIELDS)), dtype=np.int64)
+        rc, st = self.res.rule_counts, self.res.status
+        for pi, m in enumerate(self.scan.meta):
+            ks = range(m["first_rule"], m["first_rule"] + m["nrules"])
+            fail_col = 1 if m["scored"] else 2  # fail on an unscored policy is reported as warn (results.go:117-119)
+            if not m["apply_one"]:
+                for k in ks:
+                    c = rc[k]
+                    out[pi, 0] += c[K.ST_PASS]
+                    out[pi, fail_col] += c[K.ST_FAIL]
+                    out[pi, 3] += c[K.ST_ERROR]
+                    out[pi, 4] += c[K.ST_SKIP]
+                    out[pi, 5] += c[K.ST_FALLBACK] + c[K.ST_PANIC] + c[K.ST_ND]
+                continue
+            # applyRules: One (validation.go:176-178): rules after the first applied (pass / fail) one give no
+            # response; after a CPU-fallback rule the truncation point is the CPU engine's to decide
+            active = np.ones(st.shape[1], dtype=bool)
+            for k in ks:
+                s = st[k]
+                m_ = active & (s != K.ST_NONE)
+                out[pi, 0] += int(np.count_nonzero(m_ & (s == K.ST_PASS)))
+                out[pi, fail_col] += int(np.count_nonzero(m_ & (s == K.ST_FAIL)))
+                out[pi, 3] += int(np.count_nonzero(m_ & (s == K.ST_ERROR)))
+                out[pi, 4] += int(np.count_nonzero(m_ & (s == K.ST_SKIP)))
+                cpu = m_ & ((s == K.ST_FALLBACK) | (s == K.ST_PANIC) | (s == K.ST_ND))
+                out[pi, 5] += int(np.count_nonzero(cpu))
+                active &= ~((s == K.ST_PASS) | (s == K.ST_FAIL) | cpu)
+        return out
+
+    def summary(self):
+        mat = self.summary_matrix()
+        return {m["key"]: dict(zip(SUMMARY_FIELDS, map(int, mat[i]))) for i, m in enumerate(self.scan.meta)}
+
+    def results(self, i):
+        """report rows (EngineResponseToReportResults) of resource i over every scanned policy"""
+        rows = []
+        st = self.res.status
+        rules = self.scan.ruleset.rules
+        for m in self.scan.meta:
+            applied = 0
+            for k in range(m["first_rule"], m["first_rule"] + m["nrules"]):
+                s = int(st[k, i])
+                if s == K.ST_NONE:
+                    continue
+                if s in (K.ST_FALLBACK, K.ST_PANIC, K.ST_ND):
+                    rows.append({"policy": m["key"], "rule": rules[k]["name"], "result": None, "cpu_fallback": True})
+                    if m["apply_one"]:
+                        break
+                    continue
+                result = {K.ST_PASS: "pass", K.ST_FAIL: "fail", K.ST_ERROR: "error", K.ST_SKIP: "skip"}[s]
+                if result == "fail" and not m["scored"]:
+                    result = "warn"
+                row = {"source": "kyverno", "policy": m["key"], "rule": rules[k]["name"], "result": result,
+                       "message": self.res.message(i, k), "scored": m["scored"], "category": m["category"],
+                       "severity": m["severity"]}
+                if rules[k]["kind"] == "podSecurity":
+                    row["pss_mask"] = self.res.pss_mask(i, k)
+                rows.append(row)
+                if s in (K.ST_PASS, K.ST_FAIL):
+                    applied += 1
+                if m["apply_one"] and applied > 0:
+                    break
+        return rows
+
+    def fallback_pairs(self):
+        """(resource index, policy key, rule name) of every pair the CPU engine must evaluate"""
+        st = self.res.status
+        out = []
+        rule_pol = {}
+        for m in self.scan.meta:
+            for k in range(m["first_rule"], m["first_rule"] + m["nrules"]):
+                rule_pol[k] = m["key"]
+        ks, rs = np.nonzero((st == K.ST_FALLBACK) | (st == K.ST_PANIC) | (st == K.ST_ND))
+        for k, r in zip(ks.tolist(), rs.tolist()):
+            out.append((r, rule_pol.get(k), self.scan.ruleset.rules[k]["name"]))
+        return sorted(out)
+
+
+def reduce_summary(matrix, group=None, device=None):
+    """Sum per-policy summaries over the ranks of a torch.distributed group (RCCL all-reduce on GPU tensors with the
+    "nccl" backend; gloo on CPU). Every rank must pass the matrix of the same BackgroundScan policies."""
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(matrix, dtype=np.int64))
+    if device is not None:
+        t = t.to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t.cpu().numpy()
