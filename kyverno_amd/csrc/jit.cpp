@@ -344,7 +344,10 @@ struct Gen {
       }
     }
     if (P.flags & PF_META) {
-      out << "  { uint8_t o = expand_meta(w.v, w.v.metas[w.mbase + " << u(P.meta) << "], NodeTab{w.R}, rn, *w.hp, w.keys);\n"
+      // the out-of-line call gets a copy of the key slots: taking w.keys' address would put the whole walker
+      // state (JW) in scratch memory for every pattern of the kernel
+      out << "  { Keys kk = w.keys; uint8_t o = expand_meta(w.v, w.v.metas[w.mbase + " << u(P.meta)
+          << "], NodeTab{w.R}, rn, *w.hp, kk); w.keys = kk;\n"
           << "    if (o != ST_NONE) { w.ost = o; return ok_ret(); } }\n";
     }
     for (uint32_t e = 0; e < P.n; e++) {
@@ -505,7 +508,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
            "};\n";
   }
   src << "}  // namespace kyv\n"
-         "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 5\n#endif\n";
+         "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n";
   for (size_t gi = 0; gi < ngroups; gi++)
     src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE)))\n"
            "kyv_jit_walk_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, kyv::WorkLists wl, kyv::ChunkMap cm) {\n"
@@ -539,7 +542,7 @@ std::vector<char> jit_compile_uncached(const std::string& src, double* seconds) 
   const char* env = getenv("KYV_CSRC");
   std::string inc = "-I" + (env ? std::string(env) : dir + "/csrc");
   std::string inc2 = "-I" + dir + "/../include";
-  std::string wpe = std::string("-DKYV_JIT_WPE=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "5");
+  std::string wpe = std::string("-DKYV_JIT_WPE=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4");
   std::string extra = getenv("KYV_JIT_DEFS") ? getenv("KYV_JIT_DEFS") : "-DKYV_JIT_NOEXTRA";  // experiments only
   const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str(), wpe.c_str(), extra.c_str()};
   hiprtcProgram prog;
