@@ -54,6 +54,98 @@ struct DevRuleset {
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
 };
 
+// ---------------------------------------------------------------- per-batch device memory
+// Batches come and go at serving rates (admission micro-batches of 1-4096 resources): hipMalloc / hipFree and
+// stream creation per batch cost milliseconds (hipFree synchronises the device). Per-batch buffers therefore come
+// from a caching pool per device (power-of-two size classes up to 256 MiB, exact above), and streams / events from
+// a per-device free list. Buffers are returned only after the evaluation that used them has completed (every
+// kyv_eval synchronises its stream before returning).
+static std::mutex g_pool_mu;
+struct PoolSlot { int dev; size_t cls; };
+static std::vector<std::pair<PoolSlot, void*>> g_pool_free;   // cached buffers
+static std::vector<std::pair<void*, PoolSlot>> g_pool_live;   // handed out
+static constexpr size_t POOL_MAX_CACHED = 64;
+static size_t pool_class(size_t n) {
+  n = std::max<size_t>(n, 256);
+  if (n > ((size_t)256 << 20)) return (n + ((size_t)1 << 20) - 1) & ~(((size_t)1 << 20) - 1);
+  size_t c = 256;
+  while (c < n) c <<= 1;
+  return c;
+}
+static bool pool_off() {
+  static const bool off = getenv("KYV_NO_POOL") && atoi(getenv("KYV_NO_POOL")) != 0;
+  return off;
+}
+template <class T>
+static hipError_t dmalloc(T** p, size_t n) {
+  if (pool_off()) return hipMalloc((void**)p, std::max<size_t>(n, 1));
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const size_t cls = pool_class(n);
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    for (size_t i = 0; i < g_pool_free.size(); i++)
+      if (g_pool_free[i].first.dev == dev && g_pool_free[i].first.cls == cls) {
+        void* q = g_pool_free[i].second;
+        g_pool_free.erase(g_pool_free.begin() + i);
+        g_pool_live.push_back({q, PoolSlot{dev, cls}});
+        *p = (T*)q;
+        return hipSuccess;
+      }
+  }
+  void* q = nullptr;
+  e = hipMalloc(&q, cls);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  g_pool_live.push_back({q, PoolSlot{dev, cls}});
+  *p = (T*)q;
+  return hipSuccess;
+}
+static void dfree(void* q) {
+  if (!q) return;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  for (size_t i = 0; i < g_pool_live.size(); i++)
+    if (g_pool_live[i].first == q) {
+      PoolSlot s = g_pool_live[i].second;
+      g_pool_live.erase(g_pool_live.begin() + i);
+      if (g_pool_free.size() < POOL_MAX_CACHED && s.cls <= ((size_t)256 << 20)) {
+        g_pool_free.push_back({s, q});
+      } else {
+        int cur = 0;
+        hipGetDevice(&cur);
+        hipSetDevice(s.dev);
+        hipFree(q);
+        hipSetDevice(cur);
+      }
+      return;
+    }
+  hipFree(q);  // not from the pool
+}
+struct StreamSet { int dev; hipStream_t s; hipEvent_t e0, e1; };
+static std::vector<StreamSet> g_streams_free;
+static void stream_get(hipStream_t* s, hipEvent_t* e0, hipEvent_t* e1) {
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    for (size_t i = 0; i < g_streams_free.size(); i++)
+      if (g_streams_free[i].dev == dev) {
+        *s = g_streams_free[i].s; *e0 = g_streams_free[i].e0; *e1 = g_streams_free[i].e1;
+        g_streams_free.erase(g_streams_free.begin() + i);
+        return;
+      }
+  }
+  HIP_OK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+  HIP_OK(hipEventCreate(e0));
+  HIP_OK(hipEventCreate(e1));
+}
+static void stream_put(int dev, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  if (!s) return;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  g_streams_free.push_back(StreamSet{dev, s, e0, e1});
+}
+
 struct DeviceResults {
   uint8_t* status = nullptr;
   uint32_t* pss_fails = nullptr;
@@ -83,13 +175,11 @@ struct DeviceResults {
   int cus = 256;
 };
 
-static void free_dev_results(DeviceResults& d) {
-  hipFree(d.view); hipFree(d.status); hipFree(d.pss_fails); hipFree(d.pss_slot); hipFree(d.recs); hipFree(d.nrecs); hipFree(d.counts);
-  hipFree(d.stage); hipFree(d.rbase); hipFree(d.rcnt); hipFree(d.tsum);
-  hipFree(d.wl.items); hipFree(d.wl.cnt); hipFree(d.sched); hipFree(d.mrules);
-  if (d.e0) hipEventDestroy(d.e0);
-  if (d.e1) hipEventDestroy(d.e1);
-  if (d.stream) hipStreamDestroy(d.stream);
+static void free_dev_results(DeviceResults& d, int dev) {
+  dfree(d.view); dfree(d.status); dfree(d.pss_fails); dfree(d.pss_slot); dfree(d.recs); dfree(d.nrecs); dfree(d.counts);
+  dfree(d.stage); dfree(d.rbase); dfree(d.rcnt); dfree(d.tsum);
+  dfree(d.wl.items); dfree(d.wl.cnt); dfree(d.sched); dfree(d.mrules);
+  stream_put(dev, d.stream, d.e0, d.e1);
   d = DeviceResults();
 }
 
@@ -156,7 +246,7 @@ static DevBatch* upload_batch(const Batch& b, int device) {
   for (auto& E : pe) if (E.col != NONE) E.col = b.col_off[E.col];
   d->o_pe = p.add(pe);
   d->bytes = p.host.size();
-  HIP_OK(hipMalloc(&d->base, d->bytes));
+  HIP_OK(dmalloc(&d->base, d->bytes));
   HIP_OK(hipMemcpy(d->base, p.host.data(), d->bytes, hipMemcpyHostToDevice));
   d->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return d;
@@ -482,11 +572,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     size_t mr = std::max<size_t>(nres * per_res, 1);
     if (mr > 0xFFFFFFF0u) throw std::runtime_error("batch too large for one failure-record buffer");
     d.max_recs = (uint32_t)mr;
-    HIP_OK(hipMalloc(&d.status, std::max<size_t>(1, nres * nrules)));
-    HIP_OK(hipMalloc(&d.pss_fails, std::max<size_t>(4, (size_t)d.npss * nres * 4)));
-    HIP_OK(hipMalloc(&d.pss_slot, std::max<size_t>(4, nrules * 4)));
-    HIP_OK(hipMalloc(&d.recs, (size_t)d.max_recs * sizeof(FailRec)));
-    HIP_OK(hipMalloc(&d.nrecs, 4));
+    HIP_OK(dmalloc(&d.status, std::max<size_t>(1, nres * nrules)));
+    HIP_OK(dmalloc(&d.pss_fails, std::max<size_t>(4, (size_t)d.npss * nres * 4)));
+    HIP_OK(dmalloc(&d.pss_slot, std::max<size_t>(4, nrules * 4)));
+    HIP_OK(dmalloc(&d.recs, (size_t)d.max_recs * sizeof(FailRec)));
+    HIP_OK(dmalloc(&d.nrecs, 4));
     {  // staging: chunk (k, w) owns 64 * alts(k) slots
       const size_t nwv = (nres + WAVE - 1) / WAVE;
       std::vector<uint32_t> rb(std::max<size_t>(nrules, 1), 0);
@@ -498,18 +588,16 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         tot += alts * nwv * WAVE;
         if (tot > 0xFFFFFFF0ull) throw std::runtime_error("batch too large for one failure-record staging buffer");
       }
-      HIP_OK(hipMalloc(&d.stage, std::max<size_t>(tot, 1) * sizeof(FailRec)));
-      HIP_OK(hipMalloc(&d.rbase, rb.size() * 4));
+      HIP_OK(dmalloc(&d.stage, std::max<size_t>(tot, 1) * sizeof(FailRec)));
+      HIP_OK(dmalloc(&d.rbase, rb.size() * 4));
       HIP_OK(hipMemcpy(d.rbase, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
-      HIP_OK(hipMalloc(&d.rcnt, std::max<size_t>(nrules * nwv, 1) * 2));
-      HIP_OK(hipMalloc(&d.tsum, std::max<size_t>((nrules * nwv + WAVE - 1) / WAVE, 1) * 4));
+      HIP_OK(dmalloc(&d.rcnt, std::max<size_t>(nrules * nwv, 1) * 2));
+      HIP_OK(dmalloc(&d.tsum, std::max<size_t>((nrules * nwv + WAVE - 1) / WAVE, 1) * 4));
     }
-    HIP_OK(hipMalloc(&d.counts, std::max<size_t>(1, nrules) * NSTATUS * 8));
+    HIP_OK(dmalloc(&d.counts, std::max<size_t>(1, nrules) * NSTATUS * 8));
     HIP_OK(hipMemcpy(d.pss_slot, pss_slot.data(), nrules * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    HIP_OK(hipEventCreate(&d.e0));
-    HIP_OK(hipEventCreate(&d.e1));
-    HIP_OK(hipMalloc(&d.view, sizeof(View)));
+    stream_get(&d.stream, &d.e0, &d.e1);
+    HIP_OK(dmalloc(&d.view, sizeof(View)));
     HIP_OK(hipMemcpy(d.view, &v, sizeof(View), hipMemcpyHostToDevice));
     // walk work lists: one 64-slot list per (rule, match wave)
     d.wl.nwaves = (uint32_t)((nres + WAVE - 1) / WAVE);
@@ -521,11 +609,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         if (!direct) ml.push_back((uint32_t)k);
       }
       d.nm = (uint32_t)ml.size();
-      HIP_OK(hipMalloc(&d.mrules, std::max<size_t>(1, ml.size()) * 4));
+      HIP_OK(dmalloc(&d.mrules, std::max<size_t>(1, ml.size()) * 4));
       if (!ml.empty()) HIP_OK(hipMemcpy(d.mrules, ml.data(), ml.size() * 4, hipMemcpyHostToDevice));
     }
-    HIP_OK(hipMalloc(&d.wl.items, std::max<size_t>(1, nrules * (size_t)d.wl.nwaves * WAVE) * sizeof(uint2)));
-    HIP_OK(hipMalloc(&d.wl.cnt, std::max<size_t>(4, nrules * (size_t)d.wl.nwaves + 4)));
+    HIP_OK(dmalloc(&d.wl.items, std::max<size_t>(1, nrules * (size_t)d.wl.nwaves * WAVE) * sizeof(uint2)));
+    HIP_OK(dmalloc(&d.wl.cnt, std::max<size_t>(4, nrules * (size_t)d.wl.nwaves + 4)));
     // persistent grid: enough waves to fill the chip several times over, never more than the chunks
     int cus = 256;
     hipDeviceProp_t prop;
@@ -605,8 +693,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         slots[cls].swap(out);
       }
     }
-    hipFree(d.sched);
-    HIP_OK(hipMalloc(&d.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
+    dfree(d.sched);
+    d.sched = nullptr;
+    HIP_OK(dmalloc(&d.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
     d.cm.assign(ncls, ChunkMap{nullptr, 0});
     size_t at = 0;
     for (uint32_t cls = 0; cls < ncls; cls++) {
@@ -781,8 +870,8 @@ void free_device_images(Ruleset& rs, Batch* b) {
       if (p) {
         DevBatch* d = (DevBatch*)p;
         hipSetDevice(d->device);
-        hipFree(d->base);
-        if (d->out) { free_dev_results(*d->out); delete d->out; }
+        dfree(d->base);
+        if (d->out) { free_dev_results(*d->out, d->device); delete d->out; }
         delete d;
       }
     b->dev.clear();
