@@ -22,9 +22,11 @@
  *                        status, message, failing path; plus the summary counters used by
  *                        pkg/utils/report/results.go:38 (CalculateSummary).
  *
- * Rules that need the reference CPU engine (variables/JMESPath, context, preconditions, deny, foreach,
- * image verification) are classified at compile time; their pairs report KYV_ST_FALLBACK and the caller
- * runs engine.Validate for them.
+ * deny and preconditions run on the device when every variable is a plain `{{ request.object.<path> }}`
+ * reference (pkg/engine/variables/evaluate.go:21, operator/*.go). Rules that need the reference CPU engine
+ * (JMESPath functions / projections, other context variables, context entries, foreach, exceptions, image
+ * verification) are classified at compile time; their pairs report KYV_ST_FALLBACK and the caller runs
+ * engine.Validate for them.
  *
  * Threading: a kyv_ruleset is immutable after compile and may be shared; batches and results are per
  * call. No C++ exception crosses this ABI; failures return a non-zero code and kyv_last_error()

@@ -64,13 +64,16 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libkyvgpu.so not built: run `python -m kyverno_amd.build` (or __graft_entry__.build())")
-    # One HIP runtime per process: torch bundles its own libamdhip64. When this library's /opt/rocm runtime is
-    # loaded first, torch later binds to it and finds no GPUs (ProcessGroupNCCL: "no GPUs found"); loading torch
-    # first makes both use torch's runtime. (torch is plumbing here: device memory for RCCL collectives.)
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # One HIP runtime per process. torch bundles its own (older) libamdhip64; whichever is loaded first serves
+    # both. Default: this library's /opt/rocm runtime (the C3 evaluation measured 2.96 ms on it vs 3.48 ms on
+    # torch's). A process that also needs torch on the GPU (RCCL collectives through torch.distributed) must load
+    # torch first, else torch finds no GPUs (ProcessGroupNCCL: "no GPUs found"): set KYV_TORCH_FIRST=1 or import
+    # torch before kyverno_amd.
+    if os.environ.get("KYV_TORCH_FIRST", "0") != "0":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(LIB_PATH)
     vp, sz, u32, i32, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int64
     L.kyv_ruleset_compile.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(CompileOpts), ctypes.POINTER(vp)]

@@ -357,6 +357,10 @@ def decide(responses, fail_policy):
 
 
 # ------------------------------------------------------------------------------------------------------- batching
+def _dumps1(doc):
+    return json.dumps(doc, separators=(",", ":")).encode()
+
+
 def _meta(obj):
     m = obj.get("metadata") if isinstance(obj, dict) else None
     return m if isinstance(m, dict) else {}
@@ -366,7 +370,8 @@ class AdmissionBatcher:
     """Micro-batched validating admission over one compiled policy set.
 
     requests: dicts {"uid", "operation" (CREATE / UPDATE / DELETE / CONNECT), "kind" (request.Kind.Kind),
-    "namespace", "object", "oldObject", "namespace_labels"}.
+    "namespace", "object", "oldObject", "namespace_labels"}; "object_raw" / "oldObject_raw" (the request's JSON bytes,
+    AdmissionRequest.Object.Raw) are flattened as they are when present instead of re-serialising the dicts.
     cpu_engine(policy, request) -> list of rule responses [{name, status, message}] (engine.Validate on the CPU,
     the Go shim's job); when None, requests needing it come back with "cpu_pending" set and no decision."""
 
@@ -442,15 +447,15 @@ class AdmissionBatcher:
             i_new = i_old = None
             if op != "DELETE" and new:
                 i_new = len(docs)
-                docs.append(new)
+                docs.append(rq.get("object_raw") or _dumps1(new))
                 if op == "UPDATE" and old:
                     i_old = len(docs)
-                    docs.append(old)
+                    docs.append(rq.get("oldObject_raw") or _dumps1(old))
             slots.append((i_new, i_old))
         st = res = None
         quiet = cpu = None
         if docs:
-            batch = E.Batch(self.ruleset, docs, ns_labels or None)
+            batch = E.Batch(self.ruleset, b"\n".join(docs), ns_labels or None)  # NDJSON
             res = E.evaluate(self.ruleset, batch, backend=self.backend, device=self.device)
             st = res.status
             # per policy over the whole batch: "every matched rule passed" (the policy cannot change the decision)

@@ -431,7 +431,9 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
     b->rs = rs;
     b->dict = rs->dict;
     auto docs = split_docs(json, len);
-    int T = std::max(1, threads);
+    // threads scaled to the work: thread start-up is tens of microseconds, which dominates small (admission)
+    // batches when every phase spawns the machine's thread count
+    int T = std::max(1, std::min(threads, (int)(docs.size() / 256) + 1));
     size_t nchunks = std::min(docs.size(), (size_t)T * 8);
     if (nchunks == 0) nchunks = 1;
     std::vector<Chunk> chunks(nchunks);
@@ -551,7 +553,7 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
       if (h.labels != NONE) h.labels = find(KSID(LABELS));
       if (h.ann != NONE) h.ann = find(KSID(ANNOTATIONS));
     }
-    derive_strings(*b, 0, T);
+    derive_strings(*b, 0, std::max(1, std::min(T, (int)(b->dict.strs.size() / 8192) + 1)));
     order_by_kind(*b);
     resolve_path_columns(*b, T);
     (void)seed;

@@ -615,9 +615,20 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(dmalloc(&d.wl.items, std::max<size_t>(1, nrules * (size_t)d.wl.nwaves * WAVE) * sizeof(uint2)));
     HIP_OK(dmalloc(&d.wl.cnt, std::max<size_t>(4, nrules * (size_t)d.wl.nwaves + 4)));
     // persistent grid: enough waves to fill the chip several times over, never more than the chunks
-    int cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+    // CU count per device, queried once (hipGetDeviceProperties costs milliseconds per call)
+    static std::mutex cu_mu;
+    static std::vector<int> cu_count;
+    int cus = 0;
+    {
+      std::lock_guard<std::mutex> g(cu_mu);
+      if ((int)cu_count.size() <= device) cu_count.resize(device + 1, 0);
+      if (!cu_count[device]) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c <= 0) c = 256;
+        cu_count[device] = c;
+      }
+      cus = cu_count[device];
+    }
     d.cus = cus;
     db->out = dd;
   }

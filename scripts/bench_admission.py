@@ -50,6 +50,7 @@ def requests(n, seed=0x4b59564e):
         md = d.get("metadata") if isinstance(d.get("metadata"), dict) else {}
         ns = md.get("namespace") if isinstance(md.get("namespace"), str) else ""
         out.append({"uid": str(i), "operation": "CREATE", "kind": d.get("kind", ""), "namespace": ns, "object": d,
+                    "object_raw": json.dumps(d, separators=(",", ":")).encode(),  # AdmissionRequest.Object.Raw
                     "namespace_labels": nsl.get(ns) if ns else None})
     return out
 

@@ -128,28 +128,44 @@ def test_c5_conditions_gpu():
     assert st["compared"] > 40000 and st["fallback"] > 0
 
 
+_SCAN_RCCL = r"""
+import os, sys
+import numpy as np
+import torch  # loaded before libkyvgpu: torch and the library share one HIP runtime (kyverno_amd/_lib.py)
+import torch.distributed as dist
+sys.path[:0] = [os.getcwd(), os.path.join(os.getcwd(), "tests")]
+from kyverno_amd import scan as SC, synth
+import test_scan as TS
+pols = TS.policy_set()
+docs, nsl = synth.mixed(20001, seed=44, edge=True)
+g = SC.BackgroundScan(pols, backend="gpu").scan(docs, nsl)
+c = SC.BackgroundScan(pols, backend="cpu").scan(docs, nsl)
+st = g.res.status
+for k in range(st.shape[0]):
+    assert np.array_equal(np.bincount(st[k], minlength=8), g.res.rule_counts[k]), k
+assert np.array_equal(g.summary_matrix(), c.summary_matrix())
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+os.environ.setdefault("MASTER_PORT", "29531")
+dist.init_process_group("nccl", rank=0, world_size=1)
+try:
+    tot = SC.reduce_summary(g.summary_matrix(), device=torch.device("cuda", 0))
+finally:
+    dist.destroy_process_group()
+assert np.array_equal(tot, g.summary_matrix())
+print("scan-rccl ok")
+"""
+
+
 def test_scan_summary_gpu_and_rccl():
     """batched background scan on the device: per-rule verdict totals (unaligned rule rows: 20,001 resources) equal
     the verdict bytes, the per-policy summary equals the host instantiation's, and the summary all-reduce runs over
-    RCCL (single-rank "nccl" group)"""
+    RCCL (single-rank "nccl" group). Runs in a fresh interpreter that loads torch before the library (one HIP
+    runtime per process; this test process already loaded libkyvgpu on its own runtime)."""
     import os
-    import torch
-    import torch.distributed as dist
-    from kyverno_amd import scan as SC
-    import test_scan as TS
-    pols = TS.policy_set()
-    docs, nsl = synth.mixed(20001, seed=44, edge=True)
-    g = SC.BackgroundScan(pols, backend="gpu").scan(docs, nsl)
-    c = SC.BackgroundScan(pols, backend="cpu").scan(docs, nsl)
-    st = g.res.status
-    for k in range(st.shape[0]):
-        assert np.array_equal(np.bincount(st[k], minlength=8), g.res.rule_counts[k]), k
-    assert np.array_equal(g.summary_matrix(), c.summary_matrix())
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29531")
-    dist.init_process_group("nccl", rank=0, world_size=1)
-    try:
-        tot = SC.reduce_summary(g.summary_matrix(), device=torch.device("cuda", 0))
-    finally:
-        dist.destroy_process_group()
-    assert np.array_equal(tot, g.summary_matrix())
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, KYV_TORCH_FIRST="1")
+    r = subprocess.run([sys.executable, "-c", _SCAN_RCCL], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=200)
+    assert r.returncode == 0 and "scan-rccl ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
