@@ -671,7 +671,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     const bool xcd = !getenv("KYV_XCD") || atoi(getenv("KYV_XCD")) != 0;
     for (uint32_t cls = 0; cls < ncls; cls++) {
       if (slots[cls].size() > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
-      d.grid[cls] = (uint32_t)std::min<size_t>(slots[cls].size(), (size_t)d.cus * 64);
+      // walk grid: up to 1024 one-wave workgroups per CU, grid-stride beyond that. Measured on C3 (kernel ms):
+      // 16/CU 3.03, 64/CU 2.95, 128/CU 2.88, 256/CU 2.78, 512/CU 2.70, 1024/CU 2.66, 2048/CU 2.74, one per chunk 2.75
+      // (more resident-or-queued waves hide the walk's dependent-load latency; KYV_GRID overrides)
+      static const size_t gmul = getenv("KYV_GRID") ? (size_t)std::max(1, atoi(getenv("KYV_GRID"))) : 1024;
+      d.grid[cls] = (uint32_t)std::min<size_t>(slots[cls].size(), (size_t)d.cus * gmul);
       tot += slots[cls].size();
       // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs (block b and b + 8 share one L2),
       // and the grid-stride loop hands position p to block p % G. The chunks of one match wave (the same 64
