@@ -227,3 +227,11 @@ def test_admission_routing_without_cpu_engine():
 @pytest.mark.gpu
 def test_admission_gpu_matches_per_request_cpu():
     check_admission("gpu", 2000, 512)
+
+
+def test_wildcard_golden_admission(golden):
+    """the override namespace matcher vs pkg/utils/wildcard/match_test.go (52 vectors, go-wildcard v1.0.3)"""
+    recs = golden("wildcard.json")
+    assert len(recs) >= 50
+    for r in recs:
+        assert A.wildcard_match(r["pattern"], r["text"]) == r["matched"], r
