@@ -383,22 +383,35 @@ __global__ void __launch_bounds__(WAVE) compact_sum_kernel(const uint16_t* __res
 }
 __global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict__ tsum, uint32_t ntiles,
                                                             uint32_t* __restrict__ nout) {
-  __shared__ uint32_t part[1024];
-  const uint32_t t = threadIdx.x, per = (ntiles + 1023) / 1024;
-  const uint32_t lo = t * per, hi = min(ntiles, lo + per);
-  uint32_t sum = 0;
-  for (uint32_t i = lo; i < hi; i++) sum += tsum[i];
-  part[t] = sum;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
-    uint32_t y = t >= off ? part[t - off] : 0u;
+  // rounds of 1024 consecutive tiles (coalesced): wave inclusive scans, a scan of the 16 wave totals, carry across
+  // rounds
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < ntiles; base += 1024) {
+    const uint32_t i = base + t;
+    const uint32_t x = i < ntiles ? tsum[i] : 0u;
+    uint32_t v = x;
+    for (int off = 1; off < WAVE; off <<= 1) {
+      const uint32_t y = __shfl_up(v, off);
+      if ((int)lane >= off) v += y;
+    }
+    if (lane == WAVE - 1) wsum[w] = v;
     __syncthreads();
-    part[t] += y;
+    if (w == 0) {
+      uint32_t s2 = lane < 16 ? wsum[lane] : 0u;
+      for (int off = 1; off < 16; off <<= 1) {
+        const uint32_t y = __shfl_up(s2, off);
+        if ((int)lane >= off) s2 += y;
+      }
+      if (lane < 16) wsum[lane] = s2;
+    }
+    __syncthreads();
+    if (i < ntiles) tsum[i] = carry + (w ? wsum[w - 1] : 0u) + v - x;  // exclusive offset of tile i
+    carry += wsum[15];
     __syncthreads();
   }
-  uint32_t run = part[t] - sum;
-  for (uint32_t i = lo; i < hi; i++) { uint32_t x = tsum[i]; tsum[i] = run; run += x; }
-  if (t == 1023) *nout = part[1023];
+  if (t == 0) *nout = carry;
 }
 __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __restrict__ stage, const uint32_t* __restrict__ rbase,
                                                             const uint16_t* __restrict__ rcnt, const RuleDesc* __restrict__ rules,
