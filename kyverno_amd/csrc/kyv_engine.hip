@@ -770,8 +770,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, d.tsum, ntiles, d.nrecs);
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, d.rbase, d.rcnt, drules,
                          d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs);
+      // histogram blocks per CU: 8 (2.620 ms per evaluation) vs 2 (2.64 ms): more blocks stream the status bytes faster
+      static const size_t hmul = getenv("KYV_HIST") ? (size_t)std::max(1, atoi(getenv("KYV_HIST"))) : 8;
       const uint32_t hgrid = (uint32_t)std::max<size_t>(
-          1, std::min<size_t>(((size_t)d.cus * 2 + nrules - 1) / std::max<size_t>(1, nrules), (nres / 16 + HIST_BLOCK - 1) / HIST_BLOCK));
+          1, std::min<size_t>(((size_t)d.cus * hmul + nrules - 1) / std::max<size_t>(1, nrules), (nres / 16 + HIST_BLOCK - 1) / HIST_BLOCK));
       if (nrules) hipLaunchKernelGGL(status_hist_kernel, dim3(hgrid, (uint32_t)nrules), dim3(HIST_BLOCK), 0, stream, d.status, nres, d.counts);
       HIP_OK(hipGetLastError());
     }
