@@ -115,11 +115,21 @@ typedef struct {
 
 /* ---- ruleset: replaces per-call ComputeRules + pattern decoding ---- */
 int kyv_ruleset_compile(const char* policies_json, size_t len, const kyv_compile_opts* opts, kyv_ruleset** out);
+/* same, with the cluster's PolicyExceptions (kyverno.io/v2alpha1 documents, JSON array / NDJSON): replaces the
+ * per-rule lister scan of PolicyContext.FindExceptions (pkg/engine/policyContext.go:150-169). A rule some exception
+ * names (PolicyException.Contains, api/kyverno/v2alpha1/policy_exception_types.go:101) reports KYV_ST_FALLBACK with
+ * reason "exception" for every matched pair; the caller's engine.Validate then applies hasPolicyExceptions
+ * (pkg/engine/validation.go:797-848). exceptions_json may be NULL. */
+int kyv_ruleset_compile_ex(const char* policies_json, size_t len, const char* exceptions_json, size_t ex_len,
+                           const kyv_compile_opts* opts, kyv_ruleset** out);
 void kyv_ruleset_free(kyv_ruleset* rs);
 uint32_t kyv_ruleset_num_rules(const kyv_ruleset* rs);
 uint32_t kyv_ruleset_num_policies(const kyv_ruleset* rs);
 int kyv_ruleset_rule_info(const kyv_ruleset* rs, uint32_t rule, kyv_rule_info* out);
 int kyv_ruleset_policy_info(const kyv_ruleset* rs, uint32_t policy, kyv_policy_info* out);
+/* MatchResources.GetKinds() of compiled rule `rule` ('\n'-separated, autogen applied) and Rule.HasValidate(): the
+ * policy cache's kind index (policyMap.set, pkg/policycache/store.go:96-138); returns the full length or -1 */
+int64_t kyv_ruleset_rule_kinds(const kyv_ruleset* rs, uint32_t rule, char* buf, size_t cap, int32_t* has_validate);
 /* runtime-compiled walk kernel of a ruleset (diagnostics; kyv_eval compiles it on first use by itself):
    the generated HIP source (returns its full length; rules it covers in *nrules_jit) and a hipRTC compile for
    gfx950 that needs no GPU (seconds, code-object bytes) */
@@ -155,6 +165,11 @@ int64_t kyv_results_message(const kyv_results* r, const kyv_ruleset* rs, const k
 /* failing path of a single-pattern FAIL ("" otherwise); returns the full length */
 int64_t kyv_results_path(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res, uint32_t rule,
                          char* buf, size_t cap);
+/* why a KYV_ST_FALLBACK pair needs the reference engine ("" for other statuses): the rule's compile-time reason
+ * ("context", "foreach", "exception", "variables", ...) or the run-time site (value / walk outside the device subset);
+ * returns the full length, -1 on bad arguments */
+int64_t kyv_results_fallback_reason(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,
+                                    uint32_t rule, char* buf, size_t cap);
 /* PodSecurity rules: failing (check, version) slot mask after exclusions */
 uint32_t kyv_results_pss_mask(const kyv_results* r, const kyv_ruleset* rs, uint32_t res, uint32_t rule);
 

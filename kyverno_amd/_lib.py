@@ -51,7 +51,8 @@ EXPORTS = [
     "kyv_batch_num_resources", "kyv_batch_stats_get", "kyv_eval", "kyv_results_free", "kyv_results_status",
     "kyv_results_count", "kyv_results_kernel_ms", "kyv_results_alg_bytes", "kyv_results_message", "kyv_results_path",
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
-    "kyv_ruleset_jit_compile", "kyv_results_rule_counts",
+    "kyv_ruleset_jit_compile", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
+    "kyv_results_fallback_reason",
 ]
 
 _lib = None
@@ -77,6 +78,12 @@ def lib():
     L = ctypes.CDLL(LIB_PATH)
     vp, sz, u32, i32, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int64
     L.kyv_ruleset_compile.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(CompileOpts), ctypes.POINTER(vp)]
+    L.kyv_ruleset_compile_ex.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(CompileOpts),
+                                         ctypes.POINTER(vp)]
+    L.kyv_ruleset_rule_kinds.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(i32)]
+    L.kyv_ruleset_rule_kinds.restype = i64
+    L.kyv_results_fallback_reason.argtypes = [vp, vp, vp, u32, u32, ctypes.c_char_p, sz]
+    L.kyv_results_fallback_reason.restype = i64
     L.kyv_ruleset_free.argtypes = [vp]
     L.kyv_ruleset_num_rules.argtypes = [vp]
     L.kyv_ruleset_num_rules.restype = u32

@@ -164,6 +164,31 @@ def response_action(p, resource_ns, ns_labels):
     return s.get("validationFailureAction", "")
 
 
+def kind_from_gvk(s):
+    """kubeutils.GetKindFromGVK (pkg/utils/kube/kind.go:11-32) -> (groupVersion, kind)"""
+    parts = s.split("/")
+    ver = re.compile(r"v\d((alpha|beta)\d)?")
+    fmt = lambda x: x.replace(".", "/", 1)
+    if len(parts) == 2:
+        if ver.search(parts[0]) or parts[0] == "*":
+            return parts[0], fmt(parts[1])
+        return "", parts[0] + "/" + parts[1]
+    if len(parts) == 3:
+        if ver.search(parts[0]) or parts[0] == "*":
+            return parts[0], parts[1] + "/" + parts[2]
+        return parts[0] + "/" + parts[1], fmt(parts[2])
+    if len(parts) == 4:
+        return parts[0] + "/" + parts[1], parts[2] + "/" + parts[3]
+    return "", fmt(s)
+
+
+def compute_kind(gvk):
+    """policycache computeKind (store.go:70-74): GetKindFromGVK then SplitSubresource"""
+    _, k = kind_from_gvk(gvk)
+    parts = k.split("/")
+    return parts[0] if len(parts) == 2 else k
+
+
 def _uses_userinfo(block):
     if not isinstance(block, dict):
         return False
@@ -393,26 +418,36 @@ class AdmissionBatcher:
                         nm = nm[len(pre):]
                         break
                 userinfo = userinfo or rule_uses_userinfo(base.get(nm) or {})
+            # policyMap.set (store.go:96-138): kinds of the autogen-expanded rules that have a validate block
+            kinds = set()
+            for k in range(pm["first_rule"], pm["first_rule"] + pm["nrules"]):
+                ri = self.ruleset.rules[k]
+                if ri["has_validate"]:
+                    kinds.update(compute_kind(g) for g in ri["match_kinds"])
             self.pol.append({"doc": p, "name": pm["name"], "namespace": pm["namespace"], "first": pm["first_rule"],
                              "n": pm["nrules"], "apply_one": pm["apply_one"], "userinfo": userinfo,
-                             "enforce": has_validate(p) and compute_enforce_policy(p),
+                             "enforce": has_validate(p) and compute_enforce_policy(p), "kinds": kinds,
                              "fail_policy": failure_policy(p)})
         self.stats = {"requests": 0, "batches": 0, "device_policies": 0, "cpu_policies": 0}
         self._q, self._cv, self._stop, self._thr = [], threading.Condition(), False, None
         self._enforce_cache = {}
 
-    # policycache.GetPolicies(ValidateEnforce, kind, ns) (cache.go:38-57): cluster policies + the namespace's
-    # Policies, then the override filter; the kind index itself is the device's kind gate (a policy with no rule for
-    # the kind gets no rule responses and cannot change the decision)
-    def enforce_policies(self, ns):
+    # policycache.GetPolicies(ValidateEnforce, kind, ns) (cache.go:38-57): cluster policies indexed under the request
+    # kind and under "*", then the namespace's Policies under both, then the override filter (filterPolicies). A
+    # policy indexed under both keys is returned twice, as the reference's append of the two set lookups does.
+    def enforce_policies(self, ns, kind=None):
         out = []
-        for i, p in enumerate(self.pol):
-            if not p["enforce"]:
-                continue
-            if p["namespace"] and p["namespace"] != ns:
-                continue
-            if keep_for_enforce(p["doc"], ns):
-                out.append(i)
+        keys = [compute_kind(kind), "*"] if kind is not None else [None]
+        scopes = [""] + ([ns] if ns else [])
+        for scope in scopes:
+            for key in keys:
+                for i, p in enumerate(self.pol):
+                    if not p["enforce"] or p["namespace"] != scope:
+                        continue
+                    if key is not None and key not in p["kinds"]:
+                        continue
+                    if keep_for_enforce(p["doc"], ns):
+                        out.append(i)
         return out
 
     def _device_rules(self, pi, st, r, res):
@@ -427,8 +462,12 @@ class AdmissionBatcher:
                 continue
             if s in CPU_STATUSES:
                 return None
-            rules.append({"name": self.ruleset.rules[k]["name"], "status": STATUS_TEXT[s],
-                          "message": None if s == K.ST_PASS else res.message(r, k)})
+            msg = None
+            if s != K.ST_PASS:
+                msg = res.message(r, k)
+                if msg is None:  # message not renderable from device verdicts: the CPU engine decides the policy
+                    return None
+            rules.append({"name": self.ruleset.rules[k]["name"], "status": STATUS_TEXT[s], "message": msg})
             if s in (K.ST_PASS, K.ST_FAIL):
                 applied += 1
             if p["apply_one"] and applied > 0:
@@ -484,9 +523,13 @@ class AdmissionBatcher:
         dts = _meta(old).get("deletionTimestamp") if new else _meta(new).get("deletionTimestamp")
         if dts is not None and op == "UPDATE":
             return {"uid": rq.get("uid"), "allowed": True, "message": "", "warnings": None, "exact": True}
-        pols = self._enforce_cache.get(ns)
+        patched0 = new if new else old
+        rkind = rq.get("kind")
+        if rkind is None:
+            rkind = patched0.get("kind", "") if isinstance(patched0, dict) else ""
+        pols = self._enforce_cache.get((ns, rkind))
         if pols is None:
-            pols = self._enforce_cache[ns] = self.enforce_policies(ns)
+            pols = self._enforce_cache[(ns, rkind)] = self.enforce_policies(ns, rkind)
         if not pols:
             return {"uid": rq.get("uid"), "allowed": True, "message": "", "warnings": None, "exact": True}
         patched = new if new else old
@@ -560,13 +603,29 @@ class AdmissionBatcher:
                         break
                     self._cv.wait(left)
                 take, self._q = self._q[:self.max_batch], self._q[self.max_batch:]
+            # a future its caller cancelled is dropped here; the others are marked running (no later cancel)
+            take = [t for t in take if t[1].set_running_or_notify_cancel()]
+            if not take:
+                continue
             try:
                 outs = self.handle_batch([t[0] for t in take])
-                for (_, f, _), o in zip(take, outs):
-                    f.set_result(o)
             except Exception as e:  # surface device errors to every waiter of the batch
                 for _, f, _ in take:
-                    f.set_exception(e)
+                    _resolve(f, exc=e)
+                continue
+            for (_, f, _), o in zip(take, outs):
+                _resolve(f, result=o)
+
+
+def _resolve(f, result=None, exc=None):
+    """complete one waiter; a future that is already resolved must not take the batcher thread down"""
+    try:
+        if exc is not None:
+            f.set_exception(exc)
+        else:
+            f.set_result(result)
+    except Exception:  # InvalidStateError: resolved elsewhere
+        pass
 
 
 def latency_summary(lat_s):

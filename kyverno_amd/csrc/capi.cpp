@@ -13,6 +13,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
               int jit_mode);
 void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool account);
 void free_device_images(Ruleset& rs, Batch* b);
+std::string fallback_why(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule);
 }  // namespace kyv
 
 using namespace kyv;
@@ -42,11 +43,16 @@ const char* kyv_last_error(void) { return g_err.c_str(); }
 const char* kyv_version(void) { return "kyvgpu 0.1 (gfx950)"; }
 
 int kyv_ruleset_compile(const char* json, size_t len, const kyv_compile_opts* opts, kyv_ruleset** out) {
+  return kyv_ruleset_compile_ex(json, len, nullptr, 0, opts, out);
+}
+
+int kyv_ruleset_compile_ex(const char* json, size_t len, const char* exceptions_json, size_t ex_len,
+                           const kyv_compile_opts* opts, kyv_ruleset** out) {
   if (!json || !out) return fail(KYV_EINVAL, "null argument");
   if (opts && opts->abi_version != KYV_ABI_VERSION) return fail(KYV_EINVAL, "ABI version mismatch");
   try {
     std::string err;
-    Ruleset* rs = compile_ruleset(json, len, &err);
+    Ruleset* rs = compile_ruleset(json, len, &err, exceptions_json, exceptions_json ? ex_len : 0);
     if (!rs) return fail(KYV_EPARSE, err);
     *out = new kyv_ruleset{rs};
     return KYV_OK;
@@ -73,6 +79,16 @@ int kyv_ruleset_rule_info(const kyv_ruleset* rs, uint32_t k, kyv_rule_info* out)
   out->kind = m.kind;
   out->reason = m.reason.c_str();
   return KYV_OK;
+}
+
+int64_t kyv_ruleset_rule_kinds(const kyv_ruleset* rs, uint32_t k, char* buf, size_t cap, int32_t* has_validate) {
+  if (!rs || k >= rs->rs->rules.size()) return fail(KYV_ERANGE, "rule index out of range"), -1;
+  const RuleMeta& m = rs->rs->meta[k];
+  std::string s;
+  for (size_t i = 0; i < m.kinds.size(); i++) s += (i ? "\n" : "") + m.kinds[i];
+  if (has_validate) *has_validate = m.has_validate ? 1 : 0;
+  if (buf && cap) { size_t n = std::min(cap - 1, s.size()); memcpy(buf, s.data(), n); buf[n] = 0; }
+  return (int64_t)s.size();
 }
 
 int64_t kyv_ruleset_jit_source(const kyv_ruleset* rs, char* buf, size_t cap, uint32_t* nrules_jit) {
@@ -381,6 +397,19 @@ int64_t kyv_results_path(const kyv_results* cr, const kyv_ruleset* crs, const ky
   if (it == r->recidx.end()) return put("", buf, cap);
   const FailRec& f = r->r.fails[it->second];
   return put(format_path(*crs->rs, *cb->b, f.tmpl, f.idx, f.key), buf, cap);
+}
+
+int64_t kyv_results_fallback_reason(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,
+                                    uint32_t rule, char* buf, size_t cap) {
+  if (!r || !rs || !b || rule >= r->r.nrules || res >= r->r.nres) return -1;
+  try {
+    const uint32_t pos = r->inv[res];
+    if (!r->r.status.empty() && (r->r.status[(size_t)rule * r->r.nres + pos] & 7) != ST_FALLBACK) return put("", buf, cap);
+    return put(fallback_why(*rs->rs, *b->b, pos, rule), buf, cap);
+  } catch (std::exception& e) {
+    fail(KYV_EINTERNAL, e.what());
+    return -1;
+  }
 }
 
 uint32_t kyv_results_pss_mask(const kyv_results* r, const kyv_ruleset* rs, uint32_t res, uint32_t rule) {

@@ -1250,11 +1250,24 @@ std::string fallback_reason(const Value& r) {  // validator.validate dispatch (v
 
 void mark_gate_exact(Ruleset& rs);
 
-Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
+Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const char* exceptions, size_t ex_len) {
   auto rs = std::make_unique<Ruleset>();
   try {
     seed_dict(rs->dict);
     std::vector<Value> docs = pj::parse_many(json, len, true);
+    // (policy key, rule name) pairs some PolicyException lists (FindExceptions, pkg/engine/policyContext.go:150-169):
+    // the exception's match block is checked by the CPU engine (hasPolicyExceptions, validation.go:797-848)
+    std::set<std::pair<std::string, std::string>> excepted;
+    if (exceptions && ex_len) {
+      for (auto& ex : pj::parse_many(exceptions, ex_len, true)) {
+        if (ex.t != T::Obj || ex.str_or("kind") != "PolicyException") continue;
+        const Value* spec = ex.get("spec");
+        const Value* lst = spec ? spec->get("exceptions") : nullptr;
+        if (!lst || lst->t != T::Arr) continue;
+        for (auto& e : lst->a)
+          for (auto& rn : strs(e.get("ruleNames"))) excepted.insert({e.str_or("policyName"), rn});
+      }
+    }
     Cx c{*rs};
     for (auto& pol : docs) {
       if (pol.t != T::Obj) continue;
@@ -1283,6 +1296,8 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
         rm.name = r.str_or("name");
         rm.message = val ? val->str_or("message") : "";
         rm.policy = pidx;
+        rm.kinds = match_kinds(r.get("match"));
+        rm.has_validate = hasValidate;
         rm.message_vars = rm.message.find("{{") != std::string::npos || rm.message.find("$(") != std::string::npos;
         rd.policy = pidx;
         size_t mark_p = rs->pnodes.size(), mark_e = rs->pentries.size(), mark_l = rs->leaves.size(),
@@ -1294,6 +1309,8 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err) {
           rd.exclude = compile_block(c, r.get("exclude"), false, &em);
           rd.empty_may_match = em;
           std::string why = fallback_reason(r);
+          const std::string pkey = pm.ns.empty() ? pm.name : pm.ns + "/" + pm.name;  // cache.MetaNamespaceKeyFunc
+          if (why.empty() && excepted.count({pkey, rm.name})) why = "exception";
           c.nslots = 0;
           c.sites.clear();
           rd.pre = NONE;

@@ -894,6 +894,32 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
   for (auto x : bytes) out->alg_bytes += x;
 }
 
+// Reason a pair came back ST_FALLBACK (kyv_results_fallback_reason): the rule's compile-time reason, else the host
+// instantiation re-decides the one pair and reports the site that handed it over (KYV_WHY in kyv_eval.h / kyv_pss.h).
+std::string fallback_why(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule) {
+  if (rule >= rs.rules.size() || res >= b.hdr.size()) return "";
+  if (rs.rules[rule].kind == RK_FALLBACK) return rs.meta[rule].reason;
+  View v = make_view(rs, b, nullptr, nullptr, nullptr, nullptr);
+  Frame frames[MAX_DEPTH];
+  HostWalker wk{Stack{frames, 1, MAX_DEPTH}};
+  std::vector<FailRec> sink_recs;
+  HostSink sink{&sink_recs, 0};
+  const uint32_t* gate = v.gate + (size_t)v.hdr[res].kclass * v.gate_words;
+  uint32_t pf = 0;
+  g_fb_why = FBW_NONE;
+  const uint8_t st = eval_pair(v, ((gate[rule >> 5] >> (rule & 31)) & 1u) != 0, res, rule, wk, &pf, sink);
+  if ((st & 7) != ST_FALLBACK) return "";
+  switch (g_fb_why) {
+    case FBW_MATCH: return "match block outside the device subset";
+    case FBW_PHRASE: return "resource string contains an anchor-error phrase (error classified by substring)";
+    case FBW_COND: return "condition operand outside the device subset";
+    case FBW_DEPTH: return "pattern walk deeper than the device frame stack";
+    case FBW_VALUE: return "value outside the device subset (quantity beyond int128 nano units)";
+    case FBW_META: return "anchor-like key under metadata (wildcard expansion)";
+    default: return "pattern walk outside the device subset";
+  }
+}
+
 void free_device_images(Ruleset& rs, Batch* b) {
   if (b) {
     for (auto* p : b->dev)

@@ -49,6 +49,18 @@ KYV_HD void touch_row(uint32_t i) {
 }
 #endif
 
+// Why a pair was handed to the CPU engine (kyv_results_fallback_reason): the host instantiation records the site
+// of the last ST_FALLBACK it produced; the device build compiles the hook away (the reason is recomputed on the host
+// for the pairs a caller asks about).
+enum FallbackWhy : int { FBW_NONE = 0, FBW_MATCH = 1, FBW_PHRASE = 2, FBW_COND = 3, FBW_DEPTH = 4, FBW_VALUE = 5,
+                         FBW_META = 6 };
+inline thread_local int g_fb_why = FBW_NONE;
+#if defined(__HIP_DEVICE_COMPILE__)
+#define KYV_WHY(c) ((void)0)
+#else
+#define KYV_WHY(c) (::kyv::g_fb_why = (c))
+#endif
+
 // node table of one resource (rows relative to its root)
 struct NodeTab {
   const Node* p;
@@ -605,9 +617,9 @@ KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const 
         }
         if (P.flags & PF_META) {
           uint8_t o = expand_meta(v, v.metas[rd.meta_sites + P.meta], R, ern, h, keys);
-          if (o != ST_NONE) { out.status = o; return; }
+          if (o != ST_NONE) { if (o == ST_FALLBACK) KYV_WHY(FBW_META); out.status = o; return; }
         }
-        if (sp >= stk.cap) { out.status = ST_FALLBACK; return; }
+        if (sp >= stk.cap) { KYV_WHY(FBW_DEPTH); out.status = ST_FALLBACK; return; }
         Frame& f = stk.at(sp++);
         f.kind = F_MAP; f.pn = epn; f.rn = ern; f.i = 0; f.j = 0; f.st = 0;
         action = 1;
@@ -622,7 +634,7 @@ KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const 
         } else {
           okv = leaf_match(v, L, value_of(v, R, ern), &fb);
         }
-        if (fb) { out.status = ST_FALLBACK; return; }
+        if (fb) { KYV_WHY(FBW_VALUE); out.status = ST_FALLBACK; return; }
         ret = okv ? ok_ret() : mkerr(EC_NONE, 0, P.tmpl);
         action = 2;
         continue;
@@ -635,13 +647,13 @@ KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const 
         const Node& A = R[ern];
         bool okv = true;
         for (uint32_t i = 0; i < A.b && okv; i++) okv = leaf_match(v, L, value_of(v, R, A.a + i), &fb);
-        if (fb) { out.status = ST_FALLBACK; return; }
+        if (fb) { KYV_WHY(FBW_VALUE); out.status = ST_FALLBACK; return; }
         ret = okv ? ok_ret() : mkerr(EC_NONE, 0, P.tmpl);
         action = 2;
         continue;
       }
       if (P.kind == P_ARR_POS && R[ern].b < P.n) { ret = mkerr(EC_NONE, 0, NONE); action = 2; continue; }
-      if (sp >= stk.cap) { out.status = ST_FALLBACK; return; }
+      if (sp >= stk.cap) { KYV_WHY(FBW_DEPTH); out.status = ST_FALLBACK; return; }
       Frame& f = stk.at(sp++);
       f.kind = P.kind == P_ARR_MAPS ? F_AOM : F_POS;
       f.pn = epn; f.rn = ern; f.i = 0; f.j = 0; f.st = 0;
@@ -676,7 +688,7 @@ KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const 
           case H_EXISTENCE: case H_EXIST_BADPAT:
             if (c == NONE) continue;
             if (node_type(R[c]) != N_ARR || E.handler == H_EXIST_BADPAT) { ret = mkerr(EC_NONE, 0, E.tmpl); sp--; action = 2; continue; }
-            if (sp >= stk.cap) { out.status = ST_FALLBACK; return; }
+            if (sp >= stk.cap) { KYV_WHY(FBW_DEPTH); out.status = ST_FALLBACK; return; }
             {
               Frame& g = stk.at(sp++);
               g.kind = F_EXIST; g.pn = P.first + f.i - 1; g.rn = c; g.i = 0; g.j = 0; g.st = 0;

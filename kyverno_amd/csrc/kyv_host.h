@@ -43,6 +43,10 @@ struct RuleMeta {
   struct MsgPart { std::string text; std::vector<uint32_t> segs; bool var = false; };
   std::vector<MsgPart> msg_parts;
   bool msg_whole_var = false;
+  // MatchResources.GetKinds of the (autogen-expanded) rule and Rule.HasValidate: the policy cache's kind index
+  // (pkg/policycache/store.go:96-138)
+  std::vector<std::string> kinds;
+  bool has_validate = false;
 };
 
 // host-side text of a condition's references, for error messages (vars.go:395-399)
@@ -154,7 +158,10 @@ struct Results {
 };
 
 // compiler / flattener entry points
-Ruleset* compile_ruleset(const char* json, size_t len, std::string* err);
+// exceptions: PolicyException documents (kyverno.io/v2alpha1) or null; a rule named by an exception
+// (PolicyException.Contains, api/kyverno/v2alpha1/policy_exception_types.go:101) is handed to the CPU engine
+Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const char* exceptions = nullptr,
+                         size_t ex_len = 0);
 Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* nsl_json, size_t nsl_len, int threads,
                    std::string* err);
 void derive_strings(Batch& b, size_t from, int threads);

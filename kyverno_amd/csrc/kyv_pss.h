@@ -498,7 +498,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
   const RuleDesc& rd = v.rules[k];
   uint8_t st = ST_NONE;
   if (!active) return st;
-  if (rd.match.mode == MM_NONE) return ST_FALLBACK;  // match program could not be compiled
+  if (rd.match.mode == MM_NONE) return KYV_WHY(FBW_MATCH), ST_FALLBACK;  // match program could not be compiled
   const ResHeader& h = v.hdr[r];
   NodeTab R{v.nodes + h.root};
   LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
@@ -515,7 +515,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
   uint32_t ec, es, eg;
   if (rd.pre != NONE) {  // checkPreconditions (validation.go:281-288)
     int c = eval_prog(v, R, rd.pre, &ec, &es, &eg);
-    if (c == CR_FB) return ST_FALLBACK;
+    if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
     if (c == CR_PANIC) return ST_PANIC;
     if (c == CP_ERROR) return ST_ERROR | ST_MARK_PRE;
     if (c == CR_FALSE) return ST_SKIP | ST_MARK_PRE;
@@ -525,14 +525,14 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
     case RK_ERROR: return ST_ERROR;
     case RK_DENY: {  // validateDeny (validation.go:437-464)
       int c = eval_prog(v, R, rd.root, &ec, &es, &eg);
-      if (c == CR_FB) return ST_FALLBACK;
+      if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
       if (c == CR_PANIC) return ST_PANIC;
       if (c == CP_ERROR) return ST_ERROR;
       return c == CR_TRUE ? ST_FAIL : ST_PASS;
     }
     case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
     case RK_PATTERN: case RK_ANYPATTERN:
-      if (h.flags & RF_MAGIC) return ST_FALLBACK;
+      if (h.flags & RF_MAGIC) return KYV_WHY(FBW_PHRASE), ST_FALLBACK;
       *walk = true;
       return ST_NONE;
     default: return ST_NONE;

@@ -28,20 +28,29 @@ def _dumps(x):
 
 
 class Ruleset:
-    def __init__(self, policies):
-        """policies: list of ClusterPolicy/Policy dicts (or JSON text)."""
+    def __init__(self, policies, exceptions=None):
+        """policies: list of ClusterPolicy/Policy dicts (or JSON text); exceptions: PolicyException documents
+        (rules they name are handed to the CPU engine, reason "exception")."""
         L = K.lib()
         data = _dumps(policies if not isinstance(policies, dict) else [policies])
+        ex = _dumps(exceptions) if exceptions else None
         h = ctypes.c_void_p()
         opts = K.CompileOpts(K.KYV_ABI_VERSION, 0)
-        K.check(L.kyv_ruleset_compile(data, len(data), ctypes.byref(opts), ctypes.byref(h)))
+        K.check(L.kyv_ruleset_compile_ex(data, len(data), ex, len(ex) if ex else 0, ctypes.byref(opts), ctypes.byref(h)))
         self.h = h
         self.rules = []
         for k in range(L.kyv_ruleset_num_rules(h)):
             ri = K.RuleInfo()
             K.check(L.kyv_ruleset_rule_info(h, k, ctypes.byref(ri)))
+            kb = ctypes.create_string_buffer(4096)
+            hv = ctypes.c_int32(0)
+            n = L.kyv_ruleset_rule_kinds(h, k, kb, len(kb), ctypes.byref(hv))
+            if n >= len(kb):
+                kb = ctypes.create_string_buffer(n + 1)
+                L.kyv_ruleset_rule_kinds(h, k, kb, len(kb), ctypes.byref(hv))
+            kinds = kb.value.decode().split("\n") if n > 0 else []
             self.rules.append({"name": ri.name.decode(), "policy": ri.policy, "kind": K.RULE_KINDS.get(ri.kind, "?"),
-                               "reason": ri.reason.decode()})
+                               "reason": ri.reason.decode(), "match_kinds": kinds, "has_validate": bool(hv.value)})
         self.policies = []
         for p in range(L.kyv_ruleset_num_policies(h)):
             pi = K.PolicyInfo()
@@ -128,6 +137,14 @@ class Results:
     def path(self, res, rule):
         buf = ctypes.create_string_buffer(4096)
         K.lib().kyv_results_path(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
+        return buf.value.decode(errors="replace")
+
+    def fallback_reason(self, res, rule):
+        """why pair (res, rule) is KYV_ST_FALLBACK ("" otherwise)"""
+        buf = ctypes.create_string_buffer(512)
+        n = K.lib().kyv_results_fallback_reason(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
+        if n < 0:
+            raise K.KyvError(K.lib().kyv_last_error().decode(errors="replace"))
         return buf.value.decode(errors="replace")
 
     def pss_mask(self, res, rule):

@@ -37,9 +37,11 @@ class BackgroundScan:
         self.ruleset = E.Ruleset(self.policies)
         self.backend, self.device = backend, device
         self.meta = []
-        by_name = {(p.get("metadata") or {}).get("name"): p for p in self.policies}
+        # keyed like the policy cache (namespace, name): namespaced Policies may share a name across namespaces
+        by_key = {((p.get("metadata") or {}).get("namespace") or "" if p.get("kind") == "Policy" else "",
+                   (p.get("metadata") or {}).get("name")): p for p in self.policies}
         for pm in self.ruleset.policies:
-            pol = by_name.get(pm["name"]) or {}
+            pol = by_key.get((pm["namespace"], pm["name"])) or {}
             ann = (pol.get("metadata") or {}).get("annotations") or {}
             sev = ann.get("policies.kyverno.io/severity", "")
             self.meta.append({

@@ -145,35 +145,83 @@ def oracle_engine(policy, rq):
     return [{"name": r["name"], "status": r["status"], "message": r["message"]} for p in pr for r in p["rules"]]
 
 
+def _gvk_kind(gvk):
+    """pkg/policycache/store.go computeKind (GetKindFromGVK + SplitSubresource), restated for the test"""
+    parts = gvk.split("/")
+    ver = lambda x: x == "*" or any(x[i] == "v" and x[i + 1].isdigit() for i in range(len(x) - 1))
+    if len(parts) == 2:
+        k = parts[1].replace(".", "/", 1) if ver(parts[0]) else parts[0] + "/" + parts[1]
+    elif len(parts) == 3:
+        k = parts[1] + "/" + parts[2] if ver(parts[0]) else parts[2].replace(".", "/", 1)
+    elif len(parts) == 4:
+        k = parts[2] + "/" + parts[3]
+    else:
+        k = gvk.replace(".", "/", 1)
+    sp = k.split("/")
+    return sp[0] if len(sp) == 2 else k
+
+
+class PolicyCache:
+    """Independent policy cache for the test (pkg/policycache/store.go:96-170, cache.go:38-88): kinds come from the
+    oracle's ComputeRules, not from the library."""
+
+    def __init__(self, policies):
+        self.entries = []
+        for p in policies:
+            s = p.get("spec") or {}
+            enforce = A.action_enforce(s.get("validationFailureAction", "Audit")) or any(
+                A.action_enforce((o or {}).get("action")) for o in s.get("validationFailureActionOverrides") or [])
+            kinds = set()
+            for r in O.compute_rules(p):
+                if r.get("validate"):
+                    m = r.get("match") or {}
+                    ks = list((m.get("resources") or {}).get("kinds") or [])
+                    for b in (m.get("any") or []) + (m.get("all") or []):
+                        ks += (b.get("resources") or {}).get("kinds") or []
+                    kinds.update(_gvk_kind(k) for k in ks)
+            ns = (p.get("metadata") or {}).get("namespace", "") if p.get("kind") == "Policy" else ""
+            self.entries.append((p, ns, kinds, enforce))
+
+    def get_enforce(self, kind, ns):
+        out = []
+        for scope in [""] + ([ns] if ns else []):
+            for key in (_gvk_kind(kind), "*"):
+                for p, pns, kinds, enf in self.entries:
+                    if enf and pns == scope and key in kinds and A.keep_for_enforce(p, ns):
+                        out.append(p)
+        return out
+
+
 def per_request_decisions(batcher, reqs):
-    """Reference shape: every enforce policy of every request through the CPU engine, one request at a time"""
+    """Reference shape: the enforce policies of every request (independent kind-indexed policy cache) through the CPU
+    engine, one request at a time"""
     out = []
+    cache = PolicyCache(batcher.policies)
     for rq in reqs:
         new, old = rq.get("object") or {}, rq.get("oldObject") or {}
         dts = A._meta(old).get("deletionTimestamp") if new else A._meta(new).get("deletionTimestamp")
         if dts is not None and rq["operation"] == "UPDATE":
             out.append((True, "", None))
             continue
-        pols = batcher.enforce_policies(rq.get("namespace") or "")
+        pols = cache.get_enforce(rq.get("kind", ""), rq.get("namespace") or "")
         if not pols:
             out.append((True, "", None))
             continue
         md = A._meta(new)
         resource = (new.get("kind", ""), md.get("namespace", ""), md.get("name", ""))
         fp, ers = "Ignore", []
-        for pi in pols:
-            p = batcher.pol[pi]
-            if p["fail_policy"] == "Fail":
+        for p in pols:
+            if ((p.get("spec") or {}).get("failurePolicy") or "Fail") == "Fail":
                 fp = "Fail"
-            ers.append({"policy": p["name"], "rules": oracle_engine(p["doc"], rq), "resource": resource,
-                        "action": A.response_action(p["doc"], resource[1], rq.get("namespace_labels"))})
+            ers.append({"policy": p["metadata"]["name"], "rules": oracle_engine(p, rq), "resource": resource,
+                        "action": A.response_action(p, resource[1], rq.get("namespace_labels"))})
         allowed, msg, warns, _ = A.decide(ers, fp)
         out.append((allowed, msg, warns))
     return out
 
 
-def check_admission(backend, n, max_batch):
-    pols = admission_policies()
+def check_admission(backend, n, max_batch, pols=None):
+    pols = pols or admission_policies()
     reqs = admission_requests(n)
     b = A.AdmissionBatcher(pols, backend=backend, cpu_engine=oracle_engine, max_batch=max_batch)
     got = []
@@ -222,6 +270,57 @@ def test_admission_routing_without_cpu_engine():
                            "oldObject": pod}])
     assert out[0]["allowed"] is None and out[0]["cpu_pending"] == ["ui"]
     assert out[1]["allowed"] is None
+
+
+def test_admission_pss_and_quirks_enforce():
+    """PodSecurity and quirk policies under Enforce: device pairs whose message the library cannot render (PSS
+    failures, skip / error texts) send the whole policy to the CPU engine instead of failing the batch"""
+    pols = []
+    for p in [c[1] for c in cases.pss_cases()[:6]] + cases.quirk_policies():
+        p = copy.deepcopy(p)
+        p["spec"]["validationFailureAction"] = "Enforce"
+        pols.append(p)
+    check_admission("cpu", 200, 64, pols=pols)
+
+
+def test_admission_failure_policy_is_kind_indexed():
+    """policycache.GetPolicies(ValidateEnforce, kind, ns) decides failurePolicy: a default-Fail policy matching only
+    Deployments must not turn a Pod's error under an Ignore policy into a block (validation.go:105-114)"""
+    dep_only = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "dep-only"},
+                "spec": {"validationFailureAction": "Enforce", "rules": [{
+                    "name": "r", "match": {"any": [{"resources": {"kinds": ["apps/v1/Deployment"]}}]},
+                    "validate": {"pattern": {"metadata": {"labels": {"a": "?*"}}}}}]}}
+    erring = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "erring"},
+              "spec": {"validationFailureAction": "Enforce", "failurePolicy": "Ignore", "rules": [{
+                  "name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                  "validate": {"anyPattern": {"spec": {"x": "1"}}}}]}}
+    b = A.AdmissionBatcher([dep_only, erring], backend="cpu", cpu_engine=oracle_engine)
+    assert b.enforce_policies("d", "Pod") == [1]
+    assert b.enforce_policies("d", "Deployment") == [0, 1]  # erring's autogen rule covers Deployments
+    assert b.enforce_policies("d", "ConfigMap") == []
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "d"}, "spec": {"x": "2"}}
+    out = b.handle_batch([{"uid": "1", "operation": "CREATE", "kind": "Pod", "namespace": "d", "object": pod}])
+    want = per_request_decisions(b, [{"uid": "1", "operation": "CREATE", "kind": "Pod", "namespace": "d",
+                                      "object": pod}])
+    assert (out[0]["allowed"], out[0]["message"], out[0]["warnings"]) == want[0]
+    assert out[0]["allowed"] is True and out[0]["warnings"]  # the error is a warning, not a block
+
+
+def test_admission_cancelled_future_does_not_stall():
+    pols = admission_policies()
+    reqs = admission_requests(40, seed=5)
+    b = A.AdmissionBatcher(pols, backend="cpu", cpu_engine=oracle_engine, max_batch=8, max_wait_ms=50.0).start()
+    try:
+        futs = [b.submit(rq) for rq in reqs]
+        for f in futs[::3]:
+            f.cancel()
+        left = [f for f in futs if not f.cancelled()]
+        got = [f.result(timeout=120) for f in left]
+        assert len(got) == len(left)
+        again = b.submit(reqs[0]).result(timeout=60)  # the batcher thread is still alive
+        assert again["uid"] == reqs[0]["uid"]
+    finally:
+        b.stop()
 
 
 @pytest.mark.gpu
