@@ -9,6 +9,8 @@
 // register footprint is what that pattern needs. The same walk-phase pieces (pair_walk, walk_chunks,
 // leaf matching) are shared with the interpreted kernel, and parity tests run both against the oracle.
 #include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -443,6 +445,12 @@ std::string self_dir() {
 std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
   Gen g(rs);
   jit_rules->assign(rs.rules.size(), 0);
+  // one generated function tree per pattern: rulesets with thousands of pattern rules (C4: 10k policies) would
+  // give a source too large to compile in useful time; they stay on the interpreted walk kernel
+  size_t npat = 0;
+  for (auto& rd : rs.rules) npat += rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN;
+  const size_t cap = getenv("KYV_JIT_MAX_RULES") ? (size_t)atol(getenv("KYV_JIT_MAX_RULES")) : 1024;
+  if (npat > cap) return "";
   std::vector<std::pair<uint32_t, std::vector<uint32_t>>> rule_roots;  // covered rule -> its pattern roots
   for (size_t k = 0; k < rs.rules.size(); k++) {
     const RuleDesc& rd = rs.rules[k];
@@ -520,6 +528,44 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
 
 std::vector<char> jit_compile_uncached(const std::string& src, double* seconds);
 
+namespace {
+uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+  for (unsigned char c : s) { h ^= c; h *= 1099511628211ull; }
+  return h;
+}
+std::string read_file(const std::string& path) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return "";
+  std::string out;
+  char buf[65536];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) out.append(buf, n);
+  fclose(f);
+  return out;
+}
+// On-disk code-object cache: a ruleset's walk kernel is compiled once per (generated source, device headers,
+// compile options) and reused by every later process (first evaluation seconds instead of a ~20 s hipRTC compile).
+// KYV_JIT_CACHE overrides the directory (default <library dir>/jitcache); "0" disables it.
+std::string cache_path(const std::string& src) {
+  const char* env = getenv("KYV_JIT_CACHE");
+  if (env && std::string(env) == "0") return "";
+  std::string dir = env ? std::string(env) : self_dir() + "/jitcache";
+  const char* cs = getenv("KYV_CSRC");
+  std::string csrc = cs ? std::string(cs) : self_dir() + "/csrc";
+  uint64_t h = fnv1a(src);
+  for (const char* hdr : {"kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_wave.h", "kyv_walk.h"})
+    h = fnv1a(read_file(csrc + "/" + hdr), h);
+  h = fnv1a(std::string("gfx950|O3|c++17|wpe=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4") + "|" +
+                (getenv("KYV_JIT_DEFS") ? getenv("KYV_JIT_DEFS") : "-DKYV_JIT_NOEXTRA"), h);
+  int maj = 0, min = 0;
+  hiprtcVersion(&maj, &min);
+  h = fnv1a(std::to_string(maj) + "." + std::to_string(min), h);
+  char name[64];
+  snprintf(name, sizeof name, "/walk-%016llx.co", (unsigned long long)h);
+  return dir + name;
+}
+}  // namespace
+
 // hipRTC compile of the generated source for gfx950 -> code object
 std::vector<char> jit_compile(const std::string& src, double* seconds) {
   // process-wide cache: identical rulesets (same generated source) compile once
@@ -530,7 +576,28 @@ std::vector<char> jit_compile(const std::string& src, double* seconds) {
     auto it = cache.find(src);
     if (it != cache.end()) { if (seconds) *seconds = 0; return it->second; }
   }
-  std::vector<char> code = jit_compile_uncached(src, seconds);
+  const std::string path = cache_path(src);
+  std::vector<char> code;
+  if (!path.empty()) {
+    std::string blob = read_file(path);
+    if (blob.size() > 64) {  // written whole (temp file + rename)
+      code.assign(blob.begin(), blob.end());
+      if (seconds) *seconds = 0;
+    }
+  }
+  if (code.empty()) {
+    code = jit_compile_uncached(src, seconds);
+    if (!path.empty()) {  // best effort: a read-only tree just recompiles next time
+      std::string dir = path.substr(0, path.rfind('/'));
+      mkdir(dir.c_str(), 0755);
+      std::string tmp = path + ".tmp" + std::to_string((unsigned long long)getpid());
+      if (FILE* f = fopen(tmp.c_str(), "wb")) {
+        bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
+        ok = fclose(f) == 0 && ok;
+        if (!ok || rename(tmp.c_str(), path.c_str()) != 0) remove(tmp.c_str());
+      }
+    }
+  }
   std::lock_guard<std::mutex> lk(mu);
   cache.emplace(src, code);
   return code;

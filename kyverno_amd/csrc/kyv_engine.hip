@@ -146,39 +146,49 @@ static void stream_put(int dev, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   g_streams_free.push_back(StreamSet{dev, s, e0, e1});
 }
 
-struct DeviceResults {
-  uint8_t* status = nullptr;
-  uint32_t* pss_fails = nullptr;
-  uint32_t* pss_slot = nullptr;
-  FailRec* recs = nullptr;
-  uint32_t* nrecs = nullptr;
-  FailRec* stage = nullptr;      // per-chunk staging of failing-path records (DevOut)
-  uint32_t* rbase = nullptr;
-  uint16_t* rcnt = nullptr;
-  uint32_t* tsum = nullptr;      // compaction tile sums / offsets
-  unsigned long long* counts = nullptr;
-  uint32_t max_recs = 0;
-  uint32_t npss = 0;
-  size_t nres = 0, nrules = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  View* view = nullptr;  // device copy of the View the kernel reads
-  // walk work lists (match_kernel -> walk_kernel): per rule a list of resource positions
-  WorkLists wl{};                // walk work lists (kyv_wave.h)
-  uint32_t* mrules = nullptr;    // rules match_kernel evaluates: all but the direct-walk ones (pattern + RD_GATE_EXACT)
+// One rule slice of an evaluation. Work lists, failing-path staging and compaction buffers are sized per (rule,
+// resource) pair, so a ruleset whose buffers would not fit (C4: 10k+ rules x 1M resources) is evaluated as
+// consecutive slices of its rule range [k0, k1) reusing one set of those buffers; verdict bytes, PSS masks and
+// counters stay global. A ruleset that fits (C3) is one slice.
+struct SliceSched {
+  uint32_t k0 = 0, k1 = 0;
+  size_t stage_tot = 0;          // staging slots (records) of the slice
+  uint32_t* rbase = nullptr;     // [k1 - k0] first staging slot of each rule (slice-local)
+  uint32_t* mrules = nullptr;    // rules of the slice match_kernel evaluates (direct-walk rules excluded)
   uint32_t nm = 0;
-  std::vector<uint64_t> cap;     // [nrules] work-list capacity (resources of the kind classes the gate admits)
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
   int jit_state = -1;            // what the schedules were laid out for (0 interpreter only, 1 with the jit kernel)
+};
+
+struct DeviceResults {
+  uint8_t* status = nullptr;
+  uint32_t* pss_fails = nullptr;
+  uint32_t* pss_slot = nullptr;
+  FailRec* recs = nullptr;       // compacted records of the current slice
+  uint32_t* nrecs = nullptr;
+  FailRec* stage = nullptr;      // per-chunk staging of failing-path records (DevOut), sized for the largest slice
+  uint16_t* rcnt = nullptr;
+  uint32_t* tsum = nullptr;      // compaction tile sums / offsets
+  unsigned long long* counts = nullptr;
+  size_t max_recs = 0;
+  uint32_t npss = 0;
+  size_t nres = 0, nrules = 0;
+  size_t max_slice_rules = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  View* view = nullptr;  // device copy of the View the kernel reads
+  WorkLists wl{};                // walk work lists (kyv_wave.h), slice-local rule index
+  std::vector<SliceSched> slices;
   int cus = 256;
 };
 
 static void free_dev_results(DeviceResults& d, int dev) {
   dfree(d.view); dfree(d.status); dfree(d.pss_fails); dfree(d.pss_slot); dfree(d.recs); dfree(d.nrecs); dfree(d.counts);
-  dfree(d.stage); dfree(d.rbase); dfree(d.rcnt); dfree(d.tsum);
-  dfree(d.wl.items); dfree(d.wl.cnt); dfree(d.sched); dfree(d.mrules);
+  dfree(d.stage); dfree(d.rcnt); dfree(d.tsum);
+  dfree(d.wl.items); dfree(d.wl.cnt);
+  for (auto& sl : d.slices) { dfree(sl.rbase); dfree(sl.mrules); dfree(sl.sched); }
   stream_put(dev, d.stream, d.e0, d.e1);
   d = DeviceResults();
 }
@@ -337,7 +347,7 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
     const unsigned long long wm = __ballot(walk);
     const RuleDesc& rdk = v.rules[k];
     if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {  // this wave's work list for rule k
-      const size_t list = (size_t)k * wl.nwaves + blockIdx.x;
+      const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + blockIdx.x;
       if (walk) {
         const ResHeader& h = v.hdr[r];
         wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
@@ -370,6 +380,7 @@ walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, ChunkMap cm, in
 //                        non-empty chunk's records cooperatively (lane i moves record i).
 __device__ __forceinline__ const FailRec* chunk_stage(const FailRec* stage, const uint32_t* rbase, const RuleDesc* rules,
                                                       uint32_t nwaves, size_t c) {
+  // c: slice-local chunk (rule k - k0, wave w); `rules` and `rbase` are offset to the slice
   const uint32_t k = (uint32_t)(c / nwaves), w = (uint32_t)(c % nwaves);
   const uint32_t alts = rules[k].kind == RK_PATTERN ? 1u : min(rules[k].nalts, (uint32_t)MAX_ALTS);
   return stage + rbase[k] + (size_t)w * WAVE * alts;
@@ -416,7 +427,7 @@ __global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict
 __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __restrict__ stage, const uint32_t* __restrict__ rbase,
                                                             const uint16_t* __restrict__ rcnt, const RuleDesc* __restrict__ rules,
                                                             uint32_t nwaves, size_t total, const uint32_t* __restrict__ tbase,
-                                                            FailRec* __restrict__ out, uint32_t max_out) {
+                                                            FailRec* __restrict__ out, size_t max_out) {
   const uint32_t lane = threadIdx.x;
   const size_t c = (size_t)blockIdx.x * WAVE + lane;
   const uint32_t n = c < total ? rcnt[c] : 0u;
@@ -555,6 +566,108 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   return true;
 }
 
+// Walk-buffer bytes one rule costs per resource: its work-list slot (8 B), failing-path staging and compacted
+// records (32 B each per anyPattern alternative), plus per-chunk counters.
+static size_t rule_slice_bytes(const RuleDesc& rd) {
+  const size_t alts = rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, MAX_ALTS) : 0;
+  return sizeof(uint2) + 2 * alts * sizeof(FailRec) + 1;
+}
+
+// Budget for the per-slice buffers: KYV_SLICE_MB, else half of the free device memory, at most 48 GiB.
+static size_t slice_budget() {
+  if (const char* e = getenv("KYV_SLICE_MB")) return (size_t)std::max(1, atoi(e)) << 20;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr == 0) fr = (size_t)64 << 30;
+  return std::min<size_t>(fr / 2, (size_t)48 << 30);
+}
+
+// Lay out the chunk schedules of one slice's walk kernels (see ChunkMap): runs of match waves with equal gated rule
+// sets, wave-major within a run, whole waves placed on one XCD.
+static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset* dr, DeviceResults& d, SliceSched& sl,
+                            bool jit) {
+  const size_t nres = d.nres;
+  const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)std::max(1, atoi(getenv("KYV_WIN"))) : 0xFFFFu;
+  const uint32_t nw = d.wl.nwaves, gw = b.gate_words;
+  std::vector<std::pair<uint32_t, std::vector<uint32_t>>> runs;  // (first wave, gate words)
+  for (uint32_t w = 0; w < nw; w++) {
+    std::vector<uint32_t> g(gw, 0);
+    for (size_t r = (size_t)w * WAVE; r < std::min(nres, (size_t)(w + 1) * WAVE); r++)
+      for (uint32_t i = 0; i < gw; i++) g[i] |= b.gate[(size_t)b.hdr[r].kclass * gw + i];
+    if (runs.empty() || runs.back().second != g) runs.push_back({w, std::move(g)});
+  }
+  const uint32_t ncls = 1 + (jit ? (uint32_t)dr->jfns.size() : 0u);  // 0: interpreter, 1 + g: compiled group g
+  std::vector<std::vector<uint2>> slots(ncls);
+  for (size_t ri = 0; ri < runs.size(); ri++) {
+    const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
+    std::vector<std::vector<uint32_t>> ks(ncls);
+    for (uint32_t k = sl.k0; k < sl.k1; k++) {
+      if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
+      if (!((runs[ri].second[k / 32] >> (k % 32)) & 1u)) continue;
+      ks[jit ? rs.jit_rules[k] : 0].push_back(k);
+    }
+    for (uint32_t cls = 0; cls < ncls; cls++)
+      for (size_t i = 0; i < ks[cls].size(); i += WIN) {
+        const size_t n = std::min<size_t>(WIN, ks[cls].size() - i);
+        for (uint32_t w = wb; w < we; w++)
+          for (size_t t = i; t < i + n; t++) slots[cls].push_back(make_uint2(ks[cls][t], w));
+      }
+  }
+  size_t tot = 0;
+  sl.grid.assign(ncls, 0);
+  const bool xcd = !getenv("KYV_XCD") || atoi(getenv("KYV_XCD")) != 0;
+  for (uint32_t cls = 0; cls < ncls; cls++) {
+    if (slots[cls].size() > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
+    // walk grid: up to 1024 one-wave workgroups per CU, grid-stride beyond that. Measured on C3 (kernel ms):
+    // 16/CU 3.03, 64/CU 2.95, 128/CU 2.88, 256/CU 2.78, 512/CU 2.70, 1024/CU 2.66, 2048/CU 2.74, one per chunk 2.75
+    // (more resident-or-queued waves hide the walk's dependent-load latency; KYV_GRID overrides)
+    static const size_t gmul = getenv("KYV_GRID") ? (size_t)std::max(1, atoi(getenv("KYV_GRID"))) : 1024;
+    sl.grid[cls] = (uint32_t)std::min<size_t>(slots[cls].size(), (size_t)d.cus * gmul);
+    tot += slots[cls].size();
+    // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs (block b and b + 8 share one L2),
+    // and the grid-stride loop hands position p to block p % G. The chunks of one match wave (the same 64
+    // resources under its rules) are kept on ONE XCD, so its L2 serves the resources' rows to every rule; whole
+    // waves go to the XCD with the least work so far (balance), in schedule order.
+    const size_t T = slots[cls].size(), G = sl.grid[cls];
+    if (xcd && G >= 8 && T > G) {
+      std::vector<std::vector<uint32_t>> pos(8);
+      for (size_t q = 0; q < T; q++) pos[(q % G) % 8].push_back((uint32_t)q);
+      std::vector<uint2> outv(T);
+      size_t fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (size_t i = 0; i < T;) {
+        size_t j = i;
+        while (j < T && slots[cls][j].y == slots[cls][i].y) j++;  // one wave's chunks
+        int best = -1;
+        double br = 2.0;
+        for (int x = 0; x < 8; x++) {
+          if (fill[x] >= pos[x].size()) continue;
+          double r = (double)fill[x] / (double)pos[x].size();
+          if (r < br) { br = r; best = x; }
+        }
+        for (size_t t = i; t < j; t++) {
+          int x = best;
+          if (fill[x] >= pos[x].size())  // XCD full: next XCD with room
+            for (int y = 0; y < 8; y++) if (fill[y] < pos[y].size()) { x = y; break; }
+          outv[pos[x][fill[x]++]] = slots[cls][t];
+        }
+        i = j;
+      }
+      slots[cls].swap(outv);
+    }
+  }
+  dfree(sl.sched);
+  sl.sched = nullptr;
+  HIP_OK(dmalloc(&sl.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
+  sl.cm.assign(ncls, ChunkMap{nullptr, 0});
+  size_t at = 0;
+  for (uint32_t cls = 0; cls < ncls; cls++) {
+    if (!slots[cls].empty())
+      HIP_OK(hipMemcpy(sl.sched + at, slots[cls].data(), slots[cls].size() * sizeof(uint2), hipMemcpyHostToDevice));
+    sl.cm[cls] = ChunkMap{sl.sched + at, (uint32_t)slots[cls].size()};
+    at += slots[cls].size();
+  }
+  sl.jit_state = (int)jit;
+}
+
 void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back,
               int jit_mode) {
   int ndev = 0;
@@ -572,61 +685,71 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   View v = make_view(rs, b, dr->base, dr, db->base, db);
   size_t nres = b.hdr.size(), nrules = rs.rules.size();
   if (!db->out) {
-    // one record per failing pattern / anyPattern alternative at most: exact upper bound, no overflow
-    size_t per_res = 0;
-    for (auto& rd : rs.rules)
-      per_res += rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, RECS_PER_PAIR) : 0;
     auto* dd = new DeviceResults();
     DeviceResults& d = *dd;
     d.nres = nres;
     d.nrules = nrules;
     std::vector<uint32_t> pss_slot(nrules, NONE);
     for (size_t k = 0; k < nrules; k++) if (rs.rules[k].kind == RK_PSS) pss_slot[k] = d.npss++;
-    size_t mr = std::max<size_t>(nres * per_res, 1);
-    if (mr > 0xFFFFFFF0u) throw std::runtime_error("batch too large for one failure-record buffer");
-    d.max_recs = (uint32_t)mr;
     HIP_OK(dmalloc(&d.status, std::max<size_t>(1, nres * nrules)));
     HIP_OK(dmalloc(&d.pss_fails, std::max<size_t>(4, (size_t)d.npss * nres * 4)));
     HIP_OK(dmalloc(&d.pss_slot, std::max<size_t>(4, nrules * 4)));
-    HIP_OK(dmalloc(&d.recs, (size_t)d.max_recs * sizeof(FailRec)));
     HIP_OK(dmalloc(&d.nrecs, 4));
-    {  // staging: chunk (k, w) owns 64 * alts(k) slots
-      const size_t nwv = (nres + WAVE - 1) / WAVE;
-      std::vector<uint32_t> rb(std::max<size_t>(nrules, 1), 0);
-      size_t tot = 0;
-      for (size_t k = 0; k < nrules; k++) {
-        rb[k] = (uint32_t)tot;
-        const RuleDesc& rd = rs.rules[k];
-        size_t alts = rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, MAX_ALTS) : 0;
-        tot += alts * nwv * WAVE;
-        if (tot > 0xFFFFFFF0ull) throw std::runtime_error("batch too large for one failure-record staging buffer");
-      }
-      HIP_OK(dmalloc(&d.stage, std::max<size_t>(tot, 1) * sizeof(FailRec)));
-      HIP_OK(dmalloc(&d.rbase, rb.size() * 4));
-      HIP_OK(hipMemcpy(d.rbase, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
-      HIP_OK(dmalloc(&d.rcnt, std::max<size_t>(nrules * nwv, 1) * 2));
-      HIP_OK(dmalloc(&d.tsum, std::max<size_t>((nrules * nwv + WAVE - 1) / WAVE, 1) * 4));
-    }
     HIP_OK(dmalloc(&d.counts, std::max<size_t>(1, nrules) * NSTATUS * 8));
     HIP_OK(hipMemcpy(d.pss_slot, pss_slot.data(), nrules * 4, hipMemcpyHostToDevice));
     stream_get(&d.stream, &d.e0, &d.e1);
     HIP_OK(dmalloc(&d.view, sizeof(View)));
     HIP_OK(hipMemcpy(d.view, &v, sizeof(View), hipMemcpyHostToDevice));
-    // walk work lists: one 64-slot list per (rule, match wave)
     d.wl.nwaves = (uint32_t)((nres + WAVE - 1) / WAVE);
-    {
-      std::vector<uint32_t> ml;
-      for (size_t k = 0; k < nrules; k++) {
+    const size_t nwv = d.wl.nwaves;
+    // rule slices: consecutive rules while their walk buffers fit the budget (and every slice-local index fits 32 bits)
+    const size_t budget = slice_budget();
+    for (size_t k = 0; k < nrules || (nrules == 0 && d.slices.empty());) {
+      SliceSched sl;
+      sl.k0 = (uint32_t)k;
+      size_t bytes = 0, stage = 0;
+      while (k < nrules) {
         const RuleDesc& rd = rs.rules[k];
-        const bool direct = (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) && (rd.flags & RD_GATE_EXACT);
-        if (!direct) ml.push_back((uint32_t)k);
+        const size_t cost = rule_slice_bytes(rd) * nwv * WAVE + nwv * 2;
+        const size_t alts = rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, MAX_ALTS) : 0;
+        const size_t st2 = stage + alts * nwv * WAVE;
+        const size_t nk = k + 1 - sl.k0;
+        if (k > sl.k0 && (bytes + cost > budget || st2 > 0xFFFFFFF0ull || nk * nwv > 0xFFFFFFF0ull)) break;
+        if (st2 > 0xFFFFFFF0ull) throw std::runtime_error("batch too large for one rule's failure-record staging");
+        bytes += cost;
+        stage = st2;
+        k++;
       }
-      d.nm = (uint32_t)ml.size();
-      HIP_OK(dmalloc(&d.mrules, std::max<size_t>(1, ml.size()) * 4));
-      if (!ml.empty()) HIP_OK(hipMemcpy(d.mrules, ml.data(), ml.size() * 4, hipMemcpyHostToDevice));
+      sl.k1 = (uint32_t)k;
+      sl.stage_tot = stage;
+      std::vector<uint32_t> rb(std::max<size_t>(sl.k1 - sl.k0, 1), 0);
+      size_t tot = 0;
+      std::vector<uint32_t> ml;
+      for (uint32_t q = sl.k0; q < sl.k1; q++) {
+        const RuleDesc& rd = rs.rules[q];
+        rb[q - sl.k0] = (uint32_t)tot;
+        tot += (rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, MAX_ALTS) : 0) * nwv * WAVE;
+        const bool direct = (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) && (rd.flags & RD_GATE_EXACT);
+        if (!direct) ml.push_back(q);
+      }
+      HIP_OK(dmalloc(&sl.rbase, rb.size() * 4));
+      HIP_OK(hipMemcpy(sl.rbase, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
+      sl.nm = (uint32_t)ml.size();
+      HIP_OK(dmalloc(&sl.mrules, std::max<size_t>(1, ml.size()) * 4));
+      if (!ml.empty()) HIP_OK(hipMemcpy(sl.mrules, ml.data(), ml.size() * 4, hipMemcpyHostToDevice));
+      d.max_slice_rules = std::max<size_t>(d.max_slice_rules, sl.k1 - sl.k0);
+      d.max_recs = std::max<size_t>(d.max_recs, std::max<size_t>(sl.stage_tot, 1));
+      d.slices.push_back(std::move(sl));
+      if (nrules == 0) break;
     }
-    HIP_OK(dmalloc(&d.wl.items, std::max<size_t>(1, nrules * (size_t)d.wl.nwaves * WAVE) * sizeof(uint2)));
-    HIP_OK(dmalloc(&d.wl.cnt, std::max<size_t>(4, nrules * (size_t)d.wl.nwaves + 4)));
+    const size_t msr = std::max<size_t>(d.max_slice_rules, 1);
+    HIP_OK(dmalloc(&d.stage, d.max_recs * sizeof(FailRec)));
+    HIP_OK(dmalloc(&d.recs, d.max_recs * sizeof(FailRec)));
+    HIP_OK(dmalloc(&d.rcnt, std::max<size_t>(msr * nwv, 1) * 2));
+    HIP_OK(dmalloc(&d.tsum, std::max<size_t>((msr * nwv + WAVE - 1) / WAVE, 1) * 4));
+    // walk work lists: one 64-slot list per (slice rule, match wave)
+    HIP_OK(dmalloc(&d.wl.items, std::max<size_t>(1, msr * nwv * WAVE) * sizeof(uint2)));
+    HIP_OK(dmalloc(&d.wl.cnt, std::max<size_t>(4, msr * nwv + 4)));
     // persistent grid: enough waves to fill the chip several times over, never more than the chunks
     // CU count per device, queried once (hipGetDeviceProperties costs milliseconds per call)
     static std::mutex cu_mu;
@@ -649,134 +772,67 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   hipStream_t stream = d.stream;
   const bool use_jit = jit_mode == JIT_ON || (jit_mode == JIT_AUTO && nres >= JIT_AUTO_MIN_RESOURCES);
   const bool jit = use_jit && ensure_jit(mrs, dr);
-  if (d.jit_state != (int)jit) {  // lay out the two walk schedules (see ChunkMap)
-    // rules per window: all of a wave's rules back to back (wave-major) measured best together with the XCD
-    // placement below (C3 walk 3.94 ms rule-major -> 3.47 ms; windows of 2-8 rules were slower than either)
-    const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)std::max(1, atoi(getenv("KYV_WIN"))) : 0xFFFFu;
-    const uint32_t nw = d.wl.nwaves, gw = b.gate_words;
-    // gated rule set of every match wave (union over the kind classes of its lanes), as runs of equal sets
-    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> runs;  // (first wave, gate words)
-    for (uint32_t w = 0; w < nw; w++) {
-      std::vector<uint32_t> g(gw, 0);
-      for (size_t r = (size_t)w * WAVE; r < std::min(nres, (size_t)(w + 1) * WAVE); r++)
-        for (uint32_t i = 0; i < gw; i++) g[i] |= b.gate[(size_t)b.hdr[r].kclass * gw + i];
-      if (runs.empty() || runs.back().second != g) runs.push_back({w, g});
-    }
-    const uint32_t ncls = 1 + (jit ? (uint32_t)dr->jfns.size() : 0u);  // 0: interpreter, 1 + g: compiled group g
-    std::vector<std::vector<uint2>> slots(ncls);
-    for (size_t ri = 0; ri < runs.size(); ri++) {
-      const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
-      std::vector<std::vector<uint32_t>> ks(ncls);
-      for (size_t k = 0; k < nrules; k++) {
-        if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
-        if (!((runs[ri].second[k / 32] >> (k % 32)) & 1u)) continue;
-        ks[jit ? rs.jit_rules[k] : 0].push_back((uint32_t)k);
-      }
-      for (uint32_t cls = 0; cls < ncls; cls++)
-        for (size_t i = 0; i < ks[cls].size(); i += WIN) {
-          const size_t n = std::min<size_t>(WIN, ks[cls].size() - i);
-          for (uint32_t w = wb; w < we; w++)
-            for (size_t t = i; t < i + n; t++) slots[cls].push_back(make_uint2(ks[cls][t], w));
-        }
-    }
-    size_t tot = 0;
-    d.grid.assign(ncls, 0);
-    const bool xcd = !getenv("KYV_XCD") || atoi(getenv("KYV_XCD")) != 0;
-    for (uint32_t cls = 0; cls < ncls; cls++) {
-      if (slots[cls].size() > 0xFFFFFFF0ull) throw std::runtime_error("walk schedule exceeds 2^32 chunks; split the batch");
-      // walk grid: up to 1024 one-wave workgroups per CU, grid-stride beyond that. Measured on C3 (kernel ms):
-      // 16/CU 3.03, 64/CU 2.95, 128/CU 2.88, 256/CU 2.78, 512/CU 2.70, 1024/CU 2.66, 2048/CU 2.74, one per chunk 2.75
-      // (more resident-or-queued waves hide the walk's dependent-load latency; KYV_GRID overrides)
-      static const size_t gmul = getenv("KYV_GRID") ? (size_t)std::max(1, atoi(getenv("KYV_GRID"))) : 1024;
-      d.grid[cls] = (uint32_t)std::min<size_t>(slots[cls].size(), (size_t)d.cus * gmul);
-      tot += slots[cls].size();
-      // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs (block b and b + 8 share one L2),
-      // and the grid-stride loop hands position p to block p % G. The chunks of one match wave (the same 64
-      // resources under its rules) are kept on ONE XCD, so its L2 serves the resources' rows to every rule; whole
-      // waves go to the XCD with the least work so far (balance), in schedule order.
-      const size_t T = slots[cls].size(), G = d.grid[cls];
-      if (xcd && G >= 8 && T > G) {
-        std::vector<std::vector<uint32_t>> pos(8);
-        for (size_t q = 0; q < T; q++) pos[(q % G) % 8].push_back((uint32_t)q);
-        std::vector<uint2> out(T);
-        size_t fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (size_t i = 0; i < T;) {
-          size_t j = i;
-          while (j < T && slots[cls][j].y == slots[cls][i].y) j++;  // one wave's chunks
-          int best = -1;
-          double br = 2.0;
-          for (int x = 0; x < 8; x++) {
-            if (fill[x] >= pos[x].size()) continue;
-            double r = (double)fill[x] / (double)pos[x].size();
-            if (r < br) { br = r; best = x; }
-          }
-          for (size_t t = i; t < j; t++) {
-            int x = best;
-            if (fill[x] >= pos[x].size())  // XCD full: next XCD with room
-              for (int y = 0; y < 8; y++) if (fill[y] < pos[y].size()) { x = y; break; }
-            out[pos[x][fill[x]++]] = slots[cls][t];
-          }
-          i = j;
-        }
-        slots[cls].swap(out);
-      }
-    }
-    dfree(d.sched);
-    d.sched = nullptr;
-    HIP_OK(dmalloc(&d.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
-    d.cm.assign(ncls, ChunkMap{nullptr, 0});
-    size_t at = 0;
-    for (uint32_t cls = 0; cls < ncls; cls++) {
-      if (!slots[cls].empty())
-        HIP_OK(hipMemcpy(d.sched + at, slots[cls].data(), slots[cls].size() * sizeof(uint2), hipMemcpyHostToDevice));
-      d.cm[cls] = ChunkMap{d.sched + at, (uint32_t)slots[cls].size()};
-      at += slots[cls].size();
-    }
-    d.jit_state = (int)jit;
-  }
-  DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, d.rbase, d.rcnt, 0, (uint32_t)nrules};
+  for (auto& sl : d.slices)
+    if (sl.jit_state != (int)jit) layout_schedule(rs, b, dr, d, sl, jit);
+  const bool multi = d.slices.size() > 1;
   int depth = ruleset_depth(rs);
   size_t lds = (size_t)depth * (sizeof(UFrame) + BLOCK * sizeof(LaneFrame));
   dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
   double total_ms = 0;
   int n = std::max(1, iters);
+  std::vector<FailRec> host_recs;
   for (int it = 0; it < n; it++) {
+    const bool collect = copy_back && out && it == n - 1;
+    host_recs.clear();
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
-    HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
-    HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nrules * (size_t)d.wl.nwaves, 1) * 2, stream));
     HIP_OK(hipMemsetAsync(d.counts, 0, std::max<size_t>(1, nrules) * NSTATUS * 8, stream));
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
-    if (nres && nrules) {
-      if (d.nm) hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, d.mrules, d.nm);
+    for (auto& sl : d.slices) {
+      if (!nres || sl.k1 == sl.k0) continue;
+      const size_t nsr = sl.k1 - sl.k0;
+      DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, sl.rbase, d.rcnt, sl.k0, sl.k1};
+      HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
+      HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
+      if (sl.nm) hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, sl.mrules, sl.nm);
       HIP_OK(hipGetLastError());
-      if (d.grid[0]) {
-        hipLaunchKernelGGL(walk_kernel, dim3(d.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, d.cm[0],
+      if (sl.grid[0]) {
+        hipLaunchKernelGGL(walk_kernel, dim3(sl.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, sl.cm[0],
                            depth);
         HIP_OK(hipGetLastError());
       }
-      for (size_t cls = 1; cls < d.cm.size(); cls++) {
-        if (!d.grid[cls]) continue;
+      for (size_t cls = 1; cls < sl.cm.size(); cls++) {
+        if (!sl.grid[cls]) continue;
         const View* vp = d.view;
         WorkLists wl = d.wl;
-        ChunkMap cmj = d.cm[cls];
+        ChunkMap cmj = sl.cm[cls];
         void* args[] = {(void*)&vp, (void*)&o, (void*)&wl, (void*)&cmj};
-        HIP_OK(hipModuleLaunchKernel(dr->jfns[cls - 1], d.grid[cls], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        HIP_OK(hipModuleLaunchKernel(dr->jfns[cls - 1], sl.grid[cls], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
-      const size_t nchunks = nrules * (size_t)d.wl.nwaves;
+      const size_t nchunks = nsr * (size_t)d.wl.nwaves;
       const uint32_t ntiles = (uint32_t)((nchunks + WAVE - 1) / WAVE);
-      const RuleDesc* drules = (const RuleDesc*)(dr->base + dr->o_rules);
+      const RuleDesc* drules = (const RuleDesc*)(dr->base + dr->o_rules) + sl.k0;
       hipLaunchKernelGGL(compact_sum_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.rcnt, nchunks, d.tsum);
       hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, d.tsum, ntiles, d.nrecs);
-      hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, d.rbase, d.rcnt, drules,
+      hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, sl.rbase, d.rcnt, drules,
                          d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs);
-      // histogram blocks per CU: 8 (2.620 ms per evaluation) vs 2 (2.64 ms): more blocks stream the status bytes faster
-      static const size_t hmul = getenv("KYV_HIST") ? (size_t)std::max(1, atoi(getenv("KYV_HIST"))) : 8;
-      const uint32_t hgrid = (uint32_t)std::max<size_t>(
-          1, std::min<size_t>(((size_t)d.cus * hmul + nrules - 1) / std::max<size_t>(1, nrules), (nres / 16 + HIST_BLOCK - 1) / HIST_BLOCK));
-      if (nrules) hipLaunchKernelGGL(status_hist_kernel, dim3(hgrid, (uint32_t)nrules), dim3(HIST_BLOCK), 0, stream, d.status, nres, d.counts);
       HIP_OK(hipGetLastError());
+      if (collect && multi) {  // gather this slice's records before the next slice reuses the buffers
+        uint32_t nr = 0;
+        HIP_OK(hipMemcpyAsync(&nr, d.nrecs, 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        if (nr > d.max_recs) throw std::runtime_error("failure record buffer overflow");
+        const size_t at = host_recs.size();
+        host_recs.resize(at + nr);
+        if (nr) HIP_OK(hipMemcpy(host_recs.data() + at, d.recs, (size_t)nr * sizeof(FailRec), hipMemcpyDeviceToHost));
+      }
     }
+    // histogram blocks per CU: 8 (2.620 ms per evaluation) vs 2 (2.64 ms): more blocks stream the status bytes faster
+    static const size_t hmul = getenv("KYV_HIST") ? (size_t)std::max(1, atoi(getenv("KYV_HIST"))) : 8;
+    const uint32_t hgrid = (uint32_t)std::max<size_t>(
+        1, std::min<size_t>(((size_t)d.cus * hmul + nrules - 1) / std::max<size_t>(1, nrules), (nres / 16 + HIST_BLOCK - 1) / HIST_BLOCK));
+    if (nrules && nres) hipLaunchKernelGGL(status_hist_kernel, dim3(hgrid, (uint32_t)nrules), dim3(HIST_BLOCK), 0, stream, d.status, nres, d.counts);
+    HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d.e1, stream));
     HIP_OK(hipEventSynchronize(d.e1));
     float ms = 0;
@@ -818,11 +874,15 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipMemcpy(out->status.data(), d.status, nres * nrules, hipMemcpyDeviceToHost));
       out->pss_fails.resize((size_t)d.npss * nres);
       if (d.npss) HIP_OK(hipMemcpy(out->pss_fails.data(), d.pss_fails, out->pss_fails.size() * 4, hipMemcpyDeviceToHost));
-      uint32_t nr = 0;
-      HIP_OK(hipMemcpy(&nr, d.nrecs, 4, hipMemcpyDeviceToHost));
-      if (nr > d.max_recs) throw std::runtime_error("failure record buffer overflow");
-      out->fails.resize(nr);
-      if (nr) HIP_OK(hipMemcpy(out->fails.data(), d.recs, (size_t)nr * sizeof(FailRec), hipMemcpyDeviceToHost));
+      if (multi) {
+        out->fails.swap(host_recs);
+      } else {
+        uint32_t nr = 0;
+        HIP_OK(hipMemcpy(&nr, d.nrecs, 4, hipMemcpyDeviceToHost));
+        if (nr > d.max_recs) throw std::runtime_error("failure record buffer overflow");
+        out->fails.resize(nr);
+        if (nr) HIP_OK(hipMemcpy(out->fails.data(), d.recs, (size_t)nr * sizeof(FailRec), hipMemcpyDeviceToHost));
+      }
       out->d2h_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
   }

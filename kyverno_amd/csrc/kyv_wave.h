@@ -689,7 +689,7 @@ struct DevOut {
   FailRec* stage;          // failing-path records, staged per walk chunk: chunk (k, w) owns 64 * alts(k) slots
   const uint32_t* rbase;   // [nrules] first staging slot of rule k (its chunks follow, wave-major)
   uint16_t* rcnt;          // [nrules][nwaves] records staged by chunk (k, w)
-  uint32_t rule_lo, rule_hi;   // rule range handled by this launch
+  uint32_t rule_lo, rule_hi;   // rule slice of this launch: work lists, rbase and rcnt are indexed by k - rule_lo
 };
 
 // Failing-path records of one walk chunk, packed with wave ballots into the chunk's own staging slots (no
@@ -739,7 +739,7 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
   for (uint32_t c = blockIdx.x; c < cm.total; c += gridDim.x) {
     const uint2 kw = sld(cm.slots + c);
     const uint32_t k = kw.x, w = kw.y;
-    const size_t list = (size_t)k * wl.nwaves + w;
+    const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + w;
     const RuleDesc rd = sld(v.rules + k);
     bool active;
     uint32_t r;
@@ -767,7 +767,7 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
     }
     wk.rootmap = (it.x & ITEM_ROOT_MAP) != 0;
     const uint32_t alts = rd.kind == RK_PATTERN ? 1u : min(rd.nalts, (uint32_t)MAX_ALTS);
-    WaveSink sink{o.stage + sld32(o.rbase + k) + (size_t)w * WAVE * alts, 0u};
+    WaveSink sink{o.stage + sld32(o.rbase + (k - o.rule_lo)) + (size_t)w * WAVE * alts, 0u};
     uint8_t st = pair_walk(v, rd, active, r, k, v.nodes + it.y, wk, sink);
     if (magic) st = ST_FALLBACK;
     if (active || magic) o.status[(size_t)k * v.nres + r] = st;

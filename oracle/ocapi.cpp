@@ -286,8 +286,19 @@ long long oracle_validate_batch(const char* policies_json, const char* resources
 // instead of per call). out[rule * nres + res] for the policies' validate rules in order: 0 not matched / no
 // response, 1 pass, 2 fail, 3 skip, 4 error, 5 panic, 6 unsupported (CPU fallback), 7 nondeterministic.
 // Returns the rule names as a JSON array [[policy, rule], ...] (free with oracle_free), or null on error.
+extern "C" char* oracle_validate_matrix_t(const char* policies_json, const char* resources_json,
+                                          const char* nslabels_json, int nthreads, unsigned char* out, long long out_len,
+                                          double* seconds);
 extern "C" char* oracle_validate_matrix(const char* policies_json, const char* resources_json, const char* nslabels_json,
                                         int nthreads, unsigned char* out, long long out_len) {
+  return oracle_validate_matrix_t(policies_json, resources_json, nslabels_json, nthreads, out, out_len, nullptr);
+}
+
+// Same, timing the per-(resource, policy) loop only (policies compiled and resources decoded before the clock, as in
+// oracle_validate_batch): the bench's CPU baseline, whose verdicts are then compared with the device's.
+extern "C" char* oracle_validate_matrix_t(const char* policies_json, const char* resources_json,
+                                          const char* nslabels_json, int nthreads, unsigned char* out, long long out_len,
+                                          double* seconds) {
   try {
     VP pols = oj::parse(policies_json, true);
     VP res = oj::parse(resources_json, false);
@@ -324,6 +335,7 @@ extern "C" char* oracle_validate_matrix(const char* policies_json, const char* r
     if ((long long)(nrules * n) > out_len) return nullptr;
     std::fill(out, out + nrules * n, (unsigned char)0);
     std::atomic<size_t> next{0};
+    auto t0 = std::chrono::steady_clock::now();
     auto work = [&]() {
       while (true) {
         size_t i = next.fetch_add(16);
@@ -349,6 +361,7 @@ extern "C" char* oracle_validate_matrix(const char* policies_json, const char* r
     std::vector<std::thread> th;
     for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(work);
     for (auto& t : th) t.join();
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return dup(oj::dump(names));
   } catch (std::exception&) {
     return nullptr;

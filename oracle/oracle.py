@@ -35,6 +35,9 @@ def lib():
         L.oracle_format_float.restype = ctypes.c_void_p
         L.oracle_format_float.argtypes = [ctypes.c_double, ctypes.c_int]
         L.oracle_duration.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)]
+        L.oracle_validate_matrix_t.restype = ctypes.c_void_p
+        L.oracle_validate_matrix_t.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_double)]
         L.oracle_validate_batch.restype = ctypes.c_longlong
         L.oracle_validate_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
@@ -131,16 +134,20 @@ def validate_batch(policies, resources, ns_labels=None, threads=1):
 MATRIX_STATUS = ("none", "pass", "fail", "skip", "error", "panic", "unsupported", "nondeterministic")
 
 
-def validate_matrix(policies, resources, ns_labels=None, threads=8):
-    """-> (names [(policy, rule)], uint8 array [rule, resource] of MATRIX_STATUS codes)"""
+def validate_matrix(policies, resources, ns_labels=None, threads=8, nres=None, timed=False):
+    """-> (names [(policy, rule)], uint8 array [rule, resource] of MATRIX_STATUS codes)[, seconds of the timed loop]
+    resources: list of dicts, or JSON array text / bytes (then pass nres)."""
     import numpy as np
     pj, rj = _s(policies), _s(resources)
+    n = len(resources) if nres is None else nres
     # upper bound on rules: computed rules <= 3 per rule of the input (autogen)
     cap = 3 * sum(len((p.get("spec") or {}).get("rules") or []) for p in policies) + 1
-    out = np.zeros(cap * max(1, len(resources)), dtype=np.uint8)
-    ptr = lib().oracle_validate_matrix(pj, rj, _s(ns_labels) if ns_labels else b"", threads,
-                                       out.ctypes.data, out.size)
+    out = np.zeros(cap * max(1, n), dtype=np.uint8)
+    secs = ctypes.c_double(0)
+    ptr = lib().oracle_validate_matrix_t(pj, rj, _s(ns_labels) if ns_labels else b"", threads,
+                                         out.ctypes.data, out.size, ctypes.byref(secs))
     if not ptr:
         raise ValueError("oracle_validate_matrix failed")
     names = [tuple(x) for x in json.loads(_take(ptr))]
-    return names, out[: len(names) * len(resources)].reshape(len(names), len(resources))
+    m = out[: len(names) * n].reshape(len(names), n)
+    return (names, m, secs.value) if timed else (names, m)

@@ -83,14 +83,21 @@ _MATRIX_TO_DEVICE = {0: K.ST_NONE, 1: K.ST_PASS, 2: K.ST_FAIL, 3: K.ST_SKIP, 4: 
 
 
 def compare_matrix(policies, resources, ns_labels=None, backend="gpu", jit=None, threads=8):
-    """Status-level parity for large rulesets (C4): every (resource, rule) verdict of the device vs the oracle's
-    verdict matrix (oracle.validate_matrix). Nondeterministic pairs (either side) are excluded from the count.
-    Returns (stats, results); stats["nbad"] counts mismatching pairs."""
+    """Status-level parity at scale: every (resource, rule) verdict of the device vs the oracle's verdict matrix
+    (oracle.validate_matrix). resources: list of dicts, or NDJSON bytes (one resource per line). Nondeterministic
+    pairs (either side) are excluded from the count. Returns (stats, results); stats["nbad"] counts mismatching
+    pairs."""
     import numpy as np
     rs = E.Ruleset(policies)
     b = E.Batch(rs, resources, ns_labels)
     res = E.evaluate(rs, b, backend=backend, **({} if backend != "gpu" else {"jit": jit}))
-    names, m = O.validate_matrix(policies, resources, ns_labels, threads=threads)
+    if isinstance(resources, (bytes, bytearray)):
+        lines = [x for x in bytes(resources).split(b"\n") if x.strip()]
+        names, m = O.validate_matrix(policies, b"[" + b",".join(lines) + b"]", ns_labels, threads=threads,
+                                     nres=len(lines))
+        resources = lines
+    else:
+        names, m = O.validate_matrix(policies, resources, ns_labels, threads=threads)
     row = {nm: i for i, nm in enumerate(names)}
     lut = np.array([_MATRIX_TO_DEVICE[i] for i in range(8)], dtype=np.uint8)
     st = np.asarray(res.status)
@@ -109,3 +116,28 @@ def compare_matrix(policies, resources, ns_labels=None, backend="gpu", jit=None,
     stats = {"pairs": len(rs.rules) * len(resources), "compared": compared, "matched": matched, "nd": nd,
              "nbad": len(bad), "bad": bad[:20], "rules": len(rs.rules)}
     return stats, res
+
+
+def compare_status_sample(rs, res, policies, docs, ns_labels, idx, threads=8):
+    """Status parity of the device verdicts `res` (whole batch `docs`) on the resources at positions `idx` against
+    the oracle's verdict matrix of those resources alone. Returns a stats dict like compare_matrix."""
+    import numpy as np
+    sub = [docs[i] for i in idx]
+    names, m = O.validate_matrix(policies, sub, ns_labels, threads=threads)
+    row = {nm: i for i, nm in enumerate(names)}
+    lut = np.array([_MATRIX_TO_DEVICE[i] for i in range(8)], dtype=np.uint8)
+    st = np.asarray(res.status)[:, np.asarray(idx)]
+    bad, compared, nd, matched = [], 0, 0, 0
+    for k, rule in enumerate(rs.rules):
+        key = (rs.policies[rule["policy"]]["name"], rule["name"])
+        want = lut[m[row[key]]] if key in row else np.zeros(len(idx), np.uint8)
+        got = st[k]
+        ndm = (want == K.ST_ND) | (got == K.ST_ND)
+        nd += int(ndm.sum())
+        diff = np.nonzero((want != got) & ~ndm)[0]
+        matched += int((got != K.ST_NONE).sum())
+        compared += len(idx) - int(ndm.sum())
+        for ri in diff[:3]:
+            bad.append((key, int(idx[ri]), K.STATUS_NAMES[got[ri]], K.STATUS_NAMES[want[ri]]))
+    return {"pairs": len(rs.rules) * len(idx), "compared": compared, "matched": matched, "nd": nd,
+            "nbad": len(bad), "bad": bad[:20], "rules": len(rs.rules)}

@@ -67,6 +67,46 @@ def test_gpu_equals_cpu_instantiation_at_scale():
             assert g.pss_mask(int(r), int(k)) == c.pss_mask(int(r), int(k))
 
 
+def _oracle_threads():
+    import os
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
+
+
+def test_c3_oracle_matrix_at_scale_jit():
+    """configs[2] at scale through the production path (runtime-compiled walk, chosen automatically at this size):
+    every verdict of 200k mixed resources x the C3 rules against the oracle's verdict matrix"""
+    import parity_util as PU
+    data, nsl = synth.corpus_ndjson(200_000, seed=52, edge=True)
+    st, res = PU.compare_matrix(cases.best_practices() + cases.chart_restricted(), data, nsl, backend="gpu",
+                                threads=_oracle_threads())
+    assert res.jit
+    assert st["nbad"] == 0, st["bad"]
+    assert st["compared"] >= 200_000 * 80 and st["matched"] > 1_000_000
+
+
+def test_c2_oracle_matrix_at_scale():
+    """configs[1] at scale: podSecurity restricted/latest over 200k pods, every verdict against the oracle"""
+    import parity_util as PU
+    pol = [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "psa"},
+            "spec": {"rules": [{"name": "restricted", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                                "validate": {"podSecurity": {"level": "restricted", "version": "latest"}}}]}}]
+    data, nsl = synth.corpus_ndjson(200_000, kind="pods", seed=53, edge=True)
+    st, res = PU.compare_matrix(pol, data, nsl, backend="gpu", threads=_oracle_threads())
+    assert st["nbad"] == 0, st["bad"]
+    assert st["matched"] >= 200_000
+    assert res.counts["fail"] > 0 and res.counts["pass"] > 0
+
+
+def test_c5_oracle_matrix_at_scale():
+    """configs[4] at scale: 50 precondition / deny policies over 200k mixed resources, every verdict against the
+    oracle (CPU-fallback pairs must be exactly the oracle's unsupported ones)"""
+    import parity_util as PU
+    data, nsl = synth.corpus_ndjson(200_000, seed=54, edge=True)
+    st, res = PU.compare_matrix(synth.c5_policies(50), data, nsl, backend="gpu", threads=_oracle_threads())
+    assert st["nbad"] == 0, st["bad"]
+    assert res.counts["fallback"] > 0 and st["matched"] > 1_000_000
+
+
 def test_repeat_launches_deterministic():
     data, nsl = synth.corpus_ndjson(50_000, seed=35)
     rs = E.Ruleset(cases.best_practices() + cases.chart_restricted())
@@ -117,6 +157,45 @@ def test_c4_policycache_stress_gpu():
     every pair's status against the oracle's verdict matrix"""
     st, res = S.run_c4("gpu", 10000, 2000)
     assert st["rules"] >= 10000 and st["compared"] > 2e7
+
+
+def test_c4_rule_slices_gpu(monkeypatch):
+    """Rulesets whose walk buffers exceed the slice budget are evaluated in consecutive rule slices (kyv_engine.hip
+    SliceSched); a tiny budget forces ~40 slices here: every pair's status, and every failing path / message of a
+    sample, must equal the oracle and the single-slice evaluation"""
+    import parity_util as PU
+    monkeypatch.setenv("KYV_SLICE_MB", "16")
+    pols = synth.c4_policies(10000)
+    docs, nsl = synth.mixed(3000, seed=61, edge=True)
+    st, res = PU.compare_matrix(pols, docs, nsl, backend="gpu", threads=_oracle_threads())
+    assert st["nbad"] == 0, st["bad"]
+    monkeypatch.delenv("KYV_SLICE_MB")
+    rs = E.Ruleset(pols)
+    b = E.Batch(rs, docs, nsl)
+    one = E.evaluate(rs, b, backend="gpu")
+    assert np.array_equal(one.raw, res.raw)
+    fail = np.argwhere(one.status == K.ST_FAIL)
+    rng = np.random.default_rng(1)
+    for k, r in fail[rng.choice(len(fail), size=min(300, len(fail)), replace=False)]:
+        assert one.path(int(r), int(k)) == res.path(int(r), int(k))
+        assert one.message(int(r), int(k)) == res.message(int(r), int(k))
+
+
+def test_c4_at_scale_gpu():
+    """configs[3] at scale: 10,000 generated policies (~10.4k compiled rules) over 100k mixed resources on one
+    MI355X (buffers beyond the slice budget -> rule slices); the oracle (0.9 M pairs/s on C4) checks a spread
+    sample of 1,500 resources of the batch, every rule"""
+    import parity_util as PU
+    pols = synth.c4_policies(10000)
+    docs, nsl = synth.mixed(100_000, seed=62, edge=True)
+    rs = E.Ruleset(pols)
+    b = E.Batch(rs, docs, nsl)
+    res = E.evaluate(rs, b, backend="gpu")
+    assert sum(res.counts.values()) == len(rs.rules) * b.n
+    idx = np.linspace(0, b.n - 1, 1500).astype(int)
+    st = PU.compare_status_sample(rs, res, pols, docs, nsl, idx, threads=_oracle_threads())
+    assert st["nbad"] == 0, st["bad"]
+    assert st["matched"] > 100_000
 
 
 def test_condition_goldens_gpu():
