@@ -170,6 +170,12 @@ int64_t kyv_results_path(const kyv_results* r, const kyv_ruleset* rs, const kyv_
  * returns the full length, -1 on bad arguments */
 int64_t kyv_results_fallback_reason(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,
                                     uint32_t rule, char* buf, size_t cap);
+/* PodSecurity rules: RuleResponse.PodSecurityChecks (pkg/engine/api/ruleresponse.go:13, validation.go:550-564) of a
+ * pass / fail pair as JSON {"level","version","checks":[{"id","allowed","reason","detail"}]} in DefaultChecks()
+ * order (every failing check version, pkg/pss/evaluate.go:16-37); -1 when not renderable (rules with exclusions:
+ * the reference's order is Go map order) -- the caller then runs engine.Validate for the pair */
+int64_t kyv_results_pss_checks(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,
+                               uint32_t rule, char* buf, size_t cap);
 /* PodSecurity rules: failing (check, version) slot mask after exclusions */
 uint32_t kyv_results_pss_mask(const kyv_results* r, const kyv_ruleset* rs, uint32_t res, uint32_t rule);
 

@@ -52,7 +52,7 @@ EXPORTS = [
     "kyv_results_count", "kyv_results_kernel_ms", "kyv_results_alg_bytes", "kyv_results_message", "kyv_results_path",
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
     "kyv_ruleset_jit_compile", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
-    "kyv_results_fallback_reason",
+    "kyv_results_fallback_reason", "kyv_results_pss_checks",
 ]
 
 _lib = None
@@ -84,6 +84,8 @@ def lib():
     L.kyv_ruleset_rule_kinds.restype = i64
     L.kyv_results_fallback_reason.argtypes = [vp, vp, vp, u32, u32, ctypes.c_char_p, sz]
     L.kyv_results_fallback_reason.restype = i64
+    L.kyv_results_pss_checks.argtypes = [vp, vp, vp, u32, u32, ctypes.c_char_p, sz]
+    L.kyv_results_pss_checks.restype = i64
     L.kyv_ruleset_free.argtypes = [vp]
     L.kyv_ruleset_num_rules.argtypes = [vp]
     L.kyv_ruleset_num_rules.restype = u32

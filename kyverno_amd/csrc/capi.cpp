@@ -1,5 +1,6 @@
 // C-ABI (include/kyvgpu.h). No exception crosses this boundary.
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -14,6 +15,8 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
 void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool account);
 void free_device_images(Ruleset& rs, Batch* b);
 std::string fallback_why(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule);
+bool pss_checks_render(const Ruleset& rs, const Batch& b, uint32_t pos, uint32_t rule, uint32_t mask,
+                       std::vector<std::array<std::string, 3>>* out);
 }  // namespace kyv
 
 using namespace kyv;
@@ -318,6 +321,23 @@ static int64_t deny_message(const RuleMeta& m, const Batch& b, uint32_t res, cha
   return put(out, buf, cap);
 }
 
+static uint32_t pss_mask_at(const kyv_results* r, const Ruleset& rs, uint32_t pos, uint32_t rule) {
+  uint32_t slot = 0;
+  for (uint32_t k = 0; k < rule; k++) if (rs.rules[k].kind == RK_PSS) slot++;
+  size_t i = (size_t)slot * r->r.nres + pos;
+  return i < r->r.pss_fails.size() ? r->r.pss_fails[i] : 0;
+}
+
+static std::string json_str(const std::string& s) {
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
+    else if (c < 0x20) { char x[8]; snprintf(x, sizeof x, "\\u%04x", c); o += x; }
+    else o += (char)c;
+  }
+  return o + "\"";
+}
+
 // validation.go:722-758 (buildErrorMessage / buildAnyPatternErrorMessage) and :640/:665 pass messages
 int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res, uint32_t rule,
                             char* buf, size_t cap) {
@@ -349,7 +369,14 @@ int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const
   std::string msg;
   if (d.kind == RK_PSS) {
     if (st == ST_PASS) return put("Validation rule '" + m.name + "' passed.", buf, cap);
-    return -1;  // PodSecurity failure details are formatted by the caller from kyv_results_pss_mask
+    if (st != ST_FAIL) return -1;  // decode / version error texts embed Go error strings
+    std::vector<std::array<std::string, 3>> checks;
+    if (!pss_checks_render(rs, b, res, rule, pss_mask_at(r, rs, res, rule), &checks)) return -1;
+    // validation.go:561 + pss.FormatChecksPrint (evaluate.go:160-166): fmt "(%+v)\n" of each CheckResult
+    std::string msg = "Validation rule '" + m.name + "' failed. It violates PodSecurity \"" + m.pss_level + ":" +
+                      m.pss_version + "\": ";
+    for (auto& c : checks) msg += "({Allowed:false ForbiddenReason:" + c[1] + " ForbiddenDetail:" + c[2] + "})\n";
+    return put(msg, buf, cap);
   }
   if (st == ST_PASS) {
     if (d.kind == RK_ANYPATTERN) {
@@ -406,6 +433,30 @@ int64_t kyv_results_fallback_reason(const kyv_results* r, const kyv_ruleset* rs,
     const uint32_t pos = r->inv[res];
     if (!r->r.status.empty() && (r->r.status[(size_t)rule * r->r.nres + pos] & 7) != ST_FALLBACK) return put("", buf, cap);
     return put(fallback_why(*rs->rs, *b->b, pos, rule), buf, cap);
+  } catch (std::exception& e) {
+    fail(KYV_EINTERNAL, e.what());
+    return -1;
+  }
+}
+
+int64_t kyv_results_pss_checks(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res,
+                               uint32_t rule, char* buf, size_t cap) {
+  auto* r = const_cast<kyv_results*>(cr);
+  if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
+  const Ruleset& rs = *crs->rs;
+  if (rs.rules[rule].kind != RK_PSS) return -1;
+  try {
+    const uint32_t pos = r->inv[res];
+    const uint8_t st = r->r.status[(size_t)rule * r->r.nres + pos] & 7;
+    if (st != ST_PASS && st != ST_FAIL) return -1;
+    std::vector<std::array<std::string, 3>> checks;
+    if (st == ST_FAIL && !pss_checks_render(rs, *cb->b, pos, rule, pss_mask_at(r, rs, pos, rule), &checks)) return -1;
+    const RuleMeta& m = rs.meta[rule];
+    std::string o = "{\"level\":" + json_str(m.pss_level) + ",\"version\":" + json_str(m.pss_version) + ",\"checks\":[";
+    for (size_t i = 0; i < checks.size(); i++)
+      o += std::string(i ? "," : "") + "{\"id\":" + json_str(checks[i][0]) + ",\"allowed\":false,\"reason\":" +
+           json_str(checks[i][1]) + ",\"detail\":" + json_str(checks[i][2]) + "}";
+    return put(o + "]}", buf, cap);
   } catch (std::exception& e) {
     fail(KYV_EINTERNAL, e.what());
     return -1;

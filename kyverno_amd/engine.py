@@ -147,6 +147,18 @@ class Results:
             raise K.KyvError(K.lib().kyv_last_error().decode(errors="replace"))
         return buf.value.decode(errors="replace")
 
+    def pss_checks(self, res, rule):
+        """RuleResponse.PodSecurityChecks of a podSecurity pair (dict), or None when not renderable"""
+        L = K.lib()
+        buf = ctypes.create_string_buffer(8192)
+        n = L.kyv_results_pss_checks(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
+        if n < 0:
+            return None
+        if n >= len(buf):
+            buf = ctypes.create_string_buffer(n + 1)
+            L.kyv_results_pss_checks(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
+        return json.loads(buf.value.decode())
+
     def pss_mask(self, res, rule):
         return K.lib().kyv_results_pss_mask(self.h, self.ruleset.h, res, rule)
 

@@ -67,10 +67,11 @@ def test_batch_for_other_ruleset_rejected():
         E.evaluate(b, batch, backend="cpu")
 
 
-def test_jit_walk_kernel_compiles_for_gfx950():
+def test_jit_walk_kernel_compiles_for_gfx950(monkeypatch):
     """The runtime-compiled walk kernel of a ruleset: generated source covers the pattern rules and hipRTC
     compiles it for gfx950 without a GPU (the GPU tests then check its verdicts against the oracle)."""
     import cases
+    monkeypatch.setenv("KYV_JIT_CACHE", "0")  # compile for real; keep the in-tree code-object cache untouched
     from kyverno_amd import engine as E
     rs = E.Ruleset(cases.best_practices() + cases.quirk_policies())
     src, n = rs.jit_source()
