@@ -113,6 +113,16 @@ typedef struct {
   uint64_t resources, nodes, strings, heap_bytes, device_bytes;
 } kyv_batch_stats;
 
+/* one compacted failing-path record (a failing pattern, or one failing anyPattern alternative) */
+typedef struct {
+  uint32_t res;            /* resource index in the caller's input order */
+  uint32_t rule;
+  uint32_t alt;            /* anyPattern alternative (0 for single patterns) */
+  uint32_t path_template;  /* ruleset path template (0xFFFFFFFF: no path) */
+  uint16_t idx[4];         /* array indices substituted into the template */
+  uint32_t key[2];         /* batch-local string ids of resolved metadata keys (0xFFFFFFFF: none) */
+} kyv_failure;
+
 /* ---- ruleset: replaces per-call ComputeRules + pattern decoding ---- */
 int kyv_ruleset_compile(const char* policies_json, size_t len, const kyv_compile_opts* opts, kyv_ruleset** out);
 /* same, with the cluster's PolicyExceptions (kyverno.io/v2alpha1 documents, JSON array / NDJSON): replaces the
@@ -162,6 +172,10 @@ uint64_t kyv_results_alg_bytes(const kyv_results* r);
 /* RuleResponse.Message for one pair; returns the full length (may exceed cap), -1 if unavailable */
 int64_t kyv_results_message(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,
                             uint32_t rule, char* buf, size_t cap);
+/* the compacted failing-path records of the evaluation (PatternError.Path of every failing pattern / anyPattern
+ * alternative, validate.go:15-56): returns their number (copies min(count, cap)); -1 when verdicts stayed on the
+ * device */
+int64_t kyv_results_failures(const kyv_results* r, kyv_failure* out, size_t cap);
 /* failing path of a single-pattern FAIL ("" otherwise); returns the full length */
 int64_t kyv_results_path(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res, uint32_t rule,
                          char* buf, size_t cap);

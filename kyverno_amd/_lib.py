@@ -40,6 +40,11 @@ class PolicyInfo(ctypes.Structure):
                 ("nrules", ctypes.c_uint32), ("apply_one", ctypes.c_int32), ("scored_false", ctypes.c_int32)]
 
 
+class Failure(ctypes.Structure):
+    _fields_ = [("res", ctypes.c_uint32), ("rule", ctypes.c_uint32), ("alt", ctypes.c_uint32),
+                ("path_template", ctypes.c_uint32), ("idx", ctypes.c_uint16 * 4), ("key", ctypes.c_uint32 * 2)]
+
+
 class BatchStats(ctypes.Structure):
     _fields_ = [("resources", ctypes.c_uint64), ("nodes", ctypes.c_uint64), ("strings", ctypes.c_uint64),
                 ("heap_bytes", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64)]
@@ -52,7 +57,7 @@ EXPORTS = [
     "kyv_results_count", "kyv_results_kernel_ms", "kyv_results_alg_bytes", "kyv_results_message", "kyv_results_path",
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
     "kyv_ruleset_jit_compile", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
-    "kyv_results_fallback_reason", "kyv_results_pss_checks",
+    "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures",
 ]
 
 _lib = None
@@ -86,6 +91,8 @@ def lib():
     L.kyv_results_fallback_reason.restype = i64
     L.kyv_results_pss_checks.argtypes = [vp, vp, vp, u32, u32, ctypes.c_char_p, sz]
     L.kyv_results_pss_checks.restype = i64
+    L.kyv_results_failures.argtypes = [vp, vp, sz]
+    L.kyv_results_failures.restype = i64
     L.kyv_ruleset_free.argtypes = [vp]
     L.kyv_ruleset_num_rules.argtypes = [vp]
     L.kyv_ruleset_num_rules.restype = u32

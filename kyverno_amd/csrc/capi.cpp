@@ -411,6 +411,26 @@ int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const
   return put("validation error: " + m.message + ". " + joined, buf, cap);
 }
 
+int64_t kyv_results_failures(const kyv_results* r, kyv_failure* out, size_t cap) {
+  if (!r) return fail(KYV_EINVAL, "null argument"), -1;
+  if (r->r.status.empty() && r->r.nres && r->r.nrules) return fail(KYV_ERANGE, "verdicts kept on the device"), -1;
+  const size_t n = r->r.fails.size();
+  std::vector<uint32_t> order(r->inv.size());
+  for (size_t i = 0; i < r->inv.size(); i++) order[r->inv[i]] = (uint32_t)i;  // kind-major position -> input index
+  for (size_t i = 0; i < n && out && i < cap; i++) {
+    const FailRec& f = r->r.fails[i];
+    kyv_failure& o = out[i];
+    o.res = f.res < order.size() ? order[f.res] : f.res;
+    o.rule = f.rule;
+    o.alt = f.alt;
+    o.path_template = f.tmpl;
+    for (int j = 0; j < 4; j++) o.idx[j] = f.idx[j];
+    o.key[0] = f.key[0];
+    o.key[1] = f.key[1];
+  }
+  return (int64_t)n;
+}
+
 int64_t kyv_results_path(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res, uint32_t rule,
                          char* buf, size_t cap) {
   auto* r = const_cast<kyv_results*>(cr);

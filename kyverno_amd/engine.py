@@ -139,6 +139,21 @@ class Results:
         K.lib().kyv_results_path(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
         return buf.value.decode(errors="replace")
 
+    def failures(self):
+        """compacted failing-path records as a structured numpy array (res in input order, rule, alt,
+        path_template, idx[4], key[2])"""
+        L = K.lib()
+        n = L.kyv_results_failures(self.h, None, 0)
+        if n < 0:
+            raise K.KyvError(L.kyv_last_error().decode(errors="replace"))
+        dt = np.dtype([("res", "<u4"), ("rule", "<u4"), ("alt", "<u4"), ("path_template", "<u4"), ("idx", "<u2", 4),
+                       ("key", "<u4", 2)])
+        assert dt.itemsize == ctypes.sizeof(K.Failure)
+        out = np.zeros(n, dtype=dt)
+        if n:
+            L.kyv_results_failures(self.h, out.ctypes.data, n)
+        return out
+
     def fallback_reason(self, res, rule):
         """why pair (res, rule) is KYV_ST_FALLBACK ("" otherwise)"""
         buf = ctypes.create_string_buffer(512)

@@ -7,8 +7,11 @@ each background policy `scanner.ScanResource` builds a JSON context and calls `e
 (results.go:38-54). Here a whole batch goes through one `kyv_eval`; the per-policy summary is assembled from the
 device's per-rule verdict totals (`kyv_results_rule_counts`), so rows are only materialised on request.
 
-Multi-GPU: each rank scans its own shard; `reduce_summary` sums the per-policy summaries over the process group
-(RCCL with the "nccl" backend, gloo on CPU) - the only collective of the path.
+Multi-GPU: each rank scans its own contiguous shard; the collectives only assemble results, over the
+process group (RCCL with the "nccl" backend on device tensors, gloo on CPU):
+  reduce_summary   all-reduce (sum) of the per-policy summaries;
+  gather_verdicts  all-gather of every rank's verdict matrix, two pairs per byte (status values are 3-bit);
+  gather_failures  count-then-gather of the compacted failing-path records.
 
 Pairs outside the device subset (KYV_ST_FALLBACK, PANIC, ND) are listed by `fallback_pairs()`: the Go shim
 evaluates exactly those with the reference engine; they are counted as `cpu_fallback`, not in pass/fail/....
@@ -152,3 +155,72 @@ def reduce_summary(matrix, group=None, device=None):
         t = t.to(device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return t.cpu().numpy()
+
+
+def _all_gather_var(t, group, dist, torch):
+    """all-gather of a tensor whose dim 0 differs per rank: sizes first, then equal-size (padded) tensors"""
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    world = dist.get_world_size(group)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    m = max(sizes) if sizes else 0
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return [p[:k] for p, k in zip(parts, sizes)], sizes
+
+
+def gather_verdicts(status, group=None, device=None):
+    """All-gather the verdict matrices of every rank's shard: status is this rank's uint8
+    [rules, n_rank] (rule-major KYV_ST_* bytes, low 3 bits used); on the wire two pairs share a byte. Returns
+    (uint8 [rules, sum n_rank] in rank order, list of each rank's first global resource index)."""
+    import torch
+    import torch.distributed as dist
+    st = torch.from_numpy(np.ascontiguousarray(np.asarray(status) & 7, dtype=np.uint8))
+    if device is not None:
+        st = st.to(device)
+    nr, n = st.shape
+    n2 = n + (n & 1)
+    buf = torch.zeros((nr, n2), dtype=torch.uint8, device=st.device)
+    buf[:, :n] = st
+    packed = (buf[:, 0::2] | (buf[:, 1::2] << 4)).t().contiguous()  # [n2 / 2, rules]: ranks differ in dim 0
+    parts, sizes = _all_gather_var(packed, group, dist, torch)
+    cols, offs, at = [], [], 0
+    for p, k in zip(parts, sizes):
+        q = p.t()
+        full = torch.stack((q & 15, q >> 4), dim=2).reshape(nr, 2 * k)
+        cols.append(full)
+    counts = torch.tensor([n], dtype=torch.int64, device=st.device)
+    world = dist.get_world_size(group)
+    ns = [torch.zeros_like(counts) for _ in range(world)]
+    dist.all_gather(ns, counts, group=group)
+    out = []
+    for c, k in zip(cols, ns):
+        k = int(k.item())
+        out.append(c[:, :k])
+        offs.append(at)
+        at += k
+    return torch.cat(out, dim=1).cpu().numpy(), offs
+
+
+def gather_failures(failures, res_offset, group=None, device=None):
+    """Count-then-gather of the compacted failing-path records (engine.Results.failures()) of every rank: int64 rows
+    (global resource index, rule, anyPattern alternative, path template, idx0..3) in rank order. Resolved metadata
+    keys are batch-local dictionary ids and stay with the owning rank (which formats those paths)."""
+    import torch
+    import torch.distributed as dist
+    f = np.asarray(failures)
+    rows = np.zeros((len(f), 8), dtype=np.int64)
+    if len(f):
+        rows[:, 0] = f["res"].astype(np.int64) + int(res_offset)
+        rows[:, 1] = f["rule"]
+        rows[:, 2] = f["alt"]
+        rows[:, 3] = f["path_template"]
+        rows[:, 4:8] = f["idx"]
+    t = torch.from_numpy(rows)
+    if device is not None:
+        t = t.to(device)
+    parts, _ = _all_gather_var(t, group, dist, torch)
+    return torch.cat(parts, dim=0).cpu().numpy()
