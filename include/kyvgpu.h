@@ -22,11 +22,12 @@
  *                        status, message, failing path; plus the summary counters used by
  *                        pkg/utils/report/results.go:38 (CalculateSummary).
  *
- * deny and preconditions run on the device when every variable is a plain `{{ request.object.<path> }}`
- * reference (pkg/engine/variables/evaluate.go:21, operator/*.go). Rules that need the reference CPU engine
- * (JMESPath functions / projections, other context variables, context entries, foreach, exceptions, image
- * verification) are classified at compile time; their pairs report KYV_ST_FALLBACK and the caller runs
- * engine.Validate for them.
+ * deny, preconditions and foreach-deny run on the device when every variable is a `{{ request.object... }}`,
+ * `{{ request.operation }}` or `{{ element... }}` expression of the JMESPath subset the compiler restates
+ * (fields, multi-select lists, flatten projections, keys(@), `||` literals; pkg/engine/variables/evaluate.go:21,
+ * operator/*.go, validation.go:319-421). Rules that need the reference CPU engine (other JMESPath functions,
+ * context entries, foreach patterns, exceptions, image verification) are classified at compile time; their pairs
+ * report KYV_ST_FALLBACK and the caller runs engine.Validate for them.
  *
  * Threading: a kyv_ruleset is immutable after compile and may be shared; batches and results are per
  * call. No C++ exception crosses this ABI; failures return a non-zero code and kyv_last_error()
@@ -65,7 +66,11 @@ enum {
 
 /* rule kinds */
 enum { KYV_RULE_PATTERN = 1, KYV_RULE_ANYPATTERN = 2, KYV_RULE_PSS = 3, KYV_RULE_FALLBACK = 4, KYV_RULE_PANIC = 5,
-       KYV_RULE_ERROR = 6 };
+       KYV_RULE_ERROR = 6, KYV_RULE_DENY = 7, KYV_RULE_FOREACH = 8 };
+/* rule flags (kyv_ruleset_rule_flags) */
+enum { KYV_RULE_USES_OPERATION = 1u };  /* a condition reads request.operation, evaluated as the background scan's
+                                           "CREATE" (scanner.go:97); admission callers route other operations to
+                                           engine.Validate */
 
 enum { KYV_BACKEND_GPU = 0, KYV_BACKEND_CPU = 1 };
 enum { KYV_EVAL_NO_COPYBACK = 1u, KYV_EVAL_ACCOUNT_BYTES = 2u,
@@ -140,6 +145,7 @@ int kyv_ruleset_policy_info(const kyv_ruleset* rs, uint32_t policy, kyv_policy_i
 /* MatchResources.GetKinds() of compiled rule `rule` ('\n'-separated, autogen applied) and Rule.HasValidate(): the
  * policy cache's kind index (policyMap.set, pkg/policycache/store.go:96-138); returns the full length or -1 */
 int64_t kyv_ruleset_rule_kinds(const kyv_ruleset* rs, uint32_t rule, char* buf, size_t cap, int32_t* has_validate);
+uint32_t kyv_ruleset_rule_flags(const kyv_ruleset* rs, uint32_t rule);
 /* runtime-compiled walk kernel of a ruleset (diagnostics; kyv_eval compiles it on first use by itself):
    the generated HIP source (returns its full length; rules it covers in *nrules_jit) and a hipRTC compile for
    gfx950 that needs no GPU (seconds, code-object bytes) */

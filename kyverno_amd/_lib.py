@@ -15,7 +15,9 @@ EVAL_JIT_ON = 8
 
 ST_NONE, ST_PASS, ST_FAIL, ST_SKIP, ST_ERROR, ST_FALLBACK, ST_PANIC, ST_ND = range(8)
 STATUS_NAMES = ["none", "pass", "fail", "skip", "error", "fallback", "panic", "nondeterministic"]
-RULE_KINDS = {1: "pattern", 2: "anyPattern", 3: "podSecurity", 4: "fallback", 5: "panic", 6: "error", 7: "deny"}
+RULE_KINDS = {1: "pattern", 2: "anyPattern", 3: "podSecurity", 4: "fallback", 5: "panic", 6: "error", 7: "deny",
+              8: "foreach"}
+RULE_USES_OPERATION = 1
 
 
 class CompileOpts(ctypes.Structure):
@@ -57,7 +59,7 @@ EXPORTS = [
     "kyv_results_count", "kyv_results_kernel_ms", "kyv_results_alg_bytes", "kyv_results_message", "kyv_results_path",
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
     "kyv_ruleset_jit_compile", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
-    "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures",
+    "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures", "kyv_ruleset_rule_flags",
 ]
 
 _lib = None
@@ -93,6 +95,8 @@ def lib():
     L.kyv_results_pss_checks.restype = i64
     L.kyv_results_failures.argtypes = [vp, vp, sz]
     L.kyv_results_failures.restype = i64
+    L.kyv_ruleset_rule_flags.argtypes = [vp, u32]
+    L.kyv_ruleset_rule_flags.restype = u32
     L.kyv_ruleset_free.argtypes = [vp]
     L.kyv_ruleset_num_rules.argtypes = [vp]
     L.kyv_ruleset_num_rules.restype = u32

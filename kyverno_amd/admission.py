@@ -14,6 +14,8 @@ CPU engine for that whole policy (`cpu_engine`, the Go shim's engine.Validate):
   * pairs the device reports as KYV_ST_FALLBACK / PANIC / ND;
   * rules whose match or exclude names roles / clusterRoles / subjects (admission userInfo: the device path has
     background-scan semantics, where the admission info is empty, utils.go:258-262);
+  * policies with a condition on request.operation for requests other than CREATE (the device binds it to the
+    background scan's "CREATE");
   * UPDATE requests where a rule does not match the new object but matches the old one (the OldResource retry of
     validation.go:600-615 then validates the new object, which the device did not do);
   * DELETE requests (the new object is empty; validateResourceWithRule skips patterns, validation.go:568-579).
@@ -424,8 +426,10 @@ class AdmissionBatcher:
                 ri = self.ruleset.rules[k]
                 if ri["has_validate"]:
                     kinds.update(compute_kind(g) for g in ri["match_kinds"])
+            uses_op = any(self.ruleset.rules[k]["uses_operation"]
+                          for k in range(pm["first_rule"], pm["first_rule"] + pm["nrules"]))
             self.pol.append({"doc": p, "name": pm["name"], "namespace": pm["namespace"], "first": pm["first_rule"],
-                             "n": pm["nrules"], "apply_one": pm["apply_one"], "userinfo": userinfo,
+                             "n": pm["nrules"], "apply_one": pm["apply_one"], "userinfo": userinfo, "uses_op": uses_op,
                              "enforce": has_validate(p) and compute_enforce_policy(p), "kinds": kinds,
                              "fail_policy": failure_policy(p)})
         self.stats = {"requests": 0, "batches": 0, "device_policies": 0, "cpu_policies": 0}
@@ -542,7 +546,8 @@ class AdmissionBatcher:
             if p["fail_policy"] == "Fail":
                 fp = "Fail"
             rules = None
-            if i_new is not None and not p["userinfo"]:
+            # the device evaluates request.operation as the background scan's "CREATE"
+            if i_new is not None and not p["userinfo"] and not (p["uses_op"] and op != "CREATE"):
                 old_retry = i_old is not None and any(
                     int(st[k, i_new]) == K.ST_NONE and int(st[k, i_old]) != K.ST_NONE
                     for k in range(p["first"], p["first"] + p["n"]))

@@ -94,6 +94,11 @@ int64_t kyv_ruleset_rule_kinds(const kyv_ruleset* rs, uint32_t k, char* buf, siz
   return (int64_t)s.size();
 }
 
+uint32_t kyv_ruleset_rule_flags(const kyv_ruleset* rs, uint32_t k) {
+  if (!rs || k >= rs->rs->rules.size()) return 0;
+  return (rs->rs->rules[k].flags & RD_USES_OPERATION) ? KYV_RULE_USES_OPERATION : 0u;
+}
+
 int64_t kyv_ruleset_jit_source(const kyv_ruleset* rs, char* buf, size_t cap, uint32_t* nrules_jit) {
   if (!rs) return fail(KYV_EINVAL, "null argument"), -1;
   try {
@@ -364,6 +369,14 @@ int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const
     if (st == ST_ERROR && cond_error_text(rs, b, res, d.root, &e))
       return put("failed to substitute variables in deny conditions: " + e, buf, cap);
     return -1;
+  }
+  if (d.kind == RK_FOREACH) {  // validateForEach / validateElements (validation.go:319-381)
+    if (st == ST_PASS) return put("rule passed", buf, cap);
+    if (st == ST_SKIP) return put("rule skipped", buf, cap);
+    if (st == ST_FAIL)
+      return put("validation failure: " + (m.message.empty() ? "validation error: rule " + m.name + " failed" : m.message),
+                 buf, cap);
+    return -1;  // error texts embed Go error strings
   }
   if (m.message_vars && st == ST_FAIL) return -1;  // message needs variable substitution (CPU engine)
   std::string msg;

@@ -343,6 +343,8 @@ struct Cx {
   int nslots = 0;
   uint32_t nmeta = 0;
   std::vector<MetaSite> sites;
+  bool allow_element = false;  // compiling conditions of a foreach entry (`element` is bound)
+  bool uses_op = false;        // some condition read request.operation
   uint32_t tmpl(const std::string& s) {
     rs.templates.push_back(s);
     return (uint32_t)rs.templates.size() - 1;
@@ -1015,6 +1017,294 @@ bool object_var(const std::string& s, std::vector<std::string>& segs, std::strin
   return true;
 }
 bool var_syntax(const std::string& s) { return s.find("{{") != std::string::npos || s.find("$(") != std::string::npos; }
+
+uint32_t emit_cnode(Cx& c, const Value& v);
+
+// ---- JMESPath subset (OK_JMES programs, kyv_layout.h): go-jmespath's Pratt grammar for fields, quoted fields,
+// sub-expressions, multi-select lists, flatten projections, keys(@), `||` and raw-string / JSON literals, then
+// linearised into root + ops. Anything else (filters, indexes, other functions, pipes, ...) -> CPU fallback.
+struct JNode {
+  enum K { Field, Sub, Proj, Flat, Multi, Func, Cur, Ident, Or, Lit } k;
+  std::string name;
+  Value lit;
+  std::vector<std::shared_ptr<JNode>> kids;
+};
+using JP = std::shared_ptr<JNode>;
+struct JParser {
+  enum Tok { End, Id, Quoted, Dot, LBr, RBr, Flatten, Comma, LPar, RPar, At, OrT, Raw, Json };
+  std::vector<std::pair<Tok, std::string>> toks;
+  size_t at = 0;
+  explicit JParser(const std::string& s) {
+    size_t i = 0;
+    auto is0 = [](char c) { return isalpha((unsigned char)c) || c == '_'; };
+    while (i < s.size()) {
+      char c = s[i];
+      if (c == ' ' || c == '\t' || c == '\n' || c == '\r') { i++; continue; }
+      if (is0(c)) {
+        size_t j = i;
+        while (j < s.size() && (is0(s[j]) || isdigit((unsigned char)s[j]))) j++;
+        toks.push_back({Id, s.substr(i, j - i)});
+        i = j;
+        continue;
+      }
+      if (c == '"' || c == '\'' || c == '`') {
+        size_t j = i + 1;
+        while (j < s.size() && s[j] != c) { if (s[j] == '\\') throw Fallback{"JMESPath: escapes"}; j++; }
+        if (j >= s.size()) throw Fallback{"JMESPath: unterminated literal"};
+        toks.push_back({c == '"' ? Quoted : c == '\'' ? Raw : Json, s.substr(i + 1, j - i - 1)});
+        i = j + 1;
+        continue;
+      }
+      if (c == '[' && i + 1 < s.size() && s[i + 1] == ']') { toks.push_back({Flatten, "[]"}); i += 2; continue; }
+      if (c == '|' && i + 1 < s.size() && s[i + 1] == '|') { toks.push_back({OrT, "||"}); i += 2; continue; }
+      Tok t;
+      switch (c) {
+        case '.': t = Dot; break;
+        case '[': t = LBr; break;
+        case ']': t = RBr; break;
+        case ',': t = Comma; break;
+        case '(': t = LPar; break;
+        case ')': t = RPar; break;
+        case '@': t = At; break;
+        default: throw Fallback{"JMESPath: expression outside the device subset"};
+      }
+      toks.push_back({t, std::string(1, c)});
+      i++;
+    }
+    toks.push_back({End, ""});
+  }
+  static int bp(Tok t) { return t == OrT ? 2 : t == Flatten ? 9 : t == Dot ? 40 : t == LBr ? 55 : t == LPar ? 60 : 0; }
+  Tok look() const { return toks[at].first; }
+  void eat(Tok t) { if (look() != t) throw Fallback{"JMESPath: syntax"}; at++; }
+  static JP mk(JNode::K k, std::vector<JP> kids = {}, const std::string& n = "") {
+    auto x = std::make_shared<JNode>();
+    x->k = k; x->kids = std::move(kids); x->name = n;
+    return x;
+  }
+  JP expr(int b) {
+    auto t = toks[at++];
+    JP left = nud(t);
+    while (b < bp(look())) left = led(toks[at++], left);
+    return left;
+  }
+  JP nud(const std::pair<Tok, std::string>& t) {
+    switch (t.first) {
+      case Id: return mk(JNode::Field, {}, t.second);
+      case Quoted: if (look() == LPar) throw Fallback{"JMESPath: syntax"}; return mk(JNode::Field, {}, t.second);
+      case At: return mk(JNode::Cur);
+      case Raw: { JP x = mk(JNode::Lit); x->lit = Value::S(t.second); return x; }
+      case Json: { JP x = mk(JNode::Lit); x->lit = pj::parse(t.second, true); return x; }
+      case Flatten: return mk(JNode::Proj, {mk(JNode::Flat, {mk(JNode::Ident)}), proj_rhs(bp(Flatten))});
+      case LBr: return multi();
+      default: throw Fallback{"JMESPath: expression outside the device subset"};
+    }
+  }
+  JP led(const std::pair<Tok, std::string>& t, JP left) {
+    switch (t.first) {
+      case Dot: return mk(JNode::Sub, {left, dot_rhs(bp(Dot))});
+      case Flatten: return mk(JNode::Proj, {mk(JNode::Flat, {left}), proj_rhs(bp(Flatten))});
+      case OrT: return mk(JNode::Or, {left, expr(bp(OrT))});
+      case LPar: {
+        if (left->k != JNode::Field) throw Fallback{"JMESPath: syntax"};
+        std::vector<JP> args;
+        while (look() != RPar) { args.push_back(expr(0)); if (look() == Comma) eat(Comma); }
+        eat(RPar);
+        return mk(JNode::Func, args, left->name);
+      }
+      default: throw Fallback{"JMESPath: expression outside the device subset"};
+    }
+  }
+  JP dot_rhs(int b) {
+    if (look() == Id || look() == Quoted) return expr(b);
+    if (look() == LBr) { eat(LBr); return multi(); }
+    throw Fallback{"JMESPath: expression outside the device subset"};
+  }
+  JP proj_rhs(int b) {
+    if (bp(look()) < 10) return mk(JNode::Ident);
+    if (look() == LBr) return expr(b);
+    if (look() == Dot) { eat(Dot); return dot_rhs(b); }
+    throw Fallback{"JMESPath: syntax"};
+  }
+  JP multi() {
+    std::vector<JP> items;
+    for (;;) { items.push_back(expr(0)); if (look() == RBr) break; eat(Comma); }
+    eat(RBr);
+    return mk(JNode::Multi, items);
+  }
+};
+
+// linearise: ops of the expression evaluated on the current value; `list` tracks projection (List) mode
+void jlin(Cx& c, const JP& n, std::vector<uint32_t>& out, bool& list) {
+  switch (n->k) {
+    case JNode::Field: out.push_back(JO_FIELD); out.push_back(c.sid(n->name)); return;
+    case JNode::Sub:
+      jlin(c, n->kids[0], out, list);
+      jlin(c, n->kids[1], out, list);
+      return;
+    case JNode::Multi:
+      if (list) throw Fallback{"JMESPath: multi-select inside a projection"};
+      out.push_back(JO_MULTI);
+      out.push_back((uint32_t)n->kids.size());
+      for (auto& k : n->kids) {
+        if (k->k != JNode::Field) throw Fallback{"JMESPath: multi-select of non-fields"};
+        out.push_back(c.sid(k->name));
+      }
+      return;
+    case JNode::Proj: {
+      const JP& f = n->kids[0];
+      if (f->k != JNode::Flat || f->kids[0]->k == JNode::Ident) throw Fallback{"JMESPath: projection form"};
+      jlin(c, f->kids[0], out, list);
+      out.push_back(JO_FLAT);
+      list = true;
+      const JP& r = n->kids[1];
+      if (r->k == JNode::Ident) return;
+      if (r->k == JNode::Func) {  // [].keys(@) must be flattened by the next [] (fused below)
+        if (r->name != "keys" || r->kids.size() != 1 || r->kids[0]->k != JNode::Cur) throw Fallback{"JMESPath: function"};
+        out.push_back(JO_KEYS);
+        return;
+      }
+      jlin(c, r, out, list);
+      return;
+    }
+    case JNode::Func:
+      if (n->name != "keys" || n->kids.size() != 1 || n->kids[0]->k != JNode::Cur) throw Fallback{"JMESPath: function"};
+      if (list) throw Fallback{"JMESPath: keys() inside a projection"};
+      out.push_back(JO_KEYS);
+      list = true;
+      return;
+    default: throw Fallback{"JMESPath: expression outside the device subset"};
+  }
+}
+
+// `{{ <expr> }}` -> OK_JMES operand (false: not a single-variable string; throws Fallback outside the subset);
+// *uses_op when the expression reads request.operation
+bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, std::string* text, bool* uses_op) {
+  if (s.size() < 4 || s.compare(0, 2, "{{") != 0 || s.compare(s.size() - 2, 2, "}}") != 0) return false;
+  std::string inner = s.substr(2, s.size() - 4);
+  if (inner.find('{') != std::string::npos || inner.find('}') != std::string::npos) return false;
+  inner = pj::go_trim_space(inner);
+  if (text) *text = inner;
+  JParser p(inner);
+  JP n = p.expr(0);
+  if (p.look() != JParser::End) throw Fallback{"JMESPath: syntax"};
+  Value orlit;
+  bool has_or = false;
+  if (n->k == JNode::Or) {
+    if (n->kids[1]->k != JNode::Lit) throw Fallback{"JMESPath: || with a non-literal"};
+    orlit = n->kids[1]->lit;
+    has_or = true;
+    n = n->kids[0];
+  }
+  // split the root off the left spine: request.object / request.operation / element
+  std::vector<JNode*> spine;
+  for (JNode* x = n.get();;) {
+    spine.push_back(x);
+    if (x->k == JNode::Field) break;
+    if (x->k != JNode::Sub && x->k != JNode::Proj && x->k != JNode::Flat) throw Fallback{"JMESPath: root"};
+    x = x->kids[0].get();
+  }
+  std::vector<uint32_t> ops;
+  bool list = false;
+  uint32_t root;
+  JP body;
+  const std::string r0 = spine.back()->name;
+  if (r0 == "element") {
+    if (!allow_element) throw Fallback{"JMESPath: element outside foreach"};
+    root = JR_ELEMENT;
+    if (spine.size() == 1) body = nullptr;
+    else { JNode* top = spine[spine.size() - 2]; if (top->k != JNode::Sub) throw Fallback{"JMESPath: root"};
+           top->kids[0] = JParser::mk(JNode::Cur); body = n; }
+  } else if (r0 == "request") {
+    if (spine.size() < 2 || spine[spine.size() - 2]->k != JNode::Sub || spine[spine.size() - 2]->kids[1]->k != JNode::Field)
+      throw Fallback{"JMESPath: root"};
+    JNode* top = spine[spine.size() - 2];
+    const std::string r1 = top->kids[1]->name;
+    if (r1 == "operation") {
+      if (spine.size() != 2) throw Fallback{"JMESPath: request.operation path"};
+      root = JR_OPERATION;
+      body = nullptr;
+      if (uses_op) *uses_op = true;
+    } else if (r1 == "object") {
+      root = JR_OBJECT;
+      if (spine.size() == 2) body = nullptr;
+      else { JNode* nx = spine[spine.size() - 3]; nx->kids[0] = JParser::mk(JNode::Cur); body = n; }
+    } else {
+      throw Fallback{"conditions: variables beyond request.object paths"};
+    }
+  } else {
+    throw Fallback{"conditions: variables beyond request.object paths"};
+  }
+  // the body's left spine now ends in `@` (Cur): linearise without it
+  std::function<void(const JP&)> lin = [&](const JP& x) {
+    if (x->k == JNode::Cur) return;
+    if (x->k == JNode::Sub && x->kids[0]->k == JNode::Cur) { jlin(c, x->kids[1], ops, list); return; }
+    if (x->k == JNode::Sub) { lin(x->kids[0]); jlin(c, x->kids[1], ops, list); return; }
+    if (x->k == JNode::Proj) {
+      const JP& f = x->kids[0];
+      if (f->k != JNode::Flat) throw Fallback{"JMESPath: projection form"};
+      lin(f->kids[0]);
+      ops.push_back(JO_FLAT);
+      list = true;
+      const JP& rr = x->kids[1];
+      if (rr->k == JNode::Ident) return;
+      if (rr->k == JNode::Func) {
+        if (rr->name != "keys" || rr->kids.size() != 1 || rr->kids[0]->k != JNode::Cur) throw Fallback{"JMESPath: function"};
+        ops.push_back(JO_KEYS);
+        return;
+      }
+      jlin(c, rr, ops, list);
+      return;
+    }
+    throw Fallback{"JMESPath: expression outside the device subset"};
+  };
+  if (body) lin(body);
+  // fuse projection keys(@) + flatten; keys() left unflattened inside a projection is a list of lists
+  std::vector<uint32_t> fused;
+  bool pure = !has_or;
+  for (size_t i = 0; i < ops.size();) {
+    const uint32_t op = ops[i];
+    if (op == JO_FIELD) { fused.push_back(op); fused.push_back(ops[i + 1]); i += 2; continue; }
+    pure = false;
+    if (op == JO_MULTI) { uint32_t m = ops[i + 1]; fused.insert(fused.end(), ops.begin() + i, ops.begin() + i + 2 + m); i += 2 + m; continue; }
+    if (op == JO_KEYS) {
+      bool in_list = false;  // was a FLAT before it?
+      for (size_t j = 0; j < fused.size(); j++) if (fused[j] == JO_FLAT) in_list = true;
+      if (in_list) {
+        if (i + 1 >= ops.size() || ops[i + 1] != JO_FLAT) throw Fallback{"JMESPath: keys() projection without []"};
+        fused.push_back(JO_KEYS_FLAT);
+        i += 2;
+      } else {
+        fused.push_back(JO_KEYS);
+        i++;
+      }
+      continue;
+    }
+    fused.push_back(op);
+    i++;
+  }
+  // a multi-select list or keys() outside a projection is a plain list: only [] (or the end) may follow
+  for (size_t i = 0; i < fused.size();) {
+    const uint32_t op = fused[i];
+    const size_t w = op == JO_FIELD ? 2 : op == JO_MULTI ? 2 + fused[i + 1] : 1;
+    if ((op == JO_MULTI || op == JO_KEYS) && i + w < fused.size() && fused[i + w] != JO_FLAT)
+      throw Fallback{"JMESPath: list outside a projection"};
+    i += w;
+  }
+  if (has_or) {
+    Value lit = pj::parse(pj::dump(orlit), false);
+    fused.push_back(JO_OR);
+    fused.push_back(emit_cnode(c, lit));
+  }
+  // request.operation: the background scan's JSON context holds "CREATE" (scanner.go:97; CLI default common.go:287)
+  const uint32_t oplit = root == JR_OPERATION ? emit_cnode(c, Value::S("CREATE")) : NONE;
+  o->kind = OK_JMES;
+  o->a = (uint32_t)c.rs.pool.size();
+  c.rs.pool.push_back(root | (pure ? JF_PURE : 0u));
+  if (root == JR_OPERATION) c.rs.pool.push_back(oplit);
+  for (auto w : fused) c.rs.pool.push_back(w);
+  o->nseg = (uint16_t)(c.rs.pool.size() - o->a);
+  return true;
+}
 bool var_anywhere(const Value& v) {
   if (v.t == T::Str) return var_syntax(v.s);
   for (auto& e : v.a) if (var_anywhere(e)) return true;
@@ -1068,7 +1358,11 @@ CondOperand compile_operand(Cx& c, const Value* v, CondText& ct, int side, const
   if (!v || v->t == T::Null) return o;
   if (v->t == T::Str && var_syntax(v->s)) {
     std::vector<std::string> segs;
-    if (!object_var(v->s, segs, &ct.var[side])) throw Fallback{"conditions: variables beyond request.object paths"};
+    if (!object_var(v->s, segs, &ct.var[side])) {
+      if (v->s.find("$(") != std::string::npos || !jmes_var(c, v->s, c.allow_element, &o, &ct.var[side], &c.uses_op))
+        throw Fallback{"conditions: variables beyond request.object paths"};
+      return o;
+    }
     o.kind = OK_PATH;
     o.nseg = (uint16_t)segs.size();
     o.a = (uint32_t)c.rs.pool.size();
@@ -1195,6 +1489,54 @@ uint32_t compile_conds(Cx& c, const Value* doc) {
   return (uint32_t)c.rs.cprogs.size() - 1;
 }
 
+// validate.foreach (validation.go:319-421): entries with a JMESPath-subset list, deny conditions and optional
+// per-element preconditions / elementScope; patterns, nested foreach and context entries stay on the CPU
+uint32_t compile_foreach(Cx& c, const Value& fe, const std::string& message) {
+  if (fe.t != T::Arr || fe.a.empty()) throw Fallback{"foreach"};
+  if (var_syntax(message)) throw Fallback{"foreach: message with variables"};
+  std::vector<ForeachEntry> ents;
+  for (auto& e : fe.a) {
+    if (e.t != T::Obj) throw Fallback{"foreach"};
+    for (auto& kv : e.o)
+      if (kv.first != "list" && kv.first != "deny" && kv.first != "preconditions" && kv.first != "elementScope")
+        throw Fallback{"foreach: " + kv.first};
+    const Value* l = e.get("list");
+    const Value* d = e.get("deny");
+    if (!l || l->t != T::Str || !d || d->t != T::Obj) throw Fallback{"foreach"};
+    ForeachEntry fx{};
+    std::vector<std::string> segs;
+    CondText ct;
+    if (object_var("{{" + l->s + "}}", segs, nullptr)) {  // plain request.object chain
+      fx.list.kind = OK_PATH;
+      fx.list.nseg = (uint16_t)segs.size();
+      fx.list.a = (uint32_t)c.rs.pool.size();
+      for (auto& sg : segs) c.rs.pool.push_back(c.sid(sg));
+    } else {
+      const bool ae = c.allow_element;
+      c.allow_element = false;
+      if (!jmes_var(c, "{{" + l->s + "}}", false, &fx.list, nullptr, &c.uses_op)) throw Fallback{"foreach: list"};
+      c.allow_element = ae;
+    }
+    const Value* es = e.get("elementScope");
+    if (es && es->t != T::Null && es->t != T::Bool) throw Fallback{"foreach: elementScope"};
+    fx.scope = !es || es->t == T::Null ? 0u : es->b ? 2u : 1u;
+    c.allow_element = true;
+    const Value* pre = e.get("preconditions");
+    fx.pre = pre && pre->t != T::Null ? compile_conds(c, pre) : NONE;
+    fx.deny = compile_conds(c, d->get("conditions"));
+    c.allow_element = false;
+    ents.push_back(fx);
+  }
+  const uint32_t at = (uint32_t)c.rs.pool.size();
+  c.rs.pool.push_back((uint32_t)ents.size());
+  for (auto& fx : ents) {
+    uint32_t w[sizeof(ForeachEntry) / 4];
+    memcpy(w, &fx, sizeof fx);
+    for (uint32_t x : w) c.rs.pool.push_back(x);
+  }
+  return at;
+}
+
 // deny message with `{{ request.object... }}` references -> parts (false: other variables, escapes, references)
 bool compile_message(Cx& c, const std::string& msg, RuleMeta& rm) {
   rm.msg_parts.clear();
@@ -1240,8 +1582,6 @@ std::string fallback_reason(const Value& r) {  // validator.validate dispatch (v
   if (!nil(val->get("deny"))) return val->get("deny")->t == T::Obj ? "" : "deny";
   if ((val->get("pattern") && contains_vars(*val->get("pattern"))) || (val->get("anyPattern") && contains_vars(*val->get("anyPattern"))))
     return "variables";
-  if (nil(val->get("pattern")) && nil(val->get("anyPattern")) && nil(val->get("podSecurity")) && nonempty(val->get("foreach")))
-    return "foreach";
   if (!nil(val->get("manifests"))) return "manifests";
   return "";
 }
@@ -1313,6 +1653,8 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
           if (why.empty() && excepted.count({pkey, rm.name})) why = "exception";
           c.nslots = 0;
           c.sites.clear();
+          c.uses_op = false;
+          c.allow_element = false;
           rd.pre = NONE;
           if (why.empty() && !nil(r.get("preconditions"))) rd.pre = compile_conds(c, r.get("preconditions"));
           if (!why.empty()) {
@@ -1344,9 +1686,13 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
             rd.root = compile_pss(c, *val->get("podSecurity"));
             rm.pss_level = val->get("podSecurity")->str_or("level");
             rm.pss_version = val->get("podSecurity")->str_or("version");
+          } else if (val && nonempty(val->get("foreach"))) {
+            rd.kind = RK_FOREACH;
+            rd.root = compile_foreach(c, *val->get("foreach"), rm.message);
           } else {
             continue;  // "invalid validation rule": no response
           }
+          if (c.uses_op) rd.flags |= RD_USES_OPERATION;
           rd.meta_sites = (uint32_t)rs->metas.size();
           rd.nmeta = (uint32_t)c.sites.size();
           for (auto& s : c.sites) rs->metas.push_back(s);

@@ -31,6 +31,7 @@ struct CV {
   uint32_t n;      // CT_ARR: element count
   int64_t i;
   double f;
+  const uint32_t* vl;  // CT_ARR produced by a JMESPath projection: element nodes (JMES_KEYBIT: a map key; NONE: null)
 };
 
 constexpr double TWO63 = 9223372036854775808.0;
@@ -43,6 +44,7 @@ KYV_HD int64_t go_f2i(double f) {  // int64(float64) as amd64 does it (out of ra
 KYV_HD CV cv_node(const Node& n, bool res) {
   CV x;
   x.t = CT_NIL; x.res = res ? 1 : 0; x.b = 0; x.pad = 0; x.sid = KSID(NIL_STR); x.node = NONE; x.n = 0; x.i = 0; x.f = 0;
+  x.vl = nullptr;
   switch (node_type(n)) {
     case N_NULL: break;
     case N_FALSE: x.t = CT_BOOL; x.sid = SID_FALSE; break;
@@ -75,6 +77,17 @@ KYV_HD CV cv_node(const Node& n, bool res) {
 
 // element j of an array operand
 KYV_HD CV cv_elem(const View& v, NodeTab R, const CV& arr, uint32_t j) {
+  if (arr.vl) {
+    const uint32_t e = arr.vl[j];
+    if (e == NONE) return cv_node(Node{N_NULL, 0, 0, 0}, true);
+    if (e & JMES_KEYBIT) {
+      CV x = cv_node(Node{N_NULL, 0, 0, 0}, true);
+      x.t = CT_STR;
+      x.sid = node_key(R[e & ~JMES_KEYBIT]);
+      return x;
+    }
+    return cv_node(R[e], true);
+  }
   if (arr.res) {
     const Node& a = R[arr.node];
     return cv_node(R[a.a + j], true);
@@ -105,7 +118,199 @@ KYV_HD bool cv_operand(const View& v, NodeTab R, const CondOperand& o, CV* out, 
   return true;
 }
 
+
 KYV_HD uint32_t sflags(const View& v, uint32_t sid) { return v.str_flags[sid]; }
+
+// ---------------------------------------------------------------- JMESPath subset (OK_JMES, kyv_layout.h)
+// go-jmespath interpreter semantics on the resource's node table: field of a non-map -> null; a key missing from
+// a map -> null (NotFoundError only for JF_PURE chains); flatten splices arrays and a projection drops null
+// results; keys(@) of a non-map is an error the device leaves to the CPU engine; `|| lit` replaces a false-like
+// result (null, false, "", empty list / map).
+struct JList { uint32_t n; uint32_t e[JMES_MAX_LIST]; };
+struct JRes {
+  bool lst;        // result is the projection list L
+  uint32_t cur;    // single result: node (JMES_KEYBIT: a map key), NONE = null
+  uint32_t lit;    // cnode literal result (|| default, request.operation), NONE otherwise
+};
+enum JStat { JS_OK = 0, JS_NOTFOUND = 1, JS_FB = 2 };
+
+KYV_HD bool j_false(const View& v, NodeTab R, const JRes& r, const JList& L) {  // util.go isFalse
+  if (r.lst) return L.n == 0;
+  if (r.lit != NONE) {
+    const Node& c = v.cnodes[r.lit];
+    switch (node_type(c)) {
+      case N_NULL: case N_FALSE: return true;
+      case N_STR: return c.a == SID_EMPTY;
+      case N_ARR: case N_MAP: return c.b == 0;
+      default: return false;
+    }
+  }
+  if (r.cur == NONE) return true;
+  if (r.cur & JMES_KEYBIT) return node_key(R[r.cur & ~JMES_KEYBIT]) == SID_EMPTY;
+  const Node& n = R[r.cur];
+  switch (node_type(n)) {
+    case N_NULL: case N_FALSE: return true;
+    case N_STR: return n.a == SID_EMPTY;
+    case N_ARR: case N_MAP: return n.b == 0;
+    default: return false;
+  }
+}
+KYV_HD bool j_map(NodeTab R, uint32_t n) { return n != NONE && !(n & JMES_KEYBIT) && node_type(R[n]) == N_MAP; }
+KYV_HD bool j_arr(NodeTab R, uint32_t n) { return n != NONE && !(n & JMES_KEYBIT) && node_type(R[n]) == N_ARR; }
+KYV_HD uint32_t j_field(NodeTab R, uint32_t m, uint32_t key, bool* missing) {
+  *missing = false;
+  if (!j_map(R, m)) return NONE;
+  uint32_t x = map_find(R, m, key);
+  if (x == NONE) { *missing = true; return NONE; }
+  return node_type(R[x]) == N_NULL ? NONE : x;
+}
+
+// run an OK_JMES program; `elem` = the foreach element (node / JMES_KEYBIT key) or NONE.
+// A flatten starts a projection: its right-hand ops run on every element (null ones included: keys(@) of a null
+// element is an error), and the projection's null results are dropped when it ends (next [], ||, or the end).
+KYV_HD void j_drop_nulls(JList& L) {
+  uint32_t w = 0;
+  for (uint32_t j = 0; j < L.n; j++) if (L.e[j] != NONE) L.e[w++] = L.e[j];
+  L.n = w;
+}
+KYV_HD int jmes_run(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, JRes* out, uint32_t* miss) {
+  const uint32_t* p = v.pool + o.a;
+  const uint32_t n = o.nseg, root = p[0] & 0xFFu;
+  const bool pure = (p[0] & JF_PURE) != 0;
+  JRes r;
+  r.lst = false; r.cur = NONE; r.lit = NONE;
+  L.n = 0;
+  bool proj = false;
+  uint32_t i = 1, fields = 0;
+  if (root == JR_OBJECT) r.cur = 0;
+  else if (root == JR_ELEMENT) r.cur = elem;
+  else { r.lit = p[1]; i = 2; }
+  while (i < n) {
+    const uint32_t op = p[i];
+    if (op == JO_FIELD) {
+      const uint32_t key = p[i + 1];
+      i += 2;
+      bool missing;
+      if (!r.lst) {
+        r.cur = j_field(R, r.cur, key, &missing);
+        if (missing && pure) { *miss = fields; return JS_NOTFOUND; }
+      } else {
+        for (uint32_t j = 0; j < L.n; j++) L.e[j] = j_field(R, L.e[j], key, &missing);
+      }
+      fields++;
+    } else if (op == JO_MULTI) {
+      const uint32_t m = p[i + 1];
+      if (r.cur != NONE) {  // multi-select on null is null
+        if (m > JMES_MAX_LIST) return JS_FB;
+        bool missing;
+        for (uint32_t j = 0; j < m; j++) L.e[j] = j_field(R, r.cur, p[i + 2 + j], &missing);
+        L.n = m;
+        r.lst = true;
+      }
+      i += 2 + m;
+    } else if (op == JO_FLAT) {
+      i++;
+      if (!r.lst) {
+        if (!j_arr(R, r.cur)) { r.cur = NONE; proj = false; continue; }  // flatten of a non-list: null
+        const Node& a = R[r.cur];
+        if (a.b > JMES_MAX_LIST) return JS_FB;
+        for (uint32_t j = 0; j < a.b; j++) L.e[j] = node_type(R[a.a + j]) == N_NULL ? NONE : a.a + j;
+        L.n = a.b;
+        r.lst = true;
+      } else {
+        if (proj) j_drop_nulls(L);
+        uint32_t t[JMES_MAX_LIST];
+        const uint32_t tn = L.n;
+        for (uint32_t j = 0; j < tn; j++) t[j] = L.e[j];
+        uint32_t w = 0;
+        for (uint32_t j = 0; j < tn; j++) {
+          const uint32_t x = t[j];
+          if (j_arr(R, x)) {
+            const Node& a = R[x];
+            for (uint32_t q = 0; q < a.b; q++) {
+              if (w >= JMES_MAX_LIST) return JS_FB;
+              L.e[w++] = node_type(R[a.a + q]) == N_NULL ? NONE : a.a + q;
+            }
+          } else {
+            if (w >= JMES_MAX_LIST) return JS_FB;
+            L.e[w++] = x;
+          }
+        }
+        L.n = w;
+      }
+      proj = true;
+    } else if (op == JO_KEYS) {
+      i++;
+      if (r.lst || !j_map(R, r.cur)) return JS_FB;  // keys() of a non-object: the reference errors
+      const Node& m = R[r.cur];
+      if (m.b > JMES_MAX_LIST) return JS_FB;
+      for (uint32_t j = 0; j < m.b; j++) L.e[j] = (m.a + j) | JMES_KEYBIT;
+      L.n = m.b;
+      r.lst = true;
+    } else if (op == JO_KEYS_FLAT) {
+      i++;
+      if (!r.lst) continue;  // the projection's left side was null: so is the result
+      uint32_t t[JMES_MAX_LIST];
+      const uint32_t tn = L.n;
+      for (uint32_t j = 0; j < tn; j++) t[j] = L.e[j];
+      uint32_t w = 0;
+      for (uint32_t j = 0; j < tn; j++) {
+        if (!j_map(R, t[j])) return JS_FB;  // keys() of null / a non-object element: the reference errors
+        const Node& m = R[t[j]];
+        for (uint32_t q = 0; q < m.b; q++) {
+          if (w >= JMES_MAX_LIST) return JS_FB;
+          L.e[w++] = (m.a + q) | JMES_KEYBIT;
+        }
+      }
+      L.n = w;
+      proj = true;
+    } else if (op == JO_OR) {
+      const uint32_t lit = p[i + 1];
+      i += 2;
+      if (proj) { j_drop_nulls(L); proj = false; }
+      if (j_false(v, R, r, L)) { r.lst = false; r.cur = NONE; r.lit = lit; }
+    } else {
+      return JS_FB;
+    }
+  }
+  if (proj) j_drop_nulls(L);
+  *out = r;
+  return JS_OK;
+}
+
+KYV_HD CV jres_cv(const View& v, NodeTab R, const JRes& r, const JList& L) {
+  if (r.lit != NONE) {
+    CV x = cv_node(v.cnodes[r.lit], false);
+    if (x.t == CT_ARR) x.node = r.lit;
+    return x;
+  }
+  if (r.lst) {
+    CV x = cv_node(Node{N_NULL, 0, 0, 0}, true);
+    x.t = CT_ARR; x.sid = NONE; x.n = L.n; x.vl = L.e;
+    return x;
+  }
+  if (r.cur == NONE) return cv_node(Node{N_NULL, 0, 0, 0}, true);
+  if (r.cur & JMES_KEYBIT) {
+    CV x = cv_node(Node{N_NULL, 0, 0, 0}, true);
+    x.t = CT_STR;
+    x.sid = node_key(R[r.cur & ~JMES_KEYBIT]);
+    return x;
+  }
+  CV x = cv_node(R[r.cur], true);
+  if (x.t == CT_ARR) x.node = r.cur;
+  return x;
+}
+
+// any operand -> CV (JS_OK / JS_NOTFOUND with *miss / JS_FB); L backs a projection list result
+KYV_HD int operand_cv(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, CV* out, uint32_t* miss) {
+  if (o.kind != OK_JMES) return cv_operand(v, R, o, out, miss) ? JS_OK : JS_NOTFOUND;
+  JRes r;
+  const int st = jmes_run(v, R, o, elem, L, &r, miss);
+  if (st != JS_OK) return st;
+  *out = jres_cv(v, R, r, L);
+  return JS_OK;
+}
+
 
 // operator.parseDuration (operator.go:94-138): 1 both durations (seconds), 0 not durations
 KYV_HD int dur_side(const View& v, const CV& x, int64_t* d, bool* have) {
@@ -444,7 +649,8 @@ KYV_HD int eval_cond(const View& v, NodeTab R, const Cond& c, const CV& k, const
 // error), then any/all evaluation (evaluate.go:42-69). Returns CR_TRUE / CR_FALSE / CR_FB / CR_PANIC, or
 // CP_ERROR with *err_cond / *err_side / *err_seg naming the first unresolved reference (for the host message).
 constexpr int CP_ERROR = 5;
-KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond, uint32_t* err_side, uint32_t* err_seg) {
+KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond, uint32_t* err_side, uint32_t* err_seg,
+                     uint32_t elem = NONE) {
   const CondProg& p = v.cprogs[prog];
   const uint32_t nany = p.nany == NONE ? 0u : p.nany;
   for (uint32_t blk = 0; blk < 2; blk++) {
@@ -459,6 +665,12 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
           *err_cond = c0 + i; *err_side = side; *err_seg = miss;
           return CP_ERROR;
         }
+        if (o.kind == OK_JMES) {
+          JList L;
+          const int st = operand_cv(v, R, o, elem, L, &tmp, &miss);
+          if (st == JS_FB) return CR_FB;
+          if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
+        }
       }
     }
   }
@@ -466,8 +678,9 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
     const Cond& c = v.conds[ci];
     CV k, x;
     uint32_t miss;
-    cv_operand(v, R, c.key, &k, &miss);
-    cv_operand(v, R, c.value, &x, &miss);
+    JList lk, lx;
+    operand_cv(v, R, c.key, elem, lk, &k, &miss);
+    operand_cv(v, R, c.value, elem, lx, &x, &miss);
     return eval_cond(v, R, c, k, x);
   };
   if (p.nany != NONE) {

@@ -283,7 +283,7 @@ struct PssDesc {
 
 // ---------------------------------------------------------------- rules
 enum RuleKind : uint8_t { RK_NONE = 0, RK_PATTERN = 1, RK_ANYPATTERN = 2, RK_PSS = 3, RK_FALLBACK = 4, RK_PANIC = 5,
-                          RK_ERROR = 6, RK_DENY = 7 };
+                          RK_ERROR = 6, RK_DENY = 7, RK_FOREACH = 8 };
 
 // ---------------------------------------------------------------- conditions (validate.deny, rule preconditions)
 // A condition program is the any/all form of pkg/engine/variables/evaluate.go:42-69 (the old list form is an `all`
@@ -291,7 +291,22 @@ enum RuleKind : uint8_t { RK_NONE = 0, RK_PATTERN = 1, RK_ANYPATTERN = 2, RK_PSS
 // Condition.GetKey json round trip) or `{{ request.object.<path> }}` references resolved per resource.
 enum CondOp : uint8_t { CO_EQ = 0, CO_NE = 1, CO_IN = 2, CO_NOTIN = 3, CO_ANYIN = 4, CO_ALLIN = 5, CO_ANYNOTIN = 6,
                         CO_ALLNOTIN = 7, CO_GT = 8, CO_GE = 9, CO_LT = 10, CO_LE = 11, CO_FALSE = 12 };
-enum OperandKind : uint8_t { OK_NIL = 0, OK_LIT = 1, OK_PATH = 2 };
+enum OperandKind : uint8_t { OK_NIL = 0, OK_LIT = 1, OK_PATH = 2, OK_JMES = 3 };
+
+// JMESPath-subset operand program (OK_JMES; pool words at CondOperand.a, CondOperand.nseg words): go-jmespath
+// sub-expressions, multi-select lists, flatten projections, keys(@) and a trailing `|| <literal>`, linearised at
+// compile time. Word 0 is the root; then ops (opcode word + operands). Inside these programs a key missing from a
+// map is null (the kyverno/go-jmespath fork's NotFoundError applies to plain field chains only: JR flag JF_PURE).
+enum JmesRoot : uint32_t { JR_OBJECT = 0, JR_ELEMENT = 1, JR_OPERATION = 2 };
+constexpr uint32_t JF_PURE = 1u << 8;      // root word flag: plain field chain (missing key -> NotFoundError)
+enum JmesOp : uint32_t { JO_FIELD = 1,     // + key sid
+                         JO_MULTI = 2,     // + n, n key sids   (multi-select list of fields)
+                         JO_FLAT = 3,      // flatten projection (nulls dropped)
+                         JO_KEYS = 4,      // keys(@) of the current map
+                         JO_KEYS_FLAT = 5, // projection keys(@) then flatten
+                         JO_OR = 6 };      // + cnode literal: `|| <literal>` when the result is false-like
+constexpr uint32_t JMES_MAX_LIST = 32;     // virtual list capacity (longer -> CPU fallback)
+constexpr uint32_t JMES_KEYBIT = 1u << 31; // virtual list element: the key of map entry node (index & ~KEYBIT)
 enum StrValFlag : uint8_t { SV_LIST = 1, SV_JSON = 2, SV_RANGE = 4 };  // literal string value: json []string ok,
                                                                         // json.Valid, InRange operator pattern
 struct CondOperand {     // 16 bytes
@@ -315,7 +330,17 @@ struct CondProg {        // 16 bytes
 };
 static_assert(sizeof(Cond) == 48, "cond size");
 
-enum RuleFlag : uint8_t { RD_GATE_EXACT = 1 };  // match == the batch's kind gate (kinds-only filters, no exclude)
+enum RuleFlag : uint8_t { RD_GATE_EXACT = 1,    // match == the batch's kind gate (kinds-only filters, no exclude)
+                          RD_USES_OPERATION = 2 // a condition reads request.operation (background: "CREATE")
+};
+
+// foreach validation (validation.go:319-421), RK_FOREACH: RuleDesc.root = pool offset of [n, entry offsets...];
+// an entry is [list operand (pool offset of a CondOperand copy), preconditions CondProg or NONE, deny CondProg,
+// elementScope (0 unset, 1 false, 2 true)]
+struct ForeachEntry {
+  CondOperand list;
+  uint32_t pre, deny, scope, pad;
+};
 
 struct RuleDesc {
   uint8_t kind;
@@ -339,6 +364,8 @@ constexpr int NSTATUS = 8;
 // high 5 bits of a status byte: the passing anyPattern alternative (ST_PASS), or ST_MARK_PRE on a skip / error that
 // came from the rule's preconditions ("preconditions not met", validation.go:286-288)
 constexpr uint8_t ST_MARK_PRE = 30u << 3;
+// on an error of a foreach rule: an element that is not a map under elementScope: true (validation.go:395-397)
+constexpr uint8_t ST_MARK_SCOPE = 29u << 3;
 
 constexpr int MAX_IDX = 4;
 constexpr int MAX_SLOTS = 2;

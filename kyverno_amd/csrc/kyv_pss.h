@@ -490,6 +490,67 @@ KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const R
 namespace kyv {
 
 
+// validateForEach (validation.go:319-341) + validateElements (:343-381) for deny entries: each element of the
+// evaluated list (evaluateList, utils.go:343-355: a non-list result is a one-element list; a query error skips
+// the entry) runs its preconditions (not met -> element skipped) and deny conditions (true -> the rule fails);
+// an error ends the rule only on the last element; no element applied -> skip.
+KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root) {
+  const uint32_t nent = v.pool[root];
+  uint32_t applied = 0;
+  for (uint32_t e = 0; e < nent; e++) {
+    const ForeachEntry fe = *(const ForeachEntry*)(v.pool + root + 1 + e * (sizeof(ForeachEntry) / 4));
+    JList L;
+    JRes lr;
+    lr.lst = false; lr.cur = NONE; lr.lit = NONE;
+    uint32_t miss = 0;
+    if (fe.list.kind == OK_PATH) {
+      uint32_t cur = 0;
+      bool nf = false;
+      for (uint32_t s = 0; s < fe.list.nseg && cur != NONE; s++) {
+        bool missing;
+        cur = j_field(R, cur, v.pool[fe.list.a + s], &missing);
+        if (missing) nf = true;
+      }
+      if (nf) continue;  // NotFoundError: "failed to evaluate list" -> next entry
+      lr.cur = cur;
+    } else {
+      const int st = jmes_run(v, R, fe.list, NONE, L, &lr, &miss);
+      if (st == JS_NOTFOUND) continue;
+      if (st == JS_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
+      if (lr.lit != NONE) return KYV_WHY(FBW_COND), ST_FALLBACK;  // literal list elements: not restated
+    }
+    // elements: the projection list, an array's items, or the single value
+    const bool arr = !lr.lst && j_arr(R, lr.cur);
+    const uint32_t n = lr.lst ? L.n : arr ? R[lr.cur].b : 1u;
+    uint32_t count = 0;
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t el = lr.lst ? L.e[j] : arr ? R[lr.cur].a + j : lr.cur;
+      if (el == NONE || (!(el & JMES_KEYBIT) && node_type(R[el]) == N_NULL)) continue;
+      if (fe.scope == 2 && !j_map(R, el)) return ST_ERROR | ST_MARK_SCOPE;  // addElementToContext error
+      uint32_t ec, es, eg;
+      bool err = false;
+      if (fe.pre != NONE) {
+        const int c = eval_prog(v, R, fe.pre, &ec, &es, &eg, el);
+        if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
+        if (c == CR_PANIC) return ST_PANIC;
+        if (c == CR_FALSE) continue;  // "preconditions not met": skip, not applied
+        err = c == CP_ERROR;
+      }
+      if (!err) {
+        const int c = eval_prog(v, R, fe.deny, &ec, &es, &eg, el);
+        if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
+        if (c == CR_PANIC) return ST_PANIC;
+        if (c == CR_TRUE) return ST_FAIL;
+        if (c != CP_ERROR) { count++; continue; }
+      }
+      if (j + 1 < n) continue;  // an error ends the rule only on the last element
+      return ST_ERROR;
+    }
+    applied += count;
+  }
+  return applied ? ST_PASS : ST_SKIP;
+}
+
 // Match + dispatch of one pair (validation.go:134-183, :276-317). Returns the verdict, or sets *walk for a
 // pattern / anyPattern pair whose verdict comes from the pattern walk (pair_walk).
 KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k, uint32_t* pss_fails, bool* walk) {
@@ -531,6 +592,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
       return c == CR_TRUE ? ST_FAIL : ST_PASS;
     }
     case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
+    case RK_FOREACH: return eval_foreach(v, R, rd.root);
     case RK_PATTERN: case RK_ANYPATTERN:
       if (h.flags & RF_MAGIC) return KYV_WHY(FBW_PHRASE), ST_FALLBACK;
       *walk = true;

@@ -50,7 +50,8 @@ class Ruleset:
                 L.kyv_ruleset_rule_kinds(h, k, kb, len(kb), ctypes.byref(hv))
             kinds = kb.value.decode().split("\n") if n > 0 else []
             self.rules.append({"name": ri.name.decode(), "policy": ri.policy, "kind": K.RULE_KINDS.get(ri.kind, "?"),
-                               "reason": ri.reason.decode(), "match_kinds": kinds, "has_validate": bool(hv.value)})
+                               "reason": ri.reason.decode(), "match_kinds": kinds, "has_validate": bool(hv.value),
+                               "uses_operation": bool(L.kyv_ruleset_rule_flags(h, k) & K.RULE_USES_OPERATION)})
         self.policies = []
         for p in range(L.kyv_ruleset_num_policies(h)):
             pi = K.PolicyInfo()

@@ -1,5 +1,6 @@
 // ORACLE — test infrastructure only (see ojson.h header). Conditions (deny / preconditions); see ocond.h.
 #include "ocond.h"
+#include "ojmes.h"
 
 #include <cmath>
 
@@ -585,25 +586,39 @@ static bool has_var_syntax(const std::string& s) {
   return s.find("{{") != std::string::npos || s.find("$(") != std::string::npos;
 }
 
-bool conditions_supported(const VP& v) {
+// a string that is exactly one `{{ <JMESPath> }}` variable (no nested braces) -> the trimmed expression
+static bool single_var(const std::string& s, std::string* expr) {
+  if (s.size() < 4 || s.compare(0, 2, "{{") != 0 || s.compare(s.size() - 2, 2, "}}") != 0) return false;
+  std::string inner = s.substr(2, s.size() - 4);
+  if (inner.find('{') != std::string::npos || inner.find('}') != std::string::npos) return false;
+  *expr = gou::trim_space(inner);
+  return true;
+}
+
+static bool conditions_supported_in(const VP& v, bool allow_element) {
   if (!v) return true;
   if (v->t == T::Str) {
     if (!has_var_syntax(v->s)) return true;
     std::vector<std::string> segs;
-    return parse_object_var(v->s, segs);
+    if (parse_object_var(v->s, segs)) return true;
+    std::string expr;
+    return v->s.find("$(") == std::string::npos && single_var(v->s, &expr) && jmes_supported(expr, allow_element);
   }
-  if (v->t == T::Arr) { for (auto& e : v->a) if (!conditions_supported(e)) return false; return true; }
+  if (v->t == T::Arr) { for (auto& e : v->a) if (!conditions_supported_in(e, allow_element)) return false; return true; }
   if (v->t == T::Obj) {
     for (auto& kv : v->o) {
       if (has_var_syntax(kv.first)) return false;
       if (kv.first == "operator" && kv.second && kv.second->t == T::Str &&
           lower(kv.second->s).compare(0, 8, "duration") == 0)
         return false;  // deprecated Duration* operators: not in the device subset
-      if (!conditions_supported(kv.second)) return false;
+      if (!conditions_supported_in(kv.second, allow_element)) return false;
     }
   }
   return true;
 }
+
+bool conditions_supported(const VP& v) { return conditions_supported_in(v, false); }
+bool conditions_supported_element(const VP& v) { return conditions_supported_in(v, true); }
 
 static VP floats(const VP& v) {  // encoding/json decode of the JSON context: every number float64
   if (!v) return Value::null();
@@ -631,16 +646,18 @@ static std::string var_text(const std::string& s) {  // replaceBracesAndTrimSpac
 struct SubstErr {
   int n = 0;
   std::string first;
+  bool unpinned = false;
 };
+struct VarCtx { VP resource; VP element; int64_t index; };
 // substituteVariablesIfAny over the condition document (vars.go:352-431); data.Path is the JSON pointer of the
 // string ("/0/key", "/any/1/value"; '/' in keys escaped as "\/", traverse.go:93)
-static VP substitute(const VP& v, const VP& resource, const std::string& path, SubstErr& e) {
+static VP substitute(const VP& v, const VarCtx& cx, const std::string& path, SubstErr& e) {
   if (!v) return v;
   if (v->t == T::Str) {
     std::vector<std::string> segs;
     if (has_var_syntax(v->s) && parse_object_var(v->s, segs)) {
       std::string missing;
-      VP r = resolve(segs, resource, &missing);
+      VP r = resolve(segs, cx.resource, &missing);
       if (!r) {
         if (e.n++ == 0)
           e.first = "failed to resolve " + var_text(v->s) + " at path " + path +
@@ -649,11 +666,25 @@ static VP substitute(const VP& v, const VP& resource, const std::string& path, S
       }
       return r;
     }
+    std::string expr;
+    if (has_var_syntax(v->s) && single_var(v->s, &expr)) {  // JMESPath subset (ojmes.h)
+      try {
+        return jmes_query(expr, cx.resource, cx.element, cx.index);
+      } catch (JmesNotFound& nf) {
+        if (e.n++ == 0)
+          e.first = "failed to resolve " + expr + " at path " + path + ": JMESPath query failed: Unknown key \"" +
+                    nf.key + "\" in path";
+      } catch (JmesError& je) {
+        if (e.n++ == 0) e.first = "failed to resolve " + expr + " at path " + path + ": " + je.msg;
+        e.unpinned = true;
+      }
+      return Value::null();
+    }
     return v;
   }
   if (v->t == T::Arr) {
     auto o = Value::arr();
-    for (size_t i = 0; i < v->a.size(); i++) o->a.push_back(substitute(v->a[i], resource, path + "/" + std::to_string(i), e));
+    for (size_t i = 0; i < v->a.size(); i++) o->a.push_back(substitute(v->a[i], cx, path + "/" + std::to_string(i), e));
     return o;
   }
   if (v->t == T::Obj) {
@@ -661,7 +692,7 @@ static VP substitute(const VP& v, const VP& resource, const std::string& path, S
     for (auto& kv : v->o) {
       std::string k;
       for (char c : kv.first) { if (c == '/') k += "\\/"; else k += c; }
-      o->o[kv.first] = substitute(kv.second, resource, path + "/" + k, e);
+      o->o[kv.first] = substitute(kv.second, cx, path + "/" + k, e);
     }
     return o;
   }
@@ -725,11 +756,15 @@ static bool condition_fields(const VP& c, VP& key, std::string& op, VP& value) {
 }
 
 CondResult eval_conditions(const VP& conditions, const VP& resource) {
+  return eval_conditions_element(conditions, resource, nullptr, 0);
+}
+
+CondResult eval_conditions_element(const VP& conditions, const VP& resource, const VP& element, int64_t index) {
   CondResult r;
-  if (!conditions_supported(conditions)) { r.r = CondOutcome::Unsupported; return r; }
+  if (!conditions_supported_in(conditions, element != nullptr)) { r.r = CondOutcome::Unsupported; return r; }
   SubstErr se;
-  VP doc = substitute(conditions, resource, "", se);
-  if (se.n) { r.r = CondOutcome::Error; r.err = se.first; r.err_unpinned = se.n > 1; return r; }
+  VP doc = substitute(conditions, VarCtx{resource, element, index}, "", se);
+  if (se.n) { r.r = CondOutcome::Error; r.err = se.first; r.err_unpinned = se.n > 1 || se.unpinned; return r; }
   if (isnil(doc)) { r.r = CondOutcome::True; return r; }  // null -> empty old-style list -> all true
   if (doc->t == T::Arr) {  // []Condition (evaluate.go:72-81), operators checked exactly (json.go:57-72)
     std::vector<std::tuple<VP, std::string, VP>> cs;

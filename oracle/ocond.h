@@ -8,9 +8,10 @@
 //   pkg/engine/variables/vars.go:352-431            (substituteVariablesIfAny, restricted: see below)
 //   pkg/engine/validation.go:276-290,437-479        (preconditions -> skip, validateDeny, getDenyMessage)
 //
-// Variable support is the subset the device compiles: a string that is exactly one `{{ request.object<path> }}`
-// where <path> is a dotted chain of JMESPath identifiers / quoted identifiers. Anything else containing `{{` or
-// `$(` is reported unsupported (those rules stay on the reference's CPU engine).
+// Variable support is the subset the device compiles: a string that is exactly one `{{ <expr> }}` where <expr> is
+// a dotted chain of JMESPath identifiers from request.object, or an expression of the JMESPath subset of ojmes.h
+// (projections, multi-select lists, `||` literals, keys()) from request.object / request.operation / element.
+// Anything else containing `{{` or `$(` is reported unsupported (those rules stay on the reference's CPU engine).
 #pragma once
 #include <string>
 
@@ -38,6 +39,10 @@ struct CondResult {
 // whose request.object is `resource`. `conditions` is the raw JSON of rule.preconditions / deny.conditions
 // (nullptr when absent).
 CondResult eval_conditions(const oj::VP& conditions, const oj::VP& resource);
+// same inside a foreach: `element` / `elementIndex` bound (validation.go:383-413 addElementToContext)
+CondResult eval_conditions_element(const oj::VP& conditions, const oj::VP& resource, const oj::VP& element,
+                                   int64_t index);
+bool conditions_supported_element(const oj::VP& conditions);
 
 // getDenyMessage's SubstituteAll(msg) (validation.go:466-479) for messages whose variables are request.object
 // references; *unpinned when the message uses anything else (other variables, references, escapes).

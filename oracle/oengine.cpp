@@ -9,6 +9,7 @@
 //   pkg/autogen/autogen.go:70-314 + rule.go:73-319 (ComputeRules)
 //   k8s.io/apimachinery v0.26.1 labels selectors (LabelSelectorAsSelector / Requirement.Matches) — restated
 #include "oengine.h"
+#include "ojmes.h"
 
 #include <algorithm>
 #include <set>
@@ -617,6 +618,108 @@ static bool contains_vars(const VP& v) {
   return false;
 }
 
+// foreach entries the restatement covers: a JMESPath-subset list and deny conditions (+ per-element preconditions,
+// elementScope) over request.object / element; patterns, nested foreach and context entries are not restated
+static bool foreach_supported(const VP& val) {
+  VP fe = val->get("foreach");
+  if (!fe || fe->t != T::Arr) return false;
+  for (auto& e : fe->a) {
+    if (!e || e->t != T::Obj) return false;
+    for (auto& kv : e->o)
+      if (kv.first != "list" && kv.first != "deny" && kv.first != "preconditions" && kv.first != "elementScope")
+        return false;
+    VP l = e->get("list");
+    if (!l || l->t != T::Str || !jmes_supported(l->s, false)) return false;
+    VP d = e->get("deny");
+    if (isnil(d) || d->t != T::Obj || !conditions_supported_element(d->get("conditions"))) return false;
+    if (!conditions_supported_element(e->get("preconditions"))) return false;
+    VP es = e->get("elementScope");
+    if (!isnil(es) && es->t != T::Bool) return false;
+    std::string msg = oj::get_str(val, "message");
+    if (msg.find("{{") != std::string::npos || msg.find("$(") != std::string::npos) return false;
+  }
+  return true;
+}
+
+// Go %T of a decoded JSON element (addElementToContext error text, validation.go:395-397)
+static std::string go_type_name(const VP& v) {
+  if (isnil(v)) return "<nil>";
+  switch (v->t) {
+    case T::Bool: return "bool";
+    case T::Int: case T::Float: return "float64";
+    case T::Str: return "string";
+    case T::Arr: return "[]interface {}";
+    case T::Obj: return "map[string]interface {}";
+    default: return "<nil>";
+  }
+}
+
+// validateForEach (validation.go:319-341) + validateElements (:343-381) for deny entries: every element of the
+// evaluated list runs its own validator (preconditions -> skip; deny -> fail / pass; errors), fail ends the rule,
+// an error ends it only on the last element, no applied element at all -> "rule skipped"
+static RuleResult validate_foreach(const VP& rule, const VP& resource, RuleResult out) {
+  VP val = rule->get("validate");
+  const std::string msg = oj::get_str(val, "message");
+  int applyCount = 0;
+  for (auto& fe : val->get("foreach")->a) {
+    VP list;
+    try {
+      list = jmes_query(fe->get("list")->s, resource, nullptr, 0);  // evaluateList (utils.go:343-355)
+    } catch (JmesNotFound&) {
+      continue;
+    } catch (JmesError&) {
+      continue;
+    }
+    std::vector<VP> elements;
+    if (list && list->t == T::Arr) elements = list->a; else elements.push_back(list);
+    VP scope = fe->get("elementScope");
+    int count = 0;
+    for (size_t idx = 0; idx < elements.size(); idx++) {
+      const VP& el = elements[idx];
+      if (isnil(el)) continue;
+      if (!isnil(scope) && scope->b && el->t != T::Obj) {
+        out.status = "error";
+        out.message = "failed to process foreach: cannot use elementScope=true foreach rules for elements that are not "
+                      "maps, expected type=map got type=" + go_type_name(el);
+        return out;
+      }
+      std::string st, m;
+      CondResult pc = eval_conditions_element(fe->get("preconditions"), resource, el, (int64_t)idx);
+      if (pc.r == CondOutcome::Unsupported) { out.status = "unsupported"; out.message = "foreach preconditions"; return out; }
+      if (pc.r == CondOutcome::Error) {
+        st = "error";
+        m = "failed to evaluate preconditions: failed to substitute variables in preconditions: " + pc.err;
+        out.message_unpinned |= pc.err_unpinned;
+      } else if (pc.r == CondOutcome::False) {
+        continue;  // "preconditions not met" -> skip
+      } else {
+        CondResult c = eval_conditions_element(fe->get("deny")->get("conditions"), resource, el, (int64_t)idx);
+        if (c.r == CondOutcome::Unsupported) { out.status = "unsupported"; out.message = "foreach deny"; return out; }
+        if (c.r == CondOutcome::Error) {
+          st = "error";
+          m = "failed to substitute variables in deny conditions: " + c.err;
+          out.message_unpinned |= c.err_unpinned;
+        } else if (c.r == CondOutcome::True) {
+          st = "fail";
+          m = msg.empty() ? "validation error: rule " + out.name + " failed" : msg;
+        } else {
+          count++;
+          continue;
+        }
+      }
+      if (st == "error" && idx + 1 < elements.size()) continue;
+      out.status = st;
+      out.message = "validation failure: " + m;
+      return out;
+    }
+    applyCount += count;
+  }
+  if (applyCount == 0) { out.status = "skip"; out.message = "rule skipped"; return out; }
+  out.status = "pass";
+  out.message = "rule passed";
+  return out;
+}
+
 std::string rule_unsupported_reason(const VP& rule) {
   VP val = rule->get("validate");
   if (has_nonempty(rule, "context")) return "context";
@@ -628,7 +731,8 @@ std::string rule_unsupported_reason(const VP& rule) {
     if (d->t != T::Obj || !conditions_supported(d->get("conditions"))) return "deny";
   }
   if (contains_vars(val->get("pattern")) || contains_vars(val->get("anyPattern"))) return "variables";
-  if (isnil(val->get("pattern")) && isnil(val->get("anyPattern")) && isnil(val->get("podSecurity")) && has_nonempty(val, "foreach"))
+  if (isnil(val->get("pattern")) && isnil(val->get("anyPattern")) && isnil(val->get("podSecurity")) && has_nonempty(val, "foreach") &&
+      !foreach_supported(val))
     return "foreach";
   if (!isnil(val->get("manifests"))) return "manifests";
   return "";
@@ -741,6 +845,9 @@ static RuleResult validate_rule_body(const VP& rule, const VP& resource) {
       out.message = msg;
       return out;
     }
+    if (isnil(val->get("pattern")) && isnil(val->get("anyPattern")) && isnil(val->get("podSecurity")) &&
+        has_nonempty(val, "foreach"))
+      return validate_foreach(rule, resource, out);
     if (!isnil(val->get("podSecurity"))) {  // validatePodSecurity (validation.go:535-566)
       // getSpec (validation.go:481-532): typed decode of the whole object; a non-object on the way to the
       // pod template is a decode error

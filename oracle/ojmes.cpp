@@ -1,0 +1,315 @@
+// ORACLE — test infrastructure only (see ojson.h header). JMESPath subset; see ojmes.h.
+#include "ojmes.h"
+
+#include <functional>
+#include <memory>
+#include <vector>
+
+#include "goutil.h"
+
+namespace orc {
+using oj::T;
+using oj::Value;
+using oj::VP;
+
+namespace {
+
+// ---------------------------------------------------------------- lexer (go-jmespath lexer.go, subset)
+enum Tok { tEOF, tIdent, tQuoted, tDot, tLbracket, tRbracket, tFlatten, tComma, tLparen, tRparen, tCurrent, tOr,
+           tRaw, tJSON, tOther };
+struct Token { Tok t; std::string v; };
+
+std::vector<Token> lex(const std::string& s) {
+  std::vector<Token> out;
+  size_t i = 0;
+  auto ident_start = [](char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '_'; };
+  auto ident = [&](char c) { return ident_start(c) || (c >= '0' && c <= '9'); };
+  while (i < s.size()) {
+    char c = s[i];
+    if (c == ' ' || c == '\t' || c == '\n' || c == '\r') { i++; continue; }
+    if (ident_start(c)) {
+      size_t j = i;
+      while (j < s.size() && ident(s[j])) j++;
+      out.push_back({tIdent, s.substr(i, j - i)});
+      i = j;
+    } else if (c == '"') {
+      size_t j = i + 1;
+      while (j < s.size() && s[j] != '"') { if (s[j] == '\\') throw JmesUnsupported{"escaped quoted identifier"}; j++; }
+      if (j >= s.size()) throw JmesUnsupported{"unterminated quoted identifier"};
+      out.push_back({tQuoted, s.substr(i + 1, j - i - 1)});
+      i = j + 1;
+    } else if (c == '\'') {
+      size_t j = i + 1;
+      while (j < s.size() && s[j] != '\'') { if (s[j] == '\\') throw JmesUnsupported{"escaped raw string"}; j++; }
+      if (j >= s.size()) throw JmesUnsupported{"unterminated raw string"};
+      out.push_back({tRaw, s.substr(i + 1, j - i - 1)});
+      i = j + 1;
+    } else if (c == '`') {
+      size_t j = i + 1;
+      while (j < s.size() && s[j] != '`') { if (s[j] == '\\') throw JmesUnsupported{"escaped JSON literal"}; j++; }
+      if (j >= s.size()) throw JmesUnsupported{"unterminated JSON literal"};
+      out.push_back({tJSON, s.substr(i + 1, j - i - 1)});
+      i = j + 1;
+    } else if (c == '.') { out.push_back({tDot, "."}); i++; }
+    else if (c == '[') {
+      if (i + 1 < s.size() && s[i + 1] == ']') { out.push_back({tFlatten, "[]"}); i += 2; }
+      else { out.push_back({tLbracket, "["}); i++; }
+    } else if (c == ']') { out.push_back({tRbracket, "]"}); i++; }
+    else if (c == ',') { out.push_back({tComma, ","}); i++; }
+    else if (c == '(') { out.push_back({tLparen, "("}); i++; }
+    else if (c == ')') { out.push_back({tRparen, ")"}); i++; }
+    else if (c == '@') { out.push_back({tCurrent, "@"}); i++; }
+    else if (c == '|' && i + 1 < s.size() && s[i + 1] == '|') { out.push_back({tOr, "||"}); i += 2; }
+    else throw JmesUnsupported{std::string("token '") + c + "'"};
+  }
+  out.push_back({tEOF, ""});
+  return out;
+}
+
+// ---------------------------------------------------------------- parser (go-jmespath parser.go, subset)
+enum NodeKind { NField, NSubexpr, NProjection, NFlatten, NMultiList, NFunction, NCurrent, NIdentity, NOr, NLiteral };
+struct Node {
+  NodeKind k;
+  std::string name;  // NField / NFunction
+  VP lit;            // NLiteral
+  std::vector<std::shared_ptr<Node>> kids;
+};
+using NP = std::shared_ptr<Node>;
+NP mk(NodeKind k, std::vector<NP> kids = {}, const std::string& name = "") {
+  auto n = std::make_shared<Node>();
+  n->k = k;
+  n->kids = std::move(kids);
+  n->name = name;
+  return n;
+}
+
+int binding_power(Tok t) {  // parser.go bindingPowers (tokens outside the subset never reach here)
+  switch (t) {
+    case tOr: return 2;
+    case tFlatten: return 9;
+    case tDot: return 40;
+    case tLbracket: return 55;
+    case tLparen: return 60;
+    default: return 0;
+  }
+}
+
+struct Parser {
+  std::vector<Token> toks;
+  size_t at = 0;
+  Tok look() const { return toks[at].t; }
+  Token next() { return toks[at++]; }
+  void match(Tok t) { if (look() != t) throw JmesUnsupported{"syntax"}; at++; }
+
+  NP expr(int bp) {
+    NP left = nud(next());
+    while (bp < binding_power(look())) left = led(next(), left);
+    return left;
+  }
+  NP nud(const Token& t) {
+    switch (t.t) {
+      case tIdent: return mk(NField, {}, t.v);
+      case tQuoted:
+        if (look() == tLparen) throw JmesUnsupported{"quoted identifier as function name"};
+        return mk(NField, {}, t.v);
+      case tCurrent: return mk(NCurrent);
+      case tRaw: { auto n = mk(NLiteral); n->lit = Value::str(t.v); return n; }
+      case tJSON: {
+        auto n = mk(NLiteral);
+        try { n->lit = oj::parse(t.v, true); } catch (...) { throw JmesUnsupported{"JSON literal"}; }
+        return n;
+      }
+      case tFlatten: {  // nud(tFlatten): projection over the flattened current node
+        NP left = mk(NFlatten, {mk(NIdentity)});
+        return mk(NProjection, {left, projection_rhs(binding_power(tFlatten))});
+      }
+      case tLbracket:
+        return multi_list();
+      default: throw JmesUnsupported{"expression start"};
+    }
+  }
+  NP led(const Token& t, NP left) {
+    switch (t.t) {
+      case tDot: return mk(NSubexpr, {left, dot_rhs(binding_power(tDot))});
+      case tFlatten: return mk(NProjection, {mk(NFlatten, {left}), projection_rhs(binding_power(tFlatten))});
+      case tOr: return mk(NOr, {left, expr(binding_power(tOr))});
+      case tLparen: {
+        if (left->k != NField) throw JmesUnsupported{"function name"};
+        std::vector<NP> args;
+        while (look() != tRparen) {
+          args.push_back(expr(0));
+          if (look() == tComma) match(tComma);
+        }
+        match(tRparen);
+        return mk(NFunction, args, left->name);
+      }
+      default: throw JmesUnsupported{"operator"};
+    }
+  }
+  NP dot_rhs(int bp) {
+    Tok l = look();
+    if (l == tIdent || l == tQuoted) return expr(bp);
+    if (l == tLbracket) { match(tLbracket); return multi_list(); }
+    throw JmesUnsupported{"dot rhs"};
+  }
+  NP projection_rhs(int bp) {
+    if (binding_power(look()) < 10) return mk(NIdentity);  // projectionStop
+    if (look() == tLbracket) return expr(bp);
+    if (look() == tDot) { match(tDot); return dot_rhs(bp); }
+    throw JmesUnsupported{"projection rhs"};
+  }
+  NP multi_list() {  // '[' already consumed
+    std::vector<NP> items;
+    for (;;) {
+      items.push_back(expr(0));
+      if (look() == tRbracket) break;
+      match(tComma);
+    }
+    match(tRbracket);
+    return mk(NMultiList, items);
+  }
+};
+
+NP parse(const std::string& s) {
+  Parser p{lex(s), 0};
+  NP n = p.expr(0);
+  if (p.look() != tEOF) throw JmesUnsupported{"trailing tokens"};
+  return n;
+}
+
+// ---------------------------------------------------------------- interpreter (go-jmespath interpreter.go)
+bool is_false(const VP& v) {  // util.go isFalse
+  if (!v || v->t == T::Null) return true;
+  switch (v->t) {
+    case T::Bool: return !v->b;
+    case T::Str: return v->s.empty();
+    case T::Arr: return v->a.empty();
+    case T::Obj: return v->o.empty();
+    default: return false;
+  }
+}
+
+VP eval(const NP& n, const VP& value) {
+  switch (n->k) {
+    case NField:
+      if (value && value->t == T::Obj) { VP x = value->get(n->name); return x ? x : Value::null(); }
+      return Value::null();
+    case NSubexpr: return eval(n->kids[1], eval(n->kids[0], value));
+    case NProjection: {
+      VP left = eval(n->kids[0], value);
+      if (!left || left->t != T::Arr) return Value::null();
+      auto out = Value::arr();
+      for (auto& e : left->a) {
+        VP r = eval(n->kids[1], e);
+        if (r && r->t != T::Null) out->a.push_back(r);
+      }
+      return out;
+    }
+    case NFlatten: {
+      VP left = eval(n->kids[0], value);
+      if (!left || left->t != T::Arr) return Value::null();
+      auto out = Value::arr();
+      for (auto& e : left->a) {
+        if (e && e->t == T::Arr) for (auto& x : e->a) out->a.push_back(x);
+        else out->a.push_back(e ? e : Value::null());
+      }
+      return out;
+    }
+    case NMultiList: {
+      if (!value || value->t == T::Null) return Value::null();
+      auto out = Value::arr();
+      for (auto& k : n->kids) out->a.push_back(eval(k, value));
+      return out;
+    }
+    case NFunction: {
+      if (n->name != "keys" || n->kids.size() != 1) throw JmesUnsupported{"function " + n->name};
+      VP arg = eval(n->kids[0], value);
+      if (!arg || arg->t != T::Obj) throw JmesError{"invalid type for: <nil>, expected: []jpType{\"object\"}"};
+      auto out = Value::arr();  // Go map iteration order in the reference; sorted here (order-free uses only)
+      for (auto& kv : arg->o) out->a.push_back(Value::str(kv.first));
+      return out;
+    }
+    case NCurrent: case NIdentity: return value ? value : Value::null();
+    case NOr: {
+      VP m = eval(n->kids[0], value);
+      return is_false(m) ? eval(n->kids[1], value) : m;
+    }
+    case NLiteral: return n->lit;
+  }
+  return Value::null();
+}
+
+// plain field chain (the fork's NotFoundError applies): field names in order
+bool pure_chain(const NP& n, std::vector<std::string>& out) {
+  if (n->k == NField) { out.push_back(n->name); return true; }
+  if (n->k == NSubexpr) return pure_chain(n->kids[0], out) && pure_chain(n->kids[1], out);
+  return false;
+}
+
+VP floats(const VP& v) {  // encoding/json decode of the JSON context: every number float64
+  if (!v) return Value::null();
+  switch (v->t) {
+    case T::Int: return Value::flt((double)v->i);
+    case T::Arr: { auto o = Value::arr(); for (auto& e : v->a) o->a.push_back(floats(e)); return o; }
+    case T::Obj: { auto o = Value::obj(); for (auto& kv : v->o) o->o[kv.first] = floats(kv.second); return o; }
+    default: return v;
+  }
+}
+
+}  // namespace
+
+// every node within the restated interpreter (functions: keys(@) only)
+static bool nodes_ok(const NP& n) {
+  if (n->k == NFunction && (n->name != "keys" || n->kids.size() != 1 || n->kids[0]->k != NCurrent)) return false;
+  for (auto& k : n->kids) if (!nodes_ok(k)) return false;
+  return true;
+}
+
+bool jmes_supported(const std::string& expr, bool allow_element) {
+  try {
+    NP n = parse(expr);
+    if (!nodes_ok(n)) return false;
+    // left spine down to the innermost node whose left child is the root field
+    const Node* c = n.get();
+    if (c->k == NField) return c->name == "element" && allow_element;
+    for (;;) {
+      if (c->kids.empty()) return false;
+      const Node* l = c->kids[0].get();
+      if (l->k == NField) break;
+      if (l->k != NSubexpr && l->k != NProjection && l->k != NFlatten && l->k != NOr) return false;
+      c = l;
+    }
+    const std::string& root = c->kids[0]->name;
+    if (root == "element") return allow_element;
+    if (root != "request" || c->k != NSubexpr || c->kids[1]->k != NField) return false;
+    return c->kids[1]->name == "object" || c->kids[1]->name == "operation";
+  } catch (JmesUnsupported&) {
+    return false;
+  }
+}
+
+VP jmes_query(const std::string& expr, const VP& resource, const VP& element, int64_t index) {
+  NP n = parse(expr);
+  auto ctx = Value::obj();
+  auto req = Value::obj();
+  req->o["object"] = floats(resource);
+  req->o["operation"] = Value::str("CREATE");  // scanner.go:97 / CLI default (common.go:287)
+  ctx->o["request"] = req;
+  if (element) {
+    ctx->o["element"] = floats(element);
+    ctx->o["elementIndex"] = Value::flt((double)index);
+  }
+  std::vector<std::string> chain;
+  if (pure_chain(n, chain)) {  // kyverno/go-jmespath fork: a key missing from a map is NotFoundError
+    VP cur = ctx;
+    for (auto& k : chain) {
+      if (!cur || cur->t != T::Obj) return Value::null();
+      if (!cur->has(k)) throw JmesNotFound{k};
+      cur = cur->get(k);
+    }
+    return cur ? cur : Value::null();
+  }
+  return eval(n, ctx);
+}
+
+}  // namespace orc

@@ -13,6 +13,8 @@ executed or imported) and writes small JSON fixtures next to this script:
   best_practices.json test/best_practices/*.yaml                  (C1 / C3 policy set)
   chart_restricted.json charts/kyverno-policies/templates/**      (hand-rendered PSS restricted profile)
   conditions.json    pkg/engine/variables/evaluate_test.go        (condition operators: key, operator, value -> bool)
+  cli_apply.json     cmd/cli/kubectl-kyverno/apply/apply_command_test.go Test_Apply (report summaries of
+                     `kyverno apply` over local policy / resource files, incl. test/cli/apply: foreach + JMESPath)
 
 Usage: python tests/golden/extract.py [/root/reference]
 """
@@ -262,7 +264,7 @@ def extract_cli():
             names = res.get("resources") or ([res["resource"]] if res.get("resource") else [])
             for n in names:
                 results.append({"policy": res.get("policy"), "rule": res.get("rule"), "resource": n,
-                                "kind": res.get("kind"), "result": res.get("result"),
+                                "kind": res.get("kind"), "result": res.get("result") or res.get("status"),
                                 "namespace": res.get("namespace")})
         recs.append({"dir": os.path.basename(d), "policies": policies, "resources": resources, "results": results})
     write("cli.json", recs)
@@ -428,6 +430,55 @@ def extract_conditions():
     write("conditions.json", recs)
 
 
+# ---------------------------------------------------------------- CLI apply summaries
+def extract_cli_apply():
+    """Test_Apply cases whose policy and resource paths are files of the reference tree: the policies, the
+    resources (CLI default namespace applied by the consumer) and the expected report summary."""
+    src = read("cmd/cli/kubectl-kyverno/apply/apply_command_test.go")
+    body = dict(functions(src))["Test_Apply"]
+    local = re.search(r'copyFileToThisDir\("([^"]+)"\)', body).group(1)
+    recs = []
+    for blk in re.split(r"\n\t\t\{\n\t\t\tconfig: ApplyCommandConfig\{", body)[1:]:
+        def paths(key):
+            m = re.search(key + r":\s*\[\]string\{([^}]*)\}", blk)
+            return re.findall(r'"([^"]*)"', m.group(1)) if m else []
+        pols = [p for p in paths("PolicyPaths")] or (["localFileName"] if "localFileName" in blk else [])
+        if re.search(r"PolicyPaths:\s*\[\]string\{localFileName\}", blk):
+            pols = [local]
+        ress = paths("ResourcePaths")
+        stdin = re.search(r'stdinFile:\s*"([^"]+)"', blk)
+        pols = [stdin.group(1) if (x == "-" and stdin) else x for x in pols]
+        ress = [stdin.group(1) if (x == "-" and stdin) else x for x in ress]
+        if any(x.startswith("http") for x in pols + ress):
+            continue
+        summ = {k.lower(): int(v) for k, v in re.findall(r"(Pass|Fail|Skip|Error|Warn):\s*(\d+)", blk)}
+        def load(rel):
+            fp = os.path.normpath(os.path.join(REF, "cmd/cli/kubectl-kyverno/apply", rel))
+            files = sorted(glob.glob(os.path.join(fp, "*.yaml"))) if os.path.isdir(fp) else [fp]
+            out = []
+            for f in files:
+                out += [json_safe(normalize_numbers(x)) for x in yaml_docs(f)]
+            return out, [os.path.relpath(f, REF) for f in files]
+        policies, pfiles, resources, rfiles = [], [], [], []
+        for x in pols:
+            d, f = load(x)
+            policies += d
+            pfiles += f
+        for x in ress:
+            d, f = load(x)
+            resources += d
+            rfiles += f
+        recs.append({"policy_files": pfiles, "resource_files": rfiles, "policies": policies, "resources": resources,
+                     "audit_warn": "AuditWarn:     true" in blk or re.search(r"AuditWarn:\s*true", blk) is not None,
+                     "summary": summ})
+    write("cli_apply.json", recs)
+
+
+if __name__ == "__main__" and len(sys.argv) > 2:  # python extract.py <reference> <extractor> ...: selected only
+    for name in sys.argv[2:]:
+        globals()["extract_" + name]()
+    sys.exit(0)
+
 if __name__ == "__main__":
     extract_wildcard()
     extract_pattern_leaf()
@@ -438,3 +489,4 @@ if __name__ == "__main__":
     extract_best_practices()
     extract_chart()
     extract_conditions()
+    extract_cli_apply()
