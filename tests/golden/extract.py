@@ -13,6 +13,7 @@ executed or imported) and writes small JSON fixtures next to this script:
   best_practices.json test/best_practices/*.yaml                  (C1 / C3 policy set)
   chart_restricted.json charts/kyverno-policies/templates/**      (hand-rendered PSS restricted profile)
   conditions.json    pkg/engine/variables/evaluate_test.go        (condition operators: key, operator, value -> bool)
+  match.json         pkg/engine/utils_test.go TestMatchesResourceDescription(+_GenerateName) (match / exclude)
   cli_apply.json     cmd/cli/kubectl-kyverno/apply/apply_command_test.go Test_Apply (report summaries of
                      `kyverno apply` over local policy / resource files, incl. test/cli/apply: foreach + JMESPath)
 
@@ -430,6 +431,27 @@ def extract_conditions():
     write("conditions.json", recs)
 
 
+# ---------------------------------------------------------------- match / exclude (MatchesResourceDescription)
+def extract_match():
+    """pkg/engine/utils_test.go TestMatchesResourceDescription + _GenerateName: (policy JSON, resource JSON, whether
+    MatchesResourceDescription returns an error for every autogen-computed rule); the admission info of each case
+    is kept as text (it only matters for rules naming roles / clusterRoles / subjects)."""
+    src = read("pkg/engine/utils_test.go")
+    fns = dict(functions(src))
+    recs = []
+    for fn in ("TestMatchesResourceDescription", "TestMatchesResourceDescription_GenerateName"):
+        body = fns[fn]
+        for blk in re.split(r"\n\t\t\{\n\t\t\tDescription:", body)[1:]:
+            desc = re.match(r'\s*"((?:[^"\\]|\\.)*)"', blk).group(1)
+            res = re.search(r"Resource:\s*\[\]byte\(`(.*?)`\)", blk, re.S).group(1)
+            pol = re.search(r"Policy:\s*\[\]byte\(`(.*?)`\)", blk, re.S).group(1)
+            err = re.search(r"areErrorsExpected:\s*(true|false)", blk).group(1) == "true"
+            adm = re.search(r"AdmissionInfo:\s*v1beta1\.RequestInfo\{(.*?)\n\t\t\t\},", blk, re.S)
+            recs.append({"test": fn, "description": desc, "resource": json.loads(res), "policy": json.loads(pol),
+                         "errors_expected": err, "admission_info": adm.group(1).strip() if adm else ""})
+    write("match.json", recs)
+
+
 # ---------------------------------------------------------------- CLI apply summaries
 def extract_cli_apply():
     """Test_Apply cases whose policy and resource paths are files of the reference tree: the policies, the
@@ -490,3 +512,4 @@ if __name__ == "__main__":
     extract_chart()
     extract_conditions()
     extract_cli_apply()
+    extract_match()

@@ -1,0 +1,78 @@
+"""match / exclude (MatchesResourceDescription, pkg/engine/utils.go:185-289) pinned by the reference's own
+pkg/engine/utils_test.go tables (tests/golden/match.json): the oracle must reproduce every case whose rules do not
+name roles / clusterRoles / subjects (background semantics: the admission info only matters for those), and the
+device's match program (explicit CPU instantiation here; the MI355X in the -m gpu variant) must agree with the
+oracle, incl. the OldResource retry of validation.go:600-615."""
+import copy
+import json
+
+import pytest
+
+from kyverno_amd import _lib as K
+from kyverno_amd import engine as E
+from oracle import oracle as O
+
+
+def _userinfo(block):
+    if not isinstance(block, dict):
+        return False
+    if any(block.get(k) for k in ("roles", "clusterRoles", "subjects")):
+        return True
+    return any(_userinfo(b) for key in ("any", "all") for b in (block.get(key) or []))
+
+
+def cases(golden):
+    for rec in golden("match.json"):
+        for rule in O.compute_rules(rec["policy"]):
+            if _userinfo(rule.get("match")) or _userinfo(rule.get("exclude")):
+                continue
+            yield rec, rule
+
+
+def test_oracle_matches_reference_tables(golden):
+    n = 0
+    for rec, rule in cases(golden):
+        got = O.rule_matches(rule, json.dumps(rec["resource"]))
+        assert got == (not rec["errors_expected"]), (rec["test"], rec["description"], rule["name"])
+        n += 1
+    assert n >= 30
+
+
+def _device_policy(rec):
+    """the golden policy with every rule turned into a validate rule (same match / exclude, empty pattern), autogen
+    switched off so that rule names stay the golden's"""
+    p = copy.deepcopy(rec["policy"])
+    p["kind"] = "ClusterPolicy"
+    p.setdefault("metadata", {}).setdefault("annotations", {})["pod-policies.kyverno.io/autogen-controllers"] = "none"
+    for r in p["spec"]["rules"]:
+        for k in ("mutate", "generate", "validate", "verifyImages"):
+            r.pop(k, None)
+        r["validate"] = {"pattern": {}}
+    return p
+
+
+def check_device(golden, backend):
+    n = 0
+    for rec in golden("match.json"):
+        p = _device_policy(rec)
+        if any(_userinfo(r.get("match")) or _userinfo(r.get("exclude")) for r in p["spec"]["rules"]):
+            continue
+        rs = E.Ruleset([p])
+        b = E.Batch(rs, [rec["resource"]])
+        res = E.evaluate(rs, b, backend=backend)
+        for k, r in enumerate(rs.rules):
+            base = [x for x in p["spec"]["rules"] if x["name"] == r["name"]][0]
+            want = O.rule_matches(base, json.dumps(rec["resource"])) or O.rule_matches(base, None)
+            got = int(res.status[k, 0]) != K.ST_NONE
+            assert got == want, (rec["test"], rec["description"], r["name"], K.STATUS_NAMES[int(res.status[k, 0])])
+            n += 1
+    assert n >= 30
+
+
+def test_device_match_program_cpu_instantiation(golden):
+    check_device(golden, "cpu")
+
+
+@pytest.mark.gpu
+def test_device_match_program_gpu(golden):
+    check_device(golden, "gpu")
