@@ -786,6 +786,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     host_recs.clear();
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.counts, 0, std::max<size_t>(1, nrules) * NSTATUS * 8, stream));
+    HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));  // also when no slice runs (no rules / no resources)
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     for (auto& sl : d.slices) {

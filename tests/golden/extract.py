@@ -14,6 +14,7 @@ executed or imported) and writes small JSON fixtures next to this script:
   chart_restricted.json charts/kyverno-policies/templates/**      (hand-rendered PSS restricted profile)
   conditions.json    pkg/engine/variables/evaluate_test.go        (condition operators: key, operator, value -> bool)
   match.json         pkg/engine/utils_test.go TestMatchesResourceDescription(+_GenerateName) (match / exclude)
+  match_units.json   pkg/utils/match/{name,annotations,labels,kind}_test.go, pkg/utils/kube/kind_test.go
   cli_apply.json     cmd/cli/kubectl-kyverno/apply/apply_command_test.go Test_Apply (report summaries of
                      `kyverno apply` over local policy / resource files, incl. test/cli/apply: foreach + JMESPath)
 
@@ -452,6 +453,136 @@ def extract_match():
     write("match.json", recs)
 
 
+# ---------------------------------------------------------------- Go composite literals (table tests)
+class _GoExpr:
+    """Go composite-literal expressions of table-driven tests -> Python values: strings, numbers, true/false/nil,
+    [&]Type{...} (keyed elements -> dict, positional -> list), map[..]..{k: v}, qualified constants (kept as
+    their name, e.g. "metav1.LabelSelectorOpIn")."""
+
+    def __init__(self, s):
+        self.s, self.i = s, 0
+
+    def ws(self):
+        while self.i < len(self.s) and self.s[self.i] in " \t\n\r,":
+            self.i += 1
+        while self.s.startswith("//", self.i):
+            self.i = self.s.index("\n", self.i)
+            self.ws()
+
+    def value(self):
+        self.ws()
+        s, i = self.s, self.i
+        if s[i] == '"':
+            m = re.match(r'"(?:[^"\\]|\\.)*"', s[i:])
+            self.i += m.end()
+            return go_unquote(m.group(0))
+        if s[i] == "`":
+            j = s.index("`", i + 1)
+            self.i = j + 1
+            return s[i + 1:j]
+        if s[i] == "{":  # untyped composite (element of a typed slice)
+            return self.composite()
+        if s[i] == "&":
+            self.i += 1
+            return self.value()
+        m = re.match(r"(map\[[^\]]*\][\w.*\[\]{}]*?|\[\][\w.*\[\]{}]*?|[A-Za-z_][\w.]*)\{", s[i:])
+        if m:
+            self.i += m.end() - 1
+            return self.composite()
+        m = re.match(r"true|false|nil", s[i:])
+        if m:
+            self.i += m.end()
+            return {"true": True, "false": False, "nil": None}[m.group(0)]
+        m = re.match(r"-?[0-9][0-9.eE+-]*", s[i:])
+        if m:
+            self.i += m.end()
+            t = m.group(0)
+            return float(t) if any(c in t for c in ".eE") else int(t)
+        m = re.match(r"[A-Za-z_][\w.]*", s[i:])
+        self.i += m.end()
+        return m.group(0)
+
+    def composite(self):
+        assert self.s[self.i] == "{"
+        self.i += 1
+        keyed, items = {}, []
+        while True:
+            self.ws()
+            if self.s[self.i] == "}":
+                self.i += 1
+                return keyed if keyed else items
+            v = self.value()
+            self.ws()
+            if self.s[self.i] == ":":
+                self.i += 1
+                keyed[v] = self.value()
+            else:
+                items.append(v)
+
+
+def _go_table(body):
+    """the composite literal of `tests := []struct{...}{...}` (or `tcs`) -> list of dicts"""
+    m = re.search(r"(?:tests|tcs|testcases)\s*:?=\s*\[\]struct\s*\{", body)
+    i = m.end()
+    depth = 1
+    while depth:  # skip the struct type
+        depth += {"{": 1, "}": -1}.get(body[i], 0)
+        i += 1
+    g = _GoExpr(body[i:])
+    return g.composite()
+
+
+def _selector_json(sel):
+    if sel is None:
+        return None
+    if isinstance(sel, list):  # &metav1.LabelSelector{}
+        sel = {}
+    out = {}
+    if sel.get("MatchLabels") is not None:
+        out["matchLabels"] = sel["MatchLabels"]
+    if sel.get("MatchExpressions") is not None:
+        ops = {"metav1.LabelSelectorOpIn": "In", "metav1.LabelSelectorOpNotIn": "NotIn",
+               "metav1.LabelSelectorOpExists": "Exists", "metav1.LabelSelectorOpDoesNotExist": "DoesNotExist"}
+        out["matchExpressions"] = [{"key": e.get("Key", ""), "operator": ops.get(e.get("Operator"), e.get("Operator")),
+                                    "values": e.get("Values")} for e in sel["MatchExpressions"]]
+    return out
+
+
+def extract_match_units():
+    """pkg/utils/match/{name,annotations,labels,kind}_test.go and pkg/utils/kube/kind_test.go"""
+    out = {}
+    src = read("pkg/utils/match/name_test.go")
+    out["name"] = [{"expected": (t.get("args") or {}).get("expected", ""), "actual": (t.get("args") or {}).get("actual", ""),
+                    "want": t["want"]} for t in _go_table(dict(functions(src))["TestCheckName"])]
+    src = read("pkg/utils/match/annotations_test.go")
+    out["annotations"] = [{"expected": t["args"].get("expected") or {}, "actual": t["args"].get("actual") or {},
+                           "want": t["want"]} for t in _go_table(dict(functions(src))["TestCheckAnnotations"])]
+    src = read("pkg/utils/match/labels_test.go")
+    out["selector"] = [{"expected": _selector_json(t["args"].get("expected")), "actual": t["args"].get("actual") or {},
+                        "want": t.get("want", False), "wantErr": t.get("wantErr", False)}
+                       for t in _go_table(dict(functions(src))["TestCheckSelector"])]
+    src = read("pkg/utils/match/kind_test.go")
+    kinds = []
+    pat = re.compile(r'CheckKind\(subresourceGVKToAPIResource, \[\]string\{"([^"]*)"\}, schema\.GroupVersionKind\{Kind: "([^"]*)", '
+                     r'Group: "([^"]*)", Version: "([^"]*)"\}, "([^"]*)", (true|false)\)\s*assert\.Equal\(t, match, (true|false)\)', re.S)
+    subres_map = False
+    for m in pat.finditer(src):
+        before = src[:m.start()]
+        subres_map = "subresourceGVKToAPIResource[" in before
+        kinds.append({"kinds": [m.group(1)], "kind": m.group(2), "group": m.group(3), "version": m.group(4),
+                      "subresource": m.group(5), "allow_ephemeral": m.group(6) == "true", "want": m.group(7) == "true",
+                      "subresource_map": subres_map})
+    out["check_kind"] = kinds
+    src = read("pkg/utils/kube/kind_test.go")
+    out["gvk"] = [{"gvk": a, "group_version": b, "kind": c} for a, b, c in re.findall(
+        r'apiVersion, kind = GetKindFromGVK\("([^"]*)"\)\s*assert\.Equal\(t, "([^"]*)", apiVersion\)\s*'
+        r'assert\.Equal\(t, "([^"]*)", kind\)', src)]
+    out["gv_matches"] = [{"group_version": a, "server": b, "want": c == "true"} for a, b, c in re.findall(
+        r'groupVersion, serverResourceGroupVersion :?= "([^"]*)", "([^"]*)"\s*(?://[^\n]*\s*)?'
+        r'assert\.Equal\(t, GroupVersionMatches\(groupVersion, serverResourceGroupVersion\), (true|false)\)', src)]
+    write("match_units.json", out)
+
+
 # ---------------------------------------------------------------- CLI apply summaries
 def extract_cli_apply():
     """Test_Apply cases whose policy and resource paths are files of the reference tree: the policies, the
@@ -513,3 +644,4 @@ if __name__ == "__main__":
     extract_conditions()
     extract_cli_apply()
     extract_match()
+    extract_match_units()
