@@ -15,6 +15,7 @@ executed or imported) and writes small JSON fixtures next to this script:
   conditions.json    pkg/engine/variables/evaluate_test.go        (condition operators: key, operator, value -> bool)
   match.json         pkg/engine/utils_test.go TestMatchesResourceDescription(+_GenerateName) (match / exclude)
   match_units.json   pkg/utils/match/{name,annotations,labels,kind}_test.go, pkg/utils/kube/kind_test.go
+  autogen.json       pkg/autogen/autogen_test.go (rule names, CanAutoGen / GetSupportedControllers, rule counts)
   cli_apply.json     cmd/cli/kubectl-kyverno/apply/apply_command_test.go Test_Apply (report summaries of
                      `kyverno apply` over local policy / resource files, incl. test/cli/apply: foreach + JMESPath)
 
@@ -583,6 +584,27 @@ def extract_match_units():
     write("match_units.json", out)
 
 
+# ---------------------------------------------------------------- autogen
+def extract_autogen():
+    """pkg/autogen/autogen_test.go: getAutogenRuleName (name truncation), CanAutoGen / GetSupportedControllers
+    tables (policy JSON -> "none" or the pod controllers), Test_PodSecurityWithNoExceptions (3 computed rules)"""
+    src = read("pkg/autogen/autogen_test.go")
+    fns = dict(functions(src))
+    out = {"rule_names": [], "controllers": [], "rule_counts": []}
+    for name, rule, prefix, exp in re.findall(r'\{"([^"]*)", "([^"]*)", "([^"]*)", "([^"]*)"\}', fns["Test_getAutogenRuleName"]):
+        out["rule_names"].append({"rule": rule, "prefix": prefix, "expected": exp})
+    for fn in ("Test_CanAutoGen", "Test_GetSupportedControllers"):
+        for m in re.finditer(r'name:\s*"([^"]*)",\s*policy:\s*\[\]byte\(`(.*?)`\),\s*expectedControllers:\s*("[^"]*"|PodControllers)',
+                             fns[fn], re.S):
+            exp = m.group(3)
+            out["controllers"].append({"test": fn, "name": m.group(1), "policy": json.loads(m.group(2)),
+                                       "controllers": "pod" if exp == "PodControllers" else go_unquote(exp)})
+    m = re.search(r"policy := \[\]byte\(`(.*?)`\).*?assert\.Equal\(t, (\d+), len\(rules\)\)",
+                  fns["Test_PodSecurityWithNoExceptions"], re.S)
+    out["rule_counts"].append({"policy": json.loads(m.group(1)), "rules": int(m.group(2))})
+    write("autogen.json", out)
+
+
 # ---------------------------------------------------------------- CLI apply summaries
 def extract_cli_apply():
     """Test_Apply cases whose policy and resource paths are files of the reference tree: the policies, the
@@ -645,3 +667,4 @@ if __name__ == "__main__":
     extract_cli_apply()
     extract_match()
     extract_match_units()
+    extract_autogen()
