@@ -135,14 +135,8 @@ def compute_enforce_policy(p):
 
 def keep_for_enforce(p, ns):
     """cache.go checkValidationFailureActionOverrides(enforce=true, ns, policy)"""
-    s = _spec(p)
-    overrides = s.get("validationFailureActionOverrides") or []
-    if not action_enforce(s.get("validationFailureAction", "Audit")) and (ns == "" or not overrides):
-        return False
-    for o in overrides:
-        if not action_enforce(o.get("action")) and check_patterns(o.get("namespaces"), ns):
-            return False
-    return True
+    from .policycache import check_overrides
+    return check_overrides(True, ns, p)
 
 
 def response_action(p, resource_ns, ns_labels):
@@ -420,39 +414,30 @@ class AdmissionBatcher:
                         nm = nm[len(pre):]
                         break
                 userinfo = userinfo or rule_uses_userinfo(base.get(nm) or {})
-            # policyMap.set (store.go:96-138): kinds of the autogen-expanded rules that have a validate block
-            kinds = set()
-            for k in range(pm["first_rule"], pm["first_rule"] + pm["nrules"]):
-                ri = self.ruleset.rules[k]
-                if ri["has_validate"]:
-                    kinds.update(compute_kind(g) for g in ri["match_kinds"])
             uses_op = any(self.ruleset.rules[k]["uses_operation"]
                           for k in range(pm["first_rule"], pm["first_rule"] + pm["nrules"]))
             self.pol.append({"doc": p, "name": pm["name"], "namespace": pm["namespace"], "first": pm["first_rule"],
                              "n": pm["nrules"], "apply_one": pm["apply_one"], "userinfo": userinfo, "uses_op": uses_op,
-                             "enforce": has_validate(p) and compute_enforce_policy(p), "kinds": kinds,
+                             "enforce": has_validate(p) and compute_enforce_policy(p),
                              "fail_policy": failure_policy(p)})
+        # the policy cache (pkg/policycache) indexed from the compiled ruleset's autogen rules and their kinds
+        from .policycache import PolicyCache, VALIDATE_ENFORCE
+        self._vtype = VALIDATE_ENFORCE
+        self.cache, self._key_index = PolicyCache(), {}
+        for i, pm in enumerate(self.ruleset.policies):
+            key = pm["namespace"] + "/" + pm["name"] if pm["namespace"] else pm["name"]
+            rules = [(self.ruleset.rules[k]["match_kinds"], self.ruleset.rules[k]["has_validate"])
+                     for k in range(pm["first_rule"], pm["first_rule"] + pm["nrules"])]
+            self.cache.set(key, self.pol[i]["doc"], rules=rules)
+            self._key_index[key] = i
         self.stats = {"requests": 0, "batches": 0, "device_policies": 0, "cpu_policies": 0}
         self._q, self._cv, self._stop, self._thr = [], threading.Condition(), False, None
         self._enforce_cache = {}
 
-    # policycache.GetPolicies(ValidateEnforce, kind, ns) (cache.go:38-57): cluster policies indexed under the request
-    # kind and under "*", then the namespace's Policies under both, then the override filter (filterPolicies). A
-    # policy indexed under both keys is returned twice, as the reference's append of the two set lookups does.
-    def enforce_policies(self, ns, kind=None):
-        out = []
-        keys = [compute_kind(kind), "*"] if kind is not None else [None]
-        scopes = [""] + ([ns] if ns else [])
-        for scope in scopes:
-            for key in keys:
-                for i, p in enumerate(self.pol):
-                    if not p["enforce"] or p["namespace"] != scope:
-                        continue
-                    if key is not None and key not in p["kinds"]:
-                        continue
-                    if keep_for_enforce(p["doc"], ns):
-                        out.append(i)
-        return out
+    def enforce_policies(self, ns, kind):
+        """policycache.GetPolicies(ValidateEnforce, kind, ns) (cache.go:38-57) as indices into self.pol; a policy
+        indexed under both the kind and "*" comes back twice, as the reference's appends return it"""
+        return [self._key_index[k] for k in self.cache.get_policy_keys(self._vtype, kind, ns)]
 
     def _device_rules(self, pi, st, r, res):
         """rule responses of policy pi for batch resource r from the device (ApplyOne truncation as

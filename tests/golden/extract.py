@@ -16,6 +16,7 @@ executed or imported) and writes small JSON fixtures next to this script:
   match.json         pkg/engine/utils_test.go TestMatchesResourceDescription(+_GenerateName) (match / exclude)
   match_units.json   pkg/utils/match/{name,annotations,labels,kind}_test.go, pkg/utils/kube/kind_test.go
   autogen.json       pkg/autogen/autogen_test.go (rule names, CanAutoGen / GetSupportedControllers, rule counts)
+  policycache.json   pkg/policycache/cache_test.go (validate lookups by type / kind / namespace)
   cli_apply.json     cmd/cli/kubectl-kyverno/apply/apply_command_test.go Test_Apply (report summaries of
                      `kyverno apply` over local policy / resource files, incl. test/cli/apply: foreach + JMESPath)
 
@@ -605,6 +606,51 @@ def extract_autogen():
     write("autogen.json", out)
 
 
+# ---------------------------------------------------------------- policy cache
+def extract_policycache():
+    """pkg/policycache/cache_test.go: the policies of the new*Policy builders, and for every test the validate-type
+    lookups (store.get / cache.GetPolicies of ValidateEnforce / ValidateAudit) asserted before the first removal"""
+    src = read("pkg/policycache/cache_test.go")
+    fns = dict(functions(src))
+    builders = {}
+    for name, body in fns.items():
+        m = re.search(r"rawPolicy := \[\]byte\(`(.*?)`\).*?var policy \*kyvernov1\.(\w+)", body, re.S)
+        if name.startswith("new") and m:
+            doc = json.loads(m.group(1))
+            doc["kind"] = m.group(2)
+            builders[name] = doc
+    tests = []
+    for name, body in fns.items():
+        if not name.startswith("Test_"):
+            continue
+        body = body.split("unsetPolicy(")[0]
+        vars_ = dict(re.findall(r"(\w+) := (new\w+)\(t\)", body))
+        added = [v for v in re.findall(r"setPolicy\(pCache, (\w+)\)", body)]
+        added += [v for v in re.findall(r"cache\.Set\(\w+, (\w+), ", body)]
+        if not added:
+            continue
+        pols = []
+        for v in added:
+            if v in vars_ and vars_[v] not in pols:
+                pols.append(vars_[v])
+        nspace = None
+        m = re.search(r"nspace := (\w+)\.GetNamespace\(\)", body)
+        if m and m.group(1) in vars_:
+            nspace = (builders[vars_[m.group(1)]].get("metadata") or {}).get("namespace", "")
+        calls = []
+        for var, api, typ, kind, ns, rest in re.findall(
+                r"(\w+) :?= (pCache\.get|cache\.GetPolicies)\((Validate\w+), \"([^\"]*)\", (\"[^\"]*\"|nspace)\)(.*?)(?=\n\t\w+ :?= |\Z)",
+                body, re.S):
+            m = re.search(r"if len\(" + var + r"\) != (\d+)", rest)
+            if not m:
+                continue
+            calls.append({"api": "GetPolicies" if api == "cache.GetPolicies" else "get", "type": typ, "kind": kind,
+                          "namespace": nspace if ns == "nspace" else go_unquote(ns), "expected": int(m.group(1))})
+        if calls:
+            tests.append({"test": name, "policies": [builders[b] for b in pols], "calls": calls})
+    write("policycache.json", tests)
+
+
 # ---------------------------------------------------------------- CLI apply summaries
 def extract_cli_apply():
     """Test_Apply cases whose policy and resource paths are files of the reference tree: the policies, the
@@ -668,3 +714,4 @@ if __name__ == "__main__":
     extract_match()
     extract_match_units()
     extract_autogen()
+    extract_policycache()
