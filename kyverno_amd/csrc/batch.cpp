@@ -8,6 +8,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <atomic>
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <emmintrin.h>
+#include <memory>
+#include <string_view>
 #include <thread>
 
 #include "kyv_host.h"
@@ -20,193 +26,487 @@ Batch::~Batch() {}
 
 namespace {
 
-bool magic(const std::string& s) {
-  return s.find("negation anchor matched in resource") != std::string::npos ||
-         s.find("conditional anchor mismatch") != std::string::npos || s.find("global anchor mismatch") != std::string::npos;
+template <class F>
+void parallel_for(size_t n, int T, F&& f) {  // f(k) for k in [0, n) over min(T, n) threads (the caller is one)
+  if (n == 0) return;
+  size_t t = std::min<size_t>((size_t)std::max(1, T), n);
+  if (t <= 1) { for (size_t k = 0; k < n; k++) f(k); return; }
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      size_t k = next.fetch_add(1);
+      if (k >= n) break;
+      f(k);
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t q = 1; q < t; q++) th.emplace_back(work);
+  work();
+  for (auto& x : th) x.join();
 }
 
-bool is_anchor_key(const std::string& raw, const char* tag) {  // key that anchor.Parse() maps onto tag
-  std::string s = pj::go_trim_space(raw);
+bool magic(std::string_view s) {
+  if (s.size() < 22 || s.find("anchor") == std::string_view::npos) return false;
+  return s.find("negation anchor matched in resource") != std::string_view::npos ||
+         s.find("conditional anchor mismatch") != std::string_view::npos ||
+         s.find("global anchor mismatch") != std::string_view::npos;
+}
+
+bool go_space(unsigned char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
+
+bool is_anchor_key(std::string_view s, const char* tag) {  // key that anchor.Parse() maps onto tag
+  while (!s.empty() && go_space((unsigned char)s.front())) s.remove_prefix(1);
+  while (!s.empty() && go_space((unsigned char)s.back())) s.remove_suffix(1);
   if (s.size() < 3 || s.back() != ')') return false;
   size_t p = (s[0] == '+' || s[0] == '<' || s[0] == '=' || s[0] == 'X' || s[0] == '^') ? 1 : 0;
   if (s[p] != '(') return false;
   return s.substr(p + 1, s.size() - p - 2) == tag;
 }
 
-// chunk-local interning, remapped to global ids after the parallel phase
-struct Chunk {
-  std::vector<std::string> strs;
-  std::unordered_map<std::string, uint32_t> ids;
-  std::vector<Node> nodes;
-  std::vector<ResHeader> hdr;
-  std::vector<FloatAux> faux;
-  std::vector<uint32_t> ns_names;  // local sid of namespace per resource
-  std::string err;
-  uint32_t local(const std::string& s) {
-    auto it = ids.find(s);
-    if (it != ids.end()) return it->second;
+inline uint64_t hash_bytes(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xff51afd7ed558ccdull);
+  while (n >= 8) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    h = (h ^ w) * 0xbf58476d1ce4e5b9ull;
+    h ^= h >> 31;
+    p += 8;
+    n -= 8;
+  }
+  uint64_t w = 0;
+  memcpy(&w, p, n);
+  h = (h ^ w ^ ((uint64_t)n << 56)) * 0x94d049bb133111ebull;
+  h ^= h >> 29;
+  h *= 0xbf58476d1ce4e5b9ull;
+  h ^= h >> 32;
+  return h;
+}
+
+// Open-addressing string table over views (into the input buffer, the ruleset dictionary or owned storage).
+// Ids are dense in insertion order.
+struct StrTab {
+  std::vector<std::string_view> strs;
+  std::vector<uint64_t> hashes;
+  std::vector<uint64_t> slots;  // (hash high 32 bits << 32) | (id + 1); 0 = empty
+  std::deque<std::string> own;  // unescaped / formatted strings that are not in any input buffer
+  uint64_t mask = 0;
+  StrTab() { rehash(64); }
+  static uint64_t tag(uint64_t h) { return h & 0xFFFFFFFF00000000ull; }
+  void rehash(size_t cap) {
+    slots.assign(cap, 0);
+    mask = cap - 1;
+    for (uint32_t id = 0; id < strs.size(); id++) {
+      uint64_t p = hashes[id] & mask;
+      while (slots[p]) p = (p + 1) & mask;
+      slots[p] = tag(hashes[id]) | (id + 1);
+    }
+  }
+  uint32_t find(std::string_view s, uint64_t h) const {
+    const uint64_t t = tag(h);
+    for (uint64_t p = h & mask;; p = (p + 1) & mask) {
+      uint64_t e = slots[p];
+      if (!e) return NONE;
+      uint32_t id = (uint32_t)e - 1;
+      if ((e & 0xFFFFFFFF00000000ull) == t && strs[id] == s) return id;
+    }
+  }
+  // returns the id; *added set when the string was new (its view must then outlive the table)
+  uint32_t add(std::string_view s, uint64_t h, bool* added) {
+    const uint64_t t = tag(h);
+    uint64_t p = h & mask;
+    for (;; p = (p + 1) & mask) {
+      uint64_t e = slots[p];
+      if (!e) break;
+      uint32_t id = (uint32_t)e - 1;
+      if ((e & 0xFFFFFFFF00000000ull) == t && strs[id] == s) { *added = false; return id; }
+    }
     uint32_t id = (uint32_t)strs.size();
     strs.push_back(s);
-    ids.emplace(s, id);
+    hashes.push_back(h);
+    slots[p] = t | (id + 1);
+    *added = true;
+    if ((strs.size() + 1) * 2 > slots.size()) rehash(slots.size() * 2);
     return id;
   }
 };
 
-struct Emitter {
-  Chunk& ch;
-  std::vector<Node> out;
-  bool magicflag = false;
-  uint32_t put_children_map(const Value& v) {
-    uint32_t first = (uint32_t)out.size();
-    out.resize(first + v.o.size());
-    for (size_t k = 0; k < v.o.size(); k++) {
-      if (magic(v.o[k].first)) magicflag = true;
-      fill(first + (uint32_t)k, v.o[k].second, (ch.local(v.o[k].first) << 4));
+enum : uint8_t { LF_MAGIC = 1, LF_ANCHORISH = 2 };
+// chunk-local ids interned first, in this order, by every chunk
+enum : uint32_t { L_EMPTY, L_KIND, L_APIVERSION, L_METADATA, L_NAME, L_GENNAME, L_NAMESPACE, L_LABELS, L_ANN, L_FIXED };
+const char* const kLocalFixed[L_FIXED] = {"", "kind", "apiVersion", "metadata", "name", "generateName", "namespace",
+                                          "labels", "annotations"};
+
+// one worker's share of the documents: nodes, headers and float forms with chunk-local string ids, remapped to
+// batch ids after the parallel phase
+struct Chunk {
+  StrTab tab;
+  std::vector<uint8_t> lflags;  // per local id
+  std::vector<Node> nodes;
+  std::vector<ResHeader> hdr;
+  std::vector<FloatAux> faux;
+  std::string err;
+  Chunk() { for (const char* s : kLocalFixed) local(s); }
+  uint32_t local(std::string_view s) { return local(s, hash_bytes(s.data(), s.size())); }
+  // direct-mapped front cache of short strings (bytes held inline, so a hit touches one line and no table memory)
+  struct Hot { uint64_t h; uint32_t id; uint32_t len; char b[16]; };
+  std::vector<Hot> hot = std::vector<Hot>(1024, Hot{0, NONE, 0, {}});
+  uint32_t local(std::string_view s, uint64_t h) {
+    Hot* e = nullptr;
+    if (s.size() <= 16) {
+      e = &hot[(h >> 20) & 1023];
+      if (e->h == h && e->len == s.size() && e->id != NONE && memcmp(e->b, s.data(), s.size()) == 0) return e->id;
     }
-    return first;
+    uint32_t id = intern(s, h);
+    if (e) {
+      e->h = h;
+      e->id = id;
+      e->len = (uint32_t)s.size();
+      memcpy(e->b, s.data(), s.size());
+    }
+    return id;
   }
-  void fill(uint32_t idx, const Value& v, uint32_t keybits) {
-    Node n{};
-    switch (v.t) {
-      case T::Null: n.tk = N_NULL; break;
-      case T::Bool: n.tk = v.b ? N_TRUE : N_FALSE; n.a = v.b; break;
-      case T::Int: {
-        n.tk = N_INT;
-        uint64_t u = (uint64_t)v.i;
-        n.a = (uint32_t)u;
-        n.b = (uint32_t)(u >> 32);
-        n.c = ch.local(std::to_string(v.i));
-        break;
-      }
-      case T::Float: {
-        n.tk = N_FLOAT;
-        uint64_t u = __builtin_bit_cast(uint64_t, v.f);
-        n.a = (uint32_t)u;
-        n.b = (uint32_t)(u >> 32);
-        n.c = (uint32_t)ch.faux.size();
-        ch.faux.push_back(FloatAux{ch.local(pj::go_fmt_E(v.f)), ch.local(pj::go_fmt_f6(v.f))});
-        break;
-      }
-      case T::Str:
-        n.tk = N_STR;
-        n.a = ch.local(v.s);
-        if (magic(v.s)) magicflag = true;
-        break;
-      case T::Obj: {
-        n.tk = N_MAP;
-        n.b = (uint32_t)v.o.size();
-        if (v.o.size() > 0xFFFF) magicflag = true;  // walk frames count entries in 16 bits
-        out[idx] = n;  // reserve before recursion (out may grow)
-        uint32_t first = put_children_map(v);
-        out[idx].a = first;
-        out[idx].tk |= keybits;
-        return;
-      }
-      case T::Arr: {
-        n.tk = N_ARR;
-        n.b = (uint32_t)v.a.size();
-        n.c = NONE;  // path-column row of element 0, set by resolve_path_columns
-        if (v.a.size() > 0xFFFF) magicflag = true;  // walk frames count elements in 16 bits
-        out[idx] = n;
-        uint32_t first = (uint32_t)out.size();
-        out.resize(first + v.a.size());
-        for (size_t k = 0; k < v.a.size(); k++) fill(first + (uint32_t)k, v.a[k], (uint32_t)k << 4);
-        out[idx].a = first;
-        out[idx].tk |= keybits;
-        return;
-      }
-    }
-    n.tk |= keybits;
-    out[idx] = n;
+  uint32_t intern(std::string_view s, uint64_t h) {
+    bool added;
+    uint32_t id = tab.add(s, h, &added);
+    if (added) lflags.push_back((magic(s) ? LF_MAGIC : 0) |
+                                (is_anchor_key(s, "labels") || is_anchor_key(s, "annotations") ? LF_ANCHORISH : 0));
+    return id;
+  }
+  uint32_t local_owned(std::string&& s) {
+    uint64_t h = hash_bytes(s.data(), s.size());
+    uint32_t id = tab.find(s, h);
+    if (id != NONE) return id;
+    tab.own.push_back(std::move(s));
+    return local(tab.own.back(), h);
   }
 };
 
-const Value* nested(const Value& o, std::initializer_list<const char*> path) {
-  const Value* cur = &o;
-  for (const char* f : path) {
-    if (cur->t != T::Obj) return nullptr;
-    cur = cur->get(f);
-    if (!cur) return nullptr;
+// Streaming flattener: one pass over a document's bytes emits its node table directly (children blocks in
+// post-order, the root at relative node 0), with the JSON grammar, escapes, UTF-8 repair, number classification
+// and duplicate-key rule (last value wins) of the pjson reader the rest of the library uses (pjson.cpp).
+struct Flat {
+  const char* s;
+  size_t n, i = 0;
+  Chunk& ch;
+  std::vector<Node> out;
+  std::vector<Node> pend;  // children of the containers being parsed, innermost last
+  std::string tmp;
+  bool magicf = false, anchorish = false;
+  explicit Flat(Chunk& c) : s(nullptr), n(0), ch(c) {}
+
+  [[noreturn]] void fail(const char* m) { throw pj::Error(std::string("json: ") + m + " at offset " + std::to_string(i)); }
+  void ws() { while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) i++; }
+  static int hx(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
   }
-  return cur;
-}
-std::string nested_str(const Value& o, std::initializer_list<const char*> path) {
-  const Value* v = nested(o, path);
-  return v && v->t == T::Str ? v->s : "";
-}
-
-// relative node index of a string map at metadata.<key> (NestedStringMap), NONE otherwise
-uint32_t string_map_node(const std::vector<Node>& R, uint32_t meta, uint32_t keysid_local, const Value* v) {
-  if (!v || v->t != T::Obj) return NONE;
-  for (auto& kv : v->o) if (kv.second.t != T::Str) return NONE;
-  const Node& m = R[meta];
-  for (uint32_t i = 0; i < m.b; i++)
-    if (node_key(R[m.a + i]) == keysid_local) return m.a + i;
-  return NONE;
-}
-
-void flatten_one(Chunk& ch, const Value& doc) {
-  Emitter em{ch};
-  em.out.resize(1);
-  em.fill(0, doc, 0);
-  ResHeader h{};
-  h.root = (uint32_t)ch.nodes.size();
-  h.nnodes = (uint32_t)em.out.size();
-  std::string kind = nested_str(doc, {"kind"});
-  h.kind = ch.local(kind);
-  std::string av = nested_str(doc, {"apiVersion"});
-  size_t sl = std::count(av.begin(), av.end(), '/');
-  std::string g, ver;
-  bool gvok = true;
-  if (av.empty() || av == "/") {}
-  else if (sl == 0) ver = av;
-  else if (sl == 1) { g = av.substr(0, av.find('/')); ver = av.substr(av.find('/') + 1); }
-  else gvok = false;
-  h.gvk_kind = ch.local(gvok ? kind : "");
-  h.group = ch.local(g);
-  h.version = ch.local(ver);
-  h.gv = ch.local(g.empty() ? ver : g + "/" + ver);
-  h.name = ch.local(nested_str(doc, {"metadata", "name"}));
-  h.gen_name = ch.local(nested_str(doc, {"metadata", "generateName"}));
-  std::string ns = nested_str(doc, {"metadata", "namespace"});
-  h.ns = ch.local(ns);
-  h.labels = h.ann = NONE;
-  h.nsl = NONE;
-  h.flags = em.magicflag ? RF_MAGIC : 0;
-  if (doc.t == T::Obj) h.flags |= RF_ROOT_MAP;
-  const Value* meta = nested(doc, {"metadata"});
-  if (meta && meta->t == T::Obj) {
-    uint32_t mnode = NONE;
-    const Node& root = em.out[0];
-    uint32_t msid = ch.local("metadata");
-    for (uint32_t i = 0; i < root.b; i++) if (node_key(em.out[root.a + i]) == msid) mnode = root.a + i;
-    if (mnode != NONE) {
-      h.labels = string_map_node(em.out, mnode, ch.local("labels"), meta->get("labels"));
-      h.ann = string_map_node(em.out, mnode, ch.local("annotations"), meta->get("annotations"));
+  bool u4(size_t at, uint32_t* v) {
+    if (at + 4 > n) return false;
+    uint32_t x = 0;
+    for (int k = 0; k < 4; k++) { int h = hx(s[at + k]); if (h < 0) return false; x = x * 16 + h; }
+    *v = x;
+    return true;
+  }
+  // string at s[i] == '"' -> chunk-local id
+  uint32_t str() {
+    size_t st = ++i;
+    // 16 bytes at a time: stop at '"', '\\', control bytes and non-ASCII bytes (signed compare: >= 0x80 is < 0)
+    const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), sp = _mm_set1_epi8(0x20);
+    while (i + 16 <= n) {
+      __m128i v = _mm_loadu_si128((const __m128i*)(s + i));
+      __m128i hit = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, q), _mm_cmpeq_epi8(v, bs)), _mm_cmplt_epi8(v, sp));
+      int m = _mm_movemask_epi8(hit);
+      if (m) { i += __builtin_ctz(m); break; }
+      i += 16;
     }
-  }
-  // any map key directly under a "metadata" map that anchor.Parse() resolves to labels/annotations
-  std::vector<const Value*> stack{&doc};
-  while (!stack.empty()) {
-    const Value* v = stack.back();
-    stack.pop_back();
-    if (v->t == T::Obj) {
-      for (auto& kv : v->o) {
-        if (kv.first == "metadata" && kv.second.t == T::Obj)
-          for (auto& m2 : kv.second.o)
-            if (is_anchor_key(m2.first, "labels") || is_anchor_key(m2.first, "annotations")) h.flags |= RF_ANCHORISH;
-        stack.push_back(&kv.second);
+    for (;;) {
+      if (i >= n) fail("unterminated string");
+      unsigned char c = s[i];
+      if (c == '"') { i++; return ch.local(std::string_view(s + st, i - 1 - st)); }
+      if (c == '\\' || c < 0x20 || c >= 0x80) break;
+      i++;
+    }
+    // escapes, control characters or non-ASCII: the pjson string rules (UTF-8 repaired to U+FFFD)
+    tmp.assign(s + st, i - st);
+    size_t run = i;
+    bool changed = false;
+    for (;;) {
+      if (i >= n) fail("unterminated string");
+      unsigned char c = s[i];
+      if (c == '"') {
+        tmp.append(s + run, i - run);
+        i++;
+        if (!changed) return ch.local(std::string_view(s + st, i - 1 - st));
+        return ch.local_owned(std::move(tmp));
       }
-    } else if (v->t == T::Arr) {
-      for (auto& e : v->a) stack.push_back(&e);
+      if (c == '\\') {
+        changed = true;
+        tmp.append(s + run, i - run);
+        i++;
+        if (i >= n) fail("bad escape");
+        char e = s[i++];
+        switch (e) {
+          case '"': tmp += '"'; break;
+          case '\\': tmp += '\\'; break;
+          case '/': tmp += '/'; break;
+          case 'b': tmp += '\b'; break;
+          case 'f': tmp += '\f'; break;
+          case 'n': tmp += '\n'; break;
+          case 'r': tmp += '\r'; break;
+          case 't': tmp += '\t'; break;
+          case 'u': {
+            uint32_t r;
+            if (!u4(i, &r)) fail("bad \\u escape");
+            i += 4;
+            if (r >= 0xD800 && r < 0xDC00) {
+              uint32_t r2;
+              if (i + 6 <= n && s[i] == '\\' && s[i + 1] == 'u' && u4(i + 2, &r2) && r2 >= 0xDC00 && r2 < 0xE000) {
+                i += 6;
+                r = 0x10000 + ((r - 0xD800) << 10) + (r2 - 0xDC00);
+              } else {
+                r = 0xFFFD;
+              }
+            } else if (r >= 0xDC00 && r < 0xE000) {
+              r = 0xFFFD;
+            }
+            pj::utf8_put(tmp, r);
+            break;
+          }
+          default: fail("bad escape");
+        }
+        run = i;
+        continue;
+      }
+      if (c < 0x20) fail("control character in string");
+      if (c < 0x80) { i++; continue; }
+      uint32_t r;
+      int w = pj::utf8_dec(s, n, i, &r);
+      if (r == 0xFFFD && w == 1) {
+        changed = true;
+        tmp.append(s + run, i - run);
+        pj::utf8_put(tmp, 0xFFFD);
+        i++;
+        run = i;
+        continue;
+      }
+      i += w;
     }
   }
-  ch.hdr.push_back(h);
-  ch.ns_names.push_back(h.ns);
-  ch.nodes.insert(ch.nodes.end(), em.out.begin(), em.out.end());
-}
+  void num(Node& nd) {
+    size_t st = i;
+    bool integral = true;
+    if (s[i] == '-') i++;
+    if (i >= n) fail("bad number");
+    if (s[i] == '0') i++;
+    else if (s[i] >= '1' && s[i] <= '9') while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+    else fail("bad number");
+    if (i < n && s[i] == '.') {
+      integral = false;
+      i++;
+      if (i >= n || s[i] < '0' || s[i] > '9') fail("bad fraction");
+      while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+    }
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+      integral = false;
+      i++;
+      if (i < n && (s[i] == '+' || s[i] == '-')) i++;
+      if (i >= n || s[i] < '0' || s[i] > '9') fail("bad exponent");
+      while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+    }
+    std::string_view lit(s + st, i - st);
+    if (integral) {
+      int64_t v;
+      bool ok;
+      size_t d0 = lit[0] == '-' ? 1 : 0;
+      if (lit.size() - d0 <= 18) {  // fits int64 without overflow checks
+        int64_t m = 0;
+        for (size_t k = d0; k < lit.size(); k++) m = m * 10 + (lit[k] - '0');
+        v = d0 ? -m : m;
+        ok = true;
+      } else {
+        ok = pj::go_parse_int64(std::string(lit), &v);
+      }
+      if (ok) {
+        nd.tk = N_INT;
+        uint64_t u = (uint64_t)v;
+        nd.a = (uint32_t)u;
+        nd.b = (uint32_t)(u >> 32);
+        nd.c = lit == "-0" ? ch.local(std::string_view("0")) : ch.local(lit);  // strconv.FormatInt form
+        return;
+      }
+    }
+    double f;
+    if (!pj::go_parse_float(std::string(lit), &f)) fail("number out of range");
+    nd.tk = N_FLOAT;
+    uint64_t u = __builtin_bit_cast(uint64_t, f);
+    nd.a = (uint32_t)u;
+    nd.b = (uint32_t)(u >> 32);
+    nd.c = (uint32_t)ch.faux.size();
+    uint32_t e = ch.local_owned(pj::go_fmt_E(f));
+    uint32_t f6 = ch.local_owned(pj::go_fmt_f6(f));
+    ch.faux.push_back(FloatAux{e, f6});
+  }
+  // parse one value; containers append their children block to `out`
+  Node val(int depth, bool metadata_map) {
+    if (depth > 512) fail("nesting too deep");
+    ws();
+    if (i >= n) fail("unexpected end of input");
+    Node nd{};
+    char c = s[i];
+    if (c == '{') {
+      i++;
+      nd.tk = N_MAP;
+      size_t base = pend.size();
+      std::unique_ptr<std::unordered_map<uint32_t, size_t>> big;
+      ws();
+      if (i < n && s[i] == '}') {
+        i++;
+      } else {
+        for (;;) {
+          ws();
+          if (i >= n || s[i] != '"') fail("expected key");
+          uint32_t k = str();
+          uint8_t kf = ch.lflags[k];
+          if (kf & LF_MAGIC) magicf = true;
+          if (metadata_map && (kf & LF_ANCHORISH)) anchorish = true;
+          ws();
+          if (i >= n || s[i] != ':') fail("expected ':'");
+          i++;
+          Node x = val(depth + 1, k == L_METADATA);
+          x.tk |= k << 4;
+          size_t at = NONE;  // duplicate key: the later value replaces the earlier one in place
+          if (big) {
+            auto it = big->find(k);
+            if (it != big->end()) at = it->second;
+          } else {
+            for (size_t q = base; q < pend.size(); q++)
+              if (node_key(pend[q]) == k) { at = q; break; }
+          }
+          if (at != (size_t)NONE) {
+            pend[at] = x;
+          } else {
+            if (big) big->emplace(k, pend.size());
+            pend.push_back(x);
+            if (!big && pend.size() - base > 32) {
+              big = std::make_unique<std::unordered_map<uint32_t, size_t>>();
+              for (size_t q = base; q < pend.size(); q++) big->emplace(node_key(pend[q]), q);
+            }
+          }
+          ws();
+          if (i < n && s[i] == ',') { i++; continue; }
+          if (i < n && s[i] == '}') { i++; break; }
+          fail("expected ',' or '}'");
+        }
+      }
+      size_t cnt = pend.size() - base;
+      if (cnt > 0xFFFF) magicf = true;  // walk frames count entries in 16 bits
+      nd.a = (uint32_t)out.size();
+      nd.b = (uint32_t)cnt;
+      out.insert(out.end(), pend.begin() + base, pend.end());
+      pend.resize(base);
+      return nd;
+    }
+    if (c == '[') {
+      i++;
+      nd.tk = N_ARR;
+      nd.c = NONE;  // path-column row of element 0, set by resolve_path_columns
+      size_t base = pend.size();
+      ws();
+      if (i < n && s[i] == ']') {
+        i++;
+      } else {
+        for (uint32_t k = 0;; k++) {
+          Node x = val(depth + 1, false);
+          x.tk |= k << 4;
+          pend.push_back(x);
+          ws();
+          if (i < n && s[i] == ',') { i++; continue; }
+          if (i < n && s[i] == ']') { i++; break; }
+          fail("expected ',' or ']'");
+        }
+      }
+      size_t cnt = pend.size() - base;
+      if (cnt > 0xFFFF) magicf = true;  // walk frames count elements in 16 bits
+      nd.a = (uint32_t)out.size();
+      nd.b = (uint32_t)cnt;
+      out.insert(out.end(), pend.begin() + base, pend.end());
+      pend.resize(base);
+      return nd;
+    }
+    if (c == '"') {
+      nd.tk = N_STR;
+      nd.a = str();
+      if (ch.lflags[nd.a] & LF_MAGIC) magicf = true;
+      return nd;
+    }
+    if (c == 't' && n - i >= 4 && memcmp(s + i, "true", 4) == 0) { i += 4; nd.tk = N_TRUE; nd.a = 1; return nd; }
+    if (c == 'f' && n - i >= 5 && memcmp(s + i, "false", 5) == 0) { i += 5; nd.tk = N_FALSE; return nd; }
+    if (c == 'n' && n - i >= 4 && memcmp(s + i, "null", 4) == 0) { i += 4; nd.tk = N_NULL; return nd; }
+    if (c == '-' || (c >= '0' && c <= '9')) { num(nd); return nd; }
+    fail("unexpected character");
+  }
 
-// split a JSON array / NDJSON buffer into document byte ranges
+  // one document -> node table + header (unstructured accessors on the final values)
+  void doc(const char* p, size_t len) {
+    s = p; n = len; i = 0;
+    magicf = anchorish = false;
+    out.clear();
+    out.resize(1);
+    Node root = val(0, false);
+    ws();
+    if (i != n) fail("trailing data");
+    out[0] = root;
+    ResHeader h{};
+    h.root = (uint32_t)ch.nodes.size();
+    h.nnodes = (uint32_t)out.size();
+    h.labels = h.ann = h.nsl = NONE;
+    uint32_t kind = L_EMPTY, av = L_EMPTY, name = L_EMPTY, gen = L_EMPTY, ns = L_EMPTY;
+    auto child = [&](uint32_t m, uint32_t key) -> uint32_t {  // relative index of the entry with key, NONE
+      if (node_type(out[m]) != N_MAP) return NONE;
+      for (uint32_t q = 0; q < out[m].b; q++) if (node_key(out[out[m].a + q]) == key) return out[m].a + q;
+      return NONE;
+    };
+    auto sval = [&](uint32_t x) { return x != NONE && node_type(out[x]) == N_STR ? out[x].a : (uint32_t)L_EMPTY; };
+    kind = sval(child(0, L_KIND));
+    av = sval(child(0, L_APIVERSION));
+    uint32_t meta = child(0, L_METADATA);
+    if (meta != NONE && node_type(out[meta]) == N_MAP) {
+      name = sval(child(meta, L_NAME));
+      gen = sval(child(meta, L_GENNAME));
+      ns = sval(child(meta, L_NAMESPACE));
+      auto smap = [&](uint32_t x) -> uint32_t {  // NestedStringMap: a map whose values are all strings
+        if (x == NONE || node_type(out[x]) != N_MAP) return NONE;
+        for (uint32_t q = 0; q < out[x].b; q++) if (node_type(out[out[x].a + q]) != N_STR) return NONE;
+        return x;
+      };
+      h.labels = smap(child(meta, L_LABELS));
+      h.ann = smap(child(meta, L_ANN));
+    }
+    h.kind = kind;
+    h.name = name;
+    h.gen_name = gen;
+    h.ns = ns;
+    std::string_view avs = ch.tab.strs[av];
+    size_t sl = std::count(avs.begin(), avs.end(), '/');
+    std::string_view g, ver;
+    bool gvok = true;
+    if (avs.empty() || avs == "/") {}
+    else if (sl == 0) ver = avs;
+    else if (sl == 1) { g = avs.substr(0, avs.find('/')); ver = avs.substr(avs.find('/') + 1); }
+    else gvok = false;
+    h.gvk_kind = gvok ? kind : (uint32_t)L_EMPTY;
+    h.group = ch.local(g);
+    h.version = ch.local(ver);
+    h.gv = g.empty() ? h.version : av;  // GroupVersion().String(): "group/version" is the apiVersion itself
+    h.flags = (magicf ? RF_MAGIC : 0) | (anchorish ? RF_ANCHORISH : 0) | (node_type(root) == N_MAP ? RF_ROOT_MAP : 0);
+    ch.hdr.push_back(h);
+    ch.nodes.insert(ch.nodes.end(), out.begin(), out.end());
+  }
+};
+
+// split a JSON array / concatenated documents into document byte ranges (serial; any input form)
 std::vector<std::pair<size_t, size_t>> split_docs(const char* p, size_t n) {
   std::vector<std::pair<size_t, size_t>> out;
   size_t i = 0;
@@ -233,9 +533,46 @@ std::vector<std::pair<size_t, size_t>> split_docs(const char* p, size_t n) {
         if (depth == 0) { i++; break; }
       } else if (depth == 0 && (c == ',' || c == '\n')) break;
     }
+    if (i == st) i++;  // a stray separator: a one-byte document that fails to parse
     out.push_back({st, i - st});
   }
   return out;
+}
+
+// NDJSON fast path: one document per non-blank line (JSON strings cannot hold a raw newline), found with memchr in
+// parallel. Returns false for input that is not line-delimited objects; a line that turns out not to be exactly one
+// document fails its parse and the caller re-splits serially.
+bool split_lines(const char* p, size_t n, int T, std::vector<std::pair<size_t, size_t>>* docs) {
+  size_t i = 0;
+  while (i < n && isspace((unsigned char)p[i])) i++;
+  if (i >= n || p[i] != '{') return false;
+  size_t parts = std::max<size_t>(1, std::min<size_t>((size_t)T * 4, n / (1 << 20) + 1));
+  std::vector<std::vector<std::pair<size_t, size_t>>> part(parts);
+  // part k owns the lines that start in [n*k/parts, n*(k+1)/parts)
+  parallel_for(parts, T, [&](size_t k) {
+    size_t lo = n * k / parts, hi = n * (k + 1) / parts;
+    size_t a = lo;
+    if (lo > 0 && p[lo - 1] != '\n') {  // the line running through lo belongs to an earlier part
+      const char* e = (const char*)memchr(p + lo, '\n', n - lo);
+      if (!e) return;
+      a = (size_t)(e - p) + 1;
+    }
+    while (a < hi) {
+      const char* e = (const char*)memchr(p + a, '\n', n - a);
+      size_t b = e ? (size_t)(e - p) : n;
+      size_t x = a, y = b;
+      while (x < y && isspace((unsigned char)p[x])) x++;
+      while (y > x && isspace((unsigned char)p[y - 1])) y--;
+      if (y > x) part[k].push_back({x, y - x});
+      a = b + 1;
+    }
+  });
+  size_t tot = 0;
+  for (auto& v : part) tot += v.size();
+  docs->clear();
+  docs->reserve(tot);
+  for (auto& v : part) docs->insert(docs->end(), v.begin(), v.end());
+  return true;
 }
 
 }  // namespace
@@ -258,14 +595,19 @@ void derive_strings(Batch& b, size_t from, int threads) {
         bool ascii = true;
         for (unsigned char c : x) if (c >= 0x80) { ascii = false; break; }
         if (ascii) f |= SF_ASCII;
+        // time.ParseDuration and resource.ParseQuantity need a sign, digit or '.' first; strconv.ParseFloat also
+        // accepts inf / infinity / nan spellings -- every other string skips the parsers
+        const char c0 = x.empty() ? 0 : x[0];
+        const bool numish = (c0 >= '0' && c0 <= '9') || c0 == '+' || c0 == '-' || c0 == '.';
         int64_t d;
-        if (pj::go_parse_duration(x, &d)) { f |= SF_DUR; b.str_dur[s] = d; } else b.str_dur[s] = 0;
+        if (numish && pj::go_parse_duration(x, &d)) { f |= SF_DUR; b.str_dur[s] = d; } else b.str_dur[s] = 0;
         int64_t lo, hi;
-        int q = pj::go_parse_quantity(x, &lo, &hi);
+        int q = numish ? pj::go_parse_quantity(x, &lo, &hi) : 0;
         if (q == 1) { f |= SF_QTY; b.str_qty[2 * s] = lo; b.str_qty[2 * s + 1] = hi; }
         else { b.str_qty[2 * s] = 0; b.str_qty[2 * s + 1] = 0; if (q == 2) f |= SF_QTY_BIG; }
         double fv;
-        if (pj::go_parse_float(x, &fv)) { f |= SF_FLOAT; b.str_f64[s] = fv; } else b.str_f64[s] = 0;
+        const bool floatish = numish || c0 == 'i' || c0 == 'I' || c0 == 'n' || c0 == 'N';
+        if (floatish && pj::go_parse_float(x, &fv)) { f |= SF_FLOAT; b.str_f64[s] = fv; } else b.str_f64[s] = 0;
         {  // strconv.ParseInt(x, 10, 64): optional sign, decimal digits, int64 range
           size_t i0 = (!x.empty() && (x[0] == '+' || x[0] == '-')) ? 1 : 0;
           bool digits = x.size() > i0;
@@ -410,7 +752,7 @@ void order_by_kind(Batch& b) {
   // counting sort by class (stable)
   std::vector<uint32_t> start(b.nclass + 1, 0);
   for (uint32_t c = 0; c < b.nclass; c++) start[c + 1] = start[c] + cls_count[c];
-  std::vector<ResHeader> sorted(n);
+  bulk_vector<ResHeader> sorted(n);
   b.order.resize(n);
   b.inv.resize(n);
   for (size_t i = 0; i < n; i++) {
@@ -427,63 +769,150 @@ void order_by_kind(Batch& b) {
 Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* nsl_json, size_t nsl_len, int threads,
                    std::string* err) {
   auto b = std::make_unique<Batch>();
+  const bool stats = getenv("KYV_DEBUG_STATS") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {
+    if (!stats) return;
+    auto t1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kyvgpu] flatten %-12s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+    t0 = t1;
+  };
   try {
     b->rs = rs;
-    b->dict = rs->dict;
-    auto docs = split_docs(json, len);
+    b->dict.strs = rs->dict.strs;  // batch strings are appended; the batch needs no reverse map after the build
+    const int T0 = std::max(1, threads);
+    std::vector<std::pair<size_t, size_t>> docs;
+    bool lines = split_lines(json, len, T0, &docs);
+    if (!lines) docs = split_docs(json, len);
+    phase("split");
     // threads scaled to the work: thread start-up is tens of microseconds, which dominates small (admission)
     // batches when every phase spawns the machine's thread count
-    int T = std::max(1, std::min(threads, (int)(docs.size() / 256) + 1));
-    size_t nchunks = std::min(docs.size(), (size_t)T * 8);
-    if (nchunks == 0) nchunks = 1;
-    std::vector<Chunk> chunks(nchunks);
-    std::atomic<size_t> next{0};
-    auto work = [&]() {
-      for (;;) {
-        size_t c = next.fetch_add(1);
-        if (c >= nchunks) break;
+    int T = 1;
+    std::vector<Chunk> chunks;
+    auto parse_all = [&]() {
+      T = std::max(1, std::min(T0, (int)(docs.size() / 256) + 1));
+      // chunks of at most ~2k documents keep each chunk's string table cache-resident while it is parsed
+      size_t nchunks = std::max<size_t>(1, std::min(docs.size(), std::max((size_t)T * 8, docs.size() / 2048)));
+      chunks.clear();
+      chunks.resize(nchunks);
+      parallel_for(nchunks, T, [&](size_t c) {
+        Chunk& ch = chunks[c];
+        Flat f(ch);
         size_t d0 = docs.size() * c / nchunks, d1 = docs.size() * (c + 1) / nchunks;
         try {
-          for (size_t d = d0; d < d1; d++) {
-            Value doc = pj::parse(json + docs[d].first, docs[d].second, false);
-            flatten_one(chunks[c], doc);
-          }
+          for (size_t d = d0; d < d1; d++) f.doc(json + docs[d].first, docs[d].second);
         } catch (std::exception& e) {
-          chunks[c].err = e.what();
+          ch.err = e.what();
+        }
+      });
+    };
+    parse_all();
+    bool bad = false;
+    for (auto& c : chunks) bad = bad || !c.err.empty();
+    if (bad && lines) {  // not one document per line after all: split by the JSON grammar and parse again
+      docs = split_docs(json, len);
+      parse_all();
+    }
+    for (auto& c : chunks) if (!c.err.empty()) throw std::runtime_error(c.err);
+    const size_t nchunks = chunks.size();
+    phase("parse");
+
+    // batch string ids: the ruleset's dictionary keeps its ids; new strings are interned in 256 hash shards in
+    // parallel, each shard in chunk order (= first-occurrence order within the shard, independent of T)
+    const auto& seed = rs->dict.strs;
+    const size_t nseed = seed.size();
+    StrTab seedtab;
+    {
+      size_t cap = 64;
+      while (cap < 2 * nseed + 2) cap <<= 1;
+      seedtab.rehash(cap);
+      bool added;
+      for (auto& s : seed) seedtab.add(s, hash_bytes(s.data(), s.size()), &added);
+    }
+    constexpr uint32_t NSH = 256;
+    auto shard_of = [](uint64_t h) { return (uint32_t)(h >> 56); };
+    std::vector<std::vector<uint32_t>> remap(nchunks), grp(nchunks), goff(nchunks);
+    parallel_for(nchunks, T, [&](size_t c) {
+      const StrTab& tab = chunks[c].tab;
+      size_t m = tab.strs.size();
+      auto& rm = remap[c];
+      rm.assign(m, NONE);
+      std::vector<uint32_t> off(NSH + 1, 0);
+      for (size_t s = 0; s < m; s++) {
+        uint32_t id = seedtab.find(tab.strs[s], tab.hashes[s]);
+        if (id != NONE) rm[s] = id;
+        else off[shard_of(tab.hashes[s]) + 1]++;
+      }
+      for (uint32_t h = 0; h < NSH; h++) off[h + 1] += off[h];
+      std::vector<uint32_t> pos(off.begin(), off.end() - 1);
+      grp[c].resize(off[NSH]);
+      for (size_t s = 0; s < m; s++)
+        if (rm[s] == NONE) grp[c][pos[shard_of(tab.hashes[s])]++] = (uint32_t)s;
+      goff[c].swap(off);
+    });
+    std::vector<StrTab> shard(NSH);
+    parallel_for(NSH, T, [&](size_t h) {
+      StrTab& t = shard[h];
+      size_t want = 0;
+      for (size_t c = 0; c < nchunks; c++) want += goff[c][h + 1] - goff[c][h];
+      size_t cap = 64;
+      while (cap < 2 * want + 2) cap <<= 1;
+      t.rehash(cap);
+      bool added;
+      for (size_t c = 0; c < nchunks; c++) {
+        const StrTab& tab = chunks[c].tab;
+        for (uint32_t q = goff[c][h]; q < goff[c][h + 1]; q++) {
+          uint32_t s = grp[c][q];
+          remap[c][s] = 0x80000000u | t.add(tab.strs[s], tab.hashes[s], &added);
         }
       }
+    });
+    std::vector<size_t> shbase(NSH + 1, nseed);
+    for (uint32_t h = 0; h < NSH; h++) shbase[h + 1] = shbase[h] + shard[h].strs.size();
+    if (shbase[NSH] > 0x7FFFFFF0ull) throw std::runtime_error("batch dictionary exceeds 2^31 strings; split the batch");
+    b->dict.strs.resize(shbase[NSH]);
+    parallel_for(NSH, T, [&](size_t h) {
+      for (size_t j = 0; j < shard[h].strs.size(); j++) b->dict.strs[shbase[h] + j].assign(shard[h].strs[j]);
+    });
+    parallel_for(nchunks, T, [&](size_t c) {
+      const StrTab& tab = chunks[c].tab;
+      for (size_t s = 0; s < remap[c].size(); s++)
+        if (remap[c][s] & 0x80000000u)
+          remap[c][s] = (uint32_t)(shbase[shard_of(tab.hashes[s])] + (remap[c][s] & 0x7FFFFFFFu));
+    });
+    std::unordered_map<std::string, uint32_t> extra;  // namespace-label strings the batch does not hold
+    auto intern = [&](const std::string& s) -> uint32_t {
+      uint64_t h = hash_bytes(s.data(), s.size());
+      uint32_t id = seedtab.find(s, h);
+      if (id != NONE) return id;
+      id = shard[shard_of(h)].find(s, h);
+      if (id != NONE) return (uint32_t)(shbase[shard_of(h)] + id);
+      auto it = extra.find(s);
+      if (it != extra.end()) return it->second;
+      id = (uint32_t)b->dict.strs.size();
+      b->dict.strs.push_back(s);
+      extra.emplace(s, id);
+      return id;
     };
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; t++) th.emplace_back(work);
-    for (auto& t : th) t.join();
-    for (auto& c : chunks) if (!c.err.empty()) throw std::runtime_error(c.err);
-    size_t seed = b->dict.strs.size();
-    // merge dictionaries
-    std::vector<std::vector<uint32_t>> remap(nchunks);
-    for (size_t c = 0; c < nchunks; c++) {
-      remap[c].resize(chunks[c].strs.size());
-      for (size_t s = 0; s < chunks[c].strs.size(); s++) remap[c][s] = b->dict.intern(chunks[c].strs[s]);
-    }
+    phase("merge-dict");
     // namespace label sets
     std::unordered_map<uint32_t, uint32_t> ns_set;
+    b->nsl_off.push_back(0);
     if (nsl_json && nsl_len) {
       Value nsl = pj::parse(nsl_json, nsl_len, false);
-      b->nsl_off.push_back(0);
       if (nsl.t == T::Obj)
         for (auto& kv : nsl.o) {
-          ns_set[b->dict.intern(kv.first)] = (uint32_t)b->nsl_names.size();
+          ns_set[intern(kv.first)] = (uint32_t)b->nsl_names.size();
           b->nsl_names.push_back(kv.first);
           if (kv.second.t == T::Obj)
             for (auto& lv : kv.second.o) {
-              b->nsl_kv.push_back(b->dict.intern(lv.first));
-              b->nsl_kv.push_back(b->dict.intern(lv.second.t == T::Str ? lv.second.s : ""));
+              b->nsl_kv.push_back(intern(lv.first));
+              b->nsl_kv.push_back(intern(lv.second.t == T::Str ? lv.second.s : ""));
             }
           b->nsl_off.push_back((uint32_t)b->nsl_kv.size() / 2);
         }
-    } else {
-      b->nsl_off.push_back(0);
     }
-    // concatenate + remap + sort map entries
+    // concatenate + remap + sort map entries by key id (+ labels / annotations entries found again after the sort)
     size_t total_nodes = 0, total_res = 0, total_faux = 0;
     std::vector<size_t> node_base(nchunks), res_base(nchunks), faux_base(nchunks);
     for (size_t c = 0; c < nchunks; c++) {
@@ -496,67 +925,64 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
     b->nodes.resize(total_nodes);
     b->hdr.resize(total_res);
     b->faux.resize(total_faux);
-    next = 0;
-    auto fix = [&]() {
-      for (;;) {
-        size_t c = next.fetch_add(1);
-        if (c >= nchunks) break;
-        Chunk& ch = chunks[c];
-        const auto& rm = remap[c];
-        for (size_t k = 0; k < ch.faux.size(); k++)
-          b->faux[faux_base[c] + k] = FloatAux{rm[ch.faux[k].sid_E], rm[ch.faux[k].sid_F]};
-        for (size_t r = 0; r < ch.hdr.size(); r++) {
-          ResHeader h = ch.hdr[r];
-          Node* R = b->nodes.data() + node_base[c] + h.root;
-          const Node* src = ch.nodes.data() + h.root;
-          for (uint32_t i = 0; i < h.nnodes; i++) {
-            Node n = src[i];
-            uint32_t t = node_type(n);
-            // key bits hold a local sid for map entries: detect by parent type below; remap all key fields of
-            // map children after copying
-            if (t == N_STR) n.a = rm[n.a];
-            else if (t == N_INT) n.c = rm[n.c];
-            else if (t == N_FLOAT) n.c += (uint32_t)faux_base[c];
-            R[i] = n;
-          }
-          for (uint32_t i = 0; i < h.nnodes; i++) {
-            if (node_type(R[i]) != N_MAP) continue;
-            Node* ch0 = R + R[i].a;
-            for (uint32_t k = 0; k < R[i].b; k++) ch0[k].tk = (rm[ch0[k].tk >> 4] << 4) | (ch0[k].tk & 0xF);
-            std::sort(ch0, ch0 + R[i].b, [](const Node& x, const Node& y) { return (x.tk >> 4) < (y.tk >> 4); });
-          }
-          h.root = (uint32_t)(node_base[c] + h.root);
-          h.kind = rm[h.kind]; h.gvk_kind = rm[h.gvk_kind]; h.group = rm[h.group]; h.version = rm[h.version];
-          h.gv = rm[h.gv]; h.name = rm[h.name]; h.gen_name = rm[h.gen_name]; h.ns = rm[h.ns];
-          auto it = ns_set.find(h.ns);
-          h.nsl = it == ns_set.end() ? NONE : it->second;
-          b->hdr[res_base[c] + r] = h;
+    parallel_for(nchunks, T, [&](size_t c) {
+      Chunk& ch = chunks[c];
+      const auto& rm = remap[c];
+      for (size_t k = 0; k < ch.faux.size(); k++)
+        b->faux[faux_base[c] + k] = FloatAux{rm[ch.faux[k].sid_E], rm[ch.faux[k].sid_F]};
+      for (size_t r = 0; r < ch.hdr.size(); r++) {
+        ResHeader h = ch.hdr[r];
+        Node* R = b->nodes.data() + node_base[c] + h.root;
+        const Node* src = ch.nodes.data() + h.root;
+        for (uint32_t i = 0; i < h.nnodes; i++) {
+          Node n = src[i];
+          uint32_t t = node_type(n);
+          if (t == N_STR) n.a = rm[n.a];
+          else if (t == N_INT) n.c = rm[n.c];
+          else if (t == N_FLOAT) n.c += (uint32_t)faux_base[c];
+          R[i] = n;
         }
+        for (uint32_t i = 0; i < h.nnodes; i++) {  // map entries: key ids remapped, then sorted by key
+          if (node_type(R[i]) != N_MAP) continue;
+          Node* ch0 = R + R[i].a;
+          for (uint32_t k = 0; k < R[i].b; k++) ch0[k].tk = (rm[ch0[k].tk >> 4] << 4) | (ch0[k].tk & 0xF);
+          const uint32_t m = R[i].b;
+          if (m <= 24) {
+            for (uint32_t a = 1; a < m; a++) {
+              Node x = ch0[a];
+              uint32_t z = a;
+              for (; z > 0 && (ch0[z - 1].tk >> 4) > (x.tk >> 4); z--) ch0[z] = ch0[z - 1];
+              ch0[z] = x;
+            }
+          } else {
+            std::sort(ch0, ch0 + m, [](const Node& x, const Node& y) { return (x.tk >> 4) < (y.tk >> 4); });
+          }
+        }
+        if (h.labels != NONE || h.ann != NONE) {
+          auto find = [&](uint32_t m, uint32_t key) -> uint32_t {
+            if (m == NONE || node_type(R[m]) != N_MAP) return NONE;
+            for (uint32_t i = 0; i < R[m].b; i++) if (node_key(R[R[m].a + i]) == key) return R[m].a + i;
+            return NONE;
+          };
+          uint32_t meta = find(0, KSID(METADATA));
+          if (h.labels != NONE) h.labels = find(meta, KSID(LABELS));
+          if (h.ann != NONE) h.ann = find(meta, KSID(ANNOTATIONS));
+        }
+        h.root = (uint32_t)(node_base[c] + h.root);
+        h.kind = rm[h.kind]; h.gvk_kind = rm[h.gvk_kind]; h.group = rm[h.group]; h.version = rm[h.version];
+        h.gv = rm[h.gv]; h.name = rm[h.name]; h.gen_name = rm[h.gen_name]; h.ns = rm[h.ns];
+        auto it = ns_set.find(h.ns);
+        h.nsl = it == ns_set.end() ? NONE : it->second;
+        b->hdr[res_base[c] + r] = h;
       }
-    };
-    th.clear();
-    for (int t = 0; t < T; t++) th.emplace_back(fix);
-    for (auto& t : th) t.join();
-    // labels/annotations node indices moved when map entries were sorted: recompute from the sorted tables
-    for (auto& h : b->hdr) {
-      if (h.labels == NONE && h.ann == NONE) continue;
-      const Node* R = b->nodes.data() + h.root;
-      uint32_t meta = (node_type(R[0]) == N_MAP) ? [&]() {
-        for (uint32_t i = 0; i < R[0].b; i++) if (node_key(R[R[0].a + i]) == KSID(METADATA)) return R[0].a + i;
-        return NONE;
-      }() : NONE;
-      auto find = [&](uint32_t key) -> uint32_t {
-        if (meta == NONE || node_type(R[meta]) != N_MAP) return NONE;
-        for (uint32_t i = 0; i < R[meta].b; i++) if (node_key(R[R[meta].a + i]) == key) return R[meta].a + i;
-        return NONE;
-      };
-      if (h.labels != NONE) h.labels = find(KSID(LABELS));
-      if (h.ann != NONE) h.ann = find(KSID(ANNOTATIONS));
-    }
+    });
+    phase("remap");
     derive_strings(*b, 0, std::max(1, std::min(T, (int)(b->dict.strs.size() / 8192) + 1)));
+    phase("strings");
     order_by_kind(*b);
+    phase("kind-order");
     resolve_path_columns(*b, T);
-    (void)seed;
+    phase("path-cols");
     return b.release();
   } catch (std::exception& e) {
     if (err) *err = e.what();
@@ -571,6 +997,7 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
 namespace {
 struct Resolver {
   const Ruleset& rs;
+  const std::vector<std::vector<std::pair<uint32_t, uint32_t>>>& kids;  // trie kids sorted by key sid
   Node* R;
   uint64_t* colv;            // nullptr in the counting pass
   const uint32_t* col_off;
@@ -591,11 +1018,25 @@ struct Resolver {
     const Ruleset::TrieNode& T = rs.trie[t];
     const Node mn = R[m];
     if (node_type(mn) == N_MAP) {
-      for (auto& kv : T.kids) {
-        uint32_t x = find(R, mn, kv.first);
-        if (x == NONE) continue;  // columns are NONE-initialised
-        if (colv) colv[(size_t)col_off[rs.trie[kv.second].col] + row] = entry(x);
-        go(x, kv.second, row);
+      const auto& K = kids[t];
+      auto hit = [&](uint32_t x, uint32_t kid) {
+        if (colv) colv[(size_t)col_off[rs.trie[kid].col] + row] = entry(x);
+        go(x, kid, row);
+      };
+      if (mn.b <= 2 * K.size() + 4) {  // merge join of two key-sorted lists
+        uint32_t a = mn.a, e = mn.a + mn.b;
+        size_t j = 0;
+        while (a < e && j < K.size()) {
+          uint32_t k = node_key(R[a]);
+          if (k < K[j].first) a++;
+          else if (k > K[j].first) j++;
+          else { hit(a, K[j].second); a++; j++; }
+        }
+      } else {
+        for (auto& kv : K) {
+          uint32_t x = find(R, mn, kv.first);
+          if (x != NONE) hit(x, kv.second);  // columns are NONE-initialised
+        }
       }
     } else if (node_type(mn) == N_ARR && T.star != NONE) {
       uint32_t space = rs.trie[T.star].rowspace;
@@ -622,6 +1063,11 @@ void resolve_path_columns(Batch& b, int threads) {
   b.colv.clear();
   if (rs.ncols == 0 || n == 0) return;
   int T = std::max(1, threads);
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> kids(rs.trie.size());
+  for (size_t t = 0; t < rs.trie.size(); t++) {
+    kids[t] = rs.trie[t].kids;
+    std::sort(kids[t].begin(), kids[t].end());
+  }
   size_t nch = std::min(n, (size_t)T * 8);
   std::vector<std::vector<uint32_t>> cnt(nch, std::vector<uint32_t>(nsp, 0));
   auto eligible = [&](const ResHeader& h) { return h.nnodes < (1u << COL_TYPE_SHIFT); };
@@ -635,7 +1081,7 @@ void resolve_path_columns(Batch& b, int threads) {
         for (size_t r = r0; r < r1; r++) {
           ResHeader& h = b.hdr[r];
           if (!eligible(h)) continue;
-          Resolver rv{rs, b.nodes.data() + h.root, fill ? b.colv.data() : nullptr, b.col_off.data(), nexts[c].data()};
+          Resolver rv{rs, kids, b.nodes.data() + h.root, fill ? b.colv.data() : nullptr, b.col_off.data(), nexts[c].data()};
           rv.go(0, 0, (uint32_t)r);
         }
       }
@@ -661,7 +1107,14 @@ void resolve_path_columns(Batch& b, int threads) {
     total += b.rs_rows[rs.col_rowspace[c]];
     if (total > 0xFFFFFFF0ull) throw std::runtime_error("path columns exceed 2^32 entries; split the batch");
   }
-  b.colv.assign(total + 1, (uint64_t)NONE);
+  b.colv.resize(total + 1);  // NONE-initialised in parallel, one slice per worker
+  {
+    const size_t per = (1u << 20);
+    parallel_for((total + per) / per, T, [&](size_t k) {
+      size_t lo = k * per, hi = std::min<size_t>(total + 1, lo + per);
+      std::fill(b.colv.begin() + lo, b.colv.begin() + hi, (uint64_t)NONE);
+    });
+  }
   if (getenv("KYV_DEBUG_STATS")) {
     fprintf(stderr, "[kyvgpu] path columns: %u columns, %u row spaces, %llu entries (rows:", rs.ncols, nsp,
             (unsigned long long)total);

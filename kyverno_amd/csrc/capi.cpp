@@ -5,6 +5,8 @@
 #include <map>
 #include <mutex>
 #include <thread>
+#include <sched.h>
+#include <cstring>
 
 #include "../../include/kyvgpu.h"
 #include "kyv_host.h"
@@ -34,10 +36,31 @@ struct kyv_results {
 static thread_local std::string g_err;
 static int fail(int code, const std::string& m) { g_err = m; return code; }
 
+// worker threads when the caller passes 0: KYV_THREADS, else the CPUs this process may use -- its affinity mask
+// bounded by a cgroup v2 CPU quota (cpu.max), as on shared GPU hosts where the machine's CPU count is many times
+// the job's share -- capped at 64
 static int hw_threads(int t) {
   if (t > 0) return t;
-  unsigned h = std::thread::hardware_concurrency();
-  return h ? (int)std::min(h, 64u) : 4;
+  static const int n = []() {
+    if (const char* e = getenv("KYV_THREADS")) {
+      int v = atoi(e);
+      if (v > 0) return v;
+    }
+    int c = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) c = CPU_COUNT(&set);
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long period = 0;
+      if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+        long quota = atol(q);
+        if (quota > 0) c = std::min<long>(c, (quota + period - 1) / period);
+      }
+      fclose(f);
+    }
+    return std::max(1, std::min(c, 64));
+  }();
+  return n;
 }
 
 extern "C" {

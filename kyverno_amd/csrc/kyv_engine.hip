@@ -34,14 +34,26 @@ namespace kyv {
   } while (0)
 
 // ---------------------------------------------------------------- device images
+// Device-buffer layout of host arrays: offsets are assigned first (256-byte aligned, 16 zero bytes of slack after
+// each array), then the buffer is zeroed on the device and every array is copied straight from its host vector --
+// no host-side staging copy of the batch
 struct Packer {
-  std::vector<uint8_t> host;
-  template <class X>
-  size_t add(const std::vector<X>& v) {
-    size_t off = (host.size() + 255) & ~(size_t)255;
-    host.resize(off + v.size() * sizeof(X) + 16);
-    if (!v.empty()) memcpy(host.data() + off, v.data(), v.size() * sizeof(X));
+  struct Part { size_t off; const void* src; size_t bytes; };
+  std::vector<Part> parts;
+  size_t size = 0;
+  template <class V>
+  size_t add(const V& v) {
+    size_t off = (size + 255) & ~(size_t)255;
+    size_t bytes = v.size() * sizeof(*v.data());
+    parts.push_back({off, v.data(), bytes});
+    size = off + bytes + 16;
     return off;
+  }
+  hipError_t copy_to(uint8_t* dev) const {
+    hipError_t e = hipMemset(dev, 0, size);
+    for (auto& q : parts)
+      if (e == hipSuccess && q.bytes) e = hipMemcpy(dev + q.off, q.src, q.bytes, hipMemcpyHostToDevice);
+    return e;
   }
 };
 
@@ -223,9 +235,9 @@ static DevRuleset* upload_ruleset(const Ruleset& rs, int device) {
   d->o_cnodes = p.add(rs.cnodes);
   d->o_conds = p.add(rs.conds);
   d->o_cprogs = p.add(rs.cprogs);
-  d->bytes = p.host.size();
+  d->bytes = p.size;
   HIP_OK(hipMalloc(&d->base, d->bytes));
-  HIP_OK(hipMemcpy(d->base, p.host.data(), d->bytes, hipMemcpyHostToDevice));
+  HIP_OK(p.copy_to(d->base));
   return d;
 }
 
@@ -255,9 +267,9 @@ static DevBatch* upload_batch(const Batch& b, int device) {
   std::vector<PEntry> pe = b.rs->pentries;
   for (auto& E : pe) if (E.col != NONE) E.col = b.col_off[E.col];
   d->o_pe = p.add(pe);
-  d->bytes = p.host.size();
+  d->bytes = p.size;
   HIP_OK(dmalloc(&d->base, d->bytes));
-  HIP_OK(hipMemcpy(d->base, p.host.data(), d->bytes, hipMemcpyHostToDevice));
+  HIP_OK(p.copy_to(d->base));
   d->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return d;
 }

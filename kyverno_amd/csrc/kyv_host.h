@@ -12,6 +12,18 @@ namespace kyv {
 
 // String dictionary: seeded with the fixed/well-known ids, then the ruleset literals; every batch copies
 // the ruleset dictionary and appends its own strings.
+// vector storage without value-initialisation: the flattener's large tables are written once, in parallel, so
+// zero-filling them first (serially) would only add page-fault and memset time
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U> struct rebind { using other = NoInitAlloc<U>; };
+  NoInitAlloc() = default;
+  template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
+  template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+template <class T> using bulk_vector = std::vector<T, NoInitAlloc<T>>;
+
 struct Dict {
   std::vector<std::string> strs;
   std::unordered_map<std::string, uint32_t> ids;
@@ -116,8 +128,8 @@ struct Ruleset {
 struct Batch {
   const Ruleset* rs = nullptr;
   Dict dict;                      // ruleset dict + batch strings
-  std::vector<Node> nodes;
-  std::vector<ResHeader> hdr;
+  bulk_vector<Node> nodes;
+  bulk_vector<ResHeader> hdr;
   std::vector<FloatAux> faux;
   std::vector<uint32_t> str_off, str_len, str_flags;
   std::vector<int64_t> str_dur, str_qty;
@@ -132,7 +144,7 @@ struct Batch {
   std::vector<uint32_t> gate;     // [kclass][gate_words] bit k: rule k can match a resource of this class
   uint32_t gate_words = 0, nclass = 0;
   // path columns (kyv_layout.h): colv[col_off[c] + row]
-  std::vector<uint64_t> colv;
+  bulk_vector<uint64_t> colv;
   std::vector<uint32_t> col_off, rs_rows;
   std::vector<void*> dev;
   ~Batch();

@@ -1,6 +1,7 @@
 // Product-side JSON reader and Go-compatible scalar helpers (see pjson.h).
 #include "pjson.h"
 
+#include <algorithm>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
