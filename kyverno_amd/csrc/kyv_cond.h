@@ -173,7 +173,7 @@ KYV_HD void j_drop_nulls(JList& L) {
   for (uint32_t j = 0; j < L.n; j++) if (L.e[j] != NONE) L.e[w++] = L.e[j];
   L.n = w;
 }
-KYV_HD int jmes_run(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, JRes* out, uint32_t* miss) {
+__host__ __device__ __attribute__((noinline)) int jmes_run(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, JRes* out, uint32_t* miss) {
   const uint32_t* p = v.pool + o.a;
   const uint32_t n = o.nseg, root = p[0] & 0xFFu;
   const bool pure = (p[0] & JF_PURE) != 0;
@@ -648,7 +648,10 @@ KYV_HD int eval_cond(const View& v, NodeTab R, const Cond& c, const CV& k, const
 // Whole program: substitution first (every reference of the document, vars.go:352-431: any NotFoundError ->
 // error), then any/all evaluation (evaluate.go:42-69). Returns CR_TRUE / CR_FALSE / CR_FB / CR_PANIC, or
 // CP_ERROR with *err_cond / *err_side / *err_seg naming the first unresolved reference (for the host message).
+// kJ = false instantiates the program without the JMESPath interpreter (no projection lists on the stack): the
+// light match kernel evaluates only rules whose programs hold no OK_JMES operand (the host routes the others).
 constexpr int CP_ERROR = 5;
+template <bool kJ = true>
 KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond, uint32_t* err_side, uint32_t* err_seg,
                      uint32_t elem = NONE) {
   const CondProg& p = v.cprogs[prog];
@@ -666,10 +669,14 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
           return CP_ERROR;
         }
         if (o.kind == OK_JMES) {
-          JList L;
-          const int st = operand_cv(v, R, o, elem, L, &tmp, &miss);
-          if (st == JS_FB) return CR_FB;
-          if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
+          if constexpr (!kJ) {
+            return CR_FB;
+          } else {
+            JList L;
+            const int st = operand_cv(v, R, o, elem, L, &tmp, &miss);
+            if (st == JS_FB) return CR_FB;
+            if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
+          }
         }
       }
     }
@@ -678,10 +685,16 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
     const Cond& c = v.conds[ci];
     CV k, x;
     uint32_t miss;
-    JList lk, lx;
-    operand_cv(v, R, c.key, elem, lk, &k, &miss);
-    operand_cv(v, R, c.value, elem, lx, &x, &miss);
-    return eval_cond(v, R, c, k, x);
+    if constexpr (kJ) {
+      JList lk, lx;
+      operand_cv(v, R, c.key, elem, lk, &k, &miss);
+      operand_cv(v, R, c.value, elem, lx, &x, &miss);
+      return eval_cond(v, R, c, k, x);
+    } else {
+      cv_operand(v, R, c.key, &k, &miss);
+      cv_operand(v, R, c.value, &x, &miss);
+      return eval_cond(v, R, c, k, x);
+    }
   };
   if (p.nany != NONE) {
     bool any = false;

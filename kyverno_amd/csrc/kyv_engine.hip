@@ -158,6 +158,23 @@ static void stream_put(int dev, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   g_streams_free.push_back(StreamSet{dev, s, e0, e1});
 }
 
+// rules the light match kernel cannot evaluate: foreach, or a precondition / deny program with a JMESPath operand
+static bool prog_jmes(const Ruleset& rs, uint32_t prog) {
+  if (prog == NONE) return false;
+  const CondProg& p = rs.cprogs[prog];
+  auto blk = [&](uint32_t c0, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++)
+      if (rs.conds[c0 + i].key.kind == OK_JMES || rs.conds[c0 + i].value.kind == OK_JMES) return true;
+    return false;
+  };
+  return blk(p.any0, p.nany == NONE ? 0u : p.nany) || blk(p.all0, p.nall);
+}
+static bool rule_needs_jmes(const Ruleset& rs, const RuleDesc& rd) {
+  if (rd.kind == RK_FOREACH) return true;
+  if (prog_jmes(rs, rd.pre)) return true;
+  return rd.kind == RK_DENY && prog_jmes(rs, rd.root);
+}
+
 // One rule slice of an evaluation. Work lists, failing-path staging and compaction buffers are sized per (rule,
 // resource) pair, so a ruleset whose buffers would not fit (C4: 10k+ rules x 1M resources) is evaluated as
 // consecutive slices of its rule range [k0, k1) reusing one set of those buffers; verdict bytes, PSS masks and
@@ -166,8 +183,8 @@ struct SliceSched {
   uint32_t k0 = 0, k1 = 0;
   size_t stage_tot = 0;          // staging slots (records) of the slice
   uint32_t* rbase = nullptr;     // [k1 - k0] first staging slot of each rule (slice-local)
-  uint32_t* mrules = nullptr;    // rules of the slice match_kernel evaluates (direct-walk rules excluded)
-  uint32_t nm = 0;
+  uint32_t* mrules = nullptr;    // rules of the slice match_kernel evaluates (direct-walk rules excluded):
+  uint32_t nm = 0, nmj = 0;      // [0, nm) light, then [nm, nm + nmj) with JMESPath operands / foreach
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
@@ -342,6 +359,9 @@ constexpr int RECS_PER_PAIR = MAX_ALTS;
 // Phase 1 (match_eval): one lane per resource, the rule loop uniform across the wave. Kind gate, match /
 // exclude program, dispatch; verdicts that need no pattern walk are final here (incl. PodSecurity). Pairs
 // that need the walk are appended to the rule's work list (wave ballot + one atomic per wave and rule).
+// Two instantiations: kJ = false for rules without JMESPath operands or foreach (the register budget of the
+// plain match / condition / PodSecurity code), kJ = true for the rest (projection lists live in scratch)
+template <bool kJ>
 __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl,
                                                       const uint32_t* __restrict__ mrules, uint32_t nm) {
   const View& v = *vp;
@@ -355,7 +375,7 @@ __global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ v
     if (!__ballot(gated)) continue;  // status bytes are pre-set to ST_NONE, PSS masks to 0
     uint32_t pf = 0;
     bool walk = false;
-    const uint8_t st = pair_dispatch(v, gated, r, k, &pf, &walk);
+    const uint8_t st = pair_dispatch<kJ>(v, gated, r, k, &pf, &walk);
     const unsigned long long wm = __ballot(walk);
     const RuleDesc& rdk = v.rules[k];
     if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {  // this wave's work list for rule k
@@ -736,17 +756,20 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       sl.stage_tot = stage;
       std::vector<uint32_t> rb(std::max<size_t>(sl.k1 - sl.k0, 1), 0);
       size_t tot = 0;
-      std::vector<uint32_t> ml;
+      std::vector<uint32_t> ml, mj;
       for (uint32_t q = sl.k0; q < sl.k1; q++) {
         const RuleDesc& rd = rs.rules[q];
         rb[q - sl.k0] = (uint32_t)tot;
         tot += (rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, MAX_ALTS) : 0) * nwv * WAVE;
         const bool direct = (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) && (rd.flags & RD_GATE_EXACT);
-        if (!direct) ml.push_back(q);
+        if (!direct) (rule_needs_jmes(rs, rd) ? mj : ml).push_back(q);
       }
+      sl.nmj = (uint32_t)mj.size();
+      const size_t nlight = ml.size();
+      ml.insert(ml.end(), mj.begin(), mj.end());
       HIP_OK(dmalloc(&sl.rbase, rb.size() * 4));
       HIP_OK(hipMemcpy(sl.rbase, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
-      sl.nm = (uint32_t)ml.size();
+      sl.nm = (uint32_t)nlight;
       HIP_OK(dmalloc(&sl.mrules, std::max<size_t>(1, ml.size()) * 4));
       if (!ml.empty()) HIP_OK(hipMemcpy(sl.mrules, ml.data(), ml.size() * 4, hipMemcpyHostToDevice));
       d.max_slice_rules = std::max<size_t>(d.max_slice_rules, sl.k1 - sl.k0);
@@ -807,7 +830,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, sl.rbase, d.rcnt, sl.k0, sl.k1};
       HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
       HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
-      if (sl.nm) hipLaunchKernelGGL(match_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, sl.mrules, sl.nm);
+      if (sl.nm)
+        hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, sl.mrules, sl.nm);
+      if (sl.nmj)
+        hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
+                           (const uint32_t*)sl.mrules + sl.nm, sl.nmj);
       HIP_OK(hipGetLastError());
       if (sl.grid[0]) {
         hipLaunchKernelGGL(walk_kernel, dim3(sl.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, sl.cm[0],

@@ -553,6 +553,8 @@ KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root) {
 
 // Match + dispatch of one pair (validation.go:134-183, :276-317). Returns the verdict, or sets *walk for a
 // pattern / anyPattern pair whose verdict comes from the pattern walk (pair_walk).
+// kJ = false: the light instantiation (no JMESPath operands, no foreach) for rules the host classified as such
+template <bool kJ = true>
 KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k, uint32_t* pss_fails, bool* walk) {
   *pss_fails = 0;
   *walk = false;
@@ -575,7 +577,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
   if (rd.kind == RK_FALLBACK) return ST_FALLBACK;
   uint32_t ec, es, eg;
   if (rd.pre != NONE) {  // checkPreconditions (validation.go:281-288)
-    int c = eval_prog(v, R, rd.pre, &ec, &es, &eg);
+    int c = eval_prog<kJ>(v, R, rd.pre, &ec, &es, &eg);
     if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
     if (c == CR_PANIC) return ST_PANIC;
     if (c == CP_ERROR) return ST_ERROR | ST_MARK_PRE;
@@ -585,14 +587,16 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
     case RK_PANIC: return ST_PANIC;
     case RK_ERROR: return ST_ERROR;
     case RK_DENY: {  // validateDeny (validation.go:437-464)
-      int c = eval_prog(v, R, rd.root, &ec, &es, &eg);
+      int c = eval_prog<kJ>(v, R, rd.root, &ec, &es, &eg);
       if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
       if (c == CR_PANIC) return ST_PANIC;
       if (c == CP_ERROR) return ST_ERROR;
       return c == CR_TRUE ? ST_FAIL : ST_PASS;
     }
     case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
-    case RK_FOREACH: return eval_foreach(v, R, rd.root);
+    case RK_FOREACH:
+      if constexpr (kJ) return eval_foreach(v, R, rd.root);
+      else return ST_FALLBACK;
     case RK_PATTERN: case RK_ANYPATTERN:
       if (h.flags & RF_MAGIC) return KYV_WHY(FBW_PHRASE), ST_FALLBACK;
       *walk = true;
