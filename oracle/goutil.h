@@ -586,6 +586,33 @@ inline bool is_space_rune(uint32_t r) {
          r == 0x3000;
 }
 
+// path.Clean (Go): collapse slashes, drop "." elements, resolve ".." against the preceding element (kept when
+// nothing precedes it in a relative path, dropped at the root of an absolute one); "" -> "."
+inline std::string clean_path(const std::string& p) {
+  if (p.empty()) return ".";
+  const bool rooted = p[0] == '/';
+  std::vector<std::string> st;
+  size_t i = 0;
+  while (i <= p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    std::string e = p.substr(i, j - i);
+    i = j + 1;
+    if (e.empty() || e == ".") { if (j == p.size()) break; continue; }
+    if (e == "..") {
+      if (!st.empty() && st.back() != "..") st.pop_back();
+      else if (!rooted) st.push_back("..");
+    } else {
+      st.push_back(e);
+    }
+    if (j == p.size()) break;
+  }
+  std::string out = rooted ? "/" : "";
+  for (size_t k = 0; k < st.size(); k++) out += (k ? "/" : "") + st[k];
+  if (out.empty()) return ".";
+  return out;
+}
+
 inline std::string trim_space(const std::string& s) {
   size_t b = 0, e = s.size();
   while (b < e) {

@@ -412,4 +412,12 @@ char* oracle_validate_entry(const char* entry, const char* resource_json, const 
   }
   return dup(oj::dump(o));
 }
+
+char* oracle_anchor_probe(const char* op, const char* a, const char* b) {
+  try {
+    return dup(anchor_probe(op, a, b));
+  } catch (std::exception& e) {
+    return dup(std::string("{\"exception\":") + oj::dump(Value::str(e.what())) + "}");
+  }
+}
 }

@@ -38,6 +38,8 @@ def lib():
         L.oracle_validate_matrix_t.restype = ctypes.c_void_p
         L.oracle_validate_matrix_t.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                                ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_anchor_probe.restype = ctypes.c_void_p
+        L.oracle_anchor_probe.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.oracle_validate_batch.restype = ctypes.c_longlong
         L.oracle_validate_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
@@ -118,6 +120,15 @@ def rule_matches(rule, resource, ns_labels=None):
 def validate(policies, resource, ns_labels=None):
     out = json.loads(_take(lib().oracle_validate(_s(policies), _s(resource),
                                                  _s(ns_labels) if ns_labels is not None else b"")))
+    if isinstance(out, dict) and "exception" in out:
+        raise ValueError(out["exception"])
+    return out
+
+
+def anchor_probe(op, a="", b=""):
+    """anchor package helpers (pkg/engine/anchor): parse / string / is / err / has_value / keys_missing / remove_path
+    / split, for the package's unit-test tables"""
+    out = json.loads(_take(lib().oracle_anchor_probe(op.encode(), _s(a), _s(b))))
     if isinstance(out, dict) and "exception" in out:
         raise ValueError(out["exception"])
     return out

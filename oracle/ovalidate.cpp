@@ -508,14 +508,19 @@ static Ret handle(Ctx& c, const std::string& element, const VP& pattern, const s
   }
 }
 
+// anchor.GetAnchorsResourcesFromMap (anchor/utils.go:9-20): condition / existence / equality / negation keys vs the rest
+static void split_anchors(const VP& patMap, std::vector<std::string>* anchors, std::vector<std::string>* resources) {
+  for (auto& kv : patMap->o) {
+    Anchor a = parse_anchor(kv.first);
+    if (a.t == AT::Condition || a.t == AT::Existence || a.t == AT::Equality || a.t == AT::Negation) anchors->push_back(kv.first);
+    else resources->push_back(kv.first);
+  }
+}
+
 static Ret validate_map(Ctx& c, const VP& resMap, const VP& patMap, const std::string& path) {  // validate.go:118-161
   expand_in_metadata(patMap, resMap, c.fl);
   std::vector<std::string> anchors, resources;
-  for (auto& kv : patMap->o) {
-    Anchor a = parse_anchor(kv.first);
-    if (a.t == AT::Condition || a.t == AT::Existence || a.t == AT::Equality || a.t == AT::Negation) anchors.push_back(kv.first);
-    else resources.push_back(kv.first);
-  }
+  split_anchors(patMap, &anchors, &resources);
   // std::map iteration is already sorted (sort.Strings)
   for (auto& k : anchors) {
     Ret r = handle(c, k, patMap->o[k], path, resMap);
@@ -676,4 +681,90 @@ RawWalk validate_entry(const std::string& entry, const VP& res, const VP& pat0, 
 namespace orc {
 // operator.GetOperatorFromStringPattern(p) == operator.InRange (pkg/engine/operator/operator.go:35-61)
 bool is_in_range_pattern(const std::string& p) { return get_operator(p) == Op::InRange; }
+}  // namespace orc
+
+namespace orc {
+// anchor.RemoveAnchorsFromPath (anchor/utils.go:23-40): split on "/", drop a leading empty part, replace every
+// part that parses as an anchor by its key, path.Join (which Cleans), re-root when the input was absolute
+std::string remove_anchors_from_path(const std::string& str) {
+  std::vector<std::string> parts;
+  size_t st = 0;
+  for (size_t i = 0; i <= str.size(); i++)
+    if (i == str.size() || str[i] == '/') { parts.push_back(str.substr(st, i - st)); st = i + 1; }
+  if (!parts.empty() && parts[0].empty()) parts.erase(parts.begin());
+  std::string joined;
+  for (auto& p : parts) {
+    Anchor a = parse_anchor(p);
+    std::string q = a.t != AT::None ? a.key : p;
+    if (q.empty()) continue;  // path.Join ignores empty elements
+    joined += joined.empty() ? q : "/" + q;
+  }
+  std::string out = joined.empty() ? "" : gou::clean_path(joined);
+  if (!str.empty() && str[0] == '/') out = "/" + (out == "." ? std::string() : out);
+  return out;
+}
+
+static const char* at_name(AT t) {
+  switch (t) {
+    case AT::Condition: return "Condition";
+    case AT::Global: return "Global";
+    case AT::Negation: return "Negation";
+    case AT::AddIfNotPresent: return "AddIfNotPresent";
+    case AT::Equality: return "Equality";
+    case AT::Existence: return "Existence";
+    default: return "";
+  }
+}
+static AT at_from(const std::string& n) {
+  for (AT t : {AT::Condition, AT::Global, AT::Negation, AT::AddIfNotPresent, AT::Equality, AT::Existence})
+    if (n == at_name(t)) return t;
+  return AT::None;
+}
+
+// Probe of the anchor package's helpers for its unit-test tables (tests/golden/anchor.json); JSON text out.
+std::string anchor_probe(const std::string& op, const std::string& a, const std::string& b) {
+  auto q = [](const std::string& s) { return oj::dump(Value::str(s)); };
+  if (op == "parse") {
+    Anchor x = parse_anchor(a);
+    if (x.t == AT::None) return "null";
+    return std::string("{\"type\":") + q(at_name(x.t)) + ",\"key\":" + q(x.key) + "}";
+  }
+  if (op == "string") return q(anchor_string(at_from(a), b));  // anchor.New(t, key).String(): "" for an empty key
+  if (op == "is") {  // a: predicate, b: anchor type ("" = nil anchor)
+    AT t = at_from(b);
+    bool r = false;
+    if (a == "IsCondition") r = t == AT::Condition;
+    else if (a == "IsGlobal") r = t == AT::Global;
+    else if (a == "IsNegation") r = t == AT::Negation;
+    else if (a == "IsAddIfNotPresent") r = t == AT::AddIfNotPresent;
+    else if (a == "IsEquality") r = t == AT::Equality;
+    else if (a == "IsExistence") r = t == AT::Existence;
+    else if (a == "ContainsCondition") r = t == AT::Condition || t == AT::Global;
+    return r ? "true" : "false";
+  }
+  if (op == "err") {  // a: error kind; b: {"code": typed kind or -1, "msg": text} or null
+    VP e = oj::parse(b, true);
+    Err x = e->t == T::Null ? Err::none() : Err::make(e->o["msg"]->s, (int)e->o["code"]->f);
+    bool r = a == "negation" ? is_negation_err(x) : a == "conditional" ? is_conditional_err(x) : is_global_err(x);
+    return r ? "true" : "false";
+  }
+  if (op == "has_value") return AnchorMap::has_value_for_key(oj::parse(a, true), b) ? "true" : "false";
+  if (op == "keys_missing") {
+    AnchorMap m;
+    VP v = oj::parse(a, true);
+    for (auto& kv : v->o) m.m[kv.first] = kv.second->t == T::Bool && kv.second->b;
+    return m.keys_are_missing() ? "true" : "false";
+  }
+  if (op == "remove_path") return q(remove_anchors_from_path(a));
+  if (op == "split") {
+    std::vector<std::string> an, rs;
+    split_anchors(oj::parse(a, true), &an, &rs);
+    std::string o = "{\"anchors\":[";
+    for (size_t i = 0; i < an.size(); i++) o += (i ? "," : "") + q(an[i]);
+    o += "],\"resources\":[";
+    for (size_t i = 0; i < rs.size(); i++) o += (i ? "," : "") + q(rs[i]);
+    return o + "]}";
+  }
+  throw std::runtime_error("anchor_probe: unknown op " + op);
+}
 }  // namespace orc

@@ -56,3 +56,8 @@ RawWalk validate_entry(const std::string& entry, const oj::VP& res, const oj::VP
 namespace orc {
 bool is_in_range_pattern(const std::string& p);
 }  // namespace orc
+
+namespace orc {
+std::string remove_anchors_from_path(const std::string& str);
+std::string anchor_probe(const std::string& op, const std::string& a, const std::string& b);
+}  // namespace orc

@@ -17,6 +17,7 @@ executed or imported) and writes small JSON fixtures next to this script:
   match_units.json   pkg/utils/match/{name,annotations,labels,kind}_test.go, pkg/utils/kube/kind_test.go
   autogen.json       pkg/autogen/autogen_test.go (rule names, CanAutoGen / GetSupportedControllers, rule counts)
   policycache.json   pkg/policycache/cache_test.go (validate lookups by type / kind / namespace)
+  anchor.json        pkg/engine/anchor/*_test.go (Parse, String, predicates, error classes, path / map helpers)
   cli_apply.json     cmd/cli/kubectl-kyverno/apply/apply_command_test.go Test_Apply (report summaries of
                      `kyverno apply` over local policy / resource files, incl. test/cli/apply: foreach + JMESPath)
 
@@ -487,7 +488,8 @@ class _GoExpr:
         if s[i] == "&":
             self.i += 1
             return self.value()
-        m = re.match(r"(map\[[^\]]*\][\w.*\[\]{}]*?|\[\][\w.*\[\]{}]*?|[A-Za-z_][\w.]*)\{", s[i:])
+        m = re.match(r"(map\[[^\]]*\](?:interface\{\}|[\w.*\[\]])*|\[\](?:interface\{\}|[\w.*\[\]])*|[A-Za-z_][\w.]*)\{",
+                     s[i:])
         if m:
             self.i += m.end() - 1
             return self.composite()
@@ -606,6 +608,93 @@ def extract_autogen():
     write("autogen.json", out)
 
 
+# ---------------------------------------------------------------- anchor package unit tables
+def extract_anchor():
+    """pkg/engine/anchor/{anchor,error,utils,anchormap}_test.go: Parse, New / String / Type / Key, the Is*
+    predicates, the anchor-error classifiers, RemoveAnchorsFromPath, GetAnchorsResourcesFromMap,
+    resourceHasValueForKey and AnchorMap.KeysAreMissing, as (op, inputs, want) records"""
+    out = []
+    src = read("pkg/engine/anchor/anchor_test.go")
+    fns = dict(functions(src))
+    LQ = r'"(?:[^"\\]|\\.)*"'
+    lit = "(" + LQ + ")"
+    anc = r"(nil|anchor\{\w+, " + LQ + r"\})"
+
+    def anchor_want(want):
+        if want == "nil":
+            return None
+        t, k = re.match(r"anchor\{(\w+), (" + LQ + r")\}", want).groups()
+        return {"type": t, "key": go_unquote(k)}
+
+    for a, want in re.findall(r"args: args\{" + lit + r"\},\s*want: " + anc, fns["TestParse"]):
+        out.append({"test": "TestParse", "op": "parse", "a": go_unquote(a), "want": anchor_want(want)})
+    for t, k, want in re.findall(r"args: args\{(\w+), " + lit + r"\},\s*want: " + lit, fns["TestString"]):
+        out.append({"test": "TestString", "op": "string", "a": t, "b": go_unquote(k), "want": go_unquote(want)})
+    for t, k, want in re.findall(r"fields: fields\{(\w+), " + lit + r"\},\s*want: +" + lit, fns["Test_anchor_String"]):
+        out.append({"test": "Test_anchor_String", "op": "string", "a": t, "b": go_unquote(k), "want": go_unquote(want)})
+    for t, k, want in re.findall(r"args: args\{(\w+), " + lit + r"\},\s*want: " + anc, fns["TestNew"]):
+        out.append({"test": "TestNew", "op": "new", "a": t, "b": go_unquote(k), "want": anchor_want(want)})
+    for name in ("Test_anchor_Type", "Test_anchor_Key"):
+        for t, k, want in re.findall(r"fields: fields\{(\w+), " + lit + r"\},\s*want: +(\w+|" + LQ + r")", fns[name]):
+            w = {"type": t, "key": go_unquote(k)}
+            out.append({"test": name, "op": "new", "a": t, "b": go_unquote(k), "want": w,
+                        "field": want if name.endswith("Type") else go_unquote(want)})
+    for name, body in fns.items():
+        m = re.match(r"Test(Is\w+|ContainsCondition)$", name)
+        if not m or name == "TestIsOneOf":
+            continue
+        for arg, want in re.findall(r"args: args\{(nil|New\(\w+, " + LQ + r"\))\},\s*want: (true|false)", body):
+            t = "" if arg == "nil" else re.match(r"New\((\w+),", arg).group(1)
+            out.append({"test": name, "op": "is", "a": m.group(1), "b": t, "want": want == "true"})
+    esrc = read("pkg/engine/anchor/error_test.go")
+    prefix = {"Negation": ("negation", 2, "negation anchor matched in resource"),
+              "Conditional": ("conditional", 0, "conditional anchor mismatch"),
+              "Global": ("global", 1, "global anchor mismatch")}
+    for name, body in functions(esrc):
+        m = re.match(r"TestIs(\w+)AnchorError$", name)
+        if not m:
+            continue
+        kind = prefix[m.group(1)][0]
+        for err, want in re.findall(r"err: (nil|errors\.New\(" + LQ + r"\)|new\w+AnchorError\(" + LQ + r"\)),\s*\},\s*want: (true|false)",
+                                    body):
+            e = None
+            mm = re.match(r'errors\.New\((".*")\)', err)
+            if mm:
+                e = {"code": -1, "msg": go_unquote(mm.group(1))}
+            mm = re.match(r'new(\w+)AnchorError\((".*")\)', err)
+            if mm:
+                _, code, pre = prefix[mm.group(1)]
+                e = {"code": code, "msg": pre + ": " + go_unquote(mm.group(2))}
+            out.append({"test": name, "op": "err", "a": kind, "b": e, "want": want == "true"})
+    usrc = read("pkg/engine/anchor/utils_test.go")
+    ufns = dict(functions(usrc))
+    for a, want in re.findall(r"str: +" + lit + r",\s*want: " + lit, ufns["TestRemoveAnchorsFromPath"]):
+        out.append({"test": "TestRemoveAnchorsFromPath", "op": "remove_path", "a": go_unquote(a), "want": go_unquote(want)})
+    body = ufns["TestGetAnchorsResourcesFromMap"]
+    for case in re.split(r"\}, \{", body[body.index("}{{") + 3:body.index("for _, tt")]):
+        vals = {}
+        for fld in ("patternMap", "wantAnchors", "wantResources"):
+            i = case.index(fld + ":") + len(fld) + 1
+            vals[fld] = _GoExpr(case[i:]).value()
+        out.append({"test": "TestGetAnchorsResourcesFromMap", "op": "split", "a": vals["patternMap"],
+                    "want": {"anchors": sorted(vals["wantAnchors"]), "resources": sorted(vals["wantResources"])}})
+    body = ufns["Test_resourceHasValueForKey"]
+    for case in re.split(r"\}, \{", body[body.index("}{{") + 3:body.index("for _, tt")]):
+        i = case.index("resource:") + len("resource:")
+        g = _GoExpr(case[i:])
+        res = g.value()
+        key = go_unquote(re.search(r"key: +" + lit, case).group(1))
+        want = re.search(r"want: (true|false)", case).group(1) == "true"
+        out.append({"test": "Test_resourceHasValueForKey", "op": "has_value", "a": res, "b": key, "want": want})
+    body = dict(functions(read("pkg/engine/anchor/anchormap_test.go")))["TestAnchorMap_KeysAreMissing"]
+    for case in re.split(r"\}, \{", body[body.index("}{{") + 3:body.index("for _, tt")]):
+        i = case.index("anchorMap:") + len("anchorMap:")
+        m = _GoExpr(case[i:]).value()
+        want = re.search(r"want: (true|false)", case).group(1) == "true"
+        out.append({"test": "TestAnchorMap_KeysAreMissing", "op": "keys_missing", "a": m or {}, "want": want})
+    write("anchor.json", out)
+
+
 # ---------------------------------------------------------------- policy cache
 def extract_policycache():
     """pkg/policycache/cache_test.go: the policies of the new*Policy builders, and for every test the validate-type
@@ -715,3 +804,4 @@ if __name__ == "__main__":
     extract_match_units()
     extract_autogen()
     extract_policycache()
+    extract_anchor()
