@@ -1565,9 +1565,195 @@ bool compile_message(Cx& c, const std::string& msg, RuleMeta& rm) {
   return true;
 }
 
+// ---------------------------------------------------------------- $() references (variables/vars.go:244-346)
+// Pattern references resolve against the pattern document itself (substituteReferences runs on the raw pattern /
+// anyPattern before variables), so they are resolved here, once, at compile time. Resolved: a reference naming
+// exactly one leaf (or the single key of a one-entry map) whose value is a string, or a number / string under an
+// operator prefix. Everything the reference turns into a rule error (unresolvable path, nil, a non-string raw value)
+// and every order-dependent case (several elements on one path, a renamed key colliding) stays a CPU fallback.
+struct RefFail { std::string why; };
+Value str_value(const std::string& s) {
+  Value v;
+  v.t = T::Str;
+  v.s = s;
+  return v;
+}
+
+// end of `.[^ ]*\)` starting at q (the '.'), or npos: the last ')' before the first space after q
+size_t ref_tail(const std::string& s, size_t q) {
+  if (q >= s.size() || s[q] == '\n') return std::string::npos;
+  size_t lim = s.find(' ', q + 1);
+  if (lim == std::string::npos) lim = s.size();
+  for (size_t e = lim; e-- > q + 1;) if (s[e] == ')') return e;
+  return std::string::npos;
+}
+// RegexReferences `^\$\(.[^\ ]*\)|[^\\]\$\(.[^\ ]*\)` / RegexEscpReferences `\\\$\(.[^\ ]*\)` FindAllString
+std::vector<std::string> find_refs(const std::string& s, bool escaped) {
+  std::vector<std::string> out;
+  size_t p = 0;
+  while (p < s.size()) {
+    size_t e = std::string::npos;
+    if (escaped) {
+      if (s[p] == '\\' && s.compare(p + 1, 2, "$(") == 0) e = ref_tail(s, p + 3);
+    } else {
+      if (p == 0 && s.compare(0, 2, "$(") == 0) e = ref_tail(s, 2);
+      if (e == std::string::npos && s[p] != '\\' && s.compare(p + 1, 2, "$(") == 0) e = ref_tail(s, p + 3);
+    }
+    if (e == std::string::npos) { p++; continue; }
+    out.push_back(s.substr(p, e + 1 - p));
+    p = e + 1;
+  }
+  return out;
+}
+// path.Clean
+std::string clean_path(const std::string& p) {
+  if (p.empty()) return ".";
+  const bool rooted = p[0] == '/';
+  std::vector<std::string> st;
+  size_t i = 0;
+  while (i <= p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    std::string e = p.substr(i, j - i);
+    if (!(e.empty() || e == ".")) {
+      if (e == "..") {
+        if (!st.empty() && st.back() != "..") st.pop_back();
+        else if (!rooted) st.push_back("..");
+      } else {
+        st.push_back(e);
+      }
+    }
+    if (j == p.size()) break;
+    i = j + 1;
+  }
+  std::string out = rooted ? "/" : "";
+  for (size_t k = 0; k < st.size(); k++) out += (k ? "/" : "") + st[k];
+  return out.empty() ? "." : out;
+}
+// anchor.RemoveAnchorsFromPath (anchor/utils.go:23-40)
+std::string remove_anchors_from_path(const std::string& str) {
+  std::vector<std::string> parts;
+  size_t st = 0;
+  for (size_t i = 0; i <= str.size(); i++)
+    if (i == str.size() || str[i] == '/') { parts.push_back(str.substr(st, i - st)); st = i + 1; }
+  if (!parts.empty() && parts[0].empty()) parts.erase(parts.begin());
+  std::string joined;
+  for (auto& p : parts) {
+    Anc a = parse_anchor(p);
+    const std::string q = a.t != AT::None ? a.key : p;
+    if (!q.empty()) joined += joined.empty() ? q : "/" + q;
+  }
+  std::string out = joined.empty() ? "" : clean_path(joined);
+  if (!str.empty() && str[0] == '/') out = "/" + (out == "." ? std::string() : out);
+  return out;
+}
+// the elements getValueFromReference visits (vars.go:560-575 over jsonutils' OnlyForLeafsAndKeys): leaves at their
+// own path, map keys at their map's path; keyed by RemoveAnchorsFromPath(path)
+void ref_index(const Value& v, const std::string& path, std::map<std::string, std::vector<Value>>* idx) {
+  if (v.t == T::Obj) {
+    for (auto& kv : v.o) {
+      if (kv.first.find('/') != std::string::npos) throw RefFail{"a pattern key contains '/'"};
+      (*idx)[remove_anchors_from_path(path)].push_back(str_value(kv.first));
+      ref_index(kv.second, path + "/" + kv.first, idx);
+    }
+  } else if (v.t == T::Arr) {
+    for (size_t i = 0; i < v.a.size(); i++) ref_index(v.a[i], path + "/" + std::to_string(i), idx);
+  } else {
+    (*idx)[remove_anchors_from_path(path)].push_back(v);
+  }
+}
+// operator.GetOperatorFromStringPattern prefix length (operator.go:35-61); -1 for the range operators
+int ref_op_len(const std::string& p) {
+  if (p.size() < 2) return 0;
+  if (p.compare(0, 2, ">=") == 0 || p.compare(0, 2, "<=") == 0) return 2;
+  if (p[0] == '>' || p[0] == '<' || p[0] == '!') return 1;
+  std::string l, r;
+  if (range_split(p, "!-", l, r) || range_split(p, "-", l, r)) return -1;
+  return 0;
+}
+// substituteReferencesIfAny on one string at `path` (vars.go:286-346)
+std::string subst_refs(const std::string& in, const std::string& path, const std::map<std::string, std::vector<Value>>& idx) {
+  std::string value = in;
+  for (std::string v : find_refs(in, false)) {
+    const bool initial = v.compare(0, 2, "$(") == 0;
+    const std::string old = v;
+    if (!initial) v = v.substr(1);
+    // resolveReference (vars.go:472-502): strings.Trim(reference, "$()"), operator prefix, absolute path
+    size_t a = 0, b = v.size();
+    auto trim = [](char c) { return c == '$' || c == '(' || c == ')'; };
+    while (a < b && trim(v[a])) a++;
+    while (b > a && trim(v[b - 1])) b--;
+    std::string p = v.substr(a, b - a);
+    const int ol = ref_op_len(p);
+    if (ol < 0) throw RefFail{"range operator in a reference"};
+    const std::string op = p.substr(0, ol);
+    p = p.substr(ol);
+    if (p.empty()) throw RefFail{"empty reference (rule error)"};
+    const std::string abs = p[0] == '/' ? p : clean_path(path.empty() ? p : path + "/" + p);
+    auto it = idx.find(abs);
+    if (it == idx.end()) throw RefFail{"unresolved reference (rule error)"};
+    if (it->second.size() != 1) throw RefFail{"reference names several elements (map order)"};
+    const Value& x = it->second[0];
+    std::string val;
+    if (op.empty()) {
+      if (x.t != T::Str) throw RefFail{"reference to a non-string value (rule error)"};
+      val = x.s;
+    } else if (x.t == T::Str) {
+      val = op + x.s;
+    } else if (x.t == T::Float) {
+      val = op + pj::go_fmt_f6(x.f);  // fmt "%f" of the float64 the policy JSON decodes to
+    } else if (x.t == T::Int) {
+      val = op + std::to_string(x.i);
+    } else {
+      throw RefFail{"operator reference to a non-scalar (rule error)"};
+    }
+    const std::string repl = (initial ? std::string() : std::string(1, old[0])) + val;
+    size_t at = value.find(old);
+    if (at != std::string::npos) value.replace(at, old.size(), repl);
+  }
+  for (const std::string& v : find_refs(value, true)) {  // `\$(...)` -> `$(...)`, every occurrence
+    const std::string to = v.substr(1);
+    for (size_t at = value.find(v); at != std::string::npos; at = value.find(v, at + to.size())) value.replace(at, v.size(), to);
+  }
+  return value;
+}
+Value resolve_refs_rec(const Value& v, const std::string& path, const std::map<std::string, std::vector<Value>>& idx) {
+  if (v.t == T::Str) return str_value(subst_refs(v.s, path, idx));
+  if (v.t == T::Arr) {
+    Value out = v;
+    for (size_t i = 0; i < v.a.size(); i++) out.a[i] = resolve_refs_rec(v.a[i], path + "/" + std::to_string(i), idx);
+    return out;
+  }
+  if (v.t == T::Obj) {
+    Value out;
+    out.t = T::Obj;
+    for (auto& kv : v.o) {
+      std::string k = subst_refs(kv.first, path, idx);
+      Value val = resolve_refs_rec(kv.second, path + "/" + kv.first, idx);
+      for (auto& e : out.o) if (e.first == k) throw RefFail{"renamed key collides (map order)"};
+      if (k != kv.first) for (auto& e : v.o) if (e.first == k) throw RefFail{"renamed key collides (map order)"};
+      out.o.emplace_back(k, std::move(val));
+    }
+    return out;
+  }
+  return v;
+}
+bool has_ref_syntax(const Value& v) {
+  if (v.t == T::Str) return v.s.find("$(") != std::string::npos;
+  for (auto& e : v.a) if (has_ref_syntax(e)) return true;
+  for (auto& kv : v.o) if (kv.first.find("$(") != std::string::npos || has_ref_syntax(kv.second)) return true;
+  return false;
+}
+// the pattern / anyPattern document after substituteReferences, or RefFail
+Value resolve_references(const Value& doc) {
+  std::map<std::string, std::vector<Value>> idx;
+  ref_index(doc, "", &idx);
+  return resolve_refs_rec(doc, "", idx);
+}
+
 // ---------------------------------------------------------------- rule classification
-bool contains_vars(const Value& v) {
-  auto hit = [](const std::string& s) { return s.find("{{") != std::string::npos || s.find("$(") != std::string::npos; };
+bool contains_vars(const Value& v) {  // after reference resolution: `{{ }}` variables remain for the CPU engine
+  auto hit = [](const std::string& s) { return s.find("{{") != std::string::npos; };
   if (v.t == T::Str) return hit(v.s);
   if (v.t == T::Arr) { for (auto& e : v.a) if (contains_vars(e)) return true; return false; }
   if (v.t == T::Obj) { for (auto& kv : v.o) if (hit(kv.first) || contains_vars(kv.second)) return true; }
@@ -1648,7 +1834,23 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
           rd.match = compile_block(c, r.get("match"), true, &em);
           rd.exclude = compile_block(c, r.get("exclude"), false, &em);
           rd.empty_may_match = em;
-          std::string why = fallback_reason(r);
+          // $() references of the pattern / anyPattern, resolved against the document (substitutePatterns)
+          Value rr;
+          const Value* rp = &r;
+          std::string ref_why;
+          for (const char* f : {"pattern", "anyPattern"}) {
+            const Value* pv = val ? val->get(f) : nullptr;
+            if (!pv || !has_ref_syntax(*pv)) continue;
+            try {
+              Value resolved = resolve_references(*pv);
+              if (rp == &r) { rr = r; rp = &rr; }
+              rr.getm("validate")->set(f, std::move(resolved));
+            } catch (RefFail& e) {
+              ref_why = std::string("references: ") + e.why;
+            }
+          }
+          const Value* rval = rp->get("validate");
+          std::string why = ref_why.empty() ? fallback_reason(*rp) : ref_why;
           const std::string pkey = pm.ns.empty() ? pm.name : pm.ns + "/" + pm.name;  // cache.MetaNamespaceKeyFunc
           if (why.empty() && excepted.count({pkey, rm.name})) why = "exception";
           c.nslots = 0;
@@ -1666,9 +1868,9 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
             rm.message_vars = !compile_message(c, rm.message, rm);
           } else if (val && !nil(val->get("pattern"))) {
             rd.kind = RK_PATTERN;
-            rd.root = compile_pattern_root(c, *val->get("pattern"));
+            rd.root = compile_pattern_root(c, *rval->get("pattern"));
           } else if (val && !nil(val->get("anyPattern"))) {
-            const Value* ap = val->get("anyPattern");
+            const Value* ap = rval->get("anyPattern");
             if (ap->t != T::Arr) {
               rd.kind = RK_ERROR;
               rm.reason = "failed to deserialize anyPattern, expected type array";

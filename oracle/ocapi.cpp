@@ -8,6 +8,7 @@
 #include "oengine.h"
 #include "ojson.h"
 #include "opss.h"
+#include "orefs.h"
 #include "ovalidate.h"
 
 using namespace orc;
@@ -419,5 +420,22 @@ char* oracle_anchor_probe(const char* op, const char* a, const char* b) {
   } catch (std::exception& e) {
     return dup(std::string("{\"exception\":") + oj::dump(Value::str(e.what())) + "}");
   }
+}
+
+// $() reference helpers (orefs.cpp): op "subst" (a = document JSON) -> {"ok","nd","err","doc"}; op "abs"
+// (a = reference path, b = absolute path) -> formAbsolutePath
+char* oracle_refs(const char* op, const char* a, const char* b) {
+  auto o = Value::obj();
+  try {
+    if (std::string(op) == "abs") return dup(oj::dump(Value::str(form_absolute_path(a, b))));
+    RefResult r = substitute_references(oj::parse(a, true));
+    o->o["ok"] = Value::boolean(r.ok);
+    o->o["nd"] = Value::boolean(r.nd);
+    o->o["err"] = Value::str(r.err);
+    o->o["doc"] = r.doc;
+  } catch (std::exception& e) {
+    o->o["exception"] = Value::str(e.what());
+  }
+  return dup(oj::dump(o));
 }
 }

@@ -9,6 +9,7 @@
 //   pkg/autogen/autogen.go:70-314 + rule.go:73-319 (ComputeRules)
 //   k8s.io/apimachinery v0.26.1 labels selectors (LabelSelectorAsSelector / Requirement.Matches) — restated
 #include "oengine.h"
+#include "orefs.h"
 #include "ojmes.h"
 
 #include <algorithm>
@@ -618,6 +619,14 @@ static bool contains_vars(const VP& v) {
   return false;
 }
 
+static bool contains_braces(const VP& v) {
+  if (!v) return false;
+  if (v->t == T::Str) return v->s.find("{{") != std::string::npos;
+  for (auto& e : v->a) if (contains_braces(e)) return true;
+  for (auto& kv : v->o) if (kv.first.find("{{") != std::string::npos || contains_braces(kv.second)) return true;
+  return false;
+}
+
 // foreach entries the restatement covers: a JMESPath-subset list and deny conditions (+ per-element preconditions,
 // elementScope) over request.object / element; patterns, nested foreach and context entries are not restated
 static bool foreach_supported(const VP& val) {
@@ -730,7 +739,8 @@ std::string rule_unsupported_reason(const VP& rule) {
     VP d = val->get("deny");
     if (d->t != T::Obj || !conditions_supported(d->get("conditions"))) return "deny";
   }
-  if (contains_vars(val->get("pattern")) || contains_vars(val->get("anyPattern"))) return "variables";
+  // $() references are restated (orefs.cpp); `{{ }}` variables in patterns are not
+  if (contains_braces(val->get("pattern")) || contains_braces(val->get("anyPattern"))) return "variables";
   if (isnil(val->get("pattern")) && isnil(val->get("anyPattern")) && isnil(val->get("podSecurity")) && has_nonempty(val, "foreach") &&
       !foreach_supported(val))
     return "foreach";
@@ -790,10 +800,25 @@ static RuleResult validate_rule_body(const VP& rule, const VP& resource) {
       }
       return out;
     }
-    if (!isnil(val->get("pattern"))) {  // validatePatterns single pattern (validation.go:619-641)
+    VP pattern = val->get("pattern"), any_pattern = val->get("anyPattern");
+    if (!isnil(pattern) || !isnil(any_pattern)) {  // substitutePatterns (validation.go:294-297, :760-782)
+      for (VP* doc : {&pattern, &any_pattern}) {
+        if (isnil(*doc) || !has_references(*doc)) continue;
+        RefResult rr = substitute_references(*doc);
+        out.nondeterministic |= rr.nd;
+        if (!rr.ok) {
+          out.status = "error";
+          out.message = "variable substitution failed: " + rr.err;
+          out.message_unpinned = rr.err_unpinned;
+          return out;
+        }
+        *doc = rr.doc;
+      }
+    }
+    if (!isnil(pattern)) {  // validatePatterns single pattern (validation.go:619-641)
       EvalFlags fl;
-      PatternResult pr = match_pattern(resource, val->get("pattern"), fl);
-      out.nondeterministic = fl.nondeterministic;
+      PatternResult pr = match_pattern(resource, pattern, fl);
+      out.nondeterministic |= fl.nondeterministic;
       if (pr.ok) { out.status = "pass"; out.message = "validation rule '" + out.name + "' passed."; return out; }
       if (pr.skip) { out.status = "skip"; out.message = pr.err; return out; }
       if (pr.path.empty()) { out.status = "error"; out.message = build_error_message(out.name, msg, pr.err, ""); return out; }
@@ -802,8 +827,8 @@ static RuleResult validate_rule_body(const VP& rule, const VP& resource) {
       out.message = build_error_message(out.name, msg, pr.err, pr.path);
       return out;
     }
-    if (!isnil(val->get("anyPattern"))) {  // validation.go:644-701
-      VP ap = val->get("anyPattern");
+    if (!isnil(any_pattern)) {  // validation.go:644-701
+      VP ap = any_pattern;
       if (ap->t != T::Arr) {
         out.status = "error";
         out.message = "failed to deserialize anyPattern, expected type array: json: cannot unmarshal into []interface {}";

@@ -38,6 +38,8 @@ def lib():
         L.oracle_validate_matrix_t.restype = ctypes.c_void_p
         L.oracle_validate_matrix_t.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                                ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_refs.restype = ctypes.c_void_p
+        L.oracle_refs.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.oracle_anchor_probe.restype = ctypes.c_void_p
         L.oracle_anchor_probe.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.oracle_validate_batch.restype = ctypes.c_longlong
@@ -132,6 +134,18 @@ def anchor_probe(op, a="", b=""):
     if isinstance(out, dict) and "exception" in out:
         raise ValueError(out["exception"])
     return out
+
+
+def substitute_references(doc):
+    """variables.substituteReferences on a pattern document -> {"ok", "nd", "err", "doc"}"""
+    out = json.loads(_take(lib().oracle_refs(b"subst", _s(doc), b"")))
+    if "exception" in out:
+        raise ValueError(out["exception"])
+    return out
+
+
+def form_absolute_path(ref, at):
+    return json.loads(_take(lib().oracle_refs(b"abs", ref.encode(), at.encode())))
 
 
 def validate_batch(policies, resources, ns_labels=None, threads=1):

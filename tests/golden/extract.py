@@ -18,6 +18,7 @@ executed or imported) and writes small JSON fixtures next to this script:
   autogen.json       pkg/autogen/autogen_test.go (rule names, CanAutoGen / GetSupportedControllers, rule counts)
   policycache.json   pkg/policycache/cache_test.go (validate lookups by type / kind / namespace)
   anchor.json        pkg/engine/anchor/*_test.go (Parse, String, predicates, error classes, path / map helpers)
+  references.json    $() references: validate_test.go reference walks, vars_test.go substitution / absolute paths
   cli_apply.json     cmd/cli/kubectl-kyverno/apply/apply_command_test.go Test_Apply (report summaries of
                      `kyverno apply` over local policy / resource files, incl. test/cli/apply: foreach + JMESPath)
 
@@ -695,6 +696,42 @@ def extract_anchor():
     write("anchor.json", out)
 
 
+# ---------------------------------------------------------------- $() references
+def extract_references():
+    """$() references: pkg/engine/validate/validate_test.go reference cases (pattern, resource, whether the test
+    substitutes first, expected walk path / error), pkg/engine/variables/vars_test.go Test_*ReferenceSubstitution
+    (document -> expected document) and TestFormAbsolutePath_* (reference, absolute path -> result)"""
+    out = []
+    for fname, body in functions(read("pkg/engine/validate/validate_test.go")):
+        if "$(" not in body:
+            continue
+        raws = dict(re.findall(r"(\w+) := \[\]byte\(`(.*?)`\)", body, re.S))
+        mpath = re.search(r'assert\.Equal\(t, path, "([^"]*)"\)', body)
+        errnil = None
+        tail = body[body.index("validateResourceElement("):]
+        if re.search(r"assert\.Assert\(t, err != nil\)", tail):
+            errnil = False
+        elif re.search(r"assert\.(NilError\(t, err\)|Assert\(t, err == nil\))", tail):
+            errnil = True
+        out.append({"test": fname, "kind": "walk", "pattern": json.loads(raws["rawPattern"]),
+                    "resource": json.loads(raws["rawMap"]), "substitute": "SubstituteAll" in body,
+                    "path": mpath.group(1) if mpath else None, "err_nil": errnil})
+    vsrc = read("pkg/engine/variables/vars_test.go")
+    for fname, body in functions(vsrc):
+        if fname in ("Test_ReferenceSubstitution", "Test_EscpReferenceSubstitution"):
+            raws = dict(re.findall(r"(\w+) := \[\]byte\(`(.*?)`\)", body, re.S))
+            out.append({"test": fname, "kind": "subst", "document": json.loads(raws["jsonRaw"]),
+                        "expected": json.loads(raws["expectedJSON"])})
+        elif fname.startswith("TestFormAbsolutePath_"):
+            vals = dict(re.findall(r'(\w+) := ("(?:[^"\\]|\\.)*")', body))
+            want = vals.get("expectedString")
+            if want is None:
+                want = vals["referencePath"] if "result == referencePath" in body else vals["absolutePath"]
+            out.append({"test": fname, "kind": "abs", "ref": go_unquote(vals["referencePath"]),
+                        "at": go_unquote(vals["absolutePath"]), "want": go_unquote(want)})
+    write("references.json", out)
+
+
 # ---------------------------------------------------------------- policy cache
 def extract_policycache():
     """pkg/policycache/cache_test.go: the policies of the new*Policy builders, and for every test the validate-type
@@ -805,3 +842,4 @@ if __name__ == "__main__":
     extract_autogen()
     extract_policycache()
     extract_anchor()
+    extract_references()
