@@ -22,7 +22,8 @@ EVAL = ("kyv", "kyv_jit_walk")  # kernels of one evaluation: kyv::match_kernel, 
 
 
 def is_eval(name):
-    return name.startswith("kyv::") or name.startswith("kyv_jit")
+    n = name[5:] if name.startswith("void ") else name  # templates: "void kyv::match_kernel<true>(...)"
+    return n.startswith("kyv::") or n.startswith("kyv_jit")
 
 
 def main(tag):
