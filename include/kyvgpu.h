@@ -170,7 +170,8 @@ int64_t kyv_results_count(const kyv_results* r, int status);
  * CalculateSummary (pkg/utils/report/results.go:38-54) over a background-scan batch; returns KYV_OK */
 int kyv_results_rule_counts(const kyv_results* r, int64_t* out, size_t cap);
 double kyv_results_kernel_ms(const kyv_results* r);
-/* 1 when the runtime-compiled walk kernel evaluated this result's pattern rules, 0 for the interpreter */
+/* bit 0: the runtime-compiled walk kernels evaluated this result's pattern rules (else the interpreter); bit 1: the
+ * runtime-compiled condition kernel evaluated its deny / foreach rules with JMESPath operands */
 int kyv_results_jit(const kyv_results* r);
 /* CPU backend with KYV_EVAL_ACCOUNT_BYTES: algorithmic bytes of all pairs (header fields, distinct node rows,
  * verdict, PSS mask, failure records); 0 otherwise */

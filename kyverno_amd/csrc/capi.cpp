@@ -126,8 +126,9 @@ int64_t kyv_ruleset_jit_source(const kyv_ruleset* rs, char* buf, size_t cap, uin
   if (!rs) return fail(KYV_EINVAL, "null argument"), -1;
   try {
     std::vector<uint8_t> jr;
-    std::string src = jit_source(*rs->rs, &jr);
-    if (nrules_jit) { *nrules_jit = 0; for (auto x : jr) *nrules_jit += x ? 1 : 0; }
+    std::vector<uint8_t> jc;
+    std::string src = jit_source(*rs->rs, &jr, &jc);
+    if (nrules_jit) { *nrules_jit = 0; for (size_t k = 0; k < jr.size(); k++) *nrules_jit += (jr[k] || jc[k]) ? 1 : 0; }
     if (buf && cap) { size_t n = std::min(cap - 1, src.size()); memcpy(buf, src.data(), n); buf[n] = 0; }
     return (int64_t)src.size();
   } catch (std::exception& e) {
@@ -140,7 +141,8 @@ int kyv_ruleset_jit_compile(const kyv_ruleset* rs, double* seconds, size_t* code
   if (!rs) return fail(KYV_EINVAL, "null argument");
   try {
     std::vector<uint8_t> jr;
-    std::vector<char> code = jit_compile(jit_source(*rs->rs, &jr), seconds);
+    std::vector<uint8_t> jc;
+    std::vector<char> code = jit_compile(jit_source(*rs->rs, &jr, &jc), seconds);
     if (code_bytes) *code_bytes = code.size();
     return KYV_OK;
   } catch (std::exception& e) {

@@ -2004,6 +2004,82 @@ struct TrieBuilder {
       default: break;
     }
   }
+
+  // JMESPath-subset condition operands (kyv_layout.h OK_JMES) compiled by jit.cpp's CondGen read their static
+  // field / flatten steps from path columns: register those paths. Returns the trie positions the operand's
+  // result (or its list's elements) can have and whether the result is a list; NONE = no static position.
+  // The transitions are the ones CondGen::jgen / fgen take (a flatten inside a projection keeps non-array
+  // elements in place, which have no static position).
+  struct Pos { std::vector<uint32_t> t; bool list = false; };
+  uint32_t ch(uint32_t t, uint32_t key) { return t == NONE ? NONE : child(t, key); }
+  uint32_t st(uint32_t t) { return t == NONE ? NONE : star(t); }
+  Pos jmes(const CondOperand& o, const std::vector<uint32_t>& elem) {
+    Pos r;
+    r.t.push_back(NONE);
+    if (o.kind != OK_JMES) return r;
+    const uint32_t* p = rs.pool.data() + o.a;
+    const uint32_t root = p[0] & 0xFFu;
+    if ((p[0] & JF_PURE) || root == JR_OPERATION) return r;
+    std::vector<uint32_t> S = root == JR_OBJECT ? std::vector<uint32_t>{0u} : elem;
+    if (S.empty()) S.push_back(NONE);
+    bool list = false;
+    auto uniq = [](std::vector<uint32_t> v) {
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+      return v;
+    };
+    for (uint32_t q = 1; q < o.nseg;) {
+      const uint32_t op = p[q];
+      std::vector<uint32_t> N;
+      if (op == JO_FIELD) {
+        for (uint32_t t : S) N.push_back(ch(t, p[q + 1]));
+        q += 2;
+      } else if (op == JO_MULTI) {
+        const uint32_t m = p[q + 1];
+        for (uint32_t t : S) for (uint32_t j = 0; j < m; j++) N.push_back(ch(t, p[q + 2 + j]));
+        list = true;
+        q += 2 + m;
+      } else if (op == JO_FLAT) {
+        for (uint32_t t : S) N.push_back(st(t));
+        if (list) N.push_back(NONE);
+        list = true;
+        q++;
+      } else if (op == JO_KEYS || op == JO_KEYS_FLAT) {
+        N.push_back(NONE);
+        list = list || op == JO_KEYS;
+        q++;
+      } else {
+        break;  // JO_OR ends the program
+      }
+      S = uniq(N);
+    }
+    r.t = S;
+    r.list = list;
+    return r;
+  }
+  void prog(uint32_t pr, const std::vector<uint32_t>& elem) {
+    if (pr == NONE || pr >= rs.cprogs.size()) return;
+    const CondProg& P = rs.cprogs[pr];
+    const uint32_t nany = P.nany == NONE ? 0u : P.nany;
+    for (uint32_t i = 0; i < nany; i++) { jmes(rs.conds[P.any0 + i].key, elem); jmes(rs.conds[P.any0 + i].value, elem); }
+    for (uint32_t i = 0; i < P.nall; i++) { jmes(rs.conds[P.all0 + i].key, elem); jmes(rs.conds[P.all0 + i].value, elem); }
+  }
+  void cond_rule(const RuleDesc& rd) {
+    prog(rd.pre, {});
+    if (rd.kind == RK_DENY) prog(rd.root, {});
+    if (rd.kind != RK_FOREACH) return;
+    const uint32_t nent = rs.pool[rd.root];
+    for (uint32_t e = 0; e < nent; e++) {
+      ForeachEntry fe;
+      memcpy(&fe, rs.pool.data() + rd.root + 1 + e * (sizeof(ForeachEntry) / 4), sizeof fe);
+      Pos lp = jmes(fe.list, {});
+      std::vector<uint32_t> E;
+      if (lp.list) E = lp.t;
+      else for (uint32_t t : lp.t) E.push_back(st(t));  // a single array's items
+      prog(fe.pre, E);
+      prog(fe.deny, E);
+    }
+  }
 };
 }  // namespace
 
@@ -2049,6 +2125,7 @@ void build_path_trie(Ruleset& rs) {
     else if (rd.kind == RK_ANYPATTERN)
       for (uint32_t a = 0; a < rd.nalts; a++) tb.walk(rs.pool[rd.root + a], 0, 0);
   }
+  for (auto& rd : rs.rules) tb.cond_rule(rd);
   // entries of pnodes that conflicted after their first visit assigned columns: clear the whole subtree
   // (a conflicting subtree is walked with t == NONE, which already cleared its entries' columns)
 }

@@ -428,6 +428,596 @@ struct Gen {
   }
 };
 
+// ---------------------------------------------------------------- compiled condition rules
+// Deny / foreach rules (and preconditions) whose condition programs hold JMESPath-subset operands, generated as
+// straight-line code over path columns (kyv_jcond.h). Semantics follow the interpreter: jmes_run / eval_prog
+// (kyv_cond.h) and eval_foreach (kyv_pss.h); a program shape the generator does not cover leaves the rule on the
+// interpreted kernel (match_kernel<true>).
+struct CondGen {
+  const Ruleset& rs;
+  std::ostringstream defs;  // generated functions (operands, programs, rules), in dependency order
+  std::ostringstream out;   // body of the function being generated
+  bool ok = true;
+  uint32_t uid = 0;
+  uint32_t nslots = 1;      // LDS lists per lane the generated programs need (1 or 2)
+  std::unordered_map<uint64_t, std::string> progs;  // (program, element trie position) -> function name
+
+  explicit CondGen(const Ruleset& r) : rs(r) {}
+  static std::string u(uint32_t x) { return std::to_string(x) + "u"; }
+  std::string fresh(const char* p) { return std::string(p) + std::to_string(uid++); }
+
+  // trie lookups along a program's static path (the compiler registered them, compiler.cpp register_jmes)
+  uint32_t tchild(uint32_t t, uint32_t key) const {
+    if (t == NONE) return NONE;
+    for (auto& kv : rs.trie[t].kids) if (kv.first == key) return kv.second;
+    return NONE;
+  }
+  uint32_t tstar(uint32_t t) const { return t == NONE ? NONE : rs.trie[t].star; }
+  uint32_t tcol(uint32_t t) const { return t == NONE ? NONE : rs.trie[t].col; }
+  uint32_t tlen(uint32_t t) const { return t == NONE || rs.trie[t].star == NONE ? NONE : rs.trie[t].lencol; }
+
+  struct V {  // a value in generated code: variable names + static trie position
+    std::string i, t, a, row;
+    uint32_t tpos;
+    bool key;   // a map key (JMES_KEYBIT element)
+  };
+  // declare a fresh value
+  V decl(const std::string& i, const std::string& t, const std::string& a, const std::string& row, uint32_t tpos,
+         bool key) {
+    V x{fresh("vi"), fresh("vt"), fresh("va"), fresh("vr"), tpos, key};
+    out << "  uint32_t " << x.i << " = " << i << ", " << x.t << " = " << t << ", " << x.a << " = " << a << ", " << x.row
+        << " = " << row << ";\n";
+    return x;
+  }
+  V field(const V& x, uint32_t key) {
+    if (x.key) return decl("NONE", "T_UNK", "0u", "NONE", NONE, false);
+    const uint32_t ct = tchild(x.tpos, key), col = tcol(ct);
+    V y{fresh("vi"), fresh("vt"), fresh("va"), fresh("vr"), col == NONE ? NONE : ct, false};
+    out << "  uint32_t " << y.i << ", " << y.t << ", " << y.a << ";\n"
+        << "  jc_field(v, R, " << x.i << ", " << x.row << ", " << (col == NONE ? "NONE" : u(col)) << ", " << u(key) << ", &"
+        << y.i << ", &" << y.t << ", &" << y.a << ");\n"
+        << "  const uint32_t " << y.row << " = " << (col == NONE ? std::string("NONE") : x.row) << ";\n";
+    return y;
+  }
+  // loop over the elements of array value x (when it is one): opens `if (arr) { for (j) {` and returns the element;
+  // the caller emits the body, then close_loop()
+  V open_elems(const V& x, const std::string& notarr_then, const char* on_arr = "") {
+    const std::string cnt = fresh("cn"), aa = fresh("aa"), eb = fresh("eb"), j = fresh("j");
+    const uint32_t st = tstar(x.tpos);
+    out << "  { uint32_t " << cnt << " = 0u, " << aa << " = 0u, " << eb << " = NONE;\n"
+        << "  if (" << (x.key ? "false" : "jc_arr(v, R, " + x.i + ", " + x.t + ", " + x.a + ", " + x.row + ", " +
+                                              (tlen(x.tpos) == NONE ? std::string("NONE") : u(tlen(x.tpos))) + ", &" + cnt +
+                                              ", &" + aa + ", &" + eb + ")")
+        << ") {\n" << on_arr
+        << "  for (uint32_t " << j << " = 0; " << j << " < " << cnt << "; " << j << "++) {\n";
+    V e{fresh("vi"), fresh("vt"), fresh("va"), fresh("vr"), st, false};
+    out << "  uint32_t " << e.i << ", " << e.t << ", " << e.a << ", " << e.row << ";\n"
+        << "  jc_elem(v, R, " << aa << ", " << (st == NONE ? std::string("NONE") : eb) << ", " << j << ", "
+        << (tcol(st) == NONE ? std::string("NONE") : u(tcol(st))) << ", &" << e.i << ", &" << e.t << ", &" << e.a << ", &"
+        << e.row << ");\n";
+    pending_else.push_back(notarr_then);
+    return e;
+  }
+  std::vector<std::string> pending_else;
+  void close_loop() {
+    out << "  }\n  }";
+    std::string e = pending_else.back();
+    pending_else.pop_back();
+    if (!e.empty()) out << " else {\n" << e << "  }";
+    out << "\n  }\n";
+  }
+
+  // ---- JMESPath operand programs, materialising mode (condition operands): results into (*lst, *cur, L/*ln)
+  // gen(pos, x, list, proj): ops [pos, end) applied to value x in single (list=false) or list mode
+  const uint32_t* P = nullptr;
+  uint32_t PN = 0, PEND = 0;
+  void jend(const V& x, bool list, bool proj) {
+    if (!list) {
+      out << "  *cur = " << (x.key ? "(" + x.i + " | JMES_KEYBIT)" : x.i) << ";\n";
+      return;
+    }
+    const std::string e = x.key ? "(" + x.i + " | JMES_KEYBIT)" : x.i;
+    if (proj && !x.key) out << "  if (" << x.i << " != NONE) { if (!jc_push(L, ln, " << e << ")) return JS_FB; }\n";
+    else out << "  if (!jc_push(L, ln, " << e << ")) return JS_FB;\n";
+  }
+  void jgen(uint32_t pos, const V& x, bool list, bool proj, int guard) {
+    if (!ok || guard > 64) { ok = false; return; }
+    if (pos >= PEND) { jend(x, list, proj); return; }
+    const uint32_t op = P[pos];
+    switch (op) {
+      case JO_FIELD: {
+        out << "  {\n";
+        V y = field(x, P[pos + 1]);
+        jgen(pos + 2, y, list, proj, guard + 1);
+        out << "  }\n";
+        return;
+      }
+      case JO_MULTI: {
+        if (list) { ok = false; return; }  // the interpreter reads a stale single value here: not generated
+        const uint32_t m = P[pos + 1];
+        out << "  if (" << x.i << " == NONE) {\n";
+        jgen(pos + 2 + m, x, false, proj, guard + 1);
+        out << "  } else {\n  *lst = true;\n";
+        for (uint32_t o = 0; o < m; o++) {
+          out << "  {\n";
+          V y = field(x, P[pos + 2 + o]);
+          jgen(pos + 2 + m, y, true, proj, guard + 1);
+          out << "  }\n";
+        }
+        out << "  }\n";
+        return;
+      }
+      case JO_FLAT: {
+        if (!list) {
+          // flatten of a non-list: null single result, projection ends
+          std::ostringstream save;
+          save.swap(out);
+          V nul{"NONE", "T_UNK", "0u", "NONE", NONE, false};
+          jgen(pos + 1, nul, false, false, guard + 1);
+          std::string notarr = out.str();
+          out.swap(save);
+          V e = open_elems(x, notarr, "  *lst = true;\n");
+          jgen(pos + 1, e, true, true, guard + 1);
+          close_loop();
+          return;
+        }
+        // flatten inside a projection: nulls dropped first (when projecting), arrays spliced one level, other
+        // elements kept
+        out << "  if (" << (proj && !x.key ? x.i + " != NONE" : std::string("true")) << ") {\n";
+        std::ostringstream save;
+        save.swap(out);
+        V pass{x.i, x.t, x.a, "NONE", NONE, x.key};
+        jgen(pos + 1, pass, true, true, guard + 1);
+        std::string notarr = out.str();
+        out.swap(save);
+        V e = open_elems(x, notarr);
+        jgen(pos + 1, e, true, true, guard + 1);
+        close_loop();
+        out << "  }\n";
+        return;
+      }
+      case JO_KEYS: {
+        if (list) { ok = false; return; }
+        const std::string m = fresh("mn"), j = fresh("j");
+        out << "  if (" << (x.key ? std::string("true") : x.i + " == NONE || jc_type(R, " + x.i + ", " + x.t + ") != N_MAP")
+            << ") return JS_FB;\n"
+            << "  { const Node " << m << " = gnode(R + " << x.i << ");\n  *lst = true;\n"
+            << "  for (uint32_t " << j << " = 0; " << j << " < " << m << ".b; " << j << "++) {\n";
+        V k = decl(m + ".a + " + j, "T_UNK", "0u", "NONE", NONE, true);
+        jgen(pos + 1, k, true, proj, guard + 1);
+        out << "  }\n  }\n";
+        return;
+      }
+      case JO_KEYS_FLAT: {
+        if (!list) { jgen(pos + 1, x, false, proj, guard + 1); return; }
+        const std::string m = fresh("mn"), j = fresh("j");
+        out << "  if (" << (x.key ? std::string("true") : x.i + " == NONE || jc_type(R, " + x.i + ", " + x.t + ") != N_MAP")
+            << ") return JS_FB;\n"
+            << "  { const Node " << m << " = gnode(R + " << x.i << ");\n"
+            << "  for (uint32_t " << j << " = 0; " << j << " < " << m << ".b; " << j << "++) {\n";
+        V k = decl(m + ".a + " + j, "T_UNK", "0u", "NONE", NONE, true);
+        jgen(pos + 1, k, true, true, guard + 1);
+        out << "  }\n  }\n";
+        return;
+      }
+      default: ok = false; return;
+    }
+  }
+  // operand function: int joN(v, R, r, element value, L, &lst, &cur, &ln, &lit) -> JS_OK / JS_FB / JS_NOTFOUND
+  std::string operand_fn(const CondOperand& o, uint32_t etpos) {
+    const uint32_t* p = rs.pool.data() + o.a;
+    const uint32_t n = o.nseg, root = p[0] & 0xFFu;
+    const bool pure = (p[0] & JF_PURE) != 0;
+    const std::string name = fresh("jo");
+    const uint32_t* saveP = P;  // operand functions are generated from inside a foreach list's generation
+    const uint32_t savePEND = PEND;
+    std::ostringstream save;
+    save.swap(out);
+    out << "static __device__ int " << name
+        << "(const View& v, const Node* R, uint32_t r, uint32_t ei, uint32_t et, uint32_t ea, uint32_t erow, uint32_t* L, "
+           "bool* lst, uint32_t* cur, uint32_t* ln, uint32_t* lit) {\n"
+           "  *lst = false; *cur = NONE; *ln = 0u; *lit = NONE;\n";
+    uint32_t i = 1, orlit = NONE;
+    if (root == JR_OPERATION) {
+      // request.operation: the literal the compiler put in the program ("CREATE" in a background scan)
+      uint32_t lit = p[1];
+      if (n > 2 && p[2] == JO_OR) {
+        const Node& c = rs.cnodes[lit];
+        bool f = node_type(c) == N_NULL || node_type(c) == N_FALSE || (node_type(c) == N_STR && c.a == SID_EMPTY) ||
+                 ((node_type(c) == N_ARR || node_type(c) == N_MAP) && c.b == 0);
+        if (f) lit = p[3];
+      } else if (n > 2) {
+        ok = false;
+      }
+      out << "  *lit = " << u(lit) << ";\n  return JS_OK;\n}\n";
+    } else if (pure) {
+      // plain field chain: a key missing from a map is a NotFoundError (the fork's rule), else as j_field
+      out << "  uint32_t c = " << (root == JR_OBJECT ? "0u" : "ei") << ", f = 0u;\n";
+      for (; i + 1 < n; i += 2) {
+        if (p[i] != JO_FIELD) { ok = false; break; }
+        out << "  if (c != NONE) {\n"
+               "    const Node m = gnode(R + c);\n"
+               "    if (node_type(m) != N_MAP) c = NONE;\n"
+               "    else { const uint32_t x = wmap_find(R, m.a, m.b, " << u(p[i + 1]) << ");\n"
+               "      if (x == NONE) { *lit = f; return JS_NOTFOUND; }\n"
+               "      c = (gtk(R + x) & 0xFu) == N_NULL ? NONE : x; }\n"
+               "  }\n  f++;\n";
+      }
+      out << "  *cur = c;\n  return JS_OK;\n}\n";
+    } else {
+      V x = root == JR_OBJECT ? decl("0u", "T_UNK", "0u", "r", 0u, false) : decl("ei", "et", "ea", "erow", etpos, false);
+      PEND = n;
+      for (uint32_t q = 1; q < n;) {  // a trailing `|| lit` ends the ops
+        if (p[q] == JO_OR) { PEND = q; orlit = p[q + 1]; break; }
+        q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
+      }
+      P = p;
+      jgen(1, x, false, false, 0);
+      if (orlit != NONE)
+        out << "  if (*lst ? *ln == 0u : jc_false1(R, *cur)) { *lst = false; *cur = NONE; *lit = " << u(orlit) << "; }\n";
+      out << "  return JS_OK;\n}\n";
+    }
+    std::string fn = out.str();
+    out.swap(save);
+    defs << fn;
+    P = saveP;
+    PEND = savePEND;
+    return name;
+  }
+  // an operand that cannot fail (no NotFoundError, no list overflow / keys() error)
+  bool infallible(const CondOperand& o) const {
+    if (o.kind == OK_LIT || o.kind == OK_NIL) return true;
+    if (o.kind == OK_PATH) return false;
+    const uint32_t* p = rs.pool.data() + o.a;
+    const uint32_t root = p[0] & 0xFFu;
+    if (root == JR_OPERATION) return true;
+    if (p[0] & JF_PURE) return false;
+    for (uint32_t q = 1; q < o.nseg;) {
+      if (p[q] == JO_OR) break;
+      if (p[q] != JO_FIELD) return false;
+      q += 2;
+    }
+    return true;
+  }
+  static bool listy(const Ruleset& rs, const CondOperand& o) {
+    if (o.kind != OK_JMES) return false;
+    const uint32_t* p = rs.pool.data() + o.a;
+    for (uint32_t q = 1; q < o.nseg;) {
+      if (p[q] == JO_MULTI || p[q] == JO_FLAT || p[q] == JO_KEYS || p[q] == JO_KEYS_FLAT) return true;
+      if (p[q] == JO_OR) return false;
+      q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
+    }
+    return false;
+  }
+  // code computing CV `cv` of operand o (slot: LDS list of the lane); `check`: return the program status on a
+  // NotFoundError / fallback (fused single-condition programs)
+  void operand_cv(const CondOperand& o, uint32_t ci, int side, uint32_t etpos, const std::string& cv, const std::string& slot,
+                  bool check) {
+    const std::string C = "v.conds[" + u(ci) + "]." + (side ? "value" : "key");
+    switch (o.kind) {
+      case OK_LIT: out << "  const CV " << cv << " = jc_lit(v, " << u(o.a) << ");\n"; return;
+      case OK_PATH: {
+        const std::string m = fresh("ms");
+        out << "  CV " << cv << "; uint32_t " << m << ";\n"
+            << "  " << (check ? "if (!" : "(void)(") << "cv_operand(v, NodeTab{R}, " << C << ", &" << cv << ", &" << m << ")"
+            << (check ? ") return CP_ERROR;\n" : ");\n");
+        return;
+      }
+      case OK_JMES: {
+        const std::string f = operand_fn(o, etpos);
+        const std::string l = fresh("jl"), c = fresh("jc"), n = fresh("jn"), t = fresh("jt"), s = fresh("js");
+        out << "  bool " << l << "; uint32_t " << c << ", " << n << ", " << t << ";\n"
+            << "  const int " << s << " = " << f << "(v, R, r, ei, et, ea, erow, " << slot << ", &" << l << ", &" << c
+            << ", &" << n << ", &" << t << ");\n";
+        if (check) out << "  if (" << s << " == JS_FB) return CR_FB;\n  if (" << s << " == JS_NOTFOUND) return CP_ERROR;\n";
+        else out << "  (void)" << s << ";\n";
+        out << "  const CV " << cv << " = jc_cv(v, R, " << l << ", " << c << ", " << t << ", " << slot << ", " << n << ");\n";
+        return;
+      }
+      default: out << "  const CV " << cv << " = cv_node(Node{N_NULL, 0, 0, 0}, false);\n"; return;
+    }
+  }
+  // eval_cond of condition ci with the condition folded in as a constant: the operator is called directly and
+  // the value operand's literal flags (SV_*) are known, so only the branches this condition can take are compiled
+  static std::string opnd_init(const CondOperand& o) {
+    return "{" + std::to_string(o.kind) + ", " + std::to_string(o.sv) + ", " + std::to_string(o.nseg) + ", " + u(o.a) +
+           ", " + u(o.list) + ", " + u(o.nlist) + "}";
+  }
+  std::string cond_call(uint32_t ci, const std::string& K, const std::string& X) {
+    const Cond& c = rs.conds[ci];
+    const std::string C = "Cond{" + std::to_string(c.op) + ", {0, 0, 0}, " + u(c.leaf) + ", " + u(c.leaf_neg) + ", 0u, " +
+                          opnd_init(c.key) + ", " + opnd_init(c.value) + "}";
+    const std::string a = "v, NodeTab{R}, " + C + ", " + K + ", " + X;
+    switch (c.op) {
+      case CO_EQ: return "op_equal(v, NodeTab{R}, " + K + ", " + X + ", false)";
+      case CO_NE: return "op_equal(v, NodeTab{R}, " + K + ", " + X + ", true)";
+      case CO_IN: return "op_in(" + a + ", false)";
+      case CO_NOTIN: return "op_in(" + a + ", true)";
+      case CO_ANYIN: return "op_any_all(" + a + ", false, false)";
+      case CO_ALLIN: return "op_any_all(" + a + ", true, false)";
+      case CO_ANYNOTIN: return "op_any_all(" + a + ", false, true)";
+      case CO_ALLNOTIN: return "op_any_all(" + a + ", true, true)";
+      case CO_GT: case CO_GE: case CO_LT: case CO_LE:
+        return "op_numeric(v, " + K + ", " + X + ", " + std::to_string(c.op) + ")";
+      default: return "CR_FALSE";
+    }
+  }
+  // program function (eval_prog): int jpN(v, R, r, element value, L) -> CR_* / CP_ERROR
+  std::string prog_fn(uint32_t prog, uint32_t etpos) {
+    const uint64_t key = ((uint64_t)prog << 32) | etpos;
+    auto it = progs.find(key);
+    if (it != progs.end()) return it->second;
+    const CondProg& p = rs.cprogs[prog];
+    const uint32_t nany = p.nany == NONE ? 0u : p.nany;
+    std::vector<uint32_t> cis;
+    for (uint32_t i = 0; i < nany; i++) cis.push_back(p.any0 + i);
+    for (uint32_t i = 0; i < p.nall; i++) cis.push_back(p.all0 + i);
+    for (uint32_t ci : cis)
+      if (listy(rs, rs.conds[ci].key) && listy(rs, rs.conds[ci].value)) nslots = 2;
+    const std::string name = fresh("jp");
+    std::ostringstream save;
+    save.swap(out);  // the program body is generated into a fresh `out`; operand functions go to `defs`
+    const bool fused = cis.size() == 1;
+    auto cond_code = [&](uint32_t ci, bool check) {
+      const Cond& c = rs.conds[ci];
+      const bool two = listy(rs, c.key) && listy(rs, c.value);
+      const std::string K = fresh("k"), X = fresh("x");
+      operand_cv(c.key, ci, 0, etpos, K, "L", check);
+      operand_cv(c.value, ci, 1, etpos, X, two ? "(L + JCAP * 64)" : "L", check);
+      out << "  rc = " << cond_call(ci, K, X) << ";\n";
+    };
+    out << "  int rc = CR_TRUE;\n  (void)rc;\n";
+    if (!fused) {
+      // every reference of the document is substituted before any condition runs (vars.go:352-431)
+      for (uint32_t ci : cis) {
+        const Cond& c = rs.conds[ci];
+        for (int side = 0; side < 2; side++) {
+          const CondOperand& o = side ? c.value : c.key;
+          if (infallible(o)) continue;
+          out << "  {\n";
+          operand_cv(o, ci, side, etpos, fresh("pc"), "L", true);
+          out << "  }\n";
+        }
+      }
+    }
+    if (p.nany != NONE) {
+      out << "  { bool any = false;\n  do {\n";
+      for (uint32_t i = 0; i < nany; i++) {
+        out << "  {\n";
+        cond_code(p.any0 + i, fused);
+        out << "  if (rc == CR_FB || rc == CR_PANIC) return rc;\n  if (rc == CR_TRUE) { any = true; break; }\n  }\n";
+      }
+      out << "  } while (0);\n  if (!any) return CR_FALSE; }\n";
+    }
+    for (uint32_t i = 0; i < p.nall; i++) {
+      out << "  {\n";
+      cond_code(p.all0 + i, fused);
+      out << "  if (rc == CR_FB || rc == CR_PANIC) return rc;\n  if (rc == CR_FALSE) return CR_FALSE;\n  }\n";
+    }
+    out << "  return CR_TRUE;\n";
+    const std::string b = out.str();
+    out.swap(save);
+    defs << "static __device__ int " << name
+         << "(const View& v, const Node* R, uint32_t r, uint32_t ei, uint32_t et, uint32_t ea, uint32_t erow, uint32_t* L) {\n"
+         << "  (void)ei; (void)et; (void)ea; (void)erow;\n"
+         << b << "}\n";
+    progs[key] = name;
+    return name;
+  }
+
+  // ---- foreach (eval_foreach, kyv_pss.h; validation.go:319-421): the entry's list streamed, each element's
+  // preconditions / deny run in place. `pend`: the element just processed ended in an error (it is the rule's error
+  // only when no element follows it: "an error ends the rule only on the last element").
+  const ForeachEntry* FE = nullptr;
+  void elem_body(const V& e) {
+    out << "  do {\n";
+    if (FE->scope == 2) out << "  if (jc_type(R, " << e.i << ", " << e.t << ") != N_MAP) return ST_ERROR | ST_MARK_SCOPE;\n";
+    out << "  bool err = false;\n";
+    const std::string args = "(v, R, r, " + e.i + ", " + e.t + ", " + e.a + ", " + e.row + ", L)";
+    if (FE->pre != NONE) {
+      const std::string f = prog_fn(FE->pre, e.tpos);
+      out << "  { const int c = " << f << args << ";\n"
+          << "    if (c == CR_FB) return ST_FALLBACK;\n    if (c == CR_PANIC) return ST_PANIC;\n"
+          << "    if (c == CR_FALSE) break;\n    err = c == CP_ERROR; }\n";
+    }
+    const std::string f = prog_fn(FE->deny, e.tpos);
+    out << "  if (!err) { const int c = " << f << args << ";\n"
+        << "    if (c == CR_FB) return ST_FALLBACK;\n    if (c == CR_PANIC) return ST_PANIC;\n"
+        << "    if (c == CR_TRUE) return ST_FAIL;\n    if (c != CP_ERROR) { count++; break; } }\n"
+        << "  pend = true;\n  } while (0);\n";
+  }
+  // end of the list program: the elements
+  void fend(const V& x, bool list, bool proj) {
+    if (x.key) { ok = false; return; }
+    if (list) {
+      if (proj) {  // a projection's null results are not elements
+        out << "  if (" << x.i << " != NONE) {\n  pend = false;\n";
+        elem_body(x);
+        out << "  }\n";
+      } else {     // kept nulls are elements, skipped
+        out << "  pend = false;\n  if (" << x.i << " != NONE) {\n";
+        elem_body(x);
+        out << "  }\n";
+      }
+      return;
+    }
+    // a single result: an array's items (null items are elements, skipped) or the value itself
+    std::ostringstream save;
+    save.swap(out);
+    out << "  pend = false;\n  if (" << x.i << " != NONE && jc_type(R, " << x.i << ", " << x.t << ") != N_NULL) {\n";
+    elem_body(x);
+    out << "  }\n";
+    const std::string single = out.str();
+    out.swap(save);
+    V e = open_elems(x, single);
+    out << "  pend = false;\n  if (" << e.i << " != NONE) {\n";
+    elem_body(e);
+    out << "  }\n";
+    close_loop();
+  }
+  void fgen(uint32_t pos, const V& x, bool list, bool proj, int guard) {
+    if (!ok || guard > 64) { ok = false; return; }
+    if (pos >= PEND) { fend(x, list, proj); return; }
+    const uint32_t op = P[pos];
+    switch (op) {
+      case JO_FIELD: {
+        out << "  {\n";
+        V y = field(x, P[pos + 1]);
+        fgen(pos + 2, y, list, proj, guard + 1);
+        out << "  }\n";
+        return;
+      }
+      case JO_MULTI: {
+        if (list) { ok = false; return; }
+        const uint32_t m = P[pos + 1];
+        out << "  if (" << x.i << " == NONE) {\n";
+        fgen(pos + 2 + m, x, false, proj, guard + 1);
+        out << "  } else {\n";
+        for (uint32_t o = 0; o < m; o++) {
+          out << "  {\n";
+          V y = field(x, P[pos + 2 + o]);
+          fgen(pos + 2 + m, y, true, proj, guard + 1);
+          out << "  }\n";
+        }
+        out << "  }\n";
+        return;
+      }
+      case JO_FLAT: {
+        std::ostringstream save;
+        save.swap(out);
+        if (!list) {
+          V nul{"NONE", "T_UNK", "0u", "NONE", NONE, false};
+          fgen(pos + 1, nul, false, false, guard + 1);
+        } else {
+          V pass{x.i, x.t, x.a, "NONE", NONE, x.key};
+          fgen(pos + 1, pass, true, true, guard + 1);
+        }
+        const std::string notarr = out.str();
+        out.swap(save);
+        if (list) out << "  if (" << (proj ? x.i + " != NONE" : std::string("true")) << ") {\n";
+        V e = open_elems(x, notarr);
+        fgen(pos + 1, e, true, true, guard + 1);
+        close_loop();
+        if (list) out << "  }\n";
+        return;
+      }
+      default: ok = false; return;  // keys() / `||` lists stay on the interpreter
+    }
+  }
+  void foreach_entry(const ForeachEntry& fe) {
+    FE = &fe;
+    out << "  { uint32_t count = 0u; bool pend = false; bool skip = false; (void)skip;\n";
+    const CondOperand& o = fe.list;
+    const uint32_t* p = o.kind == OK_JMES ? rs.pool.data() + o.a : nullptr;
+    const bool chain = o.kind == OK_PATH || (p && (p[0] & JF_PURE));
+    if (chain) {
+      // plain path: a key missing from a map skips the entry ("failed to evaluate list")
+      const uint32_t root = p ? (p[0] & 0xFFu) : JR_OBJECT;
+      if (root != JR_OBJECT) { ok = false; return; }
+      const uint32_t nseg = p ? 0u : o.nseg;
+      std::vector<uint32_t> keys;
+      if (p) { for (uint32_t q = 1; q + 1 < o.nseg; q += 2) { if (p[q] != JO_FIELD) { ok = false; return; } keys.push_back(p[q + 1]); } }
+      else for (uint32_t s = 0; s < nseg; s++) keys.push_back(rs.pool[o.a + s]);
+      out << "  uint32_t lc = 0u;\n";
+      for (uint32_t key : keys)
+        out << "  if (lc != NONE) { const Node m = gnode(R + lc);\n"
+               "    if (node_type(m) != N_MAP) lc = NONE;\n"
+               "    else { const uint32_t x = wmap_find(R, m.a, m.b, " << u(key) << ");\n"
+               "      if (x == NONE) { skip = true; lc = NONE; } else lc = (gtk(R + x) & 0xFu) == N_NULL ? NONE : x; } }\n";
+      out << "  if (!skip) {\n";
+      V x = decl("lc", "T_UNK", "0u", "NONE", NONE, false);
+      fend(x, false, false);
+      out << "  }\n";
+    } else if (p) {
+      const uint32_t root = p[0] & 0xFFu;
+      if (root != JR_OBJECT) { ok = false; return; }
+      PEND = o.nseg;
+      for (uint32_t q = 1; q < o.nseg;) {
+        if (p[q] == JO_OR || p[q] == JO_KEYS || p[q] == JO_KEYS_FLAT) { ok = false; return; }
+        q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
+      }
+      P = p;
+      V x = decl("0u", "T_UNK", "0u", "r", 0u, false);
+      fgen(1, x, false, false, 0);
+    } else {
+      ok = false;
+      return;
+    }
+    out << "  if (pend) return ST_ERROR;\n  applied += count; }\n";
+  }
+
+  // the rule's match block is decided by the resource kind alone (mark_gate_exact's conditions, compiler.cpp,
+  // without the precondition clause, which only matters for the walk's direct schedule): the kernel's kind gate
+  // is the whole match
+  bool kind_only(const RuleDesc& rd) const {
+    if (rd.empty_may_match || rd.exclude.mode != MM_NONE) return false;
+    const MatchBlock& m = rd.match;
+    if (m.mode == MM_NONE || m.nfilters == 0 || (m.mode != MM_ANY && m.nfilters != 1)) return false;
+    for (uint32_t i = 0; i < m.nfilters; i++) {
+      const Filter& f = rs.filters[m.filters + i];
+      if (f.nkinds == 0 || f.name != NONE || f.nnames || f.nnss || f.nann ||
+          (f.flags & (FF_HAS_SEL | FF_HAS_NSSEL | FF_ZERO_RD | FF_USERINFO)))
+        return false;
+      for (uint32_t j = 0; j < f.nkinds; j++) {
+        const KindDesc& kd = rs.kinds[f.kinds + j];
+        if (kd.kind != NONE && kd.gv_mode != 0) return false;
+      }
+    }
+    return true;
+  }
+  // one rule: uint8_t jr<k>(v, r, L) -> the pair's status (pair_dispatch for deny / foreach rules)
+  void rule_fn(uint32_t k) {
+    const RuleDesc& rd = rs.rules[k];
+    std::ostringstream save;
+    save.swap(out);
+    if (kind_only(rd)) out << "  // match block = the kind gate (checked by the kernel)\n";
+    else out << "  { const int m = jc_match(v, r, " << u(k) << "); if (m >= 0) return (uint8_t)m; }\n";
+    out << "  const ResHeader& h = v.hdr[r];\n"
+        << "  if (h.nnodes >= (1u << COL_TYPE_SHIFT)) return ST_FALLBACK;  // no path columns for this resource\n"
+        << "  const Node* R = v.nodes + h.root;\n"
+        << "  const uint32_t ei = NONE, et = T_UNK, ea = 0u, erow = NONE;\n";
+    const std::string args = "(v, R, r, ei, et, ea, erow, L)";
+    if (rd.pre != NONE) {
+      const std::string f = prog_fn(rd.pre, NONE);
+      out << "  { const int c = " << f << args << ";\n"
+          << "    if (c == CR_FB) return ST_FALLBACK;\n    if (c == CR_PANIC) return ST_PANIC;\n"
+          << "    if (c == CP_ERROR) return ST_ERROR | ST_MARK_PRE;\n    if (c == CR_FALSE) return ST_SKIP | ST_MARK_PRE; }\n";
+    }
+    if (rd.kind == RK_DENY) {
+      const std::string f = prog_fn(rd.root, NONE);
+      out << "  { const int c = " << f << args << ";\n"
+          << "    if (c == CR_FB) return ST_FALLBACK;\n    if (c == CR_PANIC) return ST_PANIC;\n"
+          << "    if (c == CP_ERROR) return ST_ERROR;\n    return c == CR_TRUE ? ST_FAIL : ST_PASS; }\n";
+    } else if (rd.kind == RK_FOREACH) {
+      out << "  uint32_t applied = 0u;\n";
+      const uint32_t nent = rs.pool[rd.root];
+      std::vector<ForeachEntry> ents(nent);
+      for (uint32_t e = 0; e < nent; e++)
+        memcpy(&ents[e], rs.pool.data() + rd.root + 1 + e * (sizeof(ForeachEntry) / 4), sizeof(ForeachEntry));
+      for (uint32_t e = 0; e < nent && ok; e++) foreach_entry(ents[e]);
+      out << "  return applied ? ST_PASS : ST_SKIP;\n";
+    } else {
+      ok = false;
+    }
+    const std::string b = out.str();
+    out.swap(save);
+    defs << "static __device__ uint8_t jr" << k << "(const View& v, uint32_t r, uint32_t* L) {\n" << b << "}\n";
+  }
+};
+
+// rules the light match kernel cannot evaluate (kyv_engine.hip rule_needs_jmes): foreach, or a precondition / deny
+// program with a JMESPath operand
+bool prog_has_jmes(const Ruleset& rs, uint32_t prog) {
+  if (prog == NONE) return false;
+  const CondProg& p = rs.cprogs[prog];
+  const uint32_t nany = p.nany == NONE ? 0u : p.nany;
+  for (uint32_t i = 0; i < nany; i++)
+    if (rs.conds[p.any0 + i].key.kind == OK_JMES || rs.conds[p.any0 + i].value.kind == OK_JMES) return true;
+  for (uint32_t i = 0; i < p.nall; i++)
+    if (rs.conds[p.all0 + i].key.kind == OK_JMES || rs.conds[p.all0 + i].value.kind == OK_JMES) return true;
+  return false;
+}
+
 std::string self_dir() {
   Dl_info info;
   if (dladdr((void*)&self_dir, &info) && info.dli_fname) {
@@ -442,15 +1032,38 @@ std::string self_dir() {
 
 // Rules whose patterns the generator covers get a bit in `jit_rules`; the source holds their node functions,
 // a root switch and the walk kernel `kyv_jit_walk`.
-std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
+std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond) {
   Gen g(rs);
   jit_rules->assign(rs.rules.size(), 0);
+  if (jit_cond) jit_cond->assign(rs.rules.size(), 0);
   // one generated function tree per pattern: rulesets with thousands of pattern rules (C4: 10k policies) would
   // give a source too large to compile in useful time; they stay on the interpreted walk kernel
   size_t npat = 0;
   for (auto& rd : rs.rules) npat += rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN;
   const size_t cap = getenv("KYV_JIT_MAX_RULES") ? (size_t)atol(getenv("KYV_JIT_MAX_RULES")) : 1024;
   if (npat > cap) return "";
+  // compiled condition rules: deny / foreach rules with JMESPath operands (the rest of the interpreted
+  // match_kernel<true>'s rules); KYV_JIT_COND=0 leaves them all on the interpreter
+  CondGen cg(rs);
+  std::vector<uint32_t> crules;
+  const bool cond_on = !getenv("KYV_JIT_COND") || atoi(getenv("KYV_JIT_COND")) != 0;
+  for (size_t k = 0; k < rs.rules.size() && cond_on && crules.size() < cap; k++) {
+    const RuleDesc& rd = rs.rules[k];
+    if (rd.kind != RK_DENY && rd.kind != RK_FOREACH) continue;
+    if (rd.kind == RK_DENY && !prog_has_jmes(rs, rd.pre) && !prog_has_jmes(rs, rd.root)) continue;
+    const std::string mark = cg.defs.str();
+    const auto progs = cg.progs;
+    cg.ok = true;
+    cg.rule_fn((uint32_t)k);
+    if (!cg.ok) {  // roll back this rule's functions: it stays on the interpreted kernel
+      cg.defs.str("");
+      cg.defs.clear();
+      cg.defs << mark;
+      cg.progs = progs;
+      continue;
+    }
+    crules.push_back((uint32_t)k);
+  }
   std::vector<std::pair<uint32_t, std::vector<uint32_t>>> rule_roots;  // covered rule -> its pattern roots
   for (size_t k = 0; k < rs.rules.size(); k++) {
     const RuleDesc& rd = rs.rules[k];
@@ -478,8 +1091,18 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
     rule_roots.push_back({(uint32_t)k, rr});
   }
   std::ostringstream src;
-  src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n#include \"kyv_wave.h\"\nnamespace kyv {\n";
+  src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n#include \"kyv_jcond.h\"\nnamespace kyv {\n";
   src << g.out.str();
+  if (!crules.empty()) {
+    // the match part of pair_dispatch, out of line (one copy for every rule that needs more than the kind gate):
+    // -1 matched, else the pair's status
+    src << "static __device__ __attribute__((noinline)) int jc_match(const View& v, uint32_t r, uint32_t k) {\n"
+           "  uint8_t st;\n  return pair_match(v, r, v.rules[k], &st) ? -1 : (int)st;\n}\n";
+    src << cg.defs.str();
+    src << "static __device__ uint8_t jc_dispatch(const View& v, uint32_t r, uint32_t k, uint32_t* L) {\n  switch (k) {\n";
+    for (uint32_t k : crules) src << "    case " << k << "u: return jr" << k << "(v, r, L);\n";
+    src << "    default: return ST_FALLBACK;\n  }\n}\n";
+  }
   // Rules are split into groups of a few, one kernel per group (kyv_jit_walk_<g>): the compiler allocates
   // registers per group instead of for the worst pattern of the whole ruleset, and a group's code stays in
   // the instruction cache. jit_rules[k] = group + 1.
@@ -517,6 +1140,27 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules) {
   }
   src << "}  // namespace kyv\n"
          "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n";
+  if (!crules.empty()) {
+    // one lane per resource, the kernel's rules uniform across the wave (grid.y strides over them); operand lists
+    // in LDS, lane-interleaved
+    src << "extern \"C\" __global__ void __launch_bounds__(64)\n"
+           "kyv_jit_cond(const kyv::View* __restrict__ vp, kyv::DevOut o, const uint32_t* __restrict__ mrules, uint32_t nm) {\n"
+           "  __shared__ uint32_t jl[" << cg.nslots << "u * kyv::JCAP * 64u];\n"
+           "  const kyv::View& v = *vp;\n"
+           "  const uint32_t lane = threadIdx.x, r = blockIdx.x * 64u + lane;\n"
+           "  const bool active = r < v.nres;\n"
+           "  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;\n"
+           "  for (uint32_t mi = blockIdx.y; mi < nm; mi += gridDim.y) {\n"
+           "    const uint32_t k = kyv::sld32(mrules + mi);\n"
+           "    const bool gated = active && ((gate[k >> 5] >> (k & 31u)) & 1u);\n"
+           "    if (!__ballot(gated)) continue;\n"
+           "    uint8_t st = kyv::ST_NONE;\n"
+           "    if (gated) st = kyv::jc_dispatch(v, r, k, jl + lane);\n"
+           "    if (gated && st != kyv::ST_NONE) o.status[(size_t)k * v.nres + r] = st;\n"
+           "  }\n"
+           "}\n";
+    for (uint32_t k : crules) if (jit_cond) (*jit_cond)[k] = 1;
+  }
   for (size_t gi = 0; gi < ngroups; gi++)
     src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE)))\n"
            "kyv_jit_walk_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, kyv::WorkLists wl, kyv::ChunkMap cm) {\n"
@@ -553,7 +1197,7 @@ std::string cache_path(const std::string& src) {
   const char* cs = getenv("KYV_CSRC");
   std::string csrc = cs ? std::string(cs) : self_dir() + "/csrc";
   uint64_t h = fnv1a(src);
-  for (const char* hdr : {"kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_wave.h", "kyv_walk.h"})
+  for (const char* hdr : {"kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_wave.h", "kyv_walk.h", "kyv_jcond.h"})
     h = fnv1a(read_file(csrc + "/" + hdr), h);
   h = fnv1a(std::string("gfx950|O3|c++17|wpe=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4") + "|" +
                 (getenv("KYV_JIT_DEFS") ? getenv("KYV_JIT_DEFS") : "-DKYV_JIT_NOEXTRA"), h);

@@ -25,7 +25,8 @@ struct CV {
   uint8_t t;       // CType
   uint8_t res;     // 1: resource node table, 0: ruleset literal (cnodes)
   uint8_t b;       // CT_BOOL
-  uint8_t pad;
+  uint8_t pad;     // CT_ARR with vl: log2 of the element stride in vl (0 packed JList; 6 the compiled kernels'
+                   // lane-interleaved LDS lists)
   uint32_t sid;    // CT_STR: the string; else fmt.Sprint form (NONE when not in the dictionary)
   uint32_t node;   // CT_ARR / CT_MAP: node index (relative to the resource root / absolute in cnodes)
   uint32_t n;      // CT_ARR: element count
@@ -78,7 +79,7 @@ KYV_HD CV cv_node(const Node& n, bool res) {
 // element j of an array operand
 KYV_HD CV cv_elem(const View& v, NodeTab R, const CV& arr, uint32_t j) {
   if (arr.vl) {
-    const uint32_t e = arr.vl[j];
+    const uint32_t e = arr.vl[(size_t)j << arr.pad];
     if (e == NONE) return cv_node(Node{N_NULL, 0, 0, 0}, true);
     if (e & JMES_KEYBIT) {
       CV x = cv_node(Node{N_NULL, 0, 0, 0}, true);
@@ -472,18 +473,19 @@ KYV_HD int key_exists(const View& v, NodeTab R, uint32_t ks, const CV& x, const 
 
 constexpr uint32_t MAX_CKEYS = 16;
 
-// key list: element sids (fmt.Sprint, or v.(string) for In/NotIn which panics on non-strings)
-KYV_HD int key_list(const View& v, NodeTab R, const CV& k, bool strict, uint32_t* ks, uint32_t* n) {
+// key list: element sids (fmt.Sprint, or v.(string) for In/NotIn which panics on non-strings). key_list checks
+// every element in order (CR_PANIC / CR_FB on the first that fails); key_at(i) is element i's sid, recomputed
+// where it is used instead of copied into a per-lane array (which would live in scratch memory)
+KYV_HD int key_list(const View& v, NodeTab R, const CV& k, bool strict) {
   if (k.n > MAX_CKEYS) return CR_FB;
-  *n = k.n;
   for (uint32_t j = 0; j < k.n; j++) {
     CV e = cv_elem(v, R, k, j);
     if (strict && e.t != CT_STR) return CR_PANIC;
-    ks[j] = sprint_sid(e);
-    if (ks[j] == NONE) return CR_FB;
+    if (sprint_sid(e) == NONE) return CR_FB;
   }
   return CR_TRUE;
 }
+KYV_HD uint32_t key_at(const View& v, NodeTab R, const CV& k, uint32_t i) { return sprint_sid(cv_elem(v, R, k, i)); }
 
 KYV_HD int op_in(const View& v, NodeTab R, const Cond& c, const CV& k, const CV& x, bool notin) {
   if (k.t == CT_STR || k.t == CT_INT || k.t == CT_FLOAT) {
@@ -495,8 +497,8 @@ KYV_HD int op_in(const View& v, NodeTab R, const Cond& c, const CV& k, const CV&
     return (e == CR_TRUE) != notin ? CR_TRUE : CR_FALSE;
   }
   if (k.t != CT_ARR) return CR_FALSE;
-  uint32_t ks[MAX_CKEYS], n = 0;
-  int kr = key_list(v, R, k, true, ks, &n);
+  const uint32_t n = k.n;
+  int kr = key_list(v, R, k, true);
   if (kr != CR_TRUE) return kr;
   // setExistsInArray (in.go:104-143)
   auto found = [&](uint32_t s, const CV* arr, const CondOperand* lst) {
@@ -512,14 +514,14 @@ KYV_HD int op_in(const View& v, NodeTab R, const Cond& c, const CV& k, const CV&
     for (uint32_t j = 0; j < x.n; j++) if (cv_elem(v, R, x, j).t != CT_STR) return CR_FALSE;  // invalidType
     arr = &x;
   } else if (x.t == CT_STR) {
-    if (n == 1 && ks[0] == x.sid) return CR_TRUE;
+    if (n == 1 && key_at(v, R, k, 0) == x.sid) return CR_TRUE;
     if (x.res) return CR_FB;
     if (!(c.value.sv & SV_LIST)) return CR_FALSE;
   } else {
     return CR_FALSE;
   }
   bool all_in = true;
-  for (uint32_t i = 0; i < n; i++) if (!found(ks[i], arr, &c.value)) { all_in = false; break; }
+  for (uint32_t i = 0; i < n; i++) if (!found(key_at(v, R, k, i), arr, &c.value)) { all_in = false; break; }
   return (notin ? !all_in : all_in) ? CR_TRUE : CR_FALSE;
 }
 
@@ -534,27 +536,29 @@ KYV_HD int op_any_all(const View& v, NodeTab R, const Cond& c, const CV& k, cons
     return (e == CR_TRUE) != neg ? CR_TRUE : CR_FALSE;
   }
   if (k.t != CT_ARR) return CR_FALSE;
-  uint32_t ks[MAX_CKEYS], n = 0;
-  int kr = key_list(v, R, k, false, ks, &n);
+  const uint32_t n = k.n;
+  int kr = key_list(v, R, k, false);
   if (kr != CR_TRUE) return kr;
   // anySetExistsInArray / allSetExistsInArray (anyin.go:115-180, allin.go:115-180)
   uint32_t matched = 0;
   if (x.t == CT_ARR) {
-    for (uint32_t i = 0; i < n; i++)
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t ki = key_at(v, R, k, i);
       for (uint32_t j = 0; j < x.n; j++) {
         uint32_t es = sprint_sid(cv_elem(v, R, x, j));
         if (es == NONE) return CR_FB;
-        if (wild2(v, ks[i], es)) { matched++; break; }
+        if (wild2(v, ki, es)) { matched++; break; }
       }
+    }
   } else if (x.t == CT_STR) {
-    if (n == 1 && ks[0] == x.sid) return neg ? CR_FALSE : CR_TRUE;
+    if (n == 1 && key_at(v, R, k, 0) == x.sid) return neg ? CR_FALSE : CR_TRUE;
     if (x.res) return CR_FB;
     const CondOperand& o = c.value;
     if (o.sv & SV_RANGE) {
       uint32_t hits = 0;
       for (uint32_t i = 0; i < n; i++) {
         Val y;
-        y.t = N_STR; y.sid = y.wsid = y.nsid = ks[i]; y.i = 0; y.f = 0;
+        y.t = N_STR; y.sid = y.wsid = y.nsid = key_at(v, R, k, i); y.i = 0; y.f = 0;
         bool fb = false;
         bool r = leaf_match(v, v.leaves[(!all && neg) ? c.leaf_neg : c.leaf], y, &fb);
         if (fb) return CR_FB;
@@ -566,11 +570,13 @@ KYV_HD int op_any_all(const View& v, NodeTab R, const Cond& c, const CV& k, cons
     }
     if (o.sv & SV_JSON) {
       if (!(o.sv & SV_LIST)) return CR_FALSE;  // invalidType
-      for (uint32_t i = 0; i < n; i++)
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t ki = key_at(v, R, k, i);
         for (uint32_t j = 0; j < o.nlist; j++)
-          if (wild2(v, ks[i], v.pool[o.list + j])) { matched++; break; }
+          if (wild2(v, ki, v.pool[o.list + j])) { matched++; break; }
+      }
     } else {
-      for (uint32_t i = 0; i < n; i++) if (wild2(v, ks[i], x.sid)) matched++;
+      for (uint32_t i = 0; i < n; i++) if (wild2(v, key_at(v, R, k, i), x.sid)) matched++;
     }
   } else {
     return CR_FALSE;

@@ -64,6 +64,8 @@ struct DevRuleset {
   size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool, o_cnodes, o_conds, o_cprogs;
   hipModule_t jmod = nullptr;     // runtime-compiled walk kernels (jit.cpp) loaded on this device
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
+  hipFunction_t jcond = nullptr;    // kyv_jit_cond (compiled deny / foreach rules), if the ruleset has any
+  bool jloaded = false;
 };
 
 // ---------------------------------------------------------------- per-batch device memory
@@ -183,8 +185,10 @@ struct SliceSched {
   uint32_t k0 = 0, k1 = 0;
   size_t stage_tot = 0;          // staging slots (records) of the slice
   uint32_t* rbase = nullptr;     // [k1 - k0] first staging slot of each rule (slice-local)
-  uint32_t* mrules = nullptr;    // rules of the slice match_kernel evaluates (direct-walk rules excluded):
-  uint32_t nm = 0, nmj = 0;      // [0, nm) light, then [nm, nm + nmj) with JMESPath operands / foreach
+  uint32_t* mrules = nullptr;    // rules of the slice the match phase evaluates (direct-walk rules excluded):
+  uint32_t nm = 0, nmj = 0, nmc = 0;  // [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
+                                 // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
+  std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
@@ -573,14 +577,15 @@ static int ruleset_depth(const Ruleset& rs) {
 // Compile (once per ruleset) and load (once per device) the ruleset's walk kernel; false if unavailable.
 static std::mutex g_jit_mu;
 static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
-  if (!dr->jfns.empty()) return true;
+  if (dr->jloaded) return true;
   std::lock_guard<std::mutex> lk(g_jit_mu);
   if (!rs.jit_tried) {
     rs.jit_tried = true;
     try {
-      std::string src = jit_source(rs, &rs.jit_rules);
+      std::string src = jit_source(rs, &rs.jit_rules, &rs.jit_cond);
       bool any = false;
       for (auto x : rs.jit_rules) any |= x != 0;
+      for (auto x : rs.jit_cond) any |= x != 0;
       if (any) rs.jit_code = jit_compile(src, &rs.jit_compile_s);
     } catch (std::exception& e) {
       rs.jit_error = e.what();
@@ -595,6 +600,10 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   dr->jfns.resize(ng);
   for (uint32_t g = 0; g < ng; g++)
     HIP_OK(hipModuleGetFunction(&dr->jfns[g], dr->jmod, ("kyv_jit_walk_" + std::to_string(g)).c_str()));
+  bool anyc = false;
+  for (auto x : rs.jit_cond) anyc |= x != 0;
+  if (anyc) HIP_OK(hipModuleGetFunction(&dr->jcond, dr->jmod, "kyv_jit_cond"));
+  dr->jloaded = true;
   return true;
 }
 
@@ -686,6 +695,23 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       slots[cls].swap(outv);
     }
   }
+  // match-phase rule list: light rules, then the JMESPath / foreach rules the interpreted match_kernel<true> runs,
+  // then those the compiled kyv_jit_cond runs
+  {
+    std::vector<uint32_t> mr = sl.ml, cj;
+    for (uint32_t q : sl.mj) {
+      if (jit && dr->jcond && q < rs.jit_cond.size() && rs.jit_cond[q]) cj.push_back(q);
+      else mr.push_back(q);
+    }
+    sl.nm = (uint32_t)sl.ml.size();
+    sl.nmj = (uint32_t)(mr.size() - sl.ml.size());
+    sl.nmc = (uint32_t)cj.size();
+    mr.insert(mr.end(), cj.begin(), cj.end());
+    dfree(sl.mrules);
+    sl.mrules = nullptr;
+    HIP_OK(dmalloc(&sl.mrules, std::max<size_t>(1, mr.size()) * 4));
+    if (!mr.empty()) HIP_OK(hipMemcpy(sl.mrules, mr.data(), mr.size() * 4, hipMemcpyHostToDevice));
+  }
   dfree(sl.sched);
   sl.sched = nullptr;
   HIP_OK(dmalloc(&sl.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
@@ -764,14 +790,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         const bool direct = (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) && (rd.flags & RD_GATE_EXACT);
         if (!direct) (rule_needs_jmes(rs, rd) ? mj : ml).push_back(q);
       }
-      sl.nmj = (uint32_t)mj.size();
-      const size_t nlight = ml.size();
-      ml.insert(ml.end(), mj.begin(), mj.end());
+      sl.ml = ml;  // device list laid out by layout_schedule (depends on the compiled kernels)
+      sl.mj = mj;
       HIP_OK(dmalloc(&sl.rbase, rb.size() * 4));
       HIP_OK(hipMemcpy(sl.rbase, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
-      sl.nm = (uint32_t)nlight;
-      HIP_OK(dmalloc(&sl.mrules, std::max<size_t>(1, ml.size()) * 4));
-      if (!ml.empty()) HIP_OK(hipMemcpy(sl.mrules, ml.data(), ml.size() * 4, hipMemcpyHostToDevice));
       d.max_slice_rules = std::max<size_t>(d.max_slice_rules, sl.k1 - sl.k0);
       d.max_recs = std::max<size_t>(d.max_recs, std::max<size_t>(sl.stage_tot, 1));
       d.slices.push_back(std::move(sl));
@@ -836,6 +858,17 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
                            (const uint32_t*)sl.mrules + sl.nm, sl.nmj);
       HIP_OK(hipGetLastError());
+      if (sl.nmc) {
+        // compiled condition rules: grid.y strides over them (one rule per workgroup row by default: the waves of
+        // a kind-major batch that no rule gates exit after one ballot)
+        static const uint32_t gy_env = getenv("KYV_JC_Y") ? (uint32_t)std::max(1, atoi(getenv("KYV_JC_Y"))) : 0u;
+        const uint32_t gy = gy_env ? std::min(gy_env, sl.nmc) : sl.nmc;
+        const View* vp = d.view;
+        const uint32_t* mr = sl.mrules + sl.nm + sl.nmj;
+        uint32_t nmc = sl.nmc;
+        void* args[] = {(void*)&vp, (void*)&o, (void*)&mr, (void*)&nmc};
+        HIP_OK(hipModuleLaunchKernel(dr->jcond, grid.x, gy, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+      }
       if (sl.grid[0]) {
         hipLaunchKernelGGL(walk_kernel, dim3(sl.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, sl.cm[0],
                            depth);
@@ -891,7 +924,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     out->nres = (uint32_t)nres;
     out->nrules = (uint32_t)nrules;
     out->kernel_ms = total_ms / n;
-    out->jit_used = jit ? 1 : 0;
+    bool cond = false;
+    for (auto& sl : d.slices) cond |= sl.nmc != 0;
+    out->jit_used = (jit ? 1 : 0) | (jit && cond ? 2 : 0);
     out->h2d_ms = db->upload_ms;
     std::vector<unsigned long long> rc(nrules * NSTATUS);
     if (nrules) HIP_OK(hipMemcpy(rc.data(), d.counts, rc.size() * 8, hipMemcpyDeviceToHost));

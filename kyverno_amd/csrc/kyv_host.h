@@ -117,6 +117,7 @@ struct Ruleset {
   // runtime-compiled walk kernel (jit.cpp): generated once per ruleset, compiled on first use
   bool jit_tried = false;
   std::vector<uint8_t> jit_rules;   // rule k is walked by the compiled kernel
+  std::vector<uint8_t> jit_cond;    // rule k (deny / foreach with JMESPath operands) runs in the compiled kyv_jit_cond
   std::vector<char> jit_code;       // gfx950 code object
   std::string jit_error;
   double jit_compile_s = 0;
@@ -166,7 +167,7 @@ struct Results {
   std::vector<int64_t> rule_counts;  // [rule][status] (report summaries)
   double kernel_ms = 0, h2d_ms = 0, d2h_ms = 0;
   uint64_t alg_bytes = 0;           // CPU backend with KYV_EVAL_ACCOUNT_BYTES
-  int jit_used = 0;                 // pairs walked by the runtime-compiled kernel (1) or the interpreter only (0)
+  int jit_used = 0;                 // bit 0: the runtime-compiled walk kernels ran; bit 1: the compiled condition kernel ran
 };
 
 // compiler / flattener entry points
@@ -178,7 +179,7 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
                    std::string* err);
 void derive_strings(Batch& b, size_t from, int threads);
 void build_path_trie(Ruleset& rs);
-std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules);
+std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond = nullptr);
 std::vector<char> jit_compile(const std::string& src, double* seconds);
 enum JitMode { JIT_AUTO = 0, JIT_OFF = 1, JIT_ON = 2 };
 constexpr size_t JIT_AUTO_MIN_RESOURCES = 65536;  // smaller batches are not worth a compile

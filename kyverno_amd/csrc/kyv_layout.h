@@ -21,6 +21,12 @@ typedef __hip_internal::uint64_t uint64_t;
 typedef __hip_internal::int32_t int32_t;
 typedef __hip_internal::int64_t int64_t;
 typedef __hip_internal::size_t size_t;
+#ifndef INT64_MAX
+#define INT64_MAX 9223372036854775807LL
+#define INT64_MIN (-INT64_MAX - 1)
+#define INT32_MAX 2147483647
+#define INT32_MIN (-INT32_MAX - 1)
+#endif
 #endif
 
 namespace kyv {

@@ -113,7 +113,8 @@ KYV_HD SecCtx dec_container_sc(Dec& d, uint32_t c) {
   uint32_t caps = get(R, sc, KSID(CAPS));
   if (d.obj(caps)) {
     s.caps = caps;
-    for (uint32_t key : {KSID(ADD), KSID(DROP)}) {
+    const uint32_t ckeys[2] = {KSID(ADD), KSID(DROP)};
+    for (uint32_t key : ckeys) {
       uint32_t l = get(R, caps, key);
       if (d.arr(l)) for (uint32_t i = 0; i < R[l].b; i++) d.str(R[l].a + i);
     }
@@ -184,7 +185,8 @@ KYV_HD bool decode_ok_spec(Dec& d, uint32_t spec) {
         d.str(get(R, e, KSID(VALUE)));
       }
   }
-  for (uint32_t key : {KSID(CONTAINERS), KSID(INITCONTAINERS), KSID(EPHEMERALCONTAINERS)}) {
+  const uint32_t lkeys[3] = {KSID(CONTAINERS), KSID(INITCONTAINERS), KSID(EPHEMERALCONTAINERS)};
+  for (uint32_t key : lkeys) {
     uint32_t l = get(R, spec, key);
     if (d.arr(l)) for (uint32_t i = 0; i < R[l].b; i++) decode_container(d, R[l].a + i);
   }
@@ -363,7 +365,8 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
   if (capsRBad && !windows) fails |= 1u << PS_CAPS_R_1_25;
   {
     bool hn = false;
-    for (uint32_t key : {KSID(HOSTNETWORK), KSID(HOSTPID), KSID(HOSTIPC)}) {
+    const uint32_t hkeys[3] = {KSID(HOSTNETWORK), KSID(HOSTPID), KSID(HOSTIPC)};
+    for (uint32_t key : hkeys) {
       uint32_t n = get(R, spec, key);
       if (!nil(R, n) && node_type(R[n]) == N_TRUE) hn = true;
     }
@@ -554,6 +557,26 @@ KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root) {
 // Match + dispatch of one pair (validation.go:134-183, :276-317). Returns the verdict, or sets *walk for a
 // pattern / anyPattern pair whose verdict comes from the pattern walk (pair_walk).
 // kJ = false: the light instantiation (no JMESPath operands, no foreach) for rules the host classified as such
+// The match part of pair_dispatch (validation.go:134-183, matches with the OldResource retry :600-615): false with
+// *st = the pair's final status (not matched, nondeterministic, fallback), true when the rule body runs
+KYV_HD bool pair_match(const View& v, uint32_t r, const RuleDesc& rd, uint8_t* st) {
+  if (rd.match.mode == MM_NONE) { *st = ST_FALLBACK; return KYV_WHY(FBW_MATCH), false; }  // match program not compiled
+  const ResHeader& h = v.hdr[r];
+  NodeTab R{v.nodes + h.root};
+  LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
+  if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
+  bool nd = false;
+  bool m = true;  // RD_GATE_EXACT: the kind gate already decided the match
+  if (!(rd.flags & RD_GATE_EXACT)) {
+    m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
+    if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
+  }
+  if (!m) { *st = ST_NONE; return false; }
+  if (nd) { *st = ST_ND; return false; }
+  if (rd.kind == RK_FALLBACK) { *st = ST_FALLBACK; return false; }
+  return true;
+}
+
 template <bool kJ = true>
 KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k, uint32_t* pss_fails, bool* walk) {
   *pss_fails = 0;
@@ -561,20 +584,9 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
   const RuleDesc& rd = v.rules[k];
   uint8_t st = ST_NONE;
   if (!active) return st;
-  if (rd.match.mode == MM_NONE) return KYV_WHY(FBW_MATCH), ST_FALLBACK;  // match program could not be compiled
+  if (!pair_match(v, r, rd, &st)) return st;
   const ResHeader& h = v.hdr[r];
   NodeTab R{v.nodes + h.root};
-  LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
-  if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
-  bool nd = false;
-  bool m = true;  // RD_GATE_EXACT: `active` (the kind gate) already decided the match
-  if (!(rd.flags & RD_GATE_EXACT)) {
-    m = match_rule(v, rd, ResView{R, &h}, nsl, &nd);
-    if (!m && rd.empty_may_match) m = match_rule(v, rd, ResView{R, nullptr}, nsl, &nd);
-  }
-  if (!m) return ST_NONE;
-  if (nd) return ST_ND;
-  if (rd.kind == RK_FALLBACK) return ST_FALLBACK;
   uint32_t ec, es, eg;
   if (rd.pre != NONE) {  // checkPreconditions (validation.go:281-288)
     int c = eval_prog<kJ>(v, R, rd.pre, &ec, &es, &eg);

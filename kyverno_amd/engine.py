@@ -111,7 +111,9 @@ class Results:
         self.counts = {K.STATUS_NAMES[s]: L.kyv_results_count(h, s) for s in range(8)}
         self.kernel_ms = L.kyv_results_kernel_ms(h)
         self.alg_bytes = L.kyv_results_alg_bytes(h)
-        self.jit = bool(L.kyv_results_jit(h))
+        ju = L.kyv_results_jit(h)
+        self.jit = bool(ju & 1)          # runtime-compiled walk kernels ran
+        self.jit_cond = bool(ju & 2)     # runtime-compiled condition kernel (deny / foreach rules) ran
         rc = np.zeros(len(ruleset.rules) * 8, dtype=np.int64)
         if rc.size:
             K.check(L.kyv_results_rule_counts(h, rc.ctypes.data, rc.size))

@@ -127,3 +127,22 @@ def test_jmes_foreach_synthetic_gpu():
     st, res = PU.compare(jmes_policies(), docs, nsl, backend="gpu")
     assert st["nbad"] == 0, st["bad"]
     assert res.counts["fail"] > 100
+
+
+@pytest.mark.gpu
+def test_jmes_foreach_edge_cases_gpu_compiled():
+    """the runtime-compiled condition kernel (jit.cpp CondGen: path-column reads, streamed foreach lists, LDS operand
+    lists) on the same edge cases"""
+    st, res = PU.compare(jmes_policies(), edge_pods(), None, backend="gpu", jit=True)
+    assert res.jit_cond
+    assert st["nbad"] == 0, st["bad"]
+    assert st["compared"] > 100
+
+
+@pytest.mark.gpu
+def test_jmes_foreach_synthetic_gpu_compiled():
+    docs, nsl = synth.mixed(3000, seed=93, edge=True)
+    st, res = PU.compare(jmes_policies(), docs, nsl, backend="gpu", jit=True)
+    assert res.jit_cond
+    assert st["nbad"] == 0, st["bad"]
+    assert res.counts["fail"] > 100
