@@ -117,12 +117,13 @@ struct Gen {
     }
   }
   // preload of scope `root`'s columns at row expression `rowx` into array `name`
-  std::string preload(uint32_t root, const std::string& name, const std::string& rowx) {
+  // (`rd`: the column read, jself(w, ...) inside the walk, jc_col(v, ...) before the walker state exists)
+  std::string preload(uint32_t root, const std::string& name, const std::string& rowx, const char* rd = "jself(w, ") {
     scope(root);
     const auto& L = scope_of[root];
     std::ostringstream o;
     o << "uint64_t " << name << "[" << std::max<size_t>(1, L.size()) << "];";
-    for (size_t i = 0; i < L.size(); i++) o << " " << name << "[" << i << "] = jself(w, " << u(L[i]) << ", " << rowx << ");";
+    for (size_t i = 0; i < L.size(); i++) o << " " << name << "[" << i << "] = " << rd << u(L[i]) << ", " << rowx << ");";
     return o.str();
   }
 
@@ -844,7 +845,8 @@ struct CondGen {
     // a single result: an array's items (null items are elements, skipped) or the value itself
     std::ostringstream save;
     save.swap(out);
-    out << "  pend = false;\n  if (" << x.i << " != NONE && jc_type(R, " << x.i << ", " << x.t << ") != N_NULL) {\n";
+    out << "  pend = false;\n  if (" << (x.i == "NONE" ? std::string("false") : x.i + " != NONE && jc_type(R, " + x.i + ", " + x.t + ") != N_NULL")
+        << ") {\n";
     elem_body(x);
     out << "  }\n";
     const std::string single = out.str();
@@ -1115,12 +1117,15 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
       (*jit_rules)[rule_roots[i].first] = (uint8_t)(gi + 1);
       for (uint32_t r : rule_roots[i].second) roots.push_back(r);
     }
+    // the root scope's column preload is issued before the lane's walk predicate is known: it depends on the
+    // resource row only, so its loads overlap the header loads the predicate waits for (one memory round, not two)
     for (uint32_t r : roots)
       src << "static __device__ __forceinline__ void root" << r
-          << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, bool rootmap, PatOut& out) {\n"
+          << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, bool rootmap, bool walk, PatOut& out) {\n"
+             "  const uint32_t row0 = (uint32_t)(hp - v.hdr), row = row0 < v.nres ? row0 : NONE;\n"
+             "  " << g.preload(r, "pc", "row", "jc_col(v, ") << "\n"
+             "  if (!walk) return;\n"
              "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
-             "  const uint32_t row = (uint32_t)(hp - v.hdr);\n"
-             "  " << g.preload(r, "pc", "row") << "\n"
              "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
              "  jfinish(w, r, out);\n"
              "}\n";
@@ -1129,11 +1134,10 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
            "  __device__ __forceinline__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp,\n"
            "                                     const RuleDesc& rd, PatOut& out) {\n"
            "    out.status = ST_NONE; out.idx = 0; out.tmpl = NONE; out.key0 = NONE; out.key1 = NONE;\n"
-           "    if (!walk) return;\n"
-           "#ifdef KYV_EXP_JIT_EMPTY\n    out.status = ST_PASS; return;\n#endif\n"
+           "#ifdef KYV_EXP_JIT_EMPTY\n    if (walk) out.status = ST_PASS; return;\n#endif\n"
            "    switch (root) {\n";
-    for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, rootmap, out); break;\n";
-    src << "      default: out.status = ST_FALLBACK;\n"
+    for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, rootmap, walk, out); break;\n";
+    src << "      default: if (walk) out.status = ST_FALLBACK;\n"
            "    }\n"
            "  }\n"
            "};\n";

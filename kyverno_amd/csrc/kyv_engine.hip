@@ -630,10 +630,16 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
   const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)std::max(1, atoi(getenv("KYV_WIN"))) : 0xFFFFu;
   const uint32_t nw = d.wl.nwaves, gw = b.gate_words;
   std::vector<std::pair<uint32_t, std::vector<uint32_t>>> runs;  // (first wave, gate words)
+  std::vector<uint8_t> uniform(nw, 0);  // every resource of the wave has one kind class (SLOT_UNIFORM)
   for (uint32_t w = 0; w < nw; w++) {
     std::vector<uint32_t> g(gw, 0);
-    for (size_t r = (size_t)w * WAVE; r < std::min(nres, (size_t)(w + 1) * WAVE); r++)
+    const size_t r0 = (size_t)w * WAVE, r1 = std::min(nres, (size_t)(w + 1) * WAVE);
+    bool one = true;
+    for (size_t r = r0; r < r1; r++) {
+      one = one && b.hdr[r].kclass == b.hdr[r0].kclass;
       for (uint32_t i = 0; i < gw; i++) g[i] |= b.gate[(size_t)b.hdr[r].kclass * gw + i];
+    }
+    uniform[w] = one && !getenv("KYV_NO_UNIFORM");
     if (runs.empty() || runs.back().second != g) runs.push_back({w, std::move(g)});
   }
   const uint32_t ncls = 1 + (jit ? (uint32_t)dr->jfns.size() : 0u);  // 0: interpreter, 1 + g: compiled group g
@@ -650,7 +656,11 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       for (size_t i = 0; i < ks[cls].size(); i += WIN) {
         const size_t n = std::min<size_t>(WIN, ks[cls].size() - i);
         for (uint32_t w = wb; w < we; w++)
-          for (size_t t = i; t < i + n; t++) slots[cls].push_back(make_uint2(ks[cls][t], w));
+          for (size_t t = i; t < i + n; t++) {
+            const uint32_t k = ks[cls][t];
+            const bool u = uniform[w] && (rs.rules[k].flags & RD_GATE_EXACT);
+            slots[cls].push_back(make_uint2(k, w | (u ? SLOT_UNIFORM : 0u)));
+          }
       }
   }
   size_t tot = 0;
@@ -676,7 +686,7 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       size_t fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (size_t i = 0; i < T;) {
         size_t j = i;
-        while (j < T && slots[cls][j].y == slots[cls][i].y) j++;  // one wave's chunks
+        while (j < T && (slots[cls][j].y & ~SLOT_UNIFORM) == (slots[cls][i].y & ~SLOT_UNIFORM)) j++;  // one wave's chunks
         int best = -1;
         double br = 2.0;
         for (int x = 0; x < 8; x++) {
@@ -863,6 +873,8 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         // a kind-major batch that no rule gates exit after one ballot)
         static const uint32_t gy_env = getenv("KYV_JC_Y") ? (uint32_t)std::max(1, atoi(getenv("KYV_JC_Y"))) : 0u;
         const uint32_t gy = gy_env ? std::min(gy_env, sl.nmc) : sl.nmc;
+        // (the View goes by pointer: a by-value View would be copied to scratch memory, since the kernels take its
+        // address for out-of-line helpers; measured 40 % slower)
         const View* vp = d.view;
         const uint32_t* mr = sl.mrules + sl.nm + sl.nmj;
         uint32_t nmc = sl.nmc;

@@ -24,7 +24,7 @@ constexpr uint32_t PSS_RESTRICTED_SLOTS = (1u << PS_APE_1_8) | (1u << PS_APE_1_2
 
 KYV_HD uint32_t get(NodeTab R, uint32_t m, uint32_t key) {
   if (m == NONE || node_type(R[m]) != N_MAP) return NONE;
-  return map_find(R, m, key);
+  return map_find(R, m, key);  // (a linear 16-wide probe of small maps measured 1.5x slower on C2)
 }
 KYV_HD bool nil(NodeTab R, uint32_t n) { return n == NONE || node_type(R[n]) == N_NULL; }
 
@@ -554,9 +554,6 @@ KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root) {
   return applied ? ST_PASS : ST_SKIP;
 }
 
-// Match + dispatch of one pair (validation.go:134-183, :276-317). Returns the verdict, or sets *walk for a
-// pattern / anyPattern pair whose verdict comes from the pattern walk (pair_walk).
-// kJ = false: the light instantiation (no JMESPath operands, no foreach) for rules the host classified as such
 // The match part of pair_dispatch (validation.go:134-183, matches with the OldResource retry :600-615): false with
 // *st = the pair's final status (not matched, nondeterministic, fallback), true when the rule body runs
 KYV_HD bool pair_match(const View& v, uint32_t r, const RuleDesc& rd, uint8_t* st) {
@@ -577,6 +574,9 @@ KYV_HD bool pair_match(const View& v, uint32_t r, const RuleDesc& rd, uint8_t* s
   return true;
 }
 
+// Match + dispatch of one pair (validation.go:134-183, :276-317). Returns the verdict, or sets *walk for a
+// pattern / anyPattern pair whose verdict comes from the pattern walk (pair_walk).
+// kJ = false: the light instantiation (no JMESPath operands, no foreach) for rules the host classified as such
 template <bool kJ = true>
 KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k, uint32_t* pss_fails, bool* walk) {
   *pss_fails = 0;

@@ -27,7 +27,9 @@ template <class Sink, class Walker>
 KYV_HD uint8_t pair_walk(const View& v, const RuleDesc& rd, bool walk, uint32_t r, uint32_t k, const Node* R, Walker& wk,
                          Sink& sink) {
   uint8_t st = ST_NONE;
-  const ResHeader* hp = walk ? v.hdr + r : nullptr;  // address only; walkers read it for metadata expansion
+  // address only (walkers read it for metadata expansion); not predicated on `walk`, so a compiled walker's column
+  // preload (rows = hp - v.hdr) does not wait for the loads `walk` depends on
+  const ResHeader* hp = v.hdr + r;
   const uint32_t nalts = rd.kind == RK_PATTERN ? 1 : rd.nalts;  // uniform across the wave
   uint32_t nfail = 0, nskip = 0;
   for (uint32_t a = 0; a < nalts; a++) {

@@ -727,9 +727,12 @@ __device__ __forceinline__ uint32_t sld8(const uint8_t* p) {  // scalar load of 
 // waves with the same gated rule set, each run wave-major with its rules in windows of a few rules. Slots whose
 // work list is empty (no pair matched) are skipped.
 struct ChunkMap {
-  const uint2* slots;  // [total] (rule, match wave)
+  const uint2* slots;  // [total] (rule, match wave | SLOT_UNIFORM)
   uint32_t total;
 };
+// slot flag: every resource of the match wave has the same kind class, so a direct-walk (RD_GATE_EXACT) rule the
+// schedule lists for the wave gates all of its lanes: the chunk skips the per-lane kind-class -> gate-word loads
+constexpr uint32_t SLOT_UNIFORM = 1u << 31;
 
 // Grid-stride over the schedule; every wave walks ONE rule over the (up to 64) resources of one work list;
 // verdict bytes and records as in match_kernel (the status counts are one histogram pass afterwards).
@@ -738,7 +741,8 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   for (uint32_t c = blockIdx.x; c < cm.total; c += gridDim.x) {
     const uint2 kw = sld(cm.slots + c);
-    const uint32_t k = kw.x, w = kw.y;
+    const uint32_t k = kw.x, w = kw.y & ~SLOT_UNIFORM;
+    const bool uniform = (kw.y & SLOT_UNIFORM) != 0;
     const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + w;
     const RuleDesc rd = sld(v.rules + k);
     bool active;
@@ -751,13 +755,18 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
       bool gated = false;
       if (r < v.nres) {
         const ResHeader* h = v.hdr + r;
-        const uint32_t cls = gld32(&h->kclass), fl = gld32(&h->flags);
-        gated = (gld32(v.gate + (size_t)cls * v.gate_words + (k >> 5)) >> (k & 31)) & 1u;
+        const uint32_t fl = gld32(&h->flags);
+        if (uniform) {
+          gated = true;  // the host checked the wave's (single) kind class against the rule
+        } else {
+          const uint32_t cls = gld32(&h->kclass);
+          gated = (gld32(v.gate + (size_t)cls * v.gate_words + (k >> 5)) >> (k & 31)) & 1u;
+        }
         magic = gated && (fl & RF_MAGIC);  // pattern pairs on such resources go to the CPU engine (pair_dispatch)
         it = make_uint2(r | ((fl & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), gld32(&h->root));
       }
       active = gated && !magic;
-      if (!__ballot(gated)) continue;
+      if (!uniform && !__ballot(gated)) continue;
     } else {
       const uint32_t n = sld8(wl.cnt + list);
       if (!n) continue;
