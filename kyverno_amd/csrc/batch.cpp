@@ -579,6 +579,11 @@ bool split_lines(const char* p, size_t n, int T, std::vector<std::pair<size_t, s
 
 void derive_strings(Batch& b, size_t from, int threads) {
   size_t n = b.dict.strs.size();
+  std::vector<uint32_t> gidx;  // ruleset glob-mask index + 1 per (seeded) pattern string
+  if (b.rs) {
+    gidx.assign(std::min(n, b.rs->dict.strs.size()), 0);
+    for (size_t g = 0; g < b.rs->gpats.size(); g++) if (b.rs->gpats[g] < gidx.size()) gidx[b.rs->gpats[g]] = (uint32_t)g + 1;
+  }
   b.str_flags.resize(n);
   b.str_dur.resize(n);
   b.str_qty.resize(2 * n);
@@ -595,6 +600,8 @@ void derive_strings(Batch& b, size_t from, int threads) {
         bool ascii = true;
         for (unsigned char c : x) if (c >= 0x80) { ascii = false; break; }
         if (ascii) f |= SF_ASCII;
+        if (!ascii || x.find_first_of("*?") != std::string::npos) f |= SF_GLOBBY;
+        if (s < gidx.size()) f |= gidx[s] << SF_GIDX_SHIFT;
         // time.ParseDuration and resource.ParseQuantity need a sign, digit or '.' first; strconv.ParseFloat also
         // accepts inf / infinity / nan spellings -- every other string skips the parsers
         const char c0 = x.empty() ? 0 : x[0];

@@ -1919,6 +1919,7 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
     }
     build_path_trie(*rs);
     mark_gate_exact(*rs);
+    assign_glob_masks(*rs);
     return rs.release();
   } catch (std::exception& e) {
     if (err) *err = e.what();
@@ -2105,6 +2106,37 @@ void mark_gate_exact(Ruleset& rs) {
       }
     }
     if (ok) rd.flags |= RD_GATE_EXACT;
+  }
+}
+
+// Glob masks (kyv_layout.h SF_GIDX_SHIFT): the ruleset's wildcard patterns that would otherwise run a byte loop
+// per test -- pattern atoms (prefix / suffix / contains / general), metadata-expansion key globs, then every other
+// wildcard literal (match-program names / namespaces / annotations, condition values) -- up to MAX_GMASK of them
+void assign_glob_masks(Ruleset& rs) {
+  rs.gpats.clear();
+  std::vector<uint32_t> idx(rs.dict.strs.size(), 0);
+  auto add = [&](uint32_t sid) -> uint8_t {
+    if (sid == NONE || sid >= idx.size()) return 0;
+    if (!idx[sid]) {
+      if (rs.gpats.size() >= MAX_GMASK) return 0;
+      rs.gpats.push_back(sid);
+      idx[sid] = (uint32_t)rs.gpats.size();
+    }
+    return (uint8_t)idx[sid];
+  };
+  for (auto& a : rs.atoms) {
+    a.gidx = 0;
+    if (a.glob == G_PREFIX || a.glob == G_SUFFIX || a.glob == G_CONTAINS || a.glob == G_GENERAL) a.gidx = add(a.pat);
+  }
+  for (auto& m : rs.metas) {
+    for (uint32_t i = 0; i < m.nwild_l; i++) add(rs.pool[m.wild_l + 2 * i]);
+    for (uint32_t i = 0; i < m.nwild_a; i++) add(rs.pool[m.wild_a + 2 * i]);
+  }
+  for (uint32_t s = 0; s < rs.dict.strs.size(); s++) {
+    const std::string& x = rs.dict.strs[s];
+    bool globby = x.find_first_of("*?") != std::string::npos;
+    for (unsigned char ch : x) if (ch >= 0x80) globby = true;
+    if (globby) add(s);
   }
 }
 

@@ -135,7 +135,7 @@ struct Gen {
   // string mini-language's OR-of-AND atom groups unrolled in evaluation order.
   std::string atom_call(const Atom& a) {
     std::ostringstream o;
-    o << "jatom<" << (int)a.op << ", " << (int)a.flags << ", " << (int)a.glob << ">(w.v, x, " << u(a.pat) << ", "
+    o << "jatom<" << (int)a.op << ", " << (int)a.flags << ", " << (int)a.glob << ", " << (int)a.gidx << ">(w.v, x, " << u(a.pat) << ", "
       << u(a.lit) << ", " << i64(a.dur) << ", " << i64(a.qlo) << ", " << i64(a.qhi) << ", &fb)";
     return o.str();
   }
@@ -517,9 +517,10 @@ struct CondGen {
       out << "  *cur = " << (x.key ? "(" + x.i + " | JMES_KEYBIT)" : x.i) << ";\n";
       return;
     }
-    const std::string e = x.key ? "(" + x.i + " | JMES_KEYBIT)" : x.i;
-    if (proj && !x.key) out << "  if (" << x.i << " != NONE) { if (!jc_push(L, ln, " << e << ")) return JS_FB; }\n";
-    else out << "  if (!jc_push(L, ln, " << e << ")) return JS_FB;\n";
+    const std::string e = x.key ? "(" + x.i + " | JMES_KEYBIT)" : "jc_ent(" + x.i + ", " + x.t + ", " + x.a + ")";
+    if (x.key) out << "  if (!jc_push(L, ln, " << e << ")) return JS_FB;\n";
+    else if (proj) out << "  if (" << x.i << " != NONE) { if (!jc_push(L, ln, " << e << ")) return JS_FB; }\n";
+    else out << "  if (!jc_push(L, ln, " << x.i << " == NONE ? NONE : " << e << ")) return JS_FB;\n";
   }
   void jgen(uint32_t pos, const V& x, bool list, bool proj, int guard) {
     if (!ok || guard > 64) { ok = false; return; }

@@ -81,6 +81,12 @@ KYV_HD CV cv_elem(const View& v, NodeTab R, const CV& arr, uint32_t j) {
   if (arr.vl) {
     const uint32_t e = arr.vl[(size_t)j << arr.pad];
     if (e == NONE) return cv_node(Node{N_NULL, 0, 0, 0}, true);
+    if ((e & (JMES_KEYBIT | JMES_SIDBIT)) == JMES_SIDBIT) {
+      CV x = cv_node(Node{N_NULL, 0, 0, 0}, true);
+      x.t = CT_STR;
+      x.sid = e & ~JMES_SIDBIT;
+      return x;
+    }
     if (e & JMES_KEYBIT) {
       CV x = cv_node(Node{N_NULL, 0, 0, 0}, true);
       x.t = CT_STR;

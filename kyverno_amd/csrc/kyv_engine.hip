@@ -61,7 +61,8 @@ struct DevRuleset {
   int device = -1;
   uint8_t* base = nullptr;
   size_t bytes = 0;
-  size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool, o_cnodes, o_conds, o_cprogs;
+  size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool, o_cnodes, o_conds, o_cprogs,
+      o_gpats;
   hipModule_t jmod = nullptr;     // runtime-compiled walk kernels (jit.cpp) loaded on this device
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
   hipFunction_t jcond = nullptr;    // kyv_jit_cond (compiled deny / foreach rules), if the ruleset has any
@@ -233,6 +234,8 @@ struct DevBatch {
   size_t bytes = 0;
   size_t o_nodes, o_hdr, o_faux, o_soff, o_slen, o_sflags, o_sdur, o_sqty, o_sf64, o_heap, o_nsloff, o_nslkv, o_gate,
       o_colv, o_coloff, o_pe;
+  uint32_t* gmask = nullptr;   // [string][words] glob-mask bits, computed on the device once per batch
+  uint32_t gmask_words = 0;
   double upload_ms = 0;
 };
 
@@ -256,6 +259,7 @@ static DevRuleset* upload_ruleset(const Ruleset& rs, int device) {
   d->o_cnodes = p.add(rs.cnodes);
   d->o_conds = p.add(rs.conds);
   d->o_cprogs = p.add(rs.cprogs);
+  d->o_gpats = p.add(rs.gpats);
   d->bytes = p.size;
   HIP_OK(hipMalloc(&d->base, d->bytes));
   HIP_OK(p.copy_to(d->base));
@@ -314,7 +318,11 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
     v.gate = (const uint32_t*)(bbase + db->o_gate);
     v.colv = (const uint64_t*)(bbase + db->o_colv);
     v.col_off = (const uint32_t*)(bbase + db->o_coloff);
+    v.str_gmask = db->gmask;
+    v.gmask_words = db->gmask_words;
   } else {
+    v.str_gmask = nullptr;
+    v.gmask_words = 0;
     v.nodes = b.nodes.data(); v.hdr = b.hdr.data(); v.faux = b.faux.data();
     v.str_off = b.str_off.data(); v.str_len = b.str_len.data(); v.str_flags = b.str_flags.data();
     v.str_dur = b.str_dur.data(); v.str_qty = b.str_qty.data(); v.str_f64 = b.str_f64.data();
@@ -529,6 +537,20 @@ __global__ void __launch_bounds__(HIST_BLOCK) status_hist_kernel(const uint8_t* 
     uint32_t t = 0;
     for (int j = 0; j < HIST_BLOCK / WAVE; j++) t += part[j][threadIdx.x];
     if (t) atomicAdd(&counts[(size_t)blockIdx.y * NSTATUS + threadIdx.x], (unsigned long long)t);
+  }
+}
+
+// wildcard.Match(pattern g, string s) for every dictionary string (one thread each) and masked pattern
+__global__ void __launch_bounds__(256) gmask_kernel(const View* __restrict__ vp, const uint32_t* __restrict__ gpats,
+                                                    uint32_t ng, uint32_t nstr, uint32_t words, uint32_t* __restrict__ out) {
+  const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  if (s >= nstr) return;
+  const View& v = *vp;
+  for (uint32_t w = 0; w < words; w++) {
+    uint32_t bits = 0;
+    for (uint32_t g = 32 * w; g < ng && g < 32 * w + 32; g++)
+      if (glob_sid_raw(v, gpats[g], s)) bits |= 1u << (g - 32 * w);
+    out[(size_t)s * words + w] = bits;
   }
 }
 
@@ -750,6 +772,23 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   if (!mb.dev[device]) mb.dev[device] = upload_batch(b, device);
   DevRuleset* dr = (DevRuleset*)mrs.dev[device];
   DevBatch* db = (DevBatch*)mb.dev[device];
+  if (!db->gmask && !rs.gpats.empty() && !b.str_len.empty() && !getenv("KYV_NO_GMASK")) {
+    // glob masks of this batch's dictionary against the ruleset's wildcard patterns (once per batch and device,
+    // like the path columns on the host: derived per-string data, not per-evaluation work)
+    const size_t nstr = b.str_len.size();
+    db->gmask_words = (uint32_t)((rs.gpats.size() + 31) / 32);
+    HIP_OK(dmalloc(&db->gmask, nstr * db->gmask_words * 4));
+    View tv = make_view(rs, b, dr->base, dr, db->base, db);
+    View* dv = nullptr;
+    HIP_OK(dmalloc(&dv, sizeof(View)));
+    HIP_OK(hipMemcpy(dv, &tv, sizeof(View), hipMemcpyHostToDevice));
+    const uint32_t* gp = (const uint32_t*)(dr->base + dr->o_gpats);
+    hipLaunchKernelGGL(gmask_kernel, dim3((unsigned)((nstr + 255) / 256)), dim3(256), 0, 0, (const View*)dv, gp,
+                       (uint32_t)rs.gpats.size(), (uint32_t)nstr, db->gmask_words, db->gmask);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipDeviceSynchronize());
+    dfree(dv);
+  }
   View v = make_view(rs, b, dr->base, dr, db->base, db);
   size_t nres = b.hdr.size(), nrules = rs.rules.size();
   if (!db->out) {
@@ -1074,6 +1113,7 @@ void free_device_images(Ruleset& rs, Batch* b) {
         DevBatch* d = (DevBatch*)p;
         hipSetDevice(d->device);
         dfree(d->base);
+        dfree(d->gmask);
         if (d->out) { free_dev_results(*d->out, d->device); delete d->out; }
         delete d;
       }

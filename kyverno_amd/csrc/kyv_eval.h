@@ -85,6 +85,8 @@ struct View {
   const uint32_t* nsl_kv;
   const uint32_t* gate;     // [kind class][gate_words] rule bits (batch.cpp order_by_kind)
   uint32_t gate_words;
+  const uint32_t* str_gmask;  // [string][gmask_words] glob-mask bits (device only; nullptr: match bytes)
+  uint32_t gmask_words;
   const uint64_t* colv;     // path columns (kyv_layout.h): colv[col_off[c] + row]
   const uint32_t* col_off;  // (device View: pe[].col already holds col_off[col])
   // ruleset
@@ -190,11 +192,27 @@ KYV_HD bool glob(const View& v, uint8_t kind, uint32_t pat, uint32_t lit, uint32
 }
 
 // generic wildcard.Match for match-program globs (pattern sid; classification by content)
-KYV_HD bool glob_sid(const View& v, uint32_t pat, uint32_t s) {
+KYV_HD bool glob_sid_raw(const View& v, uint32_t pat, uint32_t s) {
   if (pat == s) return true;
+  // an ASCII pattern without '*' / '?' matches exactly its own runes: an interned string, so only itself (a
+  // non-ASCII subject decodes to runes no ASCII pattern rune equals)
+  if (!(v.str_flags[pat] & SF_GLOBBY)) return false;
   uint32_t pl = v.str_len[pat];
   if (pl == 0) return s == SID_EMPTY || v.str_len[s] == 0;
   return glob_runes(sbytes(v, pat), pl, sbytes(v, s), v.str_len[s]);
+}
+// glob-mask bit of (pattern index gi + 1, string s)
+KYV_HD bool gmask_bit(const View& v, uint32_t gi1, uint32_t s) {
+  const uint32_t g = gi1 - 1;
+  return (v.str_gmask[(size_t)s * v.gmask_words + g / 32] >> (g % 32)) & 1u;
+}
+KYV_HD bool glob_sid(const View& v, uint32_t pat, uint32_t s) {
+  if (pat == s) return true;
+  const uint32_t f = v.str_flags[pat];
+  if (!(f & SF_GLOBBY)) return false;
+  const uint32_t gi1 = (f >> SF_GIDX_SHIFT) & 0xFFu;
+  if (gi1 && v.str_gmask) return gmask_bit(v, gi1, s);
+  return glob_sid_raw(v, pat, s);
 }
 
 // ---------------------------------------------------------------- resource values

@@ -108,6 +108,7 @@ struct Ruleset {
     std::vector<std::pair<uint32_t, uint32_t>> kids;  // (key sid, child trie node)
   };
   std::vector<TrieNode> trie;   // trie[0] = resource root
+  std::vector<uint32_t> gpats;  // wildcard patterns with a per-string glob mask (index g: mask bit g, SF_GIDX_SHIFT)
   uint32_t ncols = 0, nrowspaces = 1;
   std::vector<uint32_t> col_rowspace;
   std::vector<uint32_t> pn_self;  // array pnode -> self column of its elements (NONE: none)
@@ -179,6 +180,7 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
                    std::string* err);
 void derive_strings(Batch& b, size_t from, int threads);
 void build_path_trie(Ruleset& rs);
+void assign_glob_masks(Ruleset& rs);
 std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond = nullptr);
 std::vector<char> jit_compile(const std::string& src, double* seconds);
 enum JitMode { JIT_AUTO = 0, JIT_OFF = 1, JIT_ON = 2 };

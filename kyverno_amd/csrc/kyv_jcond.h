@@ -97,6 +97,11 @@ __device__ __forceinline__ void jc_elem(const View& v, const Node* R, uint32_t a
   }
   if (jc_type(R, *oi, *ot) == N_NULL) { *oi = NONE; *ot = T_UNK; *oa = 0; }
 }
+// list entry of a (non-null) value: a string whose type and id came with its column entry goes in by id (the
+// operator reads it without loading the node), anything else by node index
+__device__ __forceinline__ uint32_t jc_ent(uint32_t i, uint32_t t, uint32_t a) {
+  return (t == N_STR && a < JMES_SIDBIT) ? (a | JMES_SIDBIT) : i;
+}
 // one list element into the lane's LDS list (lane-interleaved); false when the list is full
 __device__ __forceinline__ bool jc_push(uint32_t* L, uint32_t* n, uint32_t e) {
   if (*n >= JCAP) return false;

@@ -66,7 +66,14 @@ enum StrFlag : uint32_t {
   SF_INT = 1u << 8,        // strconv.ParseInt(s, 10, 64) ok (value = str_f64 when not SF_INT_BIG)
   SF_INT_BIG = 1u << 9,    // ... but |value| > 2^53 (not exact in str_f64) -> condition pairs fall back
   SF_SEMVERISH = 1u << 10, // could parse as blang/semver (digit first, two dots) -> numeric conditions fall back
+  SF_GLOBBY = 1u << 11,    // as a wildcard pattern it needs the rune matcher: holds '*' or '?', or is not ASCII
+                           // (else wildcard.Match(p, s) is p == s, i.e. an id compare)
 };
+// bits 16..23 of a ruleset wildcard pattern's str_flags: its glob-mask index + 1 (0: none). The device holds one
+// bit per (dictionary string, masked pattern): wildcard.Match(pattern, string), evaluated once per batch
+// (kyv_engine.hip gmask_kernel), so a glob test is one load instead of a byte loop over the heap
+constexpr uint32_t SF_GIDX_SHIFT = 16;
+constexpr uint32_t MAX_GMASK = 128;  // masked patterns per ruleset (4 words per string); the rest match bytes
 
 // fixed dictionary ids (seeded first in every batch)
 enum FixedSid : uint32_t { SID_EMPTY = 0, SID_ZERO = 1, SID_TRUE = 2, SID_FALSE = 3, SID_STAR = 4, SID_FIRST_FREE = 5 };
@@ -206,7 +213,7 @@ struct Atom {           // 48 bytes; range atoms reference two simple atoms (a, 
   uint8_t op;
   uint8_t flags;
   uint8_t glob;
-  uint8_t pad;
+  uint8_t gidx;         // glob-mask index + 1 of `pat` (PREFIX/SUFFIX/CONTAINS/GENERAL), 0 none
   uint32_t pat;         // sid of the (trimmed) pattern string for compareString
   uint32_t lit;         // sid of the literal part for PREFIX/SUFFIX/CONTAINS
   uint32_t sub;         // RANGE_*: index of first of two sub-atoms
@@ -313,6 +320,8 @@ enum JmesOp : uint32_t { JO_FIELD = 1,     // + key sid
                          JO_OR = 6 };      // + cnode literal: `|| <literal>` when the result is false-like
 constexpr uint32_t JMES_MAX_LIST = 32;     // virtual list capacity (longer -> CPU fallback)
 constexpr uint32_t JMES_KEYBIT = 1u << 31; // virtual list element: the key of map entry node (index & ~KEYBIT)
+constexpr uint32_t JMES_SIDBIT = 1u << 30; // virtual list element: a string value, by dictionary id (& ~SIDBIT)
+                                           // (compiled kernels: the string came with its path column entry)
 enum StrValFlag : uint8_t { SV_LIST = 1, SV_JSON = 2, SV_RANGE = 4 };  // literal string value: json []string ok,
                                                                         // json.Valid, InRange operator pattern
 struct CondOperand {     // 16 bytes

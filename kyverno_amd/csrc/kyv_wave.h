@@ -130,7 +130,9 @@ __device__ __forceinline__ bool wbytes_eq(const uint8_t* a, const uint8_t* b, ui
   for (uint32_t i = 0; i < n; i++) if (gld8(a + i) != gld8(b + i)) return false;
   return true;
 }
-__device__ __forceinline__ bool wglob(const View& v, uint8_t kind, uint32_t pat, uint32_t lit, uint32_t s) {
+__device__ __forceinline__ bool wglob(const View& v, uint8_t kind, uint32_t pat, uint32_t lit, uint32_t s,
+                                      uint32_t gi1 = 0) {
+  if (gi1 && v.str_gmask) return gmask_bit(v, gi1, s);  // precomputed per batch (prefix/suffix/contains/general)
   switch (kind) {
     case G_ANY: return true;
     case G_EMPTY: return s == SID_EMPTY;
@@ -164,7 +166,7 @@ __device__ __forceinline__ bool watom_simple(const View& v, const Atom& a, const
     }
   }
   if ((a.op == A_EQ || a.op == A_NE) && x.wsid != NONE) {
-    bool r = wglob(v, a.glob, a.pat, a.lit, x.wsid);
+    bool r = wglob(v, a.glob, a.pat, a.lit, x.wsid, a.gidx);
     return a.op == A_NE ? !r : r;
   }
   return false;
@@ -610,7 +612,7 @@ struct JW {
 };
 // one simple comparison with the atom's operator, flags and glob class as template constants (the generated
 // leaf code instantiates exactly the branches watom_simple would take for that atom)
-template <uint8_t OP, uint8_t FLAGS, uint8_t GLOB>
+template <uint8_t OP, uint8_t FLAGS, uint8_t GLOB, uint32_t GI1 = 0>
 __device__ __forceinline__ bool jatom(const View& v, const Val& x, uint32_t pat, uint32_t lit, int64_t dur, int64_t qlo,
                                       int64_t qhi, bool* fb) {
   if ((FLAGS & AF_DUR) && x.nsid != NONE && (gld32(v.str_flags + x.nsid) & SF_DUR)) {
@@ -626,7 +628,7 @@ __device__ __forceinline__ bool jatom(const View& v, const Val& x, uint32_t pat,
     }
   }
   if ((OP == A_EQ || OP == A_NE) && x.wsid != NONE) {
-    bool r = wglob(v, GLOB, pat, lit, x.wsid);
+    bool r = wglob(v, GLOB, pat, lit, x.wsid, GI1);
     return OP == A_NE ? !r : r;
   }
   return false;
