@@ -501,6 +501,20 @@ struct Flat {
     h.version = ch.local(ver);
     h.gv = g.empty() ? h.version : av;  // GroupVersion().String(): "group/version" is the apiVersion itself
     h.flags = (magicf ? RF_MAGIC : 0) | (anchorish ? RF_ANCHORISH : 0) | (node_type(root) == N_MAP ? RF_ROOT_MAP : 0);
+    if (meta == NONE || node_type(out[meta]) == N_NULL) {
+      h.flags |= RF_META_NONE;
+    } else if (node_type(out[meta]) != N_MAP) {
+      h.flags |= RF_META_NOTMAP;
+    } else {
+      auto bad = [&](uint32_t x) {  // present, not null, not a map of strings
+        if (x == NONE || node_type(out[x]) == N_NULL) return false;
+        if (node_type(out[x]) != N_MAP) return true;
+        for (uint32_t q = 0; q < out[x].b; q++) if (node_type(out[out[x].a + q]) != N_STR) return true;
+        return false;
+      };
+      if (bad(child(meta, L_LABELS))) h.flags |= RF_LAB_BAD;
+      if (bad(child(meta, L_ANN))) h.flags |= RF_ANN_BAD;
+    }
     ch.hdr.push_back(h);
     ch.nodes.insert(ch.nodes.end(), out.begin(), out.end());
   }

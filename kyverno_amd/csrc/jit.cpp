@@ -48,10 +48,12 @@ struct Gen {
   std::vector<int> slot_elen;                    // existence entry -> index of the candidates' length column
   std::vector<std::vector<uint32_t>> scope_of;   // scope-root pnode -> its column ids, in pc[] order
   std::vector<uint8_t> scoped;                   // pnode -> scope collected
+  std::vector<uint32_t> root_mbase;              // pattern-root pnode -> its rule's first metadata site
 
   explicit Gen(const Ruleset& r)
       : rs(r), emitted(r.pnodes.size(), 0), slot(r.pentries.size(), -1), slot_alen(r.pnodes.size(), -1),
-        slot_elen(r.pentries.size(), -1), scope_of(r.pnodes.size()), scoped(r.pnodes.size(), 0) {}
+        slot_elen(r.pentries.size(), -1), scope_of(r.pnodes.size()), scoped(r.pnodes.size(), 0),
+        root_mbase(r.pnodes.size(), NONE) {}
 
   int add(std::vector<uint32_t>& list, uint32_t col) {
     list.push_back(col);
@@ -346,7 +348,19 @@ struct Gen {
         out << "  if (!(w.found & " << B << ") && wmap_find(w.R, m.a, m.b, " << key << ") != NONE) w.found |= " << B << ";\n";
       }
     }
-    if (P.flags & PF_META) {
+    const MetaSite* site = (P.flags & PF_META) && root_mbase[pn] != NONE ? &rs.metas[root_mbase[pn] + P.meta] : nullptr;
+    if (site && site->nwild_l == 0 && site->nwild_a == 0) {
+      // ExpandInMetadata of the resource root without wildcard keys: only its type assertions, decided from the
+      // header flags the flattener computed (same order as expand_meta: absent/null metadata, non-object,
+      // anchor-like keys, labels / annotations that are not objects of strings)
+      out << "  { const uint32_t hf = gld32(&w.hp->flags);\n"
+             "    if (!(hf & RF_META_NONE)) {\n"
+             "      if (hf & RF_META_NOTMAP) { w.ost = ST_PANIC; return ok_ret(); }\n"
+             "      if (hf & RF_ANCHORISH) { w.ost = ST_FALLBACK; return ok_ret(); }\n";
+      if (site->has_labels) out << "      if (hf & RF_LAB_BAD) { w.ost = ST_PANIC; return ok_ret(); }\n";
+      if (site->has_ann) out << "      if (hf & RF_ANN_BAD) { w.ost = ST_PANIC; return ok_ret(); }\n";
+      out << "    } }\n";
+    } else if (P.flags & PF_META) {
       // the out-of-line call gets a copy of the key slots: taking w.keys' address would put the whole walker
       // state (JW) in scratch memory for every pattern of the kernel
       out << "  { Keys kk = w.keys; uint8_t o = expand_meta(w.v, w.v.metas[w.mbase + " << u(P.meta)
@@ -975,6 +989,7 @@ struct CondGen {
     save.swap(out);
     if (kind_only(rd)) out << "  // match block = the kind gate (checked by the kernel)\n";
     else out << "  { const int m = jc_match(v, r, " << u(k) << "); if (m >= 0) return (uint8_t)m; }\n";
+    out << "#ifdef KYV_EXP_JC_EMPTY\n  return ST_PASS;\n#endif\n";
     out << "  const ResHeader& h = v.hdr[r];\n"
         << "  if (h.nnodes >= (1u << COL_TYPE_SHIFT)) return ST_FALLBACK;  // no path columns for this resource\n"
         << "  const Node* R = v.nodes + h.root;\n"
@@ -1080,6 +1095,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     size_t mark = g.out.tellp();
     std::vector<uint8_t> em = g.emitted;
     g.ok = true;
+    for (uint32_t r : rr) g.root_mbase[r] = rd.meta_sites;
     for (uint32_t r : rr) { g.scope(r); g.scopes_below(r, 0); }
     for (uint32_t r : rr) g.node(r, 0);
     if (!g.ok) {  // roll back this rule's functions

@@ -731,9 +731,16 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
   // then those the compiled kyv_jit_cond runs
   {
     std::vector<uint32_t> mr = sl.ml, cj;
+    // KYV_JC_ONLY=k1,k2,...: timing experiments only (the compiled condition kernel runs just those rules; the
+    // other condition rules' verdicts are left unset)
+    std::vector<uint32_t> only;
+    if (const char* e = getenv("KYV_JC_ONLY")) for (const char* p = e; *p;) { only.push_back((uint32_t)strtoul(p, (char**)&p, 10)); if (*p) p++; }
     for (uint32_t q : sl.mj) {
-      if (jit && dr->jcond && q < rs.jit_cond.size() && rs.jit_cond[q]) cj.push_back(q);
-      else mr.push_back(q);
+      if (jit && dr->jcond && q < rs.jit_cond.size() && rs.jit_cond[q]) {
+        if (only.empty() || std::find(only.begin(), only.end(), q) != only.end()) cj.push_back(q);
+      } else {
+        mr.push_back(q);
+      }
     }
     sl.nm = (uint32_t)sl.ml.size();
     sl.nmj = (uint32_t)(mr.size() - sl.ml.size());

@@ -86,6 +86,12 @@ enum ResFlag : uint32_t {
   RF_EMPTY = 1u << 2,
   RF_TOO_DEEP = 1u << 3,
   RF_ROOT_MAP = 1u << 4,    // the resource document is a JSON object (walks skip the root row's type check load)
+  // metadata of the resource root as wildcards.go ExpandInMetadata type-asserts it (for expansion sites without
+  // wildcard keys the compiled walk decides from these flags instead of re-reading the maps):
+  RF_META_NONE = 1u << 5,   // metadata absent or null
+  RF_META_NOTMAP = 1u << 6, // metadata present, not an object
+  RF_LAB_BAD = 1u << 7,     // metadata.labels present, not null, and not an object of strings
+  RF_ANN_BAD = 1u << 8,     // metadata.annotations likewise
 };
 
 struct ResHeader {          // 64 bytes, one per resource (unstructured accessors, host-computed)
