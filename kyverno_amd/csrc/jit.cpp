@@ -496,6 +496,7 @@ struct CondGen {
   }
   // loop over the elements of array value x (when it is one): opens `if (arr) { for (j) {` and returns the element;
   // the caller emits the body, then close_loop()
+  bool unroll = false;  // operand programs: element loops unrolled so that the loads of consecutive elements overlap
   V open_elems(const V& x, const std::string& notarr_then, const char* on_arr = "") {
     const std::string cnt = fresh("cn"), aa = fresh("aa"), eb = fresh("eb"), j = fresh("j");
     const uint32_t st = tstar(x.tpos);
@@ -503,7 +504,7 @@ struct CondGen {
         << "  if (" << (x.key ? "false" : "jc_arr(v, R, " + x.i + ", " + x.t + ", " + x.a + ", " + x.row + ", " +
                                               (tlen(x.tpos) == NONE ? std::string("NONE") : u(tlen(x.tpos))) + ", &" + cnt +
                                               ", &" + aa + ", &" + eb + ")")
-        << ") {\n" << on_arr
+        << ") {\n" << on_arr << (unroll ? "  #pragma unroll 4\n" : "")
         << "  for (uint32_t " << j << " = 0; " << j << " < " << cnt << "; " << j << "++) {\n";
     V e{fresh("vi"), fresh("vt"), fresh("va"), fresh("vr"), st, false};
     out << "  uint32_t " << e.i << ", " << e.t << ", " << e.a << ", " << e.row << ";\n"
@@ -531,7 +532,7 @@ struct CondGen {
       out << "  *cur = " << (x.key ? "(" + x.i + " | JMES_KEYBIT)" : x.i) << ";\n";
       return;
     }
-    const std::string e = x.key ? "(" + x.i + " | JMES_KEYBIT)" : "jc_ent(" + x.i + ", " + x.t + ", " + x.a + ")";
+    const std::string e = x.key ? "jc_keyent(R, " + x.i + ")" : "jc_ent(" + x.i + ", " + x.t + ", " + x.a + ")";
     if (x.key) out << "  if (!jc_push(L, ln, " << e << ")) return JS_FB;\n";
     else if (proj) out << "  if (" << x.i << " != NONE) { if (!jc_push(L, ln, " << e << ")) return JS_FB; }\n";
     else out << "  if (!jc_push(L, ln, " << x.i << " == NONE ? NONE : " << e << ")) return JS_FB;\n";
@@ -610,6 +611,7 @@ struct CondGen {
         out << "  if (" << (x.key ? std::string("true") : x.i + " == NONE || jc_type(R, " + x.i + ", " + x.t + ") != N_MAP")
             << ") return JS_FB;\n"
             << "  { const Node " << m << " = gnode(R + " << x.i << ");\n"
+            << "  #pragma unroll 4\n"
             << "  for (uint32_t " << j << " = 0; " << j << " < " << m << ".b; " << j << "++) {\n";
         V k = decl(m + ".a + " + j, "T_UNK", "0u", "NONE", NONE, true);
         jgen(pos + 1, k, true, true, guard + 1);
@@ -668,7 +670,10 @@ struct CondGen {
         q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
       }
       P = p;
+      const bool su = unroll;
+      unroll = true;
       jgen(1, x, false, false, 0);
+      unroll = su;
       if (orlit != NONE)
         out << "  if (*lst ? *ln == 0u : jc_false1(R, *cur)) { *lst = false; *cur = NONE; *lit = " << u(orlit) << "; }\n";
       out << "  return JS_OK;\n}\n";
@@ -1165,13 +1170,19 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // one lane per resource, the kernel's rules uniform across the wave (grid.y strides over them); operand lists
     // in LDS, lane-interleaved
     src << "extern \"C\" __global__ void __launch_bounds__(64)\n"
-           "kyv_jit_cond(const kyv::View* __restrict__ vp, kyv::DevOut o, const uint32_t* __restrict__ mrules, uint32_t nm) {\n"
+           "kyv_jit_cond(const kyv::View* __restrict__ vp, kyv::DevOut o, const uint32_t* __restrict__ mrules, uint32_t nm,\n"
+           "             uint32_t xmode) {\n"
            "  __shared__ uint32_t jl[" << cg.nslots << "u * kyv::JCAP * 64u];\n"
            "  const kyv::View& v = *vp;\n"
-           "  const uint32_t lane = threadIdx.x, r = blockIdx.x * 64u + lane;\n"
+           "  // xmode 0: blockIdx.x = match wave, grid.y strides over the rules; xmode 1: XCD-interleaved (workgroup\n"
+           "  // L -> XCD L % 8; the rules of one match wave are consecutive workgroups of one XCD, so its L2 serves\n"
+           "  // the wave's rows to every rule)\n"
+           "  uint32_t wv = blockIdx.x, mi0 = blockIdx.y, mstep = gridDim.y;\n"
+           "  if (xmode == 1) { const uint32_t q = blockIdx.x >> 3; wv = (q / nm) * 8u + (blockIdx.x & 7u); mi0 = q % nm; mstep = nm; }\n"
+           "  const uint32_t lane = threadIdx.x, r = wv * 64u + lane;\n"
            "  const bool active = r < v.nres;\n"
            "  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;\n"
-           "  for (uint32_t mi = blockIdx.y; mi < nm; mi += gridDim.y) {\n"
+           "  for (uint32_t mi = mi0; mi < nm; mi += mstep) {\n"
            "    const uint32_t k = kyv::sld32(mrules + mi);\n"
            "    const bool gated = active && ((gate[k >> 5] >> (k & 31u)) & 1u);\n"
            "    if (!__ballot(gated)) continue;\n"

@@ -918,14 +918,21 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         // compiled condition rules: grid.y strides over them (one rule per workgroup row by default: the waves of
         // a kind-major batch that no rule gates exit after one ballot)
         static const uint32_t gy_env = getenv("KYV_JC_Y") ? (uint32_t)std::max(1, atoi(getenv("KYV_JC_Y"))) : 0u;
+        static const uint32_t xmode_env = getenv("KYV_JC_MODE") ? (uint32_t)atoi(getenv("KYV_JC_MODE")) : 0u;  // 1 measured 1.6x slower
         const uint32_t gy = gy_env ? std::min(gy_env, sl.nmc) : sl.nmc;
         // (the View goes by pointer: a by-value View would be copied to scratch memory, since the kernels take its
         // address for out-of-line helpers; measured 40 % slower)
         const View* vp = d.view;
         const uint32_t* mr = sl.mrules + sl.nm + sl.nmj;
-        uint32_t nmc = sl.nmc;
-        void* args[] = {(void*)&vp, (void*)&o, (void*)&mr, (void*)&nmc};
-        HIP_OK(hipModuleLaunchKernel(dr->jcond, grid.x, gy, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        uint32_t nmc = sl.nmc, xmode = xmode_env;
+        void* args[] = {(void*)&vp, (void*)&o, (void*)&mr, (void*)&nmc, (void*)&xmode};
+        if (xmode == 1) {
+          const size_t gx = (size_t)((grid.x + 7) / 8) * 8 * nmc;
+          if (gx > 0x7FFFFFFFull) throw std::runtime_error("condition grid too large");
+          HIP_OK(hipModuleLaunchKernel(dr->jcond, (uint32_t)gx, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        } else {
+          HIP_OK(hipModuleLaunchKernel(dr->jcond, grid.x, gy, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        }
       }
       if (sl.grid[0]) {
         hipLaunchKernelGGL(walk_kernel, dim3(sl.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, sl.cm[0],

@@ -102,6 +102,12 @@ __device__ __forceinline__ void jc_elem(const View& v, const Node* R, uint32_t a
 __device__ __forceinline__ uint32_t jc_ent(uint32_t i, uint32_t t, uint32_t a) {
   return (t == N_STR && a < JMES_SIDBIT) ? (a | JMES_SIDBIT) : i;
 }
+// list entry of a map key (keys(@)): the key string by id, read from the entry's node word here, where the loads of
+// one map's entries are independent, instead of one dependent node load per element in the operator
+__device__ __forceinline__ uint32_t jc_keyent(const Node* R, uint32_t idx) {
+  const uint32_t k = gtk(R + idx) >> 4;
+  return k < JMES_SIDBIT ? (k | JMES_SIDBIT) : (idx | JMES_KEYBIT);
+}
 // one list element into the lane's LDS list (lane-interleaved); false when the list is full
 __device__ __forceinline__ bool jc_push(uint32_t* L, uint32_t* n, uint32_t e) {
   if (*n >= JCAP) return false;

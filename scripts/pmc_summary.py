@@ -23,6 +23,8 @@ EVAL = ("kyv", "kyv_jit_walk")  # kernels of one evaluation: kyv::match_kernel, 
 
 def is_eval(name):
     n = name[5:] if name.startswith("void ") else name  # templates: "void kyv::match_kernel<true>(...)"
+    if n.startswith("kyv::gmask_kernel"):  # once per batch (glob masks of the dictionary), not per evaluation
+        return False
     return n.startswith("kyv::") or n.startswith("kyv_jit")
 
 
