@@ -6,7 +6,7 @@ variables), autogen applied (every compiled rule counts: 89), over a seeded synt
 resources per GPU (10M at 8 GPUs). One "step" = one evaluation of every (resource, compiled rule) pair of the rank's
 shard with the batch resident in HBM.
 
-  python bench.py [--gpus N --steps K --warmup W] [--workload c3|c2|c4] [--resources R]
+  python bench.py [--gpus N --steps K --warmup W] [--workload c3|c2|c4|c5] [--resources R]
 
 --gpus N > 1 without an external launcher: this script starts N rank processes itself (before any GPU call) and
 exits with the worst rank's code; under torch.distributed.run it is one rank. Every rank evaluates its own shard
@@ -43,6 +43,9 @@ def load_policies(workload):
     if workload == "c4":
         from kyverno_amd import synth
         return synth.c4_policies(10000)
+    if workload == "c5":
+        from kyverno_amd import synth
+        return synth.c5_policies(50)
     out = []
     for f in ("chart_restricted.json", "best_practices.json"):
         with open(os.path.join(gdir, f)) as fh:
@@ -192,7 +195,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4"])
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"])
     ap.add_argument("--resources", type=int, default=0, help="resources per GPU (default 1.25M c3 / 1M c2 / c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (flatten + H2D + eval + D2H) leg")
@@ -205,7 +208,7 @@ def main():
 
     rank, world, local, pg = dist_setup(args.gpus)
     nper = args.resources or (1_250_000 if args.workload == "c3" else 1_000_000)
-    kind = "pods" if args.workload == "c2" else "mixed"
+    kind = "pods" if args.workload in ("c2", "c5") else "mixed"
     policies = load_policies(args.workload)
 
     t0 = time.time()
@@ -286,7 +289,9 @@ def main():
                     "excluded, SURVEY §8(d); %d compiled rules) over %d mixed resources per GPU",
               "c2": "C2: podSecurity restricted/latest (%d compiled rules) over %d pods per GPU",
               "c4": "C4: 10,000 generated policies, wildcard match/exclude stress (%d compiled rules) over %d mixed "
-                    "resources per GPU"}[args.workload] % (nrules, batch.n)
+                    "resources per GPU",
+              "c5": "C5: 50 generated precondition / deny policies with variables (%d compiled rules) over %d pods "
+                    "per GPU"}[args.workload] % (nrules, batch.n)
         config = {"workload": wl, "resources_per_gpu": batch.n, "compiled_rules": nrules,
                   "pairs_per_step": int(total_pairs), "cpu_fallback_pairs_per_step": int(total_fb),
                   "parallelism": "shard%d" % world}

@@ -17,6 +17,7 @@
 #include <thread>
 
 #include "kyv_host.h"
+#include "kyv_pss.h"
 
 namespace kyv {
 using pj::T;
@@ -593,6 +594,9 @@ bool split_lines(const char* p, size_t n, int T, std::vector<std::pair<size_t, s
 
 void derive_strings(Batch& b, size_t from, int threads) {
   size_t n = b.dict.strs.size();
+  // the PodSecurity checks' fixed prefixes (seeded well-known strings)
+  const std::string pfx_aa = b.dict.strs[KSID(APPARMOR_PREFIX)], pfx_lh = b.dict.strs[KSID(LOCALHOST_PREFIX)],
+                    pfx_sc = b.dict.strs[KSID(SECCOMP_CONTAINER_PREFIX)];
   std::vector<uint32_t> gidx;  // ruleset glob-mask index + 1 per (seeded) pattern string
   if (b.rs) {
     gidx.assign(std::min(n, b.rs->dict.strs.size()), 0);
@@ -616,6 +620,9 @@ void derive_strings(Batch& b, size_t from, int threads) {
         if (ascii) f |= SF_ASCII;
         if (!ascii || x.find_first_of("*?") != std::string::npos) f |= SF_GLOBBY;
         if (s < gidx.size()) f |= gidx[s] << SF_GIDX_SHIFT;
+        if (x.compare(0, pfx_aa.size(), pfx_aa) == 0) f |= SF_PFX_APPARMOR;
+        if (x.compare(0, pfx_lh.size(), pfx_lh) == 0) f |= SF_PFX_LOCALHOST;
+        if (x.compare(0, pfx_sc.size(), pfx_sc) == 0) f |= SF_PFX_SECCOMP_C;
         // time.ParseDuration and resource.ParseQuantity need a sign, digit or '.' first; strconv.ParseFloat also
         // accepts inf / infinity / nan spellings -- every other string skips the parsers
         const char c0 = x.empty() ? 0 : x[0];
@@ -946,6 +953,8 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
     b->nodes.resize(total_nodes);
     b->hdr.resize(total_res);
     b->faux.resize(total_faux);
+    bool pss_rules = false;
+    for (auto& rd : rs->rules) pss_rules = pss_rules || rd.kind == RK_PSS;
     parallel_for(nchunks, T, [&](size_t c) {
       Chunk& ch = chunks[c];
       const auto& rm = remap[c];
@@ -992,6 +1001,11 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
         h.root = (uint32_t)(node_base[c] + h.root);
         h.kind = rm[h.kind]; h.gvk_kind = rm[h.gvk_kind]; h.group = rm[h.group]; h.version = rm[h.version];
         h.gv = rm[h.gv]; h.name = rm[h.name]; h.gen_name = rm[h.gen_name]; h.ns = rm[h.ns];
+        if (pss_rules) {  // typed pod decode once per resource (eval_pss skips it on RF_PSS_DONE)
+          uint32_t pm, ps;
+          const uint8_t st = pss_pod(NodeTab{R}, h.kind, true, &pm, &ps);
+          h.flags |= RF_PSS_DONE | (st == ST_ERROR ? RF_PSS_DEC_ERR : 0u);
+        }
         auto it = ns_set.find(h.ns);
         h.nsl = it == ns_set.end() ? NONE : it->second;
         b->hdr[res_base[c] + r] = h;

@@ -180,7 +180,7 @@ KYV_HD void j_drop_nulls(JList& L) {
   for (uint32_t j = 0; j < L.n; j++) if (L.e[j] != NONE) L.e[w++] = L.e[j];
   L.n = w;
 }
-__host__ __device__ __attribute__((noinline)) int jmes_run(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, JRes* out, uint32_t* miss) {
+__host__ __device__ inline __attribute__((noinline)) int jmes_run(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, JRes* out, uint32_t* miss) {
   const uint32_t* p = v.pool + o.a;
   const uint32_t n = o.nseg, root = p[0] & 0xFFu;
   const bool pure = (p[0] & JF_PURE) != 0;

@@ -19,7 +19,7 @@
 namespace kyv {
 
 #define KYV_HD __host__ __device__ inline
-#define KYV_BIG __host__ __device__ __attribute__((noinline))
+#define KYV_BIG __host__ __device__ inline __attribute__((noinline))  // inline: one definition across translation units
 // Inlining policy of the large evaluator stages (overridable for experiments)
 // (everything on the pattern path inlines into the kernel; the PodSecurity checks stay out of line)
 #ifndef KYV_FN_MATCH

@@ -68,6 +68,10 @@ enum StrFlag : uint32_t {
   SF_SEMVERISH = 1u << 10, // could parse as blang/semver (digit first, two dots) -> numeric conditions fall back
   SF_GLOBBY = 1u << 11,    // as a wildcard pattern it needs the rune matcher: holds '*' or '?', or is not ASCII
                            // (else wildcard.Match(p, s) is p == s, i.e. an id compare)
+  // PodSecurity annotation prefixes (the checks' strings.HasPrefix, decided once per string)
+  SF_PFX_APPARMOR = 1u << 12,   // "container.apparmor.security.beta.kubernetes.io/"
+  SF_PFX_LOCALHOST = 1u << 13,  // "localhost/"
+  SF_PFX_SECCOMP_C = 1u << 14,  // "container.seccomp.security.alpha.kubernetes.io/"
 };
 // bits 16..23 of a ruleset wildcard pattern's str_flags: its glob-mask index + 1 (0: none). The device holds one
 // bit per (dictionary string, masked pattern): wildcard.Match(pattern, string), evaluated once per batch
@@ -92,6 +96,10 @@ enum ResFlag : uint32_t {
   RF_META_NOTMAP = 1u << 6, // metadata present, not an object
   RF_LAB_BAD = 1u << 7,     // metadata.labels present, not null, and not an object of strings
   RF_ANN_BAD = 1u << 8,     // metadata.annotations likewise
+  // typed decode of the pod (template) a PodSecurity rule reads (validation.go:481-532), done once per resource by
+  // the flattener when the ruleset has PodSecurity rules (RF_PSS_DONE): RF_PSS_DEC_ERR = it does not decode
+  RF_PSS_DONE = 1u << 9,
+  RF_PSS_DEC_ERR = 1u << 10,
 };
 
 struct ResHeader {          // 64 bytes, one per resource (unstructured accessors, host-computed)

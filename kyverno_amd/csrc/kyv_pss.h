@@ -229,6 +229,8 @@ KYV_HD bool has_prefix(const View& v, uint32_t s, uint32_t prefix) {
   uint32_t ln = v.str_len[prefix];
   return v.str_len[s] >= ln && bytes_eq(sbytes(v, s), sbytes(v, prefix), ln);
 }
+// has_prefix for the checks' three fixed prefixes, from the per-string flags (derive_strings)
+KYV_HD bool has_pfx(const View& v, uint32_t s, uint32_t flag) { return (v.str_flags[s] & flag) != 0; }
 
 // evaluatePSS (evaluate.go:16-37): failing (check, version) slots
 KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
@@ -329,7 +331,7 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
       for (uint32_t i = 0; i < R[ann].b; i++) {
         const Node& e = R[R[ann].a + i];
         uint32_t k = node_key(e);
-        if (v.str_len[k] == pl + nl && has_prefix(v, k, KSID(SECCOMP_CONTAINER_PREFIX)) &&
+        if (has_pfx(v, k, SF_PFX_SECCOMP_C) && v.str_len[k] == pl + nl &&
             bytes_eq(sbytes(v, k) + pl, sbytes(v, cname), nl) && node_type(e) == N_STR && e.a == KSID(UNCONFINED_LC))
           secAnnBad = true;
       }
@@ -355,8 +357,8 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
     for (uint32_t i = 0; i < R[ann].b; i++) {
       const Node& e = R[R[ann].a + i];
       uint32_t val = node_type(e) == N_STR ? e.a : SID_EMPTY;
-      if (has_prefix(v, node_key(e), KSID(APPARMOR_PREFIX)) && val != KSID(RUNTIME_DEFAULT_PROFILE) &&
-          !has_prefix(v, val, KSID(LOCALHOST_PREFIX)))
+      if (has_pfx(v, node_key(e), SF_PFX_APPARMOR) && val != KSID(RUNTIME_DEFAULT_PROFILE) &&
+          !has_pfx(v, val, SF_PFX_LOCALHOST))
         fails |= 1u << PS_APPARMOR;
       if (node_key(e) == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = true;
     }
@@ -375,10 +377,18 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
   uint32_t vols = get(R, spec, KSID(VOLUMES));
   if (!nil(R, vols) && node_type(R[vols]) == N_ARR)
     for (uint32_t i = 0; i < R[vols].b; i++) {
+      // one pass over the volume's entries (keys are unique): a non-null hostPath entry, and whether some allowed
+      // source (the first V_ALLOWED volume-source sids) is set
       uint32_t vn = R[vols].a + i;
-      if (!nil(R, get(R, vn, VSID(hostPath)))) fails |= 1u << PS_HOSTPATH;
       bool okv = false;
-      for (uint32_t s = 0; s < V_ALLOWED && !okv; s++) okv = !nil(R, get(R, vn, SID_FIRST_FREE + K_COUNT + s));
+      if (node_type(R[vn]) == N_MAP)
+        for (uint32_t q = 0; q < R[vn].b; q++) {
+          const Node& e = R[R[vn].a + q];
+          if (node_type(e) == N_NULL) continue;
+          const uint32_t k = node_key(e);
+          if (k == VSID(hostPath)) fails |= 1u << PS_HOSTPATH;
+          if (k >= SID_FIRST_FREE + K_COUNT && k < SID_FIRST_FREE + K_COUNT + V_ALLOWED) okv = true;
+        }
       if (!okv) fails |= 1u << PS_RVOLUMES;
     }
   if (portsBad) fails |= 1u << PS_HOSTPORTS;
@@ -418,11 +428,10 @@ KYV_HD uint32_t pss_id_slots(uint32_t slot) {
   }
 }
 
-// validatePodSecurity (validation.go:535-566) -> status; *fails receives the remaining failing slots
-KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out) {
-  *fails_out = 0;
-  if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
-  uint32_t kind = h.kind;
+// getSpec (validation.go:481-532) for a PodSecurity rule: the pod (template) of the resource's kind, typed-decoded
+// when `decode`. ST_NONE: *meta / *spec are its metadata and spec nodes; ST_ERROR: it does not decode; ST_PANIC: a
+// kind without a pod spec (nil dereference, validation.go:542-543)
+KYV_HD uint8_t pss_pod(NodeTab R, uint32_t kind, bool decode, uint32_t* meta_out, uint32_t* spec_out) {
   uint32_t root = 0;
   uint32_t meta = NONE, spec = NONE;
   Dec d{R, false};
@@ -451,8 +460,24 @@ KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const R
     return ST_PANIC;  // nil pod spec dereference (validation.go:542-543)
   }
   if (d.bad) return ST_ERROR;
+  *meta_out = meta;
+  *spec_out = spec;
+  if (!decode) return ST_NONE;
   if (outerMeta != meta && !nil(R, outerMeta) && !decode_ok_meta(d, outerMeta)) return ST_ERROR;
   if (!decode_ok_meta(d, meta) || !decode_ok_spec(d, spec)) return ST_ERROR;
+  return ST_NONE;
+}
+
+// validatePodSecurity (validation.go:535-566) -> status; *fails receives the remaining failing slots
+KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out) {
+  *fails_out = 0;
+  if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
+  // the typed decode was done by the flattener when it could (RF_PSS_DONE); else here
+  const bool done = (h.flags & RF_PSS_DONE) != 0;
+  uint32_t meta = NONE, spec = NONE;
+  const uint8_t ps = pss_pod(R, h.kind, !done, &meta, &spec);
+  if (ps != ST_NONE) return ps;
+  if (done && (h.flags & RF_PSS_DEC_ERR)) return ST_ERROR;
   PodView pv;
   pv.meta = meta;
   pv.spec = spec;
