@@ -631,7 +631,7 @@ struct CondGen {
     const uint32_t savePEND = PEND;
     std::ostringstream save;
     save.swap(out);
-    out << "static __device__ int " << name
+    out << "static __device__ __forceinline__ int " << name
         << "(const View& v, const Node* R, uint32_t r, uint32_t ei, uint32_t et, uint32_t ea, uint32_t erow, uint32_t* L, "
            "bool* lst, uint32_t* cur, uint32_t* ln, uint32_t* lit) {\n"
            "  *lst = false; *cur = NONE; *ln = 0u; *lit = NONE;\n";
@@ -818,7 +818,7 @@ struct CondGen {
     out << "  return CR_TRUE;\n";
     const std::string b = out.str();
     out.swap(save);
-    defs << "static __device__ int " << name
+    defs << "static __device__ __forceinline__ int " << name
          << "(const View& v, const Node* R, uint32_t r, uint32_t ei, uint32_t et, uint32_t ea, uint32_t erow, uint32_t* L) {\n"
          << "  (void)ei; (void)et; (void)ea; (void)erow;\n"
          << b << "}\n";
@@ -1024,7 +1024,7 @@ struct CondGen {
     }
     const std::string b = out.str();
     out.swap(save);
-    defs << "static __device__ uint8_t jr" << k << "(const View& v, uint32_t r, uint32_t* L) {\n" << b << "}\n";
+    defs << "static __device__ __attribute__((noinline)) uint8_t jr" << k << "(const View& v, uint32_t r, uint32_t* L) {\n" << b << "}\n";
   }
 };
 
@@ -1169,7 +1169,9 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
   if (!crules.empty()) {
     // one lane per resource, the kernel's rules uniform across the wave (grid.y strides over them); operand lists
     // in LDS, lane-interleaved
-    src << "extern \"C\" __global__ void __launch_bounds__(64)\n"
+    // 5 waves/SIMD: measured 1.30 -> 1.05 ms on C3 (4: 1.11, 6: 1.08; unbounded = 3 waves at 152 VGPRs)
+    src << "#ifndef KYV_JC_WPE\n#define KYV_JC_WPE 5\n#endif\n"
+           "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JC_WPE)))\n"
            "kyv_jit_cond(const kyv::View* __restrict__ vp, kyv::DevOut o, const uint32_t* __restrict__ mrules, uint32_t nm,\n"
            "             uint32_t xmode) {\n"
            "  __shared__ uint32_t jl[" << cg.nslots << "u * kyv::JCAP * 64u];\n"
