@@ -373,8 +373,11 @@ constexpr int RECS_PER_PAIR = MAX_ALTS;
 // that need the walk are appended to the rule's work list (wave ballot + one atomic per wave and rule).
 // Two instantiations: kJ = false for rules without JMESPath operands or foreach (the register budget of the
 // plain match / condition / PodSecurity code), kJ = true for the rest (projection lists live in scratch)
+#ifndef KYV_MATCH_WPE
+#define KYV_MATCH_WPE 4  // C2 A/B: 1.50 ms unbounded (3 waves), 1.40 at 4, 1.47 at 5, 1.53 at 6
+#endif
 template <bool kJ>
-__global__ void __launch_bounds__(BLOCK) match_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl,
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_MATCH_WPE))) match_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl,
                                                       const uint32_t* __restrict__ mrules, uint32_t nm) {
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
