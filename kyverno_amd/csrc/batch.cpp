@@ -133,9 +133,10 @@ struct StrTab {
 
 enum : uint8_t { LF_MAGIC = 1, LF_ANCHORISH = 2 };
 // chunk-local ids interned first, in this order, by every chunk
-enum : uint32_t { L_EMPTY, L_KIND, L_APIVERSION, L_METADATA, L_NAME, L_GENNAME, L_NAMESPACE, L_LABELS, L_ANN, L_FIXED };
+enum : uint32_t { L_EMPTY, L_KIND, L_APIVERSION, L_METADATA, L_NAME, L_GENNAME, L_NAMESPACE, L_LABELS, L_ANN, L_SPEC,
+                  L_TEMPLATE, L_JOBTEMPLATE, L_FIXED };
 const char* const kLocalFixed[L_FIXED] = {"", "kind", "apiVersion", "metadata", "name", "generateName", "namespace",
-                                          "labels", "annotations"};
+                                          "labels", "annotations", "spec", "template", "jobTemplate"};
 
 // one worker's share of the documents: nodes, headers and float forms with chunk-local string ids, remapped to
 // batch ids after the parallel phase
@@ -465,7 +466,7 @@ struct Flat {
     h.labels = h.ann = h.nsl = NONE;
     uint32_t kind = L_EMPTY, av = L_EMPTY, name = L_EMPTY, gen = L_EMPTY, ns = L_EMPTY;
     auto child = [&](uint32_t m, uint32_t key) -> uint32_t {  // relative index of the entry with key, NONE
-      if (node_type(out[m]) != N_MAP) return NONE;
+      if (m == NONE || node_type(out[m]) != N_MAP) return NONE;
       for (uint32_t q = 0; q < out[m].b; q++) if (node_key(out[out[m].a + q]) == key) return out[m].a + q;
       return NONE;
     };
@@ -502,19 +503,27 @@ struct Flat {
     h.version = ch.local(ver);
     h.gv = g.empty() ? h.version : av;  // GroupVersion().String(): "group/version" is the apiVersion itself
     h.flags = (magicf ? RF_MAGIC : 0) | (anchorish ? RF_ANCHORISH : 0) | (node_type(root) == N_MAP ? RF_ROOT_MAP : 0);
-    if (meta == NONE || node_type(out[meta]) == N_NULL) {
-      h.flags |= RF_META_NONE;
-    } else if (node_type(out[meta]) != N_MAP) {
-      h.flags |= RF_META_NOTMAP;
-    } else {
+    // ExpandInMetadata's type assertions for the metadata of the root and of the two pod-template positions
+    auto meta_flags = [&](uint32_t m, uint32_t shift) {  // m: the map holding `metadata` (NONE: not a map there)
+      if (m == NONE || node_type(out[m]) != N_MAP) return;
+      const uint32_t md = child(m, L_METADATA);
+      if (md == NONE || node_type(out[md]) == N_NULL) { h.flags |= 1u << shift; return; }
+      if (node_type(out[md]) != N_MAP) { h.flags |= 2u << shift; return; }
       auto bad = [&](uint32_t x) {  // present, not null, not a map of strings
         if (x == NONE || node_type(out[x]) == N_NULL) return false;
         if (node_type(out[x]) != N_MAP) return true;
         for (uint32_t q = 0; q < out[x].b; q++) if (node_type(out[out[x].a + q]) != N_STR) return true;
         return false;
       };
-      if (bad(child(meta, L_LABELS))) h.flags |= RF_LAB_BAD;
-      if (bad(child(meta, L_ANN))) h.flags |= RF_ANN_BAD;
+      if (bad(child(md, L_LABELS))) h.flags |= 4u << shift;
+      if (bad(child(md, L_ANN))) h.flags |= 8u << shift;
+    };
+    meta_flags(0, RF_META_SHIFT);
+    {
+      const uint32_t sp = child(0, L_SPEC);
+      meta_flags(child(sp, L_TEMPLATE), RF_TMETA1_SHIFT);
+      const uint32_t jt = child(sp, L_JOBTEMPLATE);
+      meta_flags(child(child(jt, L_SPEC), L_TEMPLATE), RF_TMETA2_SHIFT);
     }
     ch.hdr.push_back(h);
     ch.nodes.insert(ch.nodes.end(), out.begin(), out.end());

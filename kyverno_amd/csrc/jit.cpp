@@ -48,12 +48,36 @@ struct Gen {
   std::vector<int> slot_elen;                    // existence entry -> index of the candidates' length column
   std::vector<std::vector<uint32_t>> scope_of;   // scope-root pnode -> its column ids, in pc[] order
   std::vector<uint8_t> scoped;                   // pnode -> scope collected
-  std::vector<uint32_t> root_mbase;              // pattern-root pnode -> its rule's first metadata site
+  std::vector<uint32_t> node_mbase;              // pnode -> its rule's first metadata site (marked from the roots)
+  std::vector<int8_t> meta_pos;                  // pnode -> static position whose metadata flags the flattener
+                                                 // computed: 0 root, 1 spec.template, 2 spec.jobTemplate.spec.template
 
   explicit Gen(const Ruleset& r)
       : rs(r), emitted(r.pnodes.size(), 0), slot(r.pentries.size(), -1), slot_alen(r.pnodes.size(), -1),
         slot_elen(r.pentries.size(), -1), scope_of(r.pnodes.size()), scoped(r.pnodes.size(), 0),
-        root_mbase(r.pnodes.size(), NONE) {}
+        node_mbase(r.pnodes.size(), NONE), meta_pos(r.pnodes.size(), -1) {}
+
+  // static key path of the pattern maps below a rule root (plain key entries only), for meta_pos
+  void mark_paths(uint32_t pn, uint32_t mbase, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, int depth) {
+    if (pn == NONE || pn >= rs.pnodes.size() || depth > 4) return;
+    const PNode& P = rs.pnodes[pn];
+    if (P.kind != P_MAP) return;
+    node_mbase[pn] = mbase;
+    const uint32_t S = SID_FIRST_FREE + K_SPEC, T = SID_FIRST_FREE + K_TEMPLATE, J = SID_FIRST_FREE + K_JOBTEMPLATE;
+    if (depth == 0) meta_pos[pn] = 0;
+    else if (depth == 2 && k0 == S && k1 == T) meta_pos[pn] = 1;
+    else if (depth == 4 && k0 == S && k1 == J && k2 == S && k3 == T) meta_pos[pn] = 2;
+    for (uint32_t e = 0; e < P.n; e++) {
+      const PEntry& E = rs.pentries[P.first + e];
+      if ((E.flags & EF_WILD) || E.child == NONE || E.handler == H_STAR || E.handler == H_NEGATION ||
+          E.handler == H_EXISTENCE || E.handler == H_EXIST_BADPAT)
+        continue;
+      const uint32_t k[4] = {k0, k1, k2, k3};
+      uint32_t nk[4] = {k[0], k[1], k[2], k[3]};
+      if (depth < 4) nk[depth] = E.key;
+      mark_paths(E.child, mbase, nk[0], nk[1], nk[2], nk[3], depth + 1);
+    }
+  }
 
   int add(std::vector<uint32_t>& list, uint32_t col) {
     list.push_back(col);
@@ -348,17 +372,19 @@ struct Gen {
         out << "  if (!(w.found & " << B << ") && wmap_find(w.R, m.a, m.b, " << key << ") != NONE) w.found |= " << B << ";\n";
       }
     }
-    const MetaSite* site = (P.flags & PF_META) && root_mbase[pn] != NONE ? &rs.metas[root_mbase[pn] + P.meta] : nullptr;
+    const MetaSite* site =
+        (P.flags & PF_META) && node_mbase[pn] != NONE && meta_pos[pn] >= 0 ? &rs.metas[node_mbase[pn] + P.meta] : nullptr;
     if (site && site->nwild_l == 0 && site->nwild_a == 0) {
-      // ExpandInMetadata of the resource root without wildcard keys: only its type assertions, decided from the
-      // header flags the flattener computed (same order as expand_meta: absent/null metadata, non-object,
-      // anchor-like keys, labels / annotations that are not objects of strings)
+      // ExpandInMetadata without wildcard keys at the root or a pod-template position: only its type assertions,
+      // decided from the header flags the flattener computed for that position (same order as expand_meta:
+      // absent/null metadata, non-object, anchor-like keys, labels / annotations that are not objects of strings)
+      const uint32_t sh = meta_pos[pn] == 0 ? RF_META_SHIFT : meta_pos[pn] == 1 ? RF_TMETA1_SHIFT : RF_TMETA2_SHIFT;
       out << "  { const uint32_t hf = gld32(&w.hp->flags);\n"
-             "    if (!(hf & RF_META_NONE)) {\n"
-             "      if (hf & RF_META_NOTMAP) { w.ost = ST_PANIC; return ok_ret(); }\n"
+             "    if (!(hf & (1u << " << sh << "))) {\n"
+             "      if (hf & (2u << " << sh << ")) { w.ost = ST_PANIC; return ok_ret(); }\n"
              "      if (hf & RF_ANCHORISH) { w.ost = ST_FALLBACK; return ok_ret(); }\n";
-      if (site->has_labels) out << "      if (hf & RF_LAB_BAD) { w.ost = ST_PANIC; return ok_ret(); }\n";
-      if (site->has_ann) out << "      if (hf & RF_ANN_BAD) { w.ost = ST_PANIC; return ok_ret(); }\n";
+      if (site->has_labels) out << "      if (hf & (4u << " << sh << ")) { w.ost = ST_PANIC; return ok_ret(); }\n";
+      if (site->has_ann) out << "      if (hf & (8u << " << sh << ")) { w.ost = ST_PANIC; return ok_ret(); }\n";
       out << "    } }\n";
     } else if (P.flags & PF_META) {
       // the out-of-line call gets a copy of the key slots: taking w.keys' address would put the whole walker
@@ -1100,7 +1126,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     size_t mark = g.out.tellp();
     std::vector<uint8_t> em = g.emitted;
     g.ok = true;
-    for (uint32_t r : rr) g.root_mbase[r] = rd.meta_sites;
+    for (uint32_t r : rr) g.mark_paths(r, rd.meta_sites, NONE, NONE, NONE, NONE, 0);
     for (uint32_t r : rr) { g.scope(r); g.scopes_below(r, 0); }
     for (uint32_t r : rr) g.node(r, 0);
     if (!g.ok) {  // roll back this rule's functions

@@ -1,6 +1,7 @@
 // Host-side objects behind the C-ABI handles (kyv_ruleset / kyv_batch / kyv_results).
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -143,6 +144,7 @@ struct Batch {
   // the rules that can match them); verdicts are produced in this order and un-permuted at the C ABI
   std::vector<uint32_t> order;    // sorted position -> input index
   std::vector<uint32_t> inv;      // input index -> sorted position
+  std::shared_ptr<const std::vector<uint32_t>> inv_shared;  // immutable copy handed to results (capi.cpp)
   std::vector<uint32_t> gate;     // [kclass][gate_words] bit k: rule k can match a resource of this class
   uint32_t gate_words = 0, nclass = 0;
   // path columns (kyv_layout.h): colv[col_off[c] + row]

@@ -101,6 +101,10 @@ enum ResFlag : uint32_t {
   RF_PSS_DONE = 1u << 9,
   RF_PSS_DEC_ERR = 1u << 10,
 };
+// the same four metadata flags (NONE, NOTMAP, LAB_BAD, ANN_BAD as consecutive bits) for the pod templates of the
+// autogen'd rules: spec.template.metadata at RF_TMETA1_SHIFT, spec.jobTemplate.spec.template.metadata at
+// RF_TMETA2_SHIFT (the resource root's are bits 5..8)
+constexpr uint32_t RF_META_SHIFT = 5, RF_TMETA1_SHIFT = 11, RF_TMETA2_SHIFT = 15;
 
 struct ResHeader {          // 64 bytes, one per resource (unstructured accessors, host-computed)
   uint32_t root;            // node offset of the resource root in the batch node array
