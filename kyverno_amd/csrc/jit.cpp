@@ -386,6 +386,11 @@ struct Gen {
       if (site->has_labels) out << "      if (hf & (4u << " << sh << ")) { w.ost = ST_PANIC; return ok_ret(); }\n";
       if (site->has_ann) out << "      if (hf & (8u << " << sh << ")) { w.ost = ST_PANIC; return ok_ret(); }\n";
       out << "    } }\n";
+    } else if (site && meta_pos[pn] == 0) {
+      // wildcard keys at the resource root: resolved over the header's labels / annotations nodes
+      out << "  { Keys kk = w.keys; uint8_t o = expand_meta_root(w.v, w.v.metas[w.mbase + " << u(P.meta)
+          << "], NodeTab{w.R}, *w.hp, kk); w.keys = kk;\n"
+          << "    if (o != ST_NONE) { w.ost = o; return ok_ret(); } }\n";
     } else if (P.flags & PF_META) {
       // the out-of-line call gets a copy of the key slots: taking w.keys' address would put the whole walker
       // state (JW) in scratch memory for every pattern of the kernel

@@ -603,6 +603,36 @@ KYV_BIG uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32
   return ST_NONE;
 }
 
+// expand_meta at the resource root from what the flattener already knows: the metadata shape flags and the
+// header's labels / annotations nodes (maps of strings), so no map of the metadata is searched again
+KYV_HD uint8_t expand_meta_root(const View& v, const MetaSite& ms, NodeTab R, const ResHeader& h, Keys& keys) {
+  for (uint32_t i = 0; i < ms.nwild_l; i++) keys.set(ms.slot_l + i, v.pool[ms.wild_l + 2 * i + 1]);
+  for (uint32_t i = 0; i < ms.nwild_a; i++) keys.set(ms.slot_a + i, v.pool[ms.wild_a + 2 * i + 1]);
+  if (h.flags & RF_META_NONE) return ST_NONE;
+  if (h.flags & RF_META_NOTMAP) return ST_PANIC;
+  if (h.flags & RF_ANCHORISH) return ST_FALLBACK;
+  for (int tag = 0; tag < 2; tag++) {
+    if (!(tag == 0 ? ms.has_labels : ms.has_ann)) continue;
+    if (h.flags & (tag == 0 ? RF_LAB_BAD : RF_ANN_BAD)) return ST_PANIC;
+    const uint32_t lm = tag == 0 ? h.labels : h.ann;  // NONE: absent or null
+    if (lm == NONE) continue;
+    const Node& L = R[lm];
+    uint32_t wild = tag == 0 ? ms.wild_l : ms.wild_a, nw = tag == 0 ? ms.nwild_l : ms.nwild_a;
+    uint32_t slot0 = tag == 0 ? ms.slot_l : ms.slot_a;
+    for (uint32_t w = 0; w < nw; w++) {
+      uint32_t gp = v.pool[wild + 2 * w];
+      uint32_t hit = NONE, n = 0;
+      for (uint32_t i = 0; i < L.b; i++) {
+        uint32_t k = node_key(R[L.a + i]);
+        if (glob_sid(v, gp, k)) { if (hit == NONE) hit = k; n++; }
+      }
+      if (n > 1) return ST_ND;
+      if (n == 1) keys.set(slot0 + w, hit);
+    }
+  }
+  return ST_NONE;
+}
+
 // MatchPattern (validate.go:31-56) for one compiled pattern; a walk deeper than the stack ends in ST_FALLBACK
 KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const ResHeader& h, const RuleDesc& rd, Stack stk,
                          PatOut& out) {
