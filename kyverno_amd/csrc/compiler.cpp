@@ -2058,12 +2058,20 @@ struct TrieBuilder {
     r.list = list;
     return r;
   }
+  // a plain `{{ request.object.<path> }}` operand: its whole path is one column (cv_operand reads it first)
+  void path(CondOperand& o) {
+    if (o.kind != OK_PATH) return;
+    uint32_t t = 0;
+    for (uint32_t s = 0; s < o.nseg && t != NONE; s++) t = ch(t, rs.pool[o.a + s]);
+    o.list = (t == NONE || o.nseg == 0) ? 0u : rs.trie[t].col + 1;
+  }
   void prog(uint32_t pr, const std::vector<uint32_t>& elem) {
     if (pr == NONE || pr >= rs.cprogs.size()) return;
     const CondProg& P = rs.cprogs[pr];
     const uint32_t nany = P.nany == NONE ? 0u : P.nany;
-    for (uint32_t i = 0; i < nany; i++) { jmes(rs.conds[P.any0 + i].key, elem); jmes(rs.conds[P.any0 + i].value, elem); }
-    for (uint32_t i = 0; i < P.nall; i++) { jmes(rs.conds[P.all0 + i].key, elem); jmes(rs.conds[P.all0 + i].value, elem); }
+    auto one = [&](Cond& c) { jmes(c.key, elem); jmes(c.value, elem); path(c.key); path(c.value); };
+    for (uint32_t i = 0; i < nany; i++) one(rs.conds[P.any0 + i]);
+    for (uint32_t i = 0; i < P.nall; i++) one(rs.conds[P.all0 + i]);
   }
   void cond_rule(const RuleDesc& rd) {
     prog(rd.pre, {});

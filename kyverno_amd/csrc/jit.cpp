@@ -751,7 +751,7 @@ struct CondGen {
       case OK_PATH: {
         const std::string m = fresh("ms");
         out << "  CV " << cv << "; uint32_t " << m << ";\n"
-            << "  " << (check ? "if (!" : "(void)(") << "cv_operand(v, NodeTab{R}, " << C << ", &" << cv << ", &" << m << ")"
+            << "  " << (check ? "if (!" : "(void)(") << "cv_operand(v, NodeTab{R}, " << C << ", &" << cv << ", &" << m << ", r)"
             << (check ? ") return CP_ERROR;\n" : ");\n");
         return;
       }

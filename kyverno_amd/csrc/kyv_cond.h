@@ -103,8 +103,10 @@ KYV_HD CV cv_elem(const View& v, NodeTab R, const CV& arr, uint32_t j) {
   return cv_node(v.cnodes[a.a + j], false);
 }
 
-// operand value; returns false on a NotFoundError (*miss = failing segment)
-KYV_HD bool cv_operand(const View& v, NodeTab R, const CondOperand& o, CV* out, uint32_t* miss) {
+// operand value; returns false on a NotFoundError (*miss = failing segment). `row`: the resource's position in the
+// batch; a path whose column resolved (every parent a map holding the next key) is one load, anything else takes
+// the key-by-key search (which tells a missing key -- NotFoundError -- from a null or non-map parent)
+KYV_HD bool cv_operand(const View& v, NodeTab R, const CondOperand& o, CV* out, uint32_t* miss, uint32_t row = NONE) {
   if (o.kind == OK_LIT) {
     *out = cv_node(v.cnodes[o.a], false);
     if (out->t == CT_ARR) out->node = o.a;
@@ -112,6 +114,15 @@ KYV_HD bool cv_operand(const View& v, NodeTab R, const CondOperand& o, CV* out, 
   }
   Node nil{N_NULL, 0, 0, 0};
   if (o.kind != OK_PATH) { *out = cv_node(nil, false); return true; }
+  if (o.list && row != NONE && v.colv) {
+    const uint32_t e = (uint32_t)v.colv[(size_t)v.col_off[o.list - 1] + row];
+    if (e != NONE) {
+      const uint32_t x = e & COL_INDEX_MASK;
+      *out = cv_node(R[x], true);
+      if (out->t == CT_ARR) out->node = x;
+      return true;
+    }
+  }
   uint32_t cur = 0;  // request.object = the resource root
   for (uint32_t s = 0; s < o.nseg; s++) {
     const Node& n = R[cur];
@@ -309,8 +320,9 @@ KYV_HD CV jres_cv(const View& v, NodeTab R, const JRes& r, const JList& L) {
 }
 
 // any operand -> CV (JS_OK / JS_NOTFOUND with *miss / JS_FB); L backs a projection list result
-KYV_HD int operand_cv(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, CV* out, uint32_t* miss) {
-  if (o.kind != OK_JMES) return cv_operand(v, R, o, out, miss) ? JS_OK : JS_NOTFOUND;
+KYV_HD int operand_cv(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, CV* out, uint32_t* miss,
+                      uint32_t row = NONE) {
+  if (o.kind != OK_JMES) return cv_operand(v, R, o, out, miss, row) ? JS_OK : JS_NOTFOUND;
   JRes r;
   const int st = jmes_run(v, R, o, elem, L, &r, miss);
   if (st != JS_OK) return st;
@@ -665,7 +677,7 @@ KYV_HD int eval_cond(const View& v, NodeTab R, const Cond& c, const CV& k, const
 constexpr int CP_ERROR = 5;
 template <bool kJ = true>
 KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond, uint32_t* err_side, uint32_t* err_seg,
-                     uint32_t elem = NONE) {
+                     uint32_t elem = NONE, uint32_t row = NONE) {
   const CondProg& p = v.cprogs[prog];
   const uint32_t nany = p.nany == NONE ? 0u : p.nany;
   for (uint32_t blk = 0; blk < 2; blk++) {
@@ -676,7 +688,7 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
       uint32_t miss = 0;
       for (uint32_t side = 0; side < 2; side++) {
         const CondOperand& o = side ? c.value : c.key;
-        if (o.kind == OK_PATH && !cv_operand(v, R, o, &tmp, &miss)) {
+        if (o.kind == OK_PATH && !cv_operand(v, R, o, &tmp, &miss, row)) {
           *err_cond = c0 + i; *err_side = side; *err_seg = miss;
           return CP_ERROR;
         }
@@ -685,7 +697,7 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
             return CR_FB;
           } else {
             JList L;
-            const int st = operand_cv(v, R, o, elem, L, &tmp, &miss);
+            const int st = operand_cv(v, R, o, elem, L, &tmp, &miss, row);
             if (st == JS_FB) return CR_FB;
             if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
           }
@@ -699,12 +711,12 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
     uint32_t miss;
     if constexpr (kJ) {
       JList lk, lx;
-      operand_cv(v, R, c.key, elem, lk, &k, &miss);
-      operand_cv(v, R, c.value, elem, lx, &x, &miss);
+      operand_cv(v, R, c.key, elem, lk, &k, &miss, row);
+      operand_cv(v, R, c.value, elem, lx, &x, &miss, row);
       return eval_cond(v, R, c, k, x);
     } else {
-      cv_operand(v, R, c.key, &k, &miss);
-      cv_operand(v, R, c.value, &x, &miss);
+      cv_operand(v, R, c.key, &k, &miss, row);
+      cv_operand(v, R, c.value, &x, &miss, row);
       return eval_cond(v, R, c, k, x);
     }
   };

@@ -347,7 +347,8 @@ struct CondOperand {     // 16 bytes
   uint8_t sv;            // StrValFlag (literal strings)
   uint16_t nseg;         // OK_PATH: path segments
   uint32_t a;            // OK_LIT: cnodes index; OK_PATH: pool offset of the segments' key sids
-  uint32_t list, nlist;  // SV_LIST: pool offset / count of the []string element sids
+  uint32_t list, nlist;  // SV_LIST: pool offset / count of the []string element sids; OK_PATH: list = the path
+                         // column of the whole path + 1 (0: none), read before the key-by-key search
 };
 struct Cond {            // 48 bytes
   uint8_t op;            // CondOp

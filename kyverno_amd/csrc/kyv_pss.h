@@ -522,7 +522,7 @@ namespace kyv {
 // evaluated list (evaluateList, utils.go:343-355: a non-list result is a one-element list; a query error skips
 // the entry) runs its preconditions (not met -> element skipped) and deny conditions (true -> the rule fails);
 // an error ends the rule only on the last element; no element applied -> skip.
-KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root) {
+KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root, uint32_t row = NONE) {
   const uint32_t nent = v.pool[root];
   uint32_t applied = 0;
   for (uint32_t e = 0; e < nent; e++) {
@@ -558,14 +558,14 @@ KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root) {
       uint32_t ec, es, eg;
       bool err = false;
       if (fe.pre != NONE) {
-        const int c = eval_prog(v, R, fe.pre, &ec, &es, &eg, el);
+        const int c = eval_prog(v, R, fe.pre, &ec, &es, &eg, el, row);
         if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
         if (c == CR_PANIC) return ST_PANIC;
         if (c == CR_FALSE) continue;  // "preconditions not met": skip, not applied
         err = c == CP_ERROR;
       }
       if (!err) {
-        const int c = eval_prog(v, R, fe.deny, &ec, &es, &eg, el);
+        const int c = eval_prog(v, R, fe.deny, &ec, &es, &eg, el, row);
         if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
         if (c == CR_PANIC) return ST_PANIC;
         if (c == CR_TRUE) return ST_FAIL;
@@ -614,7 +614,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
   NodeTab R{v.nodes + h.root};
   uint32_t ec, es, eg;
   if (rd.pre != NONE) {  // checkPreconditions (validation.go:281-288)
-    int c = eval_prog<kJ>(v, R, rd.pre, &ec, &es, &eg);
+    int c = eval_prog<kJ>(v, R, rd.pre, &ec, &es, &eg, NONE, r);
     if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
     if (c == CR_PANIC) return ST_PANIC;
     if (c == CP_ERROR) return ST_ERROR | ST_MARK_PRE;
@@ -624,7 +624,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
     case RK_PANIC: return ST_PANIC;
     case RK_ERROR: return ST_ERROR;
     case RK_DENY: {  // validateDeny (validation.go:437-464)
-      int c = eval_prog<kJ>(v, R, rd.root, &ec, &es, &eg);
+      int c = eval_prog<kJ>(v, R, rd.root, &ec, &es, &eg, NONE, r);
       if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
       if (c == CR_PANIC) return ST_PANIC;
       if (c == CP_ERROR) return ST_ERROR;
@@ -632,7 +632,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
     }
     case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
     case RK_FOREACH:
-      if constexpr (kJ) return eval_foreach(v, R, rd.root);
+      if constexpr (kJ) return eval_foreach(v, R, rd.root, r);
       else return ST_FALLBACK;
     case RK_PATTERN: case RK_ANYPATTERN:
       if (h.flags & RF_MAGIC) return KYV_WHY(FBW_PHRASE), ST_FALLBACK;
