@@ -346,8 +346,12 @@ struct Cx {
   bool allow_element = false;  // compiling conditions of a foreach entry (`element` is bound)
   bool uses_op = false;        // some condition read request.operation
   uint32_t tmpl(const std::string& s) {
+    auto it = rs.template_ids.find(s);
+    if (it != rs.template_ids.end()) return it->second;
     rs.templates.push_back(s);
-    return (uint32_t)rs.templates.size() - 1;
+    const uint32_t id = (uint32_t)rs.templates.size() - 1;
+    rs.template_ids.emplace(s, id);
+    return id;
   }
   uint32_t sid(const std::string& s) { return rs.dict.intern(s); }
 };

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <sstream>
 #include <unordered_map>
@@ -37,6 +38,7 @@ struct Gen {
   const Ruleset& rs;
   std::ostringstream out;
   std::vector<uint8_t> emitted;  // pnode -> function emitted
+  std::vector<uint32_t> emitted_log;  // pnodes in emission order (rollback of one root's functions)
   bool ok = true;                // pattern compilable (else the rule stays on the interpreter)
   const bool use_len = getenv("KYV_JIT_LEN") && atoi(getenv("KYV_JIT_LEN")) != 0;  // array lengths via columns (measured slower: off)
 
@@ -237,6 +239,7 @@ struct Gen {
     }
     if (!ok) return;
     emitted[pn] = 1;
+    emitted_log.push_back(pn);
     const std::string T = u(P.tmpl);
     out << "static __device__ __forceinline__ Ret p" << pn
         << "(JW& w, uint32_t rn, uint32_t rt, uint32_t ra, uint32_t row, const uint64_t* pc) {\n";
@@ -1092,10 +1095,8 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
   if (jit_cond) jit_cond->assign(rs.rules.size(), 0);
   // one generated function tree per pattern: rulesets with thousands of pattern rules (C4: 10k policies) would
   // give a source too large to compile in useful time; they stay on the interpreted walk kernel
-  size_t npat = 0;
-  for (auto& rd : rs.rules) npat += rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN;
+  // (the cap bounds the distinct pattern shapes generated; rules beyond it stay on the interpreted walk)
   const size_t cap = getenv("KYV_JIT_MAX_RULES") ? (size_t)atol(getenv("KYV_JIT_MAX_RULES")) : 1024;
-  if (npat > cap) return "";
   // compiled condition rules: deny / foreach rules with JMESPath operands (the rest of the interpreted
   // match_kernel<true>'s rules); KYV_JIT_COND=0 leaves them all on the interpreter
   CondGen cg(rs);
@@ -1119,6 +1120,34 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     crules.push_back((uint32_t)k);
   }
   std::vector<std::pair<uint32_t, std::vector<uint32_t>>> rule_roots;  // covered rule -> its pattern roots
+  // Structurally identical patterns (same keys, handlers, leaves, path templates and columns; C4's 10k generated
+  // policies use a handful) generate identical code up to pnode numbering: each root's functions are generated
+  // alone, canonicalised (function names numbered by first appearance) and kept only for the first root of that
+  // shape; later roots alias its root function
+  std::ostringstream body;
+  std::unordered_map<std::string, uint32_t> shapes;  // canonical code -> representative root
+  std::unordered_map<uint32_t, uint32_t> rep_of;     // root -> representative root
+  auto canon = [](const std::string& t) {
+    std::unordered_map<std::string, size_t> ids;
+    std::string o;
+    o.reserve(t.size());
+    for (size_t i = 0; i < t.size();) {
+      if (t[i] == 'p' && (i == 0 || !(isalnum((unsigned char)t[i - 1]) || t[i - 1] == '_')) && i + 1 < t.size() &&
+          isdigit((unsigned char)t[i + 1])) {
+        size_t j = i + 1;
+        while (j < t.size() && isdigit((unsigned char)t[j])) j++;
+        if (j < t.size() && t[j] == '(') {
+          auto it = ids.emplace(t.substr(i, j - i), ids.size()).first;
+          o += "p#" + std::to_string(it->second);
+          i = j;
+          continue;
+        }
+      }
+      o += t[i++];
+    }
+    return o;
+  };
+  size_t nshapes = 0;
   for (size_t k = 0; k < rs.rules.size(); k++) {
     const RuleDesc& rd = rs.rules[k];
     if (rd.kind != RK_PATTERN && rd.kind != RK_ANYPATTERN) continue;
@@ -1128,26 +1157,41 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     bool ok = true;
     for (uint32_t r : rr) if (pattern_depth(rs, r, 0) > MAX_DEPTH) ok = false;  // the walk would fall back
     if (!ok) continue;
-    size_t mark = g.out.tellp();
-    std::vector<uint8_t> em = g.emitted;
     g.ok = true;
     for (uint32_t r : rr) g.mark_paths(r, rd.meta_sites, NONE, NONE, NONE, NONE, 0);
     for (uint32_t r : rr) { g.scope(r); g.scopes_below(r, 0); }
-    for (uint32_t r : rr) g.node(r, 0);
-    if (!g.ok) {  // roll back this rule's functions
-      std::string s = g.out.str().substr(0, mark);
-      g.out.str("");
-      g.out.clear();
-      g.out << s;
-      g.emitted = em;
+    std::vector<std::pair<uint32_t, std::string>> texts;  // root -> its functions (new shapes only)
+    std::vector<std::pair<uint32_t, uint32_t>> alias;
+    const size_t log0 = g.emitted_log.size();
+    for (uint32_t r : rr) {
+      std::ostringstream t;
+      t.swap(g.out);
+      g.node(r, 0);
+      t.swap(g.out);
+      if (!g.ok) break;
+      std::string c = canon(t.str());
+      auto it = shapes.find(c);
+      if (it != shapes.end()) alias.push_back({r, it->second});
+      else texts.push_back({r, t.str()});
+    }
+    if (!g.ok || nshapes + texts.size() > cap) {  // roll back this rule: it stays on the interpreted walk
+      for (size_t i = log0; i < g.emitted_log.size(); i++) g.emitted[g.emitted_log[i]] = 0;
+      g.emitted_log.resize(log0);
       continue;
     }
+    for (auto& tx : texts) {
+      shapes.emplace(canon(tx.second), tx.first);
+      rep_of[tx.first] = tx.first;
+      body << tx.second;
+      nshapes++;
+    }
+    for (auto& al : alias) rep_of[al.first] = al.second;
     (*jit_rules)[k] = 1;
     rule_roots.push_back({(uint32_t)k, rr});
   }
   std::ostringstream src;
   src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n#include \"kyv_jcond.h\"\nnamespace kyv {\n";
-  src << g.out.str();
+  src << body.str();
   if (!crules.empty()) {
     // the match part of pair_dispatch, out of line (one copy for every rule that needs more than the kind gate):
     // -1 matched, else the pair's status
@@ -1173,6 +1217,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // the root scope's column preload is issued before the lane's walk predicate is known: it depends on the
     // resource row only, so its loads overlap the header loads the predicate waits for (one memory round, not two)
     for (uint32_t r : roots)
+      if (rep_of[r] == r)  // one root function per pattern shape
       src << "static __device__ __forceinline__ void root" << r
           << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, bool rootmap, bool walk, PatOut& out) {\n"
              "  const uint32_t row0 = (uint32_t)(hp - v.hdr), row = row0 < v.nres ? row0 : NONE;\n"
@@ -1182,14 +1227,41 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
              "  jfinish(w, r, out);\n"
              "}\n";
+    if (roots.size() > 256) {
+      std::map<uint32_t, std::vector<uint32_t>> br2;
+      for (uint32_t r : roots) br2[rep_of[r]].push_back(r);
+      std::vector<uint16_t> tab(rs.pnodes.size(), 0xFFFF);
+      uint16_t si = 0;
+      for (auto& b : br2) { for (uint32_t r : b.second) tab[r] = si; si++; }
+      src << "__device__ const unsigned short kyv_shape" << gi << "[" << std::max<size_t>(1, tab.size()) << "] = {";
+      for (size_t i = 0; i < tab.size(); i++) src << (i ? "," : "") << tab[i];
+      src << "};\n";
+    }
     src << "struct JitWalker" << gi << " {\n"
            "  bool rootmap;\n"
            "  __device__ __forceinline__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp,\n"
            "                                     const RuleDesc& rd, PatOut& out) {\n"
            "    out.status = ST_NONE; out.idx = 0; out.tmpl = NONE; out.key0 = NONE; out.key1 = NONE;\n"
            "#ifdef KYV_EXP_JIT_EMPTY\n    if (walk) out.status = ST_PASS; return;\n#endif\n"
-           "    switch (root) {\n";
-    for (uint32_t r : roots) src << "      case " << r << "u: root" << r << "(v, R, hp, rd.meta_sites, rootmap, walk, out); break;\n";
+           << (roots.size() <= 256 ? std::string("    switch (root) {\n") : "    switch (root < " + std::to_string(rs.pnodes.size()) +
+                                                                "u ? (uint32_t)kyv_shape" + std::to_string(gi) +
+                                                                "[root] : 0xFFFFu) {\n");
+    // roots of one shape share a case (and its root function); with many roots (C4: 10k rules over 15 shapes) the
+    // switch goes over a root -> shape table instead of one label per root (a 10k-label switch took the compiler
+    // minutes)
+    std::map<uint32_t, std::vector<uint32_t>> by_rep;
+    for (uint32_t r : roots) by_rep[rep_of[r]].push_back(r);
+    if (roots.size() <= 256) {
+      for (auto& br : by_rep) {
+        for (uint32_t r : br.second) src << "      case " << r << "u:";
+        src << " root" << br.first << "(v, R, hp, rd.meta_sites, rootmap, walk, out); break;\n";
+      }
+    } else {
+      uint32_t si = 0;
+      for (auto& br : by_rep) {
+        src << "      case " << si++ << "u: root" << br.first << "(v, R, hp, rd.meta_sites, rootmap, walk, out); break;\n";
+      }
+    }
     src << "      default: if (walk) out.status = ST_FALLBACK;\n"
            "    }\n"
            "  }\n"

@@ -99,6 +99,7 @@ struct Ruleset {
   std::vector<CondProg> cprogs;
   std::vector<CondText> cond_text;
   std::vector<std::string> templates;  // path templates: '\x01'+slot = array index, '\x02'+slot = resolved key
+  std::unordered_map<std::string, uint32_t> template_ids;  // interned: identical patterns share template ids
   // path trie over every static lookup of every compiled pattern (kyv_layout.h "Path columns")
   struct TrieNode {
     uint32_t col = NONE;        // column id (key edges; "[*]" nodes: the elements' self column)
