@@ -80,3 +80,24 @@ def test_jit_walk_kernel_compiles_for_gfx950(monkeypatch):
     assert "kyv_jit_walk" in src
     secs, size = rs.jit_compile()
     assert size > 1000
+
+
+def test_jit_shapes_deduplicated_and_compile(monkeypatch):
+    """C4's 10,000 generated policies (10,440 pattern rules) use a handful of pattern shapes: the generator emits one
+    walk function tree per shape (a root -> shape table dispatches the rest), so the whole ruleset is covered and
+    hipRTC compiles it in seconds; the chart's JMESPath / foreach rules get the compiled condition kernel."""
+    import re
+    monkeypatch.setenv("KYV_JIT_CACHE", "0")
+    from kyverno_amd import engine as E, synth
+    rs = E.Ruleset(synth.c4_policies(10000))
+    src, n = rs.jit_source()
+    npat = sum(1 for r in rs.rules if r["kind"] in ("pattern", "anyPattern"))
+    assert npat > 10000 and n == npat
+    assert len(re.findall(r"void root\d+\(", src)) <= 32
+    assert "kyv_shape0" in src
+    secs, size = rs.jit_compile()
+    assert size > 1000
+    import cases
+    rs3 = E.Ruleset(cases.chart_restricted())
+    src3, _ = rs3.jit_source()
+    assert "kyv_jit_cond" in src3 and src3.count("uint8_t jr") >= 12
