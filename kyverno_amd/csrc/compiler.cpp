@@ -1301,6 +1301,14 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
   }
   // request.operation: the background scan's JSON context holds "CREATE" (scanner.go:97; CLI default common.go:287)
   const uint32_t oplit = root == JR_OPERATION ? emit_cnode(c, Value::S("CREATE")) : NONE;
+  if (root == JR_OPERATION) {
+    // the value is that literal whatever follows (`|| <default>` never applies to the non-empty "CREATE"): a plain
+    // literal operand, so the rule needs no JMESPath evaluation (light match kernel)
+    o->kind = OK_LIT;
+    o->a = oplit;
+    o->nseg = 0;
+    return true;
+  }
   o->kind = OK_JMES;
   o->a = (uint32_t)c.rs.pool.size();
   c.rs.pool.push_back(root | (pure ? JF_PURE : 0u));

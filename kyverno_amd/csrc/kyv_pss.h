@@ -66,32 +66,36 @@ struct SecCtx {
   uint32_t proc;
 };
 
-KYV_HD void dec_selinux(Dec& d, uint32_t n, bool& set, uint32_t& user, uint32_t& role, uint32_t& type) {
+// `full` = false: the typed decode was already verified (RF_PSS_DONE), so fields read only for that validation
+// (levels, localhost profiles, gMSA, runAsGroup, readOnlyRootFilesystem, capability strings) are skipped
+KYV_HD void dec_selinux(Dec& d, uint32_t n, bool& set, uint32_t& user, uint32_t& role, uint32_t& type, bool full = true) {
   set = d.obj(n);
   user = role = type = SID_EMPTY;
   if (!set) return;
   user = d.str(get(d.R, n, KSID(USER)));
   role = d.str(get(d.R, n, KSID(ROLE)));
   type = d.str(get(d.R, n, KSID(TYPE)));
-  d.str(get(d.R, n, KSID(LEVEL)));
+  if (full) d.str(get(d.R, n, KSID(LEVEL)));
 }
-KYV_HD void dec_seccomp(Dec& d, uint32_t n, bool& set, uint32_t& type) {
+KYV_HD void dec_seccomp(Dec& d, uint32_t n, bool& set, uint32_t& type, bool full = true) {
   set = d.obj(n);
   type = SID_EMPTY;
   if (!set) return;
   type = d.str(get(d.R, n, KSID(TYPE)));
-  d.str(get(d.R, n, KSID(LOCALHOSTPROFILE)));
+  if (full) d.str(get(d.R, n, KSID(LOCALHOSTPROFILE)));
 }
-KYV_HD int dec_win(Dec& d, uint32_t n) {
+KYV_HD int dec_win(Dec& d, uint32_t n, bool full = true) {
   if (!d.obj(n)) return -1;
   int hp = d.pbool(get(d.R, n, KSID(HOSTPROCESS)));
-  d.str(get(d.R, n, KSID(GMSA_NAME)));
-  d.str(get(d.R, n, KSID(GMSA)));
-  d.str(get(d.R, n, KSID(RUNASUSERNAME)));
+  if (full) {
+    d.str(get(d.R, n, KSID(GMSA_NAME)));
+    d.str(get(d.R, n, KSID(GMSA)));
+    d.str(get(d.R, n, KSID(RUNASUSERNAME)));
+  }
   return hp;
 }
 
-KYV_HD SecCtx dec_container_sc(Dec& d, uint32_t c) {
+KYV_HD SecCtx dec_container_sc(Dec& d, uint32_t c, bool full = true) {
   SecCtx s;
   s.set = false; s.privileged = s.ape = s.runAsNonRoot = s.hostProcess = -1; s.hasRunAsUser = false; s.runAsUser = 0;
   s.selSet = false; s.selUser = s.selRole = s.selType = SID_EMPTY; s.secSet = false; s.secType = SID_EMPTY;
@@ -103,20 +107,24 @@ KYV_HD SecCtx dec_container_sc(Dec& d, uint32_t c) {
   s.privileged = d.pbool(get(R, sc, KSID(PRIVILEGED)));
   s.ape = d.pbool(get(R, sc, KSID(APE)));
   s.runAsNonRoot = d.pbool(get(R, sc, KSID(RUNASNONROOT)));
-  d.pbool(get(R, sc, KSID(READONLYROOTFS)));
+  if (full) d.pbool(get(R, sc, KSID(READONLYROOTFS)));
   s.hasRunAsUser = d.i64(get(R, sc, KSID(RUNASUSER)), INT64_MIN, INT64_MAX, &s.runAsUser);
-  int64_t g;
-  d.i64(get(R, sc, KSID(RUNASGROUP)), INT64_MIN, INT64_MAX, &g);
-  dec_selinux(d, get(R, sc, KSID(SELINUX)), s.selSet, s.selUser, s.selRole, s.selType);
-  dec_seccomp(d, get(R, sc, KSID(SECCOMP)), s.secSet, s.secType);
-  s.hostProcess = dec_win(d, get(R, sc, KSID(WINOPTS)));
+  if (full) {
+    int64_t g;
+    d.i64(get(R, sc, KSID(RUNASGROUP)), INT64_MIN, INT64_MAX, &g);
+  }
+  dec_selinux(d, get(R, sc, KSID(SELINUX)), s.selSet, s.selUser, s.selRole, s.selType, full);
+  dec_seccomp(d, get(R, sc, KSID(SECCOMP)), s.secSet, s.secType, full);
+  s.hostProcess = dec_win(d, get(R, sc, KSID(WINOPTS)), full);
   uint32_t caps = get(R, sc, KSID(CAPS));
   if (d.obj(caps)) {
     s.caps = caps;
-    const uint32_t ckeys[2] = {KSID(ADD), KSID(DROP)};
-    for (uint32_t key : ckeys) {
-      uint32_t l = get(R, caps, key);
-      if (d.arr(l)) for (uint32_t i = 0; i < R[l].b; i++) d.str(R[l].a + i);
+    if (full) {
+      const uint32_t ckeys[2] = {KSID(ADD), KSID(DROP)};
+      for (uint32_t key : ckeys) {
+        uint32_t l = get(R, caps, key);
+        if (d.arr(l)) for (uint32_t i = 0; i < R[l].b; i++) d.str(R[l].a + i);
+      }
     }
   }
   uint32_t pm = get(R, sc, KSID(PROCMOUNT));
@@ -211,6 +219,7 @@ struct PodView {
   uint32_t lists[3];   // init, containers, ephemeral (visitContainers order)
   bool fake;
   uint32_t img, nimg;  // image globs (pool)
+  bool decoded;        // the typed decode was verified by the flattener: the checks skip decode-only fields
 };
 
 KYV_HD bool container_included(const View& v, NodeTab R, const PodView& pv, uint32_t c) {
@@ -249,11 +258,12 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
   int podNonRoot = pscSet ? d.pbool(get(R, psc, KSID(RUNASNONROOT))) : -1;
   int64_t podUser = 0;
   bool podHasUser = pscSet && d.i64(get(R, psc, KSID(RUNASUSER)), INT64_MIN, INT64_MAX, &podUser);
+  const bool full = !pv.decoded;
   bool podSelSet = false; uint32_t pu = SID_EMPTY, pr = SID_EMPTY, pt = SID_EMPTY;
-  if (pscSet) dec_selinux(d, get(R, psc, KSID(SELINUX)), podSelSet, pu, pr, pt);
+  if (pscSet) dec_selinux(d, get(R, psc, KSID(SELINUX)), podSelSet, pu, pr, pt, full);
   bool podSecSet = false; uint32_t podSecType = SID_EMPTY;
-  if (pscSet) dec_seccomp(d, get(R, psc, KSID(SECCOMP)), podSecSet, podSecType);
-  int podHostProcess = pscSet ? dec_win(d, get(R, psc, KSID(WINOPTS))) : -1;
+  if (pscSet) dec_seccomp(d, get(R, psc, KSID(SECCOMP)), podSecSet, podSecType, full);
+  int podHostProcess = pscSet ? dec_win(d, get(R, psc, KSID(WINOPTS)), full) : -1;
 
   const uint32_t capsOK[13] = {KSID(CAP_AUDIT_WRITE), KSID(CAP_CHOWN), KSID(CAP_DAC_OVERRIDE), KSID(CAP_FOWNER),
                                KSID(CAP_FSETID), KSID(CAP_KILL), KSID(CAP_MKNOD), KSID(NET_BIND_SERVICE),
@@ -279,7 +289,7 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
       s.selSet = false; s.secSet = false; s.caps = NONE; s.procSet = false;
       cname = KSID(FAKE);
     } else {
-      s = dec_container_sc(d, c);
+      s = dec_container_sc(d, c, full);
       uint32_t nm = get(R, c, KSID(NAME));
       cname = nil(R, nm) ? SID_EMPTY : R[nm].a;
     }
@@ -487,6 +497,7 @@ KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const R
   pv.fake = false;
   pv.img = 0;
   pv.nimg = 0;
+  pv.decoded = done;  // (a decode error returned above)
   uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
   uint32_t fails = pss_checks(v, R, pv) & mask;
   for (uint32_t x = 0; x < pd.nexcl; x++) {
