@@ -496,7 +496,8 @@ int64_t kyv_results_fallback_reason(const kyv_results* r, const kyv_ruleset* rs,
   if (!r || !rs || !b || rule >= r->r.nrules || res >= r->r.nres) return -1;
   try {
     const uint32_t pos = (*r->inv)[res];
-    if (!r->r.status.empty() && (r->r.status[(size_t)rule * r->r.nres + pos] & 7) != ST_FALLBACK) return put("", buf, cap);
+    if (r->r.status.empty()) return fail(KYV_ERANGE, "verdicts kept on the device"), -1;  // status unknown here
+    if ((r->r.status[(size_t)rule * r->r.nres + pos] & 7) != ST_FALLBACK) return put("", buf, cap);
     return put(fallback_why(*rs->rs, *b->b, pos, rule), buf, cap);
   } catch (std::exception& e) {
     fail(KYV_EINTERNAL, e.what());

@@ -1312,7 +1312,6 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
   o->kind = OK_JMES;
   o->a = (uint32_t)c.rs.pool.size();
   c.rs.pool.push_back(root | (pure ? JF_PURE : 0u));
-  if (root == JR_OPERATION) c.rs.pool.push_back(oplit);
   for (auto w : fused) c.rs.pool.push_back(w);
   o->nseg = (uint16_t)(c.rs.pool.size() - o->a);
   return true;
@@ -1528,6 +1527,9 @@ uint32_t compile_foreach(Cx& c, const Value& fe, const std::string& message) {
       c.allow_element = false;
       if (!jmes_var(c, "{{" + l->s + "}}", false, &fx.list, nullptr, &c.uses_op)) throw Fallback{"foreach: list"};
       c.allow_element = ae;
+      // eval_foreach iterates path and JMESPath lists only; a literal (request.operation: the one-element list
+      // ["CREATE"] in the reference) is not a program it can run
+      if (fx.list.kind != OK_PATH && fx.list.kind != OK_JMES) throw Fallback{"foreach: list"};
     }
     const Value* es = e.get("elementScope");
     if (es && es->t != T::Null && es->t != T::Bool) throw Fallback{"foreach: elementScope"};
@@ -1915,6 +1917,10 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
         } catch (Fallback& f) {
           rs->pnodes.resize(mark_p); rs->pentries.resize(mark_e); rs->leaves.resize(mark_l);
           rs->atoms.resize(mark_a); rs->templates.resize(mark_t);
+          // interned templates created by the abandoned rule are gone: drop their ids so that a later rule with the
+          // same path string interns it again instead of receiving an id past the end of `templates`
+          for (auto it = rs->template_ids.begin(); it != rs->template_ids.end();)
+            it = it->second >= mark_t ? rs->template_ids.erase(it) : std::next(it);
           rs->cnodes.resize(mark_cn); rs->conds.resize(mark_cd); rs->cond_text.resize(mark_cd); rs->cprogs.resize(mark_cp);
           (void)mark_pool;
           rd.kind = RK_FALLBACK;

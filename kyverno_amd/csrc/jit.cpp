@@ -20,6 +20,7 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <utime.h>
 #include <sstream>
 #include <unordered_map>
 #include <stdexcept>
@@ -1336,7 +1337,9 @@ std::string cache_path(const std::string& src) {
   std::string dir = env ? std::string(env) : self_dir() + "/jitcache";
   const char* cs = getenv("KYV_CSRC");
   std::string csrc = cs ? std::string(cs) : self_dir() + "/csrc";
-  uint64_t h = fnv1a(src);
+  // name = walk-<toolchain hash>-<source hash>.co: the first part covers the device headers, compile options and
+  // the hipRTC version, so a cache prune can drop exactly the entries older sources produced
+  uint64_t h = fnv1a("");
   for (const char* hdr : {"kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_wave.h", "kyv_walk.h", "kyv_jcond.h"})
     h = fnv1a(read_file(csrc + "/" + hdr), h);
   h = fnv1a(std::string("gfx950|O3|c++17|wpe=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4") + "|" +
@@ -1344,8 +1347,8 @@ std::string cache_path(const std::string& src) {
   int maj = 0, min = 0;
   hiprtcVersion(&maj, &min);
   h = fnv1a(std::to_string(maj) + "." + std::to_string(min), h);
-  char name[64];
-  snprintf(name, sizeof name, "/walk-%016llx.co", (unsigned long long)h);
+  char name[80];
+  snprintf(name, sizeof name, "/walk-%08llx-%016llx.co", (unsigned long long)(h >> 32), (unsigned long long)fnv1a(src));
   return dir + name;
 }
 }  // namespace
@@ -1367,6 +1370,7 @@ std::vector<char> jit_compile(const std::string& src, double* seconds) {
     if (blob.size() > 64) {  // written whole (temp file + rename)
       code.assign(blob.begin(), blob.end());
       if (seconds) *seconds = 0;
+      utime(path.c_str(), nullptr);  // last use (build() keeps the newest entry's toolchain generation)
     }
   }
   if (code.empty()) {

@@ -133,3 +133,43 @@ def test_pss_messages_equal_oracle_on_goldens():
                     assert m == o["message"], (name, m, o["message"])
                     n += 1
     assert n > 20
+
+
+def test_template_ids_rolled_back_with_a_fallback_rule():
+    """A rule whose compile falls back after it interned path templates (here: an anchor-error phrase in a later
+    pattern value) must not leave stale template ids behind: the next rule with the same paths gets its own
+    templates and renders the oracle's failing path and message"""
+    pat = {"spec": {"containers": [{"image": "!*:latest", "name": "?*"}]}}
+    bad = json.loads(json.dumps(pat))
+    bad["spec"]["zz"] = "conditional anchor mismatch"  # compiled after the container leaves -> Fallback
+    pols = [_pod_policy("a", "r", bad), _pod_policy("b", "r", pat), _pod_policy("c", "r", {"spec": {"other": {"k": "v"}}})]
+    rs = E.Ruleset(pols)
+    assert rs.rules[0]["kind"] == "fallback"
+    pod = _pod("x")
+    pod["spec"]["containers"] = [{"name": "c", "image": "nginx"}, {"name": "d", "image": "nginx:latest"}]
+    b = E.Batch(rs, [pod])
+    res = E.evaluate(rs, b, backend="cpu")
+    ora = {(p["policy"], r["name"]): r for p in O.validate(pols, json.dumps(pod)) for r in p["rules"]}
+    for k, r in enumerate(rs.rules):
+        pol = rs.policies[r["policy"]]["name"]
+        if pol == "a":
+            continue
+        o = ora.get((pol, r["name"]))
+        if o is None:  # not matched (autogen rules vs a Pod)
+            assert res.status[k, 0] == K.ST_NONE
+            continue
+        assert K.STATUS_NAMES[int(res.status[k, 0])] == o["status"]
+        if o["status"] == "fail":
+            assert res.path(0, k) == o["path"]
+            assert res.message(0, k) == o["message"]
+
+
+def test_foreach_list_of_request_operation_falls_back():
+    """foreach over `request.operation` (the reference iterates the one-element list ["CREATE"]) is not a list
+    program the device runs: compile-time fallback, never a JMESPath program read from a literal's index"""
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "p"},
+           "spec": {"rules": [{"name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                               "validate": {"foreach": [{"list": "request.operation", "deny": {"conditions": {"any": [
+                                   {"key": "{{ element }}", "operator": "Equals", "value": "CREATE"}]}}}]}}]}}
+    rs = E.Ruleset([pol])
+    assert rs.rules[0]["kind"] == "fallback" and rs.rules[0]["reason"].startswith("foreach")
