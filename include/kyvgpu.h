@@ -170,12 +170,19 @@ int64_t kyv_results_count(const kyv_results* r, int status);
  * CalculateSummary (pkg/utils/report/results.go:38-54) over a background-scan batch; returns KYV_OK */
 int kyv_results_rule_counts(const kyv_results* r, int64_t* out, size_t cap);
 double kyv_results_kernel_ms(const kyv_results* r);
+/* GPU evaluation time split by phase (HIP events on the evaluation stream, ms averaged over the launches):
+ * out[0] verdict resets + match kernels, [1] compiled condition kernel, [2] pattern walk kernels (the dominant kernel
+ * of a pattern ruleset), [3] failing-path compaction, [4] verdict histogram; returns the number of phases (5) */
+int kyv_results_phase_ms(const kyv_results* r, double* out, size_t cap);
 /* bit 0: the runtime-compiled walk kernels evaluated this result's pattern rules (else the interpreter); bit 1: the
  * runtime-compiled condition kernel evaluated its deny / foreach rules with JMESPath operands */
 int kyv_results_jit(const kyv_results* r);
 /* CPU backend with KYV_EVAL_ACCOUNT_BYTES: algorithmic bytes of all pairs (header fields, distinct node rows,
  * verdict, PSS mask, failure records); 0 otherwise */
 uint64_t kyv_results_alg_bytes(const kyv_results* r);
+/* the same bytes split by the device phase that moves them (kyv_results_phase_ms order); a kind-gated pair counts
+ * only its verdict-reset byte (phase 0) and its histogram read (phase 4); returns 5 */
+int kyv_results_alg_bytes_phase(const kyv_results* r, uint64_t* out, size_t cap);
 /* RuleResponse.Message for one pair; returns the full length (may exceed cap), -1 if unavailable */
 int64_t kyv_results_message(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,
                             uint32_t rule, char* buf, size_t cap);
@@ -186,6 +193,16 @@ int64_t kyv_results_failures(const kyv_results* r, kyv_failure* out, size_t cap)
 /* failing path of a single-pattern FAIL ("" otherwise); returns the full length */
 int64_t kyv_results_path(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res, uint32_t rule,
                          char* buf, size_t cap);
+/* the same texts for many pairs at once (report rows of a batch: EngineResponseToReportResults,
+ * pkg/utils/report/results.go:84-124, takes RuleResponse.Message of every matched pair): what = KYV_TEXT_MESSAGE
+ * (RuleResponse.Message, as kyv_results_message) or KYV_TEXT_PATH (PatternError.Path, as kyv_results_path) of rule
+ * `rule` for resources [res0, res0 + nres) in input order. lens[i] (nres entries, may be NULL) = byte length of
+ * resource res0+i's text, -1 when it is not renderable (the caller runs engine.Validate for that pair), -2 when its
+ * status is not in status_mask (bit s = KYV_ST_s). The renderable texts are packed back to back into buf in resource
+ * order when cap >= the total. Returns the total length, -1 on bad arguments / verdicts kept on the device. */
+enum { KYV_TEXT_MESSAGE = 0, KYV_TEXT_PATH = 1 };
+int64_t kyv_results_texts(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t rule, uint32_t res0,
+                          uint32_t nres, uint32_t status_mask, int32_t what, char* buf, size_t cap, int32_t* lens);
 /* why a KYV_ST_FALLBACK pair needs the reference engine ("" for other statuses): the rule's compile-time reason
  * ("context", "foreach", "exception", "variables", ...) or the run-time site (value / walk outside the device subset);
  * returns the full length, -1 on bad arguments */

@@ -18,6 +18,7 @@ STATUS_NAMES = ["none", "pass", "fail", "skip", "error", "fallback", "panic", "n
 RULE_KINDS = {1: "pattern", 2: "anyPattern", 3: "podSecurity", 4: "fallback", 5: "panic", 6: "error", 7: "deny",
               8: "foreach"}
 RULE_USES_OPERATION = 1
+TEXT_MESSAGE, TEXT_PATH = 0, 1
 
 
 class CompileOpts(ctypes.Structure):
@@ -60,6 +61,7 @@ EXPORTS = [
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
     "kyv_ruleset_jit_compile", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
     "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures", "kyv_ruleset_rule_flags",
+    "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase",
 ]
 
 _lib = None
@@ -124,6 +126,12 @@ def lib():
     L.kyv_results_message.restype = i64
     L.kyv_results_path.argtypes = [vp, vp, vp, u32, u32, ctypes.c_char_p, sz]
     L.kyv_results_path.restype = i64
+    L.kyv_results_alg_bytes_phase.argtypes = [vp, ctypes.c_void_p, sz]
+    L.kyv_results_alg_bytes_phase.restype = i32
+    L.kyv_results_phase_ms.argtypes = [vp, ctypes.c_void_p, sz]
+    L.kyv_results_phase_ms.restype = i32
+    L.kyv_results_texts.argtypes = [vp, vp, vp, u32, u32, u32, u32, i32, ctypes.c_void_p, sz, ctypes.c_void_p]
+    L.kyv_results_texts.restype = i64
     L.kyv_results_pss_mask.argtypes = [vp, vp, u32, u32]
     L.kyv_results_pss_mask.restype = u32
     L.kyv_results_jit.argtypes = [vp]

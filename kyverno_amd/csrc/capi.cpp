@@ -1,6 +1,7 @@
 // C-ABI (include/kyvgpu.h). No exception crosses this boundary.
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -31,7 +32,7 @@ struct kyv_results {
   // ~0.4 ms of host time per call at 1.25 M resources)
   std::shared_ptr<const std::vector<uint32_t>> inv;
   std::multimap<uint64_t, uint32_t> recidx;  // (rule<<32|res) -> record
-  bool indexed = false;
+  std::atomic<bool> indexed{false};
   std::mutex mu;
 };
 
@@ -260,16 +261,29 @@ int kyv_results_rule_counts(const kyv_results* r, int64_t* out, size_t cap) {
 
 double kyv_results_kernel_ms(const kyv_results* r) { return r ? r->r.kernel_ms : 0; }
 
+int kyv_results_phase_ms(const kyv_results* r, double* out, size_t cap) {
+  if (!r || !out) return fail(KYV_EINVAL, "null argument"), -1;
+  for (size_t q = 0; q < 5 && q < cap; q++) out[q] = r->r.phase_ms[q];
+  return 5;
+}
+
 uint64_t kyv_results_alg_bytes(const kyv_results* r) { return r ? r->r.alg_bytes : 0; }
 
+int kyv_results_alg_bytes_phase(const kyv_results* r, uint64_t* out, size_t cap) {
+  if (!r || !out) return fail(KYV_EINVAL, "null argument"), -1;
+  for (size_t q = 0; q < 5 && q < cap; q++) out[q] = r->r.alg_bytes_phase[q];
+  return 5;
+}
+
 static void ensure_index(kyv_results* r) {
+  if (r->indexed.load(std::memory_order_acquire)) return;
   std::lock_guard<std::mutex> g(r->mu);
-  if (r->indexed) return;
+  if (r->indexed.load(std::memory_order_relaxed)) return;
   for (uint32_t i = 0; i < r->r.fails.size(); i++) {
     const FailRec& f = r->r.fails[i];
     r->recidx.emplace(((uint64_t)f.rule << 32) | f.res, i);
   }
-  r->indexed = true;
+  r->indexed.store(true, std::memory_order_release);
 }
 
 static int64_t put(const std::string& s, char* buf, size_t cap) {
@@ -324,19 +338,19 @@ static bool cond_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uin
 }
 
 // getDenyMessage (validation.go:466-479) with the message's request.object references resolved; -1: not renderable
-static int64_t deny_message(const RuleMeta& m, const Batch& b, uint32_t res, char* buf, size_t cap) {
-  if (m.message.empty()) return put("validation error: rule " + m.name + " failed", buf, cap);
-  if (m.msg_parts.empty()) return put(m.message, buf, cap);
+static bool deny_message(const RuleMeta& m, const Batch& b, uint32_t res, std::string* o) {
+  if (m.message.empty()) return *o = "validation error: rule " + m.name + " failed", true;
+  if (m.msg_parts.empty()) return *o = m.message, true;
   const Node* R = b.nodes.data() + b.hdr[res].root;
   std::string out;
   for (auto& part : m.msg_parts) {
     if (!part.var) { out += part.text; continue; }
     uint32_t node, miss;
-    if (!host_resolve(b, res, part.segs, &node, &miss)) return put(m.message, buf, cap);  // substitution error
+    if (!host_resolve(b, res, part.segs, &node, &miss)) return *o = m.message, true;  // substitution error
     std::string sub;
     uint32_t t = node == NONE ? N_NULL : node_type(R[node]);
     if (m.msg_whole_var)
-      return put(t == N_STR ? b.dict.strs[R[node].a] : "the produced message didn't resolve to a string, check your policy definition.", buf, cap);
+      return *o = t == N_STR ? b.dict.strs[R[node].a] : "the produced message didn't resolve to a string, check your policy definition.", true;
     switch (t) {
       case N_STR: sub = b.dict.strs[R[node].a]; break;
       case N_NULL: sub = "null"; break;
@@ -350,12 +364,12 @@ static int64_t deny_message(const RuleMeta& m, const Batch& b, uint32_t res, cha
         sub = pj::go_fmt_json(f);
         break;
       }
-      default: return -1;  // json.Marshal of a map / array
+      default: return false;  // json.Marshal of a map / array
     }
-    if (sub.find("{{") != std::string::npos) return -1;  // nested variables are substituted again
+    if (sub.find("{{") != std::string::npos) return false;  // nested variables are substituted again
     out += sub;
   }
-  return put(out, buf, cap);
+  return *o = out, true;
 }
 
 static uint32_t pss_mask_at(const kyv_results* r, const Ruleset& rs, uint32_t pos, uint32_t rule) {
@@ -375,85 +389,93 @@ static std::string json_str(const std::string& s) {
   return o + "\"";
 }
 
-// validation.go:722-758 (buildErrorMessage / buildAnyPatternErrorMessage) and :640/:665 pass messages
-int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res, uint32_t rule,
-                            char* buf, size_t cap) {
-  auto* r = const_cast<kyv_results*>(cr);
-  if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
-  res = (*r->inv)[res];
-  const Ruleset& rs = *crs->rs;
-  const Batch& b = *cb->b;
+// validation.go:722-758 (buildErrorMessage / buildAnyPatternErrorMessage) and :640/:665 pass messages of the pair at
+// kind-major position `res`; false: the text needs the reference engine (Go error strings, variables)
+static bool render_message(kyv_results* r, const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule, std::string* o) {
   uint8_t sb = r->r.status[(size_t)rule * r->r.nres + res];
   uint8_t st = sb & 7, alt = sb >> 3;
   const RuleMeta& m = rs.meta[rule];
   const RuleDesc& d = rs.rules[rule];
   if (sb >> 3 == (ST_MARK_PRE >> 3) && d.pre != NONE) {  // checkPreconditions outcome (validation.go:281-288)
-    if (st == ST_SKIP) return put("preconditions not met", buf, cap);
+    if (st == ST_SKIP) return *o = "preconditions not met", true;
     std::string e;
     if (st == ST_ERROR && cond_error_text(rs, b, res, d.pre, &e))
-      return put("failed to evaluate preconditions: failed to substitute variables in preconditions: " + e, buf, cap);
-    return -1;
+      return *o = "failed to evaluate preconditions: failed to substitute variables in preconditions: " + e, true;
+    return false;
   }
   if (d.kind == RK_DENY) {  // validateDeny (validation.go:437-479)
-    if (st == ST_PASS) return put("validation rule '" + m.name + "' passed.", buf, cap);
-    if (st == ST_FAIL) return m.message_vars ? -1 : deny_message(m, b, res, buf, cap);
+    if (st == ST_PASS) return *o = "validation rule '" + m.name + "' passed.", true;
+    if (st == ST_FAIL) return m.message_vars ? false : deny_message(m, b, res, o);
     std::string e;
     if (st == ST_ERROR && cond_error_text(rs, b, res, d.root, &e))
-      return put("failed to substitute variables in deny conditions: " + e, buf, cap);
-    return -1;
+      return *o = "failed to substitute variables in deny conditions: " + e, true;
+    return false;
   }
   if (d.kind == RK_FOREACH) {  // validateForEach / validateElements (validation.go:319-381)
-    if (st == ST_PASS) return put("rule passed", buf, cap);
-    if (st == ST_SKIP) return put("rule skipped", buf, cap);
+    if (st == ST_PASS) return *o = "rule passed", true;
+    if (st == ST_SKIP) return *o = "rule skipped", true;
     if (st == ST_FAIL)
-      return put("validation failure: " + (m.message.empty() ? "validation error: rule " + m.name + " failed" : m.message),
-                 buf, cap);
-    return -1;  // error texts embed Go error strings
+      return *o = "validation failure: " + (m.message.empty() ? "validation error: rule " + m.name + " failed" : m.message),
+             true;
+    return false;  // error texts embed Go error strings
   }
-  if (m.message_vars && st == ST_FAIL) return -1;  // message needs variable substitution (CPU engine)
-  std::string msg;
+  if (m.message_vars && st == ST_FAIL) return false;  // message needs variable substitution (CPU engine)
   if (d.kind == RK_PSS) {
-    if (st == ST_PASS) return put("Validation rule '" + m.name + "' passed.", buf, cap);
-    if (st != ST_FAIL) return -1;  // decode / version error texts embed Go error strings
+    if (st == ST_PASS) return *o = "Validation rule '" + m.name + "' passed.", true;
+    if (st != ST_FAIL) return false;  // decode / version error texts embed Go error strings
     std::vector<std::array<std::string, 3>> checks;
-    if (!pss_checks_render(rs, b, res, rule, pss_mask_at(r, rs, res, rule), &checks)) return -1;
+    if (!pss_checks_render(rs, b, res, rule, pss_mask_at(r, rs, res, rule), &checks)) return false;
     // validation.go:561 + pss.FormatChecksPrint (evaluate.go:160-166): fmt "(%+v)\n" of each CheckResult
     std::string msg = "Validation rule '" + m.name + "' failed. It violates PodSecurity \"" + m.pss_level + ":" +
                       m.pss_version + "\": ";
     for (auto& c : checks) msg += "({Allowed:false ForbiddenReason:" + c[1] + " ForbiddenDetail:" + c[2] + "})\n";
-    return put(msg, buf, cap);
+    return *o = msg, true;
   }
   if (st == ST_PASS) {
     if (d.kind == RK_ANYPATTERN) {
-      if (alt == 31) return put(m.message, buf, cap);
-      return put("validation rule '" + m.name + "' anyPattern[" + std::to_string(alt) + "] passed.", buf, cap);
+      if (alt == 31) return *o = m.message, true;
+      return *o = "validation rule '" + m.name + "' anyPattern[" + std::to_string(alt) + "] passed.", true;
     }
-    return put("validation rule '" + m.name + "' passed.", buf, cap);
+    return *o = "validation rule '" + m.name + "' passed.", true;
   }
-  if (st != ST_FAIL) return -1;  // skip / error texts embed the reference's error strings
+  if (st != ST_FAIL) return false;  // skip / error texts embed the reference's error strings
   ensure_index(r);
   auto range = r->recidx.equal_range(((uint64_t)rule << 32) | res);
   std::vector<const FailRec*> recs;
   for (auto it = range.first; it != range.second; ++it) recs.push_back(&r->r.fails[it->second]);
   std::sort(recs.begin(), recs.end(), [](const FailRec* a, const FailRec* b2) { return a->alt < b2->alt; });
-  if (recs.empty()) return -1;
+  if (recs.empty()) return false;
   if (d.kind == RK_PATTERN) {
     std::string path = format_path(rs, b, recs[0]->tmpl, recs[0]->idx, recs[0]->key);
-    if (m.message.empty()) return put("validation error: rule " + m.name + " failed at path " + path, buf, cap);
+    if (m.message.empty()) return *o = "validation error: rule " + m.name + " failed at path " + path, true;
     std::string mm = m.message;
     if (mm.back() != '.') mm += ".";
-    return put("validation error: " + mm + " rule " + m.name + " failed at path " + path, buf, cap);
+    return *o = "validation error: " + mm + " rule " + m.name + " failed at path " + path, true;
   }
   std::string joined;
   for (size_t i = 0; i < recs.size(); i++) {
-    if (recs[i]->tmpl == NONE) return -1;  // "failed: <err>" needs the reference error text
+    if (recs[i]->tmpl == NONE) return false;  // "failed: <err>" needs the reference error text
     if (i) joined += " ";
     joined += "rule " + m.name + "[" + std::to_string(recs[i]->alt) + "] failed at path " +
               format_path(rs, b, recs[i]->tmpl, recs[i]->idx, recs[i]->key);
   }
-  if (m.message.empty()) return put("validation error: " + joined, buf, cap);
-  if (m.message.back() == '.') return put("validation error: " + m.message + " " + joined, buf, cap);
-  return put("validation error: " + m.message + ". " + joined, buf, cap);
+  if (m.message.empty()) return *o = "validation error: " + joined, true;
+  if (m.message.back() == '.') return *o = "validation error: " + m.message + " " + joined, true;
+  return *o = "validation error: " + m.message + ". " + joined, true;
+}
+
+int64_t kyv_results_message(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res, uint32_t rule,
+                            char* buf, size_t cap) {
+  auto* r = const_cast<kyv_results*>(cr);
+  if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
+  std::string m;
+  try {
+    if (!render_message(r, *crs->rs, *cb->b, (*r->inv)[res], rule, &m)) return -1;
+  } catch (std::exception& e) {
+    fail(KYV_EINTERNAL, e.what());
+    return -1;
+  }
+  return put(m, buf, cap);
 }
 
 int64_t kyv_results_failures(const kyv_results* r, kyv_failure* out, size_t cap) {
@@ -476,19 +498,74 @@ int64_t kyv_results_failures(const kyv_results* r, kyv_failure* out, size_t cap)
   return (int64_t)n;
 }
 
+// PatternError.Path of a single-pattern FAIL at kind-major position `res` ("" otherwise)
+static std::string render_path(kyv_results* r, const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule) {
+  // records exist for every failing alternative walked, also when a later anyPattern alternative passed
+  if ((r->r.status[(size_t)rule * r->r.nres + res] & 7) != ST_FAIL || rs.rules[rule].kind != RK_PATTERN) return "";
+  ensure_index(r);
+  auto it = r->recidx.find(((uint64_t)rule << 32) | res);
+  if (it == r->recidx.end()) return "";
+  const FailRec& f = r->r.fails[it->second];
+  return format_path(rs, b, f.tmpl, f.idx, f.key);
+}
+
 int64_t kyv_results_path(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t res, uint32_t rule,
                          char* buf, size_t cap) {
   auto* r = const_cast<kyv_results*>(cr);
   if (!r || !crs || !cb || rule >= r->r.nrules || res >= r->r.nres || r->r.status.empty()) return -1;
-  res = (*r->inv)[res];
-  // records exist for every failing alternative walked, also when a later anyPattern alternative passed
-  if ((r->r.status[(size_t)rule * r->r.nres + res] & 7) != ST_FAIL || crs->rs->rules[rule].kind != RK_PATTERN)
-    return put("", buf, cap);
-  ensure_index(r);
-  auto it = r->recidx.find(((uint64_t)rule << 32) | res);
-  if (it == r->recidx.end()) return put("", buf, cap);
-  const FailRec& f = r->r.fails[it->second];
-  return put(format_path(*crs->rs, *cb->b, f.tmpl, f.idx, f.key), buf, cap);
+  try {
+    return put(render_path(r, *crs->rs, *cb->b, (*r->inv)[res], rule), buf, cap);
+  } catch (std::exception& e) {
+    fail(KYV_EINTERNAL, e.what());
+    return -1;
+  }
+}
+
+int64_t kyv_results_texts(const kyv_results* cr, const kyv_ruleset* crs, const kyv_batch* cb, uint32_t rule, uint32_t res0,
+                          uint32_t nres, uint32_t status_mask, int32_t what, char* buf, size_t cap, int32_t* lens) {
+  auto* r = const_cast<kyv_results*>(cr);
+  if (!r || !crs || !cb || rule >= r->r.nrules || (what != KYV_TEXT_MESSAGE && what != KYV_TEXT_PATH))
+    return fail(KYV_EINVAL, "bad argument"), -1;
+  if ((uint64_t)res0 + nres > r->r.nres) return fail(KYV_ERANGE, "resource range out of bounds"), -1;
+  if (r->r.status.empty() && r->r.nres) return fail(KYV_ERANGE, "verdicts kept on the device"), -1;
+  try {
+    const Ruleset& rs = *crs->rs;
+    const Batch& b = *cb->b;
+    ensure_index(r);
+    // rendered per thread over contiguous slices, then packed in resource order
+    const int nt = std::max(1, std::min(hw_threads(0), (int)(nres / 4096) + 1));
+    std::vector<std::string> part(nt);
+    std::vector<int32_t> len(nres);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+      th.emplace_back([&, t]() {
+        const uint32_t lo = (uint32_t)((uint64_t)nres * t / nt), hi = (uint32_t)((uint64_t)nres * (t + 1) / nt);
+        std::string one;
+        for (uint32_t i = lo; i < hi; i++) {
+          const uint32_t pos = (*r->inv)[res0 + i];
+          const uint8_t st = r->r.status[(size_t)rule * r->r.nres + pos] & 7;
+          if (!((status_mask >> st) & 1u)) { len[i] = -2; continue; }
+          bool ok = true;
+          if (what == KYV_TEXT_PATH) one = render_path(r, rs, b, pos, rule);
+          else ok = render_message(r, rs, b, pos, rule, &one);
+          if (!ok || one.size() > (size_t)INT32_MAX) { len[i] = -1; continue; }
+          len[i] = (int32_t)one.size();
+          part[t] += one;
+        }
+      });
+    for (auto& x : th) x.join();
+    size_t total = 0;
+    for (auto& p : part) total += p.size();
+    if (lens) memcpy(lens, len.data(), (size_t)nres * sizeof(int32_t));
+    if (buf && cap >= total) {
+      size_t at = 0;
+      for (auto& p : part) { memcpy(buf + at, p.data(), p.size()); at += p.size(); }
+    }
+    return (int64_t)total;
+  } catch (std::exception& e) {
+    fail(KYV_EINTERNAL, e.what());
+    return -1;
+  }
 }
 
 int64_t kyv_results_fallback_reason(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,

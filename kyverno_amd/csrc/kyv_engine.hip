@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdlib>
 #include <mutex>
@@ -193,6 +194,7 @@ struct SliceSched {
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // after match, condition, walk, compaction (phase timing)
   int jit_state = -1;            // what the schedules were laid out for (0 interpreter only, 1 with the jit kernel)
 };
 
@@ -222,7 +224,10 @@ static void free_dev_results(DeviceResults& d, int dev) {
   dfree(d.view); dfree(d.status); dfree(d.pss_fails); dfree(d.pss_slot); dfree(d.recs); dfree(d.nrecs); dfree(d.counts);
   dfree(d.stage); dfree(d.rcnt); dfree(d.tsum);
   dfree(d.wl.items); dfree(d.wl.cnt);
-  for (auto& sl : d.slices) { dfree(sl.rbase); dfree(sl.mrules); dfree(sl.sched); }
+  for (auto& sl : d.slices) {
+    dfree(sl.rbase); dfree(sl.mrules); dfree(sl.sched);
+    for (auto e : sl.ev) if (e) hipEventDestroy(e);
+  }
   stream_put(dev, d.stream, d.e0, d.e1);
   d = DeviceResults();
 }
@@ -768,6 +773,15 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
   sl.jit_state = (int)jit;
 }
 
+// accumulate one slice's phase times (ms) from its events; `start`: the evaluation's start event (first slice), else
+// the phase-0 time of later slices is not separable from the previous slice's end and counts from its own ev[0]
+static void slice_phases(const SliceSched& sl, hipEvent_t start, double* phase) {
+  float t = 0;
+  if (start && hipEventElapsedTime(&t, start, sl.ev[0]) == hipSuccess) phase[0] += t;
+  for (int q = 0; q < 3; q++)
+    if (hipEventElapsedTime(&t, sl.ev[q], sl.ev[q + 1]) == hipSuccess) phase[q + 1] += t;
+}
+
 void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back,
               int jit_mode) {
   int ndev = 0;
@@ -895,10 +909,14 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   size_t lds = (size_t)depth * (sizeof(UFrame) + BLOCK * sizeof(LaneFrame));
   dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
   double total_ms = 0;
+  double phase[5] = {0, 0, 0, 0, 0};
+  for (auto& sl : d.slices)
+    for (auto& e : sl.ev) if (!e) HIP_OK(hipEventCreate(&e));
   int n = std::max(1, iters);
   std::vector<FailRec> host_recs;
   for (int it = 0; it < n; it++) {
     const bool collect = copy_back && out && it == n - 1;
+    const double sum_before = phase[0] + phase[1] + phase[2] + phase[3];
     host_recs.clear();
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.counts, 0, std::max<size_t>(1, nrules) * NSTATUS * 8, stream));
@@ -917,6 +935,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
                            (const uint32_t*)sl.mrules + sl.nm, sl.nmj);
       HIP_OK(hipGetLastError());
+      HIP_OK(hipEventRecord(sl.ev[0], stream));
       if (sl.nmc) {
         // compiled condition rules: grid.y strides over them (one rule per workgroup row by default: the waves of
         // a kind-major batch that no rule gates exit after one ballot)
@@ -937,6 +956,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
           HIP_OK(hipModuleLaunchKernel(dr->jcond, grid.x, gy, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
         }
       }
+      HIP_OK(hipEventRecord(sl.ev[1], stream));
       if (sl.grid[0]) {
         hipLaunchKernelGGL(walk_kernel, dim3(sl.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, sl.cm[0],
                            depth);
@@ -950,6 +970,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         void* args[] = {(void*)&vp, (void*)&o, (void*)&wl, (void*)&cmj};
         HIP_OK(hipModuleLaunchKernel(dr->jfns[cls - 1], sl.grid[cls], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
+      HIP_OK(hipEventRecord(sl.ev[2], stream));
       const size_t nchunks = nsr * (size_t)d.wl.nwaves;
       const uint32_t ntiles = (uint32_t)((nchunks + WAVE - 1) / WAVE);
       const RuleDesc* drules = (const RuleDesc*)(dr->base + dr->o_rules) + sl.k0;
@@ -958,6 +979,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, sl.rbase, d.rcnt, drules,
                          d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs);
       HIP_OK(hipGetLastError());
+      HIP_OK(hipEventRecord(sl.ev[3], stream));
+      if (multi) {  // phase times of this slice before its events are recorded again
+        HIP_OK(hipEventSynchronize(sl.ev[3]));
+        slice_phases(sl, &sl == &d.slices.front() ? d.e0 : nullptr, phase);
+      }
       if (collect && multi) {  // gather this slice's records before the next slice reuses the buffers
         uint32_t nr = 0;
         HIP_OK(hipMemcpyAsync(&nr, d.nrecs, 4, hipMemcpyDeviceToHost, stream));
@@ -979,6 +1005,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, d.e0, d.e1));
     total_ms += ms;
+    if (!multi && !d.slices.empty() && nres && d.slices[0].k1 > d.slices[0].k0) slice_phases(d.slices[0], d.e0, phase);
+    const double sum_after = phase[0] + phase[1] + phase[2] + phase[3];
+    phase[4] += std::max(0.0, ms - (sum_after - sum_before));  // the rest: verdict histogram (+ slice gaps)
   }
 #ifdef KYV_EXP_STEPS
   {
@@ -992,6 +1021,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     out->nres = (uint32_t)nres;
     out->nrules = (uint32_t)nrules;
     out->kernel_ms = total_ms / n;
+    for (int q = 0; q < 5; q++) out->phase_ms[q] = phase[q] / n;
     bool cond = false;
     for (auto& sl : d.slices) cond |= sl.nmc != 0;
     out->jit_used = (jit ? 1 : 0) | (jit && cond ? 2 : 0);
@@ -1055,7 +1085,14 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
   out->pss_fails.assign((size_t)npss * nres, 0);
   int T = std::max(1, threads);
   std::vector<std::vector<FailRec>> recs(T);
-  std::vector<uint64_t> bytes(T, 0);
+  std::vector<std::array<uint64_t, 5>> bytes(T, std::array<uint64_t, 5>{0, 0, 0, 0, 0});
+  // device phase that decides each rule's pairs (kyv_results_phase_ms order): pattern walks 2, condition rules with
+  // JMESPath operands / foreach 1 (the compiled condition kernel), the rest 0 (match kernel)
+  std::vector<uint8_t> rphase(nrules, 0);
+  for (size_t k = 0; k < nrules; k++) {
+    const RuleDesc& rd = rs.rules[k];
+    rphase[k] = (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) ? 2 : rule_needs_jmes(rs, rd) ? 1 : 0;
+  }
   std::vector<std::thread> th;
   for (int t = 0; t < T; t++)
     th.emplace_back([&, t]() {
@@ -1075,10 +1112,19 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
             g_touch = &acct;
           }
           const uint32_t* gate = v.gate + (size_t)v.hdr[r].kclass * v.gate_words;
-          uint8_t st = eval_pair(v, ((gate[k >> 5] >> (k & 31)) & 1u) != 0, (uint32_t)r, (uint32_t)k, wk, &pf, sink);
+          const bool gated = ((gate[k >> 5] >> (k & 31)) & 1u) != 0;
+          uint8_t st = eval_pair(v, gated, (uint32_t)r, (uint32_t)k, wk, &pf, sink);
           if (account) {
             g_touch = nullptr;
-            bytes[t] += 16 + 16 * acct.rows + 1 + (pss_slot[k] != NONE ? 4 : 0) + (uint64_t)sink.emitted * sizeof(FailRec);
+            auto& by = bytes[t];
+            by[4] += 1;  // the verdict histogram reads every status byte
+            if (!gated) {
+              by[0] += 1;  // kind-gated pair: only the verdict reset writes it (no header or row is read)
+            } else {
+              by[rphase[k]] += 16 + 16 * acct.rows + 1 + (pss_slot[k] != NONE ? 4 : 0) +
+                               (uint64_t)sink.emitted * sizeof(FailRec);
+              by[3] += 2 * (uint64_t)sink.emitted * sizeof(FailRec);  // compaction reads + writes each record
+            }
           }
           out->status[k * nres + r] = st;
           if (pss_slot[k] != NONE) out->pss_fails[(size_t)pss_slot[k] * nres + r] = pf;
@@ -1094,7 +1140,9 @@ void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool
   for (size_t k = 0; k < nrules; k++)
     for (int s = 0; s < NSTATUS; s++) out->counts[s] += out->rule_counts[k * NSTATUS + s];
   out->alg_bytes = 0;
-  for (auto x : bytes) out->alg_bytes += x;
+  for (int q = 0; q < 5; q++) out->alg_bytes_phase[q] = 0;
+  for (auto& x : bytes)
+    for (int q = 0; q < 5; q++) { out->alg_bytes += x[q]; out->alg_bytes_phase[q] += x[q]; }
 }
 
 // Reason a pair came back ST_FALLBACK (kyv_results_fallback_reason): the rule's compile-time reason, else the host

@@ -170,7 +170,12 @@ struct Results {
   int64_t counts[NSTATUS] = {0};
   std::vector<int64_t> rule_counts;  // [rule][status] (report summaries)
   double kernel_ms = 0, h2d_ms = 0, d2h_ms = 0;
+  // GPU evaluation split by phase (HIP events on the evaluation stream, averaged over the timed launches):
+  // [0] verdict resets + match_kernel(s), [1] compiled condition kernel, [2] pattern walk kernels,
+  // [3] failing-path compaction, [4] verdict histogram
+  double phase_ms[5] = {0, 0, 0, 0, 0};
   uint64_t alg_bytes = 0;           // CPU backend with KYV_EVAL_ACCOUNT_BYTES
+  uint64_t alg_bytes_phase[5] = {0, 0, 0, 0, 0};  // the same split by the device phase that moves them (phase_ms)
   int jit_used = 0;                 // bit 0: the runtime-compiled walk kernels ran; bit 1: the compiled condition kernel ran
 };
 

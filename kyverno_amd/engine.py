@@ -110,7 +110,14 @@ class Results:
         L = K.lib()
         self.counts = {K.STATUS_NAMES[s]: L.kyv_results_count(h, s) for s in range(8)}
         self.kernel_ms = L.kyv_results_kernel_ms(h)
+        ph = (ctypes.c_double * 5)()
+        L.kyv_results_phase_ms(h, ph, 5)
+        # match (incl. verdict resets), cond (compiled condition kernel), walk, compact, hist -- ms per launch
+        self.phase_ms = dict(zip(("match", "cond", "walk", "compact", "hist"), list(ph)))
         self.alg_bytes = L.kyv_results_alg_bytes(h)
+        ab = (ctypes.c_uint64 * 5)()
+        L.kyv_results_alg_bytes_phase(h, ab, 5)
+        self.alg_bytes_phase = dict(zip(("match", "cond", "walk", "compact", "hist"), list(ab)))
         ju = L.kyv_results_jit(h)
         self.jit = bool(ju & 1)          # runtime-compiled walk kernels ran
         self.jit_cond = bool(ju & 2)     # runtime-compiled condition kernel (deny / foreach rules) ran
@@ -141,6 +148,34 @@ class Results:
         buf = ctypes.create_string_buffer(4096)
         K.lib().kyv_results_path(self.h, self.ruleset.h, self.batch.h, res, rule, buf, len(buf))
         return buf.value.decode(errors="replace")
+
+    def texts(self, rule, what="message", statuses=(K.ST_FAIL,), res0=0, nres=None):
+        """RuleResponse.Message (what="message") or PatternError.Path (what="path") of rule `rule` for resources
+        [res0, res0 + nres) whose status is in `statuses`, rendered in one library call: list of bytes, None for a
+        pair whose text needs the CPU engine, and False for a pair whose status is not in `statuses`"""
+        L = K.lib()
+        nres = self.batch.n - res0 if nres is None else nres
+        mask = 0
+        for s in statuses:
+            mask |= 1 << s
+        w = {"message": K.TEXT_MESSAGE, "path": K.TEXT_PATH}[what]
+        lens = np.zeros(max(1, nres), dtype=np.int32)
+        total = L.kyv_results_texts(self.h, self.ruleset.h, self.batch.h, rule, res0, nres, mask, w, None, 0,
+                                    lens.ctypes.data)
+        if total < 0:
+            raise K.KyvError(L.kyv_last_error().decode(errors="replace"))
+        buf = np.zeros(max(1, total), dtype=np.uint8)
+        L.kyv_results_texts(self.h, self.ruleset.h, self.batch.h, rule, res0, nres, mask, w, buf.ctypes.data, total,
+                            lens.ctypes.data)
+        raw = buf.tobytes()
+        out, at = [], 0
+        for n in lens[:nres].tolist():
+            if n >= 0:
+                out.append(raw[at:at + n])
+                at += n
+            else:
+                out.append(None if n == -1 else False)
+        return out
 
     def failures(self):
         """compacted failing-path records as a structured numpy array (res in input order, rule, alt,

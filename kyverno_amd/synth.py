@@ -279,12 +279,16 @@ def _chunk(args):
     return ("\n".join(json.dumps(make(start + i), separators=(",", ":")) for i in range(n)) + "\n").encode()
 
 
-def corpus_ndjson(n, kind="mixed", seed=SEED, edge=False, workers=None, chunk=20000):
+def corpus_ndjson(n, kind="mixed", seed=SEED, edge=False, workers=None, chunk=20000, start=0):
     """Large seeded corpus as NDJSON bytes, generated in parallel chunks (resource names stay unique:
-    the chunk's first index is part of every name). Returns (bytes, namespace labels)."""
+    the chunk's first index is part of every name). Returns (bytes, namespace labels).
+    start: generate resources [start, start + n) of the corpus seeded `seed` (start a multiple of `chunk`): a rank's
+    shard of one corpus, byte-identical to that slice of the whole corpus whatever the number of shards."""
     import multiprocessing as mp
     import os
-    jobs = [(kind, seed, s, min(chunk, n - s), edge) for s in range(0, n, chunk)]
+    if start % chunk:
+        raise ValueError("corpus shard start must be a multiple of the chunk size")
+    jobs = [(kind, seed, s, min(chunk, start + n - s), edge) for s in range(start, start + n, chunk)]
     workers = workers or min(len(jobs), int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1, 16)
     if workers <= 1 or len(jobs) == 1:
         parts = [_chunk(j) for j in jobs]
@@ -298,20 +302,20 @@ def corpus_ndjson(n, kind="mixed", seed=SEED, edge=False, workers=None, chunk=20
     return b"".join(parts), Gen(seed).ns_labels()
 
 
-def cached_corpus(n, kind="mixed", seed=SEED, edge=False, cache_dir=None):
+def cached_corpus(n, kind="mixed", seed=SEED, edge=False, cache_dir=None, start=0):
     """corpus_ndjson with an optional on-disk cache (KYV_CORPUS_CACHE): profiler runs reuse the corpus a
     plain run generated, so no worker processes are forked under the profiler."""
     import os
     cache_dir = cache_dir or os.environ.get("KYV_CORPUS_CACHE")
     if not cache_dir:
-        return corpus_ndjson(n, kind=kind, seed=seed, edge=edge)
-    base = os.path.join(cache_dir, "corpus_%s_%d_%x_%d" % (kind, n, seed, int(edge)))
+        return corpus_ndjson(n, kind=kind, seed=seed, edge=edge, start=start)
+    base = os.path.join(cache_dir, "corpus_%s_%d_%x_%d_%d" % (kind, n, seed, int(edge), start))
     if os.path.exists(base + ".ndjson") and os.path.exists(base + ".nsl.json"):
         with open(base + ".ndjson", "rb") as f:
             data = f.read()
         with open(base + ".nsl.json") as f:
             return data, json.load(f)
-    data, nsl = corpus_ndjson(n, kind=kind, seed=seed, edge=edge)
+    data, nsl = corpus_ndjson(n, kind=kind, seed=seed, edge=edge, start=start)
     os.makedirs(cache_dir, exist_ok=True)
     with open(base + ".ndjson.tmp", "wb") as f:
         f.write(data)

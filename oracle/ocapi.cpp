@@ -1,6 +1,8 @@
 // ORACLE — test infrastructure only (see ojson.h header). C entry points for ctypes (oracle/oracle.py).
 // Every function returns a malloc'ed JSON string (free with oracle_free) or an int.
+#include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <cstring>
 
 #include "goutil.h"
@@ -297,9 +299,24 @@ extern "C" char* oracle_validate_matrix(const char* policies_json, const char* r
 
 // Same, timing the per-(resource, policy) loop only (policies compiled and resources decoded before the clock, as in
 // oracle_validate_batch): the bench's CPU baseline, whose verdicts are then compared with the device's.
+extern "C" char* oracle_validate_matrix_x(const char* policies_json, const char* resources_json,
+                                          const char* nslabels_json, int nthreads, unsigned char* out, long long out_len,
+                                          double* seconds, unsigned text_mask, char** texts, long long* texts_len);
 extern "C" char* oracle_validate_matrix_t(const char* policies_json, const char* resources_json,
                                           const char* nslabels_json, int nthreads, unsigned char* out, long long out_len,
                                           double* seconds) {
+  return oracle_validate_matrix_x(policies_json, resources_json, nslabels_json, nthreads, out, out_len, seconds, 0,
+                                  nullptr, nullptr);
+}
+
+// Same, also returning the texts of the pairs whose matrix code c has bit c set in text_mask: a malloc'ed buffer
+// (*texts, *texts_len bytes; free with oracle_free) of records in (rule, resource) order
+//   u64 rule * nres + res | u32 flags (bit 0 message_unpinned) | u32 path length | u32 message length | path | message
+// where path = RuleResponse's failing PatternError.Path (single patterns) and message = RuleResponse.Message: the
+// parity tests compare the device's failing paths and messages pair by pair at scale.
+extern "C" char* oracle_validate_matrix_x(const char* policies_json, const char* resources_json,
+                                          const char* nslabels_json, int nthreads, unsigned char* out, long long out_len,
+                                          double* seconds, unsigned text_mask, char** texts, long long* texts_len) {
   try {
     VP pols = oj::parse(policies_json, true);
     VP res = oj::parse(resources_json, false);
@@ -336,8 +353,13 @@ extern "C" char* oracle_validate_matrix_t(const char* policies_json, const char*
     if ((long long)(nrules * n) > out_len) return nullptr;
     std::fill(out, out + nrules * n, (unsigned char)0);
     std::atomic<size_t> next{0};
+    struct Text { uint64_t at; uint32_t flags; std::string path, msg; };
+    std::mutex tmu;
+    std::vector<Text> all_texts;
+    const bool want_texts = texts && texts_len && text_mask;
     auto t0 = std::chrono::steady_clock::now();
     auto work = [&]() {
+      std::vector<Text> mine;
       while (true) {
         size_t i = next.fetch_add(16);
         if (i >= n) break;
@@ -354,15 +376,40 @@ extern "C" char* oracle_validate_matrix_t(const char* policies_json, const char*
                               : rr.status == "error" ? 4 : rr.status == "panic" ? 5 : 6;
               if (rr.nondeterministic && c != 6) c = 7;
               out[f->second * n + k] = c;
+              if (want_texts && ((text_mask >> c) & 1u))
+                mine.push_back(Text{(uint64_t)f->second * n + k, rr.message_unpinned ? 1u : 0u, rr.path, rr.message});
             }
           }
         }
+      }
+      if (want_texts) {
+        std::lock_guard<std::mutex> g(tmu);
+        for (auto& t : mine) all_texts.push_back(std::move(t));
       }
     };
     std::vector<std::thread> th;
     for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(work);
     for (auto& t : th) t.join();
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (want_texts) {
+      std::sort(all_texts.begin(), all_texts.end(), [](const Text& a, const Text& b) { return a.at < b.at; });
+      size_t total = 0;
+      for (auto& t : all_texts) total += 20 + t.path.size() + t.msg.size();
+      char* buf = (char*)malloc(std::max<size_t>(1, total));
+      size_t at = 0;
+      for (auto& t : all_texts) {
+        uint32_t pl = (uint32_t)t.path.size(), ml = (uint32_t)t.msg.size();
+        memcpy(buf + at, &t.at, 8);
+        memcpy(buf + at + 8, &t.flags, 4);
+        memcpy(buf + at + 12, &pl, 4);
+        memcpy(buf + at + 16, &ml, 4);
+        memcpy(buf + at + 20, t.path.data(), pl);
+        memcpy(buf + at + 20 + pl, t.msg.data(), ml);
+        at += 20 + pl + ml;
+      }
+      *texts = buf;
+      *texts_len = (long long)total;
+    }
     return dup(oj::dump(names));
   } catch (std::exception&) {
     return nullptr;

@@ -38,6 +38,11 @@ def lib():
         L.oracle_validate_matrix_t.restype = ctypes.c_void_p
         L.oracle_validate_matrix_t.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                                ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_validate_matrix_x.restype = ctypes.c_void_p
+        L.oracle_validate_matrix_x.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_double),
+                                               ctypes.c_uint, ctypes.POINTER(ctypes.c_void_p),
+                                               ctypes.POINTER(ctypes.c_longlong)]
         L.oracle_refs.restype = ctypes.c_void_p
         L.oracle_refs.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.oracle_anchor_probe.restype = ctypes.c_void_p
@@ -159,9 +164,10 @@ def validate_batch(policies, resources, ns_labels=None, threads=1):
 MATRIX_STATUS = ("none", "pass", "fail", "skip", "error", "panic", "unsupported", "nondeterministic")
 
 
-def validate_matrix(policies, resources, ns_labels=None, threads=8, nres=None, timed=False):
+def validate_matrix(policies, resources, ns_labels=None, threads=8, nres=None, timed=False, texts=()):
     """-> (names [(policy, rule)], uint8 array [rule, resource] of MATRIX_STATUS codes)[, seconds of the timed loop]
-    resources: list of dicts, or JSON array text / bytes (then pass nres)."""
+    [, texts]. resources: list of dicts, or JSON array text / bytes (then pass nres). texts: MATRIX_STATUS names whose
+    pairs' failing path and message are returned as {(rule row, resource): (path, message, message_unpinned)}."""
     import numpy as np
     pj, rj = _s(policies), _s(resources)
     n = len(resources) if nres is None else nres
@@ -169,10 +175,31 @@ def validate_matrix(policies, resources, ns_labels=None, threads=8, nres=None, t
     cap = 3 * sum(len((p.get("spec") or {}).get("rules") or []) for p in policies) + 1
     out = np.zeros(cap * max(1, n), dtype=np.uint8)
     secs = ctypes.c_double(0)
-    ptr = lib().oracle_validate_matrix_t(pj, rj, _s(ns_labels) if ns_labels else b"", threads,
-                                         out.ctypes.data, out.size, ctypes.byref(secs))
+    mask = 0
+    for t in texts:
+        mask |= 1 << MATRIX_STATUS.index(t)
+    tp, tl = ctypes.c_void_p(), ctypes.c_longlong(0)
+    ptr = lib().oracle_validate_matrix_x(pj, rj, _s(ns_labels) if ns_labels else b"", threads,
+                                         out.ctypes.data, out.size, ctypes.byref(secs), mask, ctypes.byref(tp),
+                                         ctypes.byref(tl))
     if not ptr:
         raise ValueError("oracle_validate_matrix failed")
     names = [tuple(x) for x in json.loads(_take(ptr))]
     m = out[: len(names) * n].reshape(len(names), n)
-    return (names, m, secs.value) if timed else (names, m)
+    ret = [names, m]
+    if timed:
+        ret.append(secs.value)
+    if texts:
+        tx = {}
+        if tp.value:
+            raw = ctypes.string_at(tp.value, tl.value)
+            lib().oracle_free(tp.value)
+            at, size = 0, len(raw)
+            import struct
+            while at < size:
+                pos, flags, pl, ml = struct.unpack_from("<QIII", raw, at)
+                at += 20
+                tx[divmod(pos, n)] = (raw[at:at + pl], raw[at + pl:at + pl + ml], bool(flags & 1))
+                at += pl + ml
+        ret.append(tx)
+    return tuple(ret)

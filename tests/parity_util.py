@@ -82,22 +82,23 @@ _MATRIX_TO_DEVICE = {0: K.ST_NONE, 1: K.ST_PASS, 2: K.ST_FAIL, 3: K.ST_SKIP, 4: 
                      6: K.ST_FALLBACK, 7: K.ST_ND}
 
 
-def compare_matrix(policies, resources, ns_labels=None, backend="gpu", jit=None, threads=8):
-    """Status-level parity at scale: every (resource, rule) verdict of the device vs the oracle's verdict matrix
-    (oracle.validate_matrix). resources: list of dicts, or NDJSON bytes (one resource per line). Nondeterministic
-    pairs (either side) are excluded from the count. Returns (stats, results); stats["nbad"] counts mismatching
-    pairs."""
+def compare_matrix(policies, resources, ns_labels=None, backend="gpu", jit=None, threads=8, texts=True):
+    """Parity at scale: every (resource, rule) verdict of the device vs the oracle's verdict matrix
+    (oracle.validate_matrix) and, with texts, the failing path and message of every FAIL pair (compare_fail_texts).
+    resources: list of dicts, or NDJSON bytes (one resource per line). Nondeterministic pairs (either side) are
+    excluded from the count. Returns (stats, results); stats["nbad"] counts mismatching pairs and texts."""
     import numpy as np
     rs = E.Ruleset(policies)
     b = E.Batch(rs, resources, ns_labels)
     res = E.evaluate(rs, b, backend=backend, **({} if backend != "gpu" else {"jit": jit}))
     if isinstance(resources, (bytes, bytearray)):
         lines = [x for x in bytes(resources).split(b"\n") if x.strip()]
-        names, m = O.validate_matrix(policies, b"[" + b",".join(lines) + b"]", ns_labels, threads=threads,
-                                     nres=len(lines))
+        names, m, *tx = O.validate_matrix(policies, b"[" + b",".join(lines) + b"]", ns_labels, threads=threads,
+                                          nres=len(lines), texts=("fail",) if texts else ())
         resources = lines
     else:
-        names, m = O.validate_matrix(policies, resources, ns_labels, threads=threads)
+        names, m, *tx = O.validate_matrix(policies, resources, ns_labels, threads=threads,
+                                          texts=("fail",) if texts else ())
     row = {nm: i for i, nm in enumerate(names)}
     lut = np.array([_MATRIX_TO_DEVICE[i] for i in range(8)], dtype=np.uint8)
     st = np.asarray(res.status)
@@ -115,15 +116,21 @@ def compare_matrix(policies, resources, ns_labels=None, backend="gpu", jit=None,
             bad.append((key, int(ri), K.STATUS_NAMES[got[ri]], K.STATUS_NAMES[want[ri]]))
     stats = {"pairs": len(rs.rules) * len(resources), "compared": compared, "matched": matched, "nd": nd,
              "nbad": len(bad), "bad": bad[:20], "rules": len(rs.rules)}
+    if texts:
+        ts = compare_fail_texts(rs, res, names, tx[0], len(resources))
+        stats["texts"] = ts
+        stats["nbad"] += ts["nbad"]
+        stats["bad"] += ts["bad"][:10]
     return stats, res
 
 
-def compare_status_sample(rs, res, policies, docs, ns_labels, idx, threads=8):
-    """Status parity of the device verdicts `res` (whole batch `docs`) on the resources at positions `idx` against
-    the oracle's verdict matrix of those resources alone. Returns a stats dict like compare_matrix."""
+def compare_status_sample(rs, res, policies, docs, ns_labels, idx, threads=8, texts=True):
+    """Parity of the device verdicts `res` (whole batch `docs`) on the resources at positions `idx` against the
+    oracle's verdict matrix of those resources alone, with the failing paths / messages of every FAIL pair (texts).
+    Returns a stats dict like compare_matrix."""
     import numpy as np
     sub = [docs[i] for i in idx]
-    names, m = O.validate_matrix(policies, sub, ns_labels, threads=threads)
+    names, m, *tx = O.validate_matrix(policies, sub, ns_labels, threads=threads, texts=("fail",) if texts else ())
     row = {nm: i for i, nm in enumerate(names)}
     lut = np.array([_MATRIX_TO_DEVICE[i] for i in range(8)], dtype=np.uint8)
     st = np.asarray(res.status)[:, np.asarray(idx)]
@@ -139,5 +146,59 @@ def compare_status_sample(rs, res, policies, docs, ns_labels, idx, threads=8):
         compared += len(idx) - int(ndm.sum())
         for ri in diff[:3]:
             bad.append((key, int(idx[ri]), K.STATUS_NAMES[got[ri]], K.STATUS_NAMES[want[ri]]))
-    return {"pairs": len(rs.rules) * len(idx), "compared": compared, "matched": matched, "nd": nd,
-            "nbad": len(bad), "bad": bad[:20], "rules": len(rs.rules)}
+    stats = {"pairs": len(rs.rules) * len(idx), "compared": compared, "matched": matched, "nd": nd,
+             "nbad": len(bad), "bad": bad[:20], "rules": len(rs.rules)}
+    if texts:
+        ts = compare_fail_texts(rs, res, names, tx[0], len(idx), idx=idx)
+        stats["texts"] = ts
+        stats["nbad"] += ts["nbad"]
+        stats["bad"] += ts["bad"][:10]
+    return stats
+
+
+def compare_fail_texts(rs, res, names, tx, nres, idx=None):
+    """Failing-path and message parity of every FAIL pair: the device's PatternError.Path (single patterns) and
+    RuleResponse.Message, rendered in bulk by kyv_results_texts, against the oracle's (validate_matrix(...,
+    texts=("fail",))). idx: resource positions of the device batch that the oracle's columns 0..nres-1 stand for
+    (default: the first nres). Returns a stats dict; stats["nbad"] counts path + message mismatches."""
+    import numpy as np
+    row = {nm: i for i, nm in enumerate(names)}
+    idx = np.arange(nres) if idx is None else np.asarray(idx)
+    st = {"fail_pairs": 0, "paths_compared": 0, "path_mismatches": 0, "messages_compared": 0,
+          "message_mismatches": 0, "messages_unrenderable": 0, "oracle_missing": 0, "bad": []}
+    status = np.asarray(res.status)
+    for k, rule in enumerate(rs.rules):
+        key = (rs.policies[rule["policy"]]["name"], rule["name"])
+        fails = np.nonzero(status[k, idx] == K.ST_FAIL)[0]
+        if not len(fails) or key not in row:
+            continue
+        r = row[key]
+        lo, hi = int(idx[fails[0]]), int(idx[fails[-1]]) + 1
+        msgs = res.texts(k, "message", (K.ST_FAIL,), res0=lo, nres=hi - lo)
+        paths = res.texts(k, "path", (K.ST_FAIL,), res0=lo, nres=hi - lo) if rule["kind"] == "pattern" else None
+        for j in fails.tolist():
+            st["fail_pairs"] += 1
+            o = tx.get((r, j))
+            if o is None:
+                st["oracle_missing"] += 1
+                if len(st["bad"]) < 20:
+                    st["bad"].append(("oracle has no fail text", key, j))
+                continue
+            opath, omsg, unpinned = o
+            d = int(idx[j]) - lo
+            if paths is not None:
+                st["paths_compared"] += 1
+                if paths[d] != opath:
+                    st["path_mismatches"] += 1
+                    if len(st["bad"]) < 20:
+                        st["bad"].append(("path", key, j, paths[d], opath))
+            if msgs[d] is None:
+                st["messages_unrenderable"] += 1
+            elif not unpinned:
+                st["messages_compared"] += 1
+                if msgs[d] != omsg:
+                    st["message_mismatches"] += 1
+                    if len(st["bad"]) < 20:
+                        st["bad"].append(("message", key, j, msgs[d][:200], omsg[:200]))
+    st["nbad"] = st["path_mismatches"] + st["message_mismatches"] + st["oracle_missing"]
+    return st

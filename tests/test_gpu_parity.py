@@ -74,7 +74,8 @@ def _oracle_threads():
 
 def test_c3_oracle_matrix_at_scale_jit():
     """configs[2] at scale through the production path (runtime-compiled walk, chosen automatically at this size):
-    every verdict of 200k mixed resources x the C3 rules against the oracle's verdict matrix"""
+    every verdict of 200k mixed resources x the C3 rules against the oracle's verdict matrix, and the failing path
+    (single patterns) and RuleResponse.Message of every one of the ~1M FAIL pairs against the oracle's texts"""
     import parity_util as PU
     data, nsl = synth.corpus_ndjson(200_000, seed=52, edge=True)
     st, res = PU.compare_matrix(cases.best_practices() + cases.chart_restricted(), data, nsl, backend="gpu",
@@ -82,6 +83,10 @@ def test_c3_oracle_matrix_at_scale_jit():
     assert res.jit
     assert st["nbad"] == 0, st["bad"]
     assert st["compared"] >= 200_000 * 80 and st["matched"] > 1_000_000
+    t = st["texts"]
+    print("C3 200k text parity:", {k: v for k, v in t.items() if k != "bad"})
+    assert t["fail_pairs"] > 500_000 and t["paths_compared"] > 200_000
+    assert t["messages_compared"] == t["fail_pairs"]
 
 
 def test_c2_oracle_matrix_at_scale():
@@ -191,11 +196,13 @@ def test_c4_at_scale_gpu():
     rs = E.Ruleset(pols)
     b = E.Batch(rs, docs, nsl)
     res = E.evaluate(rs, b, backend="gpu")
+    assert res.jit  # the production walk at this size (timed by bench --workload c4)
     assert sum(res.counts.values()) == len(rs.rules) * b.n
     idx = np.linspace(0, b.n - 1, 1500).astype(int)
     st = PU.compare_status_sample(rs, res, pols, docs, nsl, idx, threads=_oracle_threads())
     assert st["nbad"] == 0, st["bad"]
     assert st["matched"] > 100_000
+    assert st["texts"]["paths_compared"] > 1000
 
 
 def test_condition_goldens_gpu():
