@@ -2164,6 +2164,64 @@ void assign_glob_masks(Ruleset& rs) {
     for (unsigned char ch : x) if (ch >= 0x80) globby = true;
     if (globby) add(s);
   }
+  assign_cond_sets(rs);
+}
+
+// Condition-set masks: an AnyIn / AllIn / AnyNotIn / AllNotIn (or In / NotIn with a scalar key) condition with one
+// literal side and one JMESPath side asks, per element of the resource-side list, "does wild2(element, e) hold for
+// some literal element e" (op_any_all / key_exists, kyv_cond.h; anyin.go:115-180, in.go:52-86). That predicate depends
+// on the element's string only, so the device evaluates it once per dictionary string (gmask_kernel, mask bit
+// gpats.size() + set index) and the compiled condition kernel streams the list with one mask load per element
+// instead of materialising it (jit.cpp CondGen). Only sets whose literal elements all have a fmt.Sprint form are
+// used (a literal the device cannot render makes the operator fall back, which the set cannot express).
+static uint32_t lit_sprint(const Ruleset& rs, const Node& n) {
+  switch (node_type(n)) {
+    case N_NULL: return KSID(NIL_STR);
+    case N_FALSE: return SID_FALSE;
+    case N_TRUE: return SID_TRUE;
+    case N_INT: case N_FLOAT: return n.c;
+    case N_STR: return n.a;
+    default: return NONE;
+  }
+}
+void assign_cond_sets(Ruleset& rs) {
+  rs.gsets.clear();
+  rs.cond_set.assign(rs.conds.size(), 0);
+  std::map<std::vector<uint32_t>, uint32_t> seen;
+  for (size_t ci = 0; ci < rs.conds.size(); ci++) {
+    const Cond& c = rs.conds[ci];
+    const bool anyall = c.op == CO_ANYIN || c.op == CO_ALLIN || c.op == CO_ANYNOTIN || c.op == CO_ALLNOTIN;
+    const bool in = c.op == CO_IN || c.op == CO_NOTIN;
+    std::vector<uint32_t> set;
+    if (anyall && c.key.kind == OK_JMES && c.value.kind == OK_LIT && node_type(rs.cnodes[c.value.a]) == N_ARR) {
+      // shape A: resource-side key list, literal value list
+      const Node& a = rs.cnodes[c.value.a];
+      bool ok = true;
+      for (uint32_t j = 0; j < a.b && ok; j++) {
+        const uint32_t s = lit_sprint(rs, rs.cnodes[a.a + j]);
+        if (s == NONE) ok = false; else set.push_back(s);
+      }
+      if (!ok) continue;
+    } else if ((anyall || in) && c.key.kind == OK_LIT && c.value.kind == OK_JMES) {
+      // shape B: literal scalar key, resource-side value list
+      const Node& k = rs.cnodes[c.key.a];
+      if (node_type(k) != N_STR && node_type(k) != N_INT && node_type(k) != N_FLOAT) continue;
+      const uint32_t s = lit_sprint(rs, k);
+      if (s == NONE) continue;
+      set.push_back(s);
+    } else {
+      continue;
+    }
+    std::sort(set.begin(), set.end());
+    set.erase(std::unique(set.begin(), set.end()), set.end());
+    auto it = seen.find(set);
+    if (it == seen.end()) {
+      if (rs.gpats.size() + rs.gsets.size() >= MAX_GMASK) continue;
+      it = seen.emplace(set, (uint32_t)rs.gsets.size()).first;
+      rs.gsets.push_back(set);
+    }
+    rs.cond_set[ci] = it->second + 1;
+  }
 }
 
 void build_path_trie(Ruleset& rs) {

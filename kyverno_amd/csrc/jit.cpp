@@ -493,6 +493,8 @@ struct CondGen {
   bool ok = true;
   uint32_t uid = 0;
   uint32_t nslots = 1;      // LDS lists per lane the generated programs need (1 or 2)
+  bool lds_used = false;    // some operand materialises its list in LDS
+  uint32_t cur_etpos = NONE;  // element trie position of the program being generated (stream_cond)
   std::unordered_map<uint64_t, std::string> progs;  // (program, element trie position) -> function name
 
   explicit CondGen(const Ruleset& r) : rs(r) {}
@@ -565,9 +567,23 @@ struct CondGen {
   // gen(pos, x, list, proj): ops [pos, end) applied to value x in single (list=false) or list mode
   const uint32_t* P = nullptr;
   uint32_t PN = 0, PEND = 0;
+  // streaming mode (condition-set operands, stream_fn): list elements are not materialised; each element's
+  // fmt.Sprint sid goes through `sacc` (the condition's per-element test) and only the count is kept
+  bool streaming = false;
+  std::string sacc;
   void jend(const V& x, bool list, bool proj) {
     if (!list) {
       out << "  *cur = " << (x.key ? "(" + x.i + " | JMES_KEYBIT)" : x.i) << ";\n";
+      return;
+    }
+    if (streaming) {
+      std::string sx;
+      if (x.key) sx = "(gtk(R + " + x.i + ") >> 4)";
+      else sx = "jc_sprint(R, " + x.i + ", " + x.t + ", " + x.a + ")";
+      const std::string body = "{ const uint32_t es = " + sx + ";\n    if (++*ln > JCAP) return JS_FB;\n    " + sacc + " }";
+      if (x.key) out << "  " << body << "\n";
+      else if (proj) out << "  if (" << x.i << " != NONE) " << body << "\n";
+      else out << "  " << body << "\n";
       return;
     }
     const std::string e = x.key ? "jc_keyent(R, " + x.i + ")" : "jc_ent(" + x.i + ", " + x.t + ", " + x.a + ")";
@@ -723,6 +739,109 @@ struct CondGen {
     PEND = savePEND;
     return name;
   }
+  // Streaming operand function of a condition-set condition (compiler.cpp assign_cond_sets): the same program as
+  // operand_fn, but list elements only update the caller's accumulators through `acc` (shape A: *sf = 1 on an element
+  // without fmt.Sprint form, else *sm counts the elements in the set; shape B: the first element that is unrenderable
+  // (*sf = 2) or in the set (*sf = 1) decides, as key_exists' ordered loop does). Single (non-list) results and the
+  // `|| literal` come back as operand_fn returns them.
+  //   int jsN(v, R, r, element value, &lst, &cur, &ln, &lit, &sm, &sf) -> JS_OK / JS_FB / JS_NOTFOUND
+  std::string stream_fn(const CondOperand& o, uint32_t etpos, const std::string& acc) {
+    const uint32_t* p = rs.pool.data() + o.a;
+    const uint32_t n = o.nseg, root = p[0] & 0xFFu;
+    if (root == JR_OPERATION || (p[0] & JF_PURE)) return "";  // never a list
+    const std::string name = fresh("js");
+    const uint32_t* saveP = P;
+    const uint32_t savePEND = PEND;
+    std::ostringstream save;
+    save.swap(out);
+    out << "static __device__ __forceinline__ int " << name
+        << "(const View& v, const Node* R, uint32_t r, uint32_t ei, uint32_t et, uint32_t ea, uint32_t erow, "
+           "bool* lst, uint32_t* cur, uint32_t* ln, uint32_t* lit, uint32_t* sm, uint32_t* sf) {\n"
+           "  *lst = false; *cur = NONE; *ln = 0u; *lit = NONE; (void)sm; (void)sf;\n";
+    V x = root == JR_OBJECT ? decl("0u", "T_UNK", "0u", "r", 0u, false) : decl("ei", "et", "ea", "erow", etpos, false);
+    uint32_t orlit = NONE;
+    PEND = n;
+    for (uint32_t q = 1; q < n;) {
+      if (p[q] == JO_OR) { PEND = q; orlit = p[q + 1]; break; }
+      q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
+    }
+    P = p;
+    const bool su = unroll, ss = streaming;
+    const std::string sa = sacc;
+    unroll = true;
+    streaming = true;
+    sacc = acc;
+    jgen(1, x, false, false, 0);
+    unroll = su;
+    streaming = ss;
+    sacc = sa;
+    if (orlit != NONE)
+      out << "  if (*lst ? *ln == 0u : jc_false1(R, *cur)) { *lst = false; *cur = NONE; *lit = " << u(orlit) << "; }\n";
+    out << "  return JS_OK;\n}\n";
+    std::string fn = out.str();
+    out.swap(save);
+    P = saveP;
+    PEND = savePEND;
+    if (!ok) return "";
+    defs << fn;
+    return name;
+  }
+  // the set of a condition-set condition as a device constant (the mask-less fallback of jc_inset)
+  std::unordered_map<uint32_t, std::string> set_names;
+  std::string set_array(uint32_t q) {
+    auto it = set_names.find(q);
+    if (it != set_names.end()) return it->second;
+    std::string nm = "kyv_cset" + std::to_string(q);
+    defs << "__device__ const uint32_t " << nm << "[" << rs.gsets[q].size() << "] = {";
+    for (size_t i = 0; i < rs.gsets[q].size(); i++) defs << (i ? ", " : "") << rs.gsets[q][i] << "u";
+    defs << "};\n";
+    set_names[q] = nm;
+    return nm;
+  }
+  // a single-condition program whose condition has a set (compiler.cpp assign_cond_sets): the list side streamed
+  // (stream_fn), decided from the accumulators when it is a list, else by the operator on the single value / literal
+  bool stream_cond(uint32_t ci, const std::string& K, const std::string& X) {
+    if (ci >= rs.cond_set.size() || !rs.cond_set[ci] || getenv("KYV_JIT_NOSTREAM")) return false;
+    const Cond& c = rs.conds[ci];
+    const uint32_t q = rs.cond_set[ci] - 1;
+    const uint32_t bit = (uint32_t)rs.gpats.size() + q;
+    const bool shapeA = c.key.kind == OK_JMES && c.value.kind == OK_LIT;
+    const CondOperand& lo = shapeA ? c.key : c.value;  // the resource-side (listy) operand
+    const std::string S = set_array(q);
+    const std::string test = "jc_inset(v, " + u(bit) + ", " + S + ", " + u((uint32_t)rs.gsets[q].size()) + ", es)";
+    const std::string acc = shapeA ? "if (es == NONE) *sf = 1u; else if (" + test + ") (*sm)++;"
+                                   : "if (!*sf) { if (es == NONE) *sf = 2u; else if (" + test + ") *sf = 1u; }";
+    const std::string f = stream_fn(lo, cur_etpos, acc);
+    if (f.empty()) return false;
+    const std::string l = fresh("jl"), cc = fresh("jc"), n = fresh("jn"), t = fresh("jt"), s = fresh("js"), m = fresh("sm"),
+                      fb = fresh("sf");
+    out << "  bool " << l << "; uint32_t " << cc << ", " << n << ", " << t << ", " << m << " = 0u, " << fb << " = 0u;\n"
+        << "  const int " << s << " = " << f << "(v, R, r, ei, et, ea, erow, &" << l << ", &" << cc << ", &" << n << ", &" << t
+        << ", &" << m << ", &" << fb << ");\n"
+        << "  if (" << s << " == JS_FB) return CR_FB;\n  if (" << s << " == JS_NOTFOUND) return CP_ERROR;\n"
+        << "  if (" << l << ") {\n";
+    if (shapeA) {
+      std::string dec;
+      switch (c.op) {
+        case CO_ANYIN: dec = m + " > 0u"; break;
+        case CO_ANYNOTIN: dec = m + " < " + n; break;
+        case CO_ALLIN: dec = m + " == " + n; break;
+        default: dec = m + " == 0u"; break;  // CO_ALLNOTIN
+      }
+      out << "    rc = " << fb << " ? CR_FB : (" << dec << ") ? CR_TRUE : CR_FALSE;\n";
+    } else {
+      const bool neg = c.op == CO_NOTIN || c.op == CO_ANYNOTIN || c.op == CO_ALLNOTIN;
+      out << "    rc = " << fb << " == 2u ? CR_FB : ((" << fb << " == 1u) != " << (neg ? "true" : "false")
+          << ") ? CR_TRUE : CR_FALSE;\n";
+    }
+    out << "  } else {\n";
+    const std::string one = "jc_cv(v, R, false, " + cc + ", " + t + ", nullptr, 0u)";
+    if (shapeA) out << "    const CV " << K << " = " << one << ";\n    const CV " << X << " = jc_lit(v, " << u(c.value.a) << ");\n";
+    else out << "    const CV " << K << " = jc_lit(v, " << u(c.key.a) << ");\n    const CV " << X << " = " << one << ";\n";
+    out << "    rc = " << cond_call(ci, K, X) << ";\n  }\n";
+    return true;
+  }
+
   // an operand that cannot fail (no NotFoundError, no list overflow / keys() error)
   bool infallible(const CondOperand& o) const {
     if (o.kind == OK_LIT || o.kind == OK_NIL) return true;
@@ -763,6 +882,7 @@ struct CondGen {
         return;
       }
       case OK_JMES: {
+        lds_used = true;
         const std::string f = operand_fn(o, etpos);
         const std::string l = fresh("jl"), c = fresh("jc"), n = fresh("jn"), t = fresh("jt"), s = fresh("js");
         out << "  bool " << l << "; uint32_t " << c << ", " << n << ", " << t << ";\n"
@@ -821,6 +941,12 @@ struct CondGen {
       const Cond& c = rs.conds[ci];
       const bool two = listy(rs, c.key) && listy(rs, c.value);
       const std::string K = fresh("k"), X = fresh("x");
+      if (check && !two) {
+        cur_etpos = etpos;
+        const std::string mark = out.str();
+        if (stream_cond(ci, K, X)) return;
+        out.str(""); out.clear(); out << mark;  // stream_fn bailed out: nothing of it stays in the body
+      }
       operand_cv(c.key, ci, 0, etpos, K, "L", check);
       operand_cv(c.value, ci, 1, etpos, X, two ? "(L + JCAP * 64)" : "L", check);
       out << "  rc = " << cond_call(ci, K, X) << ";\n";
@@ -1062,7 +1188,8 @@ struct CondGen {
     }
     const std::string b = out.str();
     out.swap(save);
-    defs << "static __device__ __attribute__((noinline)) uint8_t jr" << k << "(const View& v, uint32_t r, uint32_t* L) {\n" << b << "}\n";
+    // inlined into its rule's kernel (kyv_jit_cond_<k>): no call frame (callee-saved registers in scratch memory)
+    defs << "static __device__ __forceinline__ uint8_t jr" << k << "(const View& v, uint32_t r, uint32_t* L) {\n" << b << "}\n";
   }
 };
 
@@ -1152,7 +1279,8 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     return o;
   };
   size_t nshapes = 0;
-  for (size_t k = 0; k < rs.rules.size(); k++) {
+  const bool only_cond = getenv("KYV_JIT_ONLY_COND") && atoi(getenv("KYV_JIT_ONLY_COND")) != 0;  // experiments only
+  for (size_t k = 0; k < rs.rules.size() && !only_cond; k++) {
     const RuleDesc& rd = rs.rules[k];
     if (rd.kind != RK_PATTERN && rd.kind != RK_ANYPATTERN) continue;
     std::vector<uint32_t> rr;
@@ -1202,9 +1330,6 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     src << "static __device__ __attribute__((noinline)) int jc_match(const View& v, uint32_t r, uint32_t k) {\n"
            "  uint8_t st;\n  return pair_match(v, r, v.rules[k], &st) ? -1 : (int)st;\n}\n";
     src << cg.defs.str();
-    src << "static __device__ uint8_t jc_dispatch(const View& v, uint32_t r, uint32_t k, uint32_t* L) {\n  switch (k) {\n";
-    for (uint32_t k : crules) src << "    case " << k << "u: return jr" << k << "(v, r, L);\n";
-    src << "    default: return ST_FALLBACK;\n  }\n}\n";
   }
   // Rules are split into groups of a few, one kernel per group (kyv_jit_walk_<g>): the compiler allocates
   // registers per group instead of for the worst pattern of the whole ruleset, and a group's code stays in
@@ -1274,32 +1399,25 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
   src << "}  // namespace kyv\n"
          "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n";
   if (!crules.empty()) {
-    // one lane per resource, the kernel's rules uniform across the wave (grid.y strides over them); operand lists
-    // in LDS, lane-interleaved
-    // 5 waves/SIMD: measured 1.30 -> 1.05 ms on C3 (4: 1.11, 6: 1.08; unbounded = 3 waves at 152 VGPRs)
-    src << "#ifndef KYV_JC_WPE\n#define KYV_JC_WPE 5\n#endif\n"
-           "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JC_WPE)))\n"
-           "kyv_jit_cond(const kyv::View* __restrict__ vp, kyv::DevOut o, const uint32_t* __restrict__ mrules, uint32_t nm,\n"
-           "             uint32_t xmode) {\n"
-           "  __shared__ uint32_t jl[" << cg.nslots << "u * kyv::JCAP * 64u];\n"
-           "  const kyv::View& v = *vp;\n"
-           "  // xmode 0: blockIdx.x = match wave, grid.y strides over the rules; xmode 1: XCD-interleaved (workgroup\n"
-           "  // L -> XCD L % 8; the rules of one match wave are consecutive workgroups of one XCD, so its L2 serves\n"
-           "  // the wave's rows to every rule)\n"
-           "  uint32_t wv = blockIdx.x, mi0 = blockIdx.y, mstep = gridDim.y;\n"
-           "  if (xmode == 1) { const uint32_t q = blockIdx.x >> 3; wv = (q / nm) * 8u + (blockIdx.x & 7u); mi0 = q % nm; mstep = nm; }\n"
-           "  const uint32_t lane = threadIdx.x, r = wv * 64u + lane;\n"
-           "  const bool active = r < v.nres;\n"
-           "  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;\n"
-           "  for (uint32_t mi = mi0; mi < nm; mi += mstep) {\n"
-           "    const uint32_t k = kyv::sld32(mrules + mi);\n"
-           "    const bool gated = active && ((gate[k >> 5] >> (k & 31u)) & 1u);\n"
-           "    if (!__ballot(gated)) continue;\n"
-           "    uint8_t st = kyv::ST_NONE;\n"
-           "    if (gated) st = kyv::jc_dispatch(v, r, k, jl + lane);\n"
-           "    if (gated && st != kyv::ST_NONE) o.status[(size_t)k * v.nres + r] = st;\n"
-           "  }\n"
-           "}\n";
+    // one kernel per compiled condition rule, the rule inlined (one big kernel with a switch over the rules needs an
+    // out-of-line call per rule, whose callee-saved registers go through scratch memory, or, inlined, compiles for
+    // tens of minutes); one lane per resource, launched over the match waves [w0, w0 + grid) that hold resources of
+    // the rule's kind gate (kind-major batch)
+    // 5 waves/SIMD: measured 1.30 -> 1.05 ms on C3 with the round-2 kernel (4: 1.11, 6: 1.08)
+    src << "#ifndef KYV_JC_WPE\n#define KYV_JC_WPE 5\n#endif\n";
+    for (uint32_t k : crules)
+      src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JC_WPE)))\n"
+             "kyv_jit_cond_" << k << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t w0) {\n"
+             "  __shared__ uint32_t jl[" << (cg.lds_used ? cg.nslots : 0u) << "u * kyv::JCAP * 64u + 64u];\n"
+             "  const kyv::View& v = *vp;\n"
+             "  const uint32_t lane = threadIdx.x, r = (w0 + blockIdx.x) * 64u + lane;\n"
+             "  const bool gated = r < v.nres && ((v.gate[(size_t)v.hdr[r].kclass * v.gate_words + " << k / 32 << "u] >> "
+          << k % 32 << "u) & 1u);\n"
+             "  if (!__ballot(gated)) return;\n"
+             "  uint8_t st = kyv::ST_NONE;\n"
+             "  if (gated) st = kyv::jr" << k << "(v, r, jl + lane);\n"
+             "  if (gated && st != kyv::ST_NONE) o.status[(size_t)" << k << "u * v.nres + r] = st;\n"
+             "}\n";
     for (uint32_t k : crules) if (jit_cond) (*jit_cond)[k] = 1;
   }
   for (size_t gi = 0; gi < ngroups; gi++)

@@ -63,10 +63,10 @@ struct DevRuleset {
   uint8_t* base = nullptr;
   size_t bytes = 0;
   size_t o_rules, o_filters, o_kinds, o_sels, o_reqs, o_pn, o_pe, o_leaves, o_atoms, o_metas, o_pss, o_pool, o_cnodes, o_conds, o_cprogs,
-      o_gpats;
+      o_gpats, o_gsets;
   hipModule_t jmod = nullptr;     // runtime-compiled walk kernels (jit.cpp) loaded on this device
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
-  hipFunction_t jcond = nullptr;    // kyv_jit_cond (compiled deny / foreach rules), if the ruleset has any
+  std::vector<hipFunction_t> jconds;  // [rule] kyv_jit_cond_<k> (compiled deny / foreach rule k) or null
   bool jloaded = false;
 };
 
@@ -191,6 +191,7 @@ struct SliceSched {
   uint32_t nm = 0, nmj = 0, nmc = 0;  // [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
                                  // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
   std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
+  std::vector<uint3> cw;         // compiled condition rules: (rule, first match wave, waves) of its kernel's launch
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
@@ -265,6 +266,11 @@ static DevRuleset* upload_ruleset(const Ruleset& rs, int device) {
   d->o_conds = p.add(rs.conds);
   d->o_cprogs = p.add(rs.cprogs);
   d->o_gpats = p.add(rs.gpats);
+  // condition sets for gmask_kernel: [nsets + 1] offsets into the sids that follow
+  std::vector<uint32_t> gs(rs.gsets.size() + 1, 0);
+  for (size_t q = 0; q < rs.gsets.size(); q++) gs[q + 1] = gs[q] + (uint32_t)rs.gsets[q].size();
+  for (auto& st : rs.gsets) gs.insert(gs.end(), st.begin(), st.end());
+  d->o_gsets = p.add(gs);
   d->bytes = p.size;
   HIP_OK(hipMalloc(&d->base, d->bytes));
   HIP_OK(p.copy_to(d->base));
@@ -548,16 +554,30 @@ __global__ void __launch_bounds__(HIST_BLOCK) status_hist_kernel(const uint8_t* 
   }
 }
 
-// wildcard.Match(pattern g, string s) for every dictionary string (one thread each) and masked pattern
+// wildcard.Match(pattern g, string s) for every dictionary string (one thread each) and masked pattern; then the
+// condition sets (compiler.cpp assign_cond_sets): bit ng + q = wild2(s, e) for some literal e of set q (kyv_cond.h wild2,
+// both match directions)
 __global__ void __launch_bounds__(256) gmask_kernel(const View* __restrict__ vp, const uint32_t* __restrict__ gpats,
-                                                    uint32_t ng, uint32_t nstr, uint32_t words, uint32_t* __restrict__ out) {
+                                                    uint32_t ng, const uint32_t* __restrict__ gsets, uint32_t nsets,
+                                                    uint32_t nstr, uint32_t words, uint32_t* __restrict__ out) {
   const uint32_t s = blockIdx.x * 256u + threadIdx.x;
   if (s >= nstr) return;
   const View& v = *vp;
   for (uint32_t w = 0; w < words; w++) {
     uint32_t bits = 0;
-    for (uint32_t g = 32 * w; g < ng && g < 32 * w + 32; g++)
-      if (glob_sid_raw(v, gpats[g], s)) bits |= 1u << (g - 32 * w);
+    for (uint32_t b = 32 * w; b < ng + nsets && b < 32 * w + 32; b++) {
+      bool hit = false;
+      if (b < ng) {
+        hit = glob_sid_raw(v, gpats[b], s);
+      } else {
+        const uint32_t q = b - ng;
+        for (uint32_t i = gsets[q]; i < gsets[q + 1] && !hit; i++) {
+          const uint32_t e = gsets[nsets + 1 + i];
+          hit = glob_sid_raw(v, e, s) || glob_sid_raw(v, s, e);
+        }
+      }
+      if (hit) bits |= 1u << (b - 32 * w);
+    }
     out[(size_t)s * words + w] = bits;
   }
 }
@@ -630,9 +650,9 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   dr->jfns.resize(ng);
   for (uint32_t g = 0; g < ng; g++)
     HIP_OK(hipModuleGetFunction(&dr->jfns[g], dr->jmod, ("kyv_jit_walk_" + std::to_string(g)).c_str()));
-  bool anyc = false;
-  for (auto x : rs.jit_cond) anyc |= x != 0;
-  if (anyc) HIP_OK(hipModuleGetFunction(&dr->jcond, dr->jmod, "kyv_jit_cond"));
+  dr->jconds.assign(rs.rules.size(), nullptr);
+  for (size_t k = 0; k < rs.jit_cond.size(); k++)
+    if (rs.jit_cond[k]) HIP_OK(hipModuleGetFunction(&dr->jconds[k], dr->jmod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
   dr->jloaded = true;
   return true;
 }
@@ -743,9 +763,20 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     // other condition rules' verdicts are left unset)
     std::vector<uint32_t> only;
     if (const char* e = getenv("KYV_JC_ONLY")) for (const char* p = e; *p;) { only.push_back((uint32_t)strtoul(p, (char**)&p, 10)); if (*p) p++; }
+    sl.cw.clear();
     for (uint32_t q : sl.mj) {
-      if (jit && dr->jcond && q < rs.jit_cond.size() && rs.jit_cond[q]) {
-        if (only.empty() || std::find(only.begin(), only.end(), q) != only.end()) cj.push_back(q);
+      if (jit && q < dr->jconds.size() && dr->jconds[q]) {
+        if (!only.empty() && std::find(only.begin(), only.end(), q) == only.end()) continue;
+        cj.push_back(q);
+        // the match waves holding resources of the rule's kind gate: one range in the kind-major batch (waves inside
+        // it whose resources the gate excludes exit after one ballot)
+        uint32_t lo = nw, hi = 0;
+        for (size_t ri = 0; ri < runs.size(); ri++) {
+          if (!((runs[ri].second[q / 32] >> (q % 32)) & 1u)) continue;
+          lo = std::min(lo, runs[ri].first);
+          hi = std::max(hi, ri + 1 < runs.size() ? runs[ri + 1].first : nw);
+        }
+        if (lo < hi) sl.cw.push_back(make_uint3(q, lo, hi - lo));
       } else {
         mr.push_back(q);
       }
@@ -796,19 +827,20 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   if (!mb.dev[device]) mb.dev[device] = upload_batch(b, device);
   DevRuleset* dr = (DevRuleset*)mrs.dev[device];
   DevBatch* db = (DevBatch*)mb.dev[device];
-  if (!db->gmask && !rs.gpats.empty() && !b.str_len.empty() && !getenv("KYV_NO_GMASK")) {
+  if (!db->gmask && rs.gpats.size() + rs.gsets.size() > 0 && !b.str_len.empty() && !getenv("KYV_NO_GMASK")) {
     // glob masks of this batch's dictionary against the ruleset's wildcard patterns (once per batch and device,
     // like the path columns on the host: derived per-string data, not per-evaluation work)
     const size_t nstr = b.str_len.size();
-    db->gmask_words = (uint32_t)((rs.gpats.size() + 31) / 32);
+    db->gmask_words = (uint32_t)((rs.gpats.size() + rs.gsets.size() + 31) / 32);
     HIP_OK(dmalloc(&db->gmask, nstr * db->gmask_words * 4));
     View tv = make_view(rs, b, dr->base, dr, db->base, db);
     View* dv = nullptr;
     HIP_OK(dmalloc(&dv, sizeof(View)));
     HIP_OK(hipMemcpy(dv, &tv, sizeof(View), hipMemcpyHostToDevice));
     const uint32_t* gp = (const uint32_t*)(dr->base + dr->o_gpats);
+    const uint32_t* gs = (const uint32_t*)(dr->base + dr->o_gsets);
     hipLaunchKernelGGL(gmask_kernel, dim3((unsigned)((nstr + 255) / 256)), dim3(256), 0, 0, (const View*)dv, gp,
-                       (uint32_t)rs.gpats.size(), (uint32_t)nstr, db->gmask_words, db->gmask);
+                       (uint32_t)rs.gpats.size(), gs, (uint32_t)rs.gsets.size(), (uint32_t)nstr, db->gmask_words, db->gmask);
     HIP_OK(hipGetLastError());
     HIP_OK(hipDeviceSynchronize());
     dfree(dv);
@@ -936,25 +968,14 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
                            (const uint32_t*)sl.mrules + sl.nm, sl.nmj);
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(sl.ev[0], stream));
-      if (sl.nmc) {
-        // compiled condition rules: grid.y strides over them (one rule per workgroup row by default: the waves of
-        // a kind-major batch that no rule gates exit after one ballot)
-        static const uint32_t gy_env = getenv("KYV_JC_Y") ? (uint32_t)std::max(1, atoi(getenv("KYV_JC_Y"))) : 0u;
-        static const uint32_t xmode_env = getenv("KYV_JC_MODE") ? (uint32_t)atoi(getenv("KYV_JC_MODE")) : 0u;  // 1 measured 1.6x slower
-        const uint32_t gy = gy_env ? std::min(gy_env, sl.nmc) : sl.nmc;
-        // (the View goes by pointer: a by-value View would be copied to scratch memory, since the kernels take its
-        // address for out-of-line helpers; measured 40 % slower)
+      // compiled condition rules: one kernel each over the waves of its kind gate
+      // (the View goes by pointer: a by-value View would be copied to scratch memory, since the kernels take its
+      // address for out-of-line helpers; measured 40 % slower)
+      for (const uint3& c : sl.cw) {
         const View* vp = d.view;
-        const uint32_t* mr = sl.mrules + sl.nm + sl.nmj;
-        uint32_t nmc = sl.nmc, xmode = xmode_env;
-        void* args[] = {(void*)&vp, (void*)&o, (void*)&mr, (void*)&nmc, (void*)&xmode};
-        if (xmode == 1) {
-          const size_t gx = (size_t)((grid.x + 7) / 8) * 8 * nmc;
-          if (gx > 0x7FFFFFFFull) throw std::runtime_error("condition grid too large");
-          HIP_OK(hipModuleLaunchKernel(dr->jcond, (uint32_t)gx, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
-        } else {
-          HIP_OK(hipModuleLaunchKernel(dr->jcond, grid.x, gy, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
-        }
+        uint32_t w0 = c.y;
+        void* args[] = {(void*)&vp, (void*)&o, (void*)&w0};
+        HIP_OK(hipModuleLaunchKernel(dr->jconds[c.x], c.z, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
       HIP_OK(hipEventRecord(sl.ev[1], stream));
       if (sl.grid[0]) {

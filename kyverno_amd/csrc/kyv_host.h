@@ -111,6 +111,10 @@ struct Ruleset {
   };
   std::vector<TrieNode> trie;   // trie[0] = resource root
   std::vector<uint32_t> gpats;  // wildcard patterns with a per-string glob mask (index g: mask bit g, SF_GIDX_SHIFT)
+  // condition-set masks (compiler.cpp assign_cond_sets): set q's bit (gpats.size() + q) of string s = wild2(s, e) for
+  // some literal sid e of the set; cond_set[ci] = set index + 1 of condition ci, 0 none
+  std::vector<std::vector<uint32_t>> gsets;
+  std::vector<uint32_t> cond_set;
   uint32_t ncols = 0, nrowspaces = 1;
   std::vector<uint32_t> col_rowspace;
   std::vector<uint32_t> pn_self;  // array pnode -> self column of its elements (NONE: none)
@@ -189,6 +193,7 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
 void derive_strings(Batch& b, size_t from, int threads);
 void build_path_trie(Ruleset& rs);
 void assign_glob_masks(Ruleset& rs);
+void assign_cond_sets(Ruleset& rs);
 std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond = nullptr);
 std::vector<char> jit_compile(const std::string& src, double* seconds);
 enum JitMode { JIT_AUTO = 0, JIT_OFF = 1, JIT_ON = 2 };

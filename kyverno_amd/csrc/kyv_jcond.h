@@ -127,6 +127,20 @@ __device__ __forceinline__ bool jc_false1(const Node* R, uint32_t cur) {
     default: return false;
   }
 }
+// fmt.Sprint sid of a (non-null) list element as the operators see it (sprint_sid(cv_elem(...)), kyv_cond.h): a
+// string whose id came with its column entry directly, anything else from its node (NONE: no device rendering)
+__device__ __forceinline__ uint32_t jc_sprint(const Node* R, uint32_t i, uint32_t t, uint32_t a) {
+  if (i == NONE) return KSID(NIL_STR);
+  if (t == N_STR) return a;
+  return sprint_sid(cv_node(gnode(R + i), true));
+}
+// condition-set test of string s (compiler.cpp assign_cond_sets): wild2(s, e) for some e of the set; one mask load
+// when the batch has glob masks (bit = gpats.size() + set index), else the set's literals one by one
+__device__ __forceinline__ bool jc_inset(const View& v, uint32_t bit, const uint32_t* set, uint32_t n, uint32_t s) {
+  if (v.str_gmask) return (v.str_gmask[(size_t)s * v.gmask_words + bit / 32] >> (bit % 32)) & 1u;
+  for (uint32_t j = 0; j < n; j++) if (wild2(v, s, set[j])) return true;
+  return false;
+}
 // operand value of a JMESPath result (jres_cv with the list in LDS)
 __device__ __forceinline__ CV jc_cv(const View& v, const Node* R, bool lst, uint32_t cur, uint32_t lit, const uint32_t* L,
                                     uint32_t n) {
