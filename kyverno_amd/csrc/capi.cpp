@@ -18,6 +18,8 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
 void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool account);
 void free_device_images(Ruleset& rs, Batch* b);
 std::string fallback_why(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule);
+bool pattern_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule, uint32_t root, uint8_t* status,
+                        std::string* path, std::string* text);
 bool pss_checks_render(const Ruleset& rs, const Batch& b, uint32_t pos, uint32_t rule, uint32_t mask,
                        std::vector<std::array<std::string, 3>>* out);
 }  // namespace kyv
@@ -389,6 +391,53 @@ static std::string json_str(const std::string& s) {
   return o + "\"";
 }
 
+// Messages built from the pattern walk's error texts (pattern_error_text, kyv_engine.hip): skip (PatternError.Error()),
+// error (buildErrorMessage(err, ""): "execution error: <err>") and anyPattern results with a path-less failure
+// ("rule <name>[<i>] failed: <err>") -- validation.go:618-702,722-758. The host walk must reach the device's status.
+static bool walk_text_message(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule, uint8_t st, std::string* o) {
+  const RuleMeta& m = rs.meta[rule];
+  const RuleDesc& d = rs.rules[rule];
+  if (d.kind == RK_PATTERN) {
+    uint8_t s2;
+    std::string path, text;
+    if (!pattern_error_text(rs, b, res, rule, d.root, &s2, &path, &text) || s2 != st) return false;
+    if (st == ST_SKIP) return *o = text, true;
+    if (st != ST_ERROR) return false;
+    if (m.message.empty()) return *o = "validation error: rule " + m.name + " execution error: " + text, true;
+    if (m.message_vars) return false;
+    std::string mm = m.message;
+    if (mm.back() != '.') mm += ".";
+    return *o = "validation error: " + mm + " rule " + m.name + " execution error: " + text, true;
+  }
+  if (d.kind != RK_ANYPATTERN) return false;
+  std::vector<std::string> failed, skipped;
+  for (uint32_t a = 0; a < d.nalts; a++) {
+    uint8_t s2;
+    std::string path, text;
+    if (!pattern_error_text(rs, b, res, rule, rs.pool[d.root + a], &s2, &path, &text)) return false;
+    const std::string nm = "rule " + m.name + "[" + std::to_string(a) + "]";
+    if (s2 == ST_PASS) return false;  // the device decided the pair otherwise
+    if (s2 == ST_SKIP) skipped.push_back(nm + " skipped: " + text);
+    else if (path.empty()) failed.push_back(nm + " failed: " + text);
+    else failed.push_back(nm + " failed at path " + path);
+  }
+  auto join = [](const std::vector<std::string>& v) {
+    std::string j;
+    for (size_t i = 0; i < v.size(); i++) j += (i ? " " : "") + v[i];
+    return j;
+  };
+  if (failed.empty()) {
+    if (st != ST_SKIP || skipped.empty()) return false;
+    return *o = join(skipped), true;
+  }
+  if (st != ST_FAIL) return false;
+  if (m.message_vars) return false;
+  const std::string e = join(failed);
+  if (m.message.empty()) return *o = "validation error: " + e, true;
+  if (m.message.back() == '.') return *o = "validation error: " + m.message + " " + e, true;
+  return *o = "validation error: " + m.message + ". " + e, true;
+}
+
 // validation.go:722-758 (buildErrorMessage / buildAnyPatternErrorMessage) and :640/:665 pass messages of the pair at
 // kind-major position `res`; false: the text needs the reference engine (Go error strings, variables)
 static bool render_message(kyv_results* r, const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule, std::string* o) {
@@ -438,7 +487,8 @@ static bool render_message(kyv_results* r, const Ruleset& rs, const Batch& b, ui
     }
     return *o = "validation rule '" + m.name + "' passed.", true;
   }
-  if (st != ST_FAIL) return false;  // skip / error texts embed the reference's error strings
+  if (st == ST_SKIP || st == ST_ERROR) return walk_text_message(rs, b, res, rule, st, o);
+  if (st != ST_FAIL) return false;
   ensure_index(r);
   auto range = r->recidx.equal_range(((uint64_t)rule << 32) | res);
   std::vector<const FailRec*> recs;
@@ -454,7 +504,7 @@ static bool render_message(kyv_results* r, const Ruleset& rs, const Batch& b, ui
   }
   std::string joined;
   for (size_t i = 0; i < recs.size(); i++) {
-    if (recs[i]->tmpl == NONE) return false;  // "failed: <err>" needs the reference error text
+    if (recs[i]->tmpl == NONE) return walk_text_message(rs, b, res, rule, st, o);  // "failed: <err>"
     if (i) joined += " ";
     joined += "rule " + m.name + "[" + std::to_string(recs[i]->alt) + "] failed at path " +
               format_path(rs, b, recs[i]->tmpl, recs[i]->idx, recs[i]->key);

@@ -45,6 +45,9 @@ struct Gen {
   // (C3 2.83 -> 2.73 ms per evaluation; it measured slower in round 1, before the uniform-wave schedule and glob
   // masks); KYV_JIT_LEN=0 turns it off
   const bool use_len = !getenv("KYV_JIT_LEN") || atoi(getenv("KYV_JIT_LEN")) != 0;
+  // array-of-maps elements whose column loads are issued together (KYV_JIT_BATCH; default 1 = one element at a
+  // time: batches of 2 / 4 measured 2.1x slower on C3, 1.41 -> 2.97 ms walk, registers past the 4-wave budget)
+  const size_t batch_max = getenv("KYV_JIT_BATCH") ? (size_t)std::max(1, atoi(getenv("KYV_JIT_BATCH"))) : 1;
 
   // Column scopes: the pattern root and every array-element pattern open a scope (one row of one row space);
   // every column lookup of the maps inside a scope (not crossing into array elements) is loaded up front by
@@ -305,7 +308,47 @@ struct Gen {
               << "      if (r.err) { if (ret_is_skip(r)) st |= FS_SKIP | ((uint32_t)r.mask << 2); else return r; }\n"
               << "      else st |= FS_APPLY; }\n";
         };
-        if (P.kind == P_ARR_MAPS) {
+        // elements in batches of K: the column loads of K consecutive elements (independent: rows eb + i) are
+        // issued together before the first of them is walked, so an array of <= K elements costs one memory round
+        // instead of one per element (K from the scope size: at most 8 preloaded 64-bit entries per batch)
+        scope(P.first);
+        const size_t S = scope_of[P.first].size() + (self != NONE ? 1 : 0);
+        const size_t K = P.kind == P_ARR_MAPS && batch_max > 1 && S > 0 ? std::max<size_t>(1, std::min<size_t>(batch_max, 8 / S)) : 1;
+        if (P.kind == P_ARR_MAPS && K > 1) {
+          out << "  for (uint32_t i0 = 0; i0 < cnt; i0 += " << K << "u) {\n";
+          for (size_t q = 0; q < K; q++) {
+            const std::string Q = std::to_string(q);
+            out << "    const uint32_t er" << Q << " = (eb == NONE || i0 + " << Q << "u >= cnt) ? NONE : eb + i0 + " << Q << "u;\n"
+                << "    " << preload(P.first, "pe" + Q, "er" + Q) << "\n";
+            if (self != NONE) out << "    const uint64_t sx" << Q << " = jself(w, " << u(self) << ", er" << Q << ");\n";
+          }
+          // one copy of the element body (the child is inlined): the batch's entries are selected by position
+          const size_t NS = scope_of[P.first].size();
+          out << "    #pragma nounroll\n"
+                 "    for (uint32_t q = 0; q < " << K << "u && i0 + q < cnt; q++) {\n"
+                 "      const uint32_t i = i0 + q;\n"
+                 "      w.idx = (w.idx & ~(0xFFFFull << " << 16u * P.level << ")) | ((uint64_t)i << " << 16u * P.level << ");\n";
+          auto sel = [&](const std::string& a, const std::string& b) {  // a0..a{K-1} (+ b suffix) by q
+            std::string e = a + std::to_string(K - 1) + b;
+            for (size_t q = K - 1; q-- > 0;) e = "(q == " + std::to_string(q) + "u ? " + a + std::to_string(q) + b + " : " + e + ")";
+            return e;
+          };
+          out << "      const uint32_t er = " << sel("er", "") << ";\n"
+              << "      uint64_t pe[" << std::max<size_t>(1, NS) << "];";
+          for (size_t x = 0; x < NS; x++) out << " pe[" << x << "] = " << sel("pe", "[" + std::to_string(x) + "]") << ";";
+          out << "\n";
+          if (self != NONE)
+            out << "      uint32_t et, ea; uint32_t ei = jdec(" << sel("sx", "") << ", &et, &ea);\n"
+                   "      if (ei == NONE) { ei = aa + i; et = T_UNK; }\n";
+          else
+            out << "      const uint32_t ei = aa + i, et = T_UNK, ea = 0u;\n";
+          out << "      Ret r = p" << P.first << "(w, ei, et, ea, er, pe);\n"
+              << "      if (w.ost) return r;\n"
+              << "      if (r.err) { if (ret_is_skip(r)) st |= FS_SKIP | ((uint32_t)r.mask << 2); else return r; }\n"
+              << "      else st |= FS_APPLY;\n"
+              << "    }\n";
+          out << "  }\n";
+        } else if (P.kind == P_ARR_MAPS) {
           out << "  for (uint32_t i = 0; i < cnt; i++) {\n";
           elem("i", P.first, true);
           out << "  }\n";
@@ -1334,12 +1377,63 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
   // Rules are split into groups of a few, one kernel per group (kyv_jit_walk_<g>): the compiler allocates
   // registers per group instead of for the worst pattern of the whole ruleset, and a group's code stays in
   // the instruction cache. jit_rules[k] = group + 1.
-  const size_t per = getenv("KYV_JIT_GROUP") ? (size_t)std::max(1, atoi(getenv("KYV_JIT_GROUP"))) : (size_t)1000000;
-  const size_t ngroups = std::min<size_t>(250, (rule_roots.size() + per - 1) / per);
+  // Default: two groups by register need. Rules whose patterns expand wildcard metadata keys (expand_meta: C3's
+  // apparmor rules need ~100 VGPRs alone) go to a kernel at 4 waves/SIMD; every other rule (<= ~64 VGPRs alone) to
+  // one at KYV_JIT_WPE_LIGHT (8) waves/SIMD, so the register hogs do not set the occupancy of the whole walk.
+  // KYV_JIT_GROUP=n: consecutive groups of n rules (experiments); KYV_JIT_SPLIT=0: one group.
+  std::vector<std::vector<size_t>> groups;
+  std::vector<int> gwpe;
+  std::function<bool(uint32_t, uint32_t, int)> wild_meta = [&](uint32_t pn, uint32_t mbase, int guard) -> bool {
+    if (pn == NONE || pn >= rs.pnodes.size() || guard > 4 * MAX_DEPTH) return false;
+    const PNode& P = rs.pnodes[pn];
+    switch (P.kind) {
+      case P_MAP: {
+        if (P.flags & PF_META) {
+          const MetaSite& ms = rs.metas[mbase + P.meta];
+          if (ms.nwild_l + ms.nwild_a) return true;
+        }
+        for (uint32_t e = 0; e < P.n; e++) {
+          const PEntry& E = rs.pentries[P.first + e];
+          if (E.child == NONE || E.handler == H_STAR || E.handler == H_NEGATION || E.handler == H_EXIST_BADPAT) continue;
+          if (E.handler == H_EXISTENCE) {
+            for (uint32_t j = 0; j < rs.pool[E.child]; j++) if (wild_meta(rs.pool[E.child + 1 + j], mbase, guard + 1)) return true;
+          } else if (wild_meta(E.child, mbase, guard + 1)) {
+            return true;
+          }
+        }
+        return false;
+      }
+      case P_ARR_MAPS: return wild_meta(P.first, mbase, guard + 1);
+      case P_ARR_POS:
+        for (uint32_t i = 0; i < P.n; i++) if (wild_meta(rs.pool[P.first + i], mbase, guard + 1)) return true;
+        return false;
+      default: return false;
+    }
+  };
+  if (getenv("KYV_JIT_GROUP")) {
+    const size_t per = (size_t)std::max(1, atoi(getenv("KYV_JIT_GROUP")));
+    const size_t ng = std::min<size_t>(250, (rule_roots.size() + per - 1) / per);
+    for (size_t gi = 0; gi < ng; gi++) {
+      groups.emplace_back();
+      gwpe.push_back(-1);
+      for (size_t i = rule_roots.size() * gi / ng; i < rule_roots.size() * (gi + 1) / ng; i++) groups.back().push_back(i);
+    }
+  } else {
+    const bool split = !getenv("KYV_JIT_SPLIT") || atoi(getenv("KYV_JIT_SPLIT")) != 0;
+    std::vector<size_t> light, heavy;
+    for (size_t i = 0; i < rule_roots.size(); i++) {
+      bool h = false;
+      const RuleDesc& rd = rs.rules[rule_roots[i].first];
+      for (uint32_t r : rule_roots[i].second) h = h || wild_meta(r, rd.meta_sites, 0);
+      (split && h ? heavy : light).push_back(i);
+    }
+    if (!light.empty()) { groups.push_back(light); gwpe.push_back(split ? -2 : -1); }
+    if (!heavy.empty()) { groups.push_back(heavy); gwpe.push_back(-1); }
+  }
+  const size_t ngroups = groups.size();
   for (size_t gi = 0; gi < ngroups; gi++) {
-    const size_t lo = rule_roots.size() * gi / ngroups, hi = rule_roots.size() * (gi + 1) / ngroups;
     std::vector<uint32_t> roots;
-    for (size_t i = lo; i < hi; i++) {
+    for (size_t i : groups[gi]) {
       (*jit_rules)[rule_roots[i].first] = (uint8_t)(gi + 1);
       for (uint32_t r : rule_roots[i].second) roots.push_back(r);
     }
@@ -1352,6 +1446,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "  const uint32_t row0 = (uint32_t)(hp - v.hdr), row = row0 < v.nres ? row0 : NONE;\n"
              "  " << g.preload(r, "pc", "row", "jc_col(v, ") << "\n"
              "  if (!walk) return;\n"
+             "#ifdef KYV_EXP_JIT_PRELOAD\n  { uint64_t x = 0; for (auto q : pc) x ^= q; out.status = x == 0x123456789ull ? ST_FAIL : ST_PASS; return; }\n#endif\n"
              "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
              "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
              "  jfinish(w, r, out);\n"
@@ -1420,8 +1515,10 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "}\n";
     for (uint32_t k : crules) if (jit_cond) (*jit_cond)[k] = 1;
   }
+  src << "#ifndef KYV_JIT_WPE_LIGHT\n#define KYV_JIT_WPE_LIGHT 8\n#endif\n";
   for (size_t gi = 0; gi < ngroups; gi++)
-    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE)))\n"
+    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu("
+        << (gwpe[gi] == -2 ? "KYV_JIT_WPE_LIGHT" : "KYV_JIT_WPE") << ")))\n"
            "kyv_jit_walk_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, kyv::WorkLists wl, kyv::ChunkMap cm) {\n"
            "  kyv::JitWalker" << gi << " wk{false};\n"
            "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"

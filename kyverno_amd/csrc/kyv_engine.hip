@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <cmath>
+#include <functional>
 #include <cstdlib>
 #include <mutex>
 #include <cstdio>
@@ -1190,6 +1192,296 @@ std::string fallback_why(const Ruleset& rs, const Batch& b, uint32_t res, uint32
     case FBW_META: return "anchor-like key under metadata (wildcard expansion)";
     default: return "pattern walk outside the device subset";
   }
+}
+
+// ---------------------------------------------------------------- pattern error texts (host)
+// The error text of a pattern walk, for the RuleResponse.Message of pairs whose text the failure records cannot give:
+// skip pairs (PatternError.Error() of a conditional / global anchor error), error pairs ("execution error: <err>") and
+// anyPattern alternatives that failed without a path ("failed: <err>"). The one pair is walked again on the host along
+// the compiled pattern program, in the order and with the handler semantics of eval_pattern, and with the error
+// strings of the reference:
+//   pkg/engine/validate/validate.go:31-56 (MatchPattern), :71-114 (validateResourceElement), :118-161 (validateMap),
+//   :163-247 (validateArray / validateArrayOfMaps, multierr.Combine of the skip errors);
+//   pkg/engine/anchor/handlers.go:31-275 (handler texts), anchor/error.go:12-90 (prefixes, typed vs substring checks).
+// Values print as Go's fmt %v / %T of the unstructured decode (maps with sorted keys, float64 as strconv 'g' -1).
+namespace {
+
+// strconv.FormatFloat(f, 'g', -1, 64) (fmt %v of a float64): the shortest digits that round-trip, in %e form when
+// the decimal exponent is < -4 or >= 6 (strconv/ftoa.go: eprec = 6 for the shortest precision), else %f form
+std::string go_float_g(double f) {
+  if (f != f) return "NaN";
+  if (f == __builtin_inf()) return "+Inf";
+  if (f == -__builtin_inf()) return "-Inf";
+  char buf[64];
+  std::string mant;
+  int exp10 = 0;
+  const bool neg = std::signbit(f);
+  const double a = std::fabs(f);
+  if (a == 0) {
+    mant = "0";
+  } else {
+    for (int prec = 1; prec <= 17; prec++) {
+      snprintf(buf, sizeof buf, "%.*e", prec - 1, a);
+      if (strtod(buf, nullptr) == a) break;
+    }
+    const char* e = strchr(buf, 'e');
+    exp10 = atoi(e + 1);
+    for (const char* q = buf; q < e; q++) if (*q != '.') mant += *q;
+    while (mant.size() > 1 && mant.back() == '0') mant.pop_back();
+  }
+  std::string out = neg ? "-" : "";
+  const int nd = (int)mant.size(), dp = exp10 + 1;
+  if (exp10 < -4 || exp10 >= 6) {
+    out += mant[0];
+    if (nd > 1) out += "." + mant.substr(1);
+    char eb[16];
+    snprintf(eb, sizeof eb, "e%c%02d", exp10 < 0 ? '-' : '+', exp10 < 0 ? -exp10 : exp10);
+    return out + eb;
+  }
+  if (dp <= 0) return out + "0." + std::string(-dp, '0') + mant;
+  if (dp >= nd) return out + mant + std::string(dp - nd, '0');
+  return out + mant.substr(0, dp) + "." + mant.substr(dp);
+}
+
+struct TextWalk {
+  const Ruleset& rs;
+  const View& v;
+  NodeTab R;
+  const ResHeader& h;
+  const RuleDesc& rd;
+  uint64_t seen = 0, found = 0;
+  Keys keys{NONE, NONE};
+  bool bad = false;  // a case whose text needs the reference engine
+  struct Err {
+    bool err = false;
+    uint8_t code = EC_NONE;  // typed anchor error (anchor/error.go) or EC_NONE: untyped, classified by substring
+    std::string text;
+  };
+  std::string str(uint32_t sid) const { return std::string((const char*)v.heap + v.str_off[sid], v.str_len[sid]); }
+  std::string gtype(uint32_t rn) const {  // fmt %T
+    if (rn == NONE) return "<nil>";
+    switch (node_type(R[rn])) {
+      case N_MAP: return "map[string]interface {}";
+      case N_ARR: return "[]interface {}";
+      case N_STR: return "string";
+      case N_INT: return "int64";
+      case N_FLOAT: return "float64";
+      case N_TRUE: case N_FALSE: return "bool";
+      default: return "<nil>";
+    }
+  }
+  std::string gval(uint32_t rn, int depth = 0) {  // fmt %v
+    if (rn == NONE || depth > 64) return "<nil>";
+    const Node& n = R[rn];
+    switch (node_type(n)) {
+      case N_NULL: return "<nil>";
+      case N_TRUE: return "true";
+      case N_FALSE: return "false";
+      case N_INT: return std::to_string((int64_t)(((uint64_t)n.b << 32) | n.a));
+      case N_FLOAT: return go_float_g(__builtin_bit_cast(double, ((uint64_t)n.b << 32) | n.a));
+      case N_STR: return str(n.a);
+      case N_ARR: {
+        std::string o = "[";
+        for (uint32_t i = 0; i < n.b; i++) o += (i ? " " : "") + gval(n.a + i, depth + 1);
+        return o + "]";
+      }
+      case N_MAP: {
+        std::vector<std::pair<std::string, uint32_t>> kv;
+        for (uint32_t i = 0; i < n.b; i++) kv.push_back({str(node_key(R[n.a + i])), n.a + i});
+        std::sort(kv.begin(), kv.end());
+        std::string o = "map[";
+        for (size_t i = 0; i < kv.size(); i++) o += (i ? " " : "") + kv[i].first + ":" + gval(kv[i].second, depth + 1);
+        return o + "]";
+      }
+      default: return "<nil>";
+    }
+  }
+  std::string pval(const Leaf& L) {  // %v of a pattern scalar (pattern numbers are float64 after the JSON decode)
+    switch (L.type) {
+      case L_NIL: return "<nil>";
+      case L_BOOL: return L.bval ? "true" : "false";
+      case L_FLOAT: return go_float_g(L.f);
+      case L_STR: return str(L.exact);
+      default: bad = true; return "";
+    }
+  }
+  static bool has(const std::string& t, const char* p) { return t.find(p) != std::string::npos; }
+  static bool is_skip(const Err& e) {
+    if (e.code != EC_NONE) return e.code == EC_COND || e.code == EC_GLOBAL;
+    return has(e.text, "conditional anchor mismatch") || has(e.text, "global anchor mismatch");
+  }
+  static bool is_neg(const Err& e) {
+    return e.code != EC_NONE ? e.code == EC_NEG : has(e.text, "negation anchor matched in resource");
+  }
+  static Err mk(uint8_t code, std::string t) { Err e; e.err = true; e.code = code; e.text = std::move(t); return e; }
+  bool leaf_ok(const Leaf& L, uint32_t rn) {
+    bool fb = false;
+    const bool ok = leaf_match(v, L, value_of(v, R, rn), &fb);
+    if (fb) bad = true;
+    return ok;
+  }
+  Err leaf(const Leaf& L, uint32_t rn, const std::string& path, std::string* rp) {  // validate.go:92-107
+    bool ok = true;
+    if (rn != NONE && node_type(R[rn]) == N_ARR) {
+      for (uint32_t i = 0; i < R[rn].b && ok; i++) ok = leaf_ok(L, R[rn].a + i);
+    } else {
+      ok = leaf_ok(L, rn);
+    }
+    if (ok) return Err{};
+    *rp = path;
+    return mk(EC_NONE, "resource value '" + gval(rn) + "' does not match '" + pval(L) + "' at path " + path);
+  }
+  // validateArray / validateArrayOfMaps element loop: skip errors collected, anything else returned
+  Err elems(uint32_t rn, uint32_t n, const std::function<uint32_t(uint32_t)>& pat, const std::string& path, std::string* rp) {
+    std::vector<std::string> skips;
+    uint32_t applied = 0;
+    for (uint32_t i = 0; i < n && !bad; i++) {
+      std::string p;
+      Err e = elem(R[rn].a + i, pat(i), path + std::to_string(i) + "/", &p);
+      if (!e.err) { applied++; continue; }
+      if (is_skip(e)) { skips.push_back(e.text); continue; }
+      *rp = p;
+      return e;
+    }
+    if (applied == 0 && !skips.empty()) {  // PatternError{multierr.Combine(skips...)}: untyped
+      std::string t;
+      for (size_t i = 0; i < skips.size(); i++) t += (i ? "; " : "") + skips[i];
+      *rp = path;
+      return mk(EC_NONE, t);
+    }
+    return Err{};
+  }
+  Err elem(uint32_t rn, uint32_t pn, const std::string& path, std::string* rp) {
+    if (bad || pn >= rs.pnodes.size() || path.size() > 4096) { bad = true; return Err{}; }
+    const PNode& P = rs.pnodes[pn];
+    const uint32_t rt = rn == NONE ? 0xFF : node_type(R[rn]);
+    switch (P.kind) {
+      case P_MAP:
+        if (rt != N_MAP) {
+          *rp = path;
+          return mk(EC_NONE, "pattern and resource have different structures. Path: " + path +
+                                 ". Expected map[string]interface {}, found " + gtype(rn));
+        }
+        return map(rn, P, path, rp);
+      case P_LEAF: return leaf(rs.leaves[P.first], rn, path, rp);
+      default: break;
+    }
+    if (rt != N_ARR) {
+      *rp = path;
+      return mk(EC_NONE, "validation rule failed at path " + path + ", resource does not satisfy the expected overlay pattern");
+    }
+    const uint32_t cnt = R[rn].b;
+    switch (P.kind) {
+      case P_ARR_EMPTY: *rp = path; return mk(EC_NONE, "pattern Array empty");
+      case P_ARR_SCALAR: return leaf(rs.leaves[rs.pnodes[P.first].first], rn, path, rp);
+      case P_ARR_MAPS: return elems(rn, cnt, [&](uint32_t) { return P.first; }, path, rp);
+      case P_ARR_POS:
+        if (cnt < P.n) {
+          *rp = "";
+          return mk(EC_NONE, "validate Array failed, array length mismatch, resource Array len is " + std::to_string(cnt) +
+                                 " and pattern Array len is " + std::to_string(P.n));
+        }
+        return elems(rn, P.n, [&](uint32_t i) { return rs.pool[P.first + i]; }, path, rp);
+      default: bad = true; return Err{};
+    }
+  }
+  Err map(uint32_t rn, const PNode& P, const std::string& path, std::string* rp) {
+    // AnchorMap.CheckAnchorInResource before this level's metadata expansion, as eval_pattern does
+    for (uint32_t e = 0; e < P.n; e++) {
+      const PEntry& E = rs.pentries[P.first + e];
+      if (E.abit == 0xFF) continue;
+      const uint64_t b1 = 1ull << E.abit;
+      seen |= b1;
+      const uint32_t key = (E.flags & EF_WILD) ? keys.get(E.slot) : E.key;
+      if (!(found & b1) && map_find(R, rn, key) != NONE) found |= b1;
+    }
+    if (P.flags & PF_META) {
+      if (expand_meta(v, rs.metas[rd.meta_sites + P.meta], R, rn, h, keys) != ST_NONE) { bad = true; return Err{}; }
+    }
+    for (uint32_t e = 0; e < P.n && !bad; e++) {
+      const PEntry& E = rs.pentries[P.first + e];
+      const uint32_t key = (E.flags & EF_WILD) ? keys.get(E.slot) : E.key;
+      if (key == NONE) { bad = true; return Err{}; }
+      const uint32_t c = map_find(R, rn, key);
+      const std::string cur = path + str(key) + "/";
+      std::string p;
+      switch (E.handler) {
+        case H_NEGATION:  // handlers.go:66-77
+          if (c != NONE) { *rp = cur; return mk(EC_NEG, "negation anchor matched in resource: " + cur + " is not allowed"); }
+          break;
+        case H_EQUALITY: {  // handlers.go:96-109
+          if (c == NONE) break;
+          Err x = elem(c, E.child, cur, &p);
+          if (x.err) { *rp = p; return x; }
+          break;
+        }
+        case H_GLOBAL: {  // handlers.go:195-209
+          if (c == NONE) break;
+          Err x = elem(c, E.child, cur, &p);
+          if (x.err) { *rp = p; return mk(EC_GLOBAL, "global anchor mismatch: " + x.text); }
+          break;
+        }
+        case H_CONDITION: {  // handlers.go:160-176
+          if (c == NONE) { *rp = cur; return mk(EC_COND, "conditional anchor mismatch: conditional anchor key doesn't exist in the resource"); }
+          Err x = elem(c, E.child, cur, &p);
+          if (x.err) { *rp = p; return mk(EC_COND, "conditional anchor mismatch: " + x.text); }
+          break;
+        }
+        case H_STAR:  // handlers.go:128-141: "*" needs a non-nil value; the error returns the parent path
+          if (c != NONE && node_type(R[c]) != N_NULL) break;
+          *rp = path;
+          return mk(EC_NONE, path + "/" + str(key) + " not found");
+        case H_EXISTENCE: case H_EXIST_BADPAT: {  // handlers.go:228-275
+          if (c == NONE) break;
+          if (node_type(R[c]) != N_ARR) {
+            *rp = cur;
+            return mk(EC_NONE, "invalid resource type " + gtype(c) + ": Existence ^ () anchor can be used only on list/array type resource");
+          }
+          if (E.handler == H_EXIST_BADPAT) { bad = true; return Err{}; }  // the text names the pattern's Go type
+          for (uint32_t j = 0; j < rs.pool[E.child]; j++) {
+            bool hit = false;
+            for (uint32_t i = 0; i < R[c].b && !hit && !bad; i++) {
+              std::string q;
+              hit = !elem(R[c].a + i, rs.pool[E.child + 1 + j], cur + std::to_string(i) + "/", &q).err;
+            }
+            if (!hit) { *rp = cur; return mk(EC_NONE, "existence anchor validation failed at path " + cur); }
+          }
+          break;
+        }
+        default: {  // H_DEFAULT: resourceMap[k] (absent -> nil)
+          Err x = elem(c, E.child, cur, &p);
+          if (x.err) { *rp = p; return x; }
+        }
+      }
+    }
+    return Err{};
+  }
+};
+
+}  // namespace
+
+// MatchPattern of one compiled pattern root for resource `res` (kind-major position): the status the reference
+// derives (validate.go:31-56) and, for a non-nil PatternError, its Path and Error() text. false: a case whose text the
+// host does not render (the reference engine decides the message).
+bool pattern_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule, uint32_t root, uint8_t* status,
+                        std::string* path, std::string* text) {
+  if (rule >= rs.rules.size() || res >= b.hdr.size()) return false;
+  View v = make_view(rs, b, nullptr, nullptr, nullptr, nullptr);
+  const ResHeader& h = b.hdr[res];
+  TextWalk w{rs, v, NodeTab{b.nodes.data() + h.root}, h, rs.rules[rule]};
+  std::string p;
+  TextWalk::Err e = w.elem(0, root, "/", &p);
+  if (w.bad) return false;
+  text->clear();
+  path->clear();
+  if (!e.err) { *status = ST_PASS; return true; }
+  *text = e.text;
+  if (TextWalk::is_skip(e)) { *status = ST_SKIP; return true; }
+  if (TextWalk::is_neg(e)) { *status = ST_FAIL; *path = p; return true; }
+  if (w.seen & ~w.found) { *status = ST_ERROR; return true; }  // AnchorMap.KeysAreMissing
+  *path = p;
+  *status = p.empty() ? ST_ERROR : ST_FAIL;
+  return true;
 }
 
 void free_device_images(Ruleset& rs, Batch* b) {
