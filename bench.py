@@ -233,7 +233,8 @@ def pmc_traffic(config, phase):
     """Memory-side bytes per launch of the dominant kernel (phase) from the newest committed PMC summary
     (profiles/pmc_latest.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc passes of this same
     command), used only when it was measured on the same workload configuration; else None. Returns
-    (summary, tag) with summary = {traffic raw, traffic with the guide's x2 read correction, kernel avg ns}."""
+    (summary, tag) with summary = {traffic raw, traffic with the guide's x2 read correction, kernel ns}, all per
+    evaluation (every launch of the phase's kernels in one evaluation)."""
     f = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(f):
         return None, None
@@ -243,19 +244,30 @@ def pmc_traffic(config, phase):
     keys = ("workload", "resources_per_gpu", "compiled_rules")
     if any(bc.get(k) != config.get(k) for k in keys):
         return None, s.get("tag")
+    ph = (s.get("phases") or {}).get(phase)
+    if ph:  # scripts/pmc_summary.py: per-evaluation totals of the phase's kernels
+        return {"raw": ph["traffic_bytes"], "x2read": 2 * ph["fetch_bytes"] + ph["write_bytes"], "fetch": ph["fetch_bytes"],
+                "write": ph["write_bytes"], "avg_ns": ph["ns"], "wait_frac": ph.get("wait_frac"),
+                "l2_hit": ph.get("l2_hit_rate")}, s.get("tag")
     pre = PHASE_KERNELS[phase]
     fetch = write = ns = 0.0
     found = False
+    kern = s.get("kernels") or {}
+    # launches per evaluation: the verdict histogram runs once per evaluation; a phase's kernels may run once per rule
+    # slice (the 10M-resource batch is evaluated in rule slices) and several kernels make up one phase (walk groups)
+    nev = sum(k["calls"] for kn, k in kern.items() if "status_hist" in kn) or 1
+    per_eval = {kn: k["calls"] / nev for kn, k in kern.items()}
     for kn, c in (s.get("counters_avg_per_launch") or {}).items():
         n = kn[5:] if kn.startswith("void ") else kn
         if n.startswith(pre):
             found = True
-            fetch += c.get("FETCH_SIZE", 0.0) * 1024
-            write += c.get("WRITE_SIZE", 0.0) * 1024
-    for kn, k in (s.get("kernels") or {}).items():
+            f = per_eval.get(kn, 1.0)
+            fetch += c.get("FETCH_SIZE", 0.0) * 1024 * f
+            write += c.get("WRITE_SIZE", 0.0) * 1024 * f
+    for kn, k in kern.items():
         n = kn[5:] if kn.startswith("void ") else kn
         if n.startswith(pre):
-            ns += k["avg_ns"]
+            ns += k["avg_ns"] * per_eval[kn]
     if not found:
         return None, s.get("tag")
     return {"raw": fetch + write, "x2read": 2 * fetch + write, "fetch": fetch, "write": write, "avg_ns": ns,
@@ -418,8 +430,11 @@ def main():
                          "traffic_x2read": tr["x2read"] if tr else None,
                          "counter_frac": (tr["raw"] / (dom_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if tr else None,
                          "traffic_source": "profiles/%s_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the "
-                                           "%s kernels, bytes per launch)" % (pmc_tag, dom) if tr else None,
+                                           "%s kernels, bytes per evaluation: every launch of them)" % (pmc_tag, dom)
+                                           if tr else None,
                          "profiled_kernel_ms": tr["avg_ns"] / 1e6 if tr else None,
+                         "profiled_wait_frac": tr.get("wait_frac") if tr else None,
+                         "profiled_l2_hit_rate": tr.get("l2_hit") if tr else None,
                          "kernel": {"walk": "kyv_jit_walk (runtime-compiled pattern walk)",
                                     "cond": "kyv_jit_cond (runtime-compiled deny / foreach conditions)",
                                     "match": "kyv::match_kernel (match / exclude, podSecurity, plain conditions)"}[dom],

@@ -55,31 +55,57 @@ def main(tag):
         w.writeheader()
         w.writerows(rows_out)
     avg = {kn: {c: sum(v) / len(v) for c, v in cs.items()} for kn, cs in counters.items()}
-    fetch = sum(a.get("FETCH_SIZE", 0.0) for a in avg.values()) * 1024
-    write = sum(a.get("WRITE_SIZE", 0.0) for a in avg.values()) * 1024
-    eval_ns = sum(k["avg_ns"] for k in per_kernel.values())
-    dom = max(per_kernel.items(), key=lambda kv: kv[1]["avg_ns"])[0] if per_kernel else None
+    # launches per evaluation: the verdict histogram runs once per evaluation; the other kernels once per rule slice
+    # (10M-resource batches run in two slices) or once per compiled rule (condition kernels)
+    nev = sum(k["calls"] for kn, k in per_kernel.items() if "status_hist" in kn) or 1
+    fac = {kn: k["calls"] / nev for kn, k in per_kernel.items()}
+    fetch = sum(a.get("FETCH_SIZE", 0.0) * fac.get(kn, 1.0) for kn, a in avg.items()) * 1024
+    write = sum(a.get("WRITE_SIZE", 0.0) * fac.get(kn, 1.0) for kn, a in avg.items()) * 1024
+    eval_ns = sum(k["avg_ns"] * fac[kn] for kn, k in per_kernel.items())
+    # per device phase (bench.py PHASE_KERNELS): time, memory-side bytes, stall fraction and L2 hit rate per evaluation
+    phases = {"match": ("kyv::match_kernel",), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv::walk_kernel"),
+              "compact": ("kyv::compact",), "hist": ("kyv::status_hist",)}
+    ph = {}
+    for name, pre in phases.items():
+        ks = [kn for kn in per_kernel if (kn[5:] if kn.startswith("void ") else kn).startswith(pre)]
+        if not ks:
+            continue
+        t = sum(per_kernel[kn]["avg_ns"] * fac[kn] for kn in ks)
+        acc = {}
+        for kn in ks:
+            for c, x in avg.get(kn, {}).items():
+                acc[c] = acc.get(c, 0.0) + x * fac[kn]
+        e = {"ns": t, "kernels": len(ks), "fetch_bytes": acc.get("FETCH_SIZE", 0.0) * 1024,
+             "write_bytes": acc.get("WRITE_SIZE", 0.0) * 1024}
+        e["traffic_bytes"] = e["fetch_bytes"] + e["write_bytes"]
+        e["traffic_GBs"] = e["traffic_bytes"] / max(t, 1.0)
+        if acc.get("SQ_WAVE_CYCLES"):
+            e["wait_frac"] = acc.get("SQ_WAIT_ANY", 0.0) / acc["SQ_WAVE_CYCLES"]
+        if "TCC_HIT_sum" in acc:
+            e["l2_hit_rate"] = acc["TCC_HIT_sum"] / max(1.0, acc["TCC_HIT_sum"] + acc.get("TCC_MISS_sum", 0.0))
+        ph[name] = e
+    dom_phase = max(("match", "cond", "walk"), key=lambda k: ph.get(k, {}).get("ns", 0.0))
+    dom = max(per_kernel.items(), key=lambda kv: kv[1]["avg_ns"] * fac[kv[0]])[0] if per_kernel else None
     out = {
         "tag": tag,
         "kernels": per_kernel,
+        "launches_per_evaluation": fac,
+        "evaluations": nev,
         "eval_avg_ns": eval_ns,
         "dominant_kernel": dom,
+        "dominant_phase": dom_phase,
+        "phases": ph,
         "counters_avg_per_launch": avg,
         "fetch_bytes_raw": fetch,
         "write_bytes_raw": write,
         "traffic_bytes": fetch + write,
         "traffic_bytes_x2read": 2 * fetch + write,
-        "traffic_note": "memory-side bytes of one evaluation (all its kernels) from TCC_EA (FETCH_SIZE + WRITE_SIZE, "
-                        "KiB x 1024); traffic_bytes_x2read applies the guide's x2 wide-stream read correction",
+        "traffic_note": "memory-side bytes of one evaluation (every launch of its kernels) from TCC_EA (FETCH_SIZE + "
+                        "WRITE_SIZE, KiB x 1024); traffic_bytes_x2read applies the guide's x2 wide-stream read correction",
     }
-    if dom and dom in avg:
-        d = avg[dom]
-        if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
-            out["dominant_l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
-        if "SQ_WAVE_CYCLES" in d:
-            out["dominant_wait_frac"] = d.get("SQ_WAIT_ANY", 0) / d["SQ_WAVE_CYCLES"]
-            if "GRBM_GUI_ACTIVE" in d:
-                out["clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8 / per_kernel[dom]["avg_ns"]
+    if dom_phase in ph:
+        out["dominant_l2_hit_rate"] = ph[dom_phase].get("l2_hit_rate")
+        out["dominant_wait_frac"] = ph[dom_phase].get("wait_frac")
     log = os.path.join(src, "bench_trace.log")
     if os.path.exists(log):
         for line in open(log):
