@@ -194,7 +194,7 @@ struct SliceSched {
                                  // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
   std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
   std::vector<uint3> cw;         // compiled condition rules: (rule, first match wave, waves) of its kernel's launch
-  uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
+  uint4* sched = nullptr;        // chunk schedules of the walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // after match, condition, walk, compaction (phase timing)
@@ -695,7 +695,25 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     if (runs.empty() || runs.back().second != g) runs.push_back({w, std::move(g)});
   }
   const uint32_t ncls = 1 + (jit ? (uint32_t)dr->jfns.size() : 0u);  // 0: interpreter, 1 + g: compiled group g
-  std::vector<std::vector<uint2>> slots(ncls);
+  std::vector<std::vector<uint4>> slots(ncls);
+  // chunk slot (kyv_wave.h ChunkMap): rule fields + the chunk's failure-record staging base (slice-local rbase)
+  std::vector<uint32_t> rbase(sl.k1 - sl.k0 + 1, 0);
+  {
+    size_t at = 0;
+    for (uint32_t k = sl.k0; k < sl.k1; k++) {
+      rbase[k - sl.k0] = (uint32_t)at;
+      const RuleDesc& rd = rs.rules[k];
+      at += (rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, MAX_ALTS) : 0) * (size_t)nw * WAVE;
+    }
+  }
+  if (nw > SLOT_WAVE_MASK || sl.k1 > SLOT_RULE_MASK) throw std::runtime_error("walk schedule: batch or ruleset too large for a chunk slot");
+  auto mkslot = [&](uint32_t k, uint32_t w, bool u) {
+    const RuleDesc& rd = rs.rules[k];
+    const uint32_t alts = rd.kind == RK_PATTERN ? 1u : std::min<uint32_t>(rd.nalts, MAX_ALTS);
+    return make_uint4(k | (alts << 24) | (rd.kind == RK_ANYPATTERN ? SLOT_ANY : 0u),
+                      w | (u ? SLOT_UNIFORM : 0u) | ((rd.flags & RD_GATE_EXACT) ? SLOT_GATE_EXACT : 0u),
+                      (uint32_t)(rbase[k - sl.k0] + (size_t)w * WAVE * alts), rd.root);
+  };
   for (size_t ri = 0; ri < runs.size(); ri++) {
     const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
     std::vector<std::vector<uint32_t>> ks(ncls);
@@ -711,7 +729,7 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
           for (size_t t = i; t < i + n; t++) {
             const uint32_t k = ks[cls][t];
             const bool u = uniform[w] && (rs.rules[k].flags & RD_GATE_EXACT);
-            slots[cls].push_back(make_uint2(k, w | (u ? SLOT_UNIFORM : 0u)));
+            slots[cls].push_back(mkslot(k, w, u));
           }
       }
   }
@@ -734,11 +752,11 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     if (xcd && G >= 8 && T > G) {
       std::vector<std::vector<uint32_t>> pos(8);
       for (size_t q = 0; q < T; q++) pos[(q % G) % 8].push_back((uint32_t)q);
-      std::vector<uint2> outv(T);
+      std::vector<uint4> outv(T);
       size_t fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (size_t i = 0; i < T;) {
         size_t j = i;
-        while (j < T && (slots[cls][j].y & ~SLOT_UNIFORM) == (slots[cls][i].y & ~SLOT_UNIFORM)) j++;  // one wave's chunks
+        while (j < T && (slots[cls][j].y & SLOT_WAVE_MASK) == (slots[cls][i].y & SLOT_WAVE_MASK)) j++;  // one wave's chunks
         int best = -1;
         double br = 2.0;
         for (int x = 0; x < 8; x++) {
@@ -794,12 +812,12 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
   }
   dfree(sl.sched);
   sl.sched = nullptr;
-  HIP_OK(dmalloc(&sl.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
+  HIP_OK(dmalloc(&sl.sched, std::max<size_t>(1, tot) * sizeof(uint4)));
   sl.cm.assign(ncls, ChunkMap{nullptr, 0});
   size_t at = 0;
   for (uint32_t cls = 0; cls < ncls; cls++) {
     if (!slots[cls].empty())
-      HIP_OK(hipMemcpy(sl.sched + at, slots[cls].data(), slots[cls].size() * sizeof(uint2), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(sl.sched + at, slots[cls].data(), slots[cls].size() * sizeof(uint4), hipMemcpyHostToDevice));
     sl.cm[cls] = ChunkMap{sl.sched + at, (uint32_t)slots[cls].size()};
     at += slots[cls].size();
   }

@@ -124,6 +124,17 @@ class ScanReport:
                        "severity": m["severity"]}
                 if rules[k]["kind"] == "podSecurity":
                     row["pss_mask"] = self.res.pss_mask(i, k)
+                    # results.go:102-116: properties of the failed PodSecurity checks (IDs sorted, one per failing
+                    # check version, joined with ","); None when the library cannot render the checks (exclusions
+                    # in Go-map order): the CPU engine builds that row
+                    chk = self.res.pss_checks(i, k)
+                    if chk is None:
+                        row["properties"] = None
+                    else:
+                        controls = sorted(c["id"] for c in chk["checks"] if not c["allowed"])
+                        if controls:
+                            row["properties"] = {"standard": chk["level"], "version": chk["version"],
+                                                 "controls": ",".join(controls)}
                 rows.append(row)
                 if s in (K.ST_PASS, K.ST_FAIL):
                     applied += 1

@@ -108,3 +108,54 @@ def test_two_rank_summary_allreduce():
     docs, nsl = synth.mixed(300, seed=43, edge=True)
     full = S.BackgroundScan(policy_set(), backend="cpu").scan(docs, nsl).summary_matrix()
     assert out[0][1] == out[1][1] == full.tolist()
+
+
+_KUTTL_DIR = "test/conformance/kuttl/reports/background/test-report-background-mode"
+
+
+def test_pss_report_row_kuttl_golden():
+    """The PolicyReport row of the kuttl background-scan fixture (_KUTTL_DIR/report-assert.yaml: category, message,
+    policy, result, rule, scored, severity, source) with the properties results.go:102-116 adds for the failed
+    PodSecurity checks: standard / version of the rule, controls = the failing check IDs sorted and joined (one per
+    failing check version, as PodSecurityChecks lists them)."""
+    import test_boundary as TB
+    pol = json.loads(json.dumps(TB._KUTTL_POLICY))
+    pol["metadata"]["annotations"] = {"policies.kyverno.io/category": "Pod Security",
+                                      "policies.kyverno.io/severity": "medium"}  # _KUTTL_DIR/policy.yaml
+    rep = S.BackgroundScan([pol], backend="cpu").scan([TB._KUTTL_POD])
+    rows = rep.results(0)
+    assert len(rows) == 1
+    row = rows[0]
+    line = ("({Allowed:false ForbiddenReason:unrestricted capabilities ForbiddenDetail:container \"container01\" must "
+            "set securityContext.capabilities.drop=[\"ALL\"]})\n")
+    want = {"category": "Pod Security", "policy": "podsecurity-subrule-restricted", "result": "fail",
+            "rule": "restricted", "scored": True, "severity": "medium", "source": "kyverno",
+            "message": "Validation rule 'restricted' failed. It violates PodSecurity \"restricted:latest\": " + line + line}
+    assert {k: row[k] for k in want} == want
+    assert row["properties"] == {"standard": "restricted", "version": "latest",
+                                 "controls": "capabilities_restricted,capabilities_restricted"}
+    assert rep.summary()["podsecurity-subrule-restricted"]["fail"] == 1
+
+
+def test_pss_report_properties_match_oracle_checks():
+    """report-row properties of every failing podSecurity pair of a synthetic corpus equal the ones built from the
+    oracle's PodSecurityChecks (results.go:102-116 restated on the oracle's rule responses)"""
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "psa"},
+           "spec": {"rules": [{"name": "restricted", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                               "validate": {"podSecurity": {"level": "restricted", "version": "latest"}}}]}}
+    docs, nsl = synth.mixed(600, seed=47, edge=True)
+    rep = S.BackgroundScan([pol], backend="cpu").scan(docs, nsl)
+    n = 0
+    for i, d in enumerate(docs):
+        for row in rep.results(i):
+            if row["result"] != "fail":
+                continue
+            ns = (d.get("metadata") or {}).get("namespace") if isinstance(d.get("metadata"), dict) else None
+            o = O.validate([pol], json.dumps(d), (nsl or {}).get(ns) or {})[0]["rules"][0]
+            checks = o.get("pss_checks")  # the oracle lists the failing checks
+            if checks is None or row["properties"] is None:
+                continue
+            controls = sorted(c["id"] for c in checks)
+            assert row["properties"] == {"standard": "restricted", "version": "latest", "controls": ",".join(controls)}
+            n += 1
+    assert n > 50
