@@ -981,6 +981,7 @@ uint32_t compile_pss(Cx& c, const Value& ps) {
     }
   d.excl = (uint32_t)c.rs.pool.size();
   d.nexcl = (uint32_t)recs.size();
+  d.cols = NONE;  // path-column table: build_path_trie (TrieBuilder::pss)
   for (auto r : recs) c.rs.pool.push_back(r);
   c.rs.pss.push_back(d);
   return (uint32_t)c.rs.pss.size() - 1;
@@ -2091,6 +2092,102 @@ struct TrieBuilder {
     for (uint32_t i = 0; i < nany; i++) one(rs.conds[P.any0 + i]);
     for (uint32_t i = 0; i < P.nall; i++) one(rs.conds[P.all0 + i]);
   }
+  // PodSecurity rules (kyv_pss.h pss_checks_cols): the fields the checks read, at the pod positions getSpec
+  // (validation.go:481-532) takes for the rule's kinds, as path columns; the table goes to the rule's PssDesc
+  void pss_rule(const RuleDesc& rd) {
+    if (rd.kind != RK_PSS || rd.root >= rs.pss.size()) return;
+    bool pos[PSS_NPOS] = {false, false, false};
+    bool any = rd.match.mode == MM_NONE || rd.match.nfilters == 0;
+    for (uint32_t i = 0; i < rd.match.nfilters && !any; i++) {
+      const Filter& f = rs.filters[rd.match.filters + i];
+      if (f.nkinds == 0) any = true;
+      for (uint32_t j = 0; j < f.nkinds; j++) {
+        const uint32_t k = rs.kinds[f.kinds + j].kind;
+        if (k == NONE) any = true;
+        else if (k == KSID(POD)) pos[0] = true;
+        else if (k == KSID(DAEMONSET) || k == KSID(DEPLOYMENT) || k == KSID(JOB) || k == KSID(STATEFULSET) ||
+                 k == KSID(REPLICASET) || k == KSID(RC)) pos[1] = true;
+        else if (k == KSID(CRONJOB)) pos[2] = true;
+      }
+    }
+    if (any) pos[0] = pos[1] = pos[2] = true;
+    std::vector<uint32_t> tab(PSS_NPOS * PC_COUNT, NONE);
+    auto col = [&](uint32_t t) { return rs.trie[t].col; };
+    for (uint32_t p = 0; p < PSS_NPOS; p++) {
+      if (!pos[p]) continue;
+      uint32_t* T = tab.data() + p * PC_COUNT;
+      uint32_t t = 0;
+      if (p == 1) t = child(child(t, KSID(SPEC)), KSID(TEMPLATE));
+      if (p == 2) t = child(child(child(child(t, KSID(SPEC)), KSID(JOBTEMPLATE)), KSID(SPEC)), KSID(TEMPLATE));
+      const uint32_t meta = child(t, KSID(METADATA)), spec = child(t, KSID(SPEC));
+      T[PC_ANN] = col(child(meta, KSID(ANNOTATIONS)));
+      const uint32_t psc = child(spec, KSID(SECCTX));
+      T[PC_PSC] = col(psc);
+      T[PC_PSC_NONROOT] = col(child(psc, KSID(RUNASNONROOT)));
+      T[PC_PSC_USER] = col(child(psc, KSID(RUNASUSER)));
+      const uint32_t sel = child(psc, KSID(SELINUX));
+      T[PC_PSC_SEL] = col(sel);
+      T[PC_PSC_SEL_USER] = col(child(sel, KSID(USER)));
+      T[PC_PSC_SEL_ROLE] = col(child(sel, KSID(ROLE)));
+      T[PC_PSC_SEL_TYPE] = col(child(sel, KSID(TYPE)));
+      const uint32_t sec = child(psc, KSID(SECCOMP));
+      T[PC_PSC_SEC] = col(sec);
+      T[PC_PSC_SEC_TYPE] = col(child(sec, KSID(TYPE)));
+      const uint32_t win = child(psc, KSID(WINOPTS));
+      T[PC_PSC_WIN] = col(win);
+      T[PC_PSC_WIN_HP] = col(child(win, KSID(HOSTPROCESS)));
+      T[PC_PSC_SYSCTLS] = col(child(psc, KSID(SYSCTLS)));
+      T[PC_OS_NAME] = col(child(child(spec, KSID(OS)), KSID(NAME)));
+      T[PC_HOSTNET] = col(child(spec, KSID(HOSTNETWORK)));
+      T[PC_HOSTPID] = col(child(spec, KSID(HOSTPID)));
+      T[PC_HOSTIPC] = col(child(spec, KSID(HOSTIPC)));
+      T[PC_VOLUMES] = col(child(spec, KSID(VOLUMES)));
+      const uint32_t lkeys[PSS_NLISTS] = {KSID(INITCONTAINERS), KSID(CONTAINERS), KSID(EPHEMERALCONTAINERS)};
+      for (uint32_t l = 0; l < PSS_NLISTS; l++) {
+        uint32_t* L = T + PC_LISTS + l * PCL_COUNT;
+        const uint32_t lt = child(spec, lkeys[l]), el = star(lt);
+        L[PCL_LEN] = rs.trie[lt].lencol;
+        L[PCL_SELF] = col(el);
+        L[PCL_NAME] = col(child(el, KSID(NAME)));
+        const uint32_t sc = child(el, KSID(SECCTX));
+        L[PCL_SC] = col(sc);
+        L[PCL_PRIV] = col(child(sc, KSID(PRIVILEGED)));
+        L[PCL_APE] = col(child(sc, KSID(APE)));
+        L[PCL_NONROOT] = col(child(sc, KSID(RUNASNONROOT)));
+        L[PCL_USER] = col(child(sc, KSID(RUNASUSER)));
+        const uint32_t csel = child(sc, KSID(SELINUX));
+        L[PCL_SEL] = col(csel);
+        L[PCL_SEL_USER] = col(child(csel, KSID(USER)));
+        L[PCL_SEL_ROLE] = col(child(csel, KSID(ROLE)));
+        L[PCL_SEL_TYPE] = col(child(csel, KSID(TYPE)));
+        const uint32_t csec = child(sc, KSID(SECCOMP));
+        L[PCL_SEC] = col(csec);
+        L[PCL_SEC_TYPE] = col(child(csec, KSID(TYPE)));
+        const uint32_t cwin = child(sc, KSID(WINOPTS));
+        L[PCL_WIN] = col(cwin);
+        L[PCL_WIN_HP] = col(child(cwin, KSID(HOSTPROCESS)));
+        const uint32_t caps = child(sc, KSID(CAPS));
+        L[PCL_CAPS] = col(caps);
+        const uint32_t add = child(caps, KSID(ADD)), adds = star(add);
+        L[PCL_ADD_LEN] = rs.trie[add].lencol;
+        L[PCL_ADD_SELF] = col(adds);
+        const uint32_t drop = child(caps, KSID(DROP)), drops = star(drop);
+        L[PCL_DROP_LEN] = rs.trie[drop].lencol;
+        L[PCL_DROP_SELF] = col(drops);
+        L[PCL_PROC] = col(child(sc, KSID(PROCMOUNT)));
+        const uint32_t ports = child(el, KSID(PORTS)), ps = star(ports);
+        L[PCL_PORTS_LEN] = rs.trie[ports].lencol;
+        L[PCL_PORT_HOSTPORT] = col(child(ps, KSID(HOSTPORT)));
+      }
+    }
+    PssDesc& pd = rs.pss[rd.root];
+    if (pd.cols == NONE) {
+      pd.cols = (uint32_t)rs.pool.size();
+      rs.pool.insert(rs.pool.end(), tab.begin(), tab.end());
+    } else {
+      std::copy(tab.begin(), tab.end(), rs.pool.begin() + pd.cols);
+    }
+  }
   void cond_rule(const RuleDesc& rd) {
     prog(rd.pre, {});
     if (rd.kind == RK_DENY) prog(rd.root, {});
@@ -2242,6 +2339,8 @@ void build_path_trie(Ruleset& rs) {
       for (uint32_t a = 0; a < rd.nalts; a++) tb.walk(rs.pool[rd.root + a], 0, 0);
   }
   for (auto& rd : rs.rules) tb.cond_rule(rd);
+  if (!getenv("KYV_PSS_NOCOLS"))
+    for (auto& rd : rs.rules) tb.pss_rule(rd);
   // entries of pnodes that conflicted after their first visit assigned columns: clear the whole subtree
   // (a conflicting subtree is walked with t == NONE, which already cleared its entries' columns)
 }

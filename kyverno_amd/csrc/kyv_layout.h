@@ -309,8 +309,27 @@ enum PssFlag : uint32_t { PSS_BASELINE = 1, PSS_BAD_VERSION = 2 };
 struct PssDesc {
   uint32_t flags;
   uint32_t excl, nexcl;  // exclusions (u32 pool): control bits, nimages, images...
-  uint32_t pad;
+  uint32_t cols;         // pool offset of the path-column table [PSS_NPOS][PC_COUNT] (NONE: the checks search maps)
 };
+
+// Path columns of the fields the PodSecurity checks read (compiler.cpp TrieBuilder::pss), per pod position of getSpec
+// (validation.go:481-532): 0 Pod (metadata / spec at the root), 1 pod template (spec.template), 2 CronJob
+// (spec.jobTemplate.spec.template). Pod-level fields live in the resource row space; container fields in the row
+// space of their list's elements (three lists: initContainers, containers, ephemeralContainers -- visitContainers
+// order); array fields carry their length column (count, element-0 row) and their elements' self column.
+constexpr uint32_t PSS_NPOS = 3;
+enum PssCol : uint32_t {
+  PC_ANN = 0, PC_PSC, PC_PSC_NONROOT, PC_PSC_USER, PC_PSC_SEL, PC_PSC_SEL_USER, PC_PSC_SEL_ROLE, PC_PSC_SEL_TYPE,
+  PC_PSC_SEC, PC_PSC_SEC_TYPE, PC_PSC_WIN, PC_PSC_WIN_HP, PC_PSC_SYSCTLS, PC_OS_NAME, PC_HOSTNET, PC_HOSTPID,
+  PC_HOSTIPC, PC_VOLUMES, PC_LISTS,  // then PSS_NLISTS x PCL_COUNT list columns
+};
+enum PssListCol : uint32_t {
+  PCL_LEN = 0, PCL_SELF, PCL_NAME, PCL_SC, PCL_PRIV, PCL_APE, PCL_NONROOT, PCL_USER, PCL_SEL, PCL_SEL_USER, PCL_SEL_ROLE,
+  PCL_SEL_TYPE, PCL_SEC, PCL_SEC_TYPE, PCL_WIN, PCL_WIN_HP, PCL_CAPS, PCL_ADD_LEN, PCL_ADD_SELF, PCL_DROP_LEN,
+  PCL_DROP_SELF, PCL_PROC, PCL_PORTS_LEN, PCL_PORT_HOSTPORT, PCL_COUNT
+};
+constexpr uint32_t PSS_NLISTS = 3;
+constexpr uint32_t PC_COUNT = PC_LISTS + PSS_NLISTS * PCL_COUNT;
 
 // ---------------------------------------------------------------- rules
 enum RuleKind : uint8_t { RK_NONE = 0, RK_PATTERN = 1, RK_ANYPATTERN = 2, RK_PSS = 3, RK_FALLBACK = 4, RK_PANIC = 5,

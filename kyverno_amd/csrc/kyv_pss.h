@@ -427,6 +427,201 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
   return fails;
 }
 
+// pss_checks of the resource's own pod (no exclusion sub-pod) after the typed decode was verified, with every field
+// read through its path column (compiler.cpp TrieBuilder::pss_rule; table T of the pod position): the loads of one
+// scope are independent (one round for the pod level, one per container) instead of chains of map searches. Same
+// semantics as pss_checks(decoded); pinned against it and the oracle by the PodSecurity parity tests.
+struct PCol {  // a decoded column entry
+  uint32_t i, t, a;  // node index (NONE: absent), node type, the node's `a`
+};
+KYV_HD PCol pcol(const View& v, uint32_t col, uint32_t row) {
+  PCol c{NONE, 0u, 0u};
+  if (col == NONE || row == NONE) return c;
+  const uint64_t x = v.colv[(size_t)v.col_off[col] + row];
+  const uint32_t lo = (uint32_t)x;
+  if (lo == NONE) return c;
+  c.i = lo & COL_INDEX_MASK;
+  c.t = lo >> COL_TYPE_SHIFT;
+  c.a = (uint32_t)(x >> 32);
+  return c;
+}
+KYV_HD bool pnil(const PCol& c) { return c.i == NONE || c.t == N_NULL; }
+KYV_HD int pbool(const PCol& c) { return c.i == NONE ? -1 : c.t == N_TRUE ? 1 : c.t == N_FALSE ? 0 : -1; }
+KYV_HD uint32_t pstr(const PCol& c) { return (c.i != NONE && c.t == N_STR) ? c.a : SID_EMPTY; }
+KYV_HD bool pobj(const PCol& c) { return c.i != NONE && c.t == N_MAP; }
+// an int64 field: present (decoded: an integer) and its value is zero
+KYV_HD bool pzero(NodeTab R, const PCol& c) { return c.i != NONE && c.t == N_INT && c.a == 0 && R[c.i].b == 0; }
+
+KYV_FN_PSS uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, const uint32_t* T) {
+  uint32_t fails = 0;
+  const PCol psc = pcol(v, T[PC_PSC], row);
+  const bool pscSet = pobj(psc);
+  const PCol osn = pcol(v, T[PC_OS_NAME], row);
+  const bool windows = osn.i != NONE && osn.t == N_STR && osn.a == KSID(WINDOWS);
+  // pod-level security context (the columns of a non-map securityContext have no entries)
+  const PCol pnr = pcol(v, T[PC_PSC_NONROOT], row), pus = pcol(v, T[PC_PSC_USER], row);
+  const PCol psel = pcol(v, T[PC_PSC_SEL], row), psec = pcol(v, T[PC_PSC_SEC], row), pwin = pcol(v, T[PC_PSC_WIN], row);
+  const int podNonRoot = pscSet ? pbool(pnr) : -1;
+  const bool podHasUser = pscSet && pus.i != NONE && pus.t == N_INT;
+  const bool podUserZero = podHasUser && pzero(R, pus);
+  const bool podSelSet = pscSet && pobj(psel);
+  uint32_t pu = SID_EMPTY, pr = SID_EMPTY, pt = SID_EMPTY;
+  if (podSelSet) {
+    pu = pstr(pcol(v, T[PC_PSC_SEL_USER], row));
+    pr = pstr(pcol(v, T[PC_PSC_SEL_ROLE], row));
+    pt = pstr(pcol(v, T[PC_PSC_SEL_TYPE], row));
+  }
+  const bool podSecSet = pscSet && pobj(psec);
+  const uint32_t podSecType = podSecSet ? pstr(pcol(v, T[PC_PSC_SEC_TYPE], row)) : SID_EMPTY;
+  const int podHostProcess = pscSet && pobj(pwin) ? pbool(pcol(v, T[PC_PSC_WIN_HP], row)) : -1;
+
+  const uint32_t capsOK[13] = {KSID(CAP_AUDIT_WRITE), KSID(CAP_CHOWN), KSID(CAP_DAC_OVERRIDE), KSID(CAP_FOWNER),
+                               KSID(CAP_FSETID), KSID(CAP_KILL), KSID(CAP_MKNOD), KSID(NET_BIND_SERVICE),
+                               KSID(CAP_SETFCAP), KSID(CAP_SETGID), KSID(CAP_SETPCAP), KSID(CAP_SETUID),
+                               KSID(CAP_SYS_CHROOT)};
+  const uint32_t selOK[4] = {SID_EMPTY, KSID(CONTAINER_T), KSID(CONTAINER_INIT_T), KSID(CONTAINER_KVM_T)};
+  auto selValid = [&](uint32_t u, uint32_t r, uint32_t t) { return str_in(t, selOK, 4) && u == SID_EMPTY && r == SID_EMPTY; };
+  auto secValid = [&](uint32_t t) { return t == KSID(LOCALHOST) || t == KSID(RUNTIMEDEFAULT); };
+
+  bool apeBad = false, capsBaseBad = false, capsRBad = false, portsBad = false, privBad = false, procBad = false;
+  bool nonRootExplicitBad = false, nonRootImplicitBad = false, userBad = false, selBad = false;
+  bool secBaseBad = false, secRExplicitBad = false, secRImplicitBad = false, hpBad = false, secAnnBad = false;
+  const bool podNonRootTrue = podNonRoot == 1;
+  const bool podSecValid = podSecSet && secValid(podSecType);
+  const PCol annc = pcol(v, T[PC_ANN], row);
+  const uint32_t ann = annc.i;
+  const bool annMap = pobj(annc);
+
+  for (uint32_t l = 0; l < PSS_NLISTS; l++) {
+    const uint32_t* L = T + PC_LISTS + l * PCL_COUNT;
+    if (L[PCL_LEN] == NONE) continue;
+    const uint64_t ln = v.colv[(size_t)v.col_off[L[PCL_LEN]] + row];  // (count, row of element 0)
+    if ((uint32_t)ln == NONE) continue;  // absent, null or not an array (length entries: NONE count)
+    const uint32_t cnt = (uint32_t)ln, eb = (uint32_t)(ln >> 32);
+    for (uint32_t i = 0; i < cnt; i++) {
+      const uint32_t er = eb + i;
+      // every field of the container: independent loads
+      const PCol nm = pcol(v, L[PCL_NAME], er), sc = pcol(v, L[PCL_SC], er);
+      const PCol priv = pcol(v, L[PCL_PRIV], er), ape = pcol(v, L[PCL_APE], er), nr = pcol(v, L[PCL_NONROOT], er);
+      const PCol us = pcol(v, L[PCL_USER], er), sel = pcol(v, L[PCL_SEL], er), sec = pcol(v, L[PCL_SEC], er);
+      const PCol win = pcol(v, L[PCL_WIN], er), caps = pcol(v, L[PCL_CAPS], er), pm = pcol(v, L[PCL_PROC], er);
+      const uint64_t addl = L[PCL_ADD_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_ADD_LEN]] + er];
+      const uint64_t dropl = L[PCL_DROP_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_DROP_LEN]] + er];
+      const uint64_t portl = L[PCL_PORTS_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_PORTS_LEN]] + er];
+      const bool set = pobj(sc);
+      const uint32_t cname = nm.i == NONE || nm.t == N_NULL ? SID_EMPTY : nm.a;
+      const int privileged = set ? pbool(priv) : -1, apev = set ? pbool(ape) : -1, nonRoot = set ? pbool(nr) : -1;
+      if (!set || apev != 0) apeBad = true;
+      if (set && pobj(caps)) {
+        if ((uint32_t)addl != NONE)
+          for (uint32_t j = 0; j < (uint32_t)addl; j++) {
+            const PCol e = pcol(v, L[PCL_ADD_SELF], (uint32_t)(addl >> 32) + j);
+            const uint32_t cap = e.t == N_STR ? e.a : SID_EMPTY;
+            if (!str_in(cap, capsOK, 13)) capsBaseBad = true;
+            if (cap != KSID(NET_BIND_SERVICE)) capsRBad = true;
+          }
+        bool all = false;
+        if ((uint32_t)dropl != NONE)
+          for (uint32_t j = 0; j < (uint32_t)dropl; j++) {
+            const PCol e = pcol(v, L[PCL_DROP_SELF], (uint32_t)(dropl >> 32) + j);
+            if (e.t == N_STR && e.a == KSID(ALL)) all = true;
+          }
+        if (!all) capsRBad = true;
+      } else {
+        capsRBad = true;
+      }
+      if ((uint32_t)portl != NONE)
+        for (uint32_t j = 0; j < (uint32_t)portl; j++) {
+          const PCol hp = pcol(v, L[PCL_PORT_HOSTPORT], (uint32_t)(portl >> 32) + j);
+          if (hp.i != NONE && hp.t == N_INT && (hp.a != 0 || R[hp.i].b != 0)) portsBad = true;
+        }
+      if (set && privileged == 1) privBad = true;
+      if (set && !pnil(pm) && pstr(pm) != KSID(DEFAULT)) procBad = true;
+      if (set && nonRoot != -1) { if (nonRoot == 0) nonRootExplicitBad = true; }
+      else if (!podNonRootTrue) nonRootImplicitBad = true;
+      if (set && us.i != NONE && us.t == N_INT && pzero(R, us)) userBad = true;
+      if (set && pobj(sel) && !selValid(pstr(pcol(v, L[PCL_SEL_USER], er)), pstr(pcol(v, L[PCL_SEL_ROLE], er)),
+                                        pstr(pcol(v, L[PCL_SEL_TYPE], er))))
+        selBad = true;
+      if (set && pobj(sec)) {
+        const uint32_t st = pstr(pcol(v, L[PCL_SEC_TYPE], er));
+        if (st == KSID(UNCONFINED)) secBaseBad = true;
+        if (!secValid(st)) secRExplicitBad = true;
+      } else if (!podSecValid) {
+        secRImplicitBad = true;
+      }
+      if (set && pobj(win) && pbool(pcol(v, L[PCL_WIN_HP], er)) == 1) hpBad = true;
+      // container seccomp annotation: container.seccomp.security.alpha.kubernetes.io/<name> == "unconfined"
+      if (annMap) {
+        const uint32_t pl = v.str_len[KSID(SECCOMP_CONTAINER_PREFIX)], nl = v.str_len[cname];
+        for (uint32_t q = 0; q < R[ann].b; q++) {
+          const Node& e = R[R[ann].a + q];
+          const uint32_t k = node_key(e);
+          if (has_pfx(v, k, SF_PFX_SECCOMP_C) && v.str_len[k] == pl + nl &&
+              bytes_eq(sbytes(v, k) + pl, sbytes(v, cname), nl) && node_type(e) == N_STR && e.a == KSID(UNCONFINED_LC))
+            secAnnBad = true;
+        }
+      }
+    }
+  }
+  if (apeBad) fails |= 1u << PS_APE_1_8;
+  if (apeBad && !windows) fails |= 1u << PS_APE_1_25;
+  if (annMap)
+    for (uint32_t q = 0; q < R[ann].b; q++) {
+      const Node& e = R[R[ann].a + q];
+      const uint32_t val = node_type(e) == N_STR ? e.a : SID_EMPTY;
+      if (has_pfx(v, node_key(e), SF_PFX_APPARMOR) && val != KSID(RUNTIME_DEFAULT_PROFILE) &&
+          !has_pfx(v, val, SF_PFX_LOCALHOST))
+        fails |= 1u << PS_APPARMOR;
+      if (node_key(e) == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = true;
+    }
+  if (capsBaseBad) fails |= 1u << PS_CAPS_BASE;
+  if (capsRBad) fails |= 1u << PS_CAPS_R_1_22;
+  if (capsRBad && !windows) fails |= 1u << PS_CAPS_R_1_25;
+  if (pcol(v, T[PC_HOSTNET], row).t == N_TRUE || pcol(v, T[PC_HOSTPID], row).t == N_TRUE ||
+      pcol(v, T[PC_HOSTIPC], row).t == N_TRUE)
+    fails |= 1u << PS_HOSTNS;
+  const PCol vols = pcol(v, T[PC_VOLUMES], row);
+  if (vols.i != NONE && vols.t == N_ARR)
+    for (uint32_t i = 0; i < R[vols.i].b; i++) {
+      const uint32_t vn = R[vols.i].a + i;
+      bool okv = false;
+      if (node_type(R[vn]) == N_MAP)
+        for (uint32_t q = 0; q < R[vn].b; q++) {
+          const Node& e = R[R[vn].a + q];
+          if (node_type(e) == N_NULL) continue;
+          const uint32_t k = node_key(e);
+          if (k == VSID(hostPath)) fails |= 1u << PS_HOSTPATH;
+          if (k >= SID_FIRST_FREE + K_COUNT && k < SID_FIRST_FREE + K_COUNT + V_ALLOWED) okv = true;
+        }
+      if (!okv) fails |= 1u << PS_RVOLUMES;
+    }
+  if (portsBad) fails |= 1u << PS_HOSTPORTS;
+  if (privBad) fails |= 1u << PS_PRIVILEGED;
+  if (procBad) fails |= 1u << PS_PROCMOUNT;
+  if (podNonRoot == 0 || nonRootExplicitBad || nonRootImplicitBad) fails |= 1u << PS_RUNASNONROOT;
+  if (podUserZero || userBad) fails |= 1u << PS_RUNASUSER;
+  if ((podSelSet && !selValid(pu, pr, pt)) || selBad) fails |= 1u << PS_SELINUX;
+  if (secAnnBad) fails |= 1u << PS_SECCOMP_B_1_0;
+  if ((podSecSet && podSecType == KSID(UNCONFINED)) || secBaseBad) fails |= 1u << PS_SECCOMP_B_1_19;
+  const bool secR = (podSecSet && !secValid(podSecType)) || secRExplicitBad || secRImplicitBad;
+  if (secR) fails |= 1u << PS_SECCOMP_R_1_19;
+  if (secR && !windows) fails |= 1u << PS_SECCOMP_R_1_25;
+  if (pscSet) {
+    const PCol sy = pcol(v, T[PC_PSC_SYSCTLS], row);
+    const uint32_t ok5[5] = {KSID(SYSCTL_SHM), KSID(SYSCTL_PORTRANGE), KSID(SYSCTL_SYNCOOKIES), KSID(SYSCTL_PINGRANGE),
+                             KSID(SYSCTL_UNPRIV)};
+    if (sy.i != NONE && sy.t == N_ARR)
+      for (uint32_t i = 0; i < R[sy.i].b; i++) {
+        const uint32_t nm = get(R, R[sy.i].a + i, KSID(NAME));
+        const uint32_t sname = nil(R, nm) ? SID_EMPTY : R[nm].a;
+        if (!str_in(sname, ok5, 5)) fails |= 1u << PS_SYSCTLS;
+      }
+  }
+  if (podHostProcess == 1 || hpBad) fails |= 1u << PS_WINHOSTPROCESS;
+  return fails;
+}
+
 // check-id groups: slots belonging to one check ID (exemptKyvernoExclusion removes whole IDs)
 KYV_HD uint32_t pss_id_slots(uint32_t slot) {
   switch (slot) {
@@ -484,6 +679,24 @@ KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const R
   if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
   // the typed decode was done by the flattener when it could (RF_PSS_DONE); else here
   const bool done = (h.flags & RF_PSS_DONE) != 0;
+  // path-column form of the checks: the flattener verified the typed decode (so the pod exists at the position of
+  // the resource's kind), the rule has a column table and the resource has path columns
+  if (done && pd.cols != NONE && pd.nexcl == 0 && v.colv && h.nnodes < (1u << COL_TYPE_SHIFT)) {
+    if (h.flags & RF_PSS_DEC_ERR) return ST_ERROR;
+    const uint32_t pos = h.kind == KSID(POD) ? 0u
+                       : (h.kind == KSID(DAEMONSET) || h.kind == KSID(DEPLOYMENT) || h.kind == KSID(JOB) ||
+                          h.kind == KSID(STATEFULSET) || h.kind == KSID(REPLICASET) || h.kind == KSID(RC)) ? 1u
+                       : h.kind == KSID(CRONJOB) ? 2u : NONE;
+    if (pos == NONE) return ST_PANIC;  // no pod spec for this kind (validation.go:542-543)
+    const uint32_t* T = v.pool + pd.cols + pos * PC_COUNT;
+    if (T[PC_PSC] != NONE) {  // the table has this position (the rule's kinds)
+      const uint32_t row = (uint32_t)(&h - v.hdr);
+      const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
+      const uint32_t fails = pss_checks_cols(v, R, row, T) & mask;
+      *fails_out = fails;
+      return fails ? ST_FAIL : ST_PASS;
+    }
+  }
   uint32_t meta = NONE, spec = NONE;
   const uint8_t ps = pss_pod(R, h.kind, !done, &meta, &spec);
   if (ps != ST_NONE) return ps;
