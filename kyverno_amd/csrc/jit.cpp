@@ -1439,37 +1439,12 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     }
     // the root scope's column preload is issued before the lane's walk predicate is known: it depends on the
     // resource row only, so its loads overlap the header loads the predicate waits for (one memory round, not two)
-    // the rule's metadata-site base (RuleDesc.meta_sites) is loaded only by patterns with metadata-expansion sites
-    // (walk_chunks passes the rule index: the chunk slot carries the other rule fields the walk needs)
-    std::function<bool(uint32_t, int)> any_meta = [&](uint32_t pn, int guard) -> bool {
-      if (pn == NONE || pn >= rs.pnodes.size() || guard > 4 * MAX_DEPTH) return false;
-      const PNode& P = rs.pnodes[pn];
-      if (P.kind == P_MAP) {
-        if (P.flags & PF_META) return true;
-        for (uint32_t e = 0; e < P.n; e++) {
-          const PEntry& E = rs.pentries[P.first + e];
-          if (E.child == NONE || E.handler == H_STAR || E.handler == H_NEGATION || E.handler == H_EXIST_BADPAT) continue;
-          if (E.handler == H_EXISTENCE) {
-            for (uint32_t j = 0; j < rs.pool[E.child]; j++) if (any_meta(rs.pool[E.child + 1 + j], guard + 1)) return true;
-          } else if (any_meta(E.child, guard + 1)) {
-            return true;
-          }
-        }
-        return false;
-      }
-      if (P.kind == P_ARR_MAPS) return any_meta(P.first, guard + 1);
-      if (P.kind == P_ARR_POS) {
-        for (uint32_t i = 0; i < P.n; i++) if (any_meta(rs.pool[P.first + i], guard + 1)) return true;
-      }
-      return false;
-    };
     for (uint32_t r : roots)
       if (rep_of[r] == r)  // one root function per pattern shape
       src << "static __device__ __forceinline__ void root" << r
-          << "(const View& v, const Node* R, const ResHeader* hp, uint32_t rule, bool rootmap, bool walk, PatOut& out) {\n"
+          << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, bool rootmap, bool walk, PatOut& out) {\n"
              "  const uint32_t row0 = (uint32_t)(hp - v.hdr), row = row0 < v.nres ? row0 : NONE;\n"
              "  " << g.preload(r, "pc", "row", "jc_col(v, ") << "\n"
-             "  const uint32_t mbase = " << (any_meta(r, 0) ? "sld32(&v.rules[rule].meta_sites)" : "((void)rule, 0u)") << ";\n"
              "  if (!walk) return;\n"
              "#ifdef KYV_EXP_JIT_PRELOAD\n  { uint64_t x = 0; for (auto q : pc) x ^= q; out.status = x == 0x123456789ull ? ST_FAIL : ST_PASS; return; }\n#endif\n"
              "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"

@@ -193,8 +193,9 @@ struct SliceSched {
   uint32_t nm = 0, nmj = 0, nmc = 0;  // [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
                                  // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
   std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
+  std::vector<uint3> pw;         // PodSecurity rules on pss_kernel: (rule, first match wave, waves)
   std::vector<uint3> cw;         // compiled condition rules: (rule, first match wave, waves) of its kernel's launch
-  uint4* sched = nullptr;        // chunk schedules of the walk kernels (ChunkMap slots)
+  uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // after match, condition, walk, compaction (phase timing)
@@ -420,6 +421,42 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_
       const uint32_t ps = o.pss_slot[k];
       if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
     }
+  }
+}
+
+// PodSecurity rules (without preconditions): one lane per resource over the match waves [w0, w0 + grid) of the rule's
+// kind gate, the match and the path-column checks inlined (eval_pss_cols); in the match kernel the checks are an
+// out-of-line call whose callee-saved registers go through scratch memory. Pairs the column form does not cover
+// (exclusion sub-pods, resources without path columns) take the out-of-line map walk (eval_pss).
+// kExact: the rule's match block is its kind gate (RD_GATE_EXACT), no match program compiled in; kWpe: occupancy
+// target (KYV_PSS_WPE = 4 / 6 / 8 at run time; 8 by default)
+template <bool kExact, int kWpe>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
+pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
+  const View& v = *vp;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t r = (w0 + blockIdx.x) * BLOCK + lane;
+  const bool gated = r < v.nres && ((v.gate[(size_t)v.hdr[r].kclass * v.gate_words + (k >> 5)] >> (k & 31)) & 1u);
+  if (!__ballot(gated)) return;
+  const RuleDesc& rd = v.rules[k];
+  uint8_t st = ST_NONE;
+  uint32_t pf = 0;
+  bool m;
+  if constexpr (kExact) {
+    m = rd.kind == RK_PSS;  // pair_match of a kind-gate rule: matched (a fallback rule never gets here)
+  } else {
+    m = gated && pair_match(v, r, rd, &st);
+  }
+  if (gated && m) {
+    const ResHeader& h = v.hdr[r];
+    const NodeTab R{v.nodes + h.root};
+    st = eval_pss_cols(v, v.pss[rd.root], h, R, &pf);
+    if (st == ST_NONE) st = eval_pss(v, v.pss[rd.root], R, h, &pf);
+  }
+  if (gated && st != ST_NONE) {
+    o.status[(size_t)k * v.nres + r] = st;
+    const uint32_t ps = o.pss_slot[k];
+    if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
   }
 }
 
@@ -695,25 +732,7 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     if (runs.empty() || runs.back().second != g) runs.push_back({w, std::move(g)});
   }
   const uint32_t ncls = 1 + (jit ? (uint32_t)dr->jfns.size() : 0u);  // 0: interpreter, 1 + g: compiled group g
-  std::vector<std::vector<uint4>> slots(ncls);
-  // chunk slot (kyv_wave.h ChunkMap): rule fields + the chunk's failure-record staging base (slice-local rbase)
-  std::vector<uint32_t> rbase(sl.k1 - sl.k0 + 1, 0);
-  {
-    size_t at = 0;
-    for (uint32_t k = sl.k0; k < sl.k1; k++) {
-      rbase[k - sl.k0] = (uint32_t)at;
-      const RuleDesc& rd = rs.rules[k];
-      at += (rd.kind == RK_PATTERN ? 1 : rd.kind == RK_ANYPATTERN ? std::min<uint32_t>(rd.nalts, MAX_ALTS) : 0) * (size_t)nw * WAVE;
-    }
-  }
-  if (nw > SLOT_WAVE_MASK || sl.k1 > SLOT_RULE_MASK) throw std::runtime_error("walk schedule: batch or ruleset too large for a chunk slot");
-  auto mkslot = [&](uint32_t k, uint32_t w, bool u) {
-    const RuleDesc& rd = rs.rules[k];
-    const uint32_t alts = rd.kind == RK_PATTERN ? 1u : std::min<uint32_t>(rd.nalts, MAX_ALTS);
-    return make_uint4(k | (alts << 24) | (rd.kind == RK_ANYPATTERN ? SLOT_ANY : 0u),
-                      w | (u ? SLOT_UNIFORM : 0u) | ((rd.flags & RD_GATE_EXACT) ? SLOT_GATE_EXACT : 0u),
-                      (uint32_t)(rbase[k - sl.k0] + (size_t)w * WAVE * alts), rd.root);
-  };
+  std::vector<std::vector<uint2>> slots(ncls);
   for (size_t ri = 0; ri < runs.size(); ri++) {
     const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
     std::vector<std::vector<uint32_t>> ks(ncls);
@@ -729,7 +748,7 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
           for (size_t t = i; t < i + n; t++) {
             const uint32_t k = ks[cls][t];
             const bool u = uniform[w] && (rs.rules[k].flags & RD_GATE_EXACT);
-            slots[cls].push_back(mkslot(k, w, u));
+            slots[cls].push_back(make_uint2(k, w | (u ? SLOT_UNIFORM : 0u)));
           }
       }
   }
@@ -752,11 +771,11 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     if (xcd && G >= 8 && T > G) {
       std::vector<std::vector<uint32_t>> pos(8);
       for (size_t q = 0; q < T; q++) pos[(q % G) % 8].push_back((uint32_t)q);
-      std::vector<uint4> outv(T);
+      std::vector<uint2> outv(T);
       size_t fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (size_t i = 0; i < T;) {
         size_t j = i;
-        while (j < T && (slots[cls][j].y & SLOT_WAVE_MASK) == (slots[cls][i].y & SLOT_WAVE_MASK)) j++;  // one wave's chunks
+        while (j < T && (slots[cls][j].y & ~SLOT_UNIFORM) == (slots[cls][i].y & ~SLOT_UNIFORM)) j++;  // one wave's chunks
         int best = -1;
         double br = 2.0;
         for (int x = 0; x < 8; x++) {
@@ -778,7 +797,23 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
   // match-phase rule list: light rules, then the JMESPath / foreach rules the interpreted match_kernel<true> runs,
   // then those the compiled kyv_jit_cond runs
   {
-    std::vector<uint32_t> mr = sl.ml, cj;
+    // PodSecurity rules without preconditions: pss_kernel over the waves of their kind gate (KYV_PSS_KERNEL=0: the
+    // match kernel)
+    static const bool pss_k = !getenv("KYV_PSS_KERNEL") || atoi(getenv("KYV_PSS_KERNEL")) != 0;
+    std::vector<uint32_t> mr, cj;
+    sl.pw.clear();
+    for (uint32_t q : sl.ml) {
+      const RuleDesc& rd = rs.rules[q];
+      if (!pss_k || rd.kind != RK_PSS || rd.pre != NONE) { mr.push_back(q); continue; }
+      uint32_t lo = nw, hi = 0;
+      for (size_t ri = 0; ri < runs.size(); ri++) {
+        if (!((runs[ri].second[q / 32] >> (q % 32)) & 1u)) continue;
+        lo = std::min(lo, runs[ri].first);
+        hi = std::max(hi, ri + 1 < runs.size() ? runs[ri + 1].first : nw);
+      }
+      if (lo < hi) sl.pw.push_back(make_uint3(q, lo, hi - lo));
+    }
+    const size_t nlight = mr.size();
     // KYV_JC_ONLY=k1,k2,...: timing experiments only (the compiled condition kernel runs just those rules; the
     // other condition rules' verdicts are left unset)
     std::vector<uint32_t> only;
@@ -801,8 +836,8 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
         mr.push_back(q);
       }
     }
-    sl.nm = (uint32_t)sl.ml.size();
-    sl.nmj = (uint32_t)(mr.size() - sl.ml.size());
+    sl.nm = (uint32_t)nlight;
+    sl.nmj = (uint32_t)(mr.size() - nlight);
     sl.nmc = (uint32_t)cj.size();
     mr.insert(mr.end(), cj.begin(), cj.end());
     dfree(sl.mrules);
@@ -812,12 +847,12 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
   }
   dfree(sl.sched);
   sl.sched = nullptr;
-  HIP_OK(dmalloc(&sl.sched, std::max<size_t>(1, tot) * sizeof(uint4)));
+  HIP_OK(dmalloc(&sl.sched, std::max<size_t>(1, tot) * sizeof(uint2)));
   sl.cm.assign(ncls, ChunkMap{nullptr, 0});
   size_t at = 0;
   for (uint32_t cls = 0; cls < ncls; cls++) {
     if (!slots[cls].empty())
-      HIP_OK(hipMemcpy(sl.sched + at, slots[cls].data(), slots[cls].size() * sizeof(uint4), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(sl.sched + at, slots[cls].data(), slots[cls].size() * sizeof(uint2), hipMemcpyHostToDevice));
     sl.cm[cls] = ChunkMap{sl.sched + at, (uint32_t)slots[cls].size()};
     at += slots[cls].size();
   }
@@ -986,6 +1021,15 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       if (sl.nmj)
         hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
                            (const uint32_t*)sl.mrules + sl.nm, sl.nmj);
+      {
+        static const int pwpe = getenv("KYV_PSS_WPE") ? atoi(getenv("KYV_PSS_WPE")) : 8;  // C2: 4 0.586, 6 0.587, 8 0.514 ms
+        for (const uint3& c : sl.pw) {
+          const bool ex = (rs.rules[c.x].flags & RD_GATE_EXACT) && rs.rules[c.x].match.mode != MM_NONE;
+          auto kf = ex ? (pwpe == 4 ? pss_kernel<true, 4> : pwpe == 6 ? pss_kernel<true, 6> : pss_kernel<true, 8>)
+                       : (pwpe == 4 ? pss_kernel<false, 4> : pwpe == 6 ? pss_kernel<false, 6> : pss_kernel<false, 8>);
+          hipLaunchKernelGGL(kf, dim3(c.z), dim3(BLOCK), 0, stream, (const View*)d.view, o, c.x, c.y);
+        }
+      }
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(sl.ev[0], stream));
       // compiled condition rules: one kernel each over the waves of its kind gate

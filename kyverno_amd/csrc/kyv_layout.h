@@ -286,6 +286,9 @@ enum WellKnown : uint32_t {
   K_COUNT
 };
 #define KSID(id) (SID_FIRST_FREE + K_##id)
+// sid ranges the path-column PodSecurity checks test (kyv_pss.h pss_checks_cols)
+static_assert(K_CAP_SYS_CHROOT - K_CAP_AUDIT_WRITE == 11 && K_CONTAINER_KVM_T - K_CONTAINER_T == 2 &&
+              K_SYSCTL_UNPRIV - K_SYSCTL_SHM == 4, "well-known string ranges");
 
 // typed VolumeSource members: the 8 allowed by restrictedVolumes first, then the reference switch order
 // used to name a forbidden source (pod-security-admission policy/check_restrictedVolumes.go)

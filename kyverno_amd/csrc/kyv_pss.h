@@ -452,7 +452,7 @@ KYV_HD bool pobj(const PCol& c) { return c.i != NONE && c.t == N_MAP; }
 // an int64 field: present (decoded: an integer) and its value is zero
 KYV_HD bool pzero(NodeTab R, const PCol& c) { return c.i != NONE && c.t == N_INT && c.a == 0 && R[c.i].b == 0; }
 
-KYV_FN_PSS uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, const uint32_t* T) {
+KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, const uint32_t* T) {
   uint32_t fails = 0;
   const PCol psc = pcol(v, T[PC_PSC], row);
   const bool pscSet = pobj(psc);
@@ -475,12 +475,13 @@ KYV_FN_PSS uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, cons
   const uint32_t podSecType = podSecSet ? pstr(pcol(v, T[PC_PSC_SEC_TYPE], row)) : SID_EMPTY;
   const int podHostProcess = pscSet && pobj(pwin) ? pbool(pcol(v, T[PC_PSC_WIN_HP], row)) : -1;
 
-  const uint32_t capsOK[13] = {KSID(CAP_AUDIT_WRITE), KSID(CAP_CHOWN), KSID(CAP_DAC_OVERRIDE), KSID(CAP_FOWNER),
-                               KSID(CAP_FSETID), KSID(CAP_KILL), KSID(CAP_MKNOD), KSID(NET_BIND_SERVICE),
-                               KSID(CAP_SETFCAP), KSID(CAP_SETGID), KSID(CAP_SETPCAP), KSID(CAP_SETUID),
-                               KSID(CAP_SYS_CHROOT)};
-  const uint32_t selOK[4] = {SID_EMPTY, KSID(CONTAINER_T), KSID(CONTAINER_INIT_T), KSID(CONTAINER_KVM_T)};
-  auto selValid = [&](uint32_t u, uint32_t r, uint32_t t) { return str_in(t, selOK, 4) && u == SID_EMPTY && r == SID_EMPTY; };
+  // the allowed sets as sid ranges of the seeded well-known strings (no local arrays: they would live in scratch)
+  auto capOK = [](uint32_t c) {
+    return (c >= KSID(CAP_AUDIT_WRITE) && c <= KSID(CAP_SYS_CHROOT)) || c == KSID(NET_BIND_SERVICE);
+  };
+  auto selValid = [&](uint32_t u, uint32_t r, uint32_t t) {
+    return (t == SID_EMPTY || (t >= KSID(CONTAINER_T) && t <= KSID(CONTAINER_KVM_T))) && u == SID_EMPTY && r == SID_EMPTY;
+  };
   auto secValid = [&](uint32_t t) { return t == KSID(LOCALHOST) || t == KSID(RUNTIMEDEFAULT); };
 
   bool apeBad = false, capsBaseBad = false, capsRBad = false, portsBad = false, privBad = false, procBad = false;
@@ -491,6 +492,18 @@ KYV_FN_PSS uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, cons
   const PCol annc = pcol(v, T[PC_ANN], row);
   const uint32_t ann = annc.i;
   const bool annMap = pobj(annc);
+  // one pass over the annotations: the appArmor and pod seccomp annotation checks, and whether any key carries the
+  // container seccomp prefix (the per-container check below then runs only for such pods)
+  bool annSecC = false;
+  if (annMap)
+    for (uint32_t q = 0; q < R[ann].b; q++) {
+      const Node& e = R[R[ann].a + q];
+      const uint32_t key = node_key(e), val = node_type(e) == N_STR ? e.a : SID_EMPTY;
+      if (has_pfx(v, key, SF_PFX_APPARMOR) && val != KSID(RUNTIME_DEFAULT_PROFILE) && !has_pfx(v, val, SF_PFX_LOCALHOST))
+        fails |= 1u << PS_APPARMOR;
+      if (key == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = true;
+      if (has_pfx(v, key, SF_PFX_SECCOMP_C)) annSecC = true;
+    }
 
   for (uint32_t l = 0; l < PSS_NLISTS; l++) {
     const uint32_t* L = T + PC_LISTS + l * PCL_COUNT;
@@ -517,7 +530,7 @@ KYV_FN_PSS uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, cons
           for (uint32_t j = 0; j < (uint32_t)addl; j++) {
             const PCol e = pcol(v, L[PCL_ADD_SELF], (uint32_t)(addl >> 32) + j);
             const uint32_t cap = e.t == N_STR ? e.a : SID_EMPTY;
-            if (!str_in(cap, capsOK, 13)) capsBaseBad = true;
+            if (!capOK(cap)) capsBaseBad = true;
             if (cap != KSID(NET_BIND_SERVICE)) capsRBad = true;
           }
         bool all = false;
@@ -552,7 +565,7 @@ KYV_FN_PSS uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, cons
       }
       if (set && pobj(win) && pbool(pcol(v, L[PCL_WIN_HP], er)) == 1) hpBad = true;
       // container seccomp annotation: container.seccomp.security.alpha.kubernetes.io/<name> == "unconfined"
-      if (annMap) {
+      if (annSecC) {
         const uint32_t pl = v.str_len[KSID(SECCOMP_CONTAINER_PREFIX)], nl = v.str_len[cname];
         for (uint32_t q = 0; q < R[ann].b; q++) {
           const Node& e = R[R[ann].a + q];
@@ -566,15 +579,6 @@ KYV_FN_PSS uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, cons
   }
   if (apeBad) fails |= 1u << PS_APE_1_8;
   if (apeBad && !windows) fails |= 1u << PS_APE_1_25;
-  if (annMap)
-    for (uint32_t q = 0; q < R[ann].b; q++) {
-      const Node& e = R[R[ann].a + q];
-      const uint32_t val = node_type(e) == N_STR ? e.a : SID_EMPTY;
-      if (has_pfx(v, node_key(e), SF_PFX_APPARMOR) && val != KSID(RUNTIME_DEFAULT_PROFILE) &&
-          !has_pfx(v, val, SF_PFX_LOCALHOST))
-        fails |= 1u << PS_APPARMOR;
-      if (node_key(e) == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = true;
-    }
   if (capsBaseBad) fails |= 1u << PS_CAPS_BASE;
   if (capsRBad) fails |= 1u << PS_CAPS_R_1_22;
   if (capsRBad && !windows) fails |= 1u << PS_CAPS_R_1_25;
@@ -609,13 +613,11 @@ KYV_FN_PSS uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, cons
   if (secR && !windows) fails |= 1u << PS_SECCOMP_R_1_25;
   if (pscSet) {
     const PCol sy = pcol(v, T[PC_PSC_SYSCTLS], row);
-    const uint32_t ok5[5] = {KSID(SYSCTL_SHM), KSID(SYSCTL_PORTRANGE), KSID(SYSCTL_SYNCOOKIES), KSID(SYSCTL_PINGRANGE),
-                             KSID(SYSCTL_UNPRIV)};
     if (sy.i != NONE && sy.t == N_ARR)
       for (uint32_t i = 0; i < R[sy.i].b; i++) {
         const uint32_t nm = get(R, R[sy.i].a + i, KSID(NAME));
         const uint32_t sname = nil(R, nm) ? SID_EMPTY : R[nm].a;
-        if (!str_in(sname, ok5, 5)) fails |= 1u << PS_SYSCTLS;
+        if (!(sname >= KSID(SYSCTL_SHM) && sname <= KSID(SYSCTL_UNPRIV))) fails |= 1u << PS_SYSCTLS;
       }
   }
   if (podHostProcess == 1 || hpBad) fails |= 1u << PS_WINHOSTPROCESS;
@@ -674,28 +676,38 @@ KYV_HD uint8_t pss_pod(NodeTab R, uint32_t kind, bool decode, uint32_t* meta_out
 }
 
 // validatePodSecurity (validation.go:535-566) -> status; *fails receives the remaining failing slots
+// kCols: the decoded pod's checks through path columns only (pss_kernel: inlined, no call frame); the caller routes
+// pairs that need the map walk (exclusions, no columns, typed decode not done) elsewhere
+// (returns ST_NONE with *fails_out = 0 when the column form does not apply)
+KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const PssDesc& pd, const ResHeader& h,
+                                                            NodeTab R, uint32_t* fails_out) {
+  *fails_out = 0;
+  if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
+  if (!(h.flags & RF_PSS_DONE) || pd.cols == NONE || pd.nexcl != 0 || !v.colv || h.nnodes >= (1u << COL_TYPE_SHIFT))
+    return ST_NONE;
+  if (h.flags & RF_PSS_DEC_ERR) return ST_ERROR;
+  const uint32_t pos = h.kind == KSID(POD) ? 0u
+                     : (h.kind == KSID(DAEMONSET) || h.kind == KSID(DEPLOYMENT) || h.kind == KSID(JOB) ||
+                        h.kind == KSID(STATEFULSET) || h.kind == KSID(REPLICASET) || h.kind == KSID(RC)) ? 1u
+                     : h.kind == KSID(CRONJOB) ? 2u : NONE;
+  if (pos == NONE) return ST_PANIC;  // no pod spec for this kind (validation.go:542-543)
+  const uint32_t* T = v.pool + pd.cols + pos * PC_COUNT;
+  if (T[PC_PSC] == NONE) return ST_NONE;  // the table lacks this position (the rule's kinds)
+  const uint32_t row = (uint32_t)(&h - v.hdr);
+  const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
+  const uint32_t fails = pss_checks_cols(v, R, row, T) & mask;
+  *fails_out = fails;
+  return fails ? ST_FAIL : ST_PASS;
+}
+
 KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out) {
   *fails_out = 0;
   if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
   // the typed decode was done by the flattener when it could (RF_PSS_DONE); else here
   const bool done = (h.flags & RF_PSS_DONE) != 0;
-  // path-column form of the checks: the flattener verified the typed decode (so the pod exists at the position of
-  // the resource's kind), the rule has a column table and the resource has path columns
-  if (done && pd.cols != NONE && pd.nexcl == 0 && v.colv && h.nnodes < (1u << COL_TYPE_SHIFT)) {
-    if (h.flags & RF_PSS_DEC_ERR) return ST_ERROR;
-    const uint32_t pos = h.kind == KSID(POD) ? 0u
-                       : (h.kind == KSID(DAEMONSET) || h.kind == KSID(DEPLOYMENT) || h.kind == KSID(JOB) ||
-                          h.kind == KSID(STATEFULSET) || h.kind == KSID(REPLICASET) || h.kind == KSID(RC)) ? 1u
-                       : h.kind == KSID(CRONJOB) ? 2u : NONE;
-    if (pos == NONE) return ST_PANIC;  // no pod spec for this kind (validation.go:542-543)
-    const uint32_t* T = v.pool + pd.cols + pos * PC_COUNT;
-    if (T[PC_PSC] != NONE) {  // the table has this position (the rule's kinds)
-      const uint32_t row = (uint32_t)(&h - v.hdr);
-      const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
-      const uint32_t fails = pss_checks_cols(v, R, row, T) & mask;
-      *fails_out = fails;
-      return fails ? ST_FAIL : ST_PASS;
-    }
+  {
+    const uint8_t c = eval_pss_cols(v, pd, h, R, fails_out);  // path-column form when it applies
+    if (c != ST_NONE) return c;
   }
   uint32_t meta = NONE, spec = NONE;
   const uint8_t ps = pss_pod(R, h.kind, !done, &meta, &spec);

@@ -262,7 +262,7 @@ struct WaveWalker {
     out.status = walk ? ST_PASS : ST_NONE;
     return;
 #endif
-    const uint32_t meta_base = sld32(&v.rules[rd.meta_sites].meta_sites);  // walk_chunks passes the rule index
+    const uint32_t meta_base = rd.meta_sites;
 
     int sp = 0;
     // top frame (uniform)
@@ -728,48 +728,32 @@ __device__ __forceinline__ uint32_t sld8(const uint8_t* p) {  // scalar load of 
 // Chunk schedule of a walk kernel, laid out on the host as one (rule, match wave) pair per slot: runs of match
 // waves with the same gated rule set, each run wave-major with its rules in windows of a few rules. Slots whose
 // work list is empty (no pair matched) are skipped.
-// A slot carries what the walk needs of its rule, so a chunk starts with one 16-byte scalar load (prefetched one
-// chunk ahead) instead of slot -> RuleDesc -> staging-base loads in sequence:
-//   x: rule index (bits 0..23) | alternatives walked << 24 (bits 24..27, <= MAX_ALTS) | SLOT_ANY
-//   y: match wave (bits 0..29) | SLOT_GATE_EXACT | SLOT_UNIFORM
-//   z: first failure-record staging slot of the chunk (DevOut.stage index)
-//   w: RuleDesc.root (pattern root pnode / pool offset of the alternatives' roots)
 struct ChunkMap {
-  const uint4* slots;  // [total]
+  const uint2* slots;  // [total] (rule, match wave | SLOT_UNIFORM)
   uint32_t total;
 };
 // slot flag: every resource of the match wave has the same kind class, so a direct-walk (RD_GATE_EXACT) rule the
 // schedule lists for the wave gates all of its lanes: the chunk skips the per-lane kind-class -> gate-word loads
 constexpr uint32_t SLOT_UNIFORM = 1u << 31;
-constexpr uint32_t SLOT_GATE_EXACT = 1u << 30;  // the rule's match block is its kind gate (RD_GATE_EXACT)
-constexpr uint32_t SLOT_WAVE_MASK = (1u << 30) - 1;
-constexpr uint32_t SLOT_RULE_MASK = (1u << 24) - 1;
-constexpr uint32_t SLOT_ANY = 1u << 28;     // anyPattern rule
 
 // Grid-stride over the schedule; every wave walks ONE rule over the (up to 64) resources of one work list;
 // verdict bytes and records as in match_kernel (the status counts are one histogram pass afterwards).
 template <class Walker>
 __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists wl, ChunkMap cm, Walker& wk) {
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  uint4 next = blockIdx.x < cm.total ? sld(cm.slots + blockIdx.x) : make_uint4(0u, 0u, 0u, 0u);
+  uint2 next = blockIdx.x < cm.total ? sld(cm.slots + blockIdx.x) : make_uint2(0u, 0u);
   for (uint32_t c = blockIdx.x; c < cm.total; c += gridDim.x) {
-    const uint4 kw = next;
+    const uint2 kw = next;
     if (c + gridDim.x < cm.total) next = sld(cm.slots + c + gridDim.x);  // the next chunk's slot, in flight meanwhile
-    const uint32_t k = kw.x & SLOT_RULE_MASK, w = kw.y & SLOT_WAVE_MASK;
+    const uint32_t k = kw.x, w = kw.y & ~SLOT_UNIFORM;
     const bool uniform = (kw.y & SLOT_UNIFORM) != 0;
     const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + w;
-    // the rule fields the walk reads (pair_walk: kind / nalts / root; walkers: meta_sites, loaded only by them)
-    RuleDesc rd;
-    rd.kind = (kw.x & SLOT_ANY) ? RK_ANYPATTERN : RK_PATTERN;
-    rd.nalts = (kw.x >> 24) & 15u;
-    rd.root = kw.w;
-    rd.flags = (kw.y & SLOT_GATE_EXACT) ? RD_GATE_EXACT : 0;
-    rd.meta_sites = k;  // rule index: Walker::run loads RuleDesc.meta_sites when its pattern needs it
+    const RuleDesc rd = sld(v.rules + k);
     bool active;
     uint32_t r;
     uint2 it = make_uint2(0u, 0u);
     bool magic = false;
-    if (kw.y & SLOT_GATE_EXACT) {
+    if (rd.flags & RD_GATE_EXACT) {
       // match == kind gate: the chunk's pairs are the gated lanes of match wave w, read straight from the headers
       r = w * WAVE + lane;
       bool gated = false;
@@ -795,7 +779,8 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
       r = it.x & ~ITEM_ROOT_MAP;
     }
     wk.rootmap = (it.x & ITEM_ROOT_MAP) != 0;
-    WaveSink sink{o.stage + kw.z, 0u};
+    const uint32_t alts = rd.kind == RK_PATTERN ? 1u : min(rd.nalts, (uint32_t)MAX_ALTS);
+    WaveSink sink{o.stage + sld32(o.rbase + (k - o.rule_lo)) + (size_t)w * WAVE * alts, 0u};
     uint8_t st = pair_walk(v, rd, active, r, k, v.nodes + it.y, wk, sink);
     if (magic) st = ST_FALLBACK;
     if (active || magic) o.status[(size_t)k * v.nres + r] = st;
