@@ -450,8 +450,8 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
   if (gated && m) {
     const ResHeader& h = v.hdr[r];
     const NodeTab R{v.nodes + h.root};
-    st = eval_pss_cols(v, v.pss[rd.root], h, R, &pf);
-    if (st == ST_NONE) st = eval_pss(v, v.pss[rd.root], R, h, &pf);
+    st = eval_pss_cols(v, v.pss[rd.root], h, R, &pf, r);
+    if (st == ST_NONE) st = eval_pss(v, v.pss[rd.root], R, h, &pf, r);
   }
   if (gated && st != ST_NONE) {
     o.status[(size_t)k * v.nres + r] = st;
@@ -491,15 +491,18 @@ __global__ void __launch_bounds__(WAVE) compact_sum_kernel(const uint16_t* __res
 }
 __global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict__ tsum, uint32_t ntiles,
                                                             uint32_t* __restrict__ nout) {
-  // rounds of 1024 consecutive tiles (coalesced): wave inclusive scans, a scan of the 16 wave totals, carry across
-  // rounds
+  // rounds of 8192 consecutive tiles: each thread scans 8 consecutive tiles, wave inclusive scans of the thread
+  // totals, a scan of the 16 wave totals, carry across rounds
   __shared__ uint32_t wsum[16];
+  constexpr uint32_t PER = 8;
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < ntiles; base += 1024) {
-    const uint32_t i = base + t;
-    const uint32_t x = i < ntiles ? tsum[i] : 0u;
-    uint32_t v = x;
+  for (uint32_t base = 0; base < ntiles; base += 1024 * PER) {
+    const uint32_t i0 = base + t * PER;
+    uint32_t x[PER], tot = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) { x[q] = i0 + q < ntiles ? tsum[i0 + q] : 0u; tot += x[q]; }
+    uint32_t v = tot;
     for (int off = 1; off < WAVE; off <<= 1) {
       const uint32_t y = __shfl_up(v, off);
       if ((int)lane >= off) v += y;
@@ -515,12 +518,19 @@ __global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict
       if (lane < 16) wsum[lane] = s2;
     }
     __syncthreads();
-    if (i < ntiles) tsum[i] = carry + (w ? wsum[w - 1] : 0u) + v - x;  // exclusive offset of tile i
+    uint32_t run = carry + (w ? wsum[w - 1] : 0u) + v - tot;  // exclusive offset of this thread's first tile
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+      if (i0 + q < ntiles) tsum[i0 + q] = run;
+      run += x[q];
+    }
     carry += wsum[15];
     __syncthreads();
   }
   if (t == 0) *nout = carry;
 }
+// one wave per tile of 64 chunks: every lane copies records i = lane, lane + 64, ... of the tile (the chunk of record
+// i found by a binary search over the wave's inclusive prefix of the chunk counts), so all loads are independent
 __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __restrict__ stage, const uint32_t* __restrict__ rbase,
                                                             const uint16_t* __restrict__ rcnt, const RuleDesc* __restrict__ rules,
                                                             uint32_t nwaves, size_t total, const uint32_t* __restrict__ tbase,
@@ -533,15 +543,28 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
     uint32_t y = __shfl_up(pre, off);
     if ((int)lane >= off) pre += y;
   }
+  const uint32_t T = __shfl(pre, WAVE - 1);
+  if (T == 0) return;
+  // the prefix in LDS: the per-record search below runs with part of the wave masked off (cross-lane reads from
+  // inactive lanes are undefined)
+  __shared__ uint32_t spre[WAVE];
+  spre[lane] = pre;
+  __syncthreads();
   const uint32_t base = tbase[blockIdx.x];
-  unsigned long long m = __ballot(n != 0);
-  while (m) {
-    const int j = __ffsll((long long)m) - 1;
-    m &= m - 1;
-    const uint32_t nj = __shfl(n, j), at = base + __shfl(pre, j) - nj;
-    const FailRec* src = chunk_stage(stage, rbase, rules, nwaves, (size_t)blockIdx.x * WAVE + j);
-    for (uint32_t i = lane; i < nj; i += WAVE)
-      if (at + i < max_out) out[at + i] = src[i];
+  // records as 16-byte halves: half h of record i moves from lane (2i + h) mod 64, so stores are one contiguous run
+  const uint32_t H = 2 * T;
+  for (uint32_t x = lane; x < H; x += WAVE) {
+    const uint32_t i = x >> 1;
+    uint32_t lo = 0, hi = WAVE - 1;  // smallest j with pre[j] > i
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (spre[mid] > i) hi = mid; else lo = mid + 1;
+    }
+    const uint32_t j = lo;
+    const uint32_t first = j ? spre[j - 1] : 0u;
+    const FailRec* src = chunk_stage(stage, rbase, rules, nwaves, (size_t)blockIdx.x * WAVE + j) + (i - first);
+    if (base + i < max_out)
+      reinterpret_cast<uint4*>(out + base + i)[x & 1] = reinterpret_cast<const uint4*>(src)[x & 1];
   }
 }
 

@@ -679,8 +679,12 @@ KYV_HD uint8_t pss_pod(NodeTab R, uint32_t kind, bool decode, uint32_t* meta_out
 // kCols: the decoded pod's checks through path columns only (pss_kernel: inlined, no call frame); the caller routes
 // pairs that need the map walk (exclusions, no columns, typed decode not done) elsewhere
 // (returns ST_NONE with *fails_out = 0 when the column form does not apply)
+// row: the resource's batch position (passed explicitly: a header reference handed to an out-of-line call may point
+// at a copy)
+KYV_FN_PSS uint32_t pss_checks_cols_ool(const View& v, NodeTab R, uint32_t row, const uint32_t* T);
+template <bool kOol = false>
 KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const PssDesc& pd, const ResHeader& h,
-                                                            NodeTab R, uint32_t* fails_out) {
+                                                            NodeTab R, uint32_t* fails_out, uint32_t row) {
   *fails_out = 0;
   if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
   if (!(h.flags & RF_PSS_DONE) || pd.cols == NONE || pd.nexcl != 0 || !v.colv || h.nnodes >= (1u << COL_TYPE_SHIFT))
@@ -693,20 +697,27 @@ KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const
   if (pos == NONE) return ST_PANIC;  // no pod spec for this kind (validation.go:542-543)
   const uint32_t* T = v.pool + pd.cols + pos * PC_COUNT;
   if (T[PC_PSC] == NONE) return ST_NONE;  // the table lacks this position (the rule's kinds)
-  const uint32_t row = (uint32_t)(&h - v.hdr);
   const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
-  const uint32_t fails = pss_checks_cols(v, R, row, T) & mask;
+  const uint32_t fails = (kOol ? pss_checks_cols_ool(v, R, row, T) : pss_checks_cols(v, R, row, T)) & mask;
   *fails_out = fails;
   return fails ? ST_FAIL : ST_PASS;
 }
 
-KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out) {
+// the column checks as their own out-of-line function for eval_pss (called from the match kernel; inlined into that
+// out-of-line function they measured wrong on the device -- r3i: baseline pairs with preconditions failed checks the
+// host instantiation passed -- while the same inlined code in pss_kernel is correct)
+KYV_FN_PSS uint32_t pss_checks_cols_ool(const View& v, NodeTab R, uint32_t row, const uint32_t* T) {
+  return pss_checks_cols(v, R, row, T);
+}
+
+KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out,
+                            uint32_t row) {
   *fails_out = 0;
   if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
   // the typed decode was done by the flattener when it could (RF_PSS_DONE); else here
   const bool done = (h.flags & RF_PSS_DONE) != 0;
   {
-    const uint8_t c = eval_pss_cols(v, pd, h, R, fails_out);  // path-column form when it applies
+    const uint8_t c = eval_pss_cols<true>(v, pd, h, R, fails_out, row);  // path-column form when it applies
     if (c != ST_NONE) return c;
   }
   uint32_t meta = NONE, spec = NONE;
@@ -866,7 +877,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
       if (c == CP_ERROR) return ST_ERROR;
       return c == CR_TRUE ? ST_FAIL : ST_PASS;
     }
-    case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails);
+    case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails, r);
     case RK_FOREACH:
       if constexpr (kJ) return eval_foreach(v, R, rd.root, r);
       else return ST_FALLBACK;
