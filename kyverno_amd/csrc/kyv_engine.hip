@@ -545,10 +545,12 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
   }
   const uint32_t T = __shfl(pre, WAVE - 1);
   if (T == 0) return;
-  // the prefix in LDS: the per-record search below runs with part of the wave masked off (cross-lane reads from
-  // inactive lanes are undefined)
+  // the prefix and each chunk's staging address in LDS: the per-record search below runs with part of the wave
+  // masked off (cross-lane reads from inactive lanes are undefined), and a record then needs no rule / rbase loads
   __shared__ uint32_t spre[WAVE];
+  __shared__ const FailRec* ssrc[WAVE];
   spre[lane] = pre;
+  ssrc[lane] = n ? chunk_stage(stage, rbase, rules, nwaves, c) : nullptr;
   __syncthreads();
   const uint32_t base = tbase[blockIdx.x];
   // records as 16-byte halves: half h of record i moves from lane (2i + h) mod 64, so stores are one contiguous run
@@ -562,7 +564,7 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
     }
     const uint32_t j = lo;
     const uint32_t first = j ? spre[j - 1] : 0u;
-    const FailRec* src = chunk_stage(stage, rbase, rules, nwaves, (size_t)blockIdx.x * WAVE + j) + (i - first);
+    const FailRec* src = ssrc[j] + (i - first);
     if (base + i < max_out)
       reinterpret_cast<uint4*>(out + base + i)[x & 1] = reinterpret_cast<const uint4*>(src)[x & 1];
   }
