@@ -225,7 +225,7 @@ def cpu_baseline_and_parity(policies, rs, data, nsl, jit, target_s=10.0, cap=400
 
 
 # device phase -> kernel-name prefixes of that phase in a rocprofv3 kernel trace
-PHASE_KERNELS = {"match": ("kyv::match_kernel",), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv::walk_kernel"),
+PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::pss_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv::walk_kernel"),
                  "compact": ("kyv::compact",), "hist": ("kyv::status_hist",)}
 
 
