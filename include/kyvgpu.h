@@ -131,10 +131,13 @@ typedef struct {
 /* ---- ruleset: replaces per-call ComputeRules + pattern decoding ---- */
 int kyv_ruleset_compile(const char* policies_json, size_t len, const kyv_compile_opts* opts, kyv_ruleset** out);
 /* same, with the cluster's PolicyExceptions (kyverno.io/v2alpha1 documents, JSON array / NDJSON): replaces the
- * per-rule lister scan of PolicyContext.FindExceptions (pkg/engine/policyContext.go:150-169). A rule some exception
- * names (PolicyException.Contains, api/kyverno/v2alpha1/policy_exception_types.go:101) reports KYV_ST_FALLBACK with
- * reason "exception" for every matched pair; the caller's engine.Validate then applies hasPolicyExceptions
- * (pkg/engine/validation.go:797-848). exceptions_json may be NULL. */
+ * per-rule lister scan of PolicyContext.FindExceptions (pkg/engine/policyContext.go:150-169). The match blocks of the
+ * exceptions naming a rule (PolicyException.Contains, api/kyverno/v2alpha1/policy_exception_types.go:101) are
+ * compiled as device match programs checked after the rule's match, in input order (CheckMatchesResources,
+ * pkg/utils/match/match.go:26-203): a pair the first applicable exception covers is KYV_ST_SKIP and its message is
+ * "rule skipped due to policy exception <namespace/name>" (hasPolicyExceptions, pkg/engine/validation.go:797-848);
+ * the rule's other pairs are evaluated as usual. A rule named by more than 27 exceptions reports KYV_ST_FALLBACK with
+ * reason "exception: ...". exceptions_json may be NULL. */
 int kyv_ruleset_compile_ex(const char* policies_json, size_t len, const char* exceptions_json, size_t ex_len,
                            const kyv_compile_opts* opts, kyv_ruleset** out);
 void kyv_ruleset_free(kyv_ruleset* rs);

@@ -445,6 +445,8 @@ static bool render_message(kyv_results* r, const Ruleset& rs, const Batch& b, ui
   uint8_t st = sb & 7, alt = sb >> 3;
   const RuleMeta& m = rs.meta[rule];
   const RuleDesc& d = rs.rules[rule];
+  if (st == ST_SKIP && d.exc != NONE && alt >= 1 && alt <= m.exc_keys.size())  // hasPolicyExceptions (validation.go:838-843)
+    return *o = "rule skipped due to policy exception " + m.exc_keys[alt - 1], true;
   if (sb >> 3 == (ST_MARK_PRE >> 3) && d.pre != NONE) {  // checkPreconditions outcome (validation.go:281-288)
     if (st == ST_SKIP) return *o = "preconditions not met", true;
     std::string e;

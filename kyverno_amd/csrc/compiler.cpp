@@ -933,6 +933,27 @@ MatchBlock compile_block(Cx& c, const Value* mr, bool is_match, bool* empty_may)
   return B;
 }
 
+// A PolicyException's spec.match (kyvernov2beta1.MatchResources: any / all only) as (mode, filters, nfilters) for
+// match_exception (kyv_eval.h; CheckMatchesResources, pkg/utils/match/match.go:26-76)
+void compile_exc_block(Cx& c, const Value* mr, std::vector<uint32_t>& out) {
+  const Value* any = mr ? mr->get("any") : nullptr;
+  const Value* all = mr ? mr->get("all") : nullptr;
+  uint32_t mode = MM_EXC_ALL;
+  const Value* lst = nullptr;
+  if (nonempty_list(any)) { mode = MM_ANY; lst = any; }
+  else if (nonempty_list(all)) { mode = MM_ALL; lst = all; }
+  const uint32_t f0 = (uint32_t)c.rs.filters.size();
+  bool em = false;
+  if (lst)
+    for (auto& f : lst->a) {
+      const uint32_t id = compile_filter(c, &f, f.get("resources"), &em);
+      c.rs.filters[id].flags &= (uint16_t)~FF_KINDS_STAR;  // namespaceSelector: kind != "" only (match.go:186)
+    }
+  out.push_back(mode);
+  out.push_back(f0);
+  out.push_back(lst ? (uint32_t)lst->a.size() : 0u);
+}
+
 // ---------------------------------------------------------------- PodSecurity
 uint32_t control_slots(const std::string& control) {  // pkg/pss/utils/mapping.go:45-111 -> check-version slots
   auto S = [](std::initializer_list<int> l) { uint32_t m = 0; for (int s : l) m |= 1u << s; return m; };
@@ -1796,17 +1817,24 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
   try {
     seed_dict(rs->dict);
     std::vector<Value> docs = pj::parse_many(json, len, true);
-    // (policy key, rule name) pairs some PolicyException lists (FindExceptions, pkg/engine/policyContext.go:150-169):
-    // the exception's match block is checked by the CPU engine (hasPolicyExceptions, validation.go:797-848)
-    std::set<std::pair<std::string, std::string>> excepted;
+    // PolicyExceptions in input order (the lister order FindExceptions walks, pkg/engine/policyContext.go:150-169):
+    // key (cache.MetaNamespaceKeyFunc), the (policy key, rule name) pairs it lists, its match block
+    struct Exc { std::string key; std::set<std::pair<std::string, std::string>> names; const Value* match; };
+    std::vector<Value> exdocs;
+    std::vector<Exc> excs;
     if (exceptions && ex_len) {
-      for (auto& ex : pj::parse_many(exceptions, ex_len, true)) {
+      exdocs = pj::parse_many(exceptions, ex_len, true);
+      for (auto& ex : exdocs) {
         if (ex.t != T::Obj || ex.str_or("kind") != "PolicyException") continue;
         const Value* spec = ex.get("spec");
         const Value* lst = spec ? spec->get("exceptions") : nullptr;
         if (!lst || lst->t != T::Arr) continue;
-        for (auto& e : lst->a)
-          for (auto& rn : strs(e.get("ruleNames"))) excepted.insert({e.str_or("policyName"), rn});
+        const Value* meta = ex.get("metadata");
+        const std::string ns = meta ? meta->str_or("namespace") : "", nm = meta ? meta->str_or("name") : "";
+        Exc e{ns.empty() ? nm : ns + "/" + nm, {}, spec->get("match")};
+        for (auto& x : lst->a)
+          for (auto& rn : strs(x.get("ruleNames"))) e.names.insert({x.str_or("policyName"), rn});
+        excs.push_back(std::move(e));
       }
     }
     Cx c{*rs};
@@ -1833,6 +1861,7 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
         if (!hasValidate && !nonempty(r.get("verifyImages"))) continue;  // no response (validation.go:144-149)
         RuleDesc rd{};
         rd.pre = NONE;
+        rd.exc = NONE;
         RuleMeta rm;
         rm.name = r.str_or("name");
         rm.message = val ? val->str_or("message") : "";
@@ -1867,7 +1896,20 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
           const Value* rval = rp->get("validate");
           std::string why = ref_why.empty() ? fallback_reason(*rp) : ref_why;
           const std::string pkey = pm.ns.empty() ? pm.name : pm.ns + "/" + pm.name;  // cache.MetaNamespaceKeyFunc
-          if (why.empty() && excepted.count({pkey, rm.name})) why = "exception";
+          // exception candidates of this rule (PolicyExceptionSpec.Contains), checked after the match on the device
+          rd.exc = NONE;
+          std::vector<uint32_t> cands;
+          for (auto& e : excs) {
+            if (!e.names.count({pkey, rm.name})) continue;
+            compile_exc_block(c, e.match, cands);
+            rm.exc_keys.push_back(e.key);
+          }
+          if (rm.exc_keys.size() > MAX_EXC) throw Fallback{"exception: more than 27 PolicyExceptions name the rule"};
+          if (!rm.exc_keys.empty()) {
+            rd.exc = (uint32_t)rs->pool.size();
+            rs->pool.push_back((uint32_t)rm.exc_keys.size());
+            rs->pool.insert(rs->pool.end(), cands.begin(), cands.end());
+          }
           c.nslots = 0;
           c.sites.clear();
           c.uses_op = false;
@@ -1926,6 +1968,8 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
           (void)mark_pool;
           rd.kind = RK_FALLBACK;
           rd.pre = NONE;
+          rd.exc = NONE;
+          rm.exc_keys.clear();
           rm.reason = f.why;
           rm.msg_parts.clear();
         }
@@ -2213,7 +2257,7 @@ struct TrieBuilder {
 void mark_gate_exact(Ruleset& rs) {
   for (auto& rd : rs.rules) {
     rd.flags &= (uint8_t)~RD_GATE_EXACT;
-    if (rd.empty_may_match || rd.exclude.mode != MM_NONE || rd.pre != NONE) continue;
+    if (rd.empty_may_match || rd.exclude.mode != MM_NONE || rd.pre != NONE || rd.exc != NONE) continue;
     const MatchBlock& m = rd.match;
     if (m.mode == MM_NONE || m.nfilters == 0) continue;
     if (m.mode != MM_ANY && m.nfilters != 1) continue;

@@ -1179,7 +1179,7 @@ struct CondGen {
   // without the precondition clause, which only matters for the walk's direct schedule): the kernel's kind gate
   // is the whole match
   bool kind_only(const RuleDesc& rd) const {
-    if (rd.empty_may_match || rd.exclude.mode != MM_NONE) return false;
+    if (rd.empty_may_match || rd.exclude.mode != MM_NONE || rd.exc != NONE) return false;
     const MatchBlock& m = rd.match;
     if (m.mode == MM_NONE || m.nfilters == 0 || (m.mode != MM_ANY && m.nfilters != 1)) return false;
     for (uint32_t i = 0; i < m.nfilters; i++) {

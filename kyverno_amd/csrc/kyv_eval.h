@@ -517,6 +517,32 @@ KYV_FN_MATCH bool match_rule(const View& v, const RuleDesc& rd, const ResView& r
   return true;
 }
 
+// CheckMatchesResources (pkg/utils/match/match.go:26-76) of a PolicyException's match block with empty admission
+// info: true when the exception applies. Differs from match_rule in that a statement with neither any nor all
+// matches everything (MM_EXC_ALL), the user info of a statement is checked (never satisfied in background scans, so
+// a statement carrying roles / clusterRoles / subjects fails), a statement with an empty resource description and no
+// user info fails ("statement cannot be empty", :89-91), and the namespace selector is skipped for a resource with
+// an empty kind (:186; the compiler clears FF_KINDS_STAR on exception filters)
+KYV_HD bool match_exception(const View& v, uint32_t mode, uint32_t filters, uint32_t nfilters, const ResView& rv,
+                            const LabelSet& nsl, bool* nd) {
+  if (mode == MM_EXC_ALL) return true;
+  if (mode == MM_ANY) {
+    for (uint32_t i = 0; i < nfilters; i++) {
+      const Filter& f = v.filters[filters + i];
+      if ((f.flags & FF_ZERO_RD) && !(f.flags & FF_USERINFO)) continue;
+      if (condition_block(v, f, rv, nsl, true, nd)) return true;
+    }
+    return false;
+  }
+  bool ok = true;  // MM_ALL: every statement's errors are collected (no early exit)
+  for (uint32_t i = 0; i < nfilters; i++) {
+    const Filter& f = v.filters[filters + i];
+    if ((f.flags & FF_ZERO_RD) && !(f.flags & FF_USERINFO)) { ok = false; continue; }
+    if (!condition_block(v, f, rv, nsl, true, nd)) ok = false;
+  }
+  return ok;
+}
+
 // ---------------------------------------------------------------- pattern walk
 enum FrameKind : uint8_t { F_MAP = 1, F_AOM = 2, F_POS = 3, F_EXIST = 4 };
 struct Frame {     // 16 bytes

@@ -60,6 +60,8 @@ struct RuleMeta {
   // (pkg/policycache/store.go:96-138)
   std::vector<std::string> kinds;
   bool has_validate = false;
+  // keys (cache.MetaNamespaceKeyFunc) of the PolicyExceptions naming the rule, in candidate order (RuleDesc.exc)
+  std::vector<std::string> exc_keys;
 };
 
 // host-side text of a condition's references, for error messages (vars.go:395-399)
@@ -185,7 +187,8 @@ struct Results {
 
 // compiler / flattener entry points
 // exceptions: PolicyException documents (kyverno.io/v2alpha1) or null; a rule named by an exception
-// (PolicyException.Contains, api/kyverno/v2alpha1/policy_exception_types.go:101) is handed to the CPU engine
+// (PolicyException.Contains, api/kyverno/v2alpha1/policy_exception_types.go:101) carries the exceptions' match
+// blocks as device match programs (RuleDesc.exc): a matched pair an exception applies to is a skip
 Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const char* exceptions = nullptr,
                          size_t ex_len = 0);
 Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* nsl_json, size_t nsl_len, int threads,

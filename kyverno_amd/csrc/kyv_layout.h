@@ -124,7 +124,8 @@ struct ResHeader {          // 64 bytes, one per resource (unstructured accessor
 static_assert(sizeof(ResHeader) == 64, "header size");
 
 // ---------------------------------------------------------------- match programs
-enum MatchMode : uint8_t { MM_NONE = 0, MM_PLAIN = 1, MM_ANY = 2, MM_ALL = 3 };
+enum MatchMode : uint8_t { MM_NONE = 0, MM_PLAIN = 1, MM_ANY = 2, MM_ALL = 3,
+                           MM_EXC_ALL = 4 };  // a PolicyException match with neither any nor all: matches everything
 
 enum FilterFlag : uint16_t {
   FF_ZERO_RD = 1 << 0,        // ResourceDescription is the zero value
@@ -410,7 +411,8 @@ struct RuleDesc {
   uint32_t nalts;
   uint32_t meta_sites, nmeta;
   uint32_t pre;          // precondition program (CondProg index) or NONE; RK_DENY: `root` is the deny program
-  uint32_t pad;
+  uint32_t exc;          // PolicyException candidates or NONE: pool offset of [n, then (mode, filters, nfilters) per
+                         // candidate in FindExceptions order] (compiler.cpp compile_exceptions)
 };
 
 // ---------------------------------------------------------------- results
@@ -422,6 +424,9 @@ constexpr int NSTATUS = 8;
 constexpr uint8_t ST_MARK_PRE = 30u << 3;
 // on an error of a foreach rule: an element that is not a map under elementScope: true (validation.go:395-397)
 constexpr uint8_t ST_MARK_SCOPE = 29u << 3;
+// on a skip: rule skipped due to the PolicyException candidate (mark - 1) of the rule (validation.go:824-848)
+constexpr uint32_t MAX_EXC = 27;
+// (the status byte is ST_SKIP | (i + 1) << 3 for candidate i < MAX_EXC)
 
 constexpr int MAX_IDX = 4;
 constexpr int MAX_SLOTS = 2;

@@ -842,6 +842,18 @@ KYV_HD bool pair_match(const View& v, uint32_t r, const RuleDesc& rd, uint8_t* s
   }
   if (!m) { *st = ST_NONE; return false; }
   if (nd) { *st = ST_ND; return false; }
+  if (rd.exc != NONE) {  // hasPolicyExceptions (validation.go:158-161, :797-848): the first candidate that matches
+    const uint32_t* e = v.pool + rd.exc;
+    const uint32_t n = e[0];
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t* c = e + 1 + 3 * i;
+      if (match_exception(v, c[0], c[1], c[2], ResView{R, &h}, nsl, &nd)) {
+        *st = nd ? (uint8_t)ST_ND : (uint8_t)(ST_SKIP | ((i + 1u) << 3));
+        return false;
+      }
+    }
+    if (nd) { *st = ST_ND; return false; }
+  }
   if (rd.kind == RK_FALLBACK) { *st = ST_FALLBACK; return false; }
   return true;
 }

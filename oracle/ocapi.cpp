@@ -60,6 +60,21 @@ void oracle_free(char* p) { free(p); }
 
 int oracle_wildcard(const char* pattern, const char* text) { return gou::wildcard_match(pattern, text) ? 1 : 0; }
 
+// PolicyException documents (a JSON array, or "" for none) that later validate / validate_matrix runs check
+int oracle_set_exceptions(const char* json) {
+  try {
+    std::vector<VP> ex;
+    if (json && *json) {
+      VP a = oj::parse(json, false);
+      if (a && a->t == T::Arr) ex = a->a;
+    }
+    set_exceptions(ex);
+    return 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
 // value decoded with unstructured semantics, pattern with interface{} (float) semantics
 int oracle_pattern_validate(const char* value_json, const char* pattern_json) {
   try {

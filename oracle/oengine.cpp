@@ -266,9 +266,11 @@ static bool ui_is_zero(const VP& f) {
   return true;
 }
 
-// doesResourceMatchConditionBlock (utils.go:71-160): true when no errors
+// doesResourceMatchConditionBlock (utils.go:71-160): true when no errors. exc: the checkResourceDescription /
+// checkUserInfo form of pkg/utils/match/match.go:110-203 (PolicyException match), whose namespaceSelector is skipped
+// for every resource with an empty kind
 static bool condition_block(const VP& rd, const VP& ui, const Res& r, const std::map<std::string, std::string>& nsLabels,
-                            bool* nd) {
+                            bool* nd, bool exc = false) {
   bool ok = true;
   std::vector<std::string> kinds = str_list(rd ? rd->get("kinds") : nullptr);
   if (!kinds.empty() && !check_kind(kinds, r)) ok = false;
@@ -304,7 +306,7 @@ static bool condition_block(const VP& rd, const VP& ui, const Res& r, const std:
   }
   VP nsel = rd ? rd->get("namespaceSelector") : nullptr;
   if (!isnil(nsel) && r.kind != "Namespace" &&
-      (!r.kind.empty() || std::find(kinds.begin(), kinds.end(), "*") != kinds.end())) {
+      (!r.kind.empty() || (!exc && std::find(kinds.begin(), kinds.end(), "*") != kinds.end()))) {
     if (check_selector(nsel, nsLabels, nd) != 1) ok = false;
   }
   // userInfo with empty admission info: roles / clusterRoles / subjects never satisfied
@@ -356,6 +358,53 @@ bool matches_resource_description(const VP& rule, const VP& resource, const std:
     if (exclude_helper(exclude->get("resources"), exclude, r, nsl, nd)) failed = true;
   }
   return !failed;
+}
+
+// ---------------- PolicyException (validation.go:797-848, pkg/utils/match/match.go:26-108) ----------------
+static std::vector<VP> g_exceptions;  // set before a run starts; read-only while it runs
+void set_exceptions(const std::vector<VP>& ex) { g_exceptions = ex; }
+
+// CheckMatchesResources with empty admission info: true = no errors (the exception applies)
+static bool check_matches_resources(const VP& match, const Res& r, const std::map<std::string, std::string>& nsl, bool* nd) {
+  VP any = match ? match->get("any") : nullptr, all = match ? match->get("all") : nullptr;
+  auto filter = [&](const VP& f) {  // checkResourceFilter: "statement cannot be empty" when both parts are zero
+    VP rd = f ? f->get("resources") : nullptr;
+    if (rd_is_zero(rd) && ui_is_zero(f)) return false;
+    return condition_block(rd, f, r, nsl, nd, true);
+  };
+  if (any && any->t == T::Arr && !any->a.empty()) {
+    for (auto& f : any->a) if (filter(f)) return true;
+    return false;
+  }
+  if (all && all->t == T::Arr && !all->a.empty()) {
+    bool ok = true;
+    for (auto& f : all->a) if (!filter(f)) ok = false;
+    return ok;
+  }
+  return true;  // neither any nor all: no errors
+}
+
+// matchesException: key (cache.MetaNamespaceKeyFunc) of the first exception (FindExceptions order = input order)
+// listing (policy key, rule) whose match applies to the resource, or "" when none does
+static std::string matching_exception(const std::string& pkey, const std::string& rule, const VP& resource,
+                                      const std::map<std::string, std::string>& nsl, bool* nd) {
+  Res r = res_info(resource);
+  for (auto& ex : g_exceptions) {
+    VP spec = ex ? ex->get("spec") : nullptr;
+    VP lst = spec ? spec->get("exceptions") : nullptr;
+    if (oj::get_str(ex, "kind") != "PolicyException" || !lst || lst->t != T::Arr) continue;
+    bool named = false;
+    for (auto& e : lst->a) {  // Exception.Contains (policy_exception_types.go:100-103)
+      if (oj::get_str(e, "policyName") != pkey) continue;
+      for (auto& rn : str_list(e ? e->get("ruleNames") : nullptr)) if (rn == rule) named = true;
+    }
+    if (!named) continue;
+    if (check_matches_resources(spec->get("match"), r, nsl, nd)) {
+      std::string ns = nested_string(ex, {"metadata", "namespace"}), nm = nested_string(ex, {"metadata", "name"});
+      return ns.empty() ? nm : ns + "/" + nm;
+    }
+  }
+  return "";
 }
 
 // ---------------- autogen (pkg/autogen) ----------------
@@ -967,6 +1016,20 @@ PolicyResult validate_policy_rules(const VP& policy, const std::vector<VP>& rule
     bool m = matches_resource_description(rule, resource, nsLabels, &nd);
     if (!m) m = matches_resource_description(rule, nullptr, nsLabels, &nd);  // OldResource retry (validation.go:606)
     if (!m) continue;
+    if (!g_exceptions.empty()) {  // hasPolicyExceptions (validation.go:158-161)
+      const std::string pns = nested_string(policy, {"metadata", "namespace"});
+      const std::string rname = oj::get_str(rule, "name");
+      std::string key = matching_exception(pns.empty() ? pr.name : pns + "/" + pr.name, rname, resource, nsLabels, &nd);
+      if (!key.empty()) {
+        RuleResult rr;
+        rr.name = rname;
+        rr.status = "skip";
+        rr.message = "rule skipped due to policy exception " + key;
+        rr.nondeterministic = nd;
+        pr.rules.push_back(rr);
+        continue;
+      }
+    }
     RuleResult rr = validate_rule(rule, resource);
     rr.nondeterministic |= nd;
     if (rr.status == "none") continue;

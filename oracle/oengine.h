@@ -32,6 +32,8 @@ std::vector<oj::VP> compute_rules(const oj::VP& policy);
 bool matches_resource_description(const oj::VP& rule, const oj::VP& resource, const std::map<std::string, std::string>& nsl,
                                   bool* nd);
 RuleResult validate_rule(const oj::VP& rule, const oj::VP& resource);
+// PolicyException documents the following runs check (hasPolicyExceptions); set before the run's threads start
+void set_exceptions(const std::vector<oj::VP>& ex);
 std::string nested_string(const oj::VP& obj, std::initializer_list<const char*> path);
 bool has_nonempty(const oj::VP& o, const char* k);
 PolicyResult validate_policy(const oj::VP& policy, const oj::VP& resource, const std::map<std::string, std::string>& nsLabels);

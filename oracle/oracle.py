@@ -32,6 +32,7 @@ def lib():
                                              ctypes.c_void_p, ctypes.c_longlong]
         for name in ("oracle_match_pattern", "oracle_pss", "oracle_validate", "oracle_compute_rules"):
             getattr(L, name).restype = ctypes.c_void_p
+        L.oracle_set_exceptions.argtypes = [ctypes.c_char_p]
         L.oracle_format_float.restype = ctypes.c_void_p
         L.oracle_format_float.argtypes = [ctypes.c_double, ctypes.c_int]
         L.oracle_duration.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)]
@@ -124,9 +125,23 @@ def rule_matches(rule, resource, ns_labels=None):
     return bool(r)
 
 
-def validate(policies, resource, ns_labels=None):
-    out = json.loads(_take(lib().oracle_validate(_s(policies), _s(resource),
-                                                 _s(ns_labels) if ns_labels is not None else b"")))
+class exceptions_set:
+    """PolicyException documents the oracle checks inside the block (hasPolicyExceptions,
+    pkg/engine/validation.go:797-848); process-wide, so one block at a time"""
+    def __init__(self, exceptions):
+        self.ex = exceptions
+
+    def __enter__(self):
+        lib().oracle_set_exceptions(_s(list(self.ex)) if self.ex else b"")
+
+    def __exit__(self, *a):
+        lib().oracle_set_exceptions(b"")
+
+
+def validate(policies, resource, ns_labels=None, exceptions=None):
+    with exceptions_set(exceptions):
+        out = json.loads(_take(lib().oracle_validate(_s(policies), _s(resource),
+                                                     _s(ns_labels) if ns_labels is not None else b"")))
     if isinstance(out, dict) and "exception" in out:
         raise ValueError(out["exception"])
     return out
@@ -164,7 +179,13 @@ def validate_batch(policies, resources, ns_labels=None, threads=1):
 MATRIX_STATUS = ("none", "pass", "fail", "skip", "error", "panic", "unsupported", "nondeterministic")
 
 
-def validate_matrix(policies, resources, ns_labels=None, threads=8, nres=None, timed=False, texts=()):
+def validate_matrix(policies, resources, ns_labels=None, threads=8, nres=None, timed=False, texts=(), exceptions=None):
+    """exceptions: PolicyException documents checked after each rule's match (see _validate_matrix)"""
+    with exceptions_set(exceptions):
+        return _validate_matrix(policies, resources, ns_labels, threads, nres, timed, texts)
+
+
+def _validate_matrix(policies, resources, ns_labels=None, threads=8, nres=None, timed=False, texts=()):
     """-> (names [(policy, rule)], uint8 array [rule, resource] of MATRIX_STATUS codes)[, seconds of the timed loop]
     [, texts]. resources: list of dicts, or JSON array text / bytes (then pass nres). texts: MATRIX_STATUS names whose
     pairs' failing path and message are returned as {(rule row, resource): (path, message, message_unpinned)}."""

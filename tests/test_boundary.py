@@ -21,43 +21,49 @@ def _pod(name="x", labels=None, ns="default"):
             "spec": {"containers": [{"name": "c", "image": "nginx"}]}}
 
 
-def test_policy_exception_routes_named_rules_to_cpu():
-    """A PolicyException naming (policy, rule) makes that rule's matched pairs KYV_ST_FALLBACK with reason
-    "exception" (FindExceptions, pkg/engine/policyContext.go:150-169); autogen rules are named separately
-    (the exception lists computed rule names), other policies and rules are unaffected"""
+def test_policy_exception_candidates():
+    """A PolicyException naming (policy, rule) stays a device rule: the pairs its match block applies to are skips
+    with the exception's key (hasPolicyExceptions, validation.go:797-848), the others keep their verdicts; autogen
+    rules are named separately (the exception lists computed rule names), other policies and rules are unaffected"""
     pols = [_pod_policy("p", "r"), _pod_policy("q", "r")]
     exc = [{"apiVersion": "kyverno.io/v2alpha1", "kind": "PolicyException", "metadata": {"name": "e", "namespace": "ns"},
             "spec": {"exceptions": [{"policyName": "p", "ruleNames": ["r", "autogen-cronjob-r"]},
                                     {"policyName": "nope", "ruleNames": ["r"]}],
-                     "match": {"any": [{"resources": {"kinds": ["Pod"]}}]}}}]
+                     "match": {"any": [{"resources": {"kinds": ["Pod"], "names": ["b*"]}}]}}}]
     rs = E.Ruleset(pols, exceptions=exc)
-    by = {(rs.policies[r["policy"]]["name"], r["name"]): r for r in rs.rules}
-    assert by[("p", "r")]["kind"] == "fallback" and by[("p", "r")]["reason"] == "exception"
-    assert by[("p", "autogen-cronjob-r")]["reason"] == "exception"
-    assert by[("p", "autogen-r")]["kind"] == "pattern"
-    assert by[("q", "r")]["kind"] == "pattern"
-    b = E.Batch(rs, [_pod("a", {"app": "x"}), _pod("b")])
+    assert all(r["kind"] == "pattern" for r in rs.rules)
+    b = E.Batch(rs, [_pod("a", {"app": "x"}), _pod("b"), _pod("bb", {"app": "y"}), _pod("c")])
     res = E.evaluate(rs, b, backend="cpu")
     k = [i for i, r in enumerate(rs.rules) if (rs.policies[r["policy"]]["name"], r["name"]) == ("p", "r")][0]
     q = [i for i, r in enumerate(rs.rules) if (rs.policies[r["policy"]]["name"], r["name"]) == ("q", "r")][0]
-    assert list(res.status[k]) == [K.ST_FALLBACK, K.ST_FALLBACK]
-    assert res.fallback_reason(0, k) == "exception"
-    assert list(res.status[q]) == [K.ST_PASS, K.ST_FAIL]
-    assert res.fallback_reason(1, q) == ""
-    # without exceptions the same ruleset evaluates the rule on the device
-    rs2 = E.Ruleset(pols)
-    assert all(r["kind"] == "pattern" for r in rs2.rules)
+    assert list(res.status[k]) == [K.ST_PASS, K.ST_SKIP, K.ST_SKIP, K.ST_FAIL]
+    assert res.message(1, k) == "rule skipped due to policy exception ns/e"
+    assert list(res.status[q]) == [K.ST_PASS, K.ST_FAIL, K.ST_PASS, K.ST_FAIL]
 
 
 def test_namespaced_policy_exception_key():
-    """policy keys are cache.MetaNamespaceKeyFunc: "<ns>/<name>" for a namespaced Policy"""
+    """policy keys are cache.MetaNamespaceKeyFunc: "<ns>/<name>" for a namespaced Policy; an exception whose match
+    has neither any nor all applies to every matched resource (CheckMatchesResources returns no error)"""
     pol = _pod_policy("p", "r")
     pol["kind"] = "Policy"
     pol["metadata"]["namespace"] = "team"
     exc = lambda pn: [{"apiVersion": "kyverno.io/v2alpha1", "kind": "PolicyException", "metadata": {"name": "e"},
                        "spec": {"exceptions": [{"policyName": pn, "ruleNames": ["r"]}], "match": {}}}]
-    assert E.Ruleset([pol], exceptions=exc("p")).rules[0]["kind"] == "pattern"
-    assert E.Ruleset([pol], exceptions=exc("team/p")).rules[0]["reason"] == "exception"
+    docs = [_pod("a", ns="team"), _pod("b", {"app": "x"}, ns="team")]
+    for pn, want in (("p", [K.ST_FAIL, K.ST_PASS]), ("team/p", [K.ST_SKIP, K.ST_SKIP])):
+        rs = E.Ruleset([pol], exceptions=exc(pn))
+        assert rs.rules[0]["kind"] == "pattern"
+        assert list(E.evaluate(rs, E.Batch(rs, docs), backend="cpu").status[0]) == want
+
+
+def test_policy_exception_limit_falls_back():
+    """more candidates than a skip status can name (27) hand the rule to the CPU engine"""
+    pol = _pod_policy("p", "r")
+    exc = [{"apiVersion": "kyverno.io/v2alpha1", "kind": "PolicyException", "metadata": {"name": f"e{i}"},
+            "spec": {"exceptions": [{"policyName": "p", "ruleNames": ["r"]}],
+                     "match": {"any": [{"resources": {"names": [f"n{i}"]}}]}}} for i in range(28)]
+    rs = E.Ruleset([pol], exceptions=exc)
+    assert rs.rules[0]["kind"] == "fallback" and rs.rules[0]["reason"].startswith("exception")
 
 
 def test_runtime_fallback_reason_anchor_phrase():
