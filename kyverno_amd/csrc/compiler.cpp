@@ -1221,6 +1221,14 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
     has_or = true;
     n = n->kids[0];
   }
+  // length(<path>) (go-jmespath jpfLength): the argument's ops, then JO_LENGTH
+  bool has_len = false;
+  if (n->k == JNode::Func && n->name == "length") {
+    if (has_or) throw Fallback{"JMESPath: length() with ||"};
+    if (n->kids.size() != 1) throw Fallback{"JMESPath: function"};
+    n = n->kids[0];
+    has_len = true;
+  }
   // split the root off the left spine: request.object / request.operation / element
   std::vector<JNode*> spine;
   for (JNode* x = n.get();;) {
@@ -1246,7 +1254,7 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
     JNode* top = spine[spine.size() - 2];
     const std::string r1 = top->kids[1]->name;
     if (r1 == "operation") {
-      if (spine.size() != 2) throw Fallback{"JMESPath: request.operation path"};
+      if (spine.size() != 2 || has_len) throw Fallback{"JMESPath: request.operation path"};
       root = JR_OPERATION;
       body = nullptr;
       if (uses_op) *uses_op = true;
@@ -1315,6 +1323,10 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
     if ((op == JO_MULTI || op == JO_KEYS) && i + w < fused.size() && fused[i + w] != JO_FLAT)
       throw Fallback{"JMESPath: list outside a projection"};
     i += w;
+  }
+  if (has_len) {
+    fused.push_back(JO_LENGTH);
+    pure = false;  // the argument of a function: a missing key is null, not NotFoundError
   }
   if (has_or) {
     Value lit = pj::parse(pj::dump(orlit), false);
@@ -2112,6 +2124,10 @@ struct TrieBuilder {
         N.push_back(NONE);
         list = list || op == JO_KEYS;
         q++;
+      } else if (op == JO_LENGTH) {  // a number: no trie position
+        S = {NONE};
+        list = false;
+        break;
       } else {
         break;  // JO_OR ends the program
       }

@@ -149,8 +149,11 @@ struct JRes {
   bool lst;        // result is the projection list L
   uint32_t cur;    // single result: node (JMES_KEYBIT: a map key), NONE = null
   uint32_t lit;    // cnode literal result (|| default, request.operation), NONE otherwise
+  uint32_t num;    // length() result (a number), NONE otherwise
 };
-enum JStat { JS_OK = 0, JS_NOTFOUND = 1, JS_FB = 2 };
+// JS_ERR: a run-time JMESPath error other than NotFound (length() of a null / number / boolean): the substitution
+// fails, so the condition program is an error (vars.go:352-431)
+enum JStat { JS_OK = 0, JS_NOTFOUND = 1, JS_FB = 2, JS_ERR = 3 };
 
 KYV_HD bool j_false(const View& v, NodeTab R, const JRes& r, const JList& L) {  // util.go isFalse
   if (r.lst) return L.n == 0;
@@ -196,7 +199,7 @@ __host__ __device__ inline __attribute__((noinline)) int jmes_run(const View& v,
   const uint32_t n = o.nseg, root = p[0] & 0xFFu;
   const bool pure = (p[0] & JF_PURE) != 0;
   JRes r;
-  r.lst = false; r.cur = NONE; r.lit = NONE;
+  r.lst = false; r.cur = NONE; r.lit = NONE; r.num = NONE;
   L.n = 0;
   bool proj = false;
   uint32_t i = 1, fields = 0;
@@ -282,6 +285,32 @@ __host__ __device__ inline __attribute__((noinline)) int jmes_run(const View& v,
       }
       L.n = w;
       proj = true;
+    } else if (op == JO_LENGTH) {
+      // jpfLength (go-jmespath functions.go): rune count of a string, element count of an array / object; other
+      // types fail the argument type check
+      i++;
+      if (proj) { j_drop_nulls(L); proj = false; }
+      uint32_t cnt;
+      if (r.lst) {
+        cnt = L.n;
+      } else {
+        uint32_t sid = NONE;
+        if (r.cur == NONE) return JS_ERR;
+        if (r.cur & JMES_KEYBIT) sid = node_key(R[r.cur & ~JMES_KEYBIT]);
+        else {
+          const Node& x = R[r.cur];
+          if (node_type(x) == N_ARR || node_type(x) == N_MAP) cnt = x.b;
+          else if (node_type(x) == N_STR) sid = x.a;
+          else return JS_ERR;
+        }
+        if (sid != NONE) {  // ASCII: bytes == runes; other strings go to the CPU engine
+          const uint32_t ln = v.str_len[sid];
+          const uint8_t* b = sbytes(v, sid);
+          for (uint32_t q = 0; q < ln; q++) if (b[q] >= 0x80) return JS_FB;
+          cnt = ln;
+        }
+      }
+      r.lst = false; r.cur = NONE; r.num = cnt;
     } else if (op == JO_OR) {
       const uint32_t lit = p[i + 1];
       i += 2;
@@ -297,6 +326,11 @@ __host__ __device__ inline __attribute__((noinline)) int jmes_run(const View& v,
 }
 
 KYV_HD CV jres_cv(const View& v, NodeTab R, const JRes& r, const JList& L) {
+  if (r.num != NONE) {  // float64 count; integral, so the JSON context round trip presents it as an int
+    CV x = cv_node(Node{N_NULL, 0, 0, 0}, true);
+    x.t = CT_INT; x.i = r.num; x.sid = NONE;
+    return x;
+  }
   if (r.lit != NONE) {
     CV x = cv_node(v.cnodes[r.lit], false);
     if (x.t == CT_ARR) x.node = r.lit;
@@ -700,6 +734,7 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
             const int st = operand_cv(v, R, o, elem, L, &tmp, &miss, row);
             if (st == JS_FB) return CR_FB;
             if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
+            if (st == JS_ERR) { *err_cond = c0 + i; *err_side = side; *err_seg = NONE; return CP_ERROR; }
           }
         }
       }

@@ -358,7 +358,8 @@ enum JmesOp : uint32_t { JO_FIELD = 1,     // + key sid
                          JO_FLAT = 3,      // flatten projection (nulls dropped)
                          JO_KEYS = 4,      // keys(@) of the current map
                          JO_KEYS_FLAT = 5, // projection keys(@) then flatten
-                         JO_OR = 6 };      // + cnode literal: `|| <literal>` when the result is false-like
+                         JO_OR = 6,        // + cnode literal: `|| <literal>` when the result is false-like
+                         JO_LENGTH = 7 };  // length(<the ops before>): a number (go-jmespath jpfLength)
 constexpr uint32_t JMES_MAX_LIST = 32;     // virtual list capacity (longer -> CPU fallback)
 constexpr uint32_t JMES_KEYBIT = 1u << 31; // virtual list element: the key of map entry node (index & ~KEYBIT)
 constexpr uint32_t JMES_SIDBIT = 1u << 30; // virtual list element: a string value, by dictionary id (& ~SIDBIT)

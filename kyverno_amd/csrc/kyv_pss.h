@@ -776,7 +776,7 @@ KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root, uint32_t ro
     const ForeachEntry fe = *(const ForeachEntry*)(v.pool + root + 1 + e * (sizeof(ForeachEntry) / 4));
     JList L;
     JRes lr;
-    lr.lst = false; lr.cur = NONE; lr.lit = NONE;
+    lr.lst = false; lr.cur = NONE; lr.lit = NONE; lr.num = NONE;
     uint32_t miss = 0;
     if (fe.list.kind == OK_PATH) {
       uint32_t cur = 0;
@@ -791,8 +791,8 @@ KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root, uint32_t ro
     } else {
       const int st = jmes_run(v, R, fe.list, NONE, L, &lr, &miss);
       if (st == JS_NOTFOUND) continue;
-      if (st == JS_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
-      if (lr.lit != NONE) return KYV_WHY(FBW_COND), ST_FALLBACK;  // literal list elements: not restated
+      if (st == JS_FB || st == JS_ERR) return KYV_WHY(FBW_COND), ST_FALLBACK;
+      if (lr.lit != NONE || lr.num != NONE) return KYV_WHY(FBW_COND), ST_FALLBACK;  // literal / number: not restated
     }
     // elements: the projection list, an array's items, or the single value
     const bool arr = !lr.lst && j_arr(R, lr.cur);

@@ -222,6 +222,17 @@ VP eval(const NP& n, const VP& value) {
       return out;
     }
     case NFunction: {
+      if (n->name == "length" && n->kids.size() == 1) {  // jpfLength: runes of a string, items of an array / object
+        VP arg = eval(n->kids[0], value);
+        if (arg && arg->t == T::Str) {
+          size_t runes = 0;
+          for (unsigned char ch : arg->s) runes += (ch & 0xC0) != 0x80;
+          return Value::flt((double)runes);
+        }
+        if (arg && arg->t == T::Arr) return Value::flt((double)arg->a.size());
+        if (arg && arg->t == T::Obj) return Value::flt((double)arg->o.size());
+        throw JmesError{"invalid type for: <nil>, expected: []jpType{\"string\", \"array\", \"object\"}"};
+      }
       if (n->name != "keys" || n->kids.size() != 1) throw JmesUnsupported{"function " + n->name};
       VP arg = eval(n->kids[0], value);
       if (!arg || arg->t != T::Obj) throw JmesError{"invalid type for: <nil>, expected: []jpType{\"object\"}"};
@@ -258,9 +269,11 @@ VP floats(const VP& v) {  // encoding/json decode of the JSON context: every num
 
 }  // namespace
 
-// every node within the restated interpreter (functions: keys(@) only)
+// every node within the restated interpreter (functions: keys(@) and length())
 static bool nodes_ok(const NP& n) {
-  if (n->k == NFunction && (n->name != "keys" || n->kids.size() != 1 || n->kids[0]->k != NCurrent)) return false;
+  if (n->k == NFunction && !(n->name == "length" && n->kids.size() == 1) &&
+      (n->name != "keys" || n->kids.size() != 1 || n->kids[0]->k != NCurrent))
+    return false;
   for (auto& k : n->kids) if (!nodes_ok(k)) return false;
   return true;
 }

@@ -2,7 +2,8 @@
 the device evaluator, against the oracle (oracle/ojmes.cpp restates go-jmespath + the kyverno fork's missing-key
 rule, pinned by the Test_Apply and test/cli/test/foreach goldens), pair by pair with messages, over the chart's
 projection / foreach rules and hand-built edge cases (missing and null lists, non-map elements, empty lists,
-non-string capabilities, elementScope on strings, NotFound chains)."""
+non-string capabilities, elementScope on strings, NotFound chains, length() of arrays / maps / strings /
+projections / missing values)."""
 import copy
 
 import cases
@@ -44,6 +45,19 @@ def jmes_policies():
             {"key": "{{ request.object.metadata.labels.keys(@) || `[]` }}", "operator": "AnyIn", "value": ["x-*"]}]}}}),
         _pol("op-precondition", {"message": "m", "pattern": {"metadata": {"name": "?*"}}},
              pre={"all": [{"key": "{{ request.operation || 'BACKGROUND' }}", "operator": "Equals", "value": "CREATE"}]}),
+        _pol("len-containers", {"message": "at most one container", "deny": {"conditions": {"any": [
+            {"key": "{{ length(request.object.spec.containers) }}", "operator": "GreaterThan", "value": 1}]}}}),
+        _pol("len-labels-name", {"deny": {"conditions": {"all": [
+            {"key": "{{ length(request.object.metadata.labels) }}", "operator": "Equals", "value": 1},
+            {"key": "{{length(request.object.metadata.name)}}", "operator": "LessThanOrEquals", "value": 2}]}}}),
+        _pol("len-projection", {"deny": {"conditions": {"any": [
+            {"key": "{{ length(request.object.spec.containers[].image) }}", "operator": "Equals", "value": 0},
+            {"key": "{{ length(request.object.spec.volumes[].keys(@)[]) }}", "operator": "GreaterThanOrEquals",
+             "value": 4}]}}}),
+        _pol("len-element", {"foreach": [
+            {"list": "request.object.spec.containers",
+             "deny": {"conditions": {"all": [{"key": "{{ length(element.name) }}", "operator": "LessThan",
+                                              "value": 2}]}}}]}),
         _pol("vol-keys", {"deny": {"conditions": {"all": [
             {"key": "{{ request.object.spec.volumes[].keys(@)[] || '' }}", "operator": "AnyIn",
              "value": ["hostPath", "nfs"]}]}}}),
