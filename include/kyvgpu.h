@@ -193,6 +193,18 @@ int64_t kyv_results_message(const kyv_results* r, const kyv_ruleset* rs, const k
  * alternative, validate.go:15-56): returns their number (copies min(count, cap)); -1 when verdicts stayed on the
  * device */
 int64_t kyv_results_failures(const kyv_results* r, kyv_failure* out, size_t cap);
+/* ---- device-resident results (multi-GPU assembly; replaces the per-rank report hand-off of the
+ * reports controller, pkg/controllers/report/background/controller.go:250-361): the verdicts / failing-path records
+ * the batch's last GPU evaluation left on `device`, written into caller-owned DEVICE memory on `stream` (a
+ * hipStream_t; NULL = the null stream) for an all-gather over RCCL, in input order.
+ * kyv_batch_export_status: two 3-bit verdicts per byte (low nibble = even resource), rule-major rows of
+ *   ceil(nres / 2) bytes; returns the byte count (dst NULL: only the count), -1 on error.
+ * kyv_batch_export_failures: int64 rows (resource index + res_offset, rule, anyPattern alternative, path template,
+ *   idx[4]) of every failing-path record; returns the row count (dst NULL: only the count), -1 on error or when
+ *   the evaluation was rule-sliced (its records are gathered on the host: use kyv_results_failures). */
+int64_t kyv_batch_export_status(const kyv_batch* b, int device, uint8_t* dst, size_t cap, void* stream);
+int64_t kyv_batch_export_failures(const kyv_batch* b, int device, int64_t res_offset, int64_t* dst, size_t cap_rows,
+                                  void* stream);
 /* failing path of a single-pattern FAIL ("" otherwise); returns the full length */
 int64_t kyv_results_path(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res, uint32_t rule,
                          char* buf, size_t cap);

@@ -61,7 +61,8 @@ EXPORTS = [
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
     "kyv_ruleset_jit_compile", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
     "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures", "kyv_ruleset_rule_flags",
-    "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase",
+    "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase", "kyv_batch_export_status",
+    "kyv_batch_export_failures",
 ]
 
 _lib = None
@@ -97,6 +98,10 @@ def lib():
     L.kyv_results_pss_checks.restype = i64
     L.kyv_results_failures.argtypes = [vp, vp, sz]
     L.kyv_results_failures.restype = i64
+    L.kyv_batch_export_status.argtypes = [vp, ctypes.c_int, vp, sz, vp]
+    L.kyv_batch_export_status.restype = i64
+    L.kyv_batch_export_failures.argtypes = [vp, ctypes.c_int, i64, vp, sz, vp]
+    L.kyv_batch_export_failures.restype = i64
     L.kyv_ruleset_rule_flags.argtypes = [vp, u32]
     L.kyv_ruleset_rule_flags.restype = u32
     L.kyv_ruleset_free.argtypes = [vp]

@@ -20,6 +20,8 @@ void free_device_images(Ruleset& rs, Batch* b);
 std::string fallback_why(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule);
 bool pattern_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule, uint32_t root, uint8_t* status,
                         std::string* path, std::string* text);
+int64_t export_status(const Batch& b, int device, uint8_t* dst, size_t cap, void* stream);
+int64_t export_failures(const Batch& b, int device, int64_t off, int64_t* dst, size_t cap_rows, void* stream);
 bool pss_checks_render(const Ruleset& rs, const Batch& b, uint32_t pos, uint32_t rule, uint32_t mask,
                        std::vector<std::array<std::string, 3>>* out);
 }  // namespace kyv
@@ -43,7 +45,8 @@ static int fail(int code, const std::string& m) { g_err = m; return code; }
 
 // worker threads when the caller passes 0: KYV_THREADS, else the CPUs this process may use -- its affinity mask
 // bounded by a cgroup v2 CPU quota (cpu.max), as on shared GPU hosts where the machine's CPU count is many times
-// the job's share -- capped at 64
+// the job's share -- divided among the node's ranks (LOCAL_WORLD_SIZE, set by torch.distributed.run: one process
+// per GPU shares the same mask) and capped at 64
 static int hw_threads(int t) {
   if (t > 0) return t;
   static const int n = []() {
@@ -62,6 +65,10 @@ static int hw_threads(int t) {
         if (quota > 0) c = std::min<long>(c, (quota + period - 1) / period);
       }
       fclose(f);
+    }
+    if (const char* e = getenv("LOCAL_WORLD_SIZE")) {
+      const int lw = atoi(e);
+      if (lw > 1) c /= lw;
     }
     return std::max(1, std::min(c, 64));
   }();
@@ -247,6 +254,25 @@ int kyv_results_status(const kyv_results* r, uint8_t* out, size_t cap) {
     for (size_t i = 0; i < nres; i++) dst[i] = src[(*r->inv)[i]];
   }
   return KYV_OK;
+}
+
+int64_t kyv_batch_export_status(const kyv_batch* b, int device, uint8_t* dst, size_t cap, void* stream) {
+  if (!b) return fail(KYV_EINVAL, "null argument"), -1;
+  try {
+    return export_status(*b->b, device, dst, cap, stream);
+  } catch (std::exception& e) {
+    return fail(KYV_EINVAL, e.what()), -1;
+  }
+}
+
+int64_t kyv_batch_export_failures(const kyv_batch* b, int device, int64_t res_offset, int64_t* dst, size_t cap_rows,
+                                  void* stream) {
+  if (!b) return fail(KYV_EINVAL, "null argument"), -1;
+  try {
+    return export_failures(*b->b, device, res_offset, dst, cap_rows, stream);
+  } catch (std::exception& e) {
+    return fail(KYV_EINVAL, e.what()), -1;
+  }
 }
 
 int64_t kyv_results_count(const kyv_results* r, int s) {

@@ -245,6 +245,8 @@ struct DevBatch {
       o_colv, o_coloff, o_pe;
   uint32_t* gmask = nullptr;   // [string][words] glob-mask bits, computed on the device once per batch
   uint32_t gmask_words = 0;
+  uint32_t* inv = nullptr;     // input index -> kind-major position, and its inverse: uploaded by the first export
+  uint32_t* order = nullptr;   // of device-resident results (export_status / export_failures)
   double upload_ms = 0;
 };
 
@@ -1571,6 +1573,90 @@ bool pattern_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uint32_
   return true;
 }
 
+// ---------------------------------------------------------------- device-resident result export
+// The multi-GPU collectives of scan.py (gather_verdicts / gather_failures) all-gather straight from the
+// verdicts and failing-path records a batch's last evaluation left on its device: these kernels write the wire form
+// into a caller-owned device buffer (a torch tensor) on the caller's stream, in input order, so no host copy is made.
+
+// verdicts two per byte (low nibble: even resource), rule-major rows of ceil(nres / 2) bytes
+__global__ void __launch_bounds__(256) pack_status_kernel(const uint8_t* __restrict__ status,
+                                                          const uint32_t* __restrict__ inv, size_t nres, size_t half,
+                                                          size_t total, uint8_t* __restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const size_t k = i / half, j = i - k * half;
+  const uint8_t* row = status + k * nres;
+  const uint8_t a = row[inv[2 * j]] & 7u;
+  const uint8_t b = 2 * j + 1 < nres ? (uint8_t)(row[inv[2 * j + 1]] & 7u) : (uint8_t)0;
+  dst[i] = (uint8_t)(a | (b << 4));
+}
+
+// failing-path records as int64 rows (global resource index, rule, alternative, path template, idx0..3)
+__global__ void __launch_bounds__(256) failure_rows_kernel(const FailRec* __restrict__ recs, uint32_t n,
+                                                           const uint32_t* __restrict__ order, long long off,
+                                                           long long* __restrict__ dst) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const FailRec f = recs[i];
+  long long* o = dst + (size_t)i * 8;
+  o[0] = (long long)order[f.res] + off;
+  o[1] = f.rule;
+  o[2] = f.alt;
+  o[3] = f.tmpl;  // NONE (no path) as the host rows carry it
+  for (int q = 0; q < MAX_IDX; q++) o[4 + q] = f.idx[q];
+}
+
+static DevBatch* resident(const Batch& b, int device) {
+  if (device < 0 || device >= (int)b.dev.size() || !b.dev[device] || !((DevBatch*)b.dev[device])->out)
+    throw std::runtime_error("no device-resident results for this batch on that device (evaluate with the GPU backend first)");
+  DevBatch* db = (DevBatch*)b.dev[device];
+  HIP_OK(hipSetDevice(device));
+  if (!db->inv) {
+    const size_t n = b.inv.size();
+    std::vector<uint32_t> order(n);
+    for (size_t i = 0; i < n; i++) order[b.inv[i]] = (uint32_t)i;
+    HIP_OK(dmalloc(&db->inv, std::max<size_t>(4, n * 4)));
+    HIP_OK(dmalloc(&db->order, std::max<size_t>(4, n * 4)));
+    if (n) {
+      HIP_OK(hipMemcpy(db->inv, b.inv.data(), n * 4, hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(db->order, order.data(), n * 4, hipMemcpyHostToDevice));
+    }
+  }
+  return db;
+}
+
+int64_t export_status(const Batch& b, int device, uint8_t* dst, size_t cap, void* stream) {
+  DevBatch* db = resident(b, device);
+  const DeviceResults& d = *db->out;
+  const size_t half = (d.nres + 1) / 2, total = half * d.nrules;
+  if (!dst) return (int64_t)total;
+  if (cap < total) throw std::runtime_error("export buffer too small");
+  if (total) {
+    hipLaunchKernelGGL(pack_status_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)d.status, (const uint32_t*)db->inv, d.nres, half, total, dst);
+    HIP_OK(hipGetLastError());
+  }
+  return (int64_t)total;
+}
+
+int64_t export_failures(const Batch& b, int device, int64_t off, int64_t* dst, size_t cap_rows, void* stream) {
+  DevBatch* db = resident(b, device);
+  const DeviceResults& d = *db->out;
+  if (d.slices.size() > 1)
+    throw std::runtime_error("failing-path records of a rule-sliced evaluation are gathered on the host, not resident");
+  uint32_t nr = 0;
+  HIP_OK(hipMemcpy(&nr, d.nrecs, 4, hipMemcpyDeviceToHost));
+  if (nr > d.max_recs) throw std::runtime_error("failure record buffer overflow");
+  if (!dst) return nr;
+  if (cap_rows < nr) throw std::runtime_error("export buffer too small");
+  if (nr) {
+    hipLaunchKernelGGL(failure_rows_kernel, dim3((nr + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const FailRec*)d.recs, nr, (const uint32_t*)db->order, (long long)off, (long long*)dst);
+    HIP_OK(hipGetLastError());
+  }
+  return nr;
+}
+
 void free_device_images(Ruleset& rs, Batch* b) {
   if (b) {
     for (auto* p : b->dev)
@@ -1579,6 +1665,8 @@ void free_device_images(Ruleset& rs, Batch* b) {
         hipSetDevice(d->device);
         dfree(d->base);
         dfree(d->gmask);
+        dfree(d->inv);
+        dfree(d->order);
         if (d->out) { free_dev_results(*d->out, d->device); delete d->out; }
         delete d;
       }

@@ -13,9 +13,16 @@ process group (RCCL with the "nccl" backend on device tensors, gloo on CPU):
   gather_verdicts  all-gather of every rank's verdict matrix, two pairs per byte (status values are 3-bit);
   gather_failures  count-then-gather of the compacted failing-path records.
 
+With a GPU evaluation the collectives read the rank's device-resident results (gather_verdicts_device /
+gather_failures_device: the library writes the wire form straight into a torch device tensor on the current stream,
+kyv_batch_export_status / kyv_batch_export_failures), so the verdicts never pass through host memory on the way to
+RCCL. Load torch before the library in such a process (KYV_TORCH_FIRST=1, see _lib.py).
+
 Pairs outside the device subset (KYV_ST_FALLBACK, PANIC, ND) are listed by `fallback_pairs()`: the Go shim
 evaluates exactly those with the reference engine; they are counted as `cpu_fallback`, not in pass/fail/....
 """
+import ctypes
+
 import numpy as np
 
 from . import _lib as K
@@ -235,3 +242,65 @@ def gather_failures(failures, res_offset, group=None, device=None):
         t = t.to(device)
     parts, _ = _all_gather_var(t, group, dist, torch)
     return torch.cat(parts, dim=0).cpu().numpy()
+
+
+def _export_target(device):
+    import torch
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type != "cuda":
+        raise ValueError("device-resident gather needs a GPU device, got %s" % dev)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    return torch.device("cuda", idx), idx, torch.cuda.current_stream(idx).cuda_stream
+
+
+def _export_check(n):
+    if n < 0:
+        raise K.KyvError(K.lib().kyv_last_error().decode(errors="replace"))
+    return n
+
+
+def gather_verdicts_device(batch, group=None, device=None, tensor=False):
+    """gather_verdicts over the verdicts the batch's last GPU evaluation left on `device` (its kyv_eval device
+    ordinal, normally LOCAL_RANK): the library packs them (two per byte, rule-major) into a device tensor, the ranks
+    all-gather those (RCCL), and the full matrix is unpacked on the device. Returns (uint8 [rules, sum n_rank] in rank
+    order -- a device tensor with tensor=True, else numpy --, list of each rank's first global resource index)."""
+    import torch
+    import torch.distributed as dist
+    dev, idx, stream = _export_target(device)
+    L = K.lib()
+    total = _export_check(L.kyv_batch_export_status(batch.h, idx, None, 0, None))
+    buf = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    _export_check(L.kyv_batch_export_status(batch.h, idx, ctypes.c_void_p(buf.data_ptr()), buf.numel(),
+                                            ctypes.c_void_p(stream)))
+    nr = len(batch.ruleset.rules)
+    parts, _ = _all_gather_var(buf[:total], group, dist, torch)
+    counts = torch.tensor([batch.n], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(counts) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(ns, counts, group=group)
+    cols, offs, at = [], [], 0
+    for p, k in zip(parts, ns):
+        k = int(k.item())
+        h = (k + 1) // 2
+        q = p.view(nr, h)
+        cols.append(torch.stack((q & 15, q >> 4), dim=2).reshape(nr, 2 * h)[:, :k])
+        offs.append(at)
+        at += k
+    full = torch.cat(cols, dim=1) if cols else torch.zeros((nr, 0), dtype=torch.uint8, device=dev)
+    return (full if tensor else full.cpu().numpy()), offs
+
+
+def gather_failures_device(batch, res_offset, group=None, device=None, tensor=False):
+    """gather_failures over the failing-path records resident on `device`: int64 rows (global resource index, rule,
+    alternative, path template, idx0..3) written by the library into a device tensor, then all-gathered (RCCL).
+    A rule-sliced evaluation keeps no resident records (the library says so): use gather_failures there."""
+    import torch
+    import torch.distributed as dist
+    dev, idx, stream = _export_target(device)
+    L = K.lib()
+    n = _export_check(L.kyv_batch_export_failures(batch.h, idx, int(res_offset), None, 0, None))
+    t = torch.empty((max(n, 1), 8), dtype=torch.int64, device=dev)
+    _export_check(L.kyv_batch_export_failures(batch.h, idx, int(res_offset), ctypes.c_void_p(t.data_ptr()), n,
+                                              ctypes.c_void_p(stream)))
+    parts, _ = _all_gather_var(t[:n], group, dist, torch)
+    full = torch.cat(parts, dim=0)
+    return full if tensor else full.cpu().numpy()

@@ -125,3 +125,55 @@ def test_bench_spawns_ranks_for_gpus_flag():
     assert r.returncode != 0
     assert r.stderr.count("rank 0:") >= 1 and r.stderr.count("rank 1:") >= 1, r.stderr[-2000:]
     assert "no HIP device" in r.stderr
+
+
+def _rank_device(rank, world, port, q):
+    """one rank of `bench.py --gpus 2`: its evaluations must name its own LOCAL_RANK device ordinal in kyv_eval_opts
+    (the library's kyv_eval is replaced by a recorder here: no GPU in this container)"""
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bench
+    import cases
+    from kyverno_amd import _lib as K
+    from kyverno_amd import engine as E
+    from kyverno_amd import synth
+    r, w, local, pg = bench.dist_setup(world)
+    rs = E.Ruleset(cases.best_practices()[:2])
+    b = E.Batch(rs, synth.mixed(20, seed=r)[0])
+    seen = []
+    L = K.lib()
+
+    def fake_eval(rsh, bh, opts, out):
+        o = opts._obj  # the EvalOpts behind ctypes.byref
+        seen.append((o.backend, o.device))
+        return 7  # an error code: nothing to evaluate without a GPU
+
+    real = L.kyv_eval
+    L.kyv_eval = fake_eval
+    try:
+        E.evaluate(rs, b, backend="gpu", device=local)
+    except K.KyvError:
+        pass
+    finally:
+        L.kyv_eval = real
+    q.put((rank, local, seen))
+    pg.destroy_process_group()
+
+
+def test_ranks_evaluate_on_their_local_rank_device():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_device, args=(i, 2, port, q)) for i in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    from kyverno_amd import _lib as K
+    for rank, local, seen in out:
+        assert local == rank
+        assert seen == [(K.BACKEND_GPU, rank)]

@@ -1,0 +1,59 @@
+"""Multi-GPU assembly from device-resident results: gather_verdicts_device / gather_failures_device
+all-gather over RCCL what kyv_batch_export_status / kyv_batch_export_failures write straight from the batch's resident
+verdicts and failing-path records into torch device tensors. On the one-GPU box the group is a world_size-1 RCCL
+group; the wire format, the input-order permutation and the offsets are checked against the host copies of the same
+evaluation. (Ranks > 1 run only on the driver's 8-GPU node; the gloo tests in test_dist.py cover the host gathers.)"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import os, sys
+import torch  # before the library: one HIP runtime shared with torch / RCCL (kyverno_amd/_lib.py)
+import torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"]); sys.path.insert(0, os.path.join(os.environ["ROOT"], "tests"))
+import numpy as np
+import cases
+from kyverno_amd import engine as E, scan as SC, synth
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+docs, nsl = synth.mixed(3001, seed=91, edge=True)
+rs = E.Ruleset(cases.best_practices() + cases.quirk_policies())
+b = E.Batch(rs, docs, nsl)
+res = E.evaluate(rs, b, backend="gpu", device=0)
+full, offs = SC.gather_verdicts_device(b, device="cuda:0")
+assert offs == [0], offs
+assert full.shape == res.status.shape, (full.shape, res.status.shape)
+assert np.array_equal(full, np.asarray(res.status) & 7)
+t, _ = SC.gather_verdicts_device(b, device="cuda:0", tensor=True)
+assert t.is_cuda and t.dtype == torch.uint8
+rows = SC.gather_failures_device(b, 1000, device="cuda:0")
+f = res.failures()
+want = sorted(zip((f["res"].astype(np.int64) + 1000).tolist(), f["rule"].tolist(), f["alt"].tolist(),
+                  f["path_template"].tolist(), map(tuple, f["idx"].tolist())))
+got = sorted((int(r[0]), int(r[1]), int(r[2]), int(r[3]), tuple(int(x) for x in r[4:8])) for r in rows)
+assert got == want and len(got) > 100, (len(got), len(want))
+dist.destroy_process_group()
+print("gather ok", full.shape, len(got))
+"""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_device_resident_gather_rccl():
+    env = dict(os.environ, ROOT=ROOT, KYV_TORCH_FIRST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "gather ok" in r.stdout

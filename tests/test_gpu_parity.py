@@ -109,7 +109,8 @@ def test_c5_oracle_matrix_at_scale():
     data, nsl = synth.corpus_ndjson(200_000, seed=54, edge=True)
     st, res = PU.compare_matrix(synth.c5_policies(50), data, nsl, backend="gpu", threads=_oracle_threads())
     assert st["nbad"] == 0, st["bad"]
-    assert res.counts["fallback"] > 0 and st["matched"] > 1_000_000
+    assert st["matched"] > 1_000_000
+    assert not any(r["kind"] == "fallback" for r in res.ruleset.rules)  # length() rules compile to the device
 
 
 def test_repeat_launches_deterministic():
@@ -211,7 +212,7 @@ def test_condition_goldens_gpu():
 
 def test_c5_conditions_gpu():
     st, _ = S.run_synthetic("gpu", synth.c5_policies(50), 4000, seed=34)
-    assert st["compared"] > 40000 and st["fallback"] > 0
+    assert st["compared"] > 40000
 
 
 _SCAN_RCCL = r"""
