@@ -431,6 +431,10 @@ class AdmissionBatcher:
             self.cache.set(key, self.pol[i]["doc"], rules=rules)
             self._key_index[key] = i
         self.stats = {"requests": 0, "batches": 0, "device_policies": 0, "cpu_policies": 0}
+        # kyverno_policy_results / _execution_duration_seconds of the device-decided rule responses of every batch
+        # (pkg/webhooks/utils/metrics.go:25-64); the CPU engine's responses are recorded by the Go shim
+        from .metrics import PolicyMetrics
+        self.metrics = PolicyMetrics()
         self._q, self._cv, self._stop, self._thr = [], threading.Condition(), False, None
         self._enforce_cache = {}
 
@@ -465,7 +469,7 @@ class AdmissionBatcher:
 
     def handle_batch(self, requests):
         """Evaluate a list of requests in one device batch -> list of decisions (same order)."""
-        docs, ns_labels, slots = [], {}, []
+        docs, ns_labels, slots, mkind, mns, mop = [], {}, [], [], [], []
         for rq in requests:
             op = rq.get("operation", "CREATE")
             new, old = rq.get("object") or {}, rq.get("oldObject") or {}
@@ -476,9 +480,15 @@ class AdmissionBatcher:
             if op != "DELETE" and new:
                 i_new = len(docs)
                 docs.append(rq.get("object_raw") or _dumps1(new))
+                mkind.append(new.get("kind", "") if isinstance(new, dict) else "")
+                mns.append(_meta(new).get("namespace", ""))
+                mop.append(op.lower())
                 if op == "UPDATE" and old:
                     i_old = len(docs)
                     docs.append(rq.get("oldObject_raw") or _dumps1(old))
+                    mkind.append(None)  # the OldResource retry's row: no response of its own
+                    mns.append("")
+                    mop.append("")
             slots.append((i_new, i_old))
         st = res = None
         quiet = cpu = None
@@ -486,6 +496,8 @@ class AdmissionBatcher:
             batch = E.Batch(self.ruleset, b"\n".join(docs), ns_labels or None)  # NDJSON
             res = E.evaluate(self.ruleset, batch, backend=self.backend, device=self.device)
             st = res.status
+            self.metrics.record(self.ruleset, [p["doc"] for p in self.pol], res, mkind, mns,
+                                cause="admission_request", operation=mop)
             # per policy over the whole batch: "every matched rule passed" (the policy cannot change the decision)
             # and "some pair needs the CPU engine"; only the remaining (request, policy) pairs are assembled rule
             # by rule

@@ -252,7 +252,7 @@ class Engine:
             per_policy = []
             for pi, pol in enumerate(self.ruleset.policies):
                 rules = []
-                applied = 0
+                applied = errors = 0
                 for k in range(pol["first_rule"], pol["first_rule"] + pol["nrules"]):
                     st = int(res.status[k, r])
                     if st == K.ST_NONE:
@@ -261,10 +261,15 @@ class Engine:
                     rules.append({"name": self.ruleset.rules[k]["name"], "status": name, "message": res.message(r, k)})
                     if st in (K.ST_PASS, K.ST_FAIL):
                         applied += 1
+                    elif st == K.ST_ERROR:
+                        errors += 1
                     if pol["apply_one"] and applied > 0:  # validation.go:176-178
                         break
                     if pol["apply_one"] and st == K.ST_FALLBACK:
                         break  # truncation depends on the CPU engine's verdict for this rule
-                per_policy.append({"policy": pol["name"], "rules": rules})
+                # PolicyResponse.PolicyStats (validation.go:196-208; pkg/engine/api/stats.go:16-23): the device's
+                # share (rules the CPU engine decides add theirs in the Go shim)
+                per_policy.append({"policy": pol["name"], "rules": rules,
+                                   "stats": {"rulesAppliedCount": applied, "rulesErrorCount": errors}})
             out.append(per_policy)
         return out, res, batch
