@@ -125,13 +125,19 @@ class Results:
         if rc.size:
             K.check(L.kyv_results_rule_counts(h, rc.ctypes.data, rc.size))
         self.rule_counts = rc.reshape(len(ruleset.rules), 8)  # [rule][status] verdict totals
-        self.status = None
+        self.raw = self._status = None
         if copied:
             nr, nres = len(ruleset.rules), batch.n
             buf = np.empty(nr * nres, dtype=np.uint8)
             K.check(L.kyv_results_status(h, buf.ctypes.data, buf.size))
-            self.raw = buf.reshape(nr, nres)
-            self.status = self.raw & 7
+            self.raw = buf.reshape(nr, nres)  # status bytes in input order (low 3 bits: KYV_ST_*, high bits: marks)
+
+    @property
+    def status(self):
+        """uint8 [rule, resource] KYV_ST_* verdicts (None when they stayed on the device)"""
+        if self._status is None and self.raw is not None:
+            self._status = self.raw & 7
+        return self._status
 
     def message(self, res, rule):
         L = K.lib()
