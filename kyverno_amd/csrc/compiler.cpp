@@ -1445,9 +1445,14 @@ CondOperand compile_operand(Cx& c, const Value* v, CondText& ct, int side, const
 uint8_t cond_op(const std::string& op) {
   std::string l = op;
   for (auto& ch : l) ch = (char)tolower((unsigned char)ch);
-  if (l.compare(0, 8, "duration") == 0 && (l == "durationgreaterthanorequals" || l == "durationgreaterthan" ||
-                                           l == "durationlessthanorequals" || l == "durationlessthan"))
-    throw Fallback{"conditions: Duration* operator"};
+  if (l == "durationgreaterthanorequals" || l == "durationgreaterthan" || l == "durationlessthanorequals" ||
+      l == "durationlessthan") {  // DurationOperatorHandler: durationCompareByCondition matches the exact name
+    if (op == "DurationGreaterThan") return CO_DGT;
+    if (op == "DurationGreaterThanOrEquals") return CO_DGE;
+    if (op == "DurationLessThan") return CO_DLT;
+    if (op == "DurationLessThanOrEquals") return CO_DLE;
+    return CO_FALSE;
+  }
   if (l == "equal" || l == "equals") return CO_EQ;
   if (l == "notequal" || l == "notequals") return CO_NE;
   if (l == "in") return CO_IN;

@@ -961,6 +961,8 @@ struct CondGen {
       case CO_ALLNOTIN: return "op_any_all(" + a + ", true, true)";
       case CO_GT: case CO_GE: case CO_LT: case CO_LE:
         return "op_numeric(v, " + K + ", " + X + ", " + std::to_string(c.op) + ")";
+      case CO_DGT: case CO_DGE: case CO_DLT: case CO_DLE:
+        return "op_duration(v, " + K + ", " + X + ", " + std::to_string(c.op) + ")";
       default: return "CR_FALSE";
     }
   }

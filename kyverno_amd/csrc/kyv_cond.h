@@ -688,6 +688,27 @@ KYV_HD int op_numeric(const View& v, const CV& k, const CV& x, uint8_t op) {
   }
 }
 
+// ---------------------------------------------------------------- Duration* (duration.go:30-150)
+// DurationOperatorHandler.Evaluate: an int / float operand is time.Duration(x) seconds (float truncated, the product
+// wrapping like Go's), a string one time.ParseDuration'd (failure: false); any other type: false
+KYV_HD bool dur_operand(const View& v, const CV& x, int64_t* d) {
+  if (x.t == CT_INT || x.t == CT_FLOAT) return num_secs(x, d);
+  if (x.t == CT_STR && x.sid != NONE && (sflags(v, x.sid) & SF_DUR)) { *d = v.str_dur[x.sid]; return true; }
+  return false;
+}
+KYV_HD int op_duration(const View& v, const CV& k, const CV& x, uint8_t op) {
+  int64_t kd, vd;
+  if (!dur_operand(v, k, &kd) || !dur_operand(v, x, &vd)) return CR_FALSE;
+  bool r;
+  switch (op) {
+    case CO_DGT: r = kd > vd; break;
+    case CO_DGE: r = kd >= vd; break;
+    case CO_DLT: r = kd < vd; break;
+    default: r = kd <= vd; break;
+  }
+  return r ? CR_TRUE : CR_FALSE;
+}
+
 KYV_HD int eval_cond(const View& v, NodeTab R, const Cond& c, const CV& k, const CV& x) {
   switch (c.op) {
     case CO_EQ: return op_equal(v, R, k, x, false);
@@ -699,6 +720,7 @@ KYV_HD int eval_cond(const View& v, NodeTab R, const Cond& c, const CV& k, const
     case CO_ANYNOTIN: return op_any_all(v, R, c, k, x, false, true);
     case CO_ALLNOTIN: return op_any_all(v, R, c, k, x, true, true);
     case CO_GT: case CO_GE: case CO_LT: case CO_LE: return op_numeric(v, k, x, c.op);
+    case CO_DGT: case CO_DGE: case CO_DLT: case CO_DLE: return op_duration(v, k, x, c.op);
     default: return CR_FALSE;
   }
 }

@@ -344,7 +344,8 @@ enum RuleKind : uint8_t { RK_NONE = 0, RK_PATTERN = 1, RK_ANYPATTERN = 2, RK_PSS
 // block without `any`). Operands are literals (ruleset node table `cnodes`, already put through the
 // Condition.GetKey json round trip) or `{{ request.object.<path> }}` references resolved per resource.
 enum CondOp : uint8_t { CO_EQ = 0, CO_NE = 1, CO_IN = 2, CO_NOTIN = 3, CO_ANYIN = 4, CO_ALLIN = 5, CO_ANYNOTIN = 6,
-                        CO_ALLNOTIN = 7, CO_GT = 8, CO_GE = 9, CO_LT = 10, CO_LE = 11, CO_FALSE = 12 };
+                        CO_ALLNOTIN = 7, CO_GT = 8, CO_GE = 9, CO_LT = 10, CO_LE = 11, CO_FALSE = 12,
+                        CO_DGT = 13, CO_DGE = 14, CO_DLT = 15, CO_DLE = 16 };  // Duration* (operator/duration.go)
 enum OperandKind : uint8_t { OK_NIL = 0, OK_LIT = 1, OK_PATH = 2, OK_JMES = 3 };
 
 // JMESPath-subset operand program (OK_JMES; pool words at CondOperand.a, CondOperand.nseg words): go-jmespath

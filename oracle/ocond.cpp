@@ -523,6 +523,25 @@ static bool op_numeric(const VP& k, const VP& v, const std::string& op) {
   }
 }
 
+// DurationOperatorHandler (pkg/engine/variables/operator/duration.go:30-150): Evaluate's type switches, then
+// durationCompareByCondition on the exact operator name
+static bool dur_operand(const VP& x, int64_t& d) {
+  if (!x) return false;
+  if (x->t == T::Int) { d = wrap_mul(x->i, 1000000000LL); return true; }
+  if (x->t == T::Float) { d = wrap_mul(go_f2i(x->f), 1000000000LL); return true; }
+  if (x->t == T::Str) return gou::parse_duration(x->s, d);
+  return false;
+}
+static bool op_duration(const VP& key, const VP& value, const std::string& op) {
+  int64_t kd, vd;
+  if (!dur_operand(key, kd) || !dur_operand(value, vd)) return false;
+  if (op == "DurationGreaterThanOrEquals") return kd >= vd;
+  if (op == "DurationGreaterThan") return kd > vd;
+  if (op == "DurationLessThanOrEquals") return kd <= vd;
+  if (op == "DurationLessThan") return kd < vd;
+  return false;
+}
+
 static std::string lower(std::string s) {
   for (auto& c : s) c = gou::lower(c);
   return s;
@@ -540,7 +559,10 @@ bool evaluate_condition(const VP& key, const std::string& op, const VP& value) {
   if (o == "allnotin") return op_any_all(key, value, true, true);
   if (o == "greaterthanorequals" || o == "greaterthan" || o == "lessthanorequals" || o == "lessthan")
     return op_numeric(key, value, op);
-  return false;  // no handler (Duration* operators are classified unsupported before evaluation)
+  if (o == "durationgreaterthanorequals" || o == "durationgreaterthan" || o == "durationlessthanorequals" ||
+      o == "durationlessthan")
+    return op_duration(key, value, op);
+  return false;  // no handler
 }
 
 // ---------------------------------------------------------------- substitution (vars.go, restricted)
@@ -608,9 +630,6 @@ static bool conditions_supported_in(const VP& v, bool allow_element) {
   if (v->t == T::Obj) {
     for (auto& kv : v->o) {
       if (has_var_syntax(kv.first)) return false;
-      if (kv.first == "operator" && kv.second && kv.second->t == T::Str &&
-          lower(kv.second->s).compare(0, 8, "duration") == 0)
-        return false;  // deprecated Duration* operators: not in the device subset
       if (!conditions_supported_in(kv.second, allow_element)) return false;
     }
   }

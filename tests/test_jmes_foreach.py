@@ -58,6 +58,17 @@ def jmes_policies():
             {"list": "request.object.spec.containers",
              "deny": {"conditions": {"all": [{"key": "{{ length(element.name) }}", "operator": "LessThan",
                                               "value": 2}]}}}]}),
+        _pol("dur-ttl", {"message": "ttl above one hour", "deny": {"conditions": {"any": [
+            {"key": "{{ request.object.metadata.annotations.ttl || '0s' }}", "operator": "DurationGreaterThan",
+             "value": "1h"},
+            {"key": "{{ request.object.metadata.annotations.ttl || `90` }}", "operator": "DurationLessThan",
+             "value": 60}]}}}),
+        _pol("dur-grace", {"deny": {"conditions": {"all": [
+            {"key": "{{ request.object.spec.terminationGracePeriodSeconds }}", "operator": "DurationLessThanOrEquals",
+             "value": "30s"},
+            {"key": "45s", "operator": "DurationGreaterThanOrEquals", "value": 44.9}]}}}),
+        _pol("dur-spelling", {"deny": {"conditions": {"any": [
+            {"key": "2h", "operator": "durationGreaterThan", "value": "1h"}]}}}),
         _pol("vol-keys", {"deny": {"conditions": {"all": [
             {"key": "{{ request.object.spec.volumes[].keys(@)[] || '' }}", "operator": "AnyIn",
              "value": ["hostPath", "nfs"]}]}}}),
@@ -95,7 +106,12 @@ def edge_pods():
             d["metadata"]["labels"] = {"x-team": "1"}
         if i == 5:
             d["metadata"]["labels"] = None
-        if sp is not None:
+        ttl = ("30m", "2h", "3600", "bad", "0", "1.5h", "-5s", None, "1h0m1s", "59")[i % 10]
+        if ttl is not None:
+            d["metadata"]["annotations"] = {"ttl": ttl}
+        if i % 4 == 1:
+            d["spec"] = dict(sp or {}, terminationGracePeriodSeconds=(30, 31, 29.5, "30")[(i // 4) % 4])
+        if sp is not None and "spec" not in d:
             d["spec"] = sp
         out.append(d)
     return out
