@@ -190,7 +190,8 @@ struct SliceSched {
   size_t stage_tot = 0;          // staging slots (records) of the slice
   uint32_t* rbase = nullptr;     // [k1 - k0] first staging slot of each rule (slice-local)
   uint32_t* mrules = nullptr;    // rules of the slice the match phase evaluates (direct-walk rules excluded):
-  uint32_t nm = 0, nmj = 0, nmc = 0;  // [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
+  uint32_t nmw = 0;              // leading rules of mrules on match_walk_kernel (pattern rules: match only)
+  uint32_t nm = 0, nmj = 0, nmc = 0;  // then [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
                                  // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
   std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
   std::vector<uint3> pw;         // PodSecurity rules on pss_kernel: (rule, first match wave, waves)
@@ -423,6 +424,44 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_
       const uint32_t ps = o.pss_slot[k];
       if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
     }
+  }
+}
+
+// Pattern / anyPattern rules without preconditions (and compile-time fallback rules): the match phase is only
+// pair_match (kind gate, match / exclude program, PolicyException candidates) and the work-list append, so this
+// kernel carries none of the dispatch code (conditions, PodSecurity calls) whose register need made the rule loop
+// of match_kernel spill every iteration (C4: 10,440 rules per wave, 252 GB of scratch writes per evaluation)
+// kWpe: occupancy target (KYV_MATCHW_WPE = 4 / 6 / 8 at run time; 4 by default: 97 VGPRs, none spilled; 8 spills 253)
+template <int kWpe>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
+match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint32_t* __restrict__ mrules, uint32_t nm) {
+  const View& v = *vp;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t r = blockIdx.x * BLOCK + lane;
+  const bool active = r < v.nres;
+  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
+  const uint32_t hflags = active ? v.hdr[r].flags : 0u;
+  const uint32_t hroot = active ? v.hdr[r].root : 0u;
+  for (uint32_t mi = 0; mi < nm; mi++) {
+    const uint32_t k = mrules[mi];
+    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+    if (!__ballot(gated)) continue;
+    const RuleDesc& rdk = v.rules[k];
+    uint8_t st = ST_NONE;
+    bool walk = false;
+    if (gated && pair_match(v, r, rdk, &st)) {  // a matched pattern pair: walk it (RF_MAGIC: the CPU engine)
+      if (hflags & RF_MAGIC) st = ST_FALLBACK;
+      else walk = true;
+    }
+    const unsigned long long wm = __ballot(walk);
+    if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {
+      const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + blockIdx.x;
+      if (walk)
+        wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
+            make_uint2(r | ((hflags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), hroot);
+      if (lane == 0) wl.cnt[list] = (uint8_t)__popcll(wm);
+    }
+    if (gated && !walk && st != ST_NONE) o.status[(size_t)k * v.nres + r] = st;
   }
 }
 
@@ -827,10 +866,15 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     // PodSecurity rules without preconditions: pss_kernel over the waves of their kind gate (KYV_PSS_KERNEL=0: the
     // match kernel)
     static const bool pss_k = !getenv("KYV_PSS_KERNEL") || atoi(getenv("KYV_PSS_KERNEL")) != 0;
-    std::vector<uint32_t> mr, cj;
+    static const bool mw_k = !getenv("KYV_MATCHW_KERNEL") || atoi(getenv("KYV_MATCHW_KERNEL")) != 0;
+    std::vector<uint32_t> mr, cj, mw;
     sl.pw.clear();
     for (uint32_t q : sl.ml) {
       const RuleDesc& rd = rs.rules[q];
+      if (mw_k && rd.pre == NONE && (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN || rd.kind == RK_FALLBACK)) {
+        mw.push_back(q);  // match_walk_kernel
+        continue;
+      }
       if (!pss_k || rd.kind != RK_PSS || rd.pre != NONE) { mr.push_back(q); continue; }
       uint32_t lo = nw, hi = 0;
       for (size_t ri = 0; ri < runs.size(); ri++) {
@@ -867,6 +911,8 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     sl.nmj = (uint32_t)(mr.size() - nlight);
     sl.nmc = (uint32_t)cj.size();
     mr.insert(mr.end(), cj.begin(), cj.end());
+    sl.nmw = (uint32_t)mw.size();  // device list: [match_walk_kernel rules][light][JMESPath][compiled]
+    mr.insert(mr.begin(), mw.begin(), mw.end());
     dfree(sl.mrules);
     sl.mrules = nullptr;
     HIP_OK(dmalloc(&sl.mrules, std::max<size_t>(1, mr.size()) * 4));
@@ -1043,11 +1089,18 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, sl.rbase, d.rcnt, sl.k0, sl.k1};
       HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
       HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
+      if (sl.nmw) {
+        static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
+        auto kf = mwpe == 8 ? match_walk_kernel<8> : mwpe == 6 ? match_walk_kernel<6> : match_walk_kernel<4>;
+        hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const uint32_t*)sl.mrules,
+                           sl.nmw);
+      }
       if (sl.nm)
-        hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, sl.mrules, sl.nm);
+        hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
+                           (const uint32_t*)sl.mrules + sl.nmw, sl.nm);
       if (sl.nmj)
         hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
-                           (const uint32_t*)sl.mrules + sl.nm, sl.nmj);
+                           (const uint32_t*)sl.mrules + sl.nmw + sl.nm, sl.nmj);
       {
         static const int pwpe = getenv("KYV_PSS_WPE") ? atoi(getenv("KYV_PSS_WPE")) : 8;  // C2: 4 0.586, 6 0.587, 8 0.514 ms
         for (const uint3& c : sl.pw) {
