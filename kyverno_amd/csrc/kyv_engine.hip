@@ -575,7 +575,7 @@ __global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict
 __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __restrict__ stage, const uint32_t* __restrict__ rbase,
                                                             const uint16_t* __restrict__ rcnt, const RuleDesc* __restrict__ rules,
                                                             uint32_t nwaves, size_t total, const uint32_t* __restrict__ tbase,
-                                                            FailRec* __restrict__ out, size_t max_out) {
+                                                            FailRec* __restrict__ out, size_t max_out, uint32_t k0) {
   const uint32_t lane = threadIdx.x;
   const size_t c = (size_t)blockIdx.x * WAVE + lane;
   const uint32_t n = c < total ? rcnt[c] : 0u;
@@ -590,14 +590,20 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
   // masked off (cross-lane reads from inactive lanes are undefined), and a record then needs no rule / rbase loads
   __shared__ uint32_t spre[WAVE];
   __shared__ const FailRec* ssrc[WAVE];
+  __shared__ uint32_t skw[WAVE];  // (global rule, match wave, wide): what a 16-byte StageRec leaves implicit
+  __shared__ uint32_t sw[WAVE];
   spre[lane] = pre;
   ssrc[lane] = n ? chunk_stage(stage, rbase, rules, nwaves, c) : nullptr;
+  if (n) {
+    const uint32_t k = (uint32_t)(c / nwaves);
+    skw[lane] = (k + k0) | (rules[k].uses_meta ? 0x80000000u : 0u);
+    sw[lane] = (uint32_t)(c % nwaves);
+  }
   __syncthreads();
   const uint32_t base = tbase[blockIdx.x];
-  // records as 16-byte halves: half h of record i moves from lane (2i + h) mod 64, so stores are one contiguous run
-  const uint32_t H = 2 * T;
-  for (uint32_t x = lane; x < H; x += WAVE) {
-    const uint32_t i = x >> 1;
+  // one record per lane: whole FailRecs of wide chunks copied, StageRecs expanded; stores of consecutive lanes are
+  // consecutive 32-byte records
+  for (uint32_t i = lane; i < T; i += WAVE) {
     uint32_t lo = 0, hi = WAVE - 1;  // smallest j with pre[j] > i
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -605,9 +611,29 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
     }
     const uint32_t j = lo;
     const uint32_t first = j ? spre[j - 1] : 0u;
-    const FailRec* src = ssrc[j] + (i - first);
-    if (base + i < max_out)
-      reinterpret_cast<uint4*>(out + base + i)[x & 1] = reinterpret_cast<const uint4*>(src)[x & 1];
+    if (base + i >= max_out) continue;
+    uint4* dst = reinterpret_cast<uint4*>(out + base + i);
+    const uint32_t kw = skw[j];
+    if (kw & 0x80000000u) {
+      const uint4* src = reinterpret_cast<const uint4*>(ssrc[j] + (i - first));
+      dst[0] = src[0];
+      dst[1] = src[1];
+    } else {
+      const uint4 s = reinterpret_cast<const uint4*>(ssrc[j])[i - first];  // StageRec
+      FailRec f;
+      f.res = sw[j] * WAVE + (s.y & (WAVE - 1));
+      f.rule = kw;
+      f.tmpl = s.x;
+      f.alt = (uint16_t)(s.y >> 8);
+      f.nalt = 0;
+      f.idx[0] = (uint16_t)s.z; f.idx[1] = (uint16_t)(s.z >> 16);
+      f.idx[2] = (uint16_t)s.w; f.idx[3] = (uint16_t)(s.w >> 16);
+      f.key[0] = NONE;
+      f.key[1] = NONE;
+      const uint4* fp = reinterpret_cast<const uint4*>(&f);
+      dst[0] = fp[0];
+      dst[1] = fp[1];
+    }
   }
 }
 
@@ -1142,7 +1168,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       hipLaunchKernelGGL(compact_sum_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.rcnt, nchunks, d.tsum);
       hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, d.tsum, ntiles, d.nrecs);
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, sl.rbase, d.rcnt, drules,
-                         d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs);
+                         d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs, sl.k0);
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(sl.ev[3], stream));
       if (multi) {  // phase times of this slice before its events are recorded again

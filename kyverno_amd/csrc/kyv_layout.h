@@ -444,5 +444,14 @@ struct FailRec {        // 32 bytes; one per failing pattern (per failing anyPat
   uint32_t key[MAX_SLOTS];
 };
 static_assert(sizeof(FailRec) == 32, "fail record size");
+// A failing-path record as the walk stages it for a rule without metadata-expansion sites (no resolved keys): the
+// rule and the match wave are those of the staging chunk, so 16 bytes carry the rest (compact_copy_kernel expands
+// it to a FailRec). Rules with expansion sites stage whole FailRecs.
+struct StageRec {
+  uint32_t tmpl;
+  uint32_t lane_alt;    // resource offset in the chunk's match wave (bits 0..5) | alternative << 8
+  uint16_t idx[MAX_IDX];
+};
+static_assert(sizeof(StageRec) == 16, "staged record size");
 
 }  // namespace kyv

@@ -699,6 +699,7 @@ struct DevOut {
 struct WaveSink {
   FailRec* recs;
   uint32_t n;  // wave-uniform
+  bool wide;   // wave-uniform: the rule has metadata-expansion sites, records carry keys (whole FailRecs)
   __device__ __forceinline__ void emit(bool has, const FailRec& f) {
 #ifdef KYV_EXP_NOSINK
     return;
@@ -706,7 +707,18 @@ struct WaveSink {
     unsigned long long m = __ballot(has);
     if (!m) return;
     const uint32_t lane = threadIdx.x & (WAVE - 1);
-    if (has) recs[n + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = f;
+    if (has) {
+      const uint32_t at = n + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+      if (wide) {
+        recs[at] = f;
+      } else {  // 16-byte StageRec: a wave's records are one contiguous run of 16-byte stores
+        StageRec s;
+        s.tmpl = f.tmpl;
+        s.lane_alt = (f.res & (WAVE - 1)) | ((uint32_t)f.alt << 8);
+        for (int i = 0; i < MAX_IDX; i++) s.idx[i] = f.idx[i];
+        reinterpret_cast<StageRec*>(recs)[at] = s;
+      }
+    }
     n += (uint32_t)__popcll(m);
   }
 };
@@ -780,7 +792,7 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
     }
     wk.rootmap = (it.x & ITEM_ROOT_MAP) != 0;
     const uint32_t alts = rd.kind == RK_PATTERN ? 1u : min(rd.nalts, (uint32_t)MAX_ALTS);
-    WaveSink sink{o.stage + sld32(o.rbase + (k - o.rule_lo)) + (size_t)w * WAVE * alts, 0u};
+    WaveSink sink{o.stage + sld32(o.rbase + (k - o.rule_lo)) + (size_t)w * WAVE * alts, 0u, rd.uses_meta != 0};
     uint8_t st = pair_walk(v, rd, active, r, k, v.nodes + it.y, wk, sink);
     if (magic) st = ST_FALLBACK;
     if (active || magic) o.status[(size_t)k * v.nres + r] = st;
