@@ -278,7 +278,10 @@ struct MetaSite {       // metadata-expansion site (wildcards.go:62-83)
   X(CAP_SYS_CHROOT, "SYS_CHROOT") X(SYSCTL_SHM, "kernel.shm_rmid_forced")                                    \
   X(SYSCTL_PORTRANGE, "net.ipv4.ip_local_port_range") X(SYSCTL_SYNCOOKIES, "net.ipv4.tcp_syncookies")        \
   X(SYSCTL_PINGRANGE, "net.ipv4.ping_group_range") X(SYSCTL_UNPRIV, "net.ipv4.ip_unprivileged_port_start")   \
-  X(FAKE, "fake") X(NIL_STR, "<nil>")
+  X(FAKE, "fake") X(NIL_STR, "<nil>")                                                                        \
+  X(ENV, "env") X(VALUEFROM, "valueFrom") X(COMMAND, "command") X(ARGS, "args") X(WORKINGDIR, "workingDir")   \
+  X(IMAGEPULLPOLICY, "imagePullPolicy") X(NODESELECTOR, "nodeSelector") X(SERVICEACCOUNTNAME, "serviceAccountName") \
+  X(RESTARTPOLICY, "restartPolicy") X(TGPS, "terminationGracePeriodSeconds") X(ADS, "activeDeadlineSeconds")
 
 enum WellKnown : uint32_t {
 #define KYV_WK_ENUM(id, s) K_##id,

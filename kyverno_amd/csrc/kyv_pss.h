@@ -162,6 +162,24 @@ KYV_HD void decode_container(Dec& d, uint32_t c) {
       d.str(get(R, p, KSID(PROTOCOL)));
       d.str(get(R, p, KSID(HOSTIP)));
     }
+  // the commonly set Container fields beyond what the checks read: []EnvVar{name, value, valueFrom}, command /
+  // args []string, workingDir / imagePullPolicy string
+  uint32_t env = get(R, c, KSID(ENV));
+  if (d.arr(env))
+    for (uint32_t i = 0; i < R[env].b; i++) {
+      uint32_t e = R[env].a + i;
+      if (!d.obj(e)) continue;
+      d.str(get(R, e, KSID(NAME)));
+      d.str(get(R, e, KSID(VALUE)));
+      d.obj(get(R, e, KSID(VALUEFROM)));
+    }
+  const uint32_t skeys[2] = {KSID(COMMAND), KSID(ARGS)};
+  for (uint32_t key : skeys) {
+    uint32_t l = get(R, c, key);
+    if (d.arr(l)) for (uint32_t i = 0; i < R[l].b; i++) d.str(R[l].a + i);
+  }
+  d.str(get(R, c, KSID(WORKINGDIR)));
+  d.str(get(R, c, KSID(IMAGEPULLPOLICY)));
   dec_container_sc(d, c);
 }
 
@@ -208,6 +226,15 @@ KYV_HD bool decode_ok_spec(Dec& d, uint32_t spec) {
     }
   uint32_t os = get(R, spec, KSID(OS));
   if (d.obj(os)) d.str(get(R, os, KSID(NAME)));
+  // commonly set PodSpec fields beyond what the checks read: nodeSelector map[string]string, serviceAccountName /
+  // restartPolicy string, terminationGracePeriodSeconds / activeDeadlineSeconds *int64
+  uint32_t ns = get(R, spec, KSID(NODESELECTOR));
+  if (d.obj(ns)) for (uint32_t i = 0; i < R[ns].b; i++) d.str(R[ns].a + i);
+  d.str(get(R, spec, KSID(SERVICEACCOUNTNAME)));
+  d.str(get(R, spec, KSID(RESTARTPOLICY)));
+  int64_t t;
+  d.i64(get(R, spec, KSID(TGPS)), INT64_MIN, INT64_MAX, &t);
+  d.i64(get(R, spec, KSID(ADS)), INT64_MIN, INT64_MAX, &t);
   return !d.bad;
 }
 

@@ -134,6 +134,18 @@ Container dec_container(const VP& v) {
     }
     c.hostPorts.push_back(hp);
   }
+  // commonly set fields beyond what the checks read (env, command / args, workingDir, imagePullPolicy)
+  for (auto& e : want_arr(v->get("env"), "env")) {
+    want_obj(e, "EnvVar");
+    if (isnil(e)) continue;
+    want_str(e->get("name"), "name");
+    want_str(e->get("value"), "value");
+    want_obj(e->get("valueFrom"), "EnvVarSource");
+  }
+  for (const char* k : {"command", "args"})
+    for (auto& s : want_arr(v->get(k), k)) want_str(s, k);
+  want_str(v->get("workingDir"), "workingDir");
+  want_str(v->get("imagePullPolicy"), "imagePullPolicy");
   VP sc = v->get("securityContext");
   want_obj(sc, "SecurityContext");
   if (!isnil(sc)) {
@@ -233,6 +245,15 @@ Pod dec_pod(const VP& meta, const VP& spec) {
   VP os = spec->get("os");
   want_obj(os, "PodOS");
   if (!isnil(os)) p.osName = want_str(os->get("name"), "name");
+  // commonly set fields beyond what the checks read
+  VP nsel = spec->get("nodeSelector");
+  want_obj(nsel, "nodeSelector");
+  if (!isnil(nsel)) for (auto& kv : nsel->o) want_str(kv.second, "nodeSelector");
+  want_str(spec->get("serviceAccountName"), "serviceAccountName");
+  want_str(spec->get("restartPolicy"), "restartPolicy");
+  int64_t t;
+  want_int(spec->get("terminationGracePeriodSeconds"), "terminationGracePeriodSeconds", INT64_MIN, INT64_MAX, t);
+  want_int(spec->get("activeDeadlineSeconds"), "activeDeadlineSeconds", INT64_MIN, INT64_MAX, t);
   return p;
 }
 
