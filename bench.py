@@ -492,6 +492,9 @@ def main():
                                            "verdict + PSS mask + failure records) of the pairs this kernel decides, "
                                            "CPU-accounted on a 20k-resource sample and scaled to the shard, / the "
                                            "kernel's time (HIP events on the evaluation stream)",
+                         "overlap": "the compiled condition kernels run on a second HIP stream concurrently with the "
+                                    "walk (kyv_engine.hip cstream): phase times are spans under that overlap, their "
+                                    "sum exceeds evaluation_ms; evaluation_frac is the whole evaluation's figure",
                          "phase_ms": phase,
                          "phase_alg_bytes": phase_bytes,
                          "evaluation_ms": kernel_ms,

@@ -200,6 +200,7 @@ struct SliceSched {
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // after match, condition, walk, compaction (phase timing)
+  hipEvent_t cev[2] = {nullptr, nullptr};  // the slice's condition kernels on the condition stream (start, end)
   int jit_state = -1;            // what the schedules were laid out for (0 interpreter only, 1 with the jit kernel)
 };
 
@@ -219,6 +220,10 @@ struct DeviceResults {
   size_t max_slice_rules = 0;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  // the compiled condition kernels run on a second stream, concurrently with the walk (they write other rules'
+  // verdict rows and read nothing the match / walk phases produce); joined before the verdict histogram
+  hipStream_t cstream = nullptr;
+  hipEvent_t cfork = nullptr, cjoin = nullptr;
   View* view = nullptr;  // device copy of the View the kernel reads
   WorkLists wl{};                // walk work lists (kyv_wave.h), slice-local rule index
   std::vector<SliceSched> slices;
@@ -232,8 +237,10 @@ static void free_dev_results(DeviceResults& d, int dev) {
   for (auto& sl : d.slices) {
     dfree(sl.rbase); dfree(sl.mrules); dfree(sl.sched);
     for (auto e : sl.ev) if (e) hipEventDestroy(e);
+    for (auto e : sl.cev) if (e) hipEventDestroy(e);
   }
   stream_put(dev, d.stream, d.e0, d.e1);
+  stream_put(dev, d.cstream, d.cfork, d.cjoin);
   d = DeviceResults();
 }
 
@@ -1096,13 +1103,22 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
   double total_ms = 0;
   double phase[5] = {0, 0, 0, 0, 0};
-  for (auto& sl : d.slices)
+  for (auto& sl : d.slices) {
     for (auto& e : sl.ev) if (!e) HIP_OK(hipEventCreate(&e));
+    for (auto& e : sl.cev) if (!e) HIP_OK(hipEventCreate(&e));
+  }
   int n = std::max(1, iters);
   std::vector<FailRec> host_recs;
+  // concurrent condition stream (KYV_COND_STREAM=0: the evaluation stream)
+  static const bool cond_conc = !getenv("KYV_COND_STREAM") || atoi(getenv("KYV_COND_STREAM")) != 0;
+  bool conc = false;
+  for (auto& sl : d.slices) conc = conc || !sl.cw.empty();
+  conc = conc && cond_conc;
+  if (conc && !d.cstream) stream_get(&d.cstream, &d.cfork, &d.cjoin);
   for (int it = 0; it < n; it++) {
     const bool collect = copy_back && out && it == n - 1;
     const double sum_before = phase[0] + phase[1] + phase[2] + phase[3];
+    bool joined = false;
     host_recs.clear();
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.counts, 0, std::max<size_t>(1, nrules) * NSTATUS * 8, stream));
@@ -1141,11 +1157,23 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       // compiled condition rules: one kernel each over the waves of its kind gate
       // (the View goes by pointer: a by-value View would be copied to scratch memory, since the kernels take its
       // address for out-of-line helpers; measured 40 % slower)
+      hipStream_t cs = stream;
+      if (conc && !sl.cw.empty()) {  // fork: after the resets and the match phase on the evaluation stream
+        HIP_OK(hipEventRecord(d.cfork, stream));
+        HIP_OK(hipStreamWaitEvent(d.cstream, d.cfork, 0));
+        HIP_OK(hipEventRecord(sl.cev[0], d.cstream));
+        cs = d.cstream;
+      }
       for (const uint3& c : sl.cw) {
         const View* vp = d.view;
         uint32_t w0 = c.y;
         void* args[] = {(void*)&vp, (void*)&o, (void*)&w0};
-        HIP_OK(hipModuleLaunchKernel(dr->jconds[c.x], c.z, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        HIP_OK(hipModuleLaunchKernel(dr->jconds[c.x], c.z, 1, 1, BLOCK, 1, 1, 0, cs, args, nullptr));
+      }
+      if (cs != stream) {
+        HIP_OK(hipEventRecord(sl.cev[1], d.cstream));
+        HIP_OK(hipEventRecord(d.cjoin, d.cstream));
+        joined = true;
       }
       HIP_OK(hipEventRecord(sl.ev[1], stream));
       if (sl.grid[0]) {
@@ -1189,6 +1217,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     static const size_t hmul = getenv("KYV_HIST") ? (size_t)std::max(1, atoi(getenv("KYV_HIST"))) : 8;
     const uint32_t hgrid = (uint32_t)std::max<size_t>(
         1, std::min<size_t>(((size_t)d.cus * hmul + nrules - 1) / std::max<size_t>(1, nrules), (nres / 16 + HIST_BLOCK - 1) / HIST_BLOCK));
+    if (joined) HIP_OK(hipStreamWaitEvent(stream, d.cjoin, 0));  // the histogram reads every verdict row
     if (nrules && nres) hipLaunchKernelGGL(status_hist_kernel, dim3(hgrid, (uint32_t)nrules), dim3(HIST_BLOCK), 0, stream, d.status, nres, d.counts);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d.e1, stream));
@@ -1199,6 +1228,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     if (!multi && !d.slices.empty() && nres && d.slices[0].k1 > d.slices[0].k0) slice_phases(d.slices[0], d.e0, phase);
     const double sum_after = phase[0] + phase[1] + phase[2] + phase[3];
     phase[4] += std::max(0.0, ms - (sum_after - sum_before));  // the rest: verdict histogram (+ slice gaps)
+    if (joined)  // the condition kernels' own span on their stream (overlapping the walk), per slice
+      for (auto& sl : d.slices) {
+        float cms = 0;
+        if (!sl.cw.empty() && hipEventElapsedTime(&cms, sl.cev[0], sl.cev[1]) == hipSuccess) phase[1] += cms;
+      }
   }
 #ifdef KYV_EXP_STEPS
   {
