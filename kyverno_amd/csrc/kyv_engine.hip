@@ -224,6 +224,10 @@ struct DeviceResults {
   // verdict rows and read nothing the match / walk phases produce); joined before the verdict histogram
   hipStream_t cstream = nullptr;
   hipEvent_t cfork = nullptr, cjoin = nullptr;
+  // the second and later runtime-compiled walk groups run on a third stream beside the first (independent rules:
+  // own chunk schedules, verdict rows and staging slots), joined before the slice's compaction
+  hipStream_t wstream = nullptr;
+  hipEvent_t wfork = nullptr, wjoin = nullptr;
   View* view = nullptr;  // device copy of the View the kernel reads
   WorkLists wl{};                // walk work lists (kyv_wave.h), slice-local rule index
   std::vector<SliceSched> slices;
@@ -241,6 +245,7 @@ static void free_dev_results(DeviceResults& d, int dev) {
   }
   stream_put(dev, d.stream, d.e0, d.e1);
   stream_put(dev, d.cstream, d.cfork, d.cjoin);
+  stream_put(dev, d.wstream, d.wfork, d.wjoin);
   d = DeviceResults();
 }
 
@@ -1115,6 +1120,12 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   for (auto& sl : d.slices) conc = conc || !sl.cw.empty();
   conc = conc && cond_conc;
   if (conc && !d.cstream) stream_get(&d.cstream, &d.cfork, &d.cjoin);
+  // off by default: measured 13.43 (one stream) vs 13.53 ms (groups overlapped) on C3 10M
+  static const bool walk_conc = getenv("KYV_WALK_STREAM") && atoi(getenv("KYV_WALK_STREAM")) != 0;
+  bool wconc = false;
+  for (auto& sl : d.slices) wconc = wconc || sl.cm.size() > 2;
+  wconc = wconc && walk_conc;
+  if (wconc && !d.wstream) stream_get(&d.wstream, &d.wfork, &d.wjoin);
   for (int it = 0; it < n; it++) {
     const bool collect = copy_back && out && it == n - 1;
     const double sum_before = phase[0] + phase[1] + phase[2] + phase[3];
@@ -1181,13 +1192,26 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
                            depth);
         HIP_OK(hipGetLastError());
       }
+      bool wforked = false;
+      if (wconc)  // fork after the match phase (the work lists), before the first group is queued
+        for (size_t cls = 2; cls < sl.cm.size() && !wforked; cls++)
+          if (sl.grid[cls]) {
+            HIP_OK(hipEventRecord(d.wfork, stream));
+            HIP_OK(hipStreamWaitEvent(d.wstream, d.wfork, 0));
+            wforked = true;
+          }
       for (size_t cls = 1; cls < sl.cm.size(); cls++) {
         if (!sl.grid[cls]) continue;
         const View* vp = d.view;
         WorkLists wl = d.wl;
         ChunkMap cmj = sl.cm[cls];
         void* args[] = {(void*)&vp, (void*)&o, (void*)&wl, (void*)&cmj};
-        HIP_OK(hipModuleLaunchKernel(dr->jfns[cls - 1], sl.grid[cls], 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        const hipStream_t ws = (wforked && cls >= 2) ? d.wstream : stream;
+        HIP_OK(hipModuleLaunchKernel(dr->jfns[cls - 1], sl.grid[cls], 1, 1, BLOCK, 1, 1, 0, ws, args, nullptr));
+      }
+      if (wforked) {  // the compaction reads every walk group's staged records
+        HIP_OK(hipEventRecord(d.wjoin, d.wstream));
+        HIP_OK(hipStreamWaitEvent(stream, d.wjoin, 0));
       }
       HIP_OK(hipEventRecord(sl.ev[2], stream));
       const size_t nchunks = nsr * (size_t)d.wl.nwaves;
