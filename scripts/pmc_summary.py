@@ -92,6 +92,8 @@ def main(tag):
         "launches_per_evaluation": fac,
         "evaluations": nev,
         "eval_avg_ns": eval_ns,
+        "eval_note": "sum of the evaluation's kernel durations; kernels on the concurrent condition stream overlap "
+                     "the walk, so this exceeds the evaluation's wall time (bench roofline.evaluation_ms)",
         "dominant_kernel": dom,
         "dominant_phase": dom_phase,
         "phases": ph,
