@@ -92,6 +92,62 @@ def dist_setup(gpus):
     return rank, world, local, pg
 
 
+def all_gather_obj(pg, obj):
+    if pg is None:
+        return [obj]
+    out = [None] * pg.get_world_size()
+    pg.all_gather_object(out, obj)
+    return out
+
+
+def time_gathers(batch, local, rank, world):
+    """Report assembly over the device-resident results of the last timed evaluation: RCCL
+    all-gather of every rank's packed verdicts (scan.gather_verdicts_device) and count-then-gather of its failing-path
+    rows (scan.gather_failures_device; a rule-sliced shard keeps no resident rows and reports so), each timed on its
+    own after a warm-up call, max over ranks. At world size 1 the same calls run over a one-rank RCCL group."""
+    import torch
+    import torch.distributed as dist
+    from kyverno_amd import scan
+    from kyverno_amd import _lib as K
+    torch.cuda.set_device(local)
+    dev = "cuda:%d" % local
+    if not dist.is_initialized():  # N = 1: a one-rank group, so the same RCCL path runs
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(dev))
+        g, own = None, True
+    else:
+        g, own = dist.new_group(backend="nccl"), False
+    out = {"backend": "nccl (RCCL)", "world": world}
+    try:
+        def timed(fn):
+            fn()  # warm-up (communicator setup)
+            torch.cuda.synchronize()
+            dist.barrier(group=g)
+            t0 = time.perf_counter()
+            r = fn()
+            torch.cuda.synchronize()
+            dist.barrier(group=g)
+            return r, time.perf_counter() - t0
+        full, tv = timed(lambda: scan.gather_verdicts_device(batch, group=g, device=dev, tensor=True)[0])
+        out["verdicts_ms"] = tv * 1e3
+        out["verdict_matrix"] = list(full.shape)
+        out["verdict_wire_bytes"] = int(full.shape[0]) * ((int(full.shape[1]) + 1) // 2)
+        del full
+        try:
+            rows, tf = timed(lambda: scan.gather_failures_device(batch, 0, group=g, device=dev, tensor=True))
+            out["failures_ms"] = tf * 1e3
+            out["failure_rows"] = int(rows.shape[0])
+            del rows
+        except K.KyvError as e:
+            out["failures"] = "not resident: %s" % str(e)[:160]
+        torch.cuda.empty_cache()
+    finally:
+        if own:
+            dist.destroy_process_group()
+    return out
+
+
 def barrier(pg):
     if pg is not None:
         pg.barrier()
@@ -157,13 +213,50 @@ def host_cpus():
     return info
 
 
-def cpu_baseline_and_parity(policies, rs, data, nsl, jit, target_s=10.0, cap=400000, device=0):
+def _lut():
+    import numpy as np
+    return np.array(_MATRIX_TO_DEVICE, dtype=np.uint8)
+
+
+def compare_verdicts(rs, names, m, st, n):
+    """device verdict rows st [rules, >= n] (input order) vs the oracle matrix m over the same n resources; a pair is
+    excluded only when BOTH sides say ND (a one-sided ND is a mismatch)"""
+    import numpy as np
+    row = {nm: i for i, nm in enumerate(names)}
+    lut = _lut()
+    compared = mism = nd = 0
+    first = None
+    for k, rule in enumerate(rs.rules):
+        key = (rs.policies[rule["policy"]]["name"], rule["name"])
+        exp = lut[m[row[key]]] if key in row else np.zeros(n, np.uint8)
+        got = np.asarray(st[k, :n]) & 7
+        ndm = (exp == 7) & (got == 7)
+        nd += int(ndm.sum())
+        bad = np.nonzero(exp != got)[0]
+        compared += n - int(ndm.sum())
+        mism += len(bad)
+        if len(bad) and first is None:
+            first = {"rule": list(key), "resource": int(bad[0]), "device": int(got[bad[0]]), "oracle": int(exp[bad[0]])}
+    return {"resources": n, "pairs_compared": compared, "mismatches": mism, "nondeterministic_pairs_both": nd,
+            "first_mismatch": first}
+
+
+def timed_prefix_status(batch, device, cap):
+    """the timed evaluation's OWN verdicts for the first `cap` input-order resources of the batch (resident on the
+    device after the last timed step: kind-major order and every rule slice included), copied back for parity"""
+    from kyverno_amd import scan
+    return scan.local_verdicts_device(batch, device="cuda:%d" % device, ncols=cap)
+
+
+def cpu_baseline_and_parity(policies, rs, data, nsl, jit, timed_status, target_s=10.0, cap=400000, device=0):
     """CPU baseline: the oracle (CPU restatement of engine.Validate, oracle/) over a bounded prefix of this rank's
     corpus on the job's whole CPU share, growing until one timed pass takes >= target_s, plus a single-thread pass
-    over a smaller prefix. Parity: the device evaluates the same prefix (its own batch, with the walk kernel the
-    timed region ran: jit) and every (resource, rule) verdict is compared with the oracle's, then the failing path
-    and RuleResponse.Message of every FAIL pair."""
-    import numpy as np
+    over a smaller prefix. Parity, two legs over the same prefix:
+      timed_batch  the verdicts the timed evaluation itself left on the device (timed_status: first resources of the
+                   timed batch in input order -- its kind-major layout and rule slices included) vs the oracle's;
+      texts        the failing path and RuleResponse.Message of every FAIL pair, from a device evaluation of the
+                   prefix as its own batch (the walk kernel the timed region ran: jit), whose verdicts are also
+                   compared pair by pair."""
     from oracle import oracle as O
     from kyverno_amd import engine as E
     hc = host_cpus()
@@ -192,36 +285,42 @@ def cpu_baseline_and_parity(policies, rs, data, nsl, jit, target_s=10.0, cap=400
            "nproc": hc["nproc"], "affinity_cpus": hc["affinity"], "cgroup_cpu_quota": hc["cgroup_quota"],
            "model": hc["model"], "threads_source": hc["share_source"],
            "reference_go_engine": "unavailable offline (no Go toolchain or module cache; SURVEY §8(c)/(d))"}
-    # parity on the same prefix: device verdict matrix vs the oracle's, pair by pair, then every FAIL pair's texts
+    # leg 1: the timed batch's own verdicts
+    nt = min(want, timed_status.shape[1]) if timed_status is not None else 0
+    timed = compare_verdicts(rs, names, m, timed_status, nt) if nt else None
+    # leg 2: the prefix as its own batch, pair by pair, then every FAIL pair's texts
     b = E.Batch(rs, b"\n".join(lines[:want]), nsl)
     res = E.evaluate(rs, b, backend="gpu", device=device, jit=jit)
-    row = {nm: i for i, nm in enumerate(names)}
-    lut = np.array(_MATRIX_TO_DEVICE, dtype=np.uint8)
-    st = np.asarray(res.status)
-    compared = mism = nd = 0
-    first = None
-    for k, rule in enumerate(rs.rules):
-        key = (rs.policies[rule["policy"]]["name"], rule["name"])
-        exp = lut[m[row[key]]] if key in row else np.zeros(want, np.uint8)
-        got = st[k]
-        ndm = (exp == 7) | (got == 7)
-        nd += int(ndm.sum())
-        bad = np.nonzero((exp != got) & ~ndm)[0]
-        compared += want - int(ndm.sum())
-        mism += len(bad)
-        if len(bad) and first is None:
-            first = {"rule": list(key), "resource": int(bad[0]), "device": int(got[bad[0]]), "oracle": int(exp[bad[0]])}
+    sep = compare_verdicts(rs, names, m, res.status, want)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import parity_util as PU
     ts = PU.compare_fail_texts(rs, res, names, tx, want)
-    parity = {"status": "ok" if mism == 0 and ts["nbad"] == 0 else "mismatch", "resources": want,
-              "pairs_compared": compared, "mismatches": mism, "nondeterministic_pairs": nd, "first_mismatch": first,
+    ok = sep["mismatches"] == 0 and ts["nbad"] == 0 and (timed is None or timed["mismatches"] == 0)
+    parity = {"status": "ok" if ok else "mismatch", "resources": want,
+              "timed_batch": timed, "timed_batch_note": "verdicts of the last timed evaluation, read back from the "
+                                                        "device (kyv_batch_export_status), first %d resources" % nt,
+              "pairs_compared": sep["pairs_compared"], "mismatches": sep["mismatches"],
+              "nondeterministic_pairs_both": sep["nondeterministic_pairs_both"], "first_mismatch": sep["first_mismatch"],
               "jit": bool(res.jit), "timed_jit": bool(jit),
               "fail_pairs": ts["fail_pairs"], "paths_compared": ts["paths_compared"],
               "path_mismatches": ts["path_mismatches"], "messages_compared": ts["messages_compared"],
               "message_mismatches": ts["message_mismatches"], "messages_unrenderable": ts["messages_unrenderable"],
               "first_text_mismatch": [str(x)[:300] for x in ts["bad"][:1]]}
     return cpu, parity
+
+
+def shard_parity(policies, rs, data, nsl, timed_status, cap=100000):
+    """ranks > 0 of a multi-GPU run: the timed evaluation's own verdicts on this rank's shard prefix vs the oracle"""
+    from oracle import oracle as O
+    threads = max(1, host_cpus()["share"])
+    lines = [x for x in data.split(b"\n", cap)[:cap] if x.strip()]
+    n = min(len(lines), timed_status.shape[1])
+    names, m, secs = O.validate_matrix(policies, b"[" + b",".join(lines[:n]) + b"]", nsl, threads=threads, nres=n,
+                                       timed=True)
+    out = compare_verdicts(rs, names, m, timed_status, n)
+    out["status"] = "ok" if out["mismatches"] == 0 else "mismatch"
+    out["oracle_s"] = secs
+    return out
 
 
 # device phase -> kernel-name prefixes of that phase in a rocprofv3 kernel trace
@@ -354,6 +453,7 @@ def main():
                     help="total resources over all GPUs (default 10M c3, 1M c2 / c4 / c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (flatten + H2D + eval + D2H) leg")
+    ap.add_argument("--no-gather", action="store_true", help="skip the timed RCCL all-gather of the resident results")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         spawn_ranks(args.gpus)
@@ -381,16 +481,6 @@ def main():
     log("rank %d: flattened %d resources into %d node rows in %.1f s" % (rank, batch.n, batch.stats()["nodes"], t_flat))
     pairs = nrules * batch.n
 
-    # algorithmic bytes per eval: CPU accounting over a sample of this shard, split by device phase
-    sample_n = min(batch.n, 20000)
-    sb = E.Batch(rs, b"\n".join(data.split(b"\n", sample_n)[:sample_n]), nsl)
-    acct = E.evaluate(rs, sb, backend="cpu", account_bytes=True)
-    bytes_per_eval = acct.alg_bytes / max(1, nrules * sb.n)
-    scale = batch.n / max(1, sb.n)
-    phase_bytes = {k: v * scale for k, v in acct.alg_bytes_phase.items()}  # per launch over the whole shard
-    del sb, acct
-    log("rank %d: %.1f algorithmic bytes per eval (CPU accounting over %d resources)" % (rank, bytes_per_eval, sample_n))
-
     # warmup (first call uploads the batch, loads / compiles the walk kernel, allocates the resident buffers)
     t0 = time.time()
     first = E.evaluate(rs, batch, backend="gpu", device=local, copy_back=False)
@@ -402,6 +492,18 @@ def main():
     del first
     for _ in range(max(0, args.warmup - 1)):
         E.evaluate(rs, batch, backend="gpu", device=local, copy_back=False)
+    # algorithmic bytes per launch, counted by the kernels themselves: one evaluation of this whole shard
+    # with the byte-accounting build of the same kernels (KYV_ACCT: every per-resource load and result store adds its
+    # bytes to device counters), phases serialised so each phase's bytes are its own; outside the timed region
+    t0 = time.time()
+    acct = E.evaluate(rs, batch, backend="gpu", device=local, copy_back=False, account_bytes=True, jit=timed_jit)
+    phase_bytes = dict(acct.alg_bytes_phase)
+    alg_class = dict(acct.alg_bytes_class)
+    bytes_per_eval = acct.alg_bytes / max(1, pairs)
+    acct_counts_ok = acct.counts == counts  # the accounting build decides every pair as the product build does
+    del acct
+    log("rank %d: %.1f algorithmic bytes per eval (device-counted over the shard, %.1f s): %s" % (
+        rank, bytes_per_eval, time.time() - t0, phase_bytes))
 
     barrier(pg)
     t0 = time.perf_counter()
@@ -425,6 +527,17 @@ def main():
     total_pairs = all_sum(pg, dev_pairs)
     total_fb = all_sum(pg, cpu_pairs)
 
+    # the timed evaluation's own verdicts for this rank's shard prefix (parity below), before anything else runs
+    prefix_status = None
+    if not args.no_cpu_baseline:
+        prefix_status = timed_prefix_status(batch, local, 400000 if rank == 0 else 100000)
+    # report assembly of a multi-GPU scan: RCCL all-gather of every rank's verdicts and failing-path
+    # rows straight from the device-resident results of the last timed evaluation, timed after the evaluation
+    gathers = None
+    if not args.no_gather:
+        gathers = time_gathers(batch, local, rank, world)
+        log("rank %d: device-resident gathers %s" % (rank, gathers))
+
     # end to end on this rank: JSON -> flatten -> H2D -> evaluate -> D2H of every verdict (walk kernel already loaded)
     e2e = None
     if not args.no_e2e:
@@ -435,17 +548,35 @@ def main():
                                                        e2e["upload_eval_copyback_s"]))
 
     cpu = parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, parity = cpu_baseline_and_parity(policies, rs, data, nsl, timed_jit, device=local)
-        log("rank 0: parity on the cpu_baseline prefix: %s (%d pairs, %d mismatches; %d FAIL pairs: %d path / %d "
-            "message mismatches)" % (parity["status"], parity["pairs_compared"], parity["mismatches"],
-                                     parity["fail_pairs"], parity["path_mismatches"], parity["message_mismatches"]))
+    rank_parity = None
+    if not args.no_cpu_baseline:
+        if rank == 0:  # cpu_baseline on rank 0; its prefix is also rank 0's parity sample
+            cpu, parity = cpu_baseline_and_parity(policies, rs, data, nsl, timed_jit, prefix_status, device=local)
+            log("rank 0: parity on the cpu_baseline prefix: %s (timed batch: %s; %d pairs, %d mismatches; %d FAIL "
+                "pairs: %d path / %d message mismatches)" % (
+                    parity["status"], parity["timed_batch"], parity["pairs_compared"], parity["mismatches"],
+                    parity["fail_pairs"], parity["path_mismatches"], parity["message_mismatches"]))
+            mine = {"rank": 0, "status": parity["status"], "timed_batch": parity["timed_batch"]}
+        else:  # every other rank checks its own shard prefix of the timed evaluation
+            mine = dict(shard_parity(policies, rs, data, nsl, prefix_status), rank=rank)
+        rank_parity = all_gather_obj(pg, mine)
+        if parity is not None and world > 1:
+            parity["ranks"] = rank_parity
+            if any(p.get("status") != "ok" for p in rank_parity):
+                parity["status"] = "mismatch"
+    gather_ranks = all_gather_obj(pg, gathers) if gathers is not None else None
 
     if rank == 0:
-        # dominant kernel: the device phase with the longest time per evaluation (C3 / C4: the pattern walk)
-        dom = max(("match", "cond", "walk"), key=lambda k: phase[k])
+        # dominant kernel: the device phase with the longest time per evaluation, among all five
+        dom = max(PHASE_KERNELS, key=lambda k: phase[k])
         dom_ms = phase[dom]
         achieved = phase_bytes[dom] / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
+        phase_frac = {k: (phase_bytes[k] / (phase[k] / 1e3) / 1e9 / HBM_PEAK_GBS if phase[k] > 0 else 0.0)
+                      for k in PHASE_KERNELS}
+        eval_frac = sum(phase_bytes.values()) / max(kernel_ms / 1e3, 1e-12) / 1e9 / HBM_PEAK_GBS
+        over = {k: f for k, f in phase_frac.items() if f > 1.0}
+        if eval_frac > 1.0:
+            over["evaluation"] = eval_frac
         wl = {"c3": "C3: charts/kyverno-policies restricted + test/best_practices validate policies (select-secrets "
                     "excluded, SURVEY §8(d); %d compiled rules) over %d mixed resources (%d per GPU)",
               "c2": "C2: podSecurity restricted/latest (%d compiled rules) over %d pods (%d per GPU)",
@@ -485,13 +616,25 @@ def main():
                          "profiled_l2_hit_rate": tr.get("l2_hit") if tr else None,
                          "kernel": {"walk": "kyv_jit_walk (runtime-compiled pattern walk)",
                                     "cond": "kyv_jit_cond (runtime-compiled deny / foreach conditions)",
-                                    "match": "kyv::match_kernel (match / exclude, podSecurity, plain conditions)"}[dom],
+                                    "match": "kyv::match_walk_kernel / match_kernel / pss_kernel (match / exclude, "
+                                             "podSecurity, plain conditions)",
+                                    "compact": "kyv::compact_* (failing-path record compaction)",
+                                    "hist": "kyv::status_hist_kernel (verdict totals)"}[dom],
                          "kernel_ms": dom_ms,
                          "alg_bytes_per_launch": phase_bytes[dom],
-                         "achieved_basis": "algorithmic bytes (SURVEY §8(d): header fields + distinct node rows + "
-                                           "verdict + PSS mask + failure records) of the pairs this kernel decides, "
-                                           "CPU-accounted on a 20k-resource sample and scaled to the shard, / the "
-                                           "kernel's time (HIP events on the evaluation stream)",
+                         "achieved_basis": "algorithmic bytes per launch counted by the kernels themselves: one "
+                                           "evaluation of the whole shard with the KYV_ACCT build of the same kernel "
+                                           "source (kyv_acct.hip, the runtime-compiled kernels with -DKYV_ACCT), "
+                                           "every load of resource data (16-B node rows, 8-B path-column entries, "
+                                           "header fields, work lists) and every result store (verdict bytes, PSS "
+                                           "masks, staged and compacted failing-path records, work lists) counted, "
+                                           "phases serialised; dictionary columns and rule programs excluded (SURVEY "
+                                           "§8(d)); / the kernel's time (HIP events on the evaluation stream)",
+                         "valid": not over,
+                         "frac_over_1": over or None,
+                         "phase_frac": phase_frac,
+                         "alg_bytes_by_class": alg_class,
+                         "accounting_verdicts_match": acct_counts_ok,
                          "overlap": "the compiled condition kernels run on a second HIP stream concurrently with the "
                                     "walk (kyv_engine.hip cstream): phase times are spans under that overlap, their "
                                     "sum exceeds evaluation_ms; evaluation_frac is the whole evaluation's figure",
@@ -499,18 +642,27 @@ def main():
                          "phase_alg_bytes": phase_bytes,
                          "evaluation_ms": kernel_ms,
                          "evaluation_ms_max_rank": kernel_ms_max,
-                         "evaluation_frac": sum(phase_bytes.values()) / max(kernel_ms / 1e3, 1e-12) / 1e9 / HBM_PEAK_GBS,
+                         "evaluation_frac": eval_frac,
                          "bytes_per_eval": bytes_per_eval},
             "cpu_baseline": cpu,
             "parity_prefix": parity,
             "verdicts": {k: v for k, v in counts.items()},
             "cpu_fallback_by_reason": fb_reasons,
+            "report_gather": None if not gather_ranks else {
+                "verdicts_ms_max_rank": max(g.get("verdicts_ms", 0.0) for g in gather_ranks),
+                "failures_ms_max_rank": max(g.get("failures_ms", 0.0) for g in gather_ranks),
+                "ranks": gather_ranks,
+                "note": "timed after the evaluation, outside `value`: RCCL all-gather of the packed verdicts and the "
+                        "failing-path rows from the device-resident results (kyverno_amd/scan.py)"},
             "host": {"generate_s": t_gen, "compile_s": t_compile, "flatten_s": t_flat,
                      "flatten_resources_per_s": batch.n / max(t_flat, 1e-9),
                      "first_eval_incl_upload_s": t_upload, "batch_device_bytes": batch.stats()["device_bytes"],
                      "e2e": e2e},
         }
         print(json.dumps(line), flush=True)
+        if over:  # algorithmic bytes above what HBM can move in the measured time: the accounting is wrong
+            log("roofline INVALID: frac > 1 for %s" % over)
+            sys.exit(3)
     if pg is not None:
         pg.destroy_process_group()
 

@@ -78,6 +78,12 @@ enum { KYV_EVAL_NO_COPYBACK = 1u, KYV_EVAL_ACCOUNT_BYTES = 2u,
           on first use; default = on for batches of >= 65536 resources, else the interpreted walk kernel */
        KYV_EVAL_JIT_OFF = 4u, KYV_EVAL_JIT_ON = 8u };
 
+/* compile flags (kyv_compile_opts.flags) */
+enum { KYV_COMPILE_BACKGROUND = 1u };  /* the ruleset serves background scans only (empty AdmissionInfo, scanner.go:60-110):
+                                          PolicyException match blocks with roles / clusterRoles / subjects are compiled
+                                          as never matching (checkUserInfo); without the flag such exceptions send the
+                                          rules they name to the CPU engine (reason "exception: userInfo ...") */
+
 typedef struct {
   uint32_t abi_version;
   uint32_t flags;
@@ -95,7 +101,10 @@ typedef struct {
   int32_t iterations;    /* timed kernel launches (>=1); results are those of the last launch */
   int32_t threads;       /* CPU backend threads */
   uint32_t flags;        /* KYV_EVAL_NO_COPYBACK: keep verdicts on the device (timing);
-                            KYV_EVAL_ACCOUNT_BYTES (CPU backend): sum algorithmic bytes per pair */
+                            KYV_EVAL_ACCOUNT_BYTES: algorithmic bytes; on the GPU backend one
+                            evaluation with the byte-accounting build of the same kernels (their loads and stores
+                            counted on the device, phases serialised), on the CPU backend the host instantiation's
+                            per-pair touch count */
 } kyv_eval_opts;
 
 typedef struct {
@@ -154,6 +163,10 @@ uint32_t kyv_ruleset_rule_flags(const kyv_ruleset* rs, uint32_t rule);
    gfx950 that needs no GPU (seconds, code-object bytes) */
 int64_t kyv_ruleset_jit_source(const kyv_ruleset* rs, char* buf, size_t cap, uint32_t* nrules_jit);
 int kyv_ruleset_jit_compile(const kyv_ruleset* rs, double* seconds, size_t* code_bytes);
+/* the same with flags: KYV_JIT_ACCOUNTING compiles the byte-accounting build (-DKYV_ACCT) that an accounting
+   evaluation (KYV_EVAL_ACCOUNT_BYTES on the GPU backend) loads; both land in the code-object cache */
+enum { KYV_JIT_ACCOUNTING = 1u };
+int kyv_ruleset_jit_compile_ex(const kyv_ruleset* rs, uint32_t flags, double* seconds, size_t* code_bytes);
 
 /* ---- batch: resources (JSON array or NDJSON) + namespace labels ({"ns": {"k": "v"}}) ---- */
 int kyv_batch_build(const kyv_ruleset* rs, const char* resources_json, size_t len, const char* ns_labels_json,
@@ -180,12 +193,16 @@ int kyv_results_phase_ms(const kyv_results* r, double* out, size_t cap);
 /* bit 0: the runtime-compiled walk kernels evaluated this result's pattern rules (else the interpreter); bit 1: the
  * runtime-compiled condition kernel evaluated its deny / foreach rules with JMESPath operands */
 int kyv_results_jit(const kyv_results* r);
-/* CPU backend with KYV_EVAL_ACCOUNT_BYTES: algorithmic bytes of all pairs (header fields, distinct node rows,
- * verdict, PSS mask, failure records); 0 otherwise */
+/* with KYV_EVAL_ACCOUNT_BYTES: algorithmic bytes of the evaluation (GPU: counted by the accounting build of the
+ * kernels -- node rows, path-column entries, header fields, work lists read; verdicts, PSS masks, failing-path records,
+ * work lists written; CPU: header fields, distinct node rows, verdict, PSS mask, failure records per pair); 0 otherwise */
 uint64_t kyv_results_alg_bytes(const kyv_results* r);
 /* the same bytes split by the device phase that moves them (kyv_results_phase_ms order); a kind-gated pair counts
  * only its verdict-reset byte (phase 0) and its histogram read (phase 4); returns 5 */
 int kyv_results_alg_bytes_phase(const kyv_results* r, uint64_t* out, size_t cap);
+/* GPU accounting evaluation: the counted bytes by class -- out[0] resource-data reads, [1] result / work-list writes,
+ * [2] staged failing-path records; returns 3 */
+int kyv_results_alg_bytes_class(const kyv_results* r, uint64_t* out, size_t cap);
 /* RuleResponse.Message for one pair; returns the full length (may exceed cap), -1 if unavailable */
 int64_t kyv_results_message(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res,
                             uint32_t rule, char* buf, size_t cap);

@@ -59,9 +59,9 @@ EXPORTS = [
     "kyv_batch_num_resources", "kyv_batch_stats_get", "kyv_eval", "kyv_results_free", "kyv_results_status",
     "kyv_results_count", "kyv_results_kernel_ms", "kyv_results_alg_bytes", "kyv_results_message", "kyv_results_path",
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
-    "kyv_ruleset_jit_compile", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
+    "kyv_ruleset_jit_compile", "kyv_ruleset_jit_compile_ex", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
     "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures", "kyv_ruleset_rule_flags",
-    "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase", "kyv_batch_export_status",
+    "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase", "kyv_results_alg_bytes_class", "kyv_batch_export_status",
     "kyv_batch_export_failures",
 ]
 
@@ -133,6 +133,8 @@ def lib():
     L.kyv_results_path.restype = i64
     L.kyv_results_alg_bytes_phase.argtypes = [vp, ctypes.c_void_p, sz]
     L.kyv_results_alg_bytes_phase.restype = i32
+    L.kyv_results_alg_bytes_class.argtypes = [vp, ctypes.c_void_p, sz]
+    L.kyv_results_alg_bytes_class.restype = i32
     L.kyv_results_phase_ms.argtypes = [vp, ctypes.c_void_p, sz]
     L.kyv_results_phase_ms.restype = i32
     L.kyv_results_texts.argtypes = [vp, vp, vp, u32, u32, u32, u32, i32, ctypes.c_void_p, sz, ctypes.c_void_p]
@@ -144,6 +146,7 @@ def lib():
     L.kyv_ruleset_jit_source.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
     L.kyv_ruleset_jit_source.restype = i64
     L.kyv_ruleset_jit_compile.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
+    L.kyv_ruleset_jit_compile_ex.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
     L.kyv_last_error.restype = ctypes.c_char_p
     L.kyv_version.restype = ctypes.c_char_p
     _lib = L

@@ -496,8 +496,6 @@ class AdmissionBatcher:
             batch = E.Batch(self.ruleset, b"\n".join(docs), ns_labels or None)  # NDJSON
             res = E.evaluate(self.ruleset, batch, backend=self.backend, device=self.device)
             st = res.status
-            self.metrics.record(self.ruleset, [p["doc"] for p in self.pol], res, mkind, mns,
-                                cause="admission_request", operation=mop)
             # per policy over the whole batch: "every matched rule passed" (the policy cannot change the decision)
             # and "some pair needs the CPU engine"; only the remaining (request, policy) pairs are assembled rule
             # by rule
@@ -511,13 +509,20 @@ class AdmissionBatcher:
                 cpu[pi] = np.isin(sub, CPU_STATUSES).any(axis=0)
                 quiet[pi] = ((sub == K.ST_NONE) | (sub == K.ST_PASS)).all(axis=0) & ~cpu[pi]
         out = []
+        # (policy, batch row) pairs whose engine response the device produced: only those are recorded as metrics
+        # (userInfo / operation policies, OldResource retries, CPU pairs and policies the cache does not select for
+        # the request are the CPU engine's responses, recorded by the Go shim, or no response at all)
+        rec = np.zeros((len(self.pol), len(docs)), dtype=bool) if docs else None
         for rq, (i_new, i_old) in zip(requests, slots):
-            out.append(self._decide(rq, i_new, i_old, st, res, quiet, cpu))
+            out.append(self._decide(rq, i_new, i_old, st, res, quiet, cpu, rec))
+        if docs:
+            self.metrics.record(self.ruleset, [p["doc"] for p in self.pol], res, mkind, mns,
+                                cause="admission_request", operation=mop, mask=rec)
         self.stats["requests"] += len(requests)
         self.stats["batches"] += 1
         return out
 
-    def _decide(self, rq, i_new, i_old, st, res, quiet, cpu):
+    def _decide(self, rq, i_new, i_old, st, res, quiet, cpu, rec=None):
         op = rq.get("operation", "CREATE")
         new, old = rq.get("object") or {}, rq.get("oldObject") or {}
         ns = rq.get("namespace") or ""
@@ -551,9 +556,13 @@ class AdmissionBatcher:
                 if not old_retry:  # else the OldResource retry would match: the CPU engine validates the new object
                     if quiet[pi, i_new]:
                         self.stats["device_policies"] += 1
+                        if rec is not None:
+                            rec[pi, i_new] = True
                         continue  # pass / no rule responses: no effect on blocking, messages or warnings
                     if not cpu[pi, i_new]:
                         rules = self._device_rules(pi, st, i_new, res)
+                        if rules is not None and rec is not None:
+                            rec[pi, i_new] = True
             if rules is None:
                 if self.cpu_engine is None:
                     pending.append(p["name"])

@@ -14,7 +14,7 @@
 
 namespace kyv {
 void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back,
-              int jit_mode);
+              int jit_mode, bool account);
 void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool account);
 void free_device_images(Ruleset& rs, Batch* b);
 std::string fallback_why(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule);
@@ -90,7 +90,8 @@ int kyv_ruleset_compile_ex(const char* json, size_t len, const char* exceptions_
   if (opts && opts->abi_version != KYV_ABI_VERSION) return fail(KYV_EINVAL, "ABI version mismatch");
   try {
     std::string err;
-    Ruleset* rs = compile_ruleset(json, len, &err, exceptions_json, exceptions_json ? ex_len : 0);
+    Ruleset* rs = compile_ruleset(json, len, &err, exceptions_json, exceptions_json ? ex_len : 0,
+                                  opts && (opts->flags & KYV_COMPILE_BACKGROUND));
     if (!rs) return fail(KYV_EPARSE, err);
     *out = new kyv_ruleset{rs};
     return KYV_OK;
@@ -162,6 +163,19 @@ int kyv_ruleset_jit_compile(const kyv_ruleset* rs, double* seconds, size_t* code
   }
 }
 
+int kyv_ruleset_jit_compile_ex(const kyv_ruleset* rs, uint32_t flags, double* seconds, size_t* code_bytes) {
+  if (!rs) return fail(KYV_EINVAL, "null argument");
+  try {
+    std::vector<uint8_t> jr;
+    std::vector<uint8_t> jc;
+    std::vector<char> code = jit_compile(jit_source(*rs->rs, &jr, &jc), seconds, (flags & KYV_JIT_ACCOUNTING) != 0);
+    if (code_bytes) *code_bytes = code.size();
+    return KYV_OK;
+  } catch (std::exception& e) {
+    return fail(KYV_EINTERNAL, e.what());
+  }
+}
+
 int kyv_ruleset_policy_info(const kyv_ruleset* rs, uint32_t p, kyv_policy_info* out) {
   if (!rs || !out || p >= rs->rs->policies.size()) return fail(KYV_ERANGE, "policy index out of range");
   const PolicyMeta& m = rs->rs->policies[p];
@@ -225,7 +239,7 @@ int kyv_eval(const kyv_ruleset* rs, const kyv_batch* b, const kyv_eval_opts* opt
       bool copy = !(opts && (opts->flags & KYV_EVAL_NO_COPYBACK));
       double ms = 0;
       int jm = !opts ? JIT_AUTO : (opts->flags & KYV_EVAL_JIT_OFF) ? JIT_OFF : (opts->flags & KYV_EVAL_JIT_ON) ? JIT_ON : JIT_AUTO;
-      eval_gpu(*rs->rs, *b->b, dev, iters, &res->r, &ms, copy, jm);
+      eval_gpu(*rs->rs, *b->b, dev, iters, &res->r, &ms, copy, jm, opts && (opts->flags & KYV_EVAL_ACCOUNT_BYTES));
     }
     {
       static std::mutex inv_mu;
@@ -311,6 +325,12 @@ int kyv_results_phase_ms(const kyv_results* r, double* out, size_t cap) {
 }
 
 uint64_t kyv_results_alg_bytes(const kyv_results* r) { return r ? r->r.alg_bytes : 0; }
+
+int kyv_results_alg_bytes_class(const kyv_results* r, uint64_t* out, size_t cap) {
+  if (!r || !out) return fail(KYV_EINVAL, "null argument");
+  for (size_t q = 0; q < 3 && q < cap; q++) out[q] = r->r.alg_bytes_class[q];
+  return 3;
+}
 
 int kyv_results_alg_bytes_phase(const kyv_results* r, uint64_t* out, size_t cap) {
   if (!r || !out) return fail(KYV_EINVAL, "null argument"), -1;

@@ -338,6 +338,7 @@ struct Fallback { std::string why; };
 
 struct Cx {
   Ruleset& rs;
+  bool background = false;  // KYV_COMPILE_BACKGROUND: no admission request info ever reaches these rules
   RuleDesc* rd = nullptr;
   std::map<std::string, int> abits;  // raw anchor key -> bit (per pattern)
   int nslots = 0;
@@ -946,6 +947,12 @@ void compile_exc_block(Cx& c, const Value* mr, std::vector<uint32_t>& out) {
   bool em = false;
   if (lst)
     for (auto& f : lst->a) {
+      // checkUserInfo (pkg/utils/match/match.go:110-150) compares roles / clusterRoles / subjects with the request's
+      // AdmissionInfo: empty in a background scan (never satisfied, compiled as FF_USERINFO), unknown to the device
+      // for an admission caller -> the rule goes to the CPU engine unless the ruleset is background-only
+      if (!c.background)
+        for (const char* k : {"roles", "clusterRoles", "subjects"})
+          if (nonempty_list(f.get(k))) throw Fallback{"exception: userInfo (roles / clusterRoles / subjects need the admission request)"};
       const uint32_t id = compile_filter(c, &f, f.get("resources"), &em);
       c.rs.filters[id].flags &= (uint16_t)~FF_KINDS_STAR;  // namespaceSelector: kind != "" only (match.go:186)
     }
@@ -1829,7 +1836,8 @@ std::string fallback_reason(const Value& r) {  // validator.validate dispatch (v
 
 void mark_gate_exact(Ruleset& rs);
 
-Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const char* exceptions, size_t ex_len) {
+Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const char* exceptions, size_t ex_len,
+                         bool background) {
   auto rs = std::make_unique<Ruleset>();
   try {
     seed_dict(rs->dict);
@@ -1855,6 +1863,7 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
       }
     }
     Cx c{*rs};
+    c.background = background;
     for (auto& pol : docs) {
       if (pol.t != T::Obj) continue;
       std::string kind = pol.str_or("kind");

@@ -429,7 +429,7 @@ struct Gen {
       // decided from the header flags the flattener computed for that position (same order as expand_meta:
       // absent/null metadata, non-object, anchor-like keys, labels / annotations that are not objects of strings)
       const uint32_t sh = meta_pos[pn] == 0 ? RF_META_SHIFT : meta_pos[pn] == 1 ? RF_TMETA1_SHIFT : RF_TMETA2_SHIFT;
-      out << "  { const uint32_t hf = gld32(&w.hp->flags);\n"
+      out << "  { const uint32_t hf = gld32(&w.hp->flags); KYV_ACCT_ADD(0, 4);\n"
              "    if (!(hf & (1u << " << sh << "))) {\n"
              "      if (hf & (2u << " << sh << ")) { w.ost = ST_PANIC; return ok_ret(); }\n"
              "      if (hf & RF_ANCHORISH) { w.ost = ST_FALLBACK; return ok_ret(); }\n";
@@ -1205,6 +1205,7 @@ struct CondGen {
     else out << "  { const int m = jc_match(v, r, " << u(k) << "); if (m >= 0) return (uint8_t)m; }\n";
     out << "#ifdef KYV_EXP_JC_EMPTY\n  return ST_PASS;\n#endif\n";
     out << "  const ResHeader& h = v.hdr[r];\n"
+        << "  KYV_ACCT_ADD(0, 8);  // header: node count, root\n"
         << "  if (h.nnodes >= (1u << COL_TYPE_SHIFT)) return ST_FALLBACK;  // no path columns for this resource\n"
         << "  const Node* R = v.nodes + h.root;\n"
         << "  const uint32_t ei = NONE, et = T_UNK, ea = 0u, erow = NONE;\n";
@@ -1510,10 +1511,11 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "  const uint32_t lane = threadIdx.x, r = (w0 + blockIdx.x) * 64u + lane;\n"
              "  const bool gated = r < v.nres && ((v.gate[(size_t)v.hdr[r].kclass * v.gate_words + " << k / 32 << "u] >> "
           << k % 32 << "u) & 1u);\n"
+             "  if (r < v.nres) KYV_ACCT_ADD(0, 4);  // header: kind class\n"
              "  if (!__ballot(gated)) return;\n"
              "  uint8_t st = kyv::ST_NONE;\n"
              "  if (gated) st = kyv::jr" << k << "(v, r, jl + lane);\n"
-             "  if (gated && st != kyv::ST_NONE) o.status[(size_t)" << k << "u * v.nres + r] = st;\n"
+             "  if (gated && st != kyv::ST_NONE) { o.status[(size_t)" << k << "u * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }\n"
              "}\n";
     for (uint32_t k : crules) if (jit_cond) (*jit_cond)[k] = 1;
   }
@@ -1528,7 +1530,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
   return src.str();
 }
 
-std::vector<char> jit_compile_uncached(const std::string& src, double* seconds);
+std::vector<char> jit_compile_uncached(const std::string& src, double* seconds, bool acct);
 
 namespace {
 uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
@@ -1548,7 +1550,7 @@ std::string read_file(const std::string& path) {
 // On-disk code-object cache: a ruleset's walk kernel is compiled once per (generated source, device headers,
 // compile options) and reused by every later process (first evaluation seconds instead of a ~20 s hipRTC compile).
 // KYV_JIT_CACHE overrides the directory (default <library dir>/jitcache); "0" disables it.
-std::string cache_path(const std::string& src) {
+std::string cache_path(const std::string& src, bool acct) {
   const char* env = getenv("KYV_JIT_CACHE");
   if (env && std::string(env) == "0") return "";
   std::string dir = env ? std::string(env) : self_dir() + "/jitcache";
@@ -1559,28 +1561,30 @@ std::string cache_path(const std::string& src) {
   uint64_t h = fnv1a("");
   for (const char* hdr : {"kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_wave.h", "kyv_walk.h", "kyv_jcond.h"})
     h = fnv1a(read_file(csrc + "/" + hdr), h);
-  h = fnv1a(std::string("gfx950|O3|c++17|wpe=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4") + "|" +
+  h = fnv1a(std::string(acct ? "acct|" : "") + "gfx950|O3|c++17|wpe=" + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4") + "|" +
                 (getenv("KYV_JIT_DEFS") ? getenv("KYV_JIT_DEFS") : "-DKYV_JIT_NOEXTRA"), h);
   int maj = 0, min = 0;
   hiprtcVersion(&maj, &min);
   h = fnv1a(std::to_string(maj) + "." + std::to_string(min), h);
   char name[80];
-  snprintf(name, sizeof name, "/walk-%08llx-%016llx.co", (unsigned long long)(h >> 32), (unsigned long long)fnv1a(src));
+  snprintf(name, sizeof name, "/%s-%08llx-%016llx.co", acct ? "acct" : "walk", (unsigned long long)(h >> 32),
+           (unsigned long long)fnv1a(src));
   return dir + name;
 }
 }  // namespace
 
-// hipRTC compile of the generated source for gfx950 -> code object
-std::vector<char> jit_compile(const std::string& src, double* seconds) {
+// hipRTC compile of the generated source for gfx950 -> code object (acct: the byte-accounting build, -DKYV_ACCT)
+std::vector<char> jit_compile(const std::string& src, double* seconds, bool acct) {
   // process-wide cache: identical rulesets (same generated source) compile once
   static std::mutex mu;
   static std::unordered_map<std::string, std::vector<char>> cache;
+  const std::string ckey = (acct ? "A" : "P") + src;
   {
     std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find(src);
+    auto it = cache.find(ckey);
     if (it != cache.end()) { if (seconds) *seconds = 0; return it->second; }
   }
-  const std::string path = cache_path(src);
+  const std::string path = cache_path(src, acct);
   std::vector<char> code;
   if (!path.empty()) {
     std::string blob = read_file(path);
@@ -1591,7 +1595,7 @@ std::vector<char> jit_compile(const std::string& src, double* seconds) {
     }
   }
   if (code.empty()) {
-    code = jit_compile_uncached(src, seconds);
+    code = jit_compile_uncached(src, seconds, acct);
     if (!path.empty()) {  // best effort: a read-only tree just recompiles next time
       std::string dir = path.substr(0, path.rfind('/'));
       mkdir(dir.c_str(), 0755);
@@ -1604,11 +1608,11 @@ std::vector<char> jit_compile(const std::string& src, double* seconds) {
     }
   }
   std::lock_guard<std::mutex> lk(mu);
-  cache.emplace(src, code);
+  cache.emplace(ckey, code);
   return code;
 }
 
-std::vector<char> jit_compile_uncached(const std::string& src, double* seconds) {
+std::vector<char> jit_compile_uncached(const std::string& src, double* seconds, bool acct) {
   auto t0 = std::chrono::steady_clock::now();
   std::string dir = self_dir();
   const char* env = getenv("KYV_CSRC");
@@ -1616,11 +1620,12 @@ std::vector<char> jit_compile_uncached(const std::string& src, double* seconds) 
   std::string inc2 = "-I" + dir + "/../include";
   std::string wpe = std::string("-DKYV_JIT_WPE=") + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4");
   std::string extra = getenv("KYV_JIT_DEFS") ? getenv("KYV_JIT_DEFS") : "-DKYV_JIT_NOEXTRA";  // experiments only
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str(), wpe.c_str(), extra.c_str()};
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", inc.c_str(), inc2.c_str(), wpe.c_str(), extra.c_str(),
+                        "-DKYV_ACCT=1"};
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "kyv_jit_walk.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     throw std::runtime_error("hiprtcCreateProgram failed");
-  hiprtcResult r = hiprtcCompileProgram(prog, 7, opts);
+  hiprtcResult r = hiprtcCompileProgram(prog, acct ? 8 : 7, opts);
   if (r != HIPRTC_SUCCESS) {
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);

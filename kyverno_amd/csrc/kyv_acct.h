@@ -1,0 +1,18 @@
+// Launchers of the byte-accounting build of the evaluation kernels (kyv_acct.hip: kyv_kernels.h compiled with
+// KYV_ACCT in a renamed namespace). Plain types only: the argument structs are the product's (kyv::View, DevOut,
+// WorkLists, ChunkMap), passed by address and copied into their layout-identical accounting twins.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace kyvacct {
+void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+           const uint32_t* mrules, uint32_t nm);
+void match_walk(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+                const uint32_t* mrules, uint32_t nm);
+void pss(bool exact, int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0);
+void walk(unsigned grid, size_t lds, hipStream_t s, const void* view, const void* devout, const void* wl, const void* cm,
+          int depth);
+// device address of this build's counters: unsigned long long[3][KYV_ACCT_SLOTS] (reads, writes, staged records)
+unsigned long long* counters();
+}  // namespace kyvacct

@@ -1,0 +1,64 @@
+// Byte-accounting build of the evaluation kernels (SURVEY §8(d) algorithmic bytes, bench.py `roofline`): the same
+// kernel source as the product (kyv_kernels.h) compiled with KYV_ACCT, so every per-resource load and result store
+// adds its bytes to device counters (kyv_eval.h KYV_ACCT_ADD). The namespace is renamed so both builds link into one
+// library without sharing a symbol; kyv_engine.hip runs these only in an explicit accounting evaluation.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#define KYV_ACCT 1
+#define kyv kyv_acct
+#include "kyv_kernels.h"
+#undef kyv
+#include "kyv_acct.h"
+
+namespace kyvacct {
+namespace {
+template <class T>
+T as(const void* p) {
+  T x;
+  memcpy(&x, p, sizeof x);
+  return x;
+}
+void check(hipError_t e) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error (accounting kernels): ") + hipGetErrorString(e));
+}
+}  // namespace
+
+void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+           const uint32_t* mrules, uint32_t nm) {
+  using namespace kyv_acct;
+  auto kf = kj ? match_kernel<true> : match_kernel<false>;
+  hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl), mrules, nm);
+  check(hipGetLastError());
+}
+void match_walk(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+                const uint32_t* mrules, uint32_t nm) {
+  using namespace kyv_acct;
+  auto kf = wpe == 8 ? match_walk_kernel<8> : wpe == 6 ? match_walk_kernel<6> : match_walk_kernel<4>;
+  hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl), mrules, nm);
+  check(hipGetLastError());
+}
+void pss(bool exact, int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0) {
+  using namespace kyv_acct;
+  auto kf = exact ? (wpe == 4 ? pss_kernel<true, 4> : wpe == 6 ? pss_kernel<true, 6> : pss_kernel<true, 8>)
+                  : (wpe == 4 ? pss_kernel<false, 4> : wpe == 6 ? pss_kernel<false, 6> : pss_kernel<false, 8>);
+  hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), k, w0);
+  check(hipGetLastError());
+}
+void walk(unsigned grid, size_t lds, hipStream_t s, const void* view, const void* devout, const void* wl, const void* cm,
+          int depth) {
+  using namespace kyv_acct;
+  hipLaunchKernelGGL(walk_kernel, dim3(grid), dim3(BLOCK), lds, s, (const View*)view, as<DevOut>(devout),
+                     as<WorkLists>(wl), as<ChunkMap>(cm), depth);
+  check(hipGetLastError());
+}
+unsigned long long* counters() {
+  void* p = nullptr;
+  check(hipGetSymbolAddress(&p, HIP_SYMBOL(kyv_acct::kyv_acct_bytes)));
+  return (unsigned long long*)p;
+}
+}  // namespace kyvacct

@@ -115,6 +115,7 @@ KYV_HD bool cv_operand(const View& v, NodeTab R, const CondOperand& o, CV* out, 
   Node nil{N_NULL, 0, 0, 0};
   if (o.kind != OK_PATH) { *out = cv_node(nil, false); return true; }
   if (o.list && row != NONE && v.colv) {
+    KYV_ACCT_ADD(0, 8);
     const uint32_t e = (uint32_t)v.colv[(size_t)v.col_off[o.list - 1] + row];
     if (e != NONE) {
       const uint32_t x = e & COL_INDEX_MASK;

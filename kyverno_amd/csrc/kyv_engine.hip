@@ -24,9 +24,9 @@
 #include <thread>
 #include <vector>
 
+#include "kyv_acct.h"
 #include "kyv_host.h"
-#include "kyv_pss.h"
-#include "kyv_wave.h"
+#include "kyv_kernels.h"
 
 namespace kyv {
 
@@ -70,6 +70,11 @@ struct DevRuleset {
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
   std::vector<hipFunction_t> jconds;  // [rule] kyv_jit_cond_<k> (compiled deny / foreach rule k) or null
   bool jloaded = false;
+  // the byte-accounting build of the same kernels (KYV_ACCT), loaded only by an accounting evaluation
+  hipModule_t amod = nullptr;
+  std::vector<hipFunction_t> afns, aconds;
+  unsigned long long* acnt = nullptr;  // its counters (kyv_acct_bytes)
+  bool aloaded = false;
 };
 
 // ---------------------------------------------------------------- per-batch device memory
@@ -199,6 +204,7 @@ struct SliceSched {
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint32_t> grid;
+  hipEvent_t evs = nullptr;      // slice start (before its resets): phase 0 of every slice, not only the first
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // after match, condition, walk, compaction (phase timing)
   hipEvent_t cev[2] = {nullptr, nullptr};  // the slice's condition kernels on the condition stream (start, end)
   int jit_state = -1;            // what the schedules were laid out for (0 interpreter only, 1 with the jit kernel)
@@ -240,6 +246,7 @@ static void free_dev_results(DeviceResults& d, int dev) {
   dfree(d.wl.items); dfree(d.wl.cnt);
   for (auto& sl : d.slices) {
     dfree(sl.rbase); dfree(sl.mrules); dfree(sl.sched);
+    if (sl.evs) hipEventDestroy(sl.evs);
     for (auto e : sl.ev) if (e) hipEventDestroy(e);
     for (auto e : sl.cev) if (e) hipEventDestroy(e);
   }
@@ -390,138 +397,7 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
 }
 
 // ---------------------------------------------------------------- kernels
-constexpr int BLOCK = 64;        // one wave per workgroup; LDS = depth * 64 * 16 B
-constexpr int RECS_PER_PAIR = MAX_ALTS;
-
-#ifndef KYV_WPE
-#define KYV_WPE 4
-#endif
-
-// Phase 1 (match_eval): one lane per resource, the rule loop uniform across the wave. Kind gate, match /
-// exclude program, dispatch; verdicts that need no pattern walk are final here (incl. PodSecurity). Pairs
-// that need the walk are appended to the rule's work list (wave ballot + one atomic per wave and rule).
-// Two instantiations: kJ = false for rules without JMESPath operands or foreach (the register budget of the
-// plain match / condition / PodSecurity code), kJ = true for the rest (projection lists live in scratch)
-#ifndef KYV_MATCH_WPE
-#define KYV_MATCH_WPE 4  // C2 A/B: 1.50 ms unbounded (3 waves), 1.40 at 4, 1.47 at 5, 1.53 at 6
-#endif
-template <bool kJ>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_MATCH_WPE))) match_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl,
-                                                      const uint32_t* __restrict__ mrules, uint32_t nm) {
-  const View& v = *vp;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t r = blockIdx.x * BLOCK + lane;
-  const bool active = r < v.nres;
-  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
-  for (uint32_t mi = 0; mi < nm; mi++) {  // rules that need this phase (direct-walk rules are decided in the walk)
-    const uint32_t k = mrules[mi];
-    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
-    if (!__ballot(gated)) continue;  // status bytes are pre-set to ST_NONE, PSS masks to 0
-    uint32_t pf = 0;
-    bool walk = false;
-    const uint8_t st = pair_dispatch<kJ>(v, gated, r, k, &pf, &walk);
-    const unsigned long long wm = __ballot(walk);
-    const RuleDesc& rdk = v.rules[k];
-    if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {  // this wave's work list for rule k
-      const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + blockIdx.x;
-      if (walk) {
-        const ResHeader& h = v.hdr[r];
-        wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
-            make_uint2(r | ((h.flags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), h.root);
-      }
-      if (lane == 0) wl.cnt[list] = (uint8_t)__popcll(wm);
-    }
-    if (gated && !walk && st != ST_NONE) {
-      o.status[(size_t)k * v.nres + r] = st;
-      const uint32_t ps = o.pss_slot[k];
-      if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
-    }
-  }
-}
-
-// Pattern / anyPattern rules without preconditions (and compile-time fallback rules): the match phase is only
-// pair_match (kind gate, match / exclude program, PolicyException candidates) and the work-list append, so this
-// kernel carries none of the dispatch code (conditions, PodSecurity calls) whose register need made the rule loop
-// of match_kernel spill every iteration (C4: 10,440 rules per wave, 252 GB of scratch writes per evaluation)
-// kWpe: occupancy target (KYV_MATCHW_WPE = 4 / 6 / 8 at run time; 4 by default: 97 VGPRs, none spilled; 8 spills 253)
-template <int kWpe>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
-match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint32_t* __restrict__ mrules, uint32_t nm) {
-  const View& v = *vp;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t r = blockIdx.x * BLOCK + lane;
-  const bool active = r < v.nres;
-  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
-  const uint32_t hflags = active ? v.hdr[r].flags : 0u;
-  const uint32_t hroot = active ? v.hdr[r].root : 0u;
-  for (uint32_t mi = 0; mi < nm; mi++) {
-    const uint32_t k = mrules[mi];
-    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
-    if (!__ballot(gated)) continue;
-    const RuleDesc& rdk = v.rules[k];
-    uint8_t st = ST_NONE;
-    bool walk = false;
-    if (gated && pair_match(v, r, rdk, &st)) {  // a matched pattern pair: walk it (RF_MAGIC: the CPU engine)
-      if (hflags & RF_MAGIC) st = ST_FALLBACK;
-      else walk = true;
-    }
-    const unsigned long long wm = __ballot(walk);
-    if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {
-      const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + blockIdx.x;
-      if (walk)
-        wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
-            make_uint2(r | ((hflags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), hroot);
-      if (lane == 0) wl.cnt[list] = (uint8_t)__popcll(wm);
-    }
-    if (gated && !walk && st != ST_NONE) o.status[(size_t)k * v.nres + r] = st;
-  }
-}
-
-// PodSecurity rules (without preconditions): one lane per resource over the match waves [w0, w0 + grid) of the rule's
-// kind gate, the match and the path-column checks inlined (eval_pss_cols); in the match kernel the checks are an
-// out-of-line call whose callee-saved registers go through scratch memory. Pairs the column form does not cover
-// (exclusion sub-pods, resources without path columns) take the out-of-line map walk (eval_pss).
-// kExact: the rule's match block is its kind gate (RD_GATE_EXACT), no match program compiled in; kWpe: occupancy
-// target (KYV_PSS_WPE = 4 / 6 / 8 at run time; 8 by default)
-template <bool kExact, int kWpe>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
-pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
-  const View& v = *vp;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t r = (w0 + blockIdx.x) * BLOCK + lane;
-  const bool gated = r < v.nres && ((v.gate[(size_t)v.hdr[r].kclass * v.gate_words + (k >> 5)] >> (k & 31)) & 1u);
-  if (!__ballot(gated)) return;
-  const RuleDesc& rd = v.rules[k];
-  uint8_t st = ST_NONE;
-  uint32_t pf = 0;
-  bool m;
-  if constexpr (kExact) {
-    m = rd.kind == RK_PSS;  // pair_match of a kind-gate rule: matched (a fallback rule never gets here)
-  } else {
-    m = gated && pair_match(v, r, rd, &st);
-  }
-  if (gated && m) {
-    const ResHeader& h = v.hdr[r];
-    const NodeTab R{v.nodes + h.root};
-    st = eval_pss_cols(v, v.pss[rd.root], h, R, &pf, r);
-    if (st == ST_NONE) st = eval_pss(v, v.pss[rd.root], R, h, &pf, r);
-  }
-  if (gated && st != ST_NONE) {
-    o.status[(size_t)k * v.nres + r] = st;
-    const uint32_t ps = o.pss_slot[k];
-    if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
-  }
-}
-
-// Phase 2 (pattern_eval): each wave takes chunks of 64 work items of ONE rule (grid-stride over all rules'
-// chunks), so every lane walks the same compiled pattern over a different resource with the wave-uniform
-// walker; verdict bytes as in phase 1, failing-path records staged in the chunk's own slots.
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_WPE)))
-walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, ChunkMap cm, int depth) {
-  extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
-  WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth, false};
-  walk_chunks(*vp, o, wl, cm, wk);
-}
+// match_kernel, match_walk_kernel, pss_kernel, walk_kernel: kyv_kernels.h
 
 // Gather the staged failing-path records of every walk chunk into one dense list, without atomics:
 //   compact_sum_kernel   one wave per 64 consecutive chunks: the tile's record total;
@@ -800,6 +676,31 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   return true;
 }
 
+// The accounting build of the loaded kernels (same generated source, -DKYV_ACCT): compiled (or taken from the code-object
+// cache) and loaded on first use; false when the product kernels are not the compiled ones
+static bool ensure_jit_acct(Ruleset& rs, DevRuleset* dr) {
+  if (dr->aloaded) return true;
+  if (!ensure_jit(rs, dr)) return false;
+  std::lock_guard<std::mutex> lk(g_jit_mu);
+  if (rs.jit_code_acct.empty()) {
+    std::vector<uint8_t> jr, jc;
+    rs.jit_code_acct = jit_compile(jit_source(rs, &jr, &jc), nullptr, true);
+  }
+  HIP_OK(hipModuleLoadData(&dr->amod, rs.jit_code_acct.data()));
+  dr->afns.resize(dr->jfns.size());
+  for (size_t g = 0; g < dr->jfns.size(); g++)
+    HIP_OK(hipModuleGetFunction(&dr->afns[g], dr->amod, ("kyv_jit_walk_" + std::to_string(g)).c_str()));
+  dr->aconds.assign(dr->jconds.size(), nullptr);
+  for (size_t k = 0; k < dr->jconds.size(); k++)
+    if (dr->jconds[k]) HIP_OK(hipModuleGetFunction(&dr->aconds[k], dr->amod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
+  hipDeviceptr_t p = nullptr;
+  size_t bytes = 0;
+  HIP_OK(hipModuleGetGlobal(&p, &bytes, dr->amod, "kyv_acct_bytes"));
+  dr->acnt = (unsigned long long*)p;
+  dr->aloaded = true;
+  return true;
+}
+
 // Walk-buffer bytes one rule costs per resource: its work-list slot (8 B), failing-path staging and compacted
 // records (32 B each per anyPattern alternative), plus per-chunk counters.
 static size_t rule_slice_bytes(const RuleDesc& rd) {
@@ -970,8 +871,8 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
   sl.jit_state = (int)jit;
 }
 
-// accumulate one slice's phase times (ms) from its events; `start`: the evaluation's start event (first slice), else
-// the phase-0 time of later slices is not separable from the previous slice's end and counts from its own ev[0]
+// accumulate one slice's phase times (ms) from its events; `start`: the evaluation's start event for the first slice
+// (the verdict resets count to the match phase), the slice's own start event for the others
 static void slice_phases(const SliceSched& sl, hipEvent_t start, double* phase) {
   float t = 0;
   if (start && hipEventElapsedTime(&t, start, sl.ev[0]) == hipSuccess) phase[0] += t;
@@ -980,7 +881,7 @@ static void slice_phases(const SliceSched& sl, hipEvent_t start, double* phase) 
 }
 
 void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back,
-              int jit_mode) {
+              int jit_mode, bool account) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw std::runtime_error("no HIP device available (GPU backend requested)");
   if (device < 0 || device >= ndev) throw std::runtime_error("device index out of range");
@@ -1109,22 +1010,53 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   double total_ms = 0;
   double phase[5] = {0, 0, 0, 0, 0};
   for (auto& sl : d.slices) {
+    if (!sl.evs) HIP_OK(hipEventCreate(&sl.evs));
     for (auto& e : sl.ev) if (!e) HIP_OK(hipEventCreate(&e));
     for (auto& e : sl.cev) if (!e) HIP_OK(hipEventCreate(&e));
   }
   int n = std::max(1, iters);
   std::vector<FailRec> host_recs;
+  // Byte accounting (KYV_EVAL_ACCOUNT_BYTES on the GPU backend): one evaluation with the KYV_ACCT build of every
+  // kernel (kyv_acct.hip; the runtime-compiled kernels with -DKYV_ACCT), phases serialised on the evaluation stream and
+  // the device counters read after each phase, so each phase's algorithmic bytes are what its kernels
+  // loaded and stored. Verdicts are those of the product kernels (same source).
+  const bool acct = account;
+  uint64_t aphase[5] = {0, 0, 0, 0, 0};
+  uint64_t aclass[3] = {0, 0, 0};
+  unsigned long long* acnt_lib = nullptr;
+  bool ajit = false;
+  std::vector<unsigned long long> ahost(3 * KYV_ACCT_SLOTS);
+  auto acct_take = [&]() -> std::array<uint64_t, 3> {  // counters since the last call, by class; then zeroed
+    std::array<uint64_t, 3> c{0, 0, 0};
+    HIP_OK(hipStreamSynchronize(stream));
+    for (unsigned long long* dc : {acnt_lib, ajit ? dr->acnt : nullptr}) {
+      if (!dc) continue;
+      HIP_OK(hipMemcpy(ahost.data(), dc, ahost.size() * 8, hipMemcpyDeviceToHost));
+      for (int q = 0; q < 3; q++)
+        for (uint32_t i = 0; i < KYV_ACCT_SLOTS; i++) c[q] += ahost[q * KYV_ACCT_SLOTS + i];
+      HIP_OK(hipMemset(dc, 0, ahost.size() * 8));
+    }
+    for (int q = 0; q < 3; q++) aclass[q] += c[q];
+    return c;
+  };
+  if (acct) {
+    n = 1;
+    acnt_lib = kyvacct::counters();
+    ajit = jit && ensure_jit_acct(mrs, dr);
+    if (jit && !ajit) throw std::runtime_error("accounting build of the runtime-compiled kernels unavailable");
+    acct_take();
+  }
   // concurrent condition stream (KYV_COND_STREAM=0: the evaluation stream)
   static const bool cond_conc = !getenv("KYV_COND_STREAM") || atoi(getenv("KYV_COND_STREAM")) != 0;
   bool conc = false;
   for (auto& sl : d.slices) conc = conc || !sl.cw.empty();
-  conc = conc && cond_conc;
+  conc = conc && cond_conc && !acct;
   if (conc && !d.cstream) stream_get(&d.cstream, &d.cfork, &d.cjoin);
   // off by default: measured 13.43 (one stream) vs 13.53 ms (groups overlapped) on C3 10M
   static const bool walk_conc = getenv("KYV_WALK_STREAM") && atoi(getenv("KYV_WALK_STREAM")) != 0;
   bool wconc = false;
   for (auto& sl : d.slices) wconc = wconc || sl.cm.size() > 2;
-  wconc = wconc && walk_conc;
+  wconc = wconc && walk_conc && !acct;
   if (wconc && !d.wstream) stream_get(&d.wstream, &d.wfork, &d.wjoin);
   for (int it = 0; it < n; it++) {
     const bool collect = copy_back && out && it == n - 1;
@@ -1136,35 +1068,44 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));  // also when no slice runs (no rules / no resources)
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
+    if (acct) aphase[0] += (uint64_t)nres * nrules + (uint64_t)d.npss * nres * 4;  // verdict / PSS-mask resets
     for (auto& sl : d.slices) {
       if (!nres || sl.k1 == sl.k0) continue;
       const size_t nsr = sl.k1 - sl.k0;
       DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, sl.rbase, d.rcnt, sl.k0, sl.k1};
+      HIP_OK(hipEventRecord(sl.evs, stream));
       HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
       HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
       if (sl.nmw) {
         static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
         auto kf = mwpe == 8 ? match_walk_kernel<8> : mwpe == 6 ? match_walk_kernel<6> : match_walk_kernel<4>;
-        hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const uint32_t*)sl.mrules,
-                           sl.nmw);
+        if (acct) kyvacct::match_walk(mwpe, grid.x, stream, d.view, &o, &d.wl, sl.mrules, sl.nmw);
+        else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const uint32_t*)sl.mrules,
+                                sl.nmw);
       }
-      if (sl.nm)
-        hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
-                           (const uint32_t*)sl.mrules + sl.nmw, sl.nm);
-      if (sl.nmj)
-        hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
-                           (const uint32_t*)sl.mrules + sl.nmw + sl.nm, sl.nmj);
+      if (sl.nm) {
+        if (acct) kyvacct::match(false, grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw, sl.nm);
+        else hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
+                                (const uint32_t*)sl.mrules + sl.nmw, sl.nm);
+      }
+      if (sl.nmj) {
+        if (acct) kyvacct::match(true, grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw + sl.nm, sl.nmj);
+        else hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
+                                (const uint32_t*)sl.mrules + sl.nmw + sl.nm, sl.nmj);
+      }
       {
         static const int pwpe = getenv("KYV_PSS_WPE") ? atoi(getenv("KYV_PSS_WPE")) : 8;  // C2: 4 0.586, 6 0.587, 8 0.514 ms
         for (const uint3& c : sl.pw) {
           const bool ex = (rs.rules[c.x].flags & RD_GATE_EXACT) && rs.rules[c.x].match.mode != MM_NONE;
           auto kf = ex ? (pwpe == 4 ? pss_kernel<true, 4> : pwpe == 6 ? pss_kernel<true, 6> : pss_kernel<true, 8>)
                        : (pwpe == 4 ? pss_kernel<false, 4> : pwpe == 6 ? pss_kernel<false, 6> : pss_kernel<false, 8>);
-          hipLaunchKernelGGL(kf, dim3(c.z), dim3(BLOCK), 0, stream, (const View*)d.view, o, c.x, c.y);
+          if (acct) kyvacct::pss(ex, pwpe, c.z, stream, d.view, &o, c.x, c.y);
+          else hipLaunchKernelGGL(kf, dim3(c.z), dim3(BLOCK), 0, stream, (const View*)d.view, o, c.x, c.y);
         }
       }
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(sl.ev[0], stream));
+      if (acct) { const auto c = acct_take(); aphase[0] += c[0] + c[1]; }
       // compiled condition rules: one kernel each over the waves of its kind gate
       // (the View goes by pointer: a by-value View would be copied to scratch memory, since the kernels take its
       // address for out-of-line helpers; measured 40 % slower)
@@ -1179,8 +1120,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         const View* vp = d.view;
         uint32_t w0 = c.y;
         void* args[] = {(void*)&vp, (void*)&o, (void*)&w0};
-        HIP_OK(hipModuleLaunchKernel(dr->jconds[c.x], c.z, 1, 1, BLOCK, 1, 1, 0, cs, args, nullptr));
+        HIP_OK(hipModuleLaunchKernel(acct ? dr->aconds[c.x] : dr->jconds[c.x], c.z, 1, 1, BLOCK, 1, 1, 0, cs, args, nullptr));
       }
+      if (acct) { const auto c = acct_take(); aphase[1] += c[0] + c[1]; }
       if (cs != stream) {
         HIP_OK(hipEventRecord(sl.cev[1], d.cstream));
         HIP_OK(hipEventRecord(d.cjoin, d.cstream));
@@ -1188,8 +1130,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       }
       HIP_OK(hipEventRecord(sl.ev[1], stream));
       if (sl.grid[0]) {
-        hipLaunchKernelGGL(walk_kernel, dim3(sl.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl, sl.cm[0],
-                           depth);
+        if (acct) kyvacct::walk(sl.grid[0], lds, stream, d.view, &o, &d.wl, &sl.cm[0], depth);
+        else hipLaunchKernelGGL(walk_kernel, dim3(sl.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl,
+                                sl.cm[0], depth);
         HIP_OK(hipGetLastError());
       }
       bool wforked = false;
@@ -1207,8 +1150,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         ChunkMap cmj = sl.cm[cls];
         void* args[] = {(void*)&vp, (void*)&o, (void*)&wl, (void*)&cmj};
         const hipStream_t ws = (wforked && cls >= 2) ? d.wstream : stream;
-        HIP_OK(hipModuleLaunchKernel(dr->jfns[cls - 1], sl.grid[cls], 1, 1, BLOCK, 1, 1, 0, ws, args, nullptr));
+        HIP_OK(hipModuleLaunchKernel(acct ? dr->afns[cls - 1] : dr->jfns[cls - 1], sl.grid[cls], 1, 1, BLOCK, 1, 1, 0, ws,
+                                     args, nullptr));
       }
+      uint64_t staged = 0;
+      if (acct) { const auto c = acct_take(); aphase[2] += c[0] + c[1] + c[2]; staged = c[2]; }
       if (wforked) {  // the compaction reads every walk group's staged records
         HIP_OK(hipEventRecord(d.wjoin, d.wstream));
         HIP_OK(hipStreamWaitEvent(stream, d.wjoin, 0));
@@ -1223,10 +1169,13 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
                          d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs, sl.k0);
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(sl.ev[3], stream));
-      if (multi) {  // phase times of this slice before its events are recorded again
-        HIP_OK(hipEventSynchronize(sl.ev[3]));
-        slice_phases(sl, &sl == &d.slices.front() ? d.e0 : nullptr, phase);
+      if (acct) {  // compaction: chunk counts (read twice), tile sums, the staged records read, the dense records written
+        uint32_t nr = 0;
+        HIP_OK(hipMemcpyAsync(&nr, d.nrecs, 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        aphase[3] += 4ull * nchunks + 12ull * ntiles + staged + (uint64_t)nr * sizeof(FailRec);
       }
+      // (no host synchronisation between slices: every slice has its own events, read after the evaluation)
       if (collect && multi) {  // gather this slice's records before the next slice reuses the buffers
         uint32_t nr = 0;
         HIP_OK(hipMemcpyAsync(&nr, d.nrecs, 4, hipMemcpyDeviceToHost, stream));
@@ -1244,14 +1193,17 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     if (joined) HIP_OK(hipStreamWaitEvent(stream, d.cjoin, 0));  // the histogram reads every verdict row
     if (nrules && nres) hipLaunchKernelGGL(status_hist_kernel, dim3(hgrid, (uint32_t)nrules), dim3(HIST_BLOCK), 0, stream, d.status, nres, d.counts);
     HIP_OK(hipGetLastError());
+    if (acct) aphase[4] += (uint64_t)nres * nrules;  // the histogram reads every verdict byte
     HIP_OK(hipEventRecord(d.e1, stream));
     HIP_OK(hipEventSynchronize(d.e1));
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, d.e0, d.e1));
     total_ms += ms;
-    if (!multi && !d.slices.empty() && nres && d.slices[0].k1 > d.slices[0].k0) slice_phases(d.slices[0], d.e0, phase);
+    if (nres)
+      for (auto& sl : d.slices)
+        if (sl.k1 > sl.k0) slice_phases(sl, &sl == &d.slices.front() ? d.e0 : sl.evs, phase);
     const double sum_after = phase[0] + phase[1] + phase[2] + phase[3];
-    phase[4] += std::max(0.0, ms - (sum_after - sum_before));  // the rest: verdict histogram (+ slice gaps)
+    phase[4] += std::max(0.0, ms - (sum_after - sum_before));  // the rest: verdict histogram
     if (joined)  // the condition kernels' own span on their stream (overlapping the walk), per slice
       for (auto& sl : d.slices) {
         float cms = 0;
@@ -1275,6 +1227,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     for (auto& sl : d.slices) cond |= sl.nmc != 0;
     out->jit_used = (jit ? 1 : 0) | (jit && cond ? 2 : 0);
     out->h2d_ms = db->upload_ms;
+    if (acct) {
+      out->alg_bytes = 0;
+      for (int q = 0; q < 5; q++) { out->alg_bytes_phase[q] = aphase[q]; out->alg_bytes += aphase[q]; }
+      for (int q = 0; q < 3; q++) out->alg_bytes_class[q] = aclass[q];
+    }
     std::vector<unsigned long long> rc(nrules * NSTATUS);
     if (nrules) HIP_OK(hipMemcpy(rc.data(), d.counts, rc.size() * 8, hipMemcpyDeviceToHost));
     // ST_NONE pairs are not tallied on the device

@@ -40,8 +40,29 @@ struct TouchAcct {
   uint64_t rows;   // distinct rows touched by the current pair
 };
 inline thread_local TouchAcct* g_touch = nullptr;
+
+// Device byte accounting (bench roofline), compiled in only with KYV_ACCT: the accounting build of the
+// kernels (kyv_acct.hip; the runtime-compiled kernels with -DKYV_ACCT) adds the bytes of every per-resource load and
+// result store to spread 64-bit counters, class 0 = reads of resource data (node rows, path-column entries, header
+// fields, walk work lists), class 1 = writes (verdict bytes, PSS masks, work lists), class 2 = staged failing-path
+// records (written by the walk, read back by the compaction). Dictionary columns and rule programs are amortised and
+// not counted. The product build compiles every KYV_ACCT_ADD away.
+#define KYV_ACCT_SLOTS 4096u
+#if defined(KYV_ACCT)
+extern "C" {
+__device__ unsigned long long kyv_acct_bytes[3 * KYV_ACCT_SLOTS];
+}
+#endif
+#if defined(KYV_ACCT) && defined(__HIP_DEVICE_COMPILE__)
+#define KYV_ACCT_ADD(cls, b)                                                                                      \
+  atomicAdd(&::kyv::kyv_acct_bytes[(cls) * KYV_ACCT_SLOTS + ((blockIdx.x * blockDim.x + threadIdx.x) & (KYV_ACCT_SLOTS - 1))], \
+            (unsigned long long)(b))
+#else
+#define KYV_ACCT_ADD(cls, b) ((void)0)
+#endif
+
 #if defined(__HIP_DEVICE_COMPILE__)
-KYV_HD void touch_row(uint32_t) {}
+KYV_HD void touch_row(uint32_t) { KYV_ACCT_ADD(0, 16); }
 #else
 KYV_HD void touch_row(uint32_t i) {
   TouchAcct* t = g_touch;
@@ -634,6 +655,7 @@ KYV_BIG uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32
 KYV_HD uint8_t expand_meta_root(const View& v, const MetaSite& ms, NodeTab R, const ResHeader& h, Keys& keys) {
   for (uint32_t i = 0; i < ms.nwild_l; i++) keys.set(ms.slot_l + i, v.pool[ms.wild_l + 2 * i + 1]);
   for (uint32_t i = 0; i < ms.nwild_a; i++) keys.set(ms.slot_a + i, v.pool[ms.wild_a + 2 * i + 1]);
+  KYV_ACCT_ADD(0, 8);  // header: flags, labels / annotations node
   if (h.flags & RF_META_NONE) return ST_NONE;
   if (h.flags & RF_META_NOTMAP) return ST_PANIC;
   if (h.flags & RF_ANCHORISH) return ST_FALLBACK;

@@ -128,6 +128,7 @@ struct Ruleset {
   std::vector<uint8_t> jit_rules;   // rule k is walked by the compiled kernel
   std::vector<uint8_t> jit_cond;    // rule k (deny / foreach with JMESPath operands) runs in the compiled kyv_jit_cond
   std::vector<char> jit_code;       // gfx950 code object
+  std::vector<char> jit_code_acct;  // the same source compiled with -DKYV_ACCT (byte-accounting evaluation only)
   std::string jit_error;
   double jit_compile_s = 0;
   // device copies (one per device, lazily uploaded)
@@ -182,6 +183,7 @@ struct Results {
   double phase_ms[5] = {0, 0, 0, 0, 0};
   uint64_t alg_bytes = 0;           // CPU backend with KYV_EVAL_ACCOUNT_BYTES
   uint64_t alg_bytes_phase[5] = {0, 0, 0, 0, 0};  // the same split by the device phase that moves them (phase_ms)
+  uint64_t alg_bytes_class[3] = {0, 0, 0};  // GPU accounting: counted reads, writes, staged records (kernel counters)
   int jit_used = 0;                 // bit 0: the runtime-compiled walk kernels ran; bit 1: the compiled condition kernel ran
 };
 
@@ -189,8 +191,9 @@ struct Results {
 // exceptions: PolicyException documents (kyverno.io/v2alpha1) or null; a rule named by an exception
 // (PolicyException.Contains, api/kyverno/v2alpha1/policy_exception_types.go:101) carries the exceptions' match
 // blocks as device match programs (RuleDesc.exc): a matched pair an exception applies to is a skip
+// background: the ruleset serves background scans only (empty AdmissionInfo, KYV_COMPILE_BACKGROUND)
 Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const char* exceptions = nullptr,
-                         size_t ex_len = 0);
+                         size_t ex_len = 0, bool background = false);
 Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* nsl_json, size_t nsl_len, int threads,
                    std::string* err);
 void derive_strings(Batch& b, size_t from, int threads);
@@ -198,7 +201,7 @@ void build_path_trie(Ruleset& rs);
 void assign_glob_masks(Ruleset& rs);
 void assign_cond_sets(Ruleset& rs);
 std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond = nullptr);
-std::vector<char> jit_compile(const std::string& src, double* seconds);
+std::vector<char> jit_compile(const std::string& src, double* seconds, bool acct = false);
 enum JitMode { JIT_AUTO = 0, JIT_OFF = 1, JIT_ON = 2 };
 constexpr size_t JIT_AUTO_MIN_RESOURCES = 65536;  // smaller batches are not worth a compile
 void resolve_path_columns(Batch& b, int threads);

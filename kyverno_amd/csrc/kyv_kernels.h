@@ -1,0 +1,155 @@
+// The evaluation kernels that read per-resource data (match phase, PodSecurity, interpreted walk), in a header so
+// that they are compiled twice: into the product library (kyv_engine.hip) and, with KYV_ACCT defined and the
+// namespace renamed, into the byte-accounting build (kyv_acct.hip) whose loads and stores count the algorithmic
+// bytes of SURVEY §8(d) (kyv_eval.h KYV_ACCT_ADD). Same source, so the accounting run executes exactly the
+// product's control flow.
+#pragma once
+#include "kyv_pss.h"
+#include "kyv_wave.h"
+
+namespace kyv {
+
+constexpr int BLOCK = 64;        // one wave per workgroup; LDS = depth * 64 * 16 B
+constexpr int RECS_PER_PAIR = MAX_ALTS;
+
+#ifndef KYV_WPE
+#define KYV_WPE 4
+#endif
+
+// Phase 1 (match_eval): one lane per resource, the rule loop uniform across the wave. Kind gate, match /
+// exclude program, dispatch; verdicts that need no pattern walk are final here (incl. PodSecurity). Pairs
+// that need the walk are appended to the rule's work list (wave ballot + one atomic per wave and rule).
+// Two instantiations: kJ = false for rules without JMESPath operands or foreach (the register budget of the
+// plain match / condition / PodSecurity code), kJ = true for the rest (projection lists live in scratch)
+#ifndef KYV_MATCH_WPE
+#define KYV_MATCH_WPE 4  // C2 A/B: 1.50 ms unbounded (3 waves), 1.40 at 4, 1.47 at 5, 1.53 at 6
+#endif
+template <bool kJ>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_MATCH_WPE))) match_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl,
+                                                      const uint32_t* __restrict__ mrules, uint32_t nm) {
+  const View& v = *vp;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t r = blockIdx.x * BLOCK + lane;
+  const bool active = r < v.nres;
+  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
+  if (active) KYV_ACCT_ADD(0, 4);  // header: kind class
+  for (uint32_t mi = 0; mi < nm; mi++) {  // rules that need this phase (direct-walk rules are decided in the walk)
+    const uint32_t k = mrules[mi];
+    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+    if (!__ballot(gated)) continue;  // status bytes are pre-set to ST_NONE, PSS masks to 0
+    uint32_t pf = 0;
+    bool walk = false;
+    const uint8_t st = pair_dispatch<kJ>(v, gated, r, k, &pf, &walk);
+    const unsigned long long wm = __ballot(walk);
+    const RuleDesc& rdk = v.rules[k];
+    if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {  // this wave's work list for rule k
+      const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + blockIdx.x;
+      if (walk) {
+        const ResHeader& h = v.hdr[r];
+        wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
+            make_uint2(r | ((h.flags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), h.root);
+        KYV_ACCT_ADD(0, 8);  // header: flags, root
+        KYV_ACCT_ADD(1, 8);  // work-list item
+      }
+      if (lane == 0) { wl.cnt[list] = (uint8_t)__popcll(wm); KYV_ACCT_ADD(1, 1); }
+    }
+    if (gated && !walk && st != ST_NONE) {
+      o.status[(size_t)k * v.nres + r] = st;
+      const uint32_t ps = o.pss_slot[k];
+      if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
+      KYV_ACCT_ADD(1, 1 + ((ps != NONE && pf) ? 4 : 0));
+    }
+  }
+}
+
+// Pattern / anyPattern rules without preconditions (and compile-time fallback rules): the match phase is only
+// pair_match (kind gate, match / exclude program, PolicyException candidates) and the work-list append, so this
+// kernel carries none of the dispatch code (conditions, PodSecurity calls) whose register need made the rule loop
+// of match_kernel spill every iteration (C4: 10,440 rules per wave, 252 GB of scratch writes per evaluation)
+// kWpe: occupancy target (KYV_MATCHW_WPE = 4 / 6 / 8 at run time; 4 by default: 97 VGPRs, none spilled; 8 spills 253)
+template <int kWpe>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
+match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint32_t* __restrict__ mrules, uint32_t nm) {
+  const View& v = *vp;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t r = blockIdx.x * BLOCK + lane;
+  const bool active = r < v.nres;
+  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
+  const uint32_t hflags = active ? v.hdr[r].flags : 0u;
+  const uint32_t hroot = active ? v.hdr[r].root : 0u;
+  if (active) KYV_ACCT_ADD(0, 12);  // header: kind class, flags, root
+  for (uint32_t mi = 0; mi < nm; mi++) {
+    const uint32_t k = mrules[mi];
+    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+    if (!__ballot(gated)) continue;
+    const RuleDesc& rdk = v.rules[k];
+    uint8_t st = ST_NONE;
+    bool walk = false;
+    if (gated && pair_match(v, r, rdk, &st)) {  // a matched pattern pair: walk it (RF_MAGIC: the CPU engine)
+      if (hflags & RF_MAGIC) st = ST_FALLBACK;
+      else walk = true;
+    }
+    const unsigned long long wm = __ballot(walk);
+    if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {
+      const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + blockIdx.x;
+      if (walk) {
+        wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
+            make_uint2(r | ((hflags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), hroot);
+        KYV_ACCT_ADD(1, 8);  // work-list item
+      }
+      if (lane == 0) { wl.cnt[list] = (uint8_t)__popcll(wm); KYV_ACCT_ADD(1, 1); }
+    }
+    if (gated && !walk && st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
+  }
+}
+
+// PodSecurity rules (without preconditions): one lane per resource over the match waves [w0, w0 + grid) of the rule's
+// kind gate, the match and the path-column checks inlined (eval_pss_cols); in the match kernel the checks are an
+// out-of-line call whose callee-saved registers go through scratch memory. Pairs the column form does not cover
+// (exclusion sub-pods, resources without path columns) take the out-of-line map walk (eval_pss).
+// kExact: the rule's match block is its kind gate (RD_GATE_EXACT), no match program compiled in; kWpe: occupancy
+// target (KYV_PSS_WPE = 4 / 6 / 8 at run time; 8 by default)
+template <bool kExact, int kWpe>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
+pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
+  const View& v = *vp;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t r = (w0 + blockIdx.x) * BLOCK + lane;
+  const bool gated = r < v.nres && ((v.gate[(size_t)v.hdr[r].kclass * v.gate_words + (k >> 5)] >> (k & 31)) & 1u);
+  if (r < v.nres) KYV_ACCT_ADD(0, 4);  // header: kind class
+  if (!__ballot(gated)) return;
+  const RuleDesc& rd = v.rules[k];
+  uint8_t st = ST_NONE;
+  uint32_t pf = 0;
+  bool m;
+  if constexpr (kExact) {
+    m = rd.kind == RK_PSS;  // pair_match of a kind-gate rule: matched (a fallback rule never gets here)
+  } else {
+    m = gated && pair_match(v, r, rd, &st);
+  }
+  if (gated && m) {
+    const ResHeader& h = v.hdr[r];
+    const NodeTab R{v.nodes + h.root};
+    KYV_ACCT_ADD(0, 12);  // header: root, node count, flags
+    st = eval_pss_cols(v, v.pss[rd.root], h, R, &pf, r);
+    if (st == ST_NONE) st = eval_pss(v, v.pss[rd.root], R, h, &pf, r);
+  }
+  if (gated && st != ST_NONE) {
+    o.status[(size_t)k * v.nres + r] = st;
+    const uint32_t ps = o.pss_slot[k];
+    if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
+    KYV_ACCT_ADD(1, 1 + ((ps != NONE && pf) ? 4 : 0));
+  }
+}
+
+// Phase 2 (pattern_eval): each wave takes chunks of 64 work items of ONE rule (grid-stride over all rules'
+// chunks), so every lane walks the same compiled pattern over a different resource with the wave-uniform
+// walker; verdict bytes as in phase 1, failing-path records staged in the chunk's own slots.
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_WPE)))
+walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, ChunkMap cm, int depth) {
+  extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
+  WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth, false};
+  walk_chunks(*vp, o, wl, cm, wk);
+}
+
+}  // namespace kyv

@@ -464,6 +464,7 @@ struct PCol {  // a decoded column entry
 KYV_HD PCol pcol(const View& v, uint32_t col, uint32_t row) {
   PCol c{NONE, 0u, 0u};
   if (col == NONE || row == NONE) return c;
+  KYV_ACCT_ADD(0, 8);
   const uint64_t x = v.colv[(size_t)v.col_off[col] + row];
   const uint32_t lo = (uint32_t)x;
   if (lo == NONE) return c;
@@ -535,6 +536,7 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
   for (uint32_t l = 0; l < PSS_NLISTS; l++) {
     const uint32_t* L = T + PC_LISTS + l * PCL_COUNT;
     if (L[PCL_LEN] == NONE) continue;
+    KYV_ACCT_ADD(0, 8);
     const uint64_t ln = v.colv[(size_t)v.col_off[L[PCL_LEN]] + row];  // (count, row of element 0)
     if ((uint32_t)ln == NONE) continue;  // absent, null or not an array (length entries: NONE count)
     const uint32_t cnt = (uint32_t)ln, eb = (uint32_t)(ln >> 32);
@@ -548,6 +550,7 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
       const uint64_t addl = L[PCL_ADD_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_ADD_LEN]] + er];
       const uint64_t dropl = L[PCL_DROP_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_DROP_LEN]] + er];
       const uint64_t portl = L[PCL_PORTS_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_PORTS_LEN]] + er];
+      KYV_ACCT_ADD(0, 8 * ((L[PCL_ADD_LEN] != NONE) + (L[PCL_DROP_LEN] != NONE) + (L[PCL_PORTS_LEN] != NONE)));
       const bool set = pobj(sc);
       const uint32_t cname = nm.i == NONE || nm.t == N_NULL ? SID_EMPTY : nm.a;
       const int privileged = set ? pbool(priv) : -1, apev = set ? pbool(ape) : -1, nonRoot = set ? pbool(nr) : -1;
@@ -857,6 +860,7 @@ KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root, uint32_t ro
 // *st = the pair's final status (not matched, nondeterministic, fallback), true when the rule body runs
 KYV_HD bool pair_match(const View& v, uint32_t r, const RuleDesc& rd, uint8_t* st) {
   if (rd.match.mode == MM_NONE) { *st = ST_FALLBACK; return KYV_WHY(FBW_MATCH), false; }  // match program not compiled
+  if (!(rd.flags & RD_GATE_EXACT)) KYV_ACCT_ADD(0, 16);  // header words the match program compares (model)
   const ResHeader& h = v.hdr[r];
   NodeTab R{v.nodes + h.root};
   LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};

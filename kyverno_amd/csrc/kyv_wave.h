@@ -42,13 +42,17 @@ __device__ __forceinline__ T sld(const T* p) {
 __device__ __forceinline__ uint32_t sld32(const uint32_t* p) { return *(const KYV_AS_CONST uint32_t*)p; }
 typedef uint32_t kyv_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ Node gnode(const Node* p) {
+  KYV_ACCT_ADD(0, 16);
   const KYV_AS_GLOBAL kyv_u32x4* q = (const KYV_AS_GLOBAL kyv_u32x4*)p;
   kyv_u32x4 x = *q;
   Node n;
   n.tk = x.x; n.a = x.y; n.b = x.z; n.c = x.w;
   return n;
 }
-__device__ __forceinline__ uint32_t gtk(const Node* p) { return *(const KYV_AS_GLOBAL uint32_t*)p; }
+__device__ __forceinline__ uint32_t gtk(const Node* p) {
+  KYV_ACCT_ADD(0, 4);
+  return *(const KYV_AS_GLOBAL uint32_t*)p;
+}
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
@@ -73,6 +77,7 @@ __device__ __forceinline__ uint32_t gld32(const uint32_t* p) { return *(const KY
 
 // Column entry of one map-entry lookup (the device entry table holds absolute column offsets in `col`)
 __device__ __forceinline__ uint32_t wcol(const View& v, const PEntry& E, bool al, uint32_t row) {
+  if (al) KYV_ACCT_ADD(0, 4);
   return al ? gld32((const uint32_t*)(v.colv + (size_t)E.col + row)) : NONE;
 }
 __device__ __forceinline__ uint32_t col_decode(uint32_t enc, uint32_t* ctype) {
@@ -638,11 +643,13 @@ constexpr uint64_t COL_NONE = 0xFFFFFFFFull;
 // device entry table holds the column's absolute offset in `col`
 __device__ __forceinline__ uint64_t jraw(const JW& w, uint32_t e, uint32_t row) {
   const uint32_t off = sld32(&w.v.pe[e].col);
+  if (row != NONE) KYV_ACCT_ADD(0, 8);
   return row == NONE ? COL_NONE : *(const KYV_AS_GLOBAL uint64_t*)(w.v.colv + (size_t)off + row);
 }
 // self column (array elements) by column id
 __device__ __forceinline__ uint64_t jself(const JW& w, uint32_t col, uint32_t row) {
   const uint32_t off = sld32(w.v.col_off + col);
+  if (row != NONE) KYV_ACCT_ADD(0, 8);
   return row == NONE ? COL_NONE : *(const KYV_AS_GLOBAL uint64_t*)(w.v.colv + (size_t)off + row);
 }
 // entry -> node index (NONE absent), type (T_UNK absent) and the node's `a`
@@ -708,6 +715,7 @@ struct WaveSink {
     if (!m) return;
     const uint32_t lane = threadIdx.x & (WAVE - 1);
     if (has) {
+      KYV_ACCT_ADD(2, wide ? sizeof(FailRec) : sizeof(StageRec));  // staged failing-path record
       const uint32_t at = n + (uint32_t)__popcll(m & ((1ull << lane) - 1));
       if (wide) {
         recs[at] = f;
@@ -779,15 +787,17 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
           gated = (gld32(v.gate + (size_t)cls * v.gate_words + (k >> 5)) >> (k & 31)) & 1u;
         }
         magic = gated && (fl & RF_MAGIC);  // pattern pairs on such resources go to the CPU engine (pair_dispatch)
+        if (gated) KYV_ACCT_ADD(0, uniform ? 8 : 12);  // header: flags, root (+ kind class)
         it = make_uint2(r | ((fl & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), gld32(&h->root));
       }
       active = gated && !magic;
       if (!uniform && !__ballot(gated)) continue;
     } else {
       const uint32_t n = sld8(wl.cnt + list);
+      if (lane == 0) KYV_ACCT_ADD(0, 1);  // work-list count
       if (!n) continue;
       active = lane < n;
-      if (active) it = wl.items[list * WAVE + lane];
+      if (active) { it = wl.items[list * WAVE + lane]; KYV_ACCT_ADD(0, 8); }  // work-list item
       r = it.x & ~ITEM_ROOT_MAP;
     }
     wk.rootmap = (it.x & ITEM_ROOT_MAP) != 0;
@@ -795,8 +805,8 @@ __device__ __forceinline__ void walk_chunks(const View& v, DevOut o, WorkLists w
     WaveSink sink{o.stage + sld32(o.rbase + (k - o.rule_lo)) + (size_t)w * WAVE * alts, 0u, rd.uses_meta != 0};
     uint8_t st = pair_walk(v, rd, active, r, k, v.nodes + it.y, wk, sink);
     if (magic) st = ST_FALLBACK;
-    if (active || magic) o.status[(size_t)k * v.nres + r] = st;
-    if (sink.n && lane == 0) o.rcnt[list] = (uint16_t)sink.n;
+    if (active || magic) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
+    if (sink.n && lane == 0) { o.rcnt[list] = (uint16_t)sink.n; KYV_ACCT_ADD(1, 2); }
   }
 }
 

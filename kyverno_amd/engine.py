@@ -28,14 +28,16 @@ def _dumps(x):
 
 
 class Ruleset:
-    def __init__(self, policies, exceptions=None):
-        """policies: list of ClusterPolicy/Policy dicts (or JSON text); exceptions: PolicyException documents
-        (rules they name are handed to the CPU engine, reason "exception")."""
+    def __init__(self, policies, exceptions=None, background=False):
+        """policies: list of ClusterPolicy/Policy dicts (or JSON text); exceptions: PolicyException documents (their
+        match blocks run on the device after each named rule's match); background: the ruleset serves background
+        scans only (KYV_COMPILE_BACKGROUND: exceptions keyed on roles / subjects never match instead of sending their
+        rules to the CPU engine)."""
         L = K.lib()
         data = _dumps(policies if not isinstance(policies, dict) else [policies])
         ex = _dumps(exceptions) if exceptions else None
         h = ctypes.c_void_p()
-        opts = K.CompileOpts(K.KYV_ABI_VERSION, 0)
+        opts = K.CompileOpts(K.KYV_ABI_VERSION, 1 if background else 0)
         K.check(L.kyv_ruleset_compile_ex(data, len(data), ex, len(ex) if ex else 0, ctypes.byref(opts), ctypes.byref(h)))
         self.h = h
         self.rules = []
@@ -68,10 +70,11 @@ class Ruleset:
         L.kyv_ruleset_jit_source(self.h, buf, size + 1, ctypes.byref(n))
         return buf.value.decode(), n.value
 
-    def jit_compile(self):
-        """hipRTC-compile the walk kernel for gfx950 (no GPU needed) -> (seconds, code-object bytes)"""
+    def jit_compile(self, accounting=False):
+        """hipRTC-compile the walk kernel for gfx950 (no GPU needed) -> (seconds, code-object bytes); accounting=True
+        compiles its byte-accounting build (what evaluate(..., account_bytes=True) loads on the GPU)"""
         secs, size = ctypes.c_double(), ctypes.c_size_t()
-        K.check(K.lib().kyv_ruleset_jit_compile(self.h, ctypes.byref(secs), ctypes.byref(size)))
+        K.check(K.lib().kyv_ruleset_jit_compile_ex(self.h, 1 if accounting else 0, ctypes.byref(secs), ctypes.byref(size)))
         return secs.value, size.value
 
     def __del__(self):
@@ -118,6 +121,9 @@ class Results:
         ab = (ctypes.c_uint64 * 5)()
         L.kyv_results_alg_bytes_phase(h, ab, 5)
         self.alg_bytes_phase = dict(zip(("match", "cond", "walk", "compact", "hist"), list(ab)))
+        ac = (ctypes.c_uint64 * 3)()
+        L.kyv_results_alg_bytes_class(h, ac, 3)
+        self.alg_bytes_class = dict(zip(("reads", "writes", "staged_records"), list(ac)))
         ju = L.kyv_results_jit(h)
         self.jit = bool(ju & 1)          # runtime-compiled walk kernels ran
         self.jit_cond = bool(ju & 2)     # runtime-compiled condition kernel (deny / foreach rules) ran

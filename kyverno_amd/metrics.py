@@ -42,7 +42,9 @@ def policy_infos(doc):
 
 
 def responded(status, first, n, apply_one):
-    """bool [n, nres] of the pairs of one policy's rules that produce a rule response (ApplyOne truncation)"""
+    """bool [n, nres] of the pairs of one policy's rules that produce a rule response (ApplyOne truncation). Under
+    ApplyOne a pair the CPU engine decides (fallback / panic / nd) ends the device's share of the resource: whether
+    the rules after it respond depends on the CPU verdict (engine.Engine.validate stops there too)."""
     sub = np.asarray(status[first:first + n]) & 7
     has = sub != K.ST_NONE
     if not apply_one:
@@ -51,7 +53,8 @@ def responded(status, first, n, apply_one):
     active = np.ones(sub.shape[1], dtype=bool)
     for i in range(n):
         out[i] = has[i] & active
-        active &= ~(((sub[i] == K.ST_PASS) | (sub[i] == K.ST_FAIL)) & out[i])
+        cpu = (sub[i] == K.ST_FALLBACK) | (sub[i] == K.ST_PANIC) | (sub[i] == K.ST_ND)
+        active &= ~(((sub[i] == K.ST_PASS) | (sub[i] == K.ST_FAIL) | cpu) & out[i])
     return out
 
 
@@ -81,11 +84,12 @@ class PolicyMetrics:
         self.duration_basis = "device time of the batch / decided pairs (amortised per rule response)"
 
     def record(self, ruleset, policy_docs, res, kinds, namespaces, cause="background_scan", operation="",
-               seconds=None):
+               seconds=None, mask=None):
         """one evaluated batch: res (engine.Results, verdicts copied back), kinds / namespaces: per resource (batch
         input order) resource kind (None: the row records nothing) and namespace; policy_docs: the policy documents in ruleset.policies order;
         cause: "admission_request" / "background_scan"; operation: "create" / "update" / ... ("" for scans), or one
-        per resource"""
+        per resource; mask: optional bool [policies, nres], only the (policy, resource) pairs whose engine response the
+        device produced (an admission batch hands some to the CPU engine, whose responses the Go shim records)"""
         st = np.asarray(res.status)
         nres = st.shape[1]
         include = np.array([k is not None for k in kinds], dtype=bool)  # None: a row with no response of its own
@@ -104,10 +108,11 @@ class PolicyMetrics:
             info = policy_infos(policy_docs[pi] if pi < len(policy_docs) else {})
             pns = "-" if info["type"] == "cluster" else info["namespace"]
             resp = responded(st, pm["first_rule"], pm["nrules"], pm["apply_one"])
+            pmask = include if mask is None else (include & np.asarray(mask[pi], dtype=bool))
             for i in range(pm["nrules"]):
                 k = pm["first_rule"] + i
                 s = st[k] & 7
-                m = resp[i] & np.isin(s, list(RESULT)) & include
+                m = resp[i] & np.isin(s, list(RESULT)) & pmask
                 if not m.any():
                     continue
                 c = np.bincount(gid[m] * 8 + s[m].astype(np.int64), minlength=ng * 8).reshape(ng, 8)

@@ -44,7 +44,7 @@ class BackgroundScan:
     def __init__(self, policies, backend="gpu", device=0):
         self.policies = [p for p in policies if isinstance(p, dict) and p.get("kind") in ("ClusterPolicy", "Policy")
                          and (p.get("spec") or {}).get("background", True) is not False]
-        self.ruleset = E.Ruleset(self.policies)
+        self.ruleset = E.Ruleset(self.policies, background=True)
         self.backend, self.device = backend, device
         self.meta = []
         # keyed like the policy cache (namespace, name): namespaced Policies may share a name across namespaces
@@ -223,9 +223,19 @@ def gather_verdicts(status, group=None, device=None):
     return torch.cat(out, dim=1).cpu().numpy(), offs
 
 
+def _sort_rows(t):
+    """failing-path rows in (global resource, rule, alternative) order: the device export writes them in compaction
+    order (kind-major by rule and walk chunk), the host path in input order; both gathers return this one order"""
+    import torch
+    for col in (2, 1, 0):
+        t = t[torch.sort(t[:, col], stable=True).indices]
+    return t
+
+
 def gather_failures(failures, res_offset, group=None, device=None):
     """Count-then-gather of the compacted failing-path records (engine.Results.failures()) of every rank: int64 rows
-    (global resource index, rule, anyPattern alternative, path template, idx0..3) in rank order. Resolved metadata
+    (global resource index, rule, anyPattern alternative, path template, idx0..3) sorted by (resource, rule,
+    alternative). Resolved metadata
     keys are batch-local dictionary ids and stay with the owning rank (which formats those paths)."""
     import torch
     import torch.distributed as dist
@@ -241,7 +251,7 @@ def gather_failures(failures, res_offset, group=None, device=None):
     if device is not None:
         t = t.to(device)
     parts, _ = _all_gather_var(t, group, dist, torch)
-    return torch.cat(parts, dim=0).cpu().numpy()
+    return _sort_rows(torch.cat(parts, dim=0)).cpu().numpy()
 
 
 def _export_target(device):
@@ -289,6 +299,25 @@ def gather_verdicts_device(batch, group=None, device=None, tensor=False):
     return (full if tensor else full.cpu().numpy()), offs
 
 
+def local_verdicts_device(batch, device=None, ncols=None):
+    """The verdicts the batch's last GPU evaluation left on `device`, without a collective: packed on the device by
+    the library (kyv_batch_export_status, input order), the first `ncols` resources unpacked there and copied to the
+    host -> uint8 [rules, ncols]. bench.py checks the timed evaluation's own verdicts against the oracle this way."""
+    import torch
+    dev, idx, stream = _export_target(device)
+    L = K.lib()
+    total = _export_check(L.kyv_batch_export_status(batch.h, idx, None, 0, None))
+    buf = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    _export_check(L.kyv_batch_export_status(batch.h, idx, ctypes.c_void_p(buf.data_ptr()), buf.numel(),
+                                            ctypes.c_void_p(stream)))
+    nr = len(batch.ruleset.rules)
+    n = batch.n if ncols is None else min(int(ncols), batch.n)
+    h = (batch.n + 1) // 2
+    q = buf[: nr * h].view(nr, h)[:, : (n + 1) // 2]
+    out = torch.stack((q & 15, q >> 4), dim=2).reshape(nr, -1)[:, :n]
+    return out.cpu().numpy()
+
+
 def gather_failures_device(batch, res_offset, group=None, device=None, tensor=False):
     """gather_failures over the failing-path records resident on `device`: int64 rows (global resource index, rule,
     alternative, path template, idx0..3) written by the library into a device tensor, then all-gathered (RCCL).
@@ -302,5 +331,5 @@ def gather_failures_device(batch, res_offset, group=None, device=None, tensor=Fa
     _export_check(L.kyv_batch_export_failures(batch.h, idx, int(res_offset), ctypes.c_void_p(t.data_ptr()), n,
                                               ctypes.c_void_p(stream)))
     parts, _ = _all_gather_var(t[:n], group, dist, torch)
-    full = torch.cat(parts, dim=0)
+    full = _sort_rows(torch.cat(parts, dim=0))
     return full if tensor else full.cpu().numpy()

@@ -54,7 +54,12 @@ def compare(policies, resources, ns_labels=None, backend="gpu", check_messages=T
                     bad.append(("oracle unsupported, device verdict", pol, rule["name"], ri, K.STATUS_NAMES[s]))
                 continue
             if s == K.ST_ND or o.get("nondeterministic"):
-                stats["nd"] += 1
+                # Go-map-order dependent: both sides must say so (a device that wrongly returns ND is a mismatch)
+                if s == K.ST_ND and o.get("nondeterministic"):
+                    stats["nd"] += 1
+                else:
+                    bad.append(("nondeterministic on one side", pol, rule["name"], ri, K.STATUS_NAMES[s],
+                                o["status"], bool(o.get("nondeterministic"))))
                 continue
             stats["compared"] += 1
             want = ORACLE_STATUS.get(o["status"])
@@ -85,8 +90,9 @@ _MATRIX_TO_DEVICE = {0: K.ST_NONE, 1: K.ST_PASS, 2: K.ST_FAIL, 3: K.ST_SKIP, 4: 
 def compare_matrix(policies, resources, ns_labels=None, backend="gpu", jit=None, threads=8, texts=True):
     """Parity at scale: every (resource, rule) verdict of the device vs the oracle's verdict matrix
     (oracle.validate_matrix) and, with texts, the failing path and message of every FAIL pair (compare_fail_texts).
-    resources: list of dicts, or NDJSON bytes (one resource per line). Nondeterministic pairs (either side) are
-    excluded from the count. Returns (stats, results); stats["nbad"] counts mismatching pairs and texts."""
+    resources: list of dicts, or NDJSON bytes (one resource per line). Nondeterministic pairs are excluded from the
+    count only when BOTH sides say ND (one-sided ND is a mismatch). Returns (stats, results); stats["nbad"] counts
+    mismatching pairs and texts."""
     import numpy as np
     rs = E.Ruleset(policies)
     b = E.Batch(rs, resources, ns_labels)
@@ -107,9 +113,10 @@ def compare_matrix(policies, resources, ns_labels=None, backend="gpu", jit=None,
         key = (rs.policies[rule["policy"]]["name"], rule["name"])
         want = lut[m[row[key]]] if key in row else np.zeros(len(resources), np.uint8)
         got = st[k, : len(resources)]
-        ndm = (want == K.ST_ND) | (got == K.ST_ND)
+        # ND (Go-map-order dependent) pairs are excluded only when BOTH sides say ND; one-sided ND is a mismatch
+        ndm = (want == K.ST_ND) & (got == K.ST_ND)
         nd += int(ndm.sum())
-        diff = np.nonzero((want != got) & ~ndm)[0]
+        diff = np.nonzero(want != got)[0]
         matched += int((got != K.ST_NONE).sum())
         compared += len(resources) - int(ndm.sum())
         for ri in diff[:3]:
@@ -139,9 +146,9 @@ def compare_status_sample(rs, res, policies, docs, ns_labels, idx, threads=8, te
         key = (rs.policies[rule["policy"]]["name"], rule["name"])
         want = lut[m[row[key]]] if key in row else np.zeros(len(idx), np.uint8)
         got = st[k]
-        ndm = (want == K.ST_ND) | (got == K.ST_ND)
+        ndm = (want == K.ST_ND) & (got == K.ST_ND)  # excluded only when both sides say ND
         nd += int(ndm.sum())
-        diff = np.nonzero((want != got) & ~ndm)[0]
+        diff = np.nonzero(want != got)[0]
         matched += int((got != K.ST_NONE).sum())
         compared += len(idx) - int(ndm.sum())
         for ri in diff[:3]:

@@ -1,6 +1,7 @@
 """Admission micro-batching (kyverno_amd/admission.py): decision helpers pinned by the reference's own webhook tests,
 and the batched device path vs a per-request CPU path (the oracle's engine.Validate restatement) on the same requests.
 """
+import collections
 import copy
 import json
 import random
@@ -334,3 +335,42 @@ def test_wildcard_golden_admission(golden):
     assert len(recs) >= 50
     for r in recs:
         assert A.wildcard_match(r["pattern"], r["text"]) == r["matched"], r
+
+
+def test_admission_metrics_only_device_responses():
+    """kyverno_policy_results of an admission batch counts exactly the engine responses the device produced: nothing
+    for a userInfo policy (its responses come from the CPU engine, recorded by the Go shim), nothing for a policy
+    reading request.operation on an UPDATE, nothing for the OldResource row, and one set of responses per device-decided
+    (request, policy) pair (pkg/webhooks/utils/metrics.go:25-64)"""
+    ui = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "ui"},
+          "spec": {"validationFailureAction": "Enforce", "rules": [{
+              "name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}, "subjects": [{"kind": "User", "name": "x"}]}]},
+              "validate": {"message": "m", "pattern": {"metadata": {"labels": {"a": "?*"}}}}}]}}
+    op = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "op"},
+          "spec": {"validationFailureAction": "Enforce", "rules": [{
+              "name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+              "preconditions": {"all": [{"key": "{{ request.operation }}", "operator": "Equals", "value": "CREATE"}]},
+              "validate": {"message": "m", "pattern": {"metadata": {"labels": {"a": "?*"}}}}}]}}
+    plain = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "plain"},
+             "spec": {"validationFailureAction": "Enforce", "rules": [{
+                 "name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                 "validate": {"message": "m", "pattern": {"metadata": {"labels": {"b": "?*"}}}}}]}}
+    calls = []
+
+    def engine(p, rq):
+        calls.append((p["metadata"]["name"], rq["operation"]))
+        return oracle_engine(p, rq)
+
+    b = A.AdmissionBatcher([ui, op, plain], backend="cpu", cpu_engine=engine)
+    pod = lambda n, lab: {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": n, "namespace": "d", "labels": lab},
+                          "spec": {}}
+    reqs = [{"uid": "c", "operation": "CREATE", "kind": "Pod", "namespace": "d", "object": pod("p1", {"a": "1"})},
+            {"uid": "u", "operation": "UPDATE", "kind": "Pod", "namespace": "d", "object": pod("p2", {"b": "1"}),
+             "oldObject": pod("p2", {})}]
+    b.handle_batch(reqs)
+    by = collections.Counter()
+    for key, n in b.metrics.results.items():
+        by[(key[4], key[7])] += n  # (policy name, operation)
+    # device responses: "op" for the CREATE, "plain" for both requests; "ui" never; "op" not for the UPDATE
+    assert by == {("op", "create"): 1, ("plain", "create"): 1, ("plain", "update"): 1}, by
+    assert sorted(calls) == [("op", "UPDATE"), ("ui", "CREATE"), ("ui", "UPDATE")]

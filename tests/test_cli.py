@@ -38,8 +38,15 @@ def _reference_counts(pols, docs, audit_warn=False):
 
 def _check(backend):
     pols, docs = _c1()
-    got, pending = cli.apply(pols, docs, backend=backend, cpu_engine=_oracle_engine)
+    calls = []
+
+    def recording_engine(policy, resource):  # must never run: every C1 pair is decided by the library
+        calls.append((policy["metadata"]["name"], (resource.get("metadata") or {}).get("name")))
+        return _oracle_engine(policy, resource)
+
+    got, pending = cli.apply(pols, docs, backend=backend, cpu_engine=recording_engine)
     assert not pending
+    assert calls == [], "C1 pairs handed to the CPU engine: %r" % calls[:5]
     want = _reference_counts(pols, docs)
     assert got.as_dict() == want.as_dict()
     d = got.as_dict()

@@ -86,7 +86,7 @@ def exception_suite(pols):
 
 def _run(pols, docs, nsl, backend, jit=None):
     exc = exception_suite(pols)
-    rs = E.Ruleset(pols, exceptions=exc)
+    rs = E.Ruleset(pols, exceptions=exc, background=True)  # the oracle runs background-scan semantics
     b = E.Batch(rs, docs, nsl)
     res = E.evaluate(rs, b, backend=backend, **({"jit": jit} if backend == "gpu" else {}))
     names, m, tx = O.validate_matrix(pols, docs, nsl, threads=8, texts=("skip", "fail"), exceptions=exc)
@@ -99,7 +99,7 @@ def _run(pols, docs, nsl, backend, jit=None):
         key = (rs.policies[rule["policy"]]["name"], rule["name"])
         want = lut[m[row[key]]] if key in row else np.zeros(len(docs), np.uint8)
         got = st[k, : len(docs)]
-        ok = (want == got) | (want == K.ST_ND) | (got == K.ST_ND)
+        ok = want == got  # an ND pair must be ND on both sides
         n["compared"] += int(ok.size)
         for ri in np.nonzero(~ok)[0][:3]:
             bad.append((key, int(ri), K.STATUS_NAMES[got[ri]], K.STATUS_NAMES[want[ri]]))
@@ -116,6 +116,24 @@ def _run(pols, docs, nsl, backend, jit=None):
                         if len(bad) < 20:
                             bad.append(("message", key, ri, msgs[ri], o and o[1]))
     return n, bad, rs, res
+
+
+def test_userinfo_exception_needs_background_flag():
+    """an exception keyed on roles / clusterRoles / subjects depends on the admission request (checkUserInfo,
+    pkg/utils/match/match.go:110-150): an admission-capable ruleset hands the rules it names to the CPU engine; a
+    background-only ruleset (empty AdmissionInfo) compiles it as never matching"""
+    pols = cases.best_practices()
+    exc = exception_suite(pols)
+    named = {(pn, rn) for e in exc for x in e["spec"]["exceptions"] for rn in x["ruleNames"] for pn in [x["policyName"]]
+             if any(f.get("roles") for f in (e["spec"]["match"].get("any") or []))}
+    assert named
+    adm = E.Ruleset(pols, exceptions=exc)
+    bg = E.Ruleset(pols, exceptions=exc, background=True)
+    for rs, want_fb in ((adm, True), (bg, False)):
+        for r in rs.rules:
+            key = (rs.policies[r["policy"]]["name"], r["name"])
+            if key in named:
+                assert (r["kind"] == "fallback" and r["reason"].startswith("exception: userInfo")) == want_fb, (key, r)
 
 
 def test_exceptions_cpu_vs_oracle():

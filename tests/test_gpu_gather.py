@@ -36,7 +36,8 @@ rows = SC.gather_failures_device(b, 1000, device="cuda:0")
 f = res.failures()
 want = sorted(zip((f["res"].astype(np.int64) + 1000).tolist(), f["rule"].tolist(), f["alt"].tolist(),
                   f["path_template"].tolist(), map(tuple, f["idx"].tolist())))
-got = sorted((int(r[0]), int(r[1]), int(r[2]), int(r[3]), tuple(int(x) for x in r[4:8])) for r in rows)
+# rows come back in (resource, rule, alternative) order, as the host-array gather returns them
+got = [(int(r[0]), int(r[1]), int(r[2]), int(r[3]), tuple(int(x) for x in r[4:8])) for r in rows]
 assert got == want and len(got) > 100, (len(got), len(want))
 dist.destroy_process_group()
 print("gather ok", full.shape, len(got))

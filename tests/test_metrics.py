@@ -88,3 +88,17 @@ def test_policy_response_stats():
             assert (applied[pi, r], errors[pi, r]) == (a, e)
             assert pr["stats"] == {"rulesAppliedCount": a, "rulesErrorCount": e}
     assert applied.sum() > 500
+
+
+def test_apply_one_stops_at_cpu_pair():
+    """applyRules: One -- after a pair the CPU engine decides, whether later rules respond depends on its verdict: the
+    device records none of them (as engine.Engine.validate stops there)"""
+    st = np.array([[K.ST_NONE, K.ST_FALLBACK, K.ST_PASS, K.ST_ND],
+                   [K.ST_FAIL, K.ST_PASS, K.ST_PASS, K.ST_SKIP],
+                   [K.ST_PASS, K.ST_SKIP, K.ST_FAIL, K.ST_FAIL]], dtype=np.uint8)
+    r = M.responded(st, 0, 3, True)
+    want = np.array([[False, True, True, True],
+                     [True, False, False, False],
+                     [False, False, False, False]])
+    assert np.array_equal(r, want)
+    assert np.array_equal(M.responded(st, 0, 3, False), st != K.ST_NONE)
