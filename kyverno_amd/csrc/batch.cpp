@@ -75,7 +75,7 @@ inline uint64_t hash_bytes(const char* p, size_t n) {
     n -= 8;
   }
   uint64_t w = 0;
-  memcpy(&w, p, n);
+  if (n) memcpy(&w, p, n);  // (an empty string_view may carry a null pointer)
   h = (h ^ w ^ ((uint64_t)n << 56)) * 0x94d049bb133111ebull;
   h ^= h >> 29;
   h *= 0xbf58476d1ce4e5b9ull;
@@ -156,14 +156,15 @@ struct Chunk {
     Hot* e = nullptr;
     if (s.size() <= 16) {
       e = &hot[(h >> 20) & 1023];
-      if (e->h == h && e->len == s.size() && e->id != NONE && memcmp(e->b, s.data(), s.size()) == 0) return e->id;
+      if (e->h == h && e->len == s.size() && e->id != NONE && (s.empty() || memcmp(e->b, s.data(), s.size()) == 0))
+        return e->id;
     }
     uint32_t id = intern(s, h);
     if (e) {
       e->h = h;
       e->id = id;
       e->len = (uint32_t)s.size();
-      memcpy(e->b, s.data(), s.size());
+      if (!s.empty()) memcpy(e->b, s.data(), s.size());
     }
     return id;
   }

@@ -1264,6 +1264,19 @@ std::string self_dir() {
 
 }  // namespace
 
+// A compiled pattern rule whose match is its kind gate (RD_GATE_EXACT: no work list, every gated lane walks) is walked by
+// its group's fused kernel (kyv_jit_fused_<g>): one wave per match wave of 64 resources walks every such rule of the
+// group back to back, so the wave's header / kind-gate loads and the chunk set-up are paid once per wave instead of once
+// per (rule, wave) chunk. KYV_FUSED=0: every rule on the per-chunk kernels. Rulesets whose rule count exceeds the gate
+// words a fused wave keeps in registers (KYV_FUSED_GW words) stay on the chunk kernels.
+constexpr uint32_t kFusedGW = 8;  // = KYV_FUSED_GW of the generated source (kyv_fused.h)
+bool jit_rule_fused(const Ruleset& rs, uint32_t k) {
+  static const bool on = !getenv("KYV_FUSED") || atoi(getenv("KYV_FUSED")) != 0;
+  if (!on || k >= rs.rules.size() || rs.rules.size() > 32u * kFusedGW) return false;
+  const RuleDesc& rd = rs.rules[k];
+  return (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) && (rd.flags & RD_GATE_EXACT);
+}
+
 // Rules whose patterns the generator covers get a bit in `jit_rules`; the source holds their node functions,
 // a root switch and the walk kernel `kyv_jit_walk`.
 std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond) {
@@ -1368,7 +1381,8 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     rule_roots.push_back({(uint32_t)k, rr});
   }
   std::ostringstream src;
-  src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n#include \"kyv_jcond.h\"\nnamespace kyv {\n";
+  src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n#define KYV_FUSED_GW " << kFusedGW
+      << "\n#include \"kyv_jcond.h\"\n#include \"kyv_fused.h\"\nnamespace kyv {\n";
   src << body.str();
   if (!crules.empty()) {
     // the match part of pair_dispatch, out of line (one copy for every rule that needs more than the kind gate):
@@ -1434,19 +1448,23 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     if (!heavy.empty()) { groups.push_back(heavy); gwpe.push_back(-1); }
   }
   const size_t ngroups = groups.size();
+  std::vector<size_t> fused_groups;  // groups with a fused kernel (kyv_jit_fused_<g>)
   for (size_t gi = 0; gi < ngroups; gi++) {
-    std::vector<uint32_t> roots;
+    std::vector<uint32_t> roots, chunk_roots;  // every root of the group; those of its per-chunk (non-fused) rules
+    std::vector<size_t> fused;                 // rule_roots indices of the group's fused rules
     for (size_t i : groups[gi]) {
       (*jit_rules)[rule_roots[i].first] = (uint8_t)(gi + 1);
-      for (uint32_t r : rule_roots[i].second) roots.push_back(r);
+      const bool f = jit_rule_fused(rs, rule_roots[i].first);
+      if (f) fused.push_back(i);
+      for (uint32_t r : rule_roots[i].second) { roots.push_back(r); if (!f) chunk_roots.push_back(r); }
     }
     // the root scope's column preload is issued before the lane's walk predicate is known: it depends on the
     // resource row only, so its loads overlap the header loads the predicate waits for (one memory round, not two)
     for (uint32_t r : roots)
       if (rep_of[r] == r)  // one root function per pattern shape
       src << "static __device__ __forceinline__ void root" << r
-          << "(const View& v, const Node* R, const ResHeader* hp, uint32_t mbase, bool rootmap, bool walk, PatOut& out) {\n"
-             "  const uint32_t row0 = (uint32_t)(hp - v.hdr), row = row0 < v.nres ? row0 : NONE;\n"
+          << "(const View& v, const Node* R, const ResHeader* hp, uint32_t row, uint32_t mbase, bool rootmap, bool walk,\n"
+             "    PatOut& out) {\n"
              "  " << g.preload(r, "pc", "row", "jc_col(v, ") << "\n"
              "  if (!walk) return;\n"
              "#ifdef KYV_EXP_JIT_PRELOAD\n  { uint64_t x = 0; for (auto q : pc) x ^= q; out.status = x == 0x123456789ull ? ST_FAIL : ST_PASS; return; }\n#endif\n"
@@ -1467,7 +1485,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     src << "struct JitWalker" << gi << " {\n"
            "  bool rootmap;\n"
            "  __device__ __forceinline__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp,\n"
-           "                                     const RuleDesc& rd, PatOut& out) {\n"
+           "                                     uint32_t row, const RuleDesc& rd, PatOut& out) {\n"
            "    out.status = ST_NONE; out.idx = 0; out.tmpl = NONE; out.key0 = NONE; out.key1 = NONE;\n"
            "#ifdef KYV_EXP_JIT_EMPTY\n    if (walk) out.status = ST_PASS; return;\n#endif\n"
            << (roots.size() <= 256 ? std::string("    switch (root) {\n") : "    switch (root < " + std::to_string(rs.pnodes.size()) +
@@ -1477,22 +1495,70 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // switch goes over a root -> shape table instead of one label per root (a 10k-label switch took the compiler
     // minutes)
     std::map<uint32_t, std::vector<uint32_t>> by_rep;
-    for (uint32_t r : roots) by_rep[rep_of[r]].push_back(r);
+    for (uint32_t r : chunk_roots) by_rep[rep_of[r]].push_back(r);
     if (roots.size() <= 256) {
       for (auto& br : by_rep) {
         for (uint32_t r : br.second) src << "      case " << r << "u:";
-        src << " root" << br.first << "(v, R, hp, rd.meta_sites, rootmap, walk, out); break;\n";
+        src << " root" << br.first << "(v, R, hp, row, rd.meta_sites, rootmap, walk, out); break;\n";
       }
     } else {
       uint32_t si = 0;
       for (auto& br : by_rep) {
-        src << "      case " << si++ << "u: root" << br.first << "(v, R, hp, rd.meta_sites, rootmap, walk, out); break;\n";
+        src << "      case " << si++ << "u: root" << br.first << "(v, R, hp, row, rd.meta_sites, rootmap, walk, out); break;\n";
       }
     }
     src << "      default: if (walk) out.status = ST_FALLBACK;\n"
            "    }\n"
            "  }\n"
            "};\n";
+    if (fused.empty()) continue;
+    // the group's fused rules, back to back for one wave (walk_fused, kyv_wave.h): per rule the slice / kind-gate test
+    // (uniform), the alternative loop of validatePatterns with the rule's roots as constants, the verdict bytes and the
+    // staged failing-path records of chunk (rule, wave)
+    src << "struct JitFused" << gi << " {\n"
+           "  __device__ __forceinline__ void run(const View& v, const DevOut& o, uint32_t nwaves, uint32_t w, uint32_t r,\n"
+           "                                     bool active, uint32_t hflags, uint32_t hroot, const uint32_t* gw) {\n"
+           "    const uint32_t lane = threadIdx.x & 63u;\n"
+           "    const Node* R = v.nodes + hroot;\n"
+           "    const ResHeader* hp = v.hdr + r;\n"
+           "    const uint32_t row = r < v.nres ? r : NONE;\n"
+           "    const bool rootmap = (hflags & RF_ROOT_MAP) != 0;\n"
+           "    (void)lane; (void)hp; (void)rootmap;\n";
+    for (size_t i : fused) {
+      const uint32_t k = rule_roots[i].first;
+      const RuleDesc& rd = rs.rules[k];
+      const bool pat = rd.kind == RK_PATTERN;
+      const uint32_t nalts = pat ? 1u : rd.nalts, alts = pat ? 1u : std::min<uint32_t>(rd.nalts, MAX_ALTS);
+      const std::string K = Gen::u(k);
+      src << "    if (" << K << " >= o.rule_lo && " << K << " < o.rule_hi) {\n"
+             "      const bool gated = active && ((gw[" << k / 32 << "] >> " << k % 32 << "u) & 1u);\n"
+             "      if (__ballot(gated)) {\n"
+             "        const bool magic = gated && (hflags & RF_MAGIC);\n"
+             "        WaveSink sink{o.stage + sld32(o.rbase + (" << K << " - o.rule_lo)) + (size_t)w * 64u * " << alts
+          << "u, 0u, " << (rd.uses_meta ? "true" : "false") << "};\n"
+             "        uint8_t st = pair_walk_alts(" << (pat ? "true" : "false") << ", " << nalts << "u, gated && !magic, r, " << K
+          << ", sink, [&](uint32_t a, bool wk, PatOut& po) {\n"
+             "          po.status = ST_NONE; po.idx = 0; po.tmpl = NONE; po.key0 = NONE; po.key1 = NONE;\n"
+             "          switch (a) {\n";
+      for (uint32_t a = 0; a < nalts; a++) {
+        const uint32_t root = rule_roots[i].second[a];
+        src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+            << ", rootmap, wk, po); break;\n";
+      }
+      src << "            default: break;\n"
+             "          }\n"
+             "        });\n"
+             "        if (magic) st = ST_FALLBACK;\n"
+             "        if (gated) { o.status[(size_t)" << K << " * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }\n"
+             "        if (sink.n && lane == 0) {\n"
+             "          o.rcnt[(size_t)(" << K << " - o.rule_lo) * nwaves + w] = (uint16_t)sink.n; KYV_ACCT_ADD(1, 2);\n"
+             "        }\n"
+             "      }\n"
+             "    }\n";
+    }
+    src << "  }\n"
+           "};\n";
+    fused_groups.push_back(gi);
   }
   src << "}  // namespace kyv\n"
          "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n";
@@ -1527,6 +1593,14 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
            "  kyv::JitWalker" << gi << " wk{false};\n"
            "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"
            "}\n";
+  // fused kernels: one workgroup (one wave) per match wave of the batch
+  for (size_t gi : fused_groups)
+    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu("
+        << (gwpe[gi] == -2 ? "KYV_JIT_WPE_LIGHT" : "KYV_JIT_WPE") << ")))\n"
+           "kyv_jit_fused_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t nwaves) {\n"
+           "  kyv::JitFused" << gi << " f;\n"
+           "  kyv::walk_fused(*vp, o, nwaves, f);\n"
+           "}\n";
   return src.str();
 }
 
@@ -1559,7 +1633,8 @@ std::string cache_path(const std::string& src, bool acct) {
   // name = walk-<toolchain hash>-<source hash>.co: the first part covers the device headers, compile options and
   // the hipRTC version, so a cache prune can drop exactly the entries older sources produced
   uint64_t h = fnv1a("");
-  for (const char* hdr : {"kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_wave.h", "kyv_walk.h", "kyv_jcond.h"})
+  for (const char* hdr : {"kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_wave.h", "kyv_walk.h", "kyv_jcond.h",
+                          "kyv_fused.h"})
     h = fnv1a(read_file(csrc + "/" + hdr), h);
   h = fnv1a(std::string(acct ? "acct|" : "") + "gfx950|O3|c++17|wpe=" + (getenv("KYV_JIT_WPE") ? getenv("KYV_JIT_WPE") : "4") + "|" +
                 (getenv("KYV_JIT_DEFS") ? getenv("KYV_JIT_DEFS") : "-DKYV_JIT_NOEXTRA"), h);

@@ -68,11 +68,12 @@ struct DevRuleset {
       o_gpats, o_gsets;
   hipModule_t jmod = nullptr;     // runtime-compiled walk kernels (jit.cpp) loaded on this device
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
+  std::vector<hipFunction_t> ffns;  // kyv_jit_fused_<g> per rule group, or null (the group has no fused rule)
   std::vector<hipFunction_t> jconds;  // [rule] kyv_jit_cond_<k> (compiled deny / foreach rule k) or null
   bool jloaded = false;
   // the byte-accounting build of the same kernels (KYV_ACCT), loaded only by an accounting evaluation
   hipModule_t amod = nullptr;
-  std::vector<hipFunction_t> afns, aconds;
+  std::vector<hipFunction_t> afns, aconds, affns;
   unsigned long long* acnt = nullptr;  // its counters (kyv_acct_bytes)
   bool aloaded = false;
 };
@@ -203,6 +204,7 @@ struct SliceSched {
   std::vector<uint3> cw;         // compiled condition rules: (rule, first match wave, waves) of its kernel's launch
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
+  std::vector<uint8_t> fg;       // [g]: the slice has rules of group g on its fused kernel (kyv_jit_fused_<g>)
   std::vector<uint32_t> grid;
   hipEvent_t evs = nullptr;      // slice start (before its resets): phase 0 of every slice, not only the first
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // after match, condition, walk, compaction (phase timing)
@@ -667,8 +669,13 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   uint32_t ng = 0;
   for (auto x : rs.jit_rules) ng = std::max<uint32_t>(ng, x);
   dr->jfns.resize(ng);
-  for (uint32_t g = 0; g < ng; g++)
+  dr->ffns.assign(ng, nullptr);
+  for (uint32_t g = 0; g < ng; g++) {
     HIP_OK(hipModuleGetFunction(&dr->jfns[g], dr->jmod, ("kyv_jit_walk_" + std::to_string(g)).c_str()));
+    if (hipModuleGetFunction(&dr->ffns[g], dr->jmod, ("kyv_jit_fused_" + std::to_string(g)).c_str()) != hipSuccess)
+      dr->ffns[g] = nullptr;
+  }
+  (void)hipGetLastError();
   dr->jconds.assign(rs.rules.size(), nullptr);
   for (size_t k = 0; k < rs.jit_cond.size(); k++)
     if (rs.jit_cond[k]) HIP_OK(hipModuleGetFunction(&dr->jconds[k], dr->jmod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
@@ -688,8 +695,11 @@ static bool ensure_jit_acct(Ruleset& rs, DevRuleset* dr) {
   }
   HIP_OK(hipModuleLoadData(&dr->amod, rs.jit_code_acct.data()));
   dr->afns.resize(dr->jfns.size());
-  for (size_t g = 0; g < dr->jfns.size(); g++)
+  dr->affns.assign(dr->jfns.size(), nullptr);
+  for (size_t g = 0; g < dr->jfns.size(); g++) {
     HIP_OK(hipModuleGetFunction(&dr->afns[g], dr->amod, ("kyv_jit_walk_" + std::to_string(g)).c_str()));
+    if (dr->ffns[g]) HIP_OK(hipModuleGetFunction(&dr->affns[g], dr->amod, ("kyv_jit_fused_" + std::to_string(g)).c_str()));
+  }
   dr->aconds.assign(dr->jconds.size(), nullptr);
   for (size_t k = 0; k < dr->jconds.size(); k++)
     if (dr->jconds[k]) HIP_OK(hipModuleGetFunction(&dr->aconds[k], dr->amod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
@@ -737,12 +747,17 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     if (runs.empty() || runs.back().second != g) runs.push_back({w, std::move(g)});
   }
   const uint32_t ncls = 1 + (jit ? (uint32_t)dr->jfns.size() : 0u);  // 0: interpreter, 1 + g: compiled group g
+  sl.fg.assign(jit ? dr->jfns.size() : 0, 0);
+  if (jit)
+    for (uint32_t k = sl.k0; k < sl.k1; k++)
+      if (rs.jit_rules[k] && jit_rule_fused(rs, k) && dr->ffns[rs.jit_rules[k] - 1]) sl.fg[rs.jit_rules[k] - 1] = 1;
   std::vector<std::vector<uint2>> slots(ncls);
   for (size_t ri = 0; ri < runs.size(); ri++) {
     const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
     std::vector<std::vector<uint32_t>> ks(ncls);
     for (uint32_t k = sl.k0; k < sl.k1; k++) {
       if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
+      if (jit && rs.jit_rules[k] && jit_rule_fused(rs, k)) continue;  // its group's fused kernel walks it
       if (!((runs[ri].second[k / 32] >> (k % 32)) & 1u)) continue;
       ks[jit ? rs.jit_rules[k] : 0].push_back(k);
     }
@@ -1152,6 +1167,14 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         const hipStream_t ws = (wforked && cls >= 2) ? d.wstream : stream;
         HIP_OK(hipModuleLaunchKernel(acct ? dr->afns[cls - 1] : dr->jfns[cls - 1], sl.grid[cls], 1, 1, BLOCK, 1, 1, 0, ws,
                                      args, nullptr));
+      }
+      // fused groups: one workgroup per match wave, every direct rule of the group walked back to back (kyv_fused.h)
+      for (size_t g = 0; g < sl.fg.size(); g++) {
+        if (!sl.fg[g]) continue;
+        const View* vp = d.view;
+        uint32_t nw = d.wl.nwaves;
+        void* args[] = {(void*)&vp, (void*)&o, (void*)&nw};
+        HIP_OK(hipModuleLaunchKernel(acct ? dr->affns[g] : dr->ffns[g], nw, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
       }
       uint64_t staged = 0;
       if (acct) { const auto c = acct_take(); aphase[2] += c[0] + c[1] + c[2]; staged = c[2]; }

@@ -202,6 +202,8 @@ void assign_glob_masks(Ruleset& rs);
 void assign_cond_sets(Ruleset& rs);
 std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond = nullptr);
 std::vector<char> jit_compile(const std::string& src, double* seconds, bool acct = false);
+// rule k is walked by its group's fused kernel (kyv_jit_fused_<g>) rather than the per-chunk schedule (jit.cpp)
+bool jit_rule_fused(const Ruleset& rs, uint32_t k);
 enum JitMode { JIT_AUTO = 0, JIT_OFF = 1, JIT_ON = 2 };
 constexpr size_t JIT_AUTO_MIN_RESOURCES = 65536;  // smaller batches are not worth a compile
 void resolve_path_columns(Batch& b, int threads);

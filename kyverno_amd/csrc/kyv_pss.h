@@ -709,8 +709,8 @@ KYV_HD uint8_t pss_pod(NodeTab R, uint32_t kind, bool decode, uint32_t* meta_out
 // kCols: the decoded pod's checks through path columns only (pss_kernel: inlined, no call frame); the caller routes
 // pairs that need the map walk (exclusions, no columns, typed decode not done) elsewhere
 // (returns ST_NONE with *fails_out = 0 when the column form does not apply)
-// row: the resource's batch position (passed explicitly: a header reference handed to an out-of-line call may point
-// at a copy)
+// row: the resource's batch position (its column row), passed explicitly by every caller
+// kOol: the checks as the out-of-line pss_checks_cols_ool (eval_pss, see there)
 KYV_FN_PSS uint32_t pss_checks_cols_ool(const View& v, NodeTab R, uint32_t row, const uint32_t* T);
 template <bool kOol = false>
 KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const PssDesc& pd, const ResHeader& h,
@@ -733,9 +733,13 @@ KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const
   return fails ? ST_FAIL : ST_PASS;
 }
 
-// the column checks as their own out-of-line function for eval_pss (called from the match kernel; inlined into that
-// out-of-line function they measured wrong on the device -- r3i: baseline pairs with preconditions failed checks the
-// host instantiation passed -- while the same inlined code in pss_kernel is correct)
+// The column checks stay out of line when reached from eval_pss (itself out of line, called from the match kernel).
+// Inlined there (round 3, and again in round 4 with the row passed explicitly) the device computes wrong masks for
+// the C5 baseline rule with preconditions (c5-r006: capability-add and hostPort bits from the loops over
+// column-addressed sub-arrays set where the host instantiation has none); the same source is correct inlined into
+// pss_kernel, in the byte-accounting build (whose atomics change the schedule) and on the host under ASan + UBSan
+// (clean, round 4), and the kernel's stack is statically sized (no dynamic stack). Pinned by
+// tests/test_gpu_parity.py::test_pss_with_preconditions_gpu_equals_cpu (device bytes + masks == host, jit on / off).
 KYV_FN_PSS uint32_t pss_checks_cols_ool(const View& v, NodeTab R, uint32_t row, const uint32_t* T) {
   return pss_checks_cols(v, R, row, T);
 }

@@ -11,37 +11,37 @@ namespace kyv {
 // wave-uniform points: one emit per anyPattern alternative (trip count uniform per rule), with `has` set on
 // the lanes whose alternative failed.
 //
-// `Walker::run(v, root, walk, R, hp, rd, out)` runs one compiled pattern for the lanes with `walk` set: the host
+// `Walker::run(v, root, walk, R, hp, row, rd, out)` runs one compiled pattern for the lanes with `walk` set (row: the
+// resource's batch position, i.e. its column row, passed explicitly rather than derived from `hp`): the host
 // instantiation is the per-lane eval_pattern (HostWalker below), the kernel's is the wave-uniform walker
 // (kyv_wave.h).
 struct HostWalker {
   Stack stk;
-  KYV_HD void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp, const RuleDesc& rd,
-                  PatOut& out) {
+  KYV_HD void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp, uint32_t row,
+                  const RuleDesc& rd, PatOut& out) {
+    (void)row;
     out.status = ST_NONE;
     if (walk) eval_pattern(v, root, NodeTab{R}, *hp, rd, stk, out);
   }
 };
 
-template <class Sink, class Walker>
-KYV_HD uint8_t pair_walk(const View& v, const RuleDesc& rd, bool walk, uint32_t r, uint32_t k, const Node* R, Walker& wk,
-                         Sink& sink) {
+// The alternative loop of validatePatterns over a callable that walks alternative `a` (alt(a, walk, po)): shared by
+// pair_walk (the alternative's root read from the rule) and the fused compiled walk kernels (jit.cpp), whose
+// per-rule code passes its roots as constants
+template <class Sink, class AltFn>
+KYV_HD uint8_t pair_walk_alts(bool pattern, uint32_t nalts, bool walk, uint32_t r, uint32_t k, Sink& sink, AltFn&& alt) {
   uint8_t st = ST_NONE;
-  // address only (walkers read it for metadata expansion); not predicated on `walk`, so a compiled walker's column
-  // preload (rows = hp - v.hdr) does not wait for the loads `walk` depends on
-  const ResHeader* hp = v.hdr + r;
-  const uint32_t nalts = rd.kind == RK_PATTERN ? 1 : rd.nalts;  // uniform across the wave
   uint32_t nfail = 0, nskip = 0;
   for (uint32_t a = 0; a < nalts; a++) {
     PatOut po;
-    wk.run(v, rd.kind == RK_PATTERN ? rd.root : v.pool[rd.root + a], walk, R, hp, rd, po);
+    alt(a, walk, po);
     bool rec = false;
     if (walk) {
       switch (po.status) {
         case ST_PASS: st = (uint8_t)(ST_PASS | ((a < 30 ? a : 30) << 3)); walk = false; break;  // alt index for the message
         case ST_SKIP: nskip++; break;
         case ST_FAIL: case ST_ERROR:
-          if (rd.kind == RK_PATTERN && po.status == ST_ERROR) { st = ST_ERROR; walk = false; break; }
+          if (pattern && po.status == ST_ERROR) { st = ST_ERROR; walk = false; break; }
           rec = true;
           nfail++;
           break;
@@ -58,12 +58,25 @@ KYV_HD uint8_t pair_walk(const View& v, const RuleDesc& rd, bool walk, uint32_t 
     sink.emit(rec, fr);
   }
   if (walk) {
-    if (rd.kind == RK_PATTERN) st = nfail ? ST_FAIL : ST_SKIP;
+    if (pattern) st = nfail ? ST_FAIL : ST_SKIP;
     else if (nfail) st = ST_FAIL;
     else if (nskip) st = ST_SKIP;
     else st = (uint8_t)(ST_PASS | (31 << 3));  // empty anyPattern list: pass with the rule message (validation.go:701)
   }
   return st;
+}
+
+template <class Sink, class Walker>
+KYV_HD uint8_t pair_walk(const View& v, const RuleDesc& rd, bool walk, uint32_t r, uint32_t k, const Node* R, Walker& wk,
+                         Sink& sink) {
+  // address only (walkers read it for metadata expansion); not predicated on `walk`, so a compiled walker's column
+  // preload (row r) does not wait for the loads `walk` depends on
+  const ResHeader* hp = v.hdr + r;
+  const uint32_t nalts = rd.kind == RK_PATTERN ? 1 : rd.nalts;  // uniform across the wave
+  const uint32_t row = r < v.nres ? r : NONE;
+  return pair_walk_alts(rd.kind == RK_PATTERN, nalts, walk, r, k, sink, [&](uint32_t a, bool w, PatOut& po) {
+    wk.run(v, rd.kind == RK_PATTERN ? rd.root : v.pool[rd.root + a], w, R, hp, row, rd, po);
+  });
 }
 
 }  // namespace kyv

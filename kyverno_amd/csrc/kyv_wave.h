@@ -248,8 +248,8 @@ struct WaveWalker {
   int cap;
   bool rootmap;    // per lane (unused by the interpreter)
 
-  __device__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp, const RuleDesc& rd,
-                      PatOut& out) {
+  __device__ void run(const View& v, uint32_t root, bool walk, const Node* R, const ResHeader* hp, uint32_t row,
+                      const RuleDesc& rd, PatOut& out) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lbit = 1ull << lane;
     uint64_t seen = 0, found = 0;
@@ -279,7 +279,7 @@ struct WaveWalker {
     int action = 0;
     uint32_t epn = root, ern = 0;
     uint32_t etype = T_UNK;        // per lane: type of the node being entered, when a column supplied it
-    uint32_t erow = hp ? hp - v.hdr : 0;  // per lane: column row of the node being entered (root: the resource)
+    uint32_t erow = row == NONE ? 0u : row;  // per lane: column row of the node being entered (root: the resource)
 
 #define KYV_PUSH(KIND, PN, ALIVE, A, B, ROW)                                                   \
   do {                                                                                      \

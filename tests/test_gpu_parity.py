@@ -256,3 +256,31 @@ def test_scan_summary_gpu_and_rccl():
     r = subprocess.run([sys.executable, "-c", _SCAN_RCCL], cwd=root, env=env, capture_output=True, text=True,
                        timeout=200)
     assert r.returncode == 0 and "scan-rccl ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+@pytest.mark.parametrize("jit", [False, True])
+def test_pss_with_preconditions_gpu_equals_cpu(jit):
+    """PodSecurity rules behind preconditions run eval_pss out of line from the match kernel (its column checks
+    inlined there), the others pss_kernel: the round-3 wrong-mask case (C5 policy c5-006, baseline + preconditions)
+    and its restricted / precondition-free variants, device verdict bytes and PSS masks == the host instantiation"""
+    import copy
+    data, nsl = synth.corpus_ndjson(20000, seed=54, edge=True)
+    base = [p for p in synth.c5_policies(50) if p["metadata"]["name"] == "c5-006"]
+    assert base and base[0]["spec"]["rules"][0].get("preconditions")
+    nopre = copy.deepcopy(base)
+    del nopre[0]["spec"]["rules"][0]["preconditions"]
+    restr = copy.deepcopy(base)
+    restr[0]["spec"]["rules"][0]["validate"]["podSecurity"]["level"] = "restricted"
+    for pols in (base, nopre, restr, base + nopre + restr):
+        rs = E.Ruleset(pols)
+        b = E.Batch(rs, data, nsl)
+        g = E.evaluate(rs, b, backend="gpu", jit=jit)
+        c = E.evaluate(rs, b, backend="cpu")
+        assert np.array_equal(g.raw, c.raw)
+        for k, r in enumerate(rs.rules):
+            if r["kind"] != "podSecurity":
+                continue
+            fails = np.nonzero(np.asarray(g.status[k]) == K.ST_FAIL)[0]
+            assert len(fails) > 0
+            for i in fails[:: max(1, len(fails) // 200)].tolist():
+                assert g.pss_mask(i, k) == c.pss_mask(i, k), (r["name"], i)
