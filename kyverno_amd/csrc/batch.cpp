@@ -629,6 +629,14 @@ void derive_strings(Batch& b, size_t from, int threads) {
         for (unsigned char c : x) if (c >= 0x80) { ascii = false; break; }
         if (ascii) f |= SF_ASCII;
         if (!ascii || x.find_first_of("*?") != std::string::npos) f |= SF_GLOBBY;
+        {  // SF_PLAIN (kyv_layout.h): as a pattern string, only the string itself (or a bool's FormatBool) matches it
+          const char h = x.empty() ? 0 : x[0];
+          const bool plain = ascii && x.find_first_of("|&*?") == std::string::npos &&
+                             (x.empty() || (x.front() != ' ' && x.back() != ' ')) &&
+                             !(x.size() >= 2 && (h == '<' || h == '>' || h == '!')) &&
+                             !((h >= '0' && h <= '9') || h == '+' || h == '-' || h == '.');
+          if (plain) f |= SF_PLAIN;
+        }
         if (s < gidx.size()) f |= gidx[s] << SF_GIDX_SHIFT;
         if (x.compare(0, pfx_aa.size(), pfx_aa) == 0) f |= SF_PFX_APPARMOR;
         if (x.compare(0, pfx_lh.size(), pfx_lh) == 0) f |= SF_PFX_LOCALHOST;

@@ -526,10 +526,10 @@ static bool render_message(kyv_results* r, const Ruleset& rs, const Batch& b, ui
   if (d.kind == RK_FOREACH) {  // validateForEach / validateElements (validation.go:319-381)
     if (st == ST_PASS) return *o = "rule passed", true;
     if (st == ST_SKIP) return *o = "rule skipped", true;
-    if (st == ST_FAIL)
+    if (st == ST_FAIL && m.foreach_texts)  // every entry a top-level deny: the one failure text
       return *o = "validation failure: " + (m.message.empty() ? "validation error: rule " + m.name + " failed" : m.message),
              true;
-    return false;  // error texts embed Go error strings
+    return false;  // error texts embed Go error strings; pattern / nested failures embed the element's path
   }
   if (m.message_vars && st == ST_FAIL) return false;  // message needs variable substitution (CPU engine)
   if (d.kind == RK_PSS) {

@@ -345,6 +345,10 @@ struct Cx {
   uint32_t nmeta = 0;
   std::vector<MetaSite> sites;
   bool allow_element = false;  // compiling conditions of a foreach entry (`element` is bound)
+  // compiling a foreach pattern: a value that is exactly one element variable becomes an L_DYN leaf; dyn: the
+  // entry's element variables (kind 0 path / 1 elementIndex, path segments as sids)
+  bool dyn_ok = false;
+  std::vector<std::vector<uint32_t>> dyn;
   bool uses_op = false;        // some condition read request.operation
   uint32_t tmpl(const std::string& s) {
     auto it = rs.template_ids.find(s);
@@ -456,6 +460,41 @@ std::string trim_sp(const std::string& s) {
   return s.substr(b, e - b);
 }
 
+// a foreach pattern value that is exactly one element variable (vars.go:352-431 substitutes it by its typed value):
+// `{{element}}`, `{{element.<ident>...}}` -> [0, nseg, sids...], `{{elementIndex}}` -> [1, 0]
+bool element_var_desc(Cx& c, const std::string& s, std::vector<uint32_t>* d) {
+  if (s.size() < 4 || s.compare(0, 2, "{{") != 0 || s.compare(s.size() - 2, 2, "}}") != 0) return false;
+  std::string in = s.substr(2, s.size() - 4);
+  if (in.find('{') != std::string::npos || in.find('}') != std::string::npos) return false;
+  size_t b = 0, e = in.size();
+  while (b < e && isspace((unsigned char)in[b])) b++;
+  while (e > b && isspace((unsigned char)in[e - 1])) e--;
+  in = in.substr(b, e - b);
+  if (in == "elementIndex") { *d = {1u, 0u}; return true; }
+  if (in.compare(0, 7, "element") != 0) return false;
+  std::vector<uint32_t> segs;
+  for (size_t i = 7; i < in.size();) {
+    if (in[i] != '.') return false;
+    size_t j = i + 1;
+    if (j >= in.size() || !(isalpha((unsigned char)in[j]) || in[j] == '_')) return false;
+    while (j < in.size() && (isalnum((unsigned char)in[j]) || in[j] == '_')) j++;
+    segs.push_back(c.sid(in.substr(i + 1, j - i - 1)));
+    i = j;
+  }
+  *d = {0u, (uint32_t)segs.size()};
+  d->insert(d->end(), segs.begin(), segs.end());
+  return true;
+}
+
+bool keys_have_vars(const Value& p) {
+  if (p.t == T::Obj)
+    for (auto& kv : p.o)
+      if (kv.first.find("{{") != std::string::npos || kv.first.find("$(") != std::string::npos || keys_have_vars(kv.second))
+        return true;
+  if (p.t == T::Arr) for (auto& e : p.a) if (keys_have_vars(e)) return true;
+  return false;
+}
+
 uint32_t compile_leaf(Cx& c, const Value& p) {  // pattern.Validate leaf types
   Leaf L{};
   L.exact = NONE;
@@ -474,6 +513,17 @@ uint32_t compile_leaf(Cx& c, const Value& p) {  // pattern.Validate leaf types
       break;
     }
     case T::Str: {
+      if (c.dyn_ok && (p.s.find("{{") != std::string::npos || p.s.find("$(") != std::string::npos)) {
+        std::vector<uint32_t> d;
+        if (!element_var_desc(c, p.s, &d)) throw Fallback{"foreach: pattern variables other than whole-string element values"};
+        uint32_t slot = 0;
+        while (slot < c.dyn.size() && c.dyn[slot] != d) slot++;
+        if (slot == c.dyn.size()) c.dyn.push_back(d);
+        if (c.dyn.size() > MAX_DYN) throw Fallback{"foreach: more element variables than the device resolves"};
+        L.type = L_DYN;
+        L.exact = slot;
+        break;
+      }
       if (has_magic(p.s)) throw Fallback{"pattern text contains an anchor-error phrase"};
       L.type = L_STR;
       L.exact = c.sid(p.s);
@@ -1546,23 +1596,26 @@ uint32_t compile_conds(Cx& c, const Value* doc) {
   return (uint32_t)c.rs.cprogs.size() - 1;
 }
 
-// validate.foreach (validation.go:319-421): entries with a JMESPath-subset list, deny conditions and optional
-// per-element preconditions / elementScope; patterns, nested foreach and context entries stay on the CPU
-uint32_t compile_foreach(Cx& c, const Value& fe, const std::string& message) {
+// validate.foreach (validation.go:319-421): entries with a JMESPath-subset list (over request.object; inside a nested
+// foreach also over the enclosing element), optional per-element preconditions / elementScope, and one validator:
+// deny conditions, a pattern / anyPattern (element variables as whole-string values, L_DYN), or a nested foreach (one
+// level). Context entries and other variables stay on the CPU. Returns the pool offset of [n, entries...].
+uint32_t compile_foreach_entries(Cx& c, const Value& fe, int depth, bool* plain_deny) {
   if (fe.t != T::Arr || fe.a.empty()) throw Fallback{"foreach"};
-  if (var_syntax(message)) throw Fallback{"foreach: message with variables"};
+  if (depth > 1) throw Fallback{"foreach: nested deeper than one level"};
   std::vector<ForeachEntry> ents;
   for (auto& e : fe.a) {
     if (e.t != T::Obj) throw Fallback{"foreach"};
     for (auto& kv : e.o)
-      if (kv.first != "list" && kv.first != "deny" && kv.first != "preconditions" && kv.first != "elementScope")
+      if (kv.first != "list" && kv.first != "deny" && kv.first != "preconditions" && kv.first != "elementScope" &&
+          kv.first != "pattern" && kv.first != "anyPattern" && kv.first != "foreach")
         throw Fallback{"foreach: " + kv.first};
     const Value* l = e.get("list");
-    const Value* d = e.get("deny");
-    if (!l || l->t != T::Str || !d || d->t != T::Obj) throw Fallback{"foreach"};
+    if (!l || l->t != T::Str) throw Fallback{"foreach"};
     ForeachEntry fx{};
+    fx.dyn = NONE;
+    fx.body = NONE;
     std::vector<std::string> segs;
-    CondText ct;
     if (object_var("{{" + l->s + "}}", segs, nullptr)) {  // plain request.object chain
       fx.list.kind = OK_PATH;
       fx.list.nseg = (uint16_t)segs.size();
@@ -1570,8 +1623,8 @@ uint32_t compile_foreach(Cx& c, const Value& fe, const std::string& message) {
       for (auto& sg : segs) c.rs.pool.push_back(c.sid(sg));
     } else {
       const bool ae = c.allow_element;
-      c.allow_element = false;
-      if (!jmes_var(c, "{{" + l->s + "}}", false, &fx.list, nullptr, &c.uses_op)) throw Fallback{"foreach: list"};
+      c.allow_element = depth > 0;  // a nested list reads the enclosing element
+      if (!jmes_var(c, "{{" + l->s + "}}", c.allow_element, &fx.list, nullptr, &c.uses_op)) throw Fallback{"foreach: list"};
       c.allow_element = ae;
       // eval_foreach iterates path and JMESPath lists only; a literal (request.operation: the one-element list
       // ["CREATE"] in the reference) is not a program it can run
@@ -1583,7 +1636,51 @@ uint32_t compile_foreach(Cx& c, const Value& fe, const std::string& message) {
     c.allow_element = true;
     const Value* pre = e.get("preconditions");
     fx.pre = pre && pre->t != T::Null ? compile_conds(c, pre) : NONE;
-    fx.deny = compile_conds(c, d->get("conditions"));
+    const Value* d = e.get("deny");
+    const Value* pat = e.get("pattern");
+    const Value* ap = e.get("anyPattern");
+    if (d && d->t != T::Null) {  // validate(): deny wins over pattern / anyPattern and foreach
+      if (d->t != T::Obj) throw Fallback{"foreach"};
+      fx.kind = FE_DENY;
+      fx.deny = compile_conds(c, d->get("conditions"));
+      if (depth > 0) *plain_deny = false;
+    } else if ((pat && pat->t != T::Null) || (ap && ap->t != T::Null)) {
+      *plain_deny = false;
+      fx.deny = NONE;
+      if ((pat && pat->t != T::Null && keys_have_vars(*pat)) || (ap && ap->t != T::Null && keys_have_vars(*ap)))
+        throw Fallback{"foreach: variables in pattern keys"};
+      c.dyn_ok = true;
+      c.dyn.clear();
+      if (pat && pat->t != T::Null) {
+        fx.kind = FE_PATTERN;
+        fx.body = compile_pattern_root(c, *pat);
+      } else {
+        if (ap->t != T::Arr) throw Fallback{"foreach: anyPattern is not a list"};
+        std::vector<uint32_t> roots;
+        for (auto& p : ap->a) roots.push_back(compile_pattern_root(c, p));
+        if (roots.size() > MAX_ALTS) throw Fallback{"too many anyPattern alternatives"};
+        fx.kind = FE_ANYPATTERN;
+        fx.nalts = (uint32_t)roots.size();
+        fx.body = (uint32_t)c.rs.pool.size();
+        for (auto x : roots) c.rs.pool.push_back(x);
+      }
+      c.dyn_ok = false;
+      if (!c.dyn.empty()) {
+        fx.dyn = (uint32_t)c.rs.pool.size();
+        c.rs.pool.push_back((uint32_t)c.dyn.size());
+        for (auto& dv : c.dyn) c.rs.pool.insert(c.rs.pool.end(), dv.begin(), dv.end());
+      }
+    } else if (nonempty(e.get("foreach"))) {
+      *plain_deny = false;
+      fx.deny = NONE;
+      fx.kind = FE_NESTED;
+      c.allow_element = false;
+      fx.body = compile_foreach_entries(c, *e.get("foreach"), depth + 1, plain_deny);
+    } else {
+      fx.kind = FE_NONE;  // no validator for the element: "skip rule due to empty result"
+      fx.deny = NONE;
+      *plain_deny = false;
+    }
     c.allow_element = false;
     ents.push_back(fx);
   }
@@ -1595,6 +1692,12 @@ uint32_t compile_foreach(Cx& c, const Value& fe, const std::string& message) {
     for (uint32_t x : w) c.rs.pool.push_back(x);
   }
   return at;
+}
+
+uint32_t compile_foreach(Cx& c, const Value& fe, const std::string& message, bool* plain_deny) {
+  if (var_syntax(message)) throw Fallback{"foreach: message with variables"};
+  *plain_deny = true;
+  return compile_foreach_entries(c, fe, 0, plain_deny);
 }
 
 // deny message with `{{ request.object... }}` references -> parts (false: other variables, escapes, references)
@@ -1940,6 +2043,8 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
           c.sites.clear();
           c.uses_op = false;
           c.allow_element = false;
+          c.dyn_ok = false;
+          c.dyn.clear();
           rd.pre = NONE;
           if (why.empty() && !nil(r.get("preconditions"))) rd.pre = compile_conds(c, r.get("preconditions"));
           if (!why.empty()) {
@@ -1973,7 +2078,7 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
             rm.pss_version = val->get("podSecurity")->str_or("version");
           } else if (val && nonempty(val->get("foreach"))) {
             rd.kind = RK_FOREACH;
-            rd.root = compile_foreach(c, *val->get("foreach"), rm.message);
+            rd.root = compile_foreach(c, *val->get("foreach"), rm.message, &rm.foreach_texts);
           } else {
             continue;  // "invalid validation rule": no response
           }

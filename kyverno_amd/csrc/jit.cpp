@@ -1222,13 +1222,21 @@ struct CondGen {
           << "    if (c == CR_FB) return ST_FALLBACK;\n    if (c == CR_PANIC) return ST_PANIC;\n"
           << "    if (c == CP_ERROR) return ST_ERROR;\n    return c == CR_TRUE ? ST_FAIL : ST_PASS; }\n";
     } else if (rd.kind == RK_FOREACH) {
-      out << "  uint32_t applied = 0u;\n";
       const uint32_t nent = rs.pool[rd.root];
       std::vector<ForeachEntry> ents(nent);
-      for (uint32_t e = 0; e < nent; e++)
+      bool deny_only = true;
+      for (uint32_t e = 0; e < nent; e++) {
         memcpy(&ents[e], rs.pool.data() + rd.root + 1 + e * (sizeof(ForeachEntry) / 4), sizeof(ForeachEntry));
-      for (uint32_t e = 0; e < nent && ok; e++) foreach_entry(ents[e]);
-      out << "  return applied ? ST_PASS : ST_SKIP;\n";
+        deny_only = deny_only && ents[e].kind == FE_DENY;
+      }
+      if (deny_only) {  // deny entries: streamed lists, conditions generated in place
+        out << "  uint32_t applied = 0u;\n";
+        for (uint32_t e = 0; e < nent && ok; e++) foreach_entry(ents[e]);
+        out << "  return applied ? ST_PASS : ST_SKIP;\n";
+      } else {  // pattern / anyPattern / nested entries: the evaluator's foreach (kyv_pss.h) inside this rule's kernel
+        out << "  (void)ei; (void)et; (void)ea; (void)erow; (void)L;\n"
+            << "  return eval_foreach(v, NodeTab{R}, v.rules[" << u(k) << "], r);\n";
+      }
     } else {
       ok = false;
     }

@@ -356,6 +356,40 @@ KYV_HD bool leaf_match(const View& v, const Leaf& L, const Val& x, bool* fb) {
   }
 }
 
+// pattern.Validate(value, p) for a leaf substituted from an element variable (L_DYN): p is the variable's value as the
+// JSON context holds it (numbers float64, so an integer element field is a float64 pattern); *fb for a pattern the
+// device does not decide (a string that is not SF_PLAIN, a map or array value)
+KYV_HD bool leaf_match_dyn(const View& v, const Val& p, const Val& x, bool* fb) {
+  switch (p.t) {
+    case N_NULL:  // validateNilPattern
+      switch (x.t) {
+        case 0xFF: case N_NULL: case N_FALSE: return true;
+        case N_INT: return x.i == 0;
+        case N_FLOAT: return x.f == 0.0;
+        case N_STR: return x.sid == SID_EMPTY;
+        default: return false;
+      }
+    case N_TRUE: case N_FALSE: return x.t == p.t;  // validateBoolPattern
+    case N_INT: case N_FLOAT: {  // validateFloatPattern (pattern.go:87-116)
+      const double pf = p.t == N_INT ? (double)p.i : p.f;
+      switch (x.t) {
+        case N_INT: {
+          if (pf != __builtin_trunc(pf)) return false;
+          if (!(pf > -9.223372036854775808e18 && pf < 9.223372036854775807e18)) return false;
+          return (int64_t)pf == x.i;
+        }
+        case N_FLOAT: return x.f == pf;
+        case N_STR: return (v.str_flags[x.sid] & SF_FLOAT) && v.str_f64[x.sid] == pf;
+        default: return false;
+      }
+    }
+    case N_STR:
+      if (!(v.str_flags[p.sid] & SF_PLAIN)) { *fb = true; return false; }
+      return (x.t == N_STR && x.sid == p.sid) || ((x.t == N_TRUE || x.t == N_FALSE) && x.wsid == p.sid);
+    default: *fb = true; return false;
+  }
+}
+
 // ---------------------------------------------------------------- resource helpers
 KYV_HD uint32_t map_find(NodeTab R, uint32_t m, uint32_t key) {
   const Node& mn = R[m];
@@ -681,9 +715,11 @@ KYV_HD uint8_t expand_meta_root(const View& v, const MetaSite& ms, NodeTab R, co
   return ST_NONE;
 }
 
-// MatchPattern (validate.go:31-56) for one compiled pattern; a walk deeper than the stack ends in ST_FALLBACK
+// MatchPattern (validate.go:31-56) for one compiled pattern; a walk deeper than the stack ends in ST_FALLBACK.
+// rn0: the node the pattern validates (the resource root, or a foreach element); dyn: the values of the pattern's
+// element variables (L_DYN leaves), foreach patterns only
 KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const ResHeader& h, const RuleDesc& rd, Stack stk,
-                         PatOut& out) {
+                         PatOut& out, uint32_t rn0 = 0, const Val* dyn = nullptr) {
   uint64_t seen = 0, found = 0;
   Keys keys{NONE, NONE};
   out.idx = 0;
@@ -692,7 +728,7 @@ KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const 
   bool fb = false;
   // action: 0 enter, 1 next, 2 return
   int action = 0;
-  uint32_t epn = root, ern = 0;  // enter arguments
+  uint32_t epn = root, ern = rn0;  // enter arguments
   for (;;) {
     if (action == 0) {
       const PNode& P = v.pn[epn];
@@ -724,11 +760,14 @@ KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const 
       if (P.kind == P_LEAF) {
         const Leaf& L = v.leaves[P.first];
         bool okv = true;
+        const bool dl = L.type == L_DYN;
+        if (dl && !dyn) { KYV_WHY(FBW_VALUE); out.status = ST_FALLBACK; return; }
         if (rt == N_ARR) {
           const Node& A = R[ern];
-          for (uint32_t i = 0; i < A.b && okv; i++) okv = leaf_match(v, L, value_of(v, R, A.a + i), &fb);
+          for (uint32_t i = 0; i < A.b && okv; i++)
+            okv = dl ? leaf_match_dyn(v, dyn[L.exact], value_of(v, R, A.a + i), &fb) : leaf_match(v, L, value_of(v, R, A.a + i), &fb);
         } else {
-          okv = leaf_match(v, L, value_of(v, R, ern), &fb);
+          okv = dl ? leaf_match_dyn(v, dyn[L.exact], value_of(v, R, ern), &fb) : leaf_match(v, L, value_of(v, R, ern), &fb);
         }
         if (fb) { KYV_WHY(FBW_VALUE); out.status = ST_FALLBACK; return; }
         ret = okv ? ok_ret() : mkerr(EC_NONE, 0, P.tmpl);
@@ -742,7 +781,10 @@ KYV_FN_PATTERN void eval_pattern(const View& v, uint32_t root, NodeTab R, const 
         const Leaf& L = v.leaves[v.pn[P.first].first];
         const Node& A = R[ern];
         bool okv = true;
-        for (uint32_t i = 0; i < A.b && okv; i++) okv = leaf_match(v, L, value_of(v, R, A.a + i), &fb);
+        const bool dl = L.type == L_DYN;
+        if (dl && !dyn) { KYV_WHY(FBW_VALUE); out.status = ST_FALLBACK; return; }
+        for (uint32_t i = 0; i < A.b && okv; i++)
+          okv = dl ? leaf_match_dyn(v, dyn[L.exact], value_of(v, R, A.a + i), &fb) : leaf_match(v, L, value_of(v, R, A.a + i), &fb);
         if (fb) { KYV_WHY(FBW_VALUE); out.status = ST_FALLBACK; return; }
         ret = okv ? ok_ret() : mkerr(EC_NONE, 0, P.tmpl);
         action = 2;

@@ -50,6 +50,7 @@ struct RuleMeta {
   uint8_t kind = RK_NONE;
   std::string reason;         // RK_FALLBACK / RK_PANIC / RK_ERROR reason
   bool message_vars = false;  // message needs variable substitution (CPU)
+  bool foreach_texts = true;  // foreach rule whose entries are all top-level deny: fail texts rendered by the library
   std::string pss_level, pss_version;
   // deny failure message (getDenyMessage, validation.go:466-479): literal text and `{{ request.object... }}`
   // references (key sids); msg_whole_var: the message is exactly one reference

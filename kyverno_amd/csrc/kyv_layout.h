@@ -72,6 +72,11 @@ enum StrFlag : uint32_t {
   SF_PFX_APPARMOR = 1u << 12,   // "container.apparmor.security.beta.kubernetes.io/"
   SF_PFX_LOCALHOST = 1u << 13,  // "localhost/"
   SF_PFX_SECCOMP_C = 1u << 14,  // "container.seccomp.security.alpha.kubernetes.io/"
+  // as a pattern string s, validateStringPatterns(v, s) (pattern.go:152-301) is "v is the string s, or a bool whose
+  // strconv.FormatBool is s": ASCII, no '|' '&' '*' '?', no leading / trailing blank, no operator prefix
+  // ('<' '>' '!'), no digit / sign / '.' first (range, duration and quantity forms). A foreach pattern leaf
+  // substituted from an element variable (L_DYN) is decided on the device only for such strings
+  SF_PLAIN = 1u << 15,
 };
 // bits 16..23 of a ruleset wildcard pattern's str_flags: its glob-mask index + 1 (0: none). The device holds one
 // bit per (dictionary string, masked pattern): wildcard.Match(pattern, string), evaluated once per batch
@@ -211,7 +216,11 @@ struct PEntry {         // 20 bytes
 constexpr uint32_t COL_TYPE_SHIFT = 28;
 constexpr uint32_t COL_INDEX_MASK = (1u << COL_TYPE_SHIFT) - 1;
 
-enum LeafType : uint8_t { L_NIL = 0, L_BOOL = 1, L_FLOAT = 2, L_STR = 3, L_MAP = 4, L_ARR = 5 };
+// L_DYN: a foreach pattern value that is exactly one element variable ({{element...}} / {{elementIndex}}); `exact`
+// holds its slot in the entry's dynamic-value list, resolved per element before the walk (vars.go:352-431 substitutes
+// a whole-string variable by its typed value)
+enum LeafType : uint8_t { L_NIL = 0, L_BOOL = 1, L_FLOAT = 2, L_STR = 3, L_MAP = 4, L_ARR = 5, L_DYN = 6 };
+constexpr uint32_t MAX_DYN = 4;  // element variables per foreach pattern entry (more -> CPU fallback)
 struct Leaf {           // 32 bytes
   uint8_t type;
   uint8_t bval;
@@ -399,9 +408,17 @@ enum RuleFlag : uint8_t { RD_GATE_EXACT = 1,    // match == the batch's kind gat
 // foreach validation (validation.go:319-421), RK_FOREACH: RuleDesc.root = pool offset of [n, entry offsets...];
 // an entry is [list operand (pool offset of a CondOperand copy), preconditions CondProg or NONE, deny CondProg,
 // elementScope (0 unset, 1 false, 2 true)]
+// foreach entry validator (validation.go:276-317 on the element's validator: deny > pattern / anyPattern > foreach)
+enum ForeachKind : uint32_t { FE_DENY = 0, FE_PATTERN = 1, FE_ANYPATTERN = 2, FE_NESTED = 3, FE_NONE = 4 };
 struct ForeachEntry {
   CondOperand list;
-  uint32_t pre, deny, scope, pad;
+  uint32_t pre, deny, scope;  // scope: 0 unset, 1 false, 2 true
+  uint32_t kind;              // ForeachKind
+  uint32_t body;              // FE_PATTERN: pattern root; FE_ANYPATTERN: pool offset of the roots; FE_NESTED: pool
+                              // offset of the nested entries ([n, entries...], as the rule's own list)
+  uint32_t nalts;             // FE_ANYPATTERN: alternatives
+  uint32_t dyn;               // pool offset of the element variables of its pattern(s): [n, (kind, nseg, segs...)...]
+                              // (kind 0: element path, 1: elementIndex), NONE without any
 };
 
 struct RuleDesc {

@@ -799,65 +799,169 @@ KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const R
 namespace kyv {
 
 
-// validateForEach (validation.go:319-341) + validateElements (:343-381) for deny entries: each element of the
-// evaluated list (evaluateList, utils.go:343-355: a non-list result is a one-element list; a query error skips
-// the entry) runs its preconditions (not met -> element skipped) and deny conditions (true -> the rule fails);
-// an error ends the rule only on the last element; no element applied -> skip.
-KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, uint32_t root, uint32_t row = NONE) {
-  const uint32_t nent = v.pool[root];
-  uint32_t applied = 0;
-  for (uint32_t e = 0; e < nent; e++) {
-    const ForeachEntry fe = *(const ForeachEntry*)(v.pool + root + 1 + e * (sizeof(ForeachEntry) / 4));
-    JList L;
-    JRes lr;
-    lr.lst = false; lr.cur = NONE; lr.lit = NONE; lr.num = NONE;
-    uint32_t miss = 0;
-    if (fe.list.kind == OK_PATH) {
-      uint32_t cur = 0;
-      bool nf = false;
-      for (uint32_t s = 0; s < fe.list.nseg && cur != NONE; s++) {
-        bool missing;
-        cur = j_field(R, cur, v.pool[fe.list.a + s], &missing);
-        if (missing) nf = true;
-      }
-      if (nf) continue;  // NotFoundError: "failed to evaluate list" -> next entry
-      lr.cur = cur;
-    } else {
-      const int st = jmes_run(v, R, fe.list, NONE, L, &lr, &miss);
-      if (st == JS_NOTFOUND) continue;
-      if (st == JS_FB || st == JS_ERR) return KYV_WHY(FBW_COND), ST_FALLBACK;
-      if (lr.lit != NONE || lr.num != NONE) return KYV_WHY(FBW_COND), ST_FALLBACK;  // literal / number: not restated
-    }
-    // elements: the projection list, an array's items, or the single value
-    const bool arr = !lr.lst && j_arr(R, lr.cur);
-    const uint32_t n = lr.lst ? L.n : arr ? R[lr.cur].b : 1u;
-    uint32_t count = 0;
-    for (uint32_t j = 0; j < n; j++) {
-      const uint32_t el = lr.lst ? L.e[j] : arr ? R[lr.cur].a + j : lr.cur;
-      if (el == NONE || (!(el & JMES_KEYBIT) && node_type(R[el]) == N_NULL)) continue;
-      if (fe.scope == 2 && !j_map(R, el)) return ST_ERROR | ST_MARK_SCOPE;  // addElementToContext error
-      uint32_t ec, es, eg;
-      bool err = false;
-      if (fe.pre != NONE) {
-        const int c = eval_prog(v, R, fe.pre, &ec, &es, &eg, el, row);
-        if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
-        if (c == CR_PANIC) return ST_PANIC;
-        if (c == CR_FALSE) continue;  // "preconditions not met": skip, not applied
-        err = c == CP_ERROR;
-      }
-      if (!err) {
-        const int c = eval_prog(v, R, fe.deny, &ec, &es, &eg, el, row);
-        if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
-        if (c == CR_PANIC) return ST_PANIC;
-        if (c == CR_TRUE) return ST_FAIL;
-        if (c != CP_ERROR) { count++; continue; }
-      }
-      if (j + 1 < n) continue;  // an error ends the rule only on the last element
-      return ST_ERROR;
-    }
-    applied += count;
+// validateForEach (validation.go:319-341) + validateElements (:343-381), nested foreach included: each element of
+// the evaluated list (evaluateList, utils.go:343-355: a non-list result is a one-element list; a query error skips the
+// entry) gets its own validator (newForEachValidator :242-275, validate :276-317): its preconditions (not met -> the
+// element is skipped), then deny conditions (true -> the rule fails), or a pattern / anyPattern (validatePatterns
+// :618-702 on the element when it is element-scoped -- a map, unless elementScope says otherwise (addElementToContext
+// :383-413) -- else on what the enclosing level validates: the resource at the top, the enclosing scoped element
+// inside a nested foreach, since PolicyContext.Copy keeps it), or a nested foreach over the element. A failing
+// element fails the rule; an error ends it only on the last element; a skipped element is not applied; no applied
+// element at all -> "rule skipped".
+// Element values enter patterns through the JSON context (numbers float64): an element variable of a pattern
+// (L_DYN) is resolved per element (a key missing on the way is the fork's NotFoundError -> the substitution fails:
+// an error for this element).
+struct FeCtx {
+  uint32_t el;    // enclosing element (node, JMES_KEYBIT key) or NONE at the top
+  uint32_t root;  // the node a non-scoped element's pattern validates
+};
+
+// the value of element variable `d` (pool: kind, nseg, segs...) for element `el` at list position `idx`; false when a
+// key is missing on the way (NotFoundError)
+KYV_HD bool fe_dyn_value(const View& v, NodeTab R, const uint32_t* d, uint32_t el, uint32_t idx, Val* out) {
+  if (d[0] == 1) {  // elementIndex: a number
+    *out = value_of(v, R, NONE);
+    out->t = N_FLOAT;
+    out->f = (double)idx;
+    return true;
   }
-  return applied ? ST_PASS : ST_SKIP;
+  uint32_t cur = el;
+  Val key{};
+  bool is_key = false;
+  for (uint32_t s = 0; s < d[1]; s++) {
+    if (cur == NONE || (cur & JMES_KEYBIT) || node_type(R[cur]) != N_MAP) { cur = NONE; break; }  // field of a non-map
+    const uint32_t x = map_find(R, cur, d[2 + s]);
+    if (x == NONE) return false;
+    cur = x;
+  }
+  if (cur != NONE && (cur & JMES_KEYBIT)) {  // the element is a map key (keys(@) list): a string
+    is_key = true;
+    key = value_of(v, R, NONE);
+    key.t = N_STR;
+    key.sid = key.wsid = key.nsid = node_key(R[cur & ~JMES_KEYBIT]);
+  }
+  *out = is_key ? key : value_of(v, R, cur);
+  if (out->t == 0xFF) out->t = N_NULL;  // a null value
+  return true;
+}
+
+// one entry list at nesting level D (levels beyond the compiled maximum never occur: the compiler keeps them on the
+// CPU engine)
+template <int D>
+KYV_HD uint8_t foreach_level(const View& v, NodeTab R, const RuleDesc& rd, uint32_t entries, FeCtx up, uint32_t row) {
+  if constexpr (D > 1) {
+    return KYV_WHY(FBW_COND), ST_FALLBACK;
+  } else {
+    const uint32_t nent = v.pool[entries];
+    uint32_t applied = 0;
+    for (uint32_t e = 0; e < nent; e++) {
+      const ForeachEntry fe = *(const ForeachEntry*)(v.pool + entries + 1 + e * (sizeof(ForeachEntry) / 4));
+      JList L;
+      JRes lr;
+      lr.lst = false; lr.cur = NONE; lr.lit = NONE; lr.num = NONE;
+      uint32_t miss = 0;
+      if (fe.list.kind == OK_PATH) {
+        uint32_t cur = 0;
+        bool nf = false;
+        for (uint32_t s = 0; s < fe.list.nseg && cur != NONE; s++) {
+          bool missing;
+          cur = j_field(R, cur, v.pool[fe.list.a + s], &missing);
+          if (missing) nf = true;
+        }
+        if (nf) continue;  // NotFoundError: "failed to evaluate list" -> next entry
+        lr.cur = cur;
+      } else {
+        const int st = jmes_run(v, R, fe.list, up.el, L, &lr, &miss);
+        if (st == JS_NOTFOUND) continue;
+        if (st == JS_FB || st == JS_ERR) return KYV_WHY(FBW_COND), ST_FALLBACK;
+        if (lr.lit != NONE || lr.num != NONE) return KYV_WHY(FBW_COND), ST_FALLBACK;  // literal / number: not restated
+      }
+      // elements: the projection list, an array's items, or the single value
+      const bool arr = !lr.lst && j_arr(R, lr.cur);
+      const uint32_t n = lr.lst ? L.n : arr ? R[lr.cur].b : 1u;
+      uint32_t count = 0;
+      for (uint32_t j = 0; j < n; j++) {
+        const uint32_t el = lr.lst ? L.e[j] : arr ? R[lr.cur].a + j : lr.cur;
+        if (el == NONE || (!(el & JMES_KEYBIT) && node_type(R[el]) == N_NULL)) continue;
+        const bool is_map = j_map(R, el);
+        if (fe.scope == 2 && !is_map) return ST_ERROR | ST_MARK_SCOPE;  // addElementToContext error
+        const bool scoped = fe.scope == 0 ? is_map : fe.scope == 2;
+        const uint32_t target = scoped ? el : up.root;
+        uint32_t ec, es, eg;
+        uint8_t r = ST_PASS;  // the element validator's response (ST_NONE: no validator)
+        bool err = false;
+        if (fe.pre != NONE) {
+          const int c = eval_prog(v, R, fe.pre, &ec, &es, &eg, el, row);
+          if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
+          if (c == CR_PANIC) return ST_PANIC;
+          if (c == CR_FALSE) continue;  // "preconditions not met": skip, not applied
+          err = c == CP_ERROR;
+        }
+        if (err) {
+          r = ST_ERROR;
+        } else if (fe.kind == FE_DENY) {
+          const int c = eval_prog(v, R, fe.deny, &ec, &es, &eg, el, row);
+          if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
+          if (c == CR_PANIC) return ST_PANIC;
+          r = c == CR_TRUE ? ST_FAIL : c == CP_ERROR ? ST_ERROR : ST_PASS;
+        } else if (fe.kind == FE_PATTERN || fe.kind == FE_ANYPATTERN) {
+          Val dyn[MAX_DYN];
+          bool subst_ok = true;
+          if (fe.dyn != NONE) {
+            const uint32_t nd = v.pool[fe.dyn];
+            uint32_t at = fe.dyn + 1;
+            for (uint32_t q = 0; q < nd && q < MAX_DYN && subst_ok; q++) {
+              subst_ok = fe_dyn_value(v, R, v.pool + at, el, j, &dyn[q]);
+              at += 2 + v.pool[at + 1];
+            }
+          }
+          if (!subst_ok) {
+            r = ST_ERROR;  // "variable substitution failed" (validation.go:294-297)
+          } else {
+            Frame frames[MAX_DEPTH];
+            const ResHeader& h = v.hdr[row];
+            const bool pat = fe.kind == FE_PATTERN;
+            const uint32_t nalts = pat ? 1u : fe.nalts;
+            uint32_t nfail = 0, nskip = 0;
+            r = ST_NONE;
+            for (uint32_t a = 0; a < nalts && r == ST_NONE; a++) {
+              PatOut po;
+              po.status = ST_NONE;
+              eval_pattern(v, pat ? fe.body : v.pool[fe.body + a], R, h, rd, Stack{frames, 1, MAX_DEPTH}, po, target,
+                           fe.dyn != NONE ? dyn : nullptr);
+              switch (po.status) {
+                case ST_PASS: r = ST_PASS; break;
+                case ST_SKIP: nskip++; break;
+                case ST_FAIL: nfail++; break;
+                case ST_ERROR: if (pat) r = ST_ERROR; else nfail++; break;  // anyPattern: a path-less error is a fail
+                default: return po.status;  // fallback / panic / nondeterministic
+              }
+            }
+            if (r == ST_NONE) r = nfail ? ST_FAIL : nskip ? ST_SKIP : (pat ? ST_FAIL : ST_PASS);
+          }
+        } else if (fe.kind == FE_NESTED) {
+          const uint8_t x = foreach_level<D + 1>(v, R, rd, fe.body, FeCtx{el, target}, row);
+          switch (x & 7) {
+            case ST_PASS: case ST_SKIP: case ST_FAIL: case ST_ERROR: r = x & 7; break;
+            default: return x;  // fallback / panic / nondeterministic
+          }
+        } else {
+          continue;  // no validator: "skip rule due to empty result"
+        }
+        if (r == ST_SKIP) continue;
+        if (r == ST_PASS) { count++; continue; }
+        if (r == ST_FAIL) return ST_FAIL;
+        if (j + 1 < n) continue;  // an error ends the rule only on the last element
+        return ST_ERROR;
+      }
+      applied += count;
+    }
+    return applied ? ST_PASS : ST_SKIP;
+  }
+}
+
+KYV_HD uint8_t eval_foreach(const View& v, NodeTab R, const RuleDesc& rd, uint32_t row = NONE) {
+  return foreach_level<0>(v, R, rd, rd.root, FeCtx{NONE, 0u}, row);
 }
 
 // The match part of pair_dispatch (validation.go:134-183, matches with the OldResource retry :600-615): false with
@@ -926,7 +1030,7 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
     }
     case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails, r);
     case RK_FOREACH:
-      if constexpr (kJ) return eval_foreach(v, R, rd.root, r);
+      if constexpr (kJ) return eval_foreach(v, R, rd, r);
       else return ST_FALLBACK;
     case RK_PATTERN: case RK_ANYPATTERN:
       if (h.flags & RF_MAGIC) return KYV_WHY(FBW_PHRASE), ST_FALLBACK;

@@ -676,27 +676,83 @@ static bool contains_braces(const VP& v) {
   return false;
 }
 
-// foreach entries the restatement covers: a JMESPath-subset list and deny conditions (+ per-element preconditions,
-// elementScope) over request.object / element; patterns, nested foreach and context entries are not restated
-static bool foreach_supported(const VP& val) {
-  VP fe = val->get("foreach");
-  if (!fe || fe->t != T::Arr) return false;
+// ---------------------------------------------------------------- foreach (validation.go:242-421)
+// A pattern string that is exactly one element variable: `{{element}}`, `{{element.<ident>...}}` or `{{elementIndex}}`
+// (the innermost element; vars.go:352-431 substitutes a whole-string variable by its typed value) -> its dotted path
+// after "element" ("" for the element itself) or "#" for elementIndex
+static bool element_var(const std::string& s, std::string* path) {
+  if (s.size() < 4 || s.compare(0, 2, "{{") != 0 || s.compare(s.size() - 2, 2, "}}") != 0) return false;
+  std::string in = s.substr(2, s.size() - 4);
+  if (in.find('{') != std::string::npos || in.find('}') != std::string::npos) return false;
+  in = gou::trim_space(in);
+  if (in == "elementIndex") { *path = "#"; return true; }
+  if (in.compare(0, 7, "element") != 0) return false;
+  std::string rest = in.substr(7);
+  if (!rest.empty() && rest[0] != '.') return false;
+  // identifiers only: [A-Za-z_][A-Za-z0-9_]* separated by dots
+  for (size_t i = 0; i < rest.size();) {
+    if (rest[i] != '.') return false;
+    size_t j = i + 1;
+    if (j >= rest.size() || !(isalpha((unsigned char)rest[j]) || rest[j] == '_')) return false;
+    while (j < rest.size() && (isalnum((unsigned char)rest[j]) || rest[j] == '_')) j++;
+    i = j;
+  }
+  *path = rest;
+  return true;
+}
+
+// a foreach pattern / anyPattern whose only variables are whole-string element variables in values
+static bool foreach_pattern_ok(const VP& p) {
+  if (!p) return true;
+  if (p->t == T::Str) {
+    if (p->s.find("$(") != std::string::npos) return false;
+    if (p->s.find("{{") == std::string::npos) return true;
+    std::string path;
+    return element_var(p->s, &path);
+  }
+  if (p->t == T::Arr) { for (auto& e : p->a) if (!foreach_pattern_ok(e)) return false; return true; }
+  if (p->t == T::Obj)
+    for (auto& kv : p->o) {
+      if (kv.first.find("{{") != std::string::npos || kv.first.find("$(") != std::string::npos) return false;
+      if (!foreach_pattern_ok(kv.second)) return false;
+    }
+  return true;
+}
+
+// foreach entries the restatement covers: a JMESPath-subset list (over request.object, and over the enclosing
+// element inside a nested foreach), per-element preconditions / elementScope, and one of deny conditions, pattern,
+// anyPattern (element variables as whole-string values) or a nested foreach (one level); context entries and other
+// variables are not restated
+static bool foreach_entries_supported(const VP& fe, int depth) {
+  if (!fe || fe->t != T::Arr || depth > 1) return false;
   for (auto& e : fe->a) {
     if (!e || e->t != T::Obj) return false;
     for (auto& kv : e->o)
-      if (kv.first != "list" && kv.first != "deny" && kv.first != "preconditions" && kv.first != "elementScope")
+      if (kv.first != "list" && kv.first != "deny" && kv.first != "preconditions" && kv.first != "elementScope" &&
+          kv.first != "pattern" && kv.first != "anyPattern" && kv.first != "foreach")
         return false;
     VP l = e->get("list");
-    if (!l || l->t != T::Str || !jmes_supported(l->s, false)) return false;
+    if (!l || l->t != T::Str || !jmes_supported(l->s, depth > 0)) return false;
     VP d = e->get("deny");
-    if (isnil(d) || d->t != T::Obj || !conditions_supported_element(d->get("conditions"))) return false;
+    if (!isnil(d)) {
+      if (d->t != T::Obj || !conditions_supported_element(d->get("conditions"))) return false;
+    } else if (!isnil(e->get("pattern")) || !isnil(e->get("anyPattern"))) {
+      if (!foreach_pattern_ok(e->get("pattern")) || !foreach_pattern_ok(e->get("anyPattern"))) return false;
+      VP ap = e->get("anyPattern");
+      if (isnil(e->get("pattern")) && ap->t != T::Arr) return false;
+    } else if (has_nonempty(e, "foreach")) {
+      if (!foreach_entries_supported(e->get("foreach"), depth + 1)) return false;
+    }
     if (!conditions_supported_element(e->get("preconditions"))) return false;
     VP es = e->get("elementScope");
     if (!isnil(es) && es->t != T::Bool) return false;
-    std::string msg = oj::get_str(val, "message");
-    if (msg.find("{{") != std::string::npos || msg.find("$(") != std::string::npos) return false;
   }
   return true;
+}
+static bool foreach_supported(const VP& val) {
+  std::string msg = oj::get_str(val, "message");
+  if (msg.find("{{") != std::string::npos || msg.find("$(") != std::string::npos) return false;
+  return foreach_entries_supported(val->get("foreach"), 0);
 }
 
 // Go %T of a decoded JSON element (addElementToContext error text, validation.go:395-397)
@@ -712,17 +768,106 @@ static std::string go_type_name(const VP& v) {
   }
 }
 
-// validateForEach (validation.go:319-341) + validateElements (:343-381) for deny entries: every element of the
-// evaluated list runs its own validator (preconditions -> skip; deny -> fail / pass; errors), fail ends the rule,
-// an error ends it only on the last element, no applied element at all -> "rule skipped"
-static RuleResult validate_foreach(const VP& rule, const VP& resource, RuleResult out) {
+static std::string build_error_message(const std::string& rname, const std::string& msg0, const std::string& err, const std::string& path);
+
+// substitutePatterns (validation.go:760-782) of a foreach pattern: every whole-string element variable replaced by
+// its typed value from the JSON context (numbers float64); a key missing on the way is the fork's NotFoundError
+static VP subst_element_vars(const VP& p, const VP& el, int64_t idx, std::string* err) {
+  if (!p || !err->empty()) return p;
+  if (p->t == T::Str) {
+    std::string path;
+    if (!element_var(p->s, &path)) return p;
+    if (path == "#") return Value::flt((double)idx);
+    VP cur = json_floats(el);
+    size_t i = 0;
+    while (i < path.size()) {
+      size_t j = path.find('.', i + 1);
+      const std::string k = path.substr(i + 1, (j == std::string::npos ? path.size() : j) - i - 1);
+      if (!cur || cur->t != T::Obj) { cur = Value::null(); break; }
+      if (!cur->has(k)) { *err = "Unknown key \"" + k + "\" in path"; return p; }
+      cur = cur->get(k);
+      i = j == std::string::npos ? path.size() : j;
+    }
+    return cur ? cur : Value::null();
+  }
+  if (p->t == T::Arr) {
+    auto o = Value::arr();
+    for (auto& e : p->a) o->a.push_back(subst_element_vars(e, el, idx, err));
+    return o;
+  }
+  if (p->t == T::Obj) {
+    auto o = Value::obj();
+    for (auto& kv : p->o) o->o[kv.first] = subst_element_vars(kv.second, el, idx, err);
+    return o;
+  }
+  return p;
+}
+
+// validatePatterns (validation.go:618-702) of a pattern / anyPattern against `target`: the response status and message
+static RuleResult pattern_response(const std::string& rname, const std::string& msg, const VP& pattern, const VP& any_pattern,
+                                   const VP& target) {
+  RuleResult out;
+  out.name = rname;
+  if (!isnil(pattern)) {
+    EvalFlags fl;
+    PatternResult pr = match_pattern(target, pattern, fl);
+    out.nondeterministic |= fl.nondeterministic;
+    if (pr.ok) { out.status = "pass"; out.message = "validation rule '" + rname + "' passed."; return out; }
+    if (pr.skip) { out.status = "skip"; out.message = pr.err; return out; }
+    if (pr.path.empty()) { out.status = "error"; out.message = build_error_message(rname, msg, pr.err, ""); return out; }
+    out.status = "fail";
+    out.path = pr.path;
+    out.message = build_error_message(rname, msg, pr.err, pr.path);
+    return out;
+  }
+  std::vector<std::string> failed, skipped;
+  for (size_t idx = 0; idx < any_pattern->a.size(); idx++) {
+    EvalFlags fl;
+    PatternResult pr = match_pattern(target, any_pattern->a[idx], fl);
+    out.nondeterministic |= fl.nondeterministic;
+    if (pr.ok) {
+      out.status = "pass";
+      out.message = "validation rule '" + rname + "' anyPattern[" + std::to_string(idx) + "] passed.";
+      return out;
+    }
+    std::string pre = "rule " + rname + "[" + std::to_string(idx) + "]";
+    if (pr.skip) skipped.push_back(pre + " skipped: " + pr.err);
+    else if (pr.path.empty()) failed.push_back(pre + " failed: " + pr.err);
+    else failed.push_back(pre + " failed at path " + pr.path);
+  }
+  if (!skipped.empty() && failed.empty()) {
+    out.status = "skip";
+    for (size_t i = 0; i < skipped.size(); i++) out.message += (i ? " " : "") + skipped[i];
+    return out;
+  }
+  if (!failed.empty()) {
+    std::string s;
+    for (size_t i = 0; i < failed.size(); i++) { if (i) s += " "; s += failed[i]; }
+    out.status = "fail";
+    if (msg.empty()) out.message = "validation error: " + s;
+    else if (msg.back() == '.') out.message = "validation error: " + msg + " " + s;
+    else out.message = "validation error: " + msg + ". " + s;
+    return out;
+  }
+  out.status = "pass";
+  out.message = msg;
+  return out;
+}
+
+// validateForEach (validation.go:319-341) over the entries `fes` at nesting level `depth`: `el` / `idx` the enclosing
+// element (null at the top), `root` what a pattern validates when the element is not element-scoped (the resource at
+// the top -- NewResource, integers int64 --, else the enclosing scoped element: PolicyContext.Copy keeps it)
+static RuleResult foreach_level(const VP& rule, const VP& fes, const VP& resource, const VP& el, int64_t idx, const VP& root,
+                                int depth) {
   VP val = rule->get("validate");
   const std::string msg = oj::get_str(val, "message");
+  RuleResult out;
+  out.name = oj::get_str(rule, "name");
   int applyCount = 0;
-  for (auto& fe : val->get("foreach")->a) {
+  for (auto& fe : fes->a) {
     VP list;
     try {
-      list = jmes_query(fe->get("list")->s, resource, nullptr, 0);  // evaluateList (utils.go:343-355)
+      list = jmes_query(fe->get("list")->s, resource, el, idx);  // evaluateList (utils.go:343-355)
     } catch (JmesNotFound&) {
       continue;
     } catch (JmesError&) {
@@ -732,42 +877,67 @@ static RuleResult validate_foreach(const VP& rule, const VP& resource, RuleResul
     if (list && list->t == T::Arr) elements = list->a; else elements.push_back(list);
     VP scope = fe->get("elementScope");
     int count = 0;
-    for (size_t idx = 0; idx < elements.size(); idx++) {
-      const VP& el = elements[idx];
-      if (isnil(el)) continue;
-      if (!isnil(scope) && scope->b && el->t != T::Obj) {
+    // validateElements (validation.go:343-381)
+    for (size_t i = 0; i < elements.size(); i++) {
+      const VP& e = elements[i];
+      if (isnil(e)) continue;
+      if (!isnil(scope) && scope->b && e->t != T::Obj) {  // addElementToContext error: ruleError, returned as is
         out.status = "error";
         out.message = "failed to process foreach: cannot use elementScope=true foreach rules for elements that are not "
-                      "maps, expected type=map got type=" + go_type_name(el);
+                      "maps, expected type=map got type=" + go_type_name(e);
         return out;
       }
-      std::string st, m;
-      CondResult pc = eval_conditions_element(fe->get("preconditions"), resource, el, (int64_t)idx);
+      const bool scoped = isnil(scope) ? e->t == T::Obj : scope->b;
+      const VP target = scoped ? json_floats(e) : root;
+      // the element's own validator (validate(), validation.go:276-317): preconditions, then deny / pattern / foreach
+      RuleResult r;
+      bool have = true;
+      CondResult pc = eval_conditions_element(fe->get("preconditions"), resource, e, (int64_t)i);
       if (pc.r == CondOutcome::Unsupported) { out.status = "unsupported"; out.message = "foreach preconditions"; return out; }
       if (pc.r == CondOutcome::Error) {
-        st = "error";
-        m = "failed to evaluate preconditions: failed to substitute variables in preconditions: " + pc.err;
+        r.status = "error";
+        r.message = "failed to evaluate preconditions: failed to substitute variables in preconditions: " + pc.err;
         out.message_unpinned |= pc.err_unpinned;
       } else if (pc.r == CondOutcome::False) {
-        continue;  // "preconditions not met" -> skip
-      } else {
-        CondResult c = eval_conditions_element(fe->get("deny")->get("conditions"), resource, el, (int64_t)idx);
+        r.status = "skip";  // "preconditions not met"
+      } else if (!isnil(fe->get("deny"))) {
+        CondResult c = eval_conditions_element(fe->get("deny")->get("conditions"), resource, e, (int64_t)i);
         if (c.r == CondOutcome::Unsupported) { out.status = "unsupported"; out.message = "foreach deny"; return out; }
         if (c.r == CondOutcome::Error) {
-          st = "error";
-          m = "failed to substitute variables in deny conditions: " + c.err;
+          r.status = "error";
+          r.message = "failed to substitute variables in deny conditions: " + c.err;
           out.message_unpinned |= c.err_unpinned;
         } else if (c.r == CondOutcome::True) {
-          st = "fail";
-          m = msg.empty() ? "validation error: rule " + out.name + " failed" : msg;
+          r.status = "fail";
+          r.message = msg.empty() ? "validation error: rule " + out.name + " failed" : msg;
         } else {
-          count++;
-          continue;
+          r.status = "pass";
         }
+      } else if (!isnil(fe->get("pattern")) || !isnil(fe->get("anyPattern"))) {
+        std::string err;
+        VP pat = subst_element_vars(fe->get("pattern"), e, (int64_t)i, &err);
+        VP ap = subst_element_vars(fe->get("anyPattern"), e, (int64_t)i, &err);
+        if (!err.empty()) {
+          r.status = "error";
+          r.message = "variable substitution failed: " + err;
+          out.message_unpinned = true;  // the fork's NotFoundError text is not pinned by a fixture
+        } else {
+          r = pattern_response(out.name, msg, pat, ap, target);
+          out.nondeterministic |= r.nondeterministic;
+        }
+      } else if (has_nonempty(fe, "foreach")) {
+        r = foreach_level(rule, fe->get("foreach"), resource, e, (int64_t)i, target, depth + 1);
+        if (r.status == "unsupported") return r;
+        out.nondeterministic |= r.nondeterministic;
+        out.message_unpinned |= r.message_unpinned;
+      } else {
+        have = false;  // no validator: "skip rule due to empty result"
       }
-      if (st == "error" && idx + 1 < elements.size()) continue;
-      out.status = st;
-      out.message = "validation failure: " + m;
+      if (!have || r.status == "skip") continue;
+      if (r.status == "pass") { count++; continue; }
+      if (r.status == "error" && i + 1 < elements.size()) continue;  // an error ends it only on the last element
+      out.status = r.status;
+      out.message = "validation failure: " + r.message;
       return out;
     }
     applyCount += count;
@@ -776,6 +946,12 @@ static RuleResult validate_foreach(const VP& rule, const VP& resource, RuleResul
   out.status = "pass";
   out.message = "rule passed";
   return out;
+}
+
+static RuleResult validate_foreach(const VP& rule, const VP& resource, RuleResult out) {
+  RuleResult r = foreach_level(rule, rule->get("validate")->get("foreach"), resource, nullptr, 0, resource, 0);
+  r.name = out.name;
+  return r;
 }
 
 std::string rule_unsupported_reason(const VP& rule) {

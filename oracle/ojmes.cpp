@@ -269,6 +269,8 @@ VP floats(const VP& v) {  // encoding/json decode of the JSON context: every num
 
 }  // namespace
 
+VP json_floats(const VP& v) { return floats(v); }
+
 // every node within the restated interpreter (functions: keys(@) and length())
 static bool nodes_ok(const NP& n) {
   if (n->k == NFunction && !(n->name == "length" && n->kids.size() == 1) &&

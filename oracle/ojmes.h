@@ -30,4 +30,7 @@ bool jmes_supported(const std::string& expr, bool allow_element);
 // nullptr outside foreach. Throws JmesNotFound / JmesError / JmesUnsupported.
 oj::VP jmes_query(const std::string& expr, const oj::VP& resource, const oj::VP& element, int64_t index);
 
+// the JSON context's view of a value (encoding/json: every number float64), e.g. a foreach element
+oj::VP json_floats(const oj::VP& v);
+
 }  // namespace orc

@@ -12,7 +12,7 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "liboracle.so")
+_LIB = os.environ.get("KYV_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")  # override: development builds only
 _lib = None
 
 
