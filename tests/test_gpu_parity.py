@@ -277,10 +277,12 @@ def test_pss_with_preconditions_gpu_equals_cpu(jit):
         g = E.evaluate(rs, b, backend="gpu", jit=jit)
         c = E.evaluate(rs, b, backend="cpu")
         assert np.array_equal(g.raw, c.raw)
+        nfail = 0
         for k, r in enumerate(rs.rules):
             if r["kind"] != "podSecurity":
                 continue
             fails = np.nonzero(np.asarray(g.status[k]) == K.ST_FAIL)[0]
-            assert len(fails) > 0
+            nfail += len(fails)
             for i in fails[:: max(1, len(fails) // 200)].tolist():
                 assert g.pss_mask(i, k) == c.pss_mask(i, k), (r["name"], i)
+        assert nfail > 0
