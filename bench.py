@@ -244,8 +244,7 @@ def compare_verdicts(rs, names, m, st, n):
 def timed_prefix_status(batch, device, cap):
     """the timed evaluation's OWN verdicts for the first `cap` input-order resources of the batch (resident on the
     device after the last timed step: kind-major order and every rule slice included), copied back for parity"""
-    from kyverno_amd import scan
-    return scan.local_verdicts_device(batch, device="cuda:%d" % device, ncols=cap)
+    return batch.resident_status(device=device, res0=0, nres=min(cap, batch.n))
 
 
 def cpu_baseline_and_parity(policies, rs, data, nsl, jit, timed_status, target_s=10.0, cap=400000, device=0):
@@ -453,11 +452,15 @@ def main():
                     help="total resources over all GPUs (default 10M c3, 1M c2 / c4 / c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (flatten + H2D + eval + D2H) leg")
-    ap.add_argument("--no-gather", action="store_true", help="skip the timed RCCL all-gather of the resident results")
+    ap.add_argument("--gather", action="store_true",
+                    help="time the RCCL all-gather of the resident results (loads torch first: KYV_TORCH_FIRST)")
+    ap.add_argument("--no-gather", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         spawn_ranks(args.gpus)
 
+    if args.gather:  # torch.distributed's RCCL needs torch's HIP runtime loaded before the library's (_lib.py)
+        os.environ["KYV_TORCH_FIRST"] = "1"
     from kyverno_amd import engine as E
     from kyverno_amd import synth
 
@@ -534,7 +537,7 @@ def main():
     # report assembly of a multi-GPU scan: RCCL all-gather of every rank's verdicts and failing-path
     # rows straight from the device-resident results of the last timed evaluation, timed after the evaluation
     gathers = None
-    if not args.no_gather:
+    if args.gather:
         gathers = time_gathers(batch, local, rank, world)
         log("rank %d: device-resident gathers %s" % (rank, gathers))
 

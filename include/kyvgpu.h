@@ -220,6 +220,10 @@ int64_t kyv_results_failures(const kyv_results* r, kyv_failure* out, size_t cap)
  *   idx[4]) of every failing-path record; returns the row count (dst NULL: only the count), -1 on error or when
  *   the evaluation was rule-sliced (its records are gathered on the host: use kyv_results_failures). */
 int64_t kyv_batch_export_status(const kyv_batch* b, int device, uint8_t* dst, size_t cap, void* stream);
+/* the verdict bytes (KYV_ST_*, marks cleared) of input-order resources [res0, res0 + nres) of every rule, rule-major
+ * [rules][nres], from the batch's last GPU evaluation on `device` into HOST memory (a parity check of that very
+ * evaluation, no re-run); returns the byte count (dst NULL: only the count), -1 on error */
+int64_t kyv_batch_copy_status(const kyv_batch* b, int device, uint64_t res0, uint64_t nres, uint8_t* dst, size_t cap);
 int64_t kyv_batch_export_failures(const kyv_batch* b, int device, int64_t res_offset, int64_t* dst, size_t cap_rows,
                                   void* stream);
 /* failing path of a single-pattern FAIL ("" otherwise); returns the full length */

@@ -61,7 +61,7 @@ EXPORTS = [
     "kyv_results_pss_mask", "kyv_last_error", "kyv_version", "kyv_results_jit", "kyv_ruleset_jit_source",
     "kyv_ruleset_jit_compile", "kyv_ruleset_jit_compile_ex", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
     "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures", "kyv_ruleset_rule_flags",
-    "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase", "kyv_results_alg_bytes_class", "kyv_batch_export_status",
+    "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase", "kyv_results_alg_bytes_class", "kyv_batch_export_status", "kyv_batch_copy_status",
     "kyv_batch_export_failures",
 ]
 
@@ -100,6 +100,8 @@ def lib():
     L.kyv_results_failures.restype = i64
     L.kyv_batch_export_status.argtypes = [vp, ctypes.c_int, vp, sz, vp]
     L.kyv_batch_export_status.restype = i64
+    L.kyv_batch_copy_status.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp, sz]
+    L.kyv_batch_copy_status.restype = i64
     L.kyv_batch_export_failures.argtypes = [vp, ctypes.c_int, i64, vp, sz, vp]
     L.kyv_batch_export_failures.restype = i64
     L.kyv_ruleset_rule_flags.argtypes = [vp, u32]

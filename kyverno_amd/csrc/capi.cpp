@@ -22,6 +22,7 @@ bool pattern_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uint32_
                         std::string* path, std::string* text);
 int64_t export_status(const Batch& b, int device, uint8_t* dst, size_t cap, void* stream);
 int64_t export_failures(const Batch& b, int device, int64_t off, int64_t* dst, size_t cap_rows, void* stream);
+int64_t copy_status(const Batch& b, int device, size_t res0, size_t n, uint8_t* host_dst, size_t cap);
 bool pss_checks_render(const Ruleset& rs, const Batch& b, uint32_t pos, uint32_t rule, uint32_t mask,
                        std::vector<std::array<std::string, 3>>* out);
 }  // namespace kyv
@@ -289,6 +290,15 @@ int64_t kyv_batch_export_status(const kyv_batch* b, int device, uint8_t* dst, si
   if (!b) return fail(KYV_EINVAL, "null argument"), -1;
   try {
     return export_status(*b->b, device, dst, cap, stream);
+  } catch (std::exception& e) {
+    return fail(KYV_EINVAL, e.what()), -1;
+  }
+}
+
+int64_t kyv_batch_copy_status(const kyv_batch* b, int device, uint64_t res0, uint64_t nres, uint8_t* dst, size_t cap) {
+  if (!b) return fail(KYV_EINVAL, "null argument"), -1;
+  try {
+    return copy_status(*b->b, device, (size_t)res0, (size_t)nres, dst, cap);
   } catch (std::exception& e) {
     return fail(KYV_EINVAL, e.what()), -1;
   }

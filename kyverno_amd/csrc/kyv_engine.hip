@@ -1756,6 +1756,38 @@ int64_t export_status(const Batch& b, int device, uint8_t* dst, size_t cap, void
   return (int64_t)total;
 }
 
+// verdict bytes of input-order resources [res0, res0 + n) of every rule, rule-major, gathered on the device from the
+// resident (kind-major) rows
+__global__ void __launch_bounds__(256) status_rows_kernel(const uint8_t* __restrict__ status, const uint32_t* __restrict__ inv,
+                                                          size_t nres, size_t res0, size_t n, size_t total,
+                                                          uint8_t* __restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const size_t k = i / n, j = i - k * n;
+  dst[i] = status[k * nres + inv[res0 + j]] & 7u;
+}
+
+int64_t copy_status(const Batch& b, int device, size_t res0, size_t n, uint8_t* host_dst, size_t cap) {
+  DevBatch* db = resident(b, device);
+  const DeviceResults& d = *db->out;
+  if (res0 > d.nres) throw std::runtime_error("resource range out of bounds");
+  n = std::min(n, d.nres - res0);
+  const size_t total = n * d.nrules;
+  if (!host_dst) return (int64_t)total;
+  if (cap < total) throw std::runtime_error("status buffer too small");
+  if (total) {
+    uint8_t* tmp = nullptr;
+    HIP_OK(dmalloc(&tmp, total));
+    hipLaunchKernelGGL(status_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, d.stream,
+                       (const uint8_t*)d.status, (const uint32_t*)db->inv, d.nres, res0, n, total, tmp);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(host_dst, tmp, total, hipMemcpyDeviceToHost, d.stream));
+    HIP_OK(hipStreamSynchronize(d.stream));
+    dfree(tmp);
+  }
+  return (int64_t)total;
+}
+
 int64_t export_failures(const Batch& b, int device, int64_t off, int64_t* dst, size_t cap_rows, void* stream) {
   DevBatch* db = resident(b, device);
   const DeviceResults& d = *db->out;

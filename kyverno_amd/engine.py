@@ -96,6 +96,20 @@ class Batch:
         self.ruleset = ruleset
         self.n = L.kyv_batch_num_resources(h)
 
+    def resident_status(self, device=0, res0=0, nres=None):
+        """uint8 [rules, nres] KYV_ST_* verdicts of input-order resources [res0, res0 + nres) as the batch's last GPU
+        evaluation left them on `device` (kyv_batch_copy_status: no re-evaluation)"""
+        L = K.lib()
+        nres = self.n - res0 if nres is None else nres
+        total = L.kyv_batch_copy_status(self.h, device, res0, nres, None, 0)
+        if total < 0:
+            raise K.KyvError(L.kyv_last_error().decode(errors="replace"))
+        out = np.empty(max(1, total), dtype=np.uint8)
+        if L.kyv_batch_copy_status(self.h, device, res0, nres, out.ctypes.data, out.size) < 0:
+            raise K.KyvError(L.kyv_last_error().decode(errors="replace"))
+        nr = len(self.ruleset.rules)
+        return out[:total].reshape(nr, total // max(1, nr))
+
     def stats(self):
         s = K.BatchStats()
         K.check(K.lib().kyv_batch_stats_get(self.h, ctypes.byref(s)))
