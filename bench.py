@@ -323,7 +323,7 @@ def shard_parity(policies, rs, data, nsl, timed_status, cap=100000):
 
 
 # device phase -> kernel-name prefixes of that phase in a rocprofv3 kernel trace
-PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::pss_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv::walk_kernel"),
+PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::pss_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv::walk_kernel"),
                  "compact": ("kyv::compact",), "hist": ("kyv::status_hist",)}
 
 
@@ -452,6 +452,9 @@ def main():
                     help="total resources over all GPUs (default 10M c3, 1M c2 / c4 / c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (flatten + H2D + eval + D2H) leg")
+    ap.add_argument("--no-account", action="store_true",
+                    help="profiling runs: skip the byte-accounting evaluation (its kernels share the product's names)")
+    ap.add_argument("--no-serial", action="store_true", help="profiling runs: skip the serialised phase-time evaluations")
     ap.add_argument("--gather", action="store_true",
                     help="time the RCCL all-gather of the resident results (loads torch first: KYV_TORCH_FIRST)")
     ap.add_argument("--no-gather", action="store_true", help=argparse.SUPPRESS)
@@ -499,12 +502,15 @@ def main():
     # with the byte-accounting build of the same kernels (KYV_ACCT: every per-resource load and result store adds its
     # bytes to device counters), phases serialised so each phase's bytes are its own; outside the timed region
     t0 = time.time()
-    acct = E.evaluate(rs, batch, backend="gpu", device=local, copy_back=False, account_bytes=True, jit=timed_jit)
-    phase_bytes = dict(acct.alg_bytes_phase)
-    alg_class = dict(acct.alg_bytes_class)
-    bytes_per_eval = acct.alg_bytes / max(1, pairs)
-    acct_counts_ok = acct.counts == counts  # the accounting build decides every pair as the product build does
-    del acct
+    if args.no_account:
+        phase_bytes, alg_class, bytes_per_eval, acct_counts_ok = dict.fromkeys(PHASE_KERNELS, 0), {}, 0.0, None
+    else:
+        acct = E.evaluate(rs, batch, backend="gpu", device=local, copy_back=False, account_bytes=True, jit=timed_jit)
+        phase_bytes = dict(acct.alg_bytes_phase)
+        alg_class = dict(acct.alg_bytes_class)
+        bytes_per_eval = acct.alg_bytes / max(1, pairs)
+        acct_counts_ok = acct.counts == counts  # the accounting build decides every pair as the product build does
+        del acct
     log("rank %d: %.1f algorithmic bytes per eval (device-counted over the shard, %.1f s): %s" % (
         rank, bytes_per_eval, time.time() - t0, phase_bytes))
 
@@ -522,7 +528,20 @@ def main():
     dt_max = all_max(pg, dt)
     kernel_ms = kms / max(1, args.steps)
     kernel_ms_max = all_max(pg, kernel_ms)
-    phase = {k: v / max(1, args.steps) for k, v in phase.items()}
+    phase_span = {k: v / max(1, args.steps) for k, v in phase.items()}
+    # per-phase kernel times for the roofline: evaluations with every phase on one stream (in the timed evaluations
+    # the compiled condition kernels run beside the walk, so their phase times are overlapping spans)
+    nser = 0 if args.no_serial else max(3, min(10, args.steps))
+    phase = dict.fromkeys(PHASE_KERNELS, 0.0)
+    ser_ms = 0.0
+    for _ in range(nser):
+        r = E.evaluate(rs, batch, backend="gpu", device=local, copy_back=False, serial=True)
+        ser_ms += r.kernel_ms
+        for k in phase:
+            phase[k] += r.phase_ms[k] / nser
+    ser_ms /= max(1, nser)
+    if not nser:
+        phase = dict(phase_span)
     # pairs the device decided: every (resource, compiled rule) pair except those it hands to the CPU engine
     # (FALLBACK / PANIC / ND: rules or pairs outside the GPU subset, counted separately, not in `value`)
     cpu_pairs = int(sum(counts.get(s, 0) for s in CPU_STATUSES))
@@ -638,10 +657,13 @@ def main():
                          "phase_frac": phase_frac,
                          "alg_bytes_by_class": alg_class,
                          "accounting_verdicts_match": acct_counts_ok,
-                         "overlap": "the compiled condition kernels run on a second HIP stream concurrently with the "
-                                    "walk (kyv_engine.hip cstream): phase times are spans under that overlap, their "
-                                    "sum exceeds evaluation_ms; evaluation_frac is the whole evaluation's figure",
+                         "overlap": "timed evaluations run the compiled condition kernels on a second HIP stream "
+                                    "concurrently with the walk (phase_ms_span: spans under that overlap); kernel_ms / "
+                                    "phase_ms come from %d serialised evaluations (KYV_EVAL_SERIAL: %.3f ms each), "
+                                    "evaluation_frac is the timed (overlapped) evaluation's figure" % (nser, ser_ms),
                          "phase_ms": phase,
+                         "phase_ms_span": phase_span,
+                         "serial_evaluation_ms": ser_ms,
                          "phase_alg_bytes": phase_bytes,
                          "evaluation_ms": kernel_ms,
                          "evaluation_ms_max_rank": kernel_ms_max,

@@ -76,7 +76,10 @@ enum { KYV_BACKEND_GPU = 0, KYV_BACKEND_CPU = 1 };
 enum { KYV_EVAL_NO_COPYBACK = 1u, KYV_EVAL_ACCOUNT_BYTES = 2u,
        /* GPU backend: pattern walks run in a kernel generated and compiled (hipRTC, gfx950) for this ruleset
           on first use; default = on for batches of >= 65536 resources, else the interpreted walk kernel */
-       KYV_EVAL_JIT_OFF = 4u, KYV_EVAL_JIT_ON = 8u };
+       KYV_EVAL_JIT_OFF = 4u, KYV_EVAL_JIT_ON = 8u,
+       /* GPU backend: every phase on the evaluation stream (no concurrent condition stream), so the per-phase times
+          (kyv_results_phase_ms) are each phase's own kernels, not spans under overlap */
+       KYV_EVAL_SERIAL = 16u };
 
 /* compile flags (kyv_compile_opts.flags) */
 enum { KYV_COMPILE_BACKGROUND = 1u };  /* the ruleset serves background scans only (empty AdmissionInfo, scanner.go:60-110):

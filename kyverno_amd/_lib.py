@@ -12,6 +12,7 @@ EVAL_NO_COPYBACK = 1
 EVAL_ACCOUNT_BYTES = 2
 EVAL_JIT_OFF = 4
 EVAL_JIT_ON = 8
+EVAL_SERIAL = 16
 
 ST_NONE, ST_PASS, ST_FAIL, ST_SKIP, ST_ERROR, ST_FALLBACK, ST_PANIC, ST_ND = range(8)
 STATUS_NAMES = ["none", "pass", "fail", "skip", "error", "fallback", "panic", "nondeterministic"]

@@ -14,7 +14,7 @@
 
 namespace kyv {
 void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back,
-              int jit_mode, bool account);
+              int jit_mode, bool account, bool serial);
 void eval_cpu(const Ruleset& rs, const Batch& b, int threads, Results* out, bool account);
 void free_device_images(Ruleset& rs, Batch* b);
 std::string fallback_why(const Ruleset& rs, const Batch& b, uint32_t res, uint32_t rule);
@@ -240,7 +240,8 @@ int kyv_eval(const kyv_ruleset* rs, const kyv_batch* b, const kyv_eval_opts* opt
       bool copy = !(opts && (opts->flags & KYV_EVAL_NO_COPYBACK));
       double ms = 0;
       int jm = !opts ? JIT_AUTO : (opts->flags & KYV_EVAL_JIT_OFF) ? JIT_OFF : (opts->flags & KYV_EVAL_JIT_ON) ? JIT_ON : JIT_AUTO;
-      eval_gpu(*rs->rs, *b->b, dev, iters, &res->r, &ms, copy, jm, opts && (opts->flags & KYV_EVAL_ACCOUNT_BYTES));
+      eval_gpu(*rs->rs, *b->b, dev, iters, &res->r, &ms, copy, jm, opts && (opts->flags & KYV_EVAL_ACCOUNT_BYTES),
+               opts && (opts->flags & KYV_EVAL_SERIAL));
     }
     {
       static std::mutex inv_mu;

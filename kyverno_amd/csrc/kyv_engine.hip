@@ -896,7 +896,7 @@ static void slice_phases(const SliceSched& sl, hipEvent_t start, double* phase) 
 }
 
 void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results* out, double* kernel_ms_avg, bool copy_back,
-              int jit_mode, bool account) {
+              int jit_mode, bool account, bool serial) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw std::runtime_error("no HIP device available (GPU backend requested)");
   if (device < 0 || device >= ndev) throw std::runtime_error("device index out of range");
@@ -1065,7 +1065,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   static const bool cond_conc = !getenv("KYV_COND_STREAM") || atoi(getenv("KYV_COND_STREAM")) != 0;
   bool conc = false;
   for (auto& sl : d.slices) conc = conc || !sl.cw.empty();
-  conc = conc && cond_conc && !acct;
+  conc = conc && cond_conc && !acct && !serial;
   if (conc && !d.cstream) stream_get(&d.cstream, &d.cfork, &d.cjoin);
   // off by default: measured 13.43 (one stream) vs 13.53 ms (groups overlapped) on C3 10M
   static const bool walk_conc = getenv("KYV_WALK_STREAM") && atoi(getenv("KYV_WALK_STREAM")) != 0;

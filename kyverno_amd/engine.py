@@ -248,11 +248,12 @@ class Results:
 
 
 def evaluate(ruleset, batch, backend="gpu", device=0, iterations=1, threads=0, copy_back=True, account_bytes=False,
-             jit=None):
+             jit=None, serial=False):
     """Evaluate every (resource, rule) pair. backend="gpu" is the product path; "cpu" must be explicit.
     jit: None = library default (runtime-compiled walk kernel for batches >= 65536 resources), True / False force."""
     L = K.lib()
-    flags = (0 if copy_back else K.EVAL_NO_COPYBACK) | (K.EVAL_ACCOUNT_BYTES if account_bytes else 0)
+    flags = (0 if copy_back else K.EVAL_NO_COPYBACK) | (K.EVAL_ACCOUNT_BYTES if account_bytes else 0) | \
+        (K.EVAL_SERIAL if serial else 0)
     if jit is not None:
         flags |= K.EVAL_JIT_ON if jit else K.EVAL_JIT_OFF
     opts = K.EvalOpts(K.KYV_ABI_VERSION, K.BACKEND_GPU if backend == "gpu" else K.BACKEND_CPU, device, iterations,

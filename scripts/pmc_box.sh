@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for C in "$@"; do
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-gather > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-account --no-serial > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 - "$OUT" <<'PY'
 import csv, collections, glob, sys
