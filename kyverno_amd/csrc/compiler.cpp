@@ -1104,17 +1104,18 @@ bool var_syntax(const std::string& s) { return s.find("{{") != std::string::npos
 uint32_t emit_cnode(Cx& c, const Value& v);
 
 // ---- JMESPath subset (OK_JMES programs, kyv_layout.h): go-jmespath's Pratt grammar for fields, quoted fields,
-// sub-expressions, multi-select lists, flatten projections, keys(@), `||` and raw-string / JSON literals, then
-// linearised into root + ops. Anything else (filters, indexes, other functions, pipes, ...) -> CPU fallback.
+// sub-expressions, multi-select lists, flatten projections, keys(@), `||`, raw-string / JSON literals and filter
+// projections whose predicate the device evaluates (kyv_layout.h FilterKind), then linearised into root + ops.
+// Anything else (other predicates, indexes, other functions, pipes, ...) -> CPU fallback.
 struct JNode {
-  enum K { Field, Sub, Proj, Flat, Multi, Func, Cur, Ident, Or, Lit } k;
+  enum K { Field, Sub, Proj, Flat, Multi, Func, Cur, Ident, Or, Lit, Filter, Cmp, And, Not } k;
   std::string name;
   Value lit;
   std::vector<std::shared_ptr<JNode>> kids;
 };
 using JP = std::shared_ptr<JNode>;
 struct JParser {
-  enum Tok { End, Id, Quoted, Dot, LBr, RBr, Flatten, Comma, LPar, RPar, At, OrT, Raw, Json };
+  enum Tok { End, Id, Quoted, Dot, LBr, RBr, Flatten, Comma, LPar, RPar, At, OrT, Raw, Json, FilterT, AndT, NotT, Cmp };
   std::vector<std::pair<Tok, std::string>> toks;
   size_t at = 0;
   explicit JParser(const std::string& s) {
@@ -1140,6 +1141,14 @@ struct JParser {
       }
       if (c == '[' && i + 1 < s.size() && s[i + 1] == ']') { toks.push_back({Flatten, "[]"}); i += 2; continue; }
       if (c == '|' && i + 1 < s.size() && s[i + 1] == '|') { toks.push_back({OrT, "||"}); i += 2; continue; }
+      // go-jmespath lexer.go: "[?", "&&", comparators, "!"
+      if (c == '[' && i + 1 < s.size() && s[i + 1] == '?') { toks.push_back({FilterT, "[?"}); i += 2; continue; }
+      if (c == '&' && i + 1 < s.size() && s[i + 1] == '&') { toks.push_back({AndT, "&&"}); i += 2; continue; }
+      if ((c == '=' || c == '!' || c == '<' || c == '>') && i + 1 < s.size() && s[i + 1] == '=') {
+        toks.push_back({Cmp, s.substr(i, 2)}); i += 2; continue;
+      }
+      if (c == '<' || c == '>') { toks.push_back({Cmp, std::string(1, c)}); i++; continue; }
+      if (c == '!') { toks.push_back({NotT, "!"}); i++; continue; }
       Tok t;
       switch (c) {
         case '.': t = Dot; break;
@@ -1156,7 +1165,10 @@ struct JParser {
     }
     toks.push_back({End, ""});
   }
-  static int bp(Tok t) { return t == OrT ? 2 : t == Flatten ? 9 : t == Dot ? 40 : t == LBr ? 55 : t == LPar ? 60 : 0; }
+  static int bp(Tok t) {  // parser.go bindingPowers
+    return t == OrT ? 2 : t == AndT ? 3 : t == Cmp ? 5 : t == Flatten ? 9 : t == FilterT ? 21 : t == Dot ? 40 :
+           t == NotT ? 45 : t == LBr ? 55 : t == LPar ? 60 : 0;
+  }
   Tok look() const { return toks[at].first; }
   void eat(Tok t) { if (look() != t) throw Fallback{"JMESPath: syntax"}; at++; }
   static JP mk(JNode::K k, std::vector<JP> kids = {}, const std::string& n = "") {
@@ -1179,14 +1191,26 @@ struct JParser {
       case Json: { JP x = mk(JNode::Lit); x->lit = pj::parse(t.second, true); return x; }
       case Flatten: return mk(JNode::Proj, {mk(JNode::Flat, {mk(JNode::Ident)}), proj_rhs(bp(Flatten))});
       case LBr: return multi();
+      case FilterT: return filter(mk(JNode::Ident));
+      case NotT: return mk(JNode::Not, {expr(bp(NotT))});
+      case LPar: { JP x = expr(0); eat(RPar); return x; }
       default: throw Fallback{"JMESPath: expression outside the device subset"};
     }
+  }
+  JP filter(JP left) {  // parseFilter: [left, rhs, condition]
+    JP cond = expr(0);
+    eat(RBr);
+    JP rhs = look() == Flatten ? mk(JNode::Ident) : proj_rhs(bp(FilterT));
+    return mk(JNode::Filter, {left, rhs, cond});
   }
   JP led(const std::pair<Tok, std::string>& t, JP left) {
     switch (t.first) {
       case Dot: return mk(JNode::Sub, {left, dot_rhs(bp(Dot))});
       case Flatten: return mk(JNode::Proj, {mk(JNode::Flat, {left}), proj_rhs(bp(Flatten))});
       case OrT: return mk(JNode::Or, {left, expr(bp(OrT))});
+      case AndT: return mk(JNode::And, {left, expr(bp(AndT))});
+      case Cmp: return mk(JNode::Cmp, {left, expr(bp(Cmp))}, t.second);
+      case FilterT: return filter(left);
       case LPar: {
         if (left->k != JNode::Field) throw Fallback{"JMESPath: syntax"};
         std::vector<JP> args;
@@ -1259,6 +1283,38 @@ void jlin(Cx& c, const JP& n, std::vector<uint32_t>& out, bool& list) {
   }
 }
 
+// the predicate of a filter projection -> JO_FILTER op (kyv_layout.h FilterKind); other predicates -> Fallback
+void jfilter(Cx& c, const JP& cond, std::vector<uint32_t>& out) {
+  if (cond->k == JNode::Func && cond->name == "contains" && cond->kids.size() == 2) {
+    const JP& a = cond->kids[0];
+    const JP& b = cond->kids[1];
+    if (a->k == JNode::Func && a->name == "keys" && a->kids.size() == 1 && a->kids[0]->k == JNode::Cur &&
+        b->k == JNode::Lit && b->lit.is(pj::T::Str)) {
+      out.insert(out.end(), {JO_FILTER, FK_HASKEY, c.sid(b->lit.s), 0u});
+      return;
+    }
+    throw Fallback{"JMESPath: filter predicate"};
+  }
+  if (cond->k == JNode::Cmp && (cond->name == "==" || cond->name == "!=")) {
+    JP f = cond->kids[0], l = cond->kids[1];
+    if (f->k == JNode::Lit) std::swap(f, l);  // DeepEqual is symmetric
+    if (l->k != JNode::Lit || !(l->lit.is(pj::T::Str) || l->lit.is(pj::T::Bool) || l->lit.is(pj::T::Null)))
+      throw Fallback{"JMESPath: filter comparison"};
+    std::vector<uint32_t> keys;
+    std::function<void(const JP&)> chain = [&](const JP& x) {
+      if (x->k == JNode::Field) { keys.push_back(c.sid(x->name)); return; }
+      if (x->k == JNode::Sub) { chain(x->kids[0]); chain(x->kids[1]); return; }
+      if (x->k == JNode::Cur) return;
+      throw Fallback{"JMESPath: filter comparison"};
+    };
+    chain(f);
+    out.insert(out.end(), {JO_FILTER, cond->name == "==" ? FK_EQ : FK_NE, emit_cnode(c, l->lit), (uint32_t)keys.size()});
+    out.insert(out.end(), keys.begin(), keys.end());
+    return;
+  }
+  throw Fallback{"JMESPath: filter predicate"};
+}
+
 // `{{ <expr> }}` -> OK_JMES operand (false: not a single-variable string; throws Fallback outside the subset);
 // *uses_op when the expression reads request.operation
 bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, std::string* text, bool* uses_op) {
@@ -1291,7 +1347,8 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
   for (JNode* x = n.get();;) {
     spine.push_back(x);
     if (x->k == JNode::Field) break;
-    if (x->k != JNode::Sub && x->k != JNode::Proj && x->k != JNode::Flat) throw Fallback{"JMESPath: root"};
+    if (x->k != JNode::Sub && x->k != JNode::Proj && x->k != JNode::Flat && x->k != JNode::Filter)
+      throw Fallback{"JMESPath: root"};
     x = x->kids[0].get();
   }
   std::vector<uint32_t> ops;
@@ -1346,6 +1403,16 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
       jlin(c, rr, ops, list);
       return;
     }
+    if (x->k == JNode::Filter) {
+      lin(x->kids[0]);
+      if (list) throw Fallback{"JMESPath: filter inside a projection"};
+      jfilter(c, x->kids[2], ops);
+      list = true;
+      const JP& rr = x->kids[1];
+      if (rr->k == JNode::Ident) return;
+      jlin(c, rr, ops, list);
+      return;
+    }
     throw Fallback{"JMESPath: expression outside the device subset"};
   };
   if (body) lin(body);
@@ -1356,10 +1423,16 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
     const uint32_t op = ops[i];
     if (op == JO_FIELD) { fused.push_back(op); fused.push_back(ops[i + 1]); i += 2; continue; }
     pure = false;
-    if (op == JO_MULTI) { uint32_t m = ops[i + 1]; fused.insert(fused.end(), ops.begin() + i, ops.begin() + i + 2 + m); i += 2 + m; continue; }
+    if (op == JO_MULTI || op == JO_FILTER) {
+      const uint32_t w = jop_width(ops.data() + i);
+      fused.insert(fused.end(), ops.begin() + i, ops.begin() + i + w);
+      i += w;
+      continue;
+    }
     if (op == JO_KEYS) {
       bool in_list = false;  // was a FLAT before it?
-      for (size_t j = 0; j < fused.size(); j++) if (fused[j] == JO_FLAT) in_list = true;
+      for (size_t j = 0; j < fused.size(); j += jop_width(fused.data() + j))
+        if (fused[j] == JO_FLAT || fused[j] == JO_FILTER) in_list = true;
       if (in_list) {
         if (i + 1 >= ops.size() || ops[i + 1] != JO_FLAT) throw Fallback{"JMESPath: keys() projection without []"};
         fused.push_back(JO_KEYS_FLAT);
@@ -1376,7 +1449,7 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
   // a multi-select list or keys() outside a projection is a plain list: only [] (or the end) may follow
   for (size_t i = 0; i < fused.size();) {
     const uint32_t op = fused[i];
-    const size_t w = op == JO_FIELD ? 2 : op == JO_MULTI ? 2 + fused[i + 1] : 1;
+    const size_t w = jop_width(fused.data() + i);
     if ((op == JO_MULTI || op == JO_KEYS) && i + w < fused.size() && fused[i + w] != JO_FLAT)
       throw Fallback{"JMESPath: list outside a projection"};
     i += w;
@@ -2243,6 +2316,10 @@ struct TrieBuilder {
         N.push_back(NONE);
         list = list || op == JO_KEYS;
         q++;
+      } else if (op == JO_FILTER) {  // the kept elements: array elements (compiled kernels do not generate filters)
+        for (uint32_t t : S) N.push_back(st(t));
+        list = true;
+        q += jop_width(p + q);
       } else if (op == JO_LENGTH) {  // a number: no trie position
         S = {NONE};
         list = false;

@@ -764,7 +764,7 @@ struct CondGen {
       PEND = n;
       for (uint32_t q = 1; q < n;) {  // a trailing `|| lit` ends the ops
         if (p[q] == JO_OR) { PEND = q; orlit = p[q + 1]; break; }
-        q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
+        q += jop_width(p + q);
       }
       P = p;
       const bool su = unroll;
@@ -806,7 +806,7 @@ struct CondGen {
     PEND = n;
     for (uint32_t q = 1; q < n;) {
       if (p[q] == JO_OR) { PEND = q; orlit = p[q + 1]; break; }
-      q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
+      q += jop_width(p + q);
     }
     P = p;
     const bool su = unroll, ss = streaming;
@@ -904,9 +904,9 @@ struct CondGen {
     if (o.kind != OK_JMES) return false;
     const uint32_t* p = rs.pool.data() + o.a;
     for (uint32_t q = 1; q < o.nseg;) {
-      if (p[q] == JO_MULTI || p[q] == JO_FLAT || p[q] == JO_KEYS || p[q] == JO_KEYS_FLAT) return true;
+      if (p[q] == JO_MULTI || p[q] == JO_FLAT || p[q] == JO_KEYS || p[q] == JO_KEYS_FLAT || p[q] == JO_FILTER) return true;
       if (p[q] == JO_OR) return false;
-      q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
+      q += jop_width(p + q);
     }
     return false;
   }
@@ -1164,8 +1164,8 @@ struct CondGen {
       if (root != JR_OBJECT) { ok = false; return; }
       PEND = o.nseg;
       for (uint32_t q = 1; q < o.nseg;) {
-        if (p[q] == JO_OR || p[q] == JO_KEYS || p[q] == JO_KEYS_FLAT) { ok = false; return; }
-        q += p[q] == JO_FIELD ? 2 : p[q] == JO_MULTI ? 2 + p[q + 1] : 1;
+        if (p[q] == JO_OR || p[q] == JO_KEYS || p[q] == JO_KEYS_FLAT || p[q] == JO_FILTER) { ok = false; return; }
+        q += jop_width(p + q);
       }
       P = p;
       V x = decl("0u", "T_UNK", "0u", "r", 0u, false);

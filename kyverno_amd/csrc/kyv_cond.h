@@ -154,7 +154,9 @@ struct JRes {
 };
 // JS_ERR: a run-time JMESPath error other than NotFound (length() of a null / number / boolean): the substitution
 // fails, so the condition program is an error (vars.go:352-431)
-enum JStat { JS_OK = 0, JS_NOTFOUND = 1, JS_FB = 2, JS_ERR = 3 };
+// JS_TERR: a function argument type error (keys() of a non-object inside a filter): a foreach list query that errors
+// skips its entry (validation.go:322-326); in a condition operand the CPU engine words the error
+enum JStat { JS_OK = 0, JS_NOTFOUND = 1, JS_FB = 2, JS_ERR = 3, JS_TERR = 4 };
 
 KYV_HD bool j_false(const View& v, NodeTab R, const JRes& r, const JList& L) {  // util.go isFalse
   if (r.lst) return L.n == 0;
@@ -312,6 +314,49 @@ __host__ __device__ inline __attribute__((noinline)) int jmes_run(const View& v,
         }
       }
       r.lst = false; r.cur = NONE; r.num = cnt;
+    } else if (op == JO_FILTER) {
+      // filter projection (go-jmespath ASTFilterProjection): the elements of a list whose predicate is not false-like;
+      // a non-list is null. The ops after it run per kept element (a projection: null results dropped at its end)
+      const uint32_t fk = p[i + 1], lit = p[i + 2], nf = p[i + 3];
+      const uint32_t* fkeys = p + i + 4;
+      i += 4 + nf;
+      if (r.lst) return JS_FB;  // a filter inside a projection: not compiled (compiler.cpp jmes_var)
+      if (!j_arr(R, r.cur)) { r.cur = NONE; proj = false; continue; }
+      const Node& a = R[r.cur];
+      uint32_t w = 0;
+      for (uint32_t j = 0; j < a.b; j++) {
+        const uint32_t e = a.a + j;
+        bool keep;
+        if (fk == FK_HASKEY) {  // contains(keys(@), 'lit'): keys() of a non-object fails the argument type check
+          if (node_type(R[e]) != N_MAP) return JS_TERR;
+          keep = map_find(R, e, lit) != NONE;
+        } else {  // <fields> ==/!= literal (reflect.DeepEqual): string by id, boolean, null
+          uint32_t x = node_type(R[e]) == N_NULL ? NONE : e;
+          bool missing;
+          for (uint32_t q = 0; q < nf && x != NONE; q++) x = j_field(R, x, fkeys[q], &missing);
+          const Node& c = v.cnodes[lit];
+          const uint32_t ct = node_type(c);
+          bool eq;
+          if (x == NONE) eq = ct == N_NULL;
+          else {
+            const Node& n = R[x];
+            const uint32_t nt = node_type(n);
+            if (nt == N_INT || nt == N_FLOAT || nt == N_ARR || nt == N_MAP) {
+              if (ct == N_STR || ct == N_TRUE || ct == N_FALSE || ct == N_NULL) eq = false;
+              else return JS_FB;
+            } else {
+              eq = nt == ct && (nt != N_STR || n.a == c.a);
+            }
+          }
+          keep = fk == FK_EQ ? eq : !eq;
+        }
+        if (!keep) continue;
+        if (w >= JMES_MAX_LIST) return JS_FB;
+        L.e[w++] = node_type(R[e]) == N_NULL ? NONE : e;
+      }
+      L.n = w;
+      r.lst = true;
+      proj = true;
     } else if (op == JO_OR) {
       const uint32_t lit = p[i + 1];
       i += 2;
@@ -755,7 +800,7 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
           } else {
             JList L;
             const int st = operand_cv(v, R, o, elem, L, &tmp, &miss, row);
-            if (st == JS_FB) return CR_FB;
+            if (st == JS_FB || st == JS_TERR) return CR_FB;
             if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
             if (st == JS_ERR) { *err_cond = c0 + i; *err_side = side; *err_seg = NONE; return CP_ERROR; }
           }

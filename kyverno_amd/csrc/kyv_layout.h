@@ -372,7 +372,19 @@ enum JmesOp : uint32_t { JO_FIELD = 1,     // + key sid
                          JO_KEYS = 4,      // keys(@) of the current map
                          JO_KEYS_FLAT = 5, // projection keys(@) then flatten
                          JO_OR = 6,        // + cnode literal: `|| <literal>` when the result is false-like
-                         JO_LENGTH = 7 };  // length(<the ops before>): a number (go-jmespath jpfLength)
+                         JO_LENGTH = 7,    // length(<the ops before>): a number (go-jmespath jpfLength)
+                         JO_FILTER = 8 };  // + FilterKind, literal, n, n key sids: filter projection `[?<pred>]`
+// filter predicates the device evaluates per element (the compiler keeps other predicates on the CPU engine):
+//   FK_HASKEY  contains(keys(@), '<lit>')  literal = key sid; an element that is not a map: keys() type error
+//   FK_EQ/NE   <field chain> == / != <literal>  literal = cnode (string, boolean or null)
+enum FilterKind : uint32_t { FK_HASKEY = 0, FK_EQ = 1, FK_NE = 2 };
+// words of the op at p (opcode + operands)
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+__host__ __device__
+#endif
+inline uint32_t jop_width(const uint32_t* p) {
+  return p[0] == JO_FIELD || p[0] == JO_OR ? 2u : p[0] == JO_MULTI ? 2u + p[1] : p[0] == JO_FILTER ? 4u + p[3] : 1u;
+}
 constexpr uint32_t JMES_MAX_LIST = 32;     // virtual list capacity (longer -> CPU fallback)
 constexpr uint32_t JMES_KEYBIT = 1u << 31; // virtual list element: the key of map entry node (index & ~KEYBIT)
 constexpr uint32_t JMES_SIDBIT = 1u << 30; // virtual list element: a string value, by dictionary id (& ~SIDBIT)

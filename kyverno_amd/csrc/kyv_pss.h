@@ -872,8 +872,8 @@ KYV_HD uint8_t foreach_level(const View& v, NodeTab R, const RuleDesc& rd, uint3
         lr.cur = cur;
       } else {
         const int st = jmes_run(v, R, fe.list, up.el, L, &lr, &miss);
-        if (st == JS_NOTFOUND) continue;
-        if (st == JS_FB || st == JS_ERR) return KYV_WHY(FBW_COND), ST_FALLBACK;
+        if (st == JS_NOTFOUND || st == JS_ERR || st == JS_TERR) continue;  // "failed to evaluate list": next entry
+        if (st == JS_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
         if (lr.lit != NONE || lr.num != NONE) return KYV_WHY(FBW_COND), ST_FALLBACK;  // literal / number: not restated
       }
       // elements: the projection list, an array's items, or the single value

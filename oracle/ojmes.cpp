@@ -16,7 +16,7 @@ namespace {
 
 // ---------------------------------------------------------------- lexer (go-jmespath lexer.go, subset)
 enum Tok { tEOF, tIdent, tQuoted, tDot, tLbracket, tRbracket, tFlatten, tComma, tLparen, tRparen, tCurrent, tOr,
-           tRaw, tJSON, tOther };
+           tRaw, tJSON, tFilter, tAnd, tNot, tEQ, tNE, tLT, tLTE, tGT, tGTE, tOther };
 struct Token { Tok t; std::string v; };
 
 std::vector<Token> lex(const std::string& s) {
@@ -53,6 +53,7 @@ std::vector<Token> lex(const std::string& s) {
     } else if (c == '.') { out.push_back({tDot, "."}); i++; }
     else if (c == '[') {
       if (i + 1 < s.size() && s[i + 1] == ']') { out.push_back({tFlatten, "[]"}); i += 2; }
+      else if (i + 1 < s.size() && s[i + 1] == '?') { out.push_back({tFilter, "[?"}); i += 2; }
       else { out.push_back({tLbracket, "["}); i++; }
     } else if (c == ']') { out.push_back({tRbracket, "]"}); i++; }
     else if (c == ',') { out.push_back({tComma, ","}); i++; }
@@ -60,6 +61,18 @@ std::vector<Token> lex(const std::string& s) {
     else if (c == ')') { out.push_back({tRparen, ")"}); i++; }
     else if (c == '@') { out.push_back({tCurrent, "@"}); i++; }
     else if (c == '|' && i + 1 < s.size() && s[i + 1] == '|') { out.push_back({tOr, "||"}); i += 2; }
+    else if (c == '&' && i + 1 < s.size() && s[i + 1] == '&') { out.push_back({tAnd, "&&"}); i += 2; }
+    else if (c == '=' && i + 1 < s.size() && s[i + 1] == '=') { out.push_back({tEQ, "=="}); i += 2; }
+    else if (c == '!') {  // lexer.go matchOrElse('!', '=', tNE, tNot)
+      if (i + 1 < s.size() && s[i + 1] == '=') { out.push_back({tNE, "!="}); i += 2; }
+      else { out.push_back({tNot, "!"}); i++; }
+    } else if (c == '<') {
+      if (i + 1 < s.size() && s[i + 1] == '=') { out.push_back({tLTE, "<="}); i += 2; }
+      else { out.push_back({tLT, "<"}); i++; }
+    } else if (c == '>') {
+      if (i + 1 < s.size() && s[i + 1] == '=') { out.push_back({tGTE, ">="}); i += 2; }
+      else { out.push_back({tGT, ">"}); i++; }
+    }
     else throw JmesUnsupported{std::string("token '") + c + "'"};
   }
   out.push_back({tEOF, ""});
@@ -67,10 +80,11 @@ std::vector<Token> lex(const std::string& s) {
 }
 
 // ---------------------------------------------------------------- parser (go-jmespath parser.go, subset)
-enum NodeKind { NField, NSubexpr, NProjection, NFlatten, NMultiList, NFunction, NCurrent, NIdentity, NOr, NLiteral };
+enum NodeKind { NField, NSubexpr, NProjection, NFlatten, NMultiList, NFunction, NCurrent, NIdentity, NOr, NLiteral,
+                NFilterProjection, NComparator, NAnd, NNot };
 struct Node {
   NodeKind k;
-  std::string name;  // NField / NFunction
+  std::string name;  // NField / NFunction / NComparator (the operator)
   VP lit;            // NLiteral
   std::vector<std::shared_ptr<Node>> kids;
 };
@@ -86,8 +100,12 @@ NP mk(NodeKind k, std::vector<NP> kids = {}, const std::string& name = "") {
 int binding_power(Tok t) {  // parser.go bindingPowers (tokens outside the subset never reach here)
   switch (t) {
     case tOr: return 2;
+    case tAnd: return 3;
+    case tEQ: case tNE: case tLT: case tLTE: case tGT: case tGTE: return 5;
     case tFlatten: return 9;
+    case tFilter: return 21;
     case tDot: return 40;
+    case tNot: return 45;
     case tLbracket: return 55;
     case tLparen: return 60;
     default: return 0;
@@ -125,6 +143,13 @@ struct Parser {
       }
       case tLbracket:
         return multi_list();
+      case tFilter: return filter(mk(NIdentity));
+      case tNot: return mk(NNot, {expr(binding_power(tNot))});
+      case tLparen: {  // nud(tLparen): a parenthesised expression
+        NP x = expr(0);
+        match(tRparen);
+        return x;
+      }
       default: throw JmesUnsupported{"expression start"};
     }
   }
@@ -133,6 +158,10 @@ struct Parser {
       case tDot: return mk(NSubexpr, {left, dot_rhs(binding_power(tDot))});
       case tFlatten: return mk(NProjection, {mk(NFlatten, {left}), projection_rhs(binding_power(tFlatten))});
       case tOr: return mk(NOr, {left, expr(binding_power(tOr))});
+      case tAnd: return mk(NAnd, {left, expr(binding_power(tAnd))});
+      case tEQ: case tNE: case tLT: case tLTE: case tGT: case tGTE:
+        return mk(NComparator, {left, expr(binding_power(t.t))}, t.v);
+      case tFilter: return filter(left);
       case tLparen: {
         if (left->k != NField) throw JmesUnsupported{"function name"};
         std::vector<NP> args;
@@ -154,9 +183,15 @@ struct Parser {
   }
   NP projection_rhs(int bp) {
     if (binding_power(look()) < 10) return mk(NIdentity);  // projectionStop
-    if (look() == tLbracket) return expr(bp);
+    if (look() == tLbracket || look() == tFilter) return expr(bp);
     if (look() == tDot) { match(tDot); return dot_rhs(bp); }
     throw JmesUnsupported{"projection rhs"};
+  }
+  NP filter(NP left) {  // parseFilter: children [left, right, condition]
+    NP cond = expr(0);
+    match(tRbracket);
+    NP right = look() == tFlatten ? mk(NIdentity) : projection_rhs(binding_power(tFilter));
+    return mk(NFilterProjection, {left, right, cond});
   }
   NP multi_list() {  // '[' already consumed
     std::vector<NP> items;
@@ -185,6 +220,33 @@ bool is_false(const VP& v) {  // util.go isFalse
     case T::Str: return v->s.empty();
     case T::Arr: return v->a.empty();
     case T::Obj: return v->o.empty();
+    default: return false;
+  }
+}
+
+// reflect.DeepEqual of two decoded JSON values (every number float64 in the JSON context)
+bool objs_equal(const VP& a, const VP& b) {
+  const bool an = !a || a->t == T::Null, bn = !b || b->t == T::Null;
+  if (an || bn) return an && bn;
+  auto num = [](const VP& v, double* d) {
+    if (v->t == T::Int) { *d = (double)v->i; return true; }
+    if (v->t == T::Float) { *d = v->f; return true; }
+    return false;
+  };
+  double x, y;
+  if (num(a, &x) || num(b, &y)) return num(a, &x) && num(b, &y) && x == y;
+  if (a->t != b->t) return false;
+  switch (a->t) {
+    case T::Bool: return a->b == b->b;
+    case T::Str: return a->s == b->s;
+    case T::Arr:
+      if (a->a.size() != b->a.size()) return false;
+      for (size_t i = 0; i < a->a.size(); i++) if (!objs_equal(a->a[i], b->a[i])) return false;
+      return true;
+    case T::Obj:
+      if (a->o.size() != b->o.size()) return false;
+      for (auto& kv : a->o) { if (!b->has(kv.first) || !objs_equal(kv.second, b->get(kv.first))) return false; }
+      return true;
     default: return false;
   }
 }
@@ -233,6 +295,17 @@ VP eval(const NP& n, const VP& value) {
         if (arg && arg->t == T::Obj) return Value::flt((double)arg->o.size());
         throw JmesError{"invalid type for: <nil>, expected: []jpType{\"string\", \"array\", \"object\"}"};
       }
+      if (n->name == "contains" && n->kids.size() == 2) {  // jpfContains: substring of a string, member of an array
+        VP subject = eval(n->kids[0], value), el = eval(n->kids[1], value);
+        if (subject && subject->t == T::Str) return Value::boolean(el && el->t == T::Str && subject->s.find(el->s) != std::string::npos);
+        if (!subject || subject->t != T::Arr) throw JmesError{"invalid type for: <nil>, expected: []jpType{\"array\", \"string\"}"};
+        for (auto& x : subject->a) {  // Go interface ==: same dynamic type and value (scalars here)
+          if (!x || !el) { if ((!x || x->t == T::Null) && (!el || el->t == T::Null)) return Value::boolean(true); continue; }
+          if (x->t == T::Arr || x->t == T::Obj || el->t == T::Arr || el->t == T::Obj) throw JmesUnsupported{"contains of a container"};
+          if (objs_equal(x, el)) return Value::boolean(true);
+        }
+        return Value::boolean(false);
+      }
       if (n->name != "keys" || n->kids.size() != 1) throw JmesUnsupported{"function " + n->name};
       VP arg = eval(n->kids[0], value);
       if (!arg || arg->t != T::Obj) throw JmesError{"invalid type for: <nil>, expected: []jpType{\"object\"}"};
@@ -246,6 +319,39 @@ VP eval(const NP& n, const VP& value) {
       return is_false(m) ? eval(n->kids[1], value) : m;
     }
     case NLiteral: return n->lit;
+    case NFilterProjection: {  // interpreter.go ASTFilterProjection
+      VP left = eval(n->kids[0], value);
+      if (!left || left->t != T::Arr) return Value::null();
+      auto out = Value::arr();
+      for (auto& e : left->a) {
+        VP el = e ? e : Value::null();
+        if (is_false(eval(n->kids[2], el))) continue;
+        VP r = eval(n->kids[1], el);
+        if (r && r->t != T::Null) out->a.push_back(r);
+      }
+      return out;
+    }
+    case NComparator: {  // interpreter.go ASTComparator: ==/!= by DeepEqual, ordering only for two numbers
+      VP l = eval(n->kids[0], value), r = eval(n->kids[1], value);
+      if (n->name == "==") return Value::boolean(objs_equal(l, r));
+      if (n->name == "!=") return Value::boolean(!objs_equal(l, r));
+      auto num = [](const VP& v, double* d) {
+        if (v && v->t == T::Int) { *d = (double)v->i; return true; }
+        if (v && v->t == T::Float) { *d = v->f; return true; }
+        return false;
+      };
+      double x, y;
+      if (!num(l, &x) || !num(r, &y)) return Value::null();
+      if (n->name == "<") return Value::boolean(x < y);
+      if (n->name == "<=") return Value::boolean(x <= y);
+      if (n->name == ">") return Value::boolean(x > y);
+      return Value::boolean(x >= y);
+    }
+    case NAnd: {
+      VP l = eval(n->kids[0], value);
+      return is_false(l) ? l : eval(n->kids[1], value);
+    }
+    case NNot: return Value::boolean(is_false(eval(n->kids[0], value)));
   }
   return Value::null();
 }
@@ -273,7 +379,7 @@ VP json_floats(const VP& v) { return floats(v); }
 
 // every node within the restated interpreter (functions: keys(@) and length())
 static bool nodes_ok(const NP& n) {
-  if (n->k == NFunction && !(n->name == "length" && n->kids.size() == 1) &&
+  if (n->k == NFunction && !(n->name == "length" && n->kids.size() == 1) && !(n->name == "contains" && n->kids.size() == 2) &&
       (n->name != "keys" || n->kids.size() != 1 || n->kids[0]->k != NCurrent))
     return false;
   for (auto& k : n->kids) if (!nodes_ok(k)) return false;
@@ -291,7 +397,8 @@ bool jmes_supported(const std::string& expr, bool allow_element) {
       if (c->kids.empty()) return false;
       const Node* l = c->kids[0].get();
       if (l->k == NField) break;
-      if (l->k != NSubexpr && l->k != NProjection && l->k != NFlatten && l->k != NOr) return false;
+      if (l->k != NSubexpr && l->k != NProjection && l->k != NFlatten && l->k != NOr && l->k != NFilterProjection)
+        return false;
       c = l;
     }
     const std::string& root = c->kids[0]->name;

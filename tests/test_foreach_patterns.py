@@ -3,9 +3,10 @@
 elementScope, evaluated by the library (host instantiation here, the MI355X in the -m gpu tests) against the oracle's
 restatement of validateForEach / validateElements (pkg/engine/validation.go:242-421), pair by pair.
 
-The reference's own fixture (test/cli/test/foreach/policies.yaml) additionally filters its list with a JMESPath filter
-expression; the same shapes without the filter are here, and the fixture's policies themselves are checked in
-test_foreach_fixture_* (tests/golden/cli.json)."""
+The reference's own fixture (test/cli/test/foreach/policies.yaml) filters its list with a JMESPath filter expression
+(`volumes[?contains(keys(@), 'emptyDir')]`): its two policies are here verbatim (fe-fixture-*), over a corpus whose
+containers mount the pods' volumes, plus ==/!= filters and a filter with a projection after it; the fixture's own
+resources and verdicts are checked in test_foreach_fixture_* (tests/golden/cli.json)."""
 import copy
 
 import numpy as np
@@ -59,7 +60,61 @@ def foreach_pattern_policies():
         # a controller kind: containers under spec.template.spec, and resources without the list (entry skipped)
         _pol("fe-deploy", [{"list": "request.object.spec.template.spec.containers",
                             "pattern": {"resources": {"limits": {"memory": "?*"}}}}], kinds=("Deployment", "Pod")),
+        # filter projections: the reference fixture's two policies (test/cli/test/foreach/policies.yaml) ...
+        _pol("fe-fixture-mountpath", [{"list": "request.object.spec.volumes[?contains(keys(@), 'emptyDir')]",
+                                       "elementScope": False, "pattern": {"spec": {"containers": [
+                                           {"name": "*", "volumeMounts": [{"(name)": "{{element.name}}",
+                                                                           "mountPath": "/tmp/*"}]}]}}}],
+             message="emptyDir volumes must be mounted under /tmp"),
+        _pol("fe-fixture-resources", [{"list": "request.object.spec.volumes[?contains(keys(@), 'emptyDir')]",
+                                       "elementScope": False, "pattern": {"spec": {"containers": [
+                                           {"volumeMounts": [{"<(name)": "{{element.name}}"}],
+                                            "resources": {"requests": {"ephemeral-storage": "?*"},
+                                                          "limits": {"ephemeral-storage": "?*"}}}]}}}],
+             message="ephemeral-storage requests and limits are required for emptyDir volumes"),
+        # ... equality filters on a field chain (string / boolean literals), and a projection after the filter
+        _pol("fe-filter-eq", [{"list": "request.object.spec.containers[?name == 'c0']",
+                               "pattern": {"securityContext": {"runAsNonRoot": True}}}]),
+        _pol("fe-filter-ne", [{"list": "request.object.spec.containers[?securityContext.privileged != `true`].image",
+                               "deny": {"conditions": {"any": [{"key": "{{element}}", "operator": "Equals",
+                                                                "value": "*:latest"}]}}}]),
+        _pol("fe-filter-keys", [{"list": "request.object.spec.volumes[?contains(keys(@), 'hostPath')].hostPath.path",
+                                 "deny": {"conditions": {"any": [{"key": "{{element}}", "operator": "Equals",
+                                                                  "value": "/var/run/docker.sock"}]}}}]),
     ]
+
+
+def with_mounts(docs, seed):
+    """the corpus with volumeMounts on the pods' containers (mount paths under /tmp or not, some mounts missing),
+    ephemeral-storage resources on some containers, and now and then a volume list holding a non-map element (the
+    filter's keys() type error: the reference skips the entry)"""
+    import random
+    rng = random.Random(seed)
+    out = copy.deepcopy(docs)
+    for d in out:
+        spec = d.get("spec")
+        if isinstance(spec, dict) and isinstance(spec.get("template"), dict):
+            spec = spec["template"].get("spec")
+        if not isinstance(spec, dict):
+            continue
+        vols = spec.get("volumes")
+        if not isinstance(vols, list):
+            continue
+        for c in spec.get("containers") or []:
+            if not isinstance(c, dict):
+                continue
+            mounts = [{"name": v.get("name"), "mountPath": rng.choice(["/tmp/" + str(v.get("name")), "/data", "/tmp"])}
+                      for v in vols if isinstance(v, dict) and rng.random() < 0.8]
+            if mounts:
+                c["volumeMounts"] = mounts
+            if rng.random() < 0.5:
+                res = c.setdefault("resources", {}) if isinstance(c.get("resources", {}), dict) else {}
+                res.setdefault("requests", {})["ephemeral-storage"] = "1Gi"
+                if rng.random() < 0.7:
+                    res.setdefault("limits", {})["ephemeral-storage"] = "2Gi"
+        if rng.random() < 0.02:
+            vols.append(rng.choice(["bad-volume", 7, None]))
+    return out
 
 
 @pytest.mark.parametrize("backend", ["cpu"])
@@ -69,11 +124,18 @@ def test_foreach_patterns_vs_oracle(backend):
     fb = [(r["name"], r["reason"]) for r in rs.rules if r["kind"] == "fallback"]
     assert not fb, fb  # every shape above compiles to the device
     docs, nsl = synth.mixed(3000, seed=71, edge=True)
+    docs = with_mounts(docs, 71)
     st, res = PU.compare(pols, docs, nsl, backend=backend)
     assert st["nbad"] == 0, st["bad"]
     assert st["compared"] > 3000
     counts = res.counts
     assert counts["pass"] > 0 and counts["fail"] > 0 and counts["skip"] > 0 and counts["error"] > 0
+    # every filter policy decides both ways on this corpus
+    status = np.asarray(res.status)
+    for k, rule in enumerate(rs.rules):
+        if rule["name"].startswith(("fe-fixture", "fe-filter")):
+            vals = set((status[k] & 7).tolist())
+            assert K.ST_PASS in vals and K.ST_FAIL in vals, (rule["name"], vals)
 
 
 @pytest.mark.gpu
@@ -82,6 +144,7 @@ def test_foreach_patterns_gpu_vs_oracle(jit):
     """the same corpus through the device: the interpreted match kernel and (jit) the compiled condition kernels"""
     pols = foreach_pattern_policies()
     docs, nsl = synth.mixed(20000, seed=72, edge=True)
+    docs = with_mounts(docs, 72)
     st, res = PU.compare(pols, docs, nsl, backend="gpu", jit=jit)
     assert st["nbad"] == 0, st["bad"]
     assert st["compared"] > 20000
