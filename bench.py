@@ -323,7 +323,7 @@ def shard_parity(policies, rs, data, nsl, timed_status, cap=100000):
 
 
 # device phase -> kernel-name prefixes of that phase in a rocprofv3 kernel trace
-PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::pss_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv::walk_kernel"),
+PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::pss_kernel", "kyv::pss_map_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv::walk_kernel"),
                  "compact": ("kyv::compact",), "hist": ("kyv::status_hist",)}
 
 

@@ -11,6 +11,7 @@ void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* 
 void match_walk(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
                 const uint32_t* mrules, uint32_t nm);
 void pss(bool exact, int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0);
+void pss_map(unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0);
 void walk(unsigned grid, size_t lds, hipStream_t s, const void* view, const void* devout, const void* wl, const void* cm,
           int depth);
 // device address of this build's counters: unsigned long long[3][KYV_ACCT_SLOTS] (reads, writes, staged records)

@@ -49,6 +49,11 @@ void pss(bool exact, int wpe, unsigned grid, hipStream_t s, const void* view, co
   hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), k, w0);
   check(hipGetLastError());
 }
+void pss_map(unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0) {
+  using namespace kyv_acct;
+  hipLaunchKernelGGL(pss_map_kernel, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), k, w0);
+  check(hipGetLastError());
+}
 void walk(unsigned grid, size_t lds, hipStream_t s, const void* view, const void* devout, const void* wl, const void* cm,
           int depth) {
   using namespace kyv_acct;

@@ -1109,13 +1109,17 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
                                 (const uint32_t*)sl.mrules + sl.nmw + sl.nm, sl.nmj);
       }
       {
-        static const int pwpe = getenv("KYV_PSS_WPE") ? atoi(getenv("KYV_PSS_WPE")) : 8;  // C2: 4 0.586, 6 0.587, 8 0.514 ms
+        // C2 (round 3, map walk inlined): 4 0.586, 6 0.587, 8 0.514 ms; the column-only kernel at 6 has no scratch
+        static const int pwpe = getenv("KYV_PSS_WPE") ? atoi(getenv("KYV_PSS_WPE")) : 6;
         for (const uint3& c : sl.pw) {
           const bool ex = (rs.rules[c.x].flags & RD_GATE_EXACT) && rs.rules[c.x].match.mode != MM_NONE;
           auto kf = ex ? (pwpe == 4 ? pss_kernel<true, 4> : pwpe == 6 ? pss_kernel<true, 6> : pss_kernel<true, 8>)
                        : (pwpe == 4 ? pss_kernel<false, 4> : pwpe == 6 ? pss_kernel<false, 6> : pss_kernel<false, 8>);
           if (acct) kyvacct::pss(ex, pwpe, c.z, stream, d.view, &o, c.x, c.y);
           else hipLaunchKernelGGL(kf, dim3(c.z), dim3(BLOCK), 0, stream, (const View*)d.view, o, c.x, c.y);
+          // the pairs it marked ST_PSS_MAP (exclusions, no path columns): the map walk
+          if (acct) kyvacct::pss_map(c.z, stream, d.view, &o, c.x, c.y);
+          else hipLaunchKernelGGL(pss_map_kernel, dim3(c.z), dim3(BLOCK), 0, stream, (const View*)d.view, o, c.x, c.y);
         }
       }
       HIP_OK(hipGetLastError());

@@ -104,11 +104,12 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uin
 }
 
 // PodSecurity rules (without preconditions): one lane per resource over the match waves [w0, w0 + grid) of the rule's
-// kind gate, the match and the path-column checks inlined (eval_pss_cols); in the match kernel the checks are an
-// out-of-line call whose callee-saved registers go through scratch memory. Pairs the column form does not cover
-// (exclusion sub-pods, resources without path columns) take the out-of-line map walk (eval_pss).
-// kExact: the rule's match block is its kind gate (RD_GATE_EXACT), no match program compiled in; kWpe: occupancy
-// target (KYV_PSS_WPE = 4 / 6 / 8 at run time; 8 by default)
+// kind gate, the match and the path-column checks inlined (eval_pss_cols). Pairs the column form does not cover
+// (exclusion sub-pods, resources without path columns) are marked ST_PSS_MAP and finished by pss_map_kernel: the map
+// walk (eval_pss) is a call whose frame and spills would otherwise sit in this kernel's scratch and write traffic
+// (round 3 C2 profile: 13x write amplification). kExact: the rule's match block is its kind gate (RD_GATE_EXACT), no
+// match program compiled in; kWpe: occupancy target (KYV_PSS_WPE = 4 / 6 / 8 at run time; 6 by default: 72 VGPRs, no
+// scratch, 7 waves per SIMD)
 template <bool kExact, int kWpe>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
 pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
@@ -132,7 +133,7 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
     const NodeTab R{v.nodes + h.root};
     KYV_ACCT_ADD(0, 12);  // header: root, node count, flags
     st = eval_pss_cols(v, v.pss[rd.root], h, R, &pf, r);
-    if (st == ST_NONE) st = eval_pss(v, v.pss[rd.root], R, h, &pf, r);
+    if (st == ST_NONE) st = ST_PSS_MAP;
   }
   if (gated && st != ST_NONE) {
     o.status[(size_t)k * v.nres + r] = st;
@@ -140,6 +141,24 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
     if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
     KYV_ACCT_ADD(1, 1 + ((ps != NONE && pf) ? 4 : 0));
   }
+}
+
+// The PodSecurity pairs pss_kernel marked ST_PSS_MAP (same grid): the map walk with the typed pod view, exclusion
+// sub-pods included (eval_pss, validation.go:535-566 + pkg/pss/evaluate.go:83-108)
+__global__ void __launch_bounds__(BLOCK) pss_map_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
+  const View& v = *vp;
+  const uint32_t r = (w0 + blockIdx.x) * BLOCK + threadIdx.x;
+  if (r >= v.nres) return;
+  const uint8_t s0 = o.status[(size_t)k * v.nres + r];
+  KYV_ACCT_ADD(0, 1);  // the pair's status byte
+  if (s0 != ST_PSS_MAP) return;
+  const ResHeader& h = v.hdr[r];
+  uint32_t pf = 0;
+  const uint8_t st = eval_pss(v, v.pss[v.rules[k].root], NodeTab{v.nodes + h.root}, h, &pf, r);
+  o.status[(size_t)k * v.nres + r] = st;
+  const uint32_t ps = o.pss_slot[k];
+  if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
+  KYV_ACCT_ADD(1, 1 + ((ps != NONE && pf) ? 4 : 0));
 }
 
 // Phase 2 (pattern_eval): each wave takes chunks of 64 work items of ONE rule (grid-stride over all rules'

@@ -458,6 +458,9 @@ constexpr int NSTATUS = 8;
 constexpr uint8_t ST_MARK_PRE = 30u << 3;
 // on an error of a foreach rule: an element that is not a map under elementScope: true (validation.go:395-397)
 constexpr uint8_t ST_MARK_SCOPE = 29u << 3;
+// transient (never returned): a PodSecurity pair pss_kernel left to pss_map_kernel (the map walk: exclusion
+// sub-pods, resources without path columns); low bits ST_NONE
+constexpr uint8_t ST_PSS_MAP = 28u << 3;
 // on a skip: rule skipped due to the PolicyException candidate (mark - 1) of the rule (validation.go:824-848)
 constexpr uint32_t MAX_EXC = 27;
 // (the status byte is ST_SKIP | (i + 1) << 3 for candidate i < MAX_EXC)
