@@ -973,6 +973,15 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
     b->faux.resize(total_faux);
     bool pss_rules = false;
     for (auto& rd : rs->rules) pss_rules = pss_rules || rd.kind == RK_PSS;
+    std::unique_ptr<TypedDecoder> typed;
+    if (pss_rules)
+      typed.reset(new TypedDecoder([&](const std::string& s) -> uint32_t {
+        const uint64_t h = hash_bytes(s.data(), s.size());
+        uint32_t id = seedtab.find(s, h);
+        if (id != NONE) return id;
+        id = shard[shard_of(h)].find(s, h);
+        return id == NONE ? NONE : (uint32_t)(shbase[shard_of(h)] + id);
+      }));
     parallel_for(nchunks, T, [&](size_t c) {
       Chunk& ch = chunks[c];
       const auto& rm = remap[c];
@@ -1022,7 +1031,14 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
         if (pss_rules) {  // typed pod decode once per resource (eval_pss skips it on RF_PSS_DONE)
           uint32_t pm, ps;
           const uint8_t st = pss_pod(NodeTab{R}, h.kind, true, &pm, &ps);
-          h.flags |= RF_PSS_DONE | (st == ST_ERROR ? RF_PSS_DEC_ERR : 0u);
+          uint32_t f = st == ST_ERROR ? RF_PSS_DEC_ERR : 0u;
+          if (!f && st != ST_PANIC) {  // the whole object, as getSpec's json.Unmarshal (typed.cpp)
+            const int tgt = h.kind == KSID(POD) ? TypedDecoder::POD
+                          : h.kind == KSID(CRONJOB) ? TypedDecoder::CRONJOB : TypedDecoder::DEPLOYMENT;
+            const int d = typed->decode(R, b->dict.strs, tgt);
+            f = d == TypedDecoder::DEC_ERR ? RF_PSS_DEC_ERR : d == TypedDecoder::DEC_FOLD ? RF_PSS_FOLD : 0u;
+          }
+          h.flags |= RF_PSS_DONE | f;
         }
         auto it = ns_set.find(h.ns);
         h.nsl = it == ns_set.end() ? NONE : it->second;

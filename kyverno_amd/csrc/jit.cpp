@@ -1601,10 +1601,12 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
            "  kyv::JitWalker" << gi << " wk{false};\n"
            "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"
            "}\n";
-  // fused kernels: one workgroup (one wave) per match wave of the batch
+  // fused kernels: one workgroup (one wave) per match wave of the batch. A fused kernel holds every direct rule of its
+  // group inline, so the light group's 8-waves target (64 VGPRs) would spill (round-4 C3 profile: 94-128 VGPR spills,
+  // 5 GB of scratch writes per evaluation): fused kernels get their own target
+  src << "#ifndef KYV_JIT_WPE_FUSED\n#define KYV_JIT_WPE_FUSED 4\n#endif\n";
   for (size_t gi : fused_groups)
-    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu("
-        << (gwpe[gi] == -2 ? "KYV_JIT_WPE_LIGHT" : "KYV_JIT_WPE") << ")))\n"
+    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE_FUSED)))\n"
            "kyv_jit_fused_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t nwaves) {\n"
            "  kyv::JitFused" << gi << " f;\n"
            "  kyv::walk_fused(*vp, o, nwaves, f);\n"

@@ -1,6 +1,7 @@
 // Host-side objects behind the C-ABI handles (kyv_ruleset / kyv_batch / kyv_results).
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -135,6 +136,18 @@ struct Ruleset {
   // device copies (one per device, lazily uploaded)
   std::vector<void*> dev;
   ~Ruleset();
+};
+
+// whole-object typed decode of getSpec (validation.go:481-532; typed.cpp, types in k8s_types.h), per batch: the
+// schema's field names resolved to the batch dictionary once
+struct TypedDecoder {
+  enum Target { POD = 0, DEPLOYMENT = 1, CRONJOB = 2 };
+  explicit TypedDecoder(const std::function<uint32_t(const std::string&)>& find_sid);
+  // json.Unmarshal of the resource (node table R, dictionary strs) into the target type: DEC_OK, DEC_ERR, or DEC_FOLD
+  // (it succeeds, some key matching its field only case-insensitively)
+  enum Outcome { DEC_OK = 0, DEC_ERR = 1, DEC_FOLD = 2 };
+  int decode(const Node* R, const std::vector<std::string>& strs, int target) const;
+  std::unordered_map<uint32_t, uint32_t> name_of_sid;  // dictionary id -> schema field name index
 };
 
 struct Batch {

@@ -105,6 +105,9 @@ enum ResFlag : uint32_t {
   // the flattener when the ruleset has PodSecurity rules (RF_PSS_DONE): RF_PSS_DEC_ERR = it does not decode
   RF_PSS_DONE = 1u << 9,
   RF_PSS_DEC_ERR = 1u << 10,
+  // it decodes, but some key of the object matched its Go field only case-insensitively (encoding/json's fold match):
+  // the checks read exact keys, so the resource's PodSecurity pairs go back to the caller (ST_FALLBACK)
+  RF_PSS_FOLD = 1u << 19,
 };
 // the same four metadata flags (NONE, NOTMAP, LAB_BAD, ANN_BAD as consecutive bits) for the pod templates of the
 // autogen'd rules: spec.template.metadata at RF_TMETA1_SHIFT, spec.jobTemplate.spec.template.metadata at

@@ -720,6 +720,7 @@ KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const
   if (!(h.flags & RF_PSS_DONE) || pd.cols == NONE || pd.nexcl != 0 || !v.colv || h.nnodes >= (1u << COL_TYPE_SHIFT))
     return ST_NONE;
   if (h.flags & RF_PSS_DEC_ERR) return ST_ERROR;
+  if (h.flags & RF_PSS_FOLD) return KYV_WHY(FBW_COND), ST_FALLBACK;
   const uint32_t pos = h.kind == KSID(POD) ? 0u
                      : (h.kind == KSID(DAEMONSET) || h.kind == KSID(DEPLOYMENT) || h.kind == KSID(JOB) ||
                         h.kind == KSID(STATEFULSET) || h.kind == KSID(REPLICASET) || h.kind == KSID(RC)) ? 1u
@@ -758,6 +759,7 @@ KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const R
   const uint8_t ps = pss_pod(R, h.kind, !done, &meta, &spec);
   if (ps != ST_NONE) return ps;
   if (done && (h.flags & RF_PSS_DEC_ERR)) return ST_ERROR;
+  if (done && (h.flags & RF_PSS_FOLD)) return KYV_WHY(FBW_COND), ST_FALLBACK;
   PodView pv;
   pv.meta = meta;
   pv.spec = spec;

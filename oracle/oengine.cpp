@@ -18,6 +18,7 @@
 #include "goutil.h"
 #include "ocond.h"
 #include "opss.h"
+#include "otyped.h"
 #include "ovalidate.h"
 
 namespace orc {
@@ -1112,6 +1113,23 @@ static RuleResult validate_rule_body(const VP& rule, const VP& resource) {
         return v;
       };
       static const std::set<std::string> ctl = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet", "ReplicationController"};
+      // getSpec's json.Unmarshal of the whole resource (validation.go:481-532) comes before EvaluatePod's version
+      // parse: a type error anywhere in the object is the rule's error (otyped.cpp, parity unpinned)
+      {
+        bool folded = false;
+        const std::string terr = typed_decode_error(resource, kind, &folded);
+        if (!terr.empty()) {
+          out.status = "error";
+          out.message = "Error while getting new resource: " + terr;
+          out.message_unpinned = true;
+          return out;
+        }
+        if (folded) {  // a case-folded key decodes into its field; the checks below read exact keys
+          out.status = "unsupported";
+          out.message = "podSecurity: case-folded keys";
+          return out;
+        }
+      }
       VP outerMeta = step(resource, "metadata");
       if (ctl.count(kind)) {
         VP tpl = step(step(resource, "spec"), "template");

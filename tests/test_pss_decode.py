@@ -2,9 +2,9 @@
 resource into corev1.Pod / appsv1.Deployment / batchv1.CronJob) beyond the fields the checks read: a type error in a
 commonly set field -- env[].value / name / valueFrom, command / args items, workingDir, imagePullPolicy,
 nodeSelector values, serviceAccountName, restartPolicy, terminationGracePeriodSeconds, activeDeadlineSeconds -- is a
-decode error (rule status error), on the device as in the oracle's restatement (oracle/opss.cpp dec_pod). No
-reference fixture holds such an object (the API server rejects them): parity unpinned beyond the restatement; a
-type error in a field neither side decodes still gives pass / fail on both."""
+decode error (rule status error), on the device as in the oracle's restatement (oracle/opss.cpp dec_pod,
+oracle/otyped.cpp for the whole object). No reference fixture holds such an object (the API server rejects them):
+parity unpinned beyond the restatement; keys no Go type declares are ignored on both sides."""
 import copy
 
 import pytest
@@ -56,7 +56,9 @@ def corpus():
             (_pod(spec_extra={"terminationGracePeriodSeconds": "30"}, kind=kind), K.ST_ERROR),
             (_pod(spec_extra={"terminationGracePeriodSeconds": 30, "activeDeadlineSeconds": 5}, kind=kind), K.ST_PASS),
             (_pod(spec_extra={"activeDeadlineSeconds": 1.5}, kind=kind), K.ST_ERROR),
-            (_pod(spec_extra={"hostname": 5}, kind=kind), K.ST_PASS),  # not decoded on either side (unpinned)
+            # the whole object is decoded (k8s_types.h, test_typed_decode.py): spec.hostname is a string field
+            (_pod(spec_extra={"hostname": 5}, kind=kind), K.ST_ERROR),
+            (_pod(spec_extra={"notAField": 5}, kind=kind), K.ST_PASS),  # unknown keys are ignored
         ]
     return out
 
