@@ -21,6 +21,7 @@
 #include <map>
 #include <mutex>
 #include <utime.h>
+#include <set>
 #include <sstream>
 #include <unordered_map>
 #include <stdexcept>
@@ -151,6 +152,8 @@ struct Gen {
       default: break;
     }
   }
+  // the columns of scope `root`, in pc[] order
+  const std::vector<uint32_t>& scope_cols(uint32_t root) { scope(root); return scope_of[root]; }
   // preload of scope `root`'s columns at row expression `rowx` into array `name`
   // (`rd`: the column read, jself(w, ...) inside the walk, jc_col(v, ...) before the walker state exists)
   std::string preload(uint32_t root, const std::string& name, const std::string& rowx, const char* rd = "jself(w, ") {
@@ -1523,6 +1526,33 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // the group's fused rules, back to back for one wave (walk_fused, kyv_wave.h): per rule the slice / kind-gate test
     // (uniform), the alternative loop of validatePatterns with the rule's roots as constants, the verdict bytes and the
     // staged failing-path records of chunk (rule, wave)
+    // cross-rule prefetch (KYV_FUSED_PF=1; off by default): the root-scope column loads of the next single-pattern
+    // rule issued before the current rule's walk. Measured on C3 (r4 A/B): the second register buffer spills (110
+    // VGPR spills at 5 waves/EU, 896 at 6) and the walk slows from 8.1 to 9.1 / 10.2 ms, so it is not generated
+    static const bool pf = getenv("KYV_FUSED_PF") && atoi(getenv("KYV_FUSED_PF")) != 0;
+    auto single = [&](size_t i) { return rs.rules[rule_roots[i].first].kind == RK_PATTERN; };
+    size_t npc = 1;
+    if (pf) {
+      std::set<uint32_t> shapes;
+      for (size_t i : fused)
+        if (single(i)) {
+          const uint32_t rr = rep_of[rule_roots[i].second[0]];
+          npc = std::max<size_t>(npc, g.scope_cols(rr).size());
+          if (!shapes.insert(rr).second) continue;
+          src << "static __device__ __forceinline__ void pre" << gi << "_" << rr << "(const View& v, uint32_t row, uint64_t* pc) {";
+          const auto& L = g.scope_cols(rr);
+          for (size_t q = 0; q < L.size(); q++) src << " pc[" << q << "] = jc_col(v, " << Gen::u(L[q]) << ", row);";
+          src << " }\n"
+                 "static __device__ __forceinline__ void rootw" << gi << "_" << rr
+              << "(const View& v, const Node* R, const ResHeader* hp, uint32_t row, uint32_t mbase, bool rootmap, bool walk,\n"
+                 "    PatOut& out, const uint64_t* pc) {\n"
+                 "  if (!walk) return;\n"
+                 "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
+                 "  Ret r = p" << rr << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
+                 "  jfinish(w, r, out);\n"
+                 "}\n";
+        }
+    }
     src << "struct JitFused" << gi << " {\n"
            "  __device__ __forceinline__ void run(const View& v, const DevOut& o, uint32_t nwaves, uint32_t w, uint32_t r,\n"
            "                                     bool active, uint32_t hflags, uint32_t hroot, const uint32_t* gw) {\n"
@@ -1532,12 +1562,29 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
            "    const uint32_t row = r < v.nres ? r : NONE;\n"
            "    const bool rootmap = (hflags & RF_ROOT_MAP) != 0;\n"
            "    (void)lane; (void)hp; (void)rootmap;\n";
-    for (size_t i : fused) {
+    if (pf) src << "    uint64_t pf0[" << npc << "], pf1[" << npc << "];\n";
+    // the block condition of fused rule i (slice range and a gated lane in the wave) and its prefetch
+    auto cond_of = [&](size_t i) {
+      const uint32_t k = rule_roots[i].first;
+      const std::string K = Gen::u(k);
+      return "(" + K + " >= o.rule_lo && " + K + " < o.rule_hi && __ballot(active && ((gw[" + std::to_string(k / 32) +
+             "] >> " + std::to_string(k % 32) + "u) & 1u)))";
+    };
+    auto prefetch = [&](size_t j, size_t i) {  // i = rule_roots index of fused rule number j
+      if (!pf || !single(i)) return;
+      src << "    if " << cond_of(i) << " pre" << gi << "_" << rep_of[rule_roots[i].second[0]] << "(v, row, " << (j % 2 ? "pf1" : "pf0")
+          << ");\n";
+    };
+    if (!fused.empty()) prefetch(0, fused[0]);
+    for (size_t j = 0; j < fused.size(); j++) {
+      const size_t i = fused[j];
+      if (j + 1 < fused.size()) prefetch(j + 1, fused[j + 1]);
       const uint32_t k = rule_roots[i].first;
       const RuleDesc& rd = rs.rules[k];
       const bool pat = rd.kind == RK_PATTERN;
       const uint32_t nalts = pat ? 1u : rd.nalts, alts = pat ? 1u : std::min<uint32_t>(rd.nalts, MAX_ALTS);
       const std::string K = Gen::u(k);
+      const std::string pbuf = pf && pat ? (j % 2 ? "pf1" : "pf0") : "";
       src << "    if (" << K << " >= o.rule_lo && " << K << " < o.rule_hi) {\n"
              "      const bool gated = active && ((gw[" << k / 32 << "] >> " << k % 32 << "u) & 1u);\n"
              "      if (__ballot(gated)) {\n"
@@ -1550,8 +1597,12 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "          switch (a) {\n";
       for (uint32_t a = 0; a < nalts; a++) {
         const uint32_t root = rule_roots[i].second[a];
-        src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
-            << ", rootmap, wk, po); break;\n";
+        if (!pbuf.empty())
+          src << "            case " << a << "u: rootw" << gi << "_" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+              << ", rootmap, wk, po, " << pbuf << "); break;\n";
+        else
+          src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+              << ", rootmap, wk, po); break;\n";
       }
       src << "            default: break;\n"
              "          }\n"
@@ -1602,9 +1653,10 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
            "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"
            "}\n";
   // fused kernels: one workgroup (one wave) per match wave of the batch. A fused kernel holds every direct rule of its
-  // group inline, so the light group's 8-waves target (64 VGPRs) would spill (round-4 C3 profile: 94-128 VGPR spills,
-  // 5 GB of scratch writes per evaluation): fused kernels get their own target
-  src << "#ifndef KYV_JIT_WPE_FUSED\n#define KYV_JIT_WPE_FUSED 4\n#endif\n";
+  // group inline, so the light group's 8-waves target (64 VGPRs) spills (round-4 C3 profile: 94-128 VGPR spills,
+  // 5 GB of scratch writes per evaluation): fused kernels get their own target. C3 walk (ms, r4 A/B): 8 waves 9.44,
+  // 7: 8.14, 6: 8.11 (29 spills), 5: 8.46, 4: 9.53 (no spills, half the waves)
+  src << "#ifndef KYV_JIT_WPE_FUSED\n#define KYV_JIT_WPE_FUSED 6\n#endif\n";
   for (size_t gi : fused_groups)
     src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE_FUSED)))\n"
            "kyv_jit_fused_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t nwaves) {\n"

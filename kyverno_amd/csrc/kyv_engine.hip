@@ -718,12 +718,14 @@ static size_t rule_slice_bytes(const RuleDesc& rd) {
   return sizeof(uint2) + 2 * alts * sizeof(FailRec) + 1;
 }
 
-// Budget for the per-slice buffers: KYV_SLICE_MB, else half of the free device memory, at most 48 GiB.
+// Budget for the per-slice buffers: KYV_SLICE_MB, else half of the free device memory, at most 128 GiB (288 GB of
+// HBM3E: C3 at 10 M resources is one slice, 56 GB; each further slice re-reads the headers and kind gates of every
+// match wave in the fused walk -- C3 walk 8.11 ms in two slices, 7.92 in one, r4 A/B)
 static size_t slice_budget() {
   if (const char* e = getenv("KYV_SLICE_MB")) return (size_t)std::max(1, atoi(e)) << 20;
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr == 0) fr = (size_t)64 << 30;
-  return std::min<size_t>(fr / 2, (size_t)48 << 30);
+  return std::min<size_t>(fr / 2, (size_t)128 << 30);
 }
 
 // Lay out the chunk schedules of one slice's walk kernels (see ChunkMap): runs of match waves with equal gated rule
