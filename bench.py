@@ -148,6 +148,42 @@ def time_gathers(batch, local, rank, world):
     return out
 
 
+def native_gathers(batch, local, rank, world, pg, res_offset):
+    """Report assembly over the device-resident results of the last timed evaluation with the
+    library's own RCCL communicator (kyv_comm_*; no torch in the process): all-gather of every rank's packed verdicts
+    and failing-path rows, each timed with HIP events on the communicator's stream after a warm-up gather, plus the
+    wall time of the call; max over ranks. Checked: this rank's gathered segment equals the host packing of its
+    resident verdicts, and every rank sees every segment with the checksum its owner computed."""
+    import zlib
+    import numpy as np
+    from kyverno_amd import scan
+    uid = scan.Comm.unique_id() if rank == 0 else None
+    if pg is not None:
+        box = [uid]
+        pg.broadcast_object_list(box, src=0)
+        uid = box[0]
+    comm = scan.Comm(uid, world, rank, local)
+    try:
+        comm.gather(batch, res_offset)  # warm-up: communicator setup, buffers
+        barrier(pg)
+        t0 = time.perf_counter()
+        st = comm.gather(batch, res_offset)
+        wall = time.perf_counter() - t0
+        barrier(pg)
+        own = scan.pack_status(batch.resident_status(device=local))
+        seg = comm.status_of(rank)
+        own_ok = bool(np.array_equal(seg[:own.size], own))
+        owners = all_gather_obj(pg, (rank, zlib.crc32(own.tobytes()), int(own.size)))
+        seen_ok = all(zlib.crc32(comm.status_of(q)[:n].tobytes()) == c for q, c, n in owners)
+    finally:
+        comm.close()
+    return {"backend": "RCCL (kyv_comm, library-owned communicator)", "world": world,
+            "verdicts_ms": st["status_ms"], "failures_ms": st["failures_ms"], "wall_ms": wall * 1e3,
+            "verdict_wire_bytes_per_rank": st["status_bytes_per_rank"], "failure_rows_total": st["failure_rows_total"],
+            "failure_rows_per_rank_max": st["failure_rows_per_rank_max"], "own_segment_ok": own_ok,
+            "segments_ok": bool(seen_ok)}
+
+
 def barrier(pg):
     if pg is not None:
         pg.barrier()
@@ -323,7 +359,7 @@ def shard_parity(policies, rs, data, nsl, timed_status, cap=100000):
 
 
 # device phase -> kernel-name prefixes of that phase in a rocprofv3 kernel trace
-PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::pss_kernel", "kyv::pss_map_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv::walk_kernel"),
+PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::pss_kernel", "kyv::pss_map_kernel", "kyv::match_deny_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv::walk_kernel"),
                  "compact": ("kyv::compact",), "hist": ("kyv::status_hist",)}
 
 
@@ -457,7 +493,7 @@ def main():
     ap.add_argument("--no-serial", action="store_true", help="profiling runs: skip the serialised phase-time evaluations")
     ap.add_argument("--gather", action="store_true",
                     help="time the RCCL all-gather of the resident results (loads torch first: KYV_TORCH_FIRST)")
-    ap.add_argument("--no-gather", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-gather", action="store_true", help="skip the report-assembly gather after the timed region")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         spawn_ranks(args.gpus)
@@ -556,8 +592,14 @@ def main():
     # report assembly of a multi-GPU scan: RCCL all-gather of every rank's verdicts and failing-path
     # rows straight from the device-resident results of the last timed evaluation, timed after the evaluation
     gathers = None
-    if args.gather:
+    if args.gather:  # torch.distributed's RCCL (scan.gather_*_device)
         gathers = time_gathers(batch, local, rank, world)
+        log("rank %d: device-resident gathers %s" % (rank, gathers))
+    elif not args.no_gather:  # the library's own RCCL communicator
+        try:
+            gathers = native_gathers(batch, local, rank, world, pg, lo)
+        except Exception as e:  # reported, never fatal for the timed line
+            gathers = {"error": str(e)[:300]}
         log("rank %d: device-resident gathers %s" % (rank, gathers))
 
     # end to end on this rank: JSON -> flatten -> H2D -> evaluate -> D2H of every verdict (walk kernel already loaded)
@@ -677,8 +719,11 @@ def main():
                 "verdicts_ms_max_rank": max(g.get("verdicts_ms", 0.0) for g in gather_ranks),
                 "failures_ms_max_rank": max(g.get("failures_ms", 0.0) for g in gather_ranks),
                 "ranks": gather_ranks,
+                "ok": all(g.get("own_segment_ok", True) and g.get("segments_ok", True) and "error" not in g
+                          for g in gather_ranks),
                 "note": "timed after the evaluation, outside `value`: RCCL all-gather of the packed verdicts and the "
-                        "failing-path rows from the device-resident results (kyverno_amd/scan.py)"},
+                        "failing-path rows from the device-resident results (kyv_comm_gather_results; --gather: "
+                        "torch.distributed's RCCL, kyverno_amd/scan.py)"},
             "host": {"generate_s": t_gen, "compile_s": t_compile, "flatten_s": t_flat,
                      "flatten_resources_per_s": batch.n / max(t_flat, 1e-9),
                      "first_eval_incl_upload_s": t_upload, "batch_device_bytes": batch.stats()["device_bytes"],

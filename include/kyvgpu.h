@@ -229,6 +229,30 @@ int64_t kyv_batch_export_status(const kyv_batch* b, int device, uint8_t* dst, si
 int64_t kyv_batch_copy_status(const kyv_batch* b, int device, uint64_t res0, uint64_t nres, uint8_t* dst, size_t cap);
 int64_t kyv_batch_export_failures(const kyv_batch* b, int device, int64_t res_offset, int64_t* dst, size_t cap_rows,
                                   void* stream);
+/* ---- multi-GPU report gather (one process per GPU). The library creates its own RCCL communicator:
+ * rank 0 calls kyv_comm_unique_id and hands the bytes to the other ranks out of band (a TCP store, a file), then
+ * every rank calls kyv_comm_init on its device. kyv_comm_gather_results all-gathers the device-resident results of
+ * the batch's last GPU evaluation on that device -- packed verdicts (kyv_batch_export_status layout, padded to the
+ * largest shard) and failing-path rows (kyv_batch_export_failures rows + res_offset, padded to the largest count) --
+ * into buffers the communicator owns, timed with HIP events on its stream. Replaces the per-controller report
+ * assembly of pkg/controllers/report (one process there; one rank per GPU here). */
+typedef struct kyv_comm kyv_comm;
+typedef struct {
+  double status_ms, failures_ms;       /* export + all-gather, HIP-event time on the communicator's stream (failures_ms -1:
+                                          a rule-sliced evaluation, whose failing-path rows are not resident) */
+  uint64_t status_bytes_per_rank;      /* padded verdict bytes per rank */
+  uint64_t failure_rows_per_rank_max;  /* padded rows per rank */
+  uint64_t failure_rows_total;
+} kyv_gather_stats;
+int kyv_comm_unique_id(uint8_t* id, size_t cap);  /* writes the 128-byte id (cap >= 128) */
+int kyv_comm_init(const uint8_t* id, size_t len, int nranks, int rank, int device, kyv_comm** out);
+void kyv_comm_free(kyv_comm* c);
+int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset, kyv_gather_stats* st);
+/* rank q's segment of the last gather, to host memory: its packed verdicts (bytes) / its failing-path rows (rows of
+   8 int64); dst NULL: only the size */
+int64_t kyv_comm_gathered_status(const kyv_comm* c, int rank, uint8_t* host_dst, size_t cap);
+int64_t kyv_comm_gathered_failures(const kyv_comm* c, int rank, int64_t* host_dst, size_t cap_rows);
+
 /* failing path of a single-pattern FAIL ("" otherwise); returns the full length */
 int64_t kyv_results_path(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res, uint32_t rule,
                          char* buf, size_t cap);

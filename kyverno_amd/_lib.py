@@ -63,8 +63,15 @@ EXPORTS = [
     "kyv_ruleset_jit_compile", "kyv_ruleset_jit_compile_ex", "kyv_results_rule_counts", "kyv_ruleset_compile_ex", "kyv_ruleset_rule_kinds",
     "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures", "kyv_ruleset_rule_flags",
     "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase", "kyv_results_alg_bytes_class", "kyv_batch_export_status", "kyv_batch_copy_status",
-    "kyv_batch_export_failures",
+    "kyv_batch_export_failures", "kyv_comm_unique_id", "kyv_comm_init", "kyv_comm_free", "kyv_comm_gather_results",
+    "kyv_comm_gathered_status", "kyv_comm_gathered_failures",
 ]
+
+
+class GatherStats(ctypes.Structure):
+    _fields_ = [("status_ms", ctypes.c_double), ("failures_ms", ctypes.c_double),
+                ("status_bytes_per_rank", ctypes.c_uint64), ("failure_rows_per_rank_max", ctypes.c_uint64),
+                ("failure_rows_total", ctypes.c_uint64)]
 
 _lib = None
 
@@ -105,6 +112,15 @@ def lib():
     L.kyv_batch_copy_status.restype = i64
     L.kyv_batch_export_failures.argtypes = [vp, ctypes.c_int, i64, vp, sz, vp]
     L.kyv_batch_export_failures.restype = i64
+    L.kyv_comm_unique_id.argtypes = [vp, sz]
+    L.kyv_comm_init.argtypes = [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.kyv_comm_free.argtypes = [vp]
+    L.kyv_comm_free.restype = None
+    L.kyv_comm_gather_results.argtypes = [vp, vp, i64, ctypes.POINTER(GatherStats)]
+    L.kyv_comm_gathered_status.argtypes = [vp, ctypes.c_int, vp, sz]
+    L.kyv_comm_gathered_status.restype = i64
+    L.kyv_comm_gathered_failures.argtypes = [vp, ctypes.c_int, vp, sz]
+    L.kyv_comm_gathered_failures.restype = i64
     L.kyv_ruleset_rule_flags.argtypes = [vp, u32]
     L.kyv_ruleset_rule_flags.restype = u32
     L.kyv_ruleset_free.argtypes = [vp]

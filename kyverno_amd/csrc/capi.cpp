@@ -741,3 +741,167 @@ uint32_t kyv_results_pss_mask(const kyv_results* r, const kyv_ruleset* rs, uint3
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- multi-GPU report gather over RCCL
+// One process per GPU; the communicator is created by the library itself (no framework in the data path): rank 0
+// draws the unique id, the caller hands it to the other ranks out of band (bench.py: a gloo broadcast), every rank
+// calls kyv_comm_init on its device. kyv_comm_gather_results all-gathers the device-resident results of a batch's
+// last GPU evaluation: the packed verdicts (kyv_batch_export_status layout per rank, padded to the largest shard)
+// and the failing-path rows (count, then rows padded to the largest count), each into buffers the communicator owns,
+// timed with HIP events on its stream.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+struct kyv_comm {
+  ncclComm_t comm = nullptr;
+  int device = 0, rank = 0, nranks = 1;
+  hipStream_t stream = nullptr;
+  uint8_t* status = nullptr;   // [nranks][status_bytes]
+  size_t status_cap = 0, status_bytes = 0;
+  int64_t* rows = nullptr;     // [nranks][rows_max][8]
+  size_t rows_cap = 0, rows_max = 0;
+  std::vector<int64_t> row_counts;
+};
+
+namespace {
+int nccl_fail(ncclResult_t r, const char* what) {
+  return fail(KYV_EDEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+}
+#define KYV_NCCL(x) do { ncclResult_t r_ = (x); if (r_ != ncclSuccess) return nccl_fail(r_, #x); } while (0)
+#define KYV_HIPC(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail(KYV_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); } while (0)
+template <class T>
+int grow(T** p, size_t* cap, size_t n) {
+  if (n <= *cap && *p) return KYV_OK;
+  if (*p) KYV_HIPC(hipFree(*p));
+  *p = nullptr;
+  KYV_HIPC(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+  *cap = n;
+  return KYV_OK;
+}
+}  // namespace
+
+int kyv_comm_unique_id(uint8_t* id, size_t cap) {
+  if (!id || cap < sizeof(ncclUniqueId)) return fail(KYV_ERANGE, "unique id buffer too small");
+  ncclUniqueId u;
+  KYV_NCCL(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof u);
+  return KYV_OK;
+}
+
+int kyv_comm_init(const uint8_t* id, size_t len, int nranks, int rank, int device, kyv_comm** out) {
+  if (!id || !out || len < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(KYV_EINVAL, "bad communicator arguments");
+  auto* c = new kyv_comm();
+  c->device = device;
+  c->rank = rank;
+  c->nranks = nranks;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) { delete c; return fail(KYV_EDEVICE, std::string("comm stream: ") + hipGetErrorString(e)); }
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) { (void)hipStreamDestroy(c->stream); delete c; return nccl_fail(r, "ncclCommInitRank"); }
+  *out = c;
+  return KYV_OK;
+}
+
+void kyv_comm_free(kyv_comm* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->status) (void)hipFree(c->status);
+  if (c->rows) (void)hipFree(c->rows);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset, kyv_gather_stats* st) {
+  if (!c || !b || !st) return fail(KYV_EINVAL, "null argument");
+  try {
+    KYV_HIPC(hipSetDevice(c->device));
+    *st = kyv_gather_stats{};
+    hipEvent_t e0, e1, e2;
+    KYV_HIPC(hipEventCreate(&e0));
+    KYV_HIPC(hipEventCreate(&e1));
+    KYV_HIPC(hipEventCreate(&e2));
+    struct Ev { hipEvent_t a, b, c; ~Ev() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); (void)hipEventDestroy(c); } } ev{e0, e1, e2};
+    const int n = c->nranks;
+    // sizes of every rank (one small all-gather): verdict bytes and failing-path rows
+    // a rule-sliced evaluation keeps no resident failing-path rows (they were gathered per slice on the host): its
+    // rows are not part of the gather (failures_ms = -1)
+    bool rows_ok = true;
+    int64_t nrows = 0;
+    try {
+      nrows = export_failures(*b->b, c->device, res_offset, nullptr, 0, c->stream);
+    } catch (std::exception&) {
+      rows_ok = false;
+    }
+    const int64_t mine[2] = {export_status(*b->b, c->device, nullptr, 0, c->stream), nrows};
+    int64_t* dsz = nullptr;
+    KYV_HIPC(hipMalloc((void**)&dsz, sizeof(int64_t) * 2 * (n + 1)));
+    struct Free { void* p; ~Free() { (void)hipFree(p); } } fz{dsz};
+    KYV_HIPC(hipMemcpyAsync(dsz + 2 * n, mine, sizeof mine, hipMemcpyHostToDevice, c->stream));
+    KYV_NCCL(ncclAllGather(dsz + 2 * n, dsz, 2, ncclInt64, c->comm, c->stream));
+    std::vector<int64_t> sz(2 * n);
+    KYV_HIPC(hipMemcpyAsync(sz.data(), dsz, sizeof(int64_t) * 2 * n, hipMemcpyDeviceToHost, c->stream));
+    KYV_HIPC(hipStreamSynchronize(c->stream));
+    size_t smax = 0, rmax = 0;
+    c->row_counts.assign(n, 0);
+    for (int q = 0; q < n; q++) {
+      smax = std::max<size_t>(smax, (size_t)sz[2 * q]);
+      rmax = std::max<size_t>(rmax, (size_t)sz[2 * q + 1]);
+      c->row_counts[q] = sz[2 * q + 1];
+      st->failure_rows_total += (uint64_t)sz[2 * q + 1];
+    }
+    if (int rc = grow(&c->status, &c->status_cap, smax * (n + 1))) return rc;
+    if (int rc = grow(&c->rows, &c->rows_cap, rmax * 8 * (n + 1))) return rc;
+    c->status_bytes = smax;
+    c->rows_max = rmax;
+    uint8_t* sendv = c->status + smax * n;  // this rank's packed verdicts, then the all-gather into [0, n * smax)
+    int64_t* sendr = c->rows + rmax * 8 * n;
+    KYV_HIPC(hipEventRecord(e0, c->stream));
+    if (smax) {
+      export_status(*b->b, c->device, sendv, smax, c->stream);
+      KYV_NCCL(ncclAllGather(sendv, c->status, smax, ncclUint8, c->comm, c->stream));
+    }
+    KYV_HIPC(hipEventRecord(e1, c->stream));
+    if (rmax) {
+      if (rows_ok) export_failures(*b->b, c->device, res_offset, sendr, rmax, c->stream);
+      KYV_NCCL(ncclAllGather(sendr, c->rows, rmax * 8, ncclInt64, c->comm, c->stream));
+    }
+    KYV_HIPC(hipEventRecord(e2, c->stream));
+    KYV_HIPC(hipStreamSynchronize(c->stream));
+    float t0 = 0, t1 = 0;
+    KYV_HIPC(hipEventElapsedTime(&t0, e0, e1));
+    KYV_HIPC(hipEventElapsedTime(&t1, e1, e2));
+    st->status_ms = t0;
+    st->failures_ms = rows_ok ? t1 : -1.0;
+    st->status_bytes_per_rank = smax;
+    st->failure_rows_per_rank_max = rmax;
+    return KYV_OK;
+  } catch (std::exception& e) {
+    return fail(KYV_EINVAL, e.what());
+  }
+}
+
+int64_t kyv_comm_gathered_status(const kyv_comm* c, int rank, uint8_t* host_dst, size_t cap) {
+  if (!c || rank < 0 || rank >= c->nranks) return fail(KYV_EINVAL, "bad rank"), -1;
+  if (!host_dst) return (int64_t)c->status_bytes;
+  if (cap < c->status_bytes) return fail(KYV_ERANGE, "buffer too small"), -1;
+  if (hipSetDevice(c->device) != hipSuccess ||
+      hipMemcpy(host_dst, c->status + c->status_bytes * rank, c->status_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(KYV_EDEVICE, "copy of the gathered verdicts failed"), -1;
+  return (int64_t)c->status_bytes;
+}
+
+int64_t kyv_comm_gathered_failures(const kyv_comm* c, int rank, int64_t* host_dst, size_t cap_rows) {
+  if (!c || rank < 0 || rank >= c->nranks) return fail(KYV_EINVAL, "bad rank"), -1;
+  const size_t nr = (size_t)c->row_counts[rank];
+  if (!host_dst) return (int64_t)nr;
+  if (cap_rows < nr) return fail(KYV_ERANGE, "buffer too small"), -1;
+  if (nr && (hipSetDevice(c->device) != hipSuccess ||
+             hipMemcpy(host_dst, c->rows + c->rows_max * 8 * rank, nr * 8 * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess))
+    return fail(KYV_EDEVICE, "copy of the gathered rows failed"), -1;
+  return (int64_t)nr;
+}

@@ -49,6 +49,11 @@ void pss(bool exact, int wpe, unsigned grid, hipStream_t s, const void* view, co
   hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), k, w0);
   check(hipGetLastError());
 }
+void match_deny(unsigned grid, hipStream_t s, const void* view, const void* devout, const uint32_t* mrules, uint32_t nm) {
+  using namespace kyv_acct;
+  hipLaunchKernelGGL(match_deny_kernel, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), mrules, nm);
+  check(hipGetLastError());
+}
 void pss_map(unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0) {
   using namespace kyv_acct;
   hipLaunchKernelGGL(pss_map_kernel, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), k, w0);

@@ -197,6 +197,7 @@ struct SliceSched {
   uint32_t* rbase = nullptr;     // [k1 - k0] first staging slot of each rule (slice-local)
   uint32_t* mrules = nullptr;    // rules of the slice the match phase evaluates (direct-walk rules excluded):
   uint32_t nmw = 0;              // leading rules of mrules on match_walk_kernel (pattern rules: match only)
+  uint32_t nmd = 0;              // then deny rules without JMESPath on match_deny_kernel
   uint32_t nm = 0, nmj = 0, nmc = 0;  // then [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
                                  // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
   std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
@@ -840,6 +841,14 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       }
       if (lo < hi) sl.pw.push_back(make_uint3(q, lo, hi - lo));
     }
+    // plain deny rules: match_deny_kernel (KYV_DENY_KERNEL=0: the light match kernel)
+    static const bool deny_k = !getenv("KYV_DENY_KERNEL") || atoi(getenv("KYV_DENY_KERNEL")) != 0;
+    std::vector<uint32_t> md;
+    if (deny_k) {
+      std::vector<uint32_t> rest;
+      for (uint32_t q : mr) (rs.rules[q].kind == RK_DENY ? md : rest).push_back(q);
+      mr.swap(rest);
+    }
     const size_t nlight = mr.size();
     // KYV_JC_ONLY=k1,k2,...: timing experiments only (the compiled condition kernel runs just those rules; the
     // other condition rules' verdicts are left unset)
@@ -867,7 +876,9 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     sl.nmj = (uint32_t)(mr.size() - nlight);
     sl.nmc = (uint32_t)cj.size();
     mr.insert(mr.end(), cj.begin(), cj.end());
-    sl.nmw = (uint32_t)mw.size();  // device list: [match_walk_kernel rules][light][JMESPath][compiled]
+    sl.nmw = (uint32_t)mw.size();  // device list: [match_walk_kernel rules][deny][light][JMESPath][compiled]
+    sl.nmd = (uint32_t)md.size();
+    mr.insert(mr.begin(), md.begin(), md.end());
     mr.insert(mr.begin(), mw.begin(), mw.end());
     dfree(sl.mrules);
     sl.mrules = nullptr;
@@ -1100,15 +1111,21 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const uint32_t*)sl.mrules,
                                 sl.nmw);
       }
+      if (sl.nmd) {
+        if (acct) kyvacct::match_deny(grid.x, stream, d.view, &o, sl.mrules + sl.nmw, sl.nmd);
+        else hipLaunchKernelGGL(match_deny_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o,
+                                (const uint32_t*)sl.mrules + sl.nmw, sl.nmd);
+      }
+      const uint32_t ml0 = sl.nmw + sl.nmd;
       if (sl.nm) {
-        if (acct) kyvacct::match(false, grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw, sl.nm);
+        if (acct) kyvacct::match(false, grid.x, stream, d.view, &o, &d.wl, sl.mrules + ml0, sl.nm);
         else hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
-                                (const uint32_t*)sl.mrules + sl.nmw, sl.nm);
+                                (const uint32_t*)sl.mrules + ml0, sl.nm);
       }
       if (sl.nmj) {
-        if (acct) kyvacct::match(true, grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw + sl.nm, sl.nmj);
+        if (acct) kyvacct::match(true, grid.x, stream, d.view, &o, &d.wl, sl.mrules + ml0 + sl.nm, sl.nmj);
         else hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
-                                (const uint32_t*)sl.mrules + sl.nmw + sl.nm, sl.nmj);
+                                (const uint32_t*)sl.mrules + ml0 + sl.nm, sl.nmj);
       }
       {
         // C2 (round 3, map walk inlined): 4 0.586, 6 0.587, 8 0.514 ms; the column-only kernel at 6 has no scratch

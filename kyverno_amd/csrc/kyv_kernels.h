@@ -62,6 +62,46 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_
   }
 }
 
+// Deny rules whose conditions need no JMESPath (plain request.object operands; C5's 50 deny / precondition policies):
+// pair_match, then the preconditions and deny programs of validateDeny (validation.go:281-288, 437-464), without
+// the PodSecurity call and work-list code of match_kernel's dispatch, whose call frame and register need spilled the
+// rule loop (C5 round 4: match_kernel<false> 4.47 ms, 5.3 GB of scratch writes per evaluation)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_MATCH_WPE)))
+match_deny_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restrict__ mrules, uint32_t nm) {
+  const View& v = *vp;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t r = blockIdx.x * BLOCK + lane;
+  const bool active = r < v.nres;
+  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
+  if (active) KYV_ACCT_ADD(0, 4);  // header: kind class
+  (void)lane;
+  for (uint32_t mi = 0; mi < nm; mi++) {
+    const uint32_t k = mrules[mi];
+    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+    if (!__ballot(gated)) continue;
+    if (!gated) continue;
+    const RuleDesc& rd = v.rules[k];
+    uint8_t st = ST_NONE;
+    if (pair_match(v, r, rd, &st)) {
+      const NodeTab R{v.nodes + v.hdr[r].root};
+      KYV_ACCT_ADD(0, 4);  // header: root
+      uint32_t ec, es, eg;
+      int c = CR_TRUE;
+      if (rd.pre != NONE) c = eval_prog<false>(v, R, rd.pre, &ec, &es, &eg, NONE, r);
+      if (c == CR_FB) st = (KYV_WHY(FBW_COND), ST_FALLBACK);
+      else if (c == CR_PANIC) st = ST_PANIC;
+      else if (c == CP_ERROR) st = ST_ERROR | ST_MARK_PRE;
+      else if (c == CR_FALSE) st = ST_SKIP | ST_MARK_PRE;
+      else {
+        c = eval_prog<false>(v, R, rd.root, &ec, &es, &eg, NONE, r);
+        st = c == CR_FB ? (KYV_WHY(FBW_COND), ST_FALLBACK) : c == CR_PANIC ? ST_PANIC : c == CP_ERROR ? ST_ERROR
+           : c == CR_TRUE ? ST_FAIL : ST_PASS;
+      }
+    }
+    if (st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
+  }
+}
+
 // Pattern / anyPattern rules without preconditions (and compile-time fallback rules): the match phase is only
 // pair_match (kind gate, match / exclude program, PolicyException candidates) and the work-list append, so this
 // kernel carries none of the dispatch code (conditions, PodSecurity calls) whose register need made the rule loop

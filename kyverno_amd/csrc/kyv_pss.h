@@ -523,15 +523,26 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
   // one pass over the annotations: the appArmor and pod seccomp annotation checks, and whether any key carries the
   // container seccomp prefix (the per-container check below then runs only for such pods)
   bool annSecC = false;
-  if (annMap)
-    for (uint32_t q = 0; q < R[ann].b; q++) {
-      const Node& e = R[R[ann].a + q];
-      const uint32_t key = node_key(e), val = node_type(e) == N_STR ? e.a : SID_EMPTY;
-      if (has_pfx(v, key, SF_PFX_APPARMOR) && val != KSID(RUNTIME_DEFAULT_PROFILE) && !has_pfx(v, val, SF_PFX_LOCALHOST))
+  // four entries per step: their node rows, then their keys' flag words, as independent loads (a loop of one entry
+  // per iteration is a chain of two dependent loads per annotation)
+  const uint32_t nann = annMap ? R[ann].b : 0u, ann0 = annMap ? R[ann].a : 0u;
+  for (uint32_t q = 0; q < nann; q += 4) {
+    Node e[4];
+    uint32_t kf[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) e[j] = q + j < nann ? R[ann0 + q + j] : Node{N_NULL, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) kf[j] = q + j < nann ? v.str_flags[node_key(e[j])] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      if (q + j >= nann) break;
+      const uint32_t key = node_key(e[j]), val = node_type(e[j]) == N_STR ? e[j].a : SID_EMPTY;
+      if ((kf[j] & SF_PFX_APPARMOR) && val != KSID(RUNTIME_DEFAULT_PROFILE) && !has_pfx(v, val, SF_PFX_LOCALHOST))
         fails |= 1u << PS_APPARMOR;
       if (key == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = true;
-      if (has_pfx(v, key, SF_PFX_SECCOMP_C)) annSecC = true;
+      if (kf[j] & SF_PFX_SECCOMP_C) annSecC = true;
     }
+  }
 
   for (uint32_t l = 0; l < PSS_NLISTS; l++) {
     const uint32_t* L = T + PC_LISTS + l * PCL_COUNT;
@@ -616,20 +627,37 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
       pcol(v, T[PC_HOSTIPC], row).t == N_TRUE)
     fails |= 1u << PS_HOSTNS;
   const PCol vols = pcol(v, T[PC_VOLUMES], row);
-  if (vols.i != NONE && vols.t == N_ARR)
-    for (uint32_t i = 0; i < R[vols.i].b; i++) {
-      const uint32_t vn = R[vols.i].a + i;
+  // two volumes per step, and each volume's first four entries (name and source) with them: the loads of one step
+  // are independent of each other
+  const uint32_t nvol = vols.i != NONE && vols.t == N_ARR ? R[vols.i].b : 0u, vol0 = nvol ? R[vols.i].a : 0u;
+  auto vol_entry = [&](const Node& e, bool* okv) {
+    if (node_type(e) == N_NULL) return;
+    const uint32_t k = node_key(e);
+    if (k == VSID(hostPath)) fails |= 1u << PS_HOSTPATH;
+    if (k >= SID_FIRST_FREE + K_COUNT && k < SID_FIRST_FREE + K_COUNT + V_ALLOWED) *okv = true;
+  };
+  for (uint32_t i = 0; i < nvol; i += 2) {
+    Node vn[2];
+#pragma unroll
+    for (uint32_t j = 0; j < 2; j++) vn[j] = i + j < nvol ? R[vol0 + i + j] : Node{N_NULL, 0, 0, 0};
+    Node en[2][4];
+#pragma unroll
+    for (uint32_t j = 0; j < 2; j++)
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++)
+        en[j][q] = node_type(vn[j]) == N_MAP && q < vn[j].b ? R[vn[j].a + q] : Node{N_NULL, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < 2; j++) {
+      if (i + j >= nvol) break;
       bool okv = false;
-      if (node_type(R[vn]) == N_MAP)
-        for (uint32_t q = 0; q < R[vn].b; q++) {
-          const Node& e = R[R[vn].a + q];
-          if (node_type(e) == N_NULL) continue;
-          const uint32_t k = node_key(e);
-          if (k == VSID(hostPath)) fails |= 1u << PS_HOSTPATH;
-          if (k >= SID_FIRST_FREE + K_COUNT && k < SID_FIRST_FREE + K_COUNT + V_ALLOWED) okv = true;
-        }
+      if (node_type(vn[j]) == N_MAP) {
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) vol_entry(en[j][q], &okv);
+        for (uint32_t q = 4; q < vn[j].b; q++) vol_entry(R[vn[j].a + q], &okv);
+      }
       if (!okv) fails |= 1u << PS_RVOLUMES;
     }
+  }
   if (portsBad) fails |= 1u << PS_HOSTPORTS;
   if (privBad) fails |= 1u << PS_PRIVILEGED;
   if (procBad) fails |= 1u << PS_PROCMOUNT;

@@ -333,3 +333,77 @@ def gather_failures_device(batch, res_offset, group=None, device=None, tensor=Fa
     parts, _ = _all_gather_var(t[:n], group, dist, torch)
     full = _sort_rows(torch.cat(parts, dim=0))
     return full if tensor else full.cpu().numpy()
+
+
+class Comm:
+    """The library's own RCCL communicator (kyv_comm_*, include/kyvgpu.h): report assembly of a one-process-per-GPU
+    scan with no framework on the device path. Rank 0 draws the id (`Comm.unique_id()`), the caller hands it to the
+    other ranks out of band (bench.py: a gloo broadcast), and every rank builds `Comm(id, nranks, rank, device)`.
+    `gather(batch, res_offset)` all-gathers the device-resident results of the batch's last GPU evaluation (packed
+    verdicts, failing-path rows) into communicator-owned device buffers and returns their HIP-event times."""
+
+    def __init__(self, uid, nranks, rank, device):
+        import ctypes
+        L = K.lib()
+        self._h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+        K.check(L.kyv_comm_init(buf, len(uid), int(nranks), int(rank), int(device), ctypes.byref(self._h)))
+        self.nranks, self.rank, self.device = int(nranks), int(rank), int(device)
+
+    @staticmethod
+    def unique_id():
+        import ctypes
+        buf = ctypes.create_string_buffer(128)
+        K.check(K.lib().kyv_comm_unique_id(buf, 128))
+        return bytes(buf.raw[:128])
+
+    def gather(self, batch, res_offset=0):
+        import ctypes
+        st = K.GatherStats()
+        K.check(K.lib().kyv_comm_gather_results(self._h, batch.h, int(res_offset), ctypes.byref(st)))
+        return {"status_ms": st.status_ms, "failures_ms": st.failures_ms,
+                "status_bytes_per_rank": int(st.status_bytes_per_rank),
+                "failure_rows_per_rank_max": int(st.failure_rows_per_rank_max),
+                "failure_rows_total": int(st.failure_rows_total)}
+
+    def status_of(self, q):
+        """rank q's packed verdicts from the last gather (kyv_batch_export_status layout, padded)"""
+        L = K.lib()
+        n = L.kyv_comm_gathered_status(self._h, int(q), None, 0)
+        out = np.empty(max(n, 0), dtype=np.uint8)
+        if n > 0 and L.kyv_comm_gathered_status(self._h, int(q), out.ctypes.data, n) != n:
+            raise K.KyvError(K.lib().kyv_last_error().decode())
+        return out
+
+    def failures_of(self, q):
+        """rank q's failing-path rows from the last gather: int64 [rows, 8]"""
+        L = K.lib()
+        n = L.kyv_comm_gathered_failures(self._h, int(q), None, 0)
+        out = np.empty((max(n, 0), 8), dtype=np.int64)
+        if n > 0 and L.kyv_comm_gathered_failures(self._h, int(q), out.ctypes.data, n) != n:
+            raise K.KyvError(K.lib().kyv_last_error().decode())
+        return out
+
+    def close(self):
+        if self._h:
+            K.lib().kyv_comm_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pack_status(status):
+    """host packing of input-order verdict bytes [rules][n] into the kyv_batch_export_status layout (low nibble =
+    even resource) -- the checker of a gathered segment"""
+    st = np.asarray(status, dtype=np.uint8) & 7
+    rules, n = st.shape
+    half = (n + 1) // 2
+    out = np.zeros((rules, half), dtype=np.uint8)
+    out[:, :] = st[:, 0::2]
+    if n > 1:
+        out[:, :n // 2] |= (st[:, 1::2] << 4).astype(np.uint8)
+    return out.reshape(-1)

@@ -58,3 +58,39 @@ def test_device_resident_gather_rccl():
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     assert "gather ok" in r.stdout
+
+
+NATIVE = r"""
+import os, sys
+sys.path.insert(0, os.environ["ROOT"]); sys.path.insert(0, os.path.join(os.environ["ROOT"], "tests"))
+import numpy as np
+import cases
+from kyverno_amd import engine as E, scan as SC, synth
+docs, nsl = synth.mixed(3001, seed=92, edge=True)
+rs = E.Ruleset(cases.best_practices() + cases.quirk_policies())
+b = E.Batch(rs, docs, nsl)
+res = E.evaluate(rs, b, backend="gpu", device=0)
+comm = SC.Comm(SC.Comm.unique_id(), 1, 0, 0)
+st = comm.gather(b, 1000)
+st = comm.gather(b, 1000)  # a second gather reuses the communicator's buffers
+assert st["status_ms"] > 0 and st["status_bytes_per_rank"] == len(rs.rules) * ((b.n + 1) // 2), st
+packed = comm.status_of(0)
+assert np.array_equal(packed, SC.pack_status(np.asarray(res.status))), "gathered verdicts differ"
+rows = comm.failures_of(0)
+f = res.failures()
+want = sorted(zip((f["res"].astype(np.int64) + 1000).tolist(), f["rule"].tolist(), f["alt"].tolist(),
+                  f["path_template"].tolist(), map(tuple, f["idx"].tolist())))
+got = sorted((int(r[0]), int(r[1]), int(r[2]), int(r[3]), tuple(int(x) for x in r[4:8])) for r in rows)
+assert got == want and len(got) > 100 and st["failure_rows_total"] == len(got), (len(got), len(want), st)
+comm.close()
+print("native gather ok", packed.size, len(got), st)
+"""
+
+
+@pytest.mark.gpu
+def test_native_rccl_gather():
+    """the library's own RCCL communicator (kyv_comm_*): no torch in the process; a one-rank group on this box"""
+    env = dict(os.environ, ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", NATIVE], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "native gather ok" in r.stdout
