@@ -36,10 +36,109 @@ namespace kyv {
     if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
   } while (0)
 
+// ---------------------------------------------------------------- pinned staging
+// Host arrays live in pageable memory (the flattener's vectors). A pageable hipMemcpy moves them through the runtime's
+// own small staging buffers one chunk at a time; here they go through a per-process ring of pinned buffers instead:
+// chunk i is copied into its pinned slot by several host threads while chunks i-1, i-2 are in flight on the DMA
+// engine (hipMemcpyAsync), and a slot is reused only after its transfer's event has completed. The same ring serves
+// device-to-host copies of verdicts (DMA into the slot, then a parallel copy out).
+struct Staging {
+  static constexpr int NSLOT = 3;
+  static constexpr size_t CHUNK = (size_t)64 << 20;
+  std::mutex mu;
+  void* buf[NSLOT] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev[NSLOT] = {nullptr, nullptr, nullptr};
+  int dev = -1;
+  bool ok = false;
+  bool init(int device) {
+    if (ok && dev == device) return true;
+    release();
+    dev = device;
+    for (int i = 0; i < NSLOT; i++) {
+      if (hipHostMalloc(&buf[i], CHUNK, hipHostMallocDefault) != hipSuccess) { release(); return false; }
+      if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) { release(); return false; }
+    }
+    ok = true;
+    return true;
+  }
+  void release() {
+    for (int i = 0; i < NSLOT; i++) {
+      if (ev[i]) (void)hipEventSynchronize(ev[i]);  // no transfer still reads or writes the slot
+      if (buf[i]) (void)hipHostFree(buf[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+      buf[i] = nullptr;
+      ev[i] = nullptr;
+    }
+    ok = false;
+  }
+};
+static Staging g_staging;
+static bool staging_off() {
+  static const bool off = getenv("KYV_PINNED") && atoi(getenv("KYV_PINNED")) == 0;
+  return off;
+}
+// memcpy of n bytes with up to 8 threads (pageable source pages are touched once by the copy)
+static void par_memcpy(void* dst, const void* src, size_t n) {
+  const size_t per = (size_t)8 << 20;
+  const size_t nt = std::min<size_t>(8, (n + per - 1) / per);
+  if (nt <= 1) { memcpy(dst, src, n); return; }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; t++)
+    th.emplace_back([=] {
+      const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+      memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo);
+    });
+  for (auto& x : th) x.join();
+}
+// host -> device through the pinned ring on `stream` (pageable hipMemcpy when the ring is off or unavailable)
+static hipError_t staged_h2d(uint8_t* dev, const void* src, size_t n, hipStream_t stream) {
+  if (!n) return hipSuccess;
+  int device = 0;
+  hipError_t e = hipGetDevice(&device);
+  if (e != hipSuccess) return e;
+  std::unique_lock<std::mutex> lk(g_staging.mu);
+  if (staging_off() || !g_staging.init(device)) return hipMemcpy(dev, src, n, hipMemcpyHostToDevice);
+  static int slot = 0;
+  for (size_t off = 0; off < n; off += Staging::CHUNK) {
+    const size_t m = std::min(Staging::CHUNK, n - off);
+    if ((e = hipEventSynchronize(g_staging.ev[slot])) != hipSuccess) return e;  // the slot's last transfer is done
+    par_memcpy(g_staging.buf[slot], (const uint8_t*)src + off, m);
+    if ((e = hipMemcpyAsync(dev + off, g_staging.buf[slot], m, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
+    if ((e = hipEventRecord(g_staging.ev[slot], stream)) != hipSuccess) return e;
+    slot = (slot + 1) % Staging::NSLOT;
+  }
+  return hipSuccess;
+}
+// device -> host through the pinned ring: chunk i's DMA overlaps the copy-out of chunk i-1
+static hipError_t staged_d2h(void* dst, const uint8_t* dev, size_t n, hipStream_t stream) {
+  if (!n) return hipSuccess;
+  int device = 0;
+  hipError_t e = hipGetDevice(&device);
+  if (e != hipSuccess) return e;
+  std::unique_lock<std::mutex> lk(g_staging.mu);
+  if (staging_off() || !g_staging.init(device)) return hipMemcpy(dst, dev, n, hipMemcpyDeviceToHost);
+  const size_t nch = (n + Staging::CHUNK - 1) / Staging::CHUNK;
+  auto issue = [&](size_t c) -> hipError_t {
+    const int sl = (int)(c % Staging::NSLOT);
+    const size_t off = c * Staging::CHUNK, m = std::min(Staging::CHUNK, n - off);
+    hipError_t r = hipMemcpyAsync(g_staging.buf[sl], dev + off, m, hipMemcpyDeviceToHost, stream);
+    return r == hipSuccess ? hipEventRecord(g_staging.ev[sl], stream) : r;
+  };
+  for (size_t c = 0; c < nch && c < (size_t)Staging::NSLOT - 1; c++)
+    if ((e = issue(c)) != hipSuccess) return e;
+  for (size_t c = 0; c < nch; c++) {
+    const int sl = (int)(c % Staging::NSLOT);
+    if ((e = hipEventSynchronize(g_staging.ev[sl])) != hipSuccess) return e;
+    if (c + Staging::NSLOT - 1 < nch && (e = issue(c + Staging::NSLOT - 1)) != hipSuccess) return e;
+    const size_t off = c * Staging::CHUNK, m = std::min(Staging::CHUNK, n - off);
+    par_memcpy((uint8_t*)dst + off, g_staging.buf[sl], m);
+  }
+  return hipSuccess;
+}
+
 // ---------------------------------------------------------------- device images
 // Device-buffer layout of host arrays: offsets are assigned first (256-byte aligned, 16 zero bytes of slack after
-// each array), then the buffer is zeroed on the device and every array is copied straight from its host vector --
-// no host-side staging copy of the batch
+// each array), then the buffer is zeroed on the device and every array goes up through the pinned ring
 struct Packer {
   struct Part { size_t off; const void* src; size_t bytes; };
   std::vector<Part> parts;
@@ -53,10 +152,15 @@ struct Packer {
     return off;
   }
   hipError_t copy_to(uint8_t* dev) const {
-    hipError_t e = hipMemset(dev, 0, size);
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(dev, 0, size, s);
     for (auto& q : parts)
-      if (e == hipSuccess && q.bytes) e = hipMemcpy(dev + q.off, q.src, q.bytes, hipMemcpyHostToDevice);
-    return e;
+      if (e == hipSuccess && q.bytes) e = staged_h2d(dev + q.off, q.src, q.bytes, s);
+    hipError_t e2 = hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    return e != hipSuccess ? e : e2;
   }
 };
 
@@ -1296,7 +1400,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     if (copy_back) {
       auto t0 = std::chrono::steady_clock::now();
       out->status.resize(nres * nrules);
-      HIP_OK(hipMemcpy(out->status.data(), d.status, nres * nrules, hipMemcpyDeviceToHost));
+      HIP_OK(staged_d2h(out->status.data(), d.status, nres * nrules, d.stream));
       out->pss_fails.resize((size_t)d.npss * nres);
       if (d.npss) HIP_OK(hipMemcpy(out->pss_fails.data(), d.pss_fails, out->pss_fails.size() * 4, hipMemcpyDeviceToHost));
       if (multi) {
