@@ -1459,7 +1459,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     if (!heavy.empty()) { groups.push_back(heavy); gwpe.push_back(-1); }
   }
   const size_t ngroups = groups.size();
-  std::vector<size_t> fused_groups;  // groups with a fused kernel (kyv_jit_fused_<g>)
+  std::vector<std::pair<size_t, size_t>> fused_kernels;  // (group, part): kyv_jit_fused_<g>[p<part>]
   for (size_t gi = 0; gi < ngroups; gi++) {
     std::vector<uint32_t> roots, chunk_roots;  // every root of the group; those of its per-chunk (non-fused) rules
     std::vector<size_t> fused;                 // rule_roots indices of the group's fused rules
@@ -1525,66 +1525,33 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     if (fused.empty()) continue;
     // the group's fused rules, back to back for one wave (walk_fused, kyv_wave.h): per rule the slice / kind-gate test
     // (uniform), the alternative loop of validatePatterns with the rule's roots as constants, the verdict bytes and the
-    // staged failing-path records of chunk (rule, wave)
-    // cross-rule prefetch (KYV_FUSED_PF=1; off by default): the root-scope column loads of the next single-pattern
-    // rule issued before the current rule's walk. Measured on C3 (r4 A/B): the second register buffer spills (110
-    // VGPR spills at 5 waves/EU, 896 at 6) and the walk slows from 8.1 to 9.1 / 10.2 ms, so it is not generated
-    static const bool pf = getenv("KYV_FUSED_PF") && atoi(getenv("KYV_FUSED_PF")) != 0;
-    auto single = [&](size_t i) { return rs.rules[rule_roots[i].first].kind == RK_PATTERN; };
-    size_t npc = 1;
-    if (pf) {
-      std::set<uint32_t> shapes;
-      for (size_t i : fused)
-        if (single(i)) {
-          const uint32_t rr = rep_of[rule_roots[i].second[0]];
-          npc = std::max<size_t>(npc, g.scope_cols(rr).size());
-          if (!shapes.insert(rr).second) continue;
-          src << "static __device__ __forceinline__ void pre" << gi << "_" << rr << "(const View& v, uint32_t row, uint64_t* pc) {";
-          const auto& L = g.scope_cols(rr);
-          for (size_t q = 0; q < L.size(); q++) src << " pc[" << q << "] = jc_col(v, " << Gen::u(L[q]) << ", row);";
-          src << " }\n"
-                 "static __device__ __forceinline__ void rootw" << gi << "_" << rr
-              << "(const View& v, const Node* R, const ResHeader* hp, uint32_t row, uint32_t mbase, bool rootmap, bool walk,\n"
-                 "    PatOut& out, const uint64_t* pc) {\n"
-                 "  if (!walk) return;\n"
-                 "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
-                 "  Ret r = p" << rr << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
-                 "  jfinish(w, r, out);\n"
-                 "}\n";
-        }
-    }
-    src << "struct JitFused" << gi << " {\n"
-           "  __device__ __forceinline__ void run(const View& v, const DevOut& o, uint32_t nwaves, uint32_t w, uint32_t r,\n"
-           "                                     bool active, uint32_t hflags, uint32_t hroot, const uint32_t* gw) {\n"
-           "    const uint32_t lane = threadIdx.x & 63u;\n"
-           "    const Node* R = v.nodes + hroot;\n"
-           "    const ResHeader* hp = v.hdr + r;\n"
-           "    const uint32_t row = r < v.nres ? r : NONE;\n"
-           "    const bool rootmap = (hflags & RF_ROOT_MAP) != 0;\n"
-           "    (void)lane; (void)hp; (void)rootmap;\n";
-    if (pf) src << "    uint64_t pf0[" << npc << "], pf1[" << npc << "];\n";
-    // the block condition of fused rule i (slice range and a gated lane in the wave) and its prefetch
-    auto cond_of = [&](size_t i) {
-      const uint32_t k = rule_roots[i].first;
-      const std::string K = Gen::u(k);
-      return "(" + K + " >= o.rule_lo && " + K + " < o.rule_hi && __ballot(active && ((gw[" + std::to_string(k / 32) +
-             "] >> " + std::to_string(k % 32) + "u) & 1u)))";
-    };
-    auto prefetch = [&](size_t j, size_t i) {  // i = rule_roots index of fused rule number j
-      if (!pf || !single(i)) return;
-      src << "    if " << cond_of(i) << " pre" << gi << "_" << rep_of[rule_roots[i].second[0]] << "(v, row, " << (j % 2 ? "pf1" : "pf0")
-          << ");\n";
-    };
-    if (!fused.empty()) prefetch(0, fused[0]);
-    for (size_t j = 0; j < fused.size(); j++) {
-      const size_t i = fused[j];
-      if (j + 1 < fused.size()) prefetch(j + 1, fused[j + 1]);
+    // staged failing-path records of chunk (rule, wave). KYV_FUSED_SPLIT=n splits the group's fused rules into n
+    // kernels (contiguous runs; part p > 0 is kyv_jit_fused_<g>p<p>), each with the register need of its own rules.
+    // (Tried and removed, round 4: prefetching the next rule's root-scope columns into registers before the current
+    // rule's walk -- 110 VGPR spills at 5 waves/EU, 896 at 6; C3 walk 8.1 -> 9.1 / 10.2 ms.)
+    // C3 (r4 A/B, evaluation / walk ms): one kernel at 6 waves/EU 12.04 / 7.74; 2 parts at 8 waves 11.35 / 7.43; 3 at 8
+    // 11.25 / 7.34; 4 at 8 11.33 / 7.26 (smaller kernels: fewer spills at 8 waves, and they interleave with the
+    // condition kernels on the other stream)
+    const size_t nparts = std::max<size_t>(1, std::min<size_t>(fused.size(), getenv("KYV_FUSED_SPLIT") ? (size_t)atoi(getenv("KYV_FUSED_SPLIT")) : 3));
+    for (size_t pi = 0; pi < nparts; pi++) {
+      const std::vector<size_t> part(fused.begin() + fused.size() * pi / nparts, fused.begin() + fused.size() * (pi + 1) / nparts);
+      const std::string sname = "JitFused" + std::to_string(gi) + (pi ? "p" + std::to_string(pi) : std::string());
+      src << "struct " << sname << " {\n"
+             "  __device__ __forceinline__ void run(const View& v, const DevOut& o, uint32_t nwaves, uint32_t w, uint32_t r,\n"
+             "                                     bool active, uint32_t hflags, uint32_t hroot, const uint32_t* gw) {\n"
+             "    const uint32_t lane = threadIdx.x & 63u;\n"
+             "    const Node* R = v.nodes + hroot;\n"
+             "    const ResHeader* hp = v.hdr + r;\n"
+             "    const uint32_t row = r < v.nres ? r : NONE;\n"
+             "    const bool rootmap = (hflags & RF_ROOT_MAP) != 0;\n"
+             "    (void)lane; (void)hp; (void)rootmap;\n";
+      for (size_t j = 0; j < part.size(); j++) {
+      const size_t i = part[j];
       const uint32_t k = rule_roots[i].first;
       const RuleDesc& rd = rs.rules[k];
       const bool pat = rd.kind == RK_PATTERN;
       const uint32_t nalts = pat ? 1u : rd.nalts, alts = pat ? 1u : std::min<uint32_t>(rd.nalts, MAX_ALTS);
       const std::string K = Gen::u(k);
-      const std::string pbuf = pf && pat ? (j % 2 ? "pf1" : "pf0") : "";
       src << "    if (" << K << " >= o.rule_lo && " << K << " < o.rule_hi) {\n"
              "      const bool gated = active && ((gw[" << k / 32 << "] >> " << k % 32 << "u) & 1u);\n"
              "      if (__ballot(gated)) {\n"
@@ -1597,12 +1564,8 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "          switch (a) {\n";
       for (uint32_t a = 0; a < nalts; a++) {
         const uint32_t root = rule_roots[i].second[a];
-        if (!pbuf.empty())
-          src << "            case " << a << "u: rootw" << gi << "_" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
-              << ", rootmap, wk, po, " << pbuf << "); break;\n";
-        else
-          src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
-              << ", rootmap, wk, po); break;\n";
+        src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+            << ", rootmap, wk, po); break;\n";
       }
       src << "            default: break;\n"
              "          }\n"
@@ -1615,9 +1578,10 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "      }\n"
              "    }\n";
     }
-    src << "  }\n"
-           "};\n";
-    fused_groups.push_back(gi);
+      src << "  }\n"
+             "};\n";
+      fused_kernels.push_back(std::make_pair(gi, pi));
+    }
   }
   src << "}  // namespace kyv\n"
          "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n";
@@ -1653,16 +1617,22 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
            "  kyv::walk_chunks(*vp, o, wl, cm, wk);\n"
            "}\n";
   // fused kernels: one workgroup (one wave) per match wave of the batch. A fused kernel holds every direct rule of its
-  // group inline, so the light group's 8-waves target (64 VGPRs) spills (round-4 C3 profile: 94-128 VGPR spills,
-  // 5 GB of scratch writes per evaluation): fused kernels get their own target. C3 walk (ms, r4 A/B): 8 waves 9.44,
-  // 7: 8.14, 6: 8.11 (29 spills), 5: 8.46, 4: 9.53 (no spills, half the waves)
-  src << "#ifndef KYV_JIT_WPE_FUSED\n#define KYV_JIT_WPE_FUSED 6\n#endif\n";
-  for (size_t gi : fused_groups)
-    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE_FUSED)))\n"
-           "kyv_jit_fused_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t nwaves) {\n"
-           "  kyv::JitFused" << gi << " f;\n"
+  // group inline: as one kernel at the light group's 8-waves target (64 VGPRs) it spills (round-4 C3 profile: 94-128
+  // VGPR spills, 5 GB of scratch writes per evaluation; one kernel, C3 walk ms: 8 waves 9.44, 7: 8.14, 6: 8.11,
+  // 5: 8.46, 4: 9.53); split in parts (KYV_FUSED_SPLIT, above) each part fits 8 waves with a few spills
+  // (the group of wildcard-metadata rules keeps the walk's heavy target, KYV_JIT_WPE_FUSED_HEAVY = 4)
+  src << "#ifndef KYV_JIT_WPE_FUSED\n#define KYV_JIT_WPE_FUSED 8\n#endif\n"
+         "#ifndef KYV_JIT_WPE_FUSED_HEAVY\n#define KYV_JIT_WPE_FUSED_HEAVY 4\n#endif\n";
+  for (const auto& gp : fused_kernels) {
+    const std::string sfx = std::to_string(gp.first) + (gp.second ? "p" + std::to_string(gp.second) : std::string());
+    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu("
+        << (gwpe[gp.first] == -1 && std::count(gwpe.begin(), gwpe.end(), -2) ? "KYV_JIT_WPE_FUSED_HEAVY" : "KYV_JIT_WPE_FUSED")
+        << ")))\n"
+           "kyv_jit_fused_" << sfx << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t nwaves) {\n"
+           "  kyv::JitFused" << sfx << " f;\n"
            "  kyv::walk_fused(*vp, o, nwaves, f);\n"
            "}\n";
+  }
   return src.str();
 }
 

@@ -173,6 +173,7 @@ struct DevRuleset {
   hipModule_t jmod = nullptr;     // runtime-compiled walk kernels (jit.cpp) loaded on this device
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
   std::vector<hipFunction_t> ffns;  // kyv_jit_fused_<g> per rule group, or null (the group has no fused rule)
+  std::vector<std::vector<hipFunction_t>> fparts, afparts;  // its further parts kyv_jit_fused_<g>p<1..> (KYV_FUSED_SPLIT)
   std::vector<hipFunction_t> jconds;  // [rule] kyv_jit_cond_<k> (compiled deny / foreach rule k) or null
   bool jloaded = false;
   // the byte-accounting build of the same kernels (KYV_ACCT), loaded only by an accounting evaluation
@@ -779,6 +780,13 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
     HIP_OK(hipModuleGetFunction(&dr->jfns[g], dr->jmod, ("kyv_jit_walk_" + std::to_string(g)).c_str()));
     if (hipModuleGetFunction(&dr->ffns[g], dr->jmod, ("kyv_jit_fused_" + std::to_string(g)).c_str()) != hipSuccess)
       dr->ffns[g] = nullptr;
+    dr->fparts.resize(ng);
+    for (int p = 1; dr->ffns[g]; p++) {
+      hipFunction_t f = nullptr;
+      if (hipModuleGetFunction(&f, dr->jmod, ("kyv_jit_fused_" + std::to_string(g) + "p" + std::to_string(p)).c_str()) != hipSuccess)
+        break;
+      dr->fparts[g].push_back(f);
+    }
   }
   (void)hipGetLastError();
   dr->jconds.assign(rs.rules.size(), nullptr);
@@ -804,6 +812,11 @@ static bool ensure_jit_acct(Ruleset& rs, DevRuleset* dr) {
   for (size_t g = 0; g < dr->jfns.size(); g++) {
     HIP_OK(hipModuleGetFunction(&dr->afns[g], dr->amod, ("kyv_jit_walk_" + std::to_string(g)).c_str()));
     if (dr->ffns[g]) HIP_OK(hipModuleGetFunction(&dr->affns[g], dr->amod, ("kyv_jit_fused_" + std::to_string(g)).c_str()));
+    dr->afparts.resize(dr->jfns.size());
+    dr->afparts[g].assign(g < dr->fparts.size() ? dr->fparts[g].size() : 0, nullptr);
+    for (size_t p = 0; p < dr->afparts[g].size(); p++)
+      HIP_OK(hipModuleGetFunction(&dr->afparts[g][p], dr->amod,
+                                  ("kyv_jit_fused_" + std::to_string(g) + "p" + std::to_string(p + 1)).c_str()));
   }
   dr->aconds.assign(dr->jconds.size(), nullptr);
   for (size_t k = 0; k < dr->jconds.size(); k++)
@@ -1163,10 +1176,13 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipStreamSynchronize(stream));
     for (unsigned long long* dc : {acnt_lib, ajit ? dr->acnt : nullptr}) {
       if (!dc) continue;
-      HIP_OK(hipMemcpy(ahost.data(), dc, ahost.size() * 8, hipMemcpyDeviceToHost));
+      // on the evaluation stream (a non-blocking stream: null-stream copies / memsets would not order with its
+      // kernels, and a counter reset could land after the next phase's first adds)
+      HIP_OK(hipMemcpyAsync(ahost.data(), dc, ahost.size() * 8, hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipMemsetAsync(dc, 0, ahost.size() * 8, stream));
+      HIP_OK(hipStreamSynchronize(stream));
       for (int q = 0; q < 3; q++)
         for (uint32_t i = 0; i < KYV_ACCT_SLOTS; i++) c[q] += ahost[q * KYV_ACCT_SLOTS + i];
-      HIP_OK(hipMemset(dc, 0, ahost.size() * 8));
     }
     for (int q = 0; q < 3; q++) aclass[q] += c[q];
     return c;
@@ -1302,6 +1318,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         uint32_t nw = d.wl.nwaves;
         void* args[] = {(void*)&vp, (void*)&o, (void*)&nw};
         HIP_OK(hipModuleLaunchKernel(acct ? dr->affns[g] : dr->ffns[g], nw, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+        if (g < dr->fparts.size())
+          for (size_t p = 0; p < dr->fparts[g].size(); p++)
+            HIP_OK(hipModuleLaunchKernel(acct ? dr->afparts[g][p] : dr->fparts[g][p], nw, 1, 1, BLOCK, 1, 1, 0, stream,
+                                         args, nullptr));
       }
       uint64_t staged = 0;
       if (acct) { const auto c = acct_take(); aphase[2] += c[0] + c[1] + c[2]; staged = c[2]; }
