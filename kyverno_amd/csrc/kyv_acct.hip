@@ -2,6 +2,10 @@
 // kernel source as the product (kyv_kernels.h) compiled with KYV_ACCT, so every per-resource load and result store
 // adds its bytes to device counters (kyv_eval.h KYV_ACCT_ADD). The namespace is renamed so both builds link into one
 // library without sharing a symbol; kyv_engine.hip runs these only in an explicit accounting evaluation.
+// the label-selector check inlined into the statically compiled kernels: as an out-of-line call its callee-saved
+// registers went through scratch for every (resource, rule) pair with a selector (C4 round 4: 220 GB of scratch
+// writes per evaluation in match_walk_kernel; inlined: 86 VGPRs, no scratch)
+#define KYV_SEL_INLINE 1
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

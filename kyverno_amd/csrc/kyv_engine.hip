@@ -8,6 +8,10 @@
 //                 (kyv_wave.h) with no idle lanes from gated / non-matching pairs.
 // Verdicts are written rule-major (coalesced bytes); failing-path records are staged per walk chunk and compacted
 // without atomics (compact_*_kernel); verdict totals are one histogram pass over the status bytes.
+// the label-selector check inlined into the statically compiled kernels: as an out-of-line call its callee-saved
+// registers went through scratch for every (resource, rule) pair with a selector (C4 round 4: 220 GB of scratch
+// writes per evaluation in match_walk_kernel; inlined: 86 VGPRs, no scratch)
+#define KYV_SEL_INLINE 1
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

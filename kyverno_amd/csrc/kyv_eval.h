@@ -422,7 +422,12 @@ KYV_HD uint32_t ls_find(const LabelSet& s, uint32_t key) {
 }
 
 // CheckSelector incl. ReplaceInSelector (pkg/utils/match/labels.go:10-24, wildcards.go:13-50): 1 match, 0 no, -1 error
-KYV_BIG int check_selector(const View& v, const SelDesc& sd, const LabelSet& ls, bool* nd) {
+#ifdef KYV_SEL_INLINE
+KYV_HD __attribute__((always_inline))
+#else
+KYV_BIG
+#endif
+int check_selector(const View& v, const SelDesc& sd, const LabelSet& ls, bool* nd) {
   if (sd.invalid) return -1;
   int res = 1;
   for (uint32_t q = 0; q < sd.nreqs; q++) {
