@@ -1252,8 +1252,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
                                 (const uint32_t*)sl.mrules + ml0 + sl.nm, sl.nmj);
       }
       {
-        // C2 (round 3, map walk inlined): 4 0.586, 6 0.587, 8 0.514 ms; the column-only kernel at 6 has no scratch
-        static const int pwpe = getenv("KYV_PSS_WPE") ? atoi(getenv("KYV_PSS_WPE")) : 6;
+        // C2 (round 3, map walk inlined): 4 0.586, 6 0.587, 8 0.514 ms; round 4: the column-only kernel with the
+        // containers spread over the wave's lanes needs 41 VGPRs, no scratch at 8
+        static const int pwpe = getenv("KYV_PSS_WPE") ? atoi(getenv("KYV_PSS_WPE")) : 8;
         for (const uint3& c : sl.pw) {
           const bool ex = (rs.rules[c.x].flags & RD_GATE_EXACT) && rs.rules[c.x].match.mode != MM_NONE;
           auto kf = ex ? (pwpe == 4 ? pss_kernel<true, 4> : pwpe == 6 ? pss_kernel<true, 6> : pss_kernel<true, 8>)

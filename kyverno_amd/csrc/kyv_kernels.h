@@ -144,15 +144,23 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uin
 }
 
 // PodSecurity rules (without preconditions): one lane per resource over the match waves [w0, w0 + grid) of the rule's
-// kind gate, the match and the path-column checks inlined (eval_pss_cols). Pairs the column form does not cover
+// kind gate, the match and the path-column checks inlined. The per-container checks (pss_container_facts) run with
+// one container per lane across the wave -- the 64 pods' container lists concatenated, a lane's facts OR-ed into its
+// pod's word in LDS -- instead of each lane walking its pod's containers one after the other (the longest chain of
+// dependent loads in the kernel); each lane then combines its pod's facts with the pod-level checks. Pairs the column
+// form does not cover
 // (exclusion sub-pods, resources without path columns) are marked ST_PSS_MAP and finished by pss_map_kernel: the map
 // walk (eval_pss) is a call whose frame and spills would otherwise sit in this kernel's scratch and write traffic
 // (round 3 C2 profile: 13x write amplification). kExact: the rule's match block is its kind gate (RD_GATE_EXACT), no
-// match program compiled in; kWpe: occupancy target (KYV_PSS_WPE = 4 / 6 / 8 at run time; 6 by default: 72 VGPRs, no
-// scratch, 7 waves per SIMD)
+// match program compiled in; kWpe: occupancy target (KYV_PSS_WPE = 4 / 6 / 8 at run time; 8 by default: 41 VGPRs, no
+// scratch)
 template <bool kExact, int kWpe>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
 pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
+  // the wave's containers, one per lane (lists of all 64 pods concatenated): per list the pods' counts, exclusive
+  // prefix and first element row; per pod its resource root, pod position and the OR of its containers' facts
+  __shared__ uint32_t s_pre[PSS_NLISTS][BLOCK], s_eb[PSS_NLISTS][BLOCK];
+  __shared__ uint32_t s_root[BLOCK], s_pos[BLOCK], s_fact[BLOCK];
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
   const uint32_t r = (w0 + blockIdx.x) * BLOCK + lane;
@@ -160,6 +168,7 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
   if (r < v.nres) KYV_ACCT_ADD(0, 4);  // header: kind class
   if (!__ballot(gated)) return;
   const RuleDesc& rd = v.rules[k];
+  const PssDesc& pd = v.pss[rd.root];
   uint8_t st = ST_NONE;
   uint32_t pf = 0;
   bool m;
@@ -168,12 +177,62 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
   } else {
     m = gated && pair_match(v, r, rd, &st);
   }
+  const uint32_t* T = nullptr;
+  uint32_t hroot = 0;
   if (gated && m) {
     const ResHeader& h = v.hdr[r];
-    const NodeTab R{v.nodes + h.root};
     KYV_ACCT_ADD(0, 12);  // header: root, node count, flags
-    st = eval_pss_cols(v, v.pss[rd.root], h, R, &pf, r);
-    if (st == ST_NONE) st = ST_PSS_MAP;
+    hroot = h.root;
+    st = pss_cols_table(v, pd, h, &T);
+  }
+  uint32_t tot[PSS_NLISTS];
+#pragma unroll
+  for (uint32_t l = 0; l < PSS_NLISTS; l++) {
+    uint32_t cnt = 0, eb = 0;
+    if (T) {
+      const uint32_t* L = T + PC_LISTS + l * PCL_COUNT;
+      if (L[PCL_LEN] != NONE) {
+        KYV_ACCT_ADD(0, 8);
+        const uint64_t ln = v.colv[(size_t)v.col_off[L[PCL_LEN]] + r];  // (count, row of element 0)
+        if ((uint32_t)ln != NONE) { cnt = (uint32_t)ln; eb = (uint32_t)(ln >> 32); }
+      }
+    }
+    uint32_t incl = cnt;  // inclusive prefix over the wave
+#pragma unroll
+    for (uint32_t d = 1; d < BLOCK; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    s_pre[l][lane] = incl - cnt;
+    s_eb[l][lane] = eb;
+    tot[l] = __shfl(incl, BLOCK - 1);
+  }
+  s_root[lane] = hroot;
+  s_pos[lane] = T ? (uint32_t)((T - (v.pool + pd.cols)) / PC_COUNT) : 0u;
+  s_fact[lane] = 0;
+  __syncthreads();
+  // the checks of every container of the wave, a container per lane (its facts OR-ed into its pod's word)
+  const uint32_t ncont = tot[0] + tot[1] + tot[2];
+  for (uint32_t base = 0; base < ncont; base += BLOCK) {
+    const uint32_t s = base + lane;
+    if (s < ncont) {
+      const uint32_t l = s < tot[0] ? 0u : s < tot[0] + tot[1] ? 1u : 2u;
+      const uint32_t q = s - (l == 0 ? 0u : l == 1 ? tot[0] : tot[0] + tot[1]);
+      uint32_t lo = 0, hi = BLOCK - 1;  // the last pod whose list starts at or before q
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_pre[l][mid] <= q) lo = mid; else hi = mid - 1;
+      }
+      const uint32_t* L = v.pool + pd.cols + s_pos[lo] * PC_COUNT + PC_LISTS + l * PCL_COUNT;
+      const uint32_t f = pss_container_facts(v, NodeTab{v.nodes + s_root[lo]}, L, s_eb[l][lo] + (q - s_pre[l][lo]));
+      atomicOr(&s_fact[lo], f);
+    }
+  }
+  __syncthreads();
+  if (T) {
+    const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
+    pf = pss_checks_cols(v, NodeTab{v.nodes + hroot}, r, T, s_fact[lane], true) & mask;
+    st = pf ? ST_FAIL : ST_PASS;
   }
   if (gated && st != ST_NONE) {
     o.status[(size_t)k * v.nres + r] = st;

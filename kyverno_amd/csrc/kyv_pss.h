@@ -480,8 +480,82 @@ KYV_HD bool pobj(const PCol& c) { return c.i != NONE && c.t == N_MAP; }
 // an int64 field: present (decoded: an integer) and its value is zero
 KYV_HD bool pzero(NodeTab R, const PCol& c) { return c.i != NONE && c.t == N_INT && c.a == 0 && R[c.i].b == 0; }
 
-KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, const uint32_t* T) {
+// the per-container part of the checks (one container: element row `er` of list table L), as fact bits the pod-level
+// part combines; F_NRUNSET / F_SECUNSET become failures only when the pod-level field does not supply the value
+enum PssFact : uint32_t {
+  F_APE = 1u << 0, F_CAPSB = 1u << 1, F_CAPSR = 1u << 2, F_PORTS = 1u << 3, F_PRIV = 1u << 4, F_PROC = 1u << 5,
+  F_NREXP = 1u << 6, F_NRUNSET = 1u << 7, F_USER = 1u << 8, F_SEL = 1u << 9, F_SECB = 1u << 10, F_SECREXP = 1u << 11,
+  F_SECUNSET = 1u << 12, F_HP = 1u << 13,
+};
+KYV_HD __attribute__((always_inline)) uint32_t pss_container_facts(const View& v, NodeTab R, const uint32_t* L, uint32_t er) {
+  auto capOK = [](uint32_t c) {
+    return (c >= KSID(CAP_AUDIT_WRITE) && c <= KSID(CAP_SYS_CHROOT)) || c == KSID(NET_BIND_SERVICE);
+  };
+  auto selValid = [&](uint32_t u, uint32_t r, uint32_t t) {
+    return (t == SID_EMPTY || (t >= KSID(CONTAINER_T) && t <= KSID(CONTAINER_KVM_T))) && u == SID_EMPTY && r == SID_EMPTY;
+  };
+  auto secValid = [&](uint32_t t) { return t == KSID(LOCALHOST) || t == KSID(RUNTIMEDEFAULT); };
+  uint32_t f = 0;
+  // every field of the container: independent loads
+  const PCol sc = pcol(v, L[PCL_SC], er);
+  const PCol priv = pcol(v, L[PCL_PRIV], er), ape = pcol(v, L[PCL_APE], er), nr = pcol(v, L[PCL_NONROOT], er);
+  const PCol us = pcol(v, L[PCL_USER], er), sel = pcol(v, L[PCL_SEL], er), sec = pcol(v, L[PCL_SEC], er);
+  const PCol win = pcol(v, L[PCL_WIN], er), caps = pcol(v, L[PCL_CAPS], er), pm = pcol(v, L[PCL_PROC], er);
+  const uint64_t addl = L[PCL_ADD_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_ADD_LEN]] + er];
+  const uint64_t dropl = L[PCL_DROP_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_DROP_LEN]] + er];
+  const uint64_t portl = L[PCL_PORTS_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_PORTS_LEN]] + er];
+  KYV_ACCT_ADD(0, 8 * ((L[PCL_ADD_LEN] != NONE) + (L[PCL_DROP_LEN] != NONE) + (L[PCL_PORTS_LEN] != NONE)));
+  const bool set = pobj(sc);
+  const int privileged = set ? pbool(priv) : -1, apev = set ? pbool(ape) : -1, nonRoot = set ? pbool(nr) : -1;
+  if (!set || apev != 0) f |= F_APE;
+  if (set && pobj(caps)) {
+    if ((uint32_t)addl != NONE)
+      for (uint32_t j = 0; j < (uint32_t)addl; j++) {
+        const PCol e = pcol(v, L[PCL_ADD_SELF], (uint32_t)(addl >> 32) + j);
+        const uint32_t cap = e.t == N_STR ? e.a : SID_EMPTY;
+        if (!capOK(cap)) f |= F_CAPSB;
+        if (cap != KSID(NET_BIND_SERVICE)) f |= F_CAPSR;
+      }
+    bool all = false;
+    if ((uint32_t)dropl != NONE)
+      for (uint32_t j = 0; j < (uint32_t)dropl; j++) {
+        const PCol e = pcol(v, L[PCL_DROP_SELF], (uint32_t)(dropl >> 32) + j);
+        if (e.t == N_STR && e.a == KSID(ALL)) all = true;
+      }
+    if (!all) f |= F_CAPSR;
+  } else {
+    f |= F_CAPSR;
+  }
+  if ((uint32_t)portl != NONE)
+    for (uint32_t j = 0; j < (uint32_t)portl; j++) {
+      const PCol hp = pcol(v, L[PCL_PORT_HOSTPORT], (uint32_t)(portl >> 32) + j);
+      if (hp.i != NONE && hp.t == N_INT && (hp.a != 0 || R[hp.i].b != 0)) f |= F_PORTS;
+    }
+  if (set && privileged == 1) f |= F_PRIV;
+  if (set && !pnil(pm) && pstr(pm) != KSID(DEFAULT)) f |= F_PROC;
+  if (set && nonRoot != -1) { if (nonRoot == 0) f |= F_NREXP; }
+  else f |= F_NRUNSET;
+  if (set && us.i != NONE && us.t == N_INT && pzero(R, us)) f |= F_USER;
+  if (set && pobj(sel) && !selValid(pstr(pcol(v, L[PCL_SEL_USER], er)), pstr(pcol(v, L[PCL_SEL_ROLE], er)),
+                                    pstr(pcol(v, L[PCL_SEL_TYPE], er))))
+    f |= F_SEL;
+  if (set && pobj(sec)) {
+    const uint32_t st = pstr(pcol(v, L[PCL_SEC_TYPE], er));
+    if (st == KSID(UNCONFINED)) f |= F_SECB;
+    if (!secValid(st)) f |= F_SECREXP;
+  } else {
+    f |= F_SECUNSET;
+  }
+  if (set && pobj(win) && pbool(pcol(v, L[PCL_WIN_HP], er)) == 1) f |= F_HP;
+  return f;
+}
+
+// cf_given: the OR of every container's facts (pss_kernel computes them with one container per lane across the
+// wave); else the containers are visited here, one after the other
+KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, const uint32_t* T,
+                                                              uint32_t cf = 0, bool cf_given = false) {
   uint32_t fails = 0;
+
   const PCol psc = pcol(v, T[PC_PSC], row);
   const bool pscSet = pobj(psc);
   const PCol osn = pcol(v, T[PC_OS_NAME], row);
@@ -544,7 +618,9 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
     }
   }
 
-  for (uint32_t l = 0; l < PSS_NLISTS; l++) {
+  // the containers: facts (given, or gathered here) and, for pods with container seccomp annotations, the per-name
+  // annotation check (container.seccomp.security.alpha.kubernetes.io/<name> == "unconfined")
+  for (uint32_t l = 0; l < PSS_NLISTS && (!cf_given || annSecC); l++) {
     const uint32_t* L = T + PC_LISTS + l * PCL_COUNT;
     if (L[PCL_LEN] == NONE) continue;
     KYV_ACCT_ADD(0, 8);
@@ -553,60 +629,10 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
     const uint32_t cnt = (uint32_t)ln, eb = (uint32_t)(ln >> 32);
     for (uint32_t i = 0; i < cnt; i++) {
       const uint32_t er = eb + i;
-      // every field of the container: independent loads
-      const PCol nm = pcol(v, L[PCL_NAME], er), sc = pcol(v, L[PCL_SC], er);
-      const PCol priv = pcol(v, L[PCL_PRIV], er), ape = pcol(v, L[PCL_APE], er), nr = pcol(v, L[PCL_NONROOT], er);
-      const PCol us = pcol(v, L[PCL_USER], er), sel = pcol(v, L[PCL_SEL], er), sec = pcol(v, L[PCL_SEC], er);
-      const PCol win = pcol(v, L[PCL_WIN], er), caps = pcol(v, L[PCL_CAPS], er), pm = pcol(v, L[PCL_PROC], er);
-      const uint64_t addl = L[PCL_ADD_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_ADD_LEN]] + er];
-      const uint64_t dropl = L[PCL_DROP_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_DROP_LEN]] + er];
-      const uint64_t portl = L[PCL_PORTS_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_PORTS_LEN]] + er];
-      KYV_ACCT_ADD(0, 8 * ((L[PCL_ADD_LEN] != NONE) + (L[PCL_DROP_LEN] != NONE) + (L[PCL_PORTS_LEN] != NONE)));
-      const bool set = pobj(sc);
-      const uint32_t cname = nm.i == NONE || nm.t == N_NULL ? SID_EMPTY : nm.a;
-      const int privileged = set ? pbool(priv) : -1, apev = set ? pbool(ape) : -1, nonRoot = set ? pbool(nr) : -1;
-      if (!set || apev != 0) apeBad = true;
-      if (set && pobj(caps)) {
-        if ((uint32_t)addl != NONE)
-          for (uint32_t j = 0; j < (uint32_t)addl; j++) {
-            const PCol e = pcol(v, L[PCL_ADD_SELF], (uint32_t)(addl >> 32) + j);
-            const uint32_t cap = e.t == N_STR ? e.a : SID_EMPTY;
-            if (!capOK(cap)) capsBaseBad = true;
-            if (cap != KSID(NET_BIND_SERVICE)) capsRBad = true;
-          }
-        bool all = false;
-        if ((uint32_t)dropl != NONE)
-          for (uint32_t j = 0; j < (uint32_t)dropl; j++) {
-            const PCol e = pcol(v, L[PCL_DROP_SELF], (uint32_t)(dropl >> 32) + j);
-            if (e.t == N_STR && e.a == KSID(ALL)) all = true;
-          }
-        if (!all) capsRBad = true;
-      } else {
-        capsRBad = true;
-      }
-      if ((uint32_t)portl != NONE)
-        for (uint32_t j = 0; j < (uint32_t)portl; j++) {
-          const PCol hp = pcol(v, L[PCL_PORT_HOSTPORT], (uint32_t)(portl >> 32) + j);
-          if (hp.i != NONE && hp.t == N_INT && (hp.a != 0 || R[hp.i].b != 0)) portsBad = true;
-        }
-      if (set && privileged == 1) privBad = true;
-      if (set && !pnil(pm) && pstr(pm) != KSID(DEFAULT)) procBad = true;
-      if (set && nonRoot != -1) { if (nonRoot == 0) nonRootExplicitBad = true; }
-      else if (!podNonRootTrue) nonRootImplicitBad = true;
-      if (set && us.i != NONE && us.t == N_INT && pzero(R, us)) userBad = true;
-      if (set && pobj(sel) && !selValid(pstr(pcol(v, L[PCL_SEL_USER], er)), pstr(pcol(v, L[PCL_SEL_ROLE], er)),
-                                        pstr(pcol(v, L[PCL_SEL_TYPE], er))))
-        selBad = true;
-      if (set && pobj(sec)) {
-        const uint32_t st = pstr(pcol(v, L[PCL_SEC_TYPE], er));
-        if (st == KSID(UNCONFINED)) secBaseBad = true;
-        if (!secValid(st)) secRExplicitBad = true;
-      } else if (!podSecValid) {
-        secRImplicitBad = true;
-      }
-      if (set && pobj(win) && pbool(pcol(v, L[PCL_WIN_HP], er)) == 1) hpBad = true;
-      // container seccomp annotation: container.seccomp.security.alpha.kubernetes.io/<name> == "unconfined"
+      if (!cf_given) cf |= pss_container_facts(v, R, L, er);
       if (annSecC) {
+        const PCol nm = pcol(v, L[PCL_NAME], er);
+        const uint32_t cname = nm.i == NONE || nm.t == N_NULL ? SID_EMPTY : nm.a;
         const uint32_t pl = v.str_len[KSID(SECCOMP_CONTAINER_PREFIX)], nl = v.str_len[cname];
         for (uint32_t q = 0; q < R[ann].b; q++) {
           const Node& e = R[R[ann].a + q];
@@ -618,6 +644,11 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
       }
     }
   }
+  apeBad = cf & F_APE; capsBaseBad = cf & F_CAPSB; capsRBad = cf & F_CAPSR; portsBad = cf & F_PORTS;
+  privBad = cf & F_PRIV; procBad = cf & F_PROC; nonRootExplicitBad = cf & F_NREXP;
+  nonRootImplicitBad = (cf & F_NRUNSET) && !podNonRootTrue; userBad = cf & F_USER; selBad = cf & F_SEL;
+  secBaseBad = cf & F_SECB; secRExplicitBad = cf & F_SECREXP; secRImplicitBad = (cf & F_SECUNSET) && !podSecValid;
+  hpBad = cf & F_HP;
   if (apeBad) fails |= 1u << PS_APE_1_8;
   if (apeBad && !windows) fails |= 1u << PS_APE_1_25;
   if (capsBaseBad) fails |= 1u << PS_CAPS_BASE;
@@ -740,13 +771,14 @@ KYV_HD uint8_t pss_pod(NodeTab R, uint32_t kind, bool decode, uint32_t* meta_out
 // row: the resource's batch position (its column row), passed explicitly by every caller
 // kOol: the checks as the out-of-line pss_checks_cols_ool (eval_pss, see there)
 KYV_FN_PSS uint32_t pss_checks_cols_ool(const View& v, NodeTab R, uint32_t row, const uint32_t* T);
-template <bool kOol = false>
-KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const PssDesc& pd, const ResHeader& h,
-                                                            NodeTab R, uint32_t* fails_out, uint32_t row) {
-  *fails_out = 0;
+// the column form's preconditions: ST_NONE with *T = the pod position's column table when the checks run over path
+// columns; ST_ERROR / ST_PANIC / ST_FALLBACK when that is the pair's status already; ST_PSS_MAP when the column form
+// does not apply (exclusion sub-pods, no columns, typed decode not done)
+KYV_HD uint8_t pss_cols_table(const View& v, const PssDesc& pd, const ResHeader& h, const uint32_t** T) {
+  *T = nullptr;
   if (pd.flags & PSS_BAD_VERSION) return ST_ERROR;
   if (!(h.flags & RF_PSS_DONE) || pd.cols == NONE || pd.nexcl != 0 || !v.colv || h.nnodes >= (1u << COL_TYPE_SHIFT))
-    return ST_NONE;
+    return ST_PSS_MAP;
   if (h.flags & RF_PSS_DEC_ERR) return ST_ERROR;
   if (h.flags & RF_PSS_FOLD) return KYV_WHY(FBW_COND), ST_FALLBACK;
   const uint32_t pos = h.kind == KSID(POD) ? 0u
@@ -754,8 +786,20 @@ KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const
                         h.kind == KSID(STATEFULSET) || h.kind == KSID(REPLICASET) || h.kind == KSID(RC)) ? 1u
                      : h.kind == KSID(CRONJOB) ? 2u : NONE;
   if (pos == NONE) return ST_PANIC;  // no pod spec for this kind (validation.go:542-543)
-  const uint32_t* T = v.pool + pd.cols + pos * PC_COUNT;
-  if (T[PC_PSC] == NONE) return ST_NONE;  // the table lacks this position (the rule's kinds)
+  const uint32_t* t = v.pool + pd.cols + pos * PC_COUNT;
+  if (t[PC_PSC] == NONE) return ST_PSS_MAP;  // the table lacks this position (the rule's kinds)
+  *T = t;
+  return ST_NONE;
+}
+
+template <bool kOol = false>
+KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const PssDesc& pd, const ResHeader& h,
+                                                            NodeTab R, uint32_t* fails_out, uint32_t row) {
+  *fails_out = 0;
+  const uint32_t* T;
+  const uint8_t pre = pss_cols_table(v, pd, h, &T);
+  if (pre == ST_PSS_MAP) return ST_NONE;
+  if (pre != ST_NONE) return pre;
   const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
   const uint32_t fails = (kOol ? pss_checks_cols_ool(v, R, row, T) : pss_checks_cols(v, R, row, T)) & mask;
   *fails_out = fails;
