@@ -729,12 +729,7 @@ void derive_strings(Batch& b, size_t from, int threads) {
 // Kind gate of one compiled rule: the gvk kinds its match block can accept (MatchesResourceDescription
 // checks kinds first, utils.go:81-85). `any` when some reachable filter has no kinds or "*", when the empty
 // OldResource retry may match, or when the match program fell back.
-struct KindGate {
-  bool any = false;
-  std::vector<uint32_t> kinds;
-};
-
-static KindGate rule_gate(const Ruleset& rs, const RuleDesc& rd) {
+KindGate rule_gate(const Ruleset& rs, const RuleDesc& rd) {
   KindGate g;
   if (rd.empty_may_match || rd.match.mode == MM_NONE) { g.any = true; return g; }
   const MatchBlock& m = rd.match;

@@ -1586,26 +1586,52 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
   src << "}  // namespace kyv\n"
          "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n";
   if (!crules.empty()) {
-    // one kernel per compiled condition rule, the rule inlined (one big kernel with a switch over the rules needs an
-    // out-of-line call per rule, whose callee-saved registers go through scratch memory, or, inlined, compiles for
-    // tens of minutes); one lane per resource, launched over the match waves [w0, w0 + grid) that hold resources of
-    // the rule's kind gate (kind-major batch)
+    // compiled condition rules, inlined (one big kernel with a switch over the rules needs an out-of-line call per
+    // rule, whose callee-saved registers go through scratch memory, or, inlined, compiles for tens of minutes); one
+    // lane per resource, launched over the match waves [w0, w0 + grid) that hold resources of the rule's kind gate
+    // (kind-major batch). Rules with the same kind gate share one kernel (kyv_jit_condg_<first rule>, jit_cond_groups;
+    // `mask`: the members the launch runs, those of the current rule slice): a wave loads its resources' header once
+    // for all of them and the later rules find the lists the first one read (C3: the three capability rules of a pod
+    // kind read the same container lists) in the caches. KYV_JC_GROUP=0: one kernel per rule (kyv_jit_cond_<k>)
     // 5 waves/SIMD: measured 1.30 -> 1.05 ms on C3 with the round-2 kernel (4: 1.11, 6: 1.08)
     src << "#ifndef KYV_JC_WPE\n#define KYV_JC_WPE 5\n#endif\n";
-    for (uint32_t k : crules)
-      src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JC_WPE)))\n"
-             "kyv_jit_cond_" << k << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t w0) {\n"
-             "  __shared__ uint32_t jl[" << (cg.lds_used ? cg.nslots : 0u) << "u * kyv::JCAP * 64u + 64u];\n"
-             "  const kyv::View& v = *vp;\n"
-             "  const uint32_t lane = threadIdx.x, r = (w0 + blockIdx.x) * 64u + lane;\n"
-             "  const bool gated = r < v.nres && ((v.gate[(size_t)v.hdr[r].kclass * v.gate_words + " << k / 32 << "u] >> "
-          << k % 32 << "u) & 1u);\n"
-             "  if (r < v.nres) KYV_ACCT_ADD(0, 4);  // header: kind class\n"
-             "  if (!__ballot(gated)) return;\n"
-             "  uint8_t st = kyv::ST_NONE;\n"
-             "  if (gated) st = kyv::jr" << k << "(v, r, jl + lane);\n"
-             "  if (gated && st != kyv::ST_NONE) { o.status[(size_t)" << k << "u * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }\n"
-             "}\n";
+    const bool grouped = !getenv("KYV_JC_GROUP") || atoi(getenv("KYV_JC_GROUP")) != 0;
+    const std::string lds = std::to_string(cg.lds_used ? cg.nslots : 0u) + "u * kyv::JCAP * 64u + 64u";
+    auto member = [&](uint32_t k, const std::string& on) {
+      src << "  {\n"
+             "    const bool gated = " << on << "((gw[" << k / 32 << "u] >> " << k % 32 << "u) & 1u);\n"
+             "    if (__ballot(gated)) {\n"
+             "      uint8_t st = kyv::ST_NONE;\n"
+             "      if (gated) st = kyv::jr" << k << "(v, r, jl + lane);\n"
+             "      if (gated && st != kyv::ST_NONE) { o.status[(size_t)" << k << "u * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }\n"
+             "    }\n"
+             "  }\n";
+    };
+    if (grouped) {
+      for (const auto& grp : jit_cond_groups(rs, crules)) {
+        src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JC_WPE)))\n"
+               "kyv_jit_condg_" << grp[0] << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t w0, uint32_t mask) {\n"
+               "  __shared__ uint32_t jl[" << lds << "];\n"
+               "  const kyv::View& v = *vp;\n"
+               "  const uint32_t lane = threadIdx.x, r = (w0 + blockIdx.x) * 64u + lane;\n"
+               "  const uint32_t* gw = r < v.nres ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;\n"
+               "  if (r < v.nres) KYV_ACCT_ADD(0, 4);  // header: kind class\n";
+        for (size_t i = 0; i < grp.size(); i++) member(grp[i], "gw && (mask & " + std::to_string(1u << i) + "u) && ");
+        src << "}\n";
+      }
+    } else {
+      for (uint32_t k : crules) {
+        src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JC_WPE)))\n"
+               "kyv_jit_cond_" << k << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t w0) {\n"
+               "  __shared__ uint32_t jl[" << lds << "];\n"
+               "  const kyv::View& v = *vp;\n"
+               "  const uint32_t lane = threadIdx.x, r = (w0 + blockIdx.x) * 64u + lane;\n"
+               "  const uint32_t* gw = r < v.nres ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;\n"
+               "  if (r < v.nres) KYV_ACCT_ADD(0, 4);  // header: kind class\n";
+        member(k, "gw && ");
+        src << "}\n";
+      }
+    }
     for (uint32_t k : crules) if (jit_cond) (*jit_cond)[k] = 1;
   }
   src << "#ifndef KYV_JIT_WPE_LIGHT\n#define KYV_JIT_WPE_LIGHT 8\n#endif\n";
@@ -1634,6 +1660,26 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
            "}\n";
   }
   return src.str();
+}
+
+std::vector<std::vector<uint32_t>> jit_cond_groups(const Ruleset& rs, const std::vector<uint32_t>& crules) {
+  std::vector<std::vector<uint32_t>> out;
+  std::map<std::pair<bool, std::vector<uint32_t>>, size_t> open;  // kind gate -> its group still taking members
+  for (uint32_t k : crules) {
+    KindGate g = rule_gate(rs, rs.rules[k]);
+    std::sort(g.kinds.begin(), g.kinds.end());
+    g.kinds.erase(std::unique(g.kinds.begin(), g.kinds.end()), g.kinds.end());
+    if (g.any) g.kinds.clear();
+    const auto key = std::make_pair(g.any, g.kinds);
+    auto it = open.find(key);
+    if (it == open.end() || out[it->second].size() >= 8) {
+      open[key] = out.size();
+      out.push_back({});
+      it = open.find(key);
+    }
+    out[it->second].push_back(k);
+  }
+  return out;
 }
 
 std::vector<char> jit_compile_uncached(const std::string& src, double* seconds, bool acct);

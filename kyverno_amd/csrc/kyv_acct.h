@@ -9,7 +9,9 @@ namespace kyvacct {
 void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
            const uint32_t* mrules, uint32_t nm);
 void match_walk(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
-                const uint32_t* mrules, uint32_t nm);
+                const void* recs, uint32_t nm);
+void match_walk_generic(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+                        const uint32_t* mrules, uint32_t nm);
 void pss(bool exact, int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0);
 void match_deny(unsigned grid, hipStream_t s, const void* view, const void* devout, const uint32_t* mrules, uint32_t nm);
 void pss_map(unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0);

@@ -40,9 +40,17 @@ void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* 
   check(hipGetLastError());
 }
 void match_walk(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
-                const uint32_t* mrules, uint32_t nm) {
+                const void* recs, uint32_t nm) {
   using namespace kyv_acct;
   auto kf = wpe == 8 ? match_walk_kernel<8> : wpe == 6 ? match_walk_kernel<6> : match_walk_kernel<4>;
+  hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl),
+                     (const MRec*)recs, nm);
+  check(hipGetLastError());
+}
+void match_walk_generic(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+                        const uint32_t* mrules, uint32_t nm) {
+  using namespace kyv_acct;
+  auto kf = wpe == 8 ? match_walk_generic_kernel<8> : wpe == 6 ? match_walk_generic_kernel<6> : match_walk_generic_kernel<4>;
   hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl), mrules, nm);
   check(hipGetLastError());
 }

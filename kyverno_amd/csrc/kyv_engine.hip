@@ -179,6 +179,11 @@ struct DevRuleset {
   std::vector<hipFunction_t> ffns;  // kyv_jit_fused_<g> per rule group, or null (the group has no fused rule)
   std::vector<std::vector<hipFunction_t>> fparts, afparts;  // its further parts kyv_jit_fused_<g>p<1..> (KYV_FUSED_SPLIT)
   std::vector<hipFunction_t> jconds;  // [rule] kyv_jit_cond_<k> (compiled deny / foreach rule k) or null
+  // compiled condition rules in kernel groups (jit_cond_groups): [group] kyv_jit_condg_<first rule>, its members,
+  // the accounting build's kernel; [rule] its group or -1
+  std::vector<hipFunction_t> jcg, ajcg;
+  std::vector<std::vector<uint32_t>> jcg_members;
+  std::vector<int32_t> jc_group;
   bool jloaded = false;
   // the byte-accounting build of the same kernels (KYV_ACCT), loaded only by an accounting evaluation
   hipModule_t amod = nullptr;
@@ -305,13 +310,16 @@ struct SliceSched {
   size_t stage_tot = 0;          // staging slots (records) of the slice
   uint32_t* rbase = nullptr;     // [k1 - k0] first staging slot of each rule (slice-local)
   uint32_t* mrules = nullptr;    // rules of the slice the match phase evaluates (direct-walk rules excluded):
-  uint32_t nmw = 0;              // leading rules of mrules on match_walk_kernel (pattern rules: match only)
+  uint32_t nmw = 0;              // leading rules of mrules on match_walk_generic_kernel (pattern rules: match only)
+  uint32_t nmr = 0;              // pattern rules on match_walk_kernel, as staged match records (kyv_kernels.h MRec)
+  MRec* mrec = nullptr;          // [nmr]
   uint32_t nmd = 0;              // then deny rules without JMESPath on match_deny_kernel
   uint32_t nm = 0, nmj = 0, nmc = 0;  // then [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
                                  // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
   std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
   std::vector<uint3> pw;         // PodSecurity rules on pss_kernel: (rule, first match wave, waves)
   std::vector<uint3> cw;         // compiled condition rules: (rule, first match wave, waves) of its kernel's launch
+  std::vector<uint32_t> cwm;     // [i] 0: cw[i] is a per-rule kernel; else the member mask of group cw[i].x
   uint2* sched = nullptr;        // chunk schedules of the two walk kernels (ChunkMap slots)
   std::vector<ChunkMap> cm;      // [0] interpreted walk kernel, [1 + g] runtime-compiled group g
   std::vector<uint8_t> fg;       // [g]: the slice has rules of group g on its fused kernel (kyv_jit_fused_<g>)
@@ -357,7 +365,7 @@ static void free_dev_results(DeviceResults& d, int dev) {
   dfree(d.stage); dfree(d.rcnt); dfree(d.tsum);
   dfree(d.wl.items); dfree(d.wl.cnt);
   for (auto& sl : d.slices) {
-    dfree(sl.rbase); dfree(sl.mrules); dfree(sl.sched);
+    dfree(sl.rbase); dfree(sl.mrules); dfree(sl.mrec); dfree(sl.sched);
     if (sl.evs) hipEventDestroy(sl.evs);
     for (auto e : sl.ev) if (e) hipEventDestroy(e);
     for (auto e : sl.cev) if (e) hipEventDestroy(e);
@@ -794,8 +802,24 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   }
   (void)hipGetLastError();
   dr->jconds.assign(rs.rules.size(), nullptr);
+  dr->jc_group.assign(rs.rules.size(), -1);
+  dr->jcg.clear();
+  dr->jcg_members.clear();
+  {
+    std::vector<uint32_t> crules;
+    for (size_t k = 0; k < rs.jit_cond.size(); k++) if (rs.jit_cond[k]) crules.push_back((uint32_t)k);
+    for (auto& grp : jit_cond_groups(rs, crules)) {
+      hipFunction_t f = nullptr;
+      if (hipModuleGetFunction(&f, dr->jmod, ("kyv_jit_condg_" + std::to_string(grp[0])).c_str()) != hipSuccess) continue;
+      for (uint32_t k : grp) dr->jc_group[k] = (int32_t)dr->jcg.size();
+      dr->jcg.push_back(f);
+      dr->jcg_members.push_back(grp);
+    }
+    (void)hipGetLastError();
+  }
   for (size_t k = 0; k < rs.jit_cond.size(); k++)
-    if (rs.jit_cond[k]) HIP_OK(hipModuleGetFunction(&dr->jconds[k], dr->jmod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
+    if (rs.jit_cond[k] && dr->jc_group[k] < 0)
+      HIP_OK(hipModuleGetFunction(&dr->jconds[k], dr->jmod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
   dr->jloaded = true;
   return true;
 }
@@ -825,6 +849,9 @@ static bool ensure_jit_acct(Ruleset& rs, DevRuleset* dr) {
   dr->aconds.assign(dr->jconds.size(), nullptr);
   for (size_t k = 0; k < dr->jconds.size(); k++)
     if (dr->jconds[k]) HIP_OK(hipModuleGetFunction(&dr->aconds[k], dr->amod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
+  dr->ajcg.assign(dr->jcg.size(), nullptr);
+  for (size_t g = 0; g < dr->jcg.size(); g++)
+    HIP_OK(hipModuleGetFunction(&dr->ajcg[g], dr->amod, ("kyv_jit_condg_" + std::to_string(dr->jcg_members[g][0])).c_str()));
   hipDeviceptr_t p = nullptr;
   size_t bytes = 0;
   HIP_OK(hipModuleGetGlobal(&p, &bytes, dr->amod, "kyv_acct_bytes"));
@@ -852,6 +879,57 @@ static size_t slice_budget() {
 
 // Lay out the chunk schedules of one slice's walk kernels (see ChunkMap): runs of match waves with equal gated rule
 // sets, wave-major within a run, whole waves placed on one XCD.
+// The staged match record of match_walk rule q (kyv_kernels.h MRec): MR_FAST when its match block fits the record
+// (compiled, no PolicyException candidates, no empty-OldResource retry, at most MREC_F filters, 4 kinds, 2 names and 2
+// namespaces per filter, every wildcard pattern with a glob-mask bit); else the kernel runs pair_match for it
+static void build_mrec(const Ruleset& rs, uint32_t q, const std::vector<uint32_t>& gidx, bool masks_on, bool on, MRec& R) {
+  memset(&R, 0, sizeof R);
+  const RuleDesc& rd = rs.rules[q];
+  R.k = q;
+  R.kind = rd.kind;
+  R.flags = rd.flags;
+  bool fast = on && rd.match.mode != MM_NONE && !rd.empty_may_match && rd.exc == NONE &&
+              rd.match.nfilters + rd.exclude.nfilters <= MREC_F;
+  bool uses = false;
+  auto pat = [&](uint32_t sid) -> uint32_t {  // glob_sid's classification (kyv_eval.h), by the string's content
+    if (sid >= rs.dict.strs.size()) { fast = false; return 0; }
+    const std::string& x = rs.dict.strs[sid];
+    bool globby = x.find_first_of("*?") != std::string::npos;
+    for (unsigned char ch : x) if (ch >= 0x80) globby = true;
+    if (!globby) {
+      if (sid & PAT_MASK) fast = false;
+      return sid;
+    }
+    uses = true;
+    const uint32_t g = gidx[sid];
+    if (!g || g > 0xFFu || !masks_on) { fast = false; return 0; }
+    return PAT_MASK | g;
+  };
+  auto fill = [&](uint32_t fi, MRecFilter& F) {
+    const Filter& f = rs.filters[fi];
+    F.idx = fi;
+    if (f.nkinds > 4 || f.nnames > 2 || f.nnss > 2) { fast = false; return; }
+    uint32_t b = (uint32_t)f.flags | ((uint32_t)f.nkinds << 16) | (f.nnames << 19) | ((f.name != NONE ? 1u : 0u) << 21) |
+                 (f.nnss << 22);
+    for (uint32_t i = 0; i < f.nkinds; i++) {
+      const KindDesc& kd = rs.kinds[f.kinds + i];
+      F.kinds[i] = kd.kind;
+      if (kd.kind != NONE && kd.gv_mode != 0) b |= 1u << (24 + i);
+    }
+    if (f.name != NONE) F.pats[0] = pat(f.name);
+    for (uint32_t i = 0; i < f.nnames; i++) F.pats[1 + i] = pat(rs.pool[f.names + i]);
+    for (uint32_t i = 0; i < f.nnss; i++) F.pats[3 + i] = pat(rs.pool[f.nss + i]);
+    if (f.nann || (f.flags & (FF_HAS_SEL | FF_HAS_NSSEL))) b |= 1u << 28;
+    F.bits = b;
+  };
+  if (fast) {
+    for (uint32_t i = 0; i < rd.match.nfilters; i++) fill(rd.match.filters + i, R.f[i]);
+    for (uint32_t i = 0; i < rd.exclude.nfilters; i++) fill(rd.exclude.filters + i, R.f[rd.match.nfilters + i]);
+  }
+  R.bits = (fast ? MR_FAST : 0u) | (uses ? MR_MASKS : 0u) | ((uint32_t)rd.match.mode << 8) |
+           ((uint32_t)rd.exclude.mode << 16) | (fast ? (rd.match.nfilters << 24) | (rd.exclude.nfilters << 28) : 0u);
+}
+
 static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset* dr, DeviceResults& d, SliceSched& sl,
                             bool jit) {
   const size_t nres = d.nres;
@@ -976,28 +1054,63 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     std::vector<uint32_t> only;
     if (const char* e = getenv("KYV_JC_ONLY")) for (const char* p = e; *p;) { only.push_back((uint32_t)strtoul(p, (char**)&p, 10)); if (*p) p++; }
     sl.cw.clear();
+    sl.cwm.clear();
+    // the match waves holding resources of a rule's kind gate: one range in the kind-major batch (waves inside it
+    // whose resources the gate excludes exit after one ballot)
+    auto gate_range = [&](uint32_t q, uint32_t& lo, uint32_t& hi) {
+      for (size_t ri = 0; ri < runs.size(); ri++) {
+        if (!((runs[ri].second[q / 32] >> (q % 32)) & 1u)) continue;
+        lo = std::min(lo, runs[ri].first);
+        hi = std::max(hi, ri + 1 < runs.size() ? runs[ri + 1].first : nw);
+      }
+    };
+    std::vector<uint32_t> gmask(dr->jcg.size(), 0), glo(dr->jcg.size(), nw), ghi(dr->jcg.size(), 0);
     for (uint32_t q : sl.mj) {
-      if (jit && q < dr->jconds.size() && dr->jconds[q]) {
+      const int32_t grp = jit && q < dr->jc_group.size() ? dr->jc_group[q] : -1;
+      if (jit && (grp >= 0 || (q < dr->jconds.size() && dr->jconds[q]))) {
         if (!only.empty() && std::find(only.begin(), only.end(), q) == only.end()) continue;
         cj.push_back(q);
-        // the match waves holding resources of the rule's kind gate: one range in the kind-major batch (waves inside
-        // it whose resources the gate excludes exit after one ballot)
-        uint32_t lo = nw, hi = 0;
-        for (size_t ri = 0; ri < runs.size(); ri++) {
-          if (!((runs[ri].second[q / 32] >> (q % 32)) & 1u)) continue;
-          lo = std::min(lo, runs[ri].first);
-          hi = std::max(hi, ri + 1 < runs.size() ? runs[ri + 1].first : nw);
+        if (grp >= 0) {  // its group's kernel, with the members of this slice
+          const auto& mem = dr->jcg_members[grp];
+          gmask[grp] |= 1u << (std::find(mem.begin(), mem.end(), q) - mem.begin());
+          gate_range(q, glo[grp], ghi[grp]);
+          continue;
         }
-        if (lo < hi) sl.cw.push_back(make_uint3(q, lo, hi - lo));
+        uint32_t lo = nw, hi = 0;
+        gate_range(q, lo, hi);
+        if (lo < hi) { sl.cw.push_back(make_uint3(q, lo, hi - lo)); sl.cwm.push_back(0); }
       } else {
         mr.push_back(q);
       }
     }
+    for (size_t g = 0; g < gmask.size(); g++)
+      if (gmask[g] && glo[g] < ghi[g]) { sl.cw.push_back(make_uint3((uint32_t)g, glo[g], ghi[g] - glo[g])); sl.cwm.push_back(gmask[g]); }
     sl.nm = (uint32_t)nlight;
     sl.nmj = (uint32_t)(mr.size() - nlight);
     sl.nmc = (uint32_t)cj.size();
     mr.insert(mr.end(), cj.begin(), cj.end());
-    sl.nmw = (uint32_t)mw.size();  // device list: [match_walk_kernel rules][deny][light][JMESPath][compiled]
+    dfree(sl.mrec);
+    sl.mrec = nullptr;
+    {  // match_walk rules whose match block fits a staged record go to match_walk_kernel, the rest stay in mrules
+      std::vector<MRec> recs;
+      std::vector<uint32_t> gidx(rs.dict.strs.size(), 0);
+      for (size_t g = 0; g < rs.gpats.size(); g++) if (rs.gpats[g] < gidx.size()) gidx[rs.gpats[g]] = (uint32_t)g + 1;
+      static const bool masks_on = !getenv("KYV_NO_GMASK");
+      static const bool recs_on = !getenv("KYV_MREC") || atoi(getenv("KYV_MREC")) != 0;
+      std::vector<uint32_t> gen;
+      for (uint32_t q : mw) {
+        MRec R;
+        build_mrec(rs, q, gidx, masks_on, recs_on, R);
+        if (R.bits & MR_FAST) recs.push_back(R);
+        else gen.push_back(q);
+      }
+      mw.swap(gen);
+      sl.nmr = (uint32_t)recs.size();
+      recs.resize(std::max<size_t>(1, recs.size()));
+      HIP_OK(dmalloc(&sl.mrec, recs.size() * sizeof(MRec)));
+      HIP_OK(hipMemcpy(sl.mrec, recs.data(), recs.size() * sizeof(MRec), hipMemcpyHostToDevice));
+    }
+    sl.nmw = (uint32_t)mw.size();  // device list: [match_walk_generic_kernel rules][deny][light][JMESPath][compiled]
     sl.nmd = (uint32_t)md.size();
     mr.insert(mr.begin(), md.begin(), md.end());
     mr.insert(mr.begin(), mw.begin(), mw.end());
@@ -1228,10 +1341,17 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipEventRecord(sl.evs, stream));
       HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
       HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
-      if (sl.nmw) {
-        static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
+      static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
+      if (sl.nmr) {
         auto kf = mwpe == 8 ? match_walk_kernel<8> : mwpe == 6 ? match_walk_kernel<6> : match_walk_kernel<4>;
-        if (acct) kyvacct::match_walk(mwpe, grid.x, stream, d.view, &o, &d.wl, sl.mrules, sl.nmw);
+        if (acct) kyvacct::match_walk(mwpe, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr);
+        else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const MRec*)sl.mrec,
+                                sl.nmr);
+      }
+      if (sl.nmw) {
+        auto kf = mwpe == 8 ? match_walk_generic_kernel<8> : mwpe == 6 ? match_walk_generic_kernel<6>
+                                                                         : match_walk_generic_kernel<4>;
+        if (acct) kyvacct::match_walk_generic(mwpe, grid.x, stream, d.view, &o, &d.wl, sl.mrules, sl.nmw);
         else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const uint32_t*)sl.mrules,
                                 sl.nmw);
       }
@@ -1279,11 +1399,13 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         HIP_OK(hipEventRecord(sl.cev[0], d.cstream));
         cs = d.cstream;
       }
-      for (const uint3& c : sl.cw) {
+      for (size_t i = 0; i < sl.cw.size(); i++) {
+        const uint3 c = sl.cw[i];
         const View* vp = d.view;
-        uint32_t w0 = c.y;
-        void* args[] = {(void*)&vp, (void*)&o, (void*)&w0};
-        HIP_OK(hipModuleLaunchKernel(acct ? dr->aconds[c.x] : dr->jconds[c.x], c.z, 1, 1, BLOCK, 1, 1, 0, cs, args, nullptr));
+        uint32_t w0 = c.y, mask = sl.cwm[i];
+        void* args[] = {(void*)&vp, (void*)&o, (void*)&w0, (void*)&mask};
+        hipFunction_t f = mask ? (acct ? dr->ajcg[c.x] : dr->jcg[c.x]) : (acct ? dr->aconds[c.x] : dr->jconds[c.x]);
+        HIP_OK(hipModuleLaunchKernel(f, c.z, 1, 1, BLOCK, 1, 1, 0, cs, args, nullptr));
       }
       if (acct) { const auto c = acct_take(); aphase[1] += c[0] + c[1]; }
       if (cs != stream) {

@@ -218,6 +218,15 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
 std::vector<char> jit_compile(const std::string& src, double* seconds, bool acct = false);
 // rule k is walked by its group's fused kernel (kyv_jit_fused_<g>) rather than the per-chunk schedule (jit.cpp)
 bool jit_rule_fused(const Ruleset& rs, uint32_t k);
+// the compiled condition rules (jit_cond) in kernel groups: rules with the same kind gate share one kernel
+// (kyv_jit_condg_<first rule>, jit.cpp), at most 8 per group, in rule order
+std::vector<std::vector<uint32_t>> jit_cond_groups(const Ruleset& rs, const std::vector<uint32_t>& crules);
+// kind gate of a rule (batch.cpp): the gvk kinds its match block can accept, or any
+struct KindGate {
+  bool any = false;
+  std::vector<uint32_t> kinds;
+};
+KindGate rule_gate(const Ruleset& rs, const RuleDesc& rd);
 enum JitMode { JIT_AUTO = 0, JIT_OFF = 1, JIT_ON = 2 };
 constexpr size_t JIT_AUTO_MIN_RESOURCES = 65536;  // smaller batches are not worth a compile
 void resolve_path_columns(Batch& b, int threads);

@@ -102,14 +102,157 @@ match_deny_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restr
   }
 }
 
+// Staged match records of match_walk_kernel. Every wave runs the same rule loop, so a rule's match program was a chain
+// of dependent uniform loads (rule list -> RuleDesc -> Filter -> KindDesc / pattern sids -> pattern flags -> the
+// string's glob mask) paid by every wave for every rule: the C4 loop (10,440 rules) was latency-bound (wait 0.85).
+// The host lays each rule's match block out as one fixed-size record (kinds, name / names / namespaces patterns with
+// their glob-mask bit resolved); a wave copies MREC_CHUNK records into LDS with one coalesced load and evaluates them
+// against the lane's resource facts (kind, name, namespace and their glob-mask words) held in registers. A filter with
+// annotations or selectors, or one whose matching kind carries a group / version, runs condition_block itself after
+// the record's checks passed; a rule the record cannot hold (exceptions, the empty-OldResource retry, more than
+// MREC_F filters / 4 kinds / 2 names / 2 namespaces, a glob without a mask) runs pair_match.
+constexpr uint32_t MREC_F = 3, MREC_CHUNK = 32, PAT_MASK = 0x80000000u;
+enum MRecBits : uint32_t { MR_FAST = 1u, MR_MASKS = 2u };
+struct MRecFilter {   // 48 bytes
+  uint32_t idx;       // Filter index (condition_block of a tail filter)
+  uint32_t bits;      // [0,16) FilterFlag, [16,19) kinds, [19,21) names, 21 name, [22,24) namespaces,
+                      // [24,28) kind i has a group / version, 28 tail (annotations / selector / namespace selector)
+  uint32_t kinds[4];  // kind sids (NONE: "*")
+  uint32_t pats[5];   // name, names[2], namespaces[2]: PAT_MASK | glob-mask index + 1, or the exact sid
+  uint32_t pad;
+};
+struct MRec {         // 160 bytes
+  uint32_t k;         // rule
+  uint32_t bits;      // MRecBits | match mode << 8 | exclude mode << 16 | match filters << 24 | exclude filters << 28
+  uint32_t kind, flags;  // RuleDesc.kind / .flags
+  MRecFilter f[MREC_F];  // match filters, then exclude filters
+};
+static_assert(sizeof(MRec) == 160, "match record size");
+
+struct MFacts {       // the lane's resource: what condition_block compares, and the glob-mask words of its strings
+  uint32_t gk, rname, rns;
+  uint32_t n0, n1, n2, n3;  // mask words of rname
+  uint32_t s0, s1, s2, s3;  // mask words of rns
+};
+KYV_HD bool mf_bit(uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3, uint32_t g) {
+  const uint32_t w = g >> 5;
+  const uint32_t x = w == 0 ? m0 : w == 1 ? m1 : w == 2 ? m2 : m3;
+  return (x >> (g & 31u)) & 1u;
+}
+// glob_sid(pattern, s) for a record pattern: the mask bit (which holds pattern == s too), or sid equality for a
+// pattern without '*' / '?' / non-ASCII runes
+KYV_HD bool pat_name(const MFacts& mf, uint32_t p) {
+  return (p & PAT_MASK) ? mf_bit(mf.n0, mf.n1, mf.n2, mf.n3, (p & 0xFFu) - 1u) : p == mf.rname;
+}
+KYV_HD bool pat_ns(const MFacts& mf, uint32_t p) {
+  return (p & PAT_MASK) ? mf_bit(mf.s0, mf.s1, mf.s2, mf.s3, (p & 0xFFu) - 1u) : p == mf.rns;
+}
+
+// condition_block (kyv_eval.h) of a record filter
+KYV_HD bool cb_rec(const View& v, const MRecFilter& F, const MFacts& mf, const ResView& rv, const LabelSet& nsl, bool uic,
+                   bool* nd) {
+  const uint32_t b = F.bits;
+  bool full = (b >> 28) & 1u;
+  const uint32_t nk = (b >> 16) & 7u;
+  if (nk) {  // kinds_match: "*", or the first equal kind (one with a group / version: condition_block decides)
+    bool ok = false;
+    for (uint32_t i = 0; i < nk && !ok; i++) {
+      const uint32_t kd = F.kinds[i];
+      if (kd == NONE) ok = true;
+      else if (kd == mf.gk) { ok = true; if ((b >> (24 + i)) & 1u) full = true; }
+    }
+    if (!ok) return false;
+  }
+  if (((b >> 21) & 1u) && !pat_name(mf, F.pats[0])) return false;
+  const uint32_t nn = (b >> 19) & 3u;
+  if (nn && !(pat_name(mf, F.pats[1]) || (nn > 1 && pat_name(mf, F.pats[2])))) return false;
+  const uint32_t ns = (b >> 22) & 3u;
+  if (ns && !(pat_ns(mf, F.pats[3]) || (ns > 1 && pat_ns(mf, F.pats[4])))) return false;
+  if (full) return condition_block(v, v.filters[F.idx], rv, nsl, uic, nd);
+  return !(uic && (b & FF_USERINFO));
+}
+
+// match_rule (kyv_eval.h) over a record
+KYV_HD bool match_rule_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& nsl,
+                           bool* nd) {
+  const uint32_t mm = (R.bits >> 8) & 0xFFu, em = (R.bits >> 16) & 0xFFu, nmf = (R.bits >> 24) & 0xFu, nef = R.bits >> 28;
+  bool failed = false;
+  if (mm == MM_ANY) {
+    bool one = false;
+    for (uint32_t i = 0; i < nmf && !one; i++)
+      if (!(R.f[i].bits & FF_ZERO_RD) && cb_rec(v, R.f[i], mf, rv, nsl, false, nd)) one = true;
+    if (!one) failed = true;
+  } else if (mm == MM_ALL || mm == MM_PLAIN) {
+    for (uint32_t i = 0; i < nmf && !failed; i++)
+      if ((R.f[i].bits & FF_ZERO_RD) || !cb_rec(v, R.f[i], mf, rv, nsl, false, nd)) failed = true;
+  } else {
+    failed = true;
+  }
+  if (failed) return false;
+  if (em == MM_ANY || em == MM_PLAIN) {
+    for (uint32_t i = 0; i < nef; i++) {
+      const MRecFilter& F = R.f[nmf + i];
+      if ((F.bits & FF_ZERO_RD) && !(F.bits & FF_USERINFO)) continue;
+      if (cb_rec(v, F, mf, rv, nsl, true, nd)) return false;
+    }
+  } else if (em == MM_ALL) {
+    bool byAll = true;
+    for (uint32_t i = 0; i < nef && byAll; i++) {
+      const MRecFilter& F = R.f[nmf + i];
+      const bool excl = !((F.bits & FF_ZERO_RD) && !(F.bits & FF_USERINFO)) && cb_rec(v, F, mf, rv, nsl, true, nd);
+      if (!excl) byAll = false;
+    }
+    if (byAll && nef > 0) return false;
+  }
+  return true;
+}
+
+// pair_match (kyv_pss.h) of a record rule (compiled match block, no exceptions, no empty-OldResource retry)
+KYV_HD bool pair_match_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& nsl,
+                           uint8_t* st) {
+  bool nd = false;
+  if (!(R.flags & RD_GATE_EXACT)) {
+    KYV_ACCT_ADD(0, 16);  // header words the match program compares (model, as pair_match)
+    if (!match_rule_rec(v, R, mf, rv, nsl, &nd)) { *st = ST_NONE; return false; }
+  }
+  if (nd) { *st = ST_ND; return false; }
+  if (R.kind == RK_FALLBACK) { *st = ST_FALLBACK; return false; }
+  return true;
+}
+
 // Pattern / anyPattern rules without preconditions (and compile-time fallback rules): the match phase is only
-// pair_match (kind gate, match / exclude program, PolicyException candidates) and the work-list append, so this
-// kernel carries none of the dispatch code (conditions, PodSecurity calls) whose register need made the rule loop
-// of match_kernel spill every iteration (C4: 10,440 rules per wave, 252 GB of scratch writes per evaluation)
-// kWpe: occupancy target (KYV_MATCHW_WPE = 4 / 6 / 8 at run time; 4 by default: 97 VGPRs, none spilled; 8 spills 253)
+// pair_match (kind gate, match / exclude program, PolicyException candidates) and the work-list append, so these
+// kernels carry none of the dispatch code (conditions, PodSecurity calls) whose register need made the rule loop
+// of match_kernel spill every iteration (C4: 10,440 rules per wave, 252 GB of scratch writes per evaluation).
+// match_walk_kernel takes the rules as staged match records (above), MREC_CHUNK at a time through LDS;
+// match_walk_generic_kernel the rules whose match block does not fit a record (pair_match; one kernel for both needs
+// both match programs' registers: 111 VGPRs, 4 waves/SIMD).
+// kWpe: occupancy target (KYV_MATCHW_WPE = 4 / 6 / 8 at run time; 4 by default)
+KYV_HD void match_walk_append(const View& v, DevOut& o, WorkLists& wl, uint32_t k, uint32_t rkind, uint32_t r, bool gated,
+                              bool m, uint8_t st, uint32_t hflags, uint32_t hroot) {
+  const uint32_t lane = threadIdx.x;
+  bool walk = false;
+  if (m) {  // a matched pattern pair: walk it (RF_MAGIC: the CPU engine)
+    if (hflags & RF_MAGIC) st = ST_FALLBACK;
+    else walk = true;
+  }
+  const unsigned long long wm = __ballot(walk);
+  if (rkind == RK_PATTERN || rkind == RK_ANYPATTERN) {
+    const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + blockIdx.x;
+    if (walk) {
+      wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
+          make_uint2(r | ((hflags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), hroot);
+      KYV_ACCT_ADD(1, 8);  // work-list item
+    }
+    if (lane == 0) { wl.cnt[list] = (uint8_t)__popcll(wm); KYV_ACCT_ADD(1, 1); }
+  }
+  if (gated && !walk && st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
+}
+
 template <int kWpe>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
-match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint32_t* __restrict__ mrules, uint32_t nm) {
+match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRec* __restrict__ recs, uint32_t nm) {
+  __shared__ MRec s_rec[MREC_CHUNK];
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
   const uint32_t r = blockIdx.x * BLOCK + lane;
@@ -118,28 +261,70 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uin
   const uint32_t hflags = active ? v.hdr[r].flags : 0u;
   const uint32_t hroot = active ? v.hdr[r].root : 0u;
   if (active) KYV_ACCT_ADD(0, 12);  // header: kind class, flags, root
+  MFacts mf{};
+  LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
+  const ResHeader* hp = active ? &v.hdr[r] : nullptr;
+  if (active) {
+    const ResHeader& h = *hp;
+    const uint32_t name = h.name, kind = h.kind;
+    mf.gk = h.gvk_kind;
+    mf.rname = name == SID_EMPTY ? h.gen_name : name;
+    const bool isNs = v.str_len[kind] == 9 && bytes_eq(sbytes(v, kind), (const uint8_t*)"Namespace", 9);
+    mf.rns = isNs ? name : h.ns;
+    if (v.str_gmask) {  // (records with a glob-mask pattern are only built when the batch has masks)
+      const uint32_t w = v.gmask_words;
+      const uint32_t* a = v.str_gmask + (size_t)mf.rname * w;
+      const uint32_t* b = v.str_gmask + (size_t)mf.rns * w;
+      mf.n0 = a[0]; mf.s0 = b[0];
+      if (w > 1) { mf.n1 = a[1]; mf.s1 = b[1]; }
+      if (w > 2) { mf.n2 = a[2]; mf.s2 = b[2]; }
+      if (w > 3) { mf.n3 = a[3]; mf.s3 = b[3]; }
+    }
+    if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
+  }
+  const ResView rv{NodeTab{v.nodes + hroot}, hp};
+  for (uint32_t c0 = 0; c0 < nm; c0 += MREC_CHUNK) {
+    const uint32_t n = nm - c0 < MREC_CHUNK ? nm - c0 : MREC_CHUNK;
+    __syncthreads();  // the previous chunk's records are read
+    {
+      const uint32_t* src = (const uint32_t*)(recs + c0);
+      uint32_t* dst = (uint32_t*)s_rec;
+      for (uint32_t i = lane; i < n * (uint32_t)(sizeof(MRec) / 4); i += BLOCK) dst[i] = src[i];
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < n; j++) {
+      const MRec& R = s_rec[j];
+      const uint32_t k = __builtin_amdgcn_readfirstlane(R.k);
+      const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+      if (!__ballot(gated)) continue;
+      uint8_t st = ST_NONE;
+      const bool m = gated && pair_match_rec(v, R, mf, rv, nsl, &st);
+      match_walk_append(v, o, wl, k, __builtin_amdgcn_readfirstlane(R.kind), r, gated, m, st, hflags, hroot);
+    }
+  }
+}
+
+template <int kWpe>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
+match_walk_generic_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint32_t* __restrict__ mrules,
+                          uint32_t nm) {
+  const View& v = *vp;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t r = blockIdx.x * BLOCK + lane;
+  const bool active = r < v.nres;
+  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
+  const uint32_t hflags = active ? v.hdr[r].flags : 0u;
+  const uint32_t hroot = active ? v.hdr[r].root : 0u;
+  if (active) KYV_ACCT_ADD(0, 12);  // header: kind class, flags, root
+  (void)lane;
   for (uint32_t mi = 0; mi < nm; mi++) {
     const uint32_t k = mrules[mi];
     const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
     if (!__ballot(gated)) continue;
     const RuleDesc& rdk = v.rules[k];
     uint8_t st = ST_NONE;
-    bool walk = false;
-    if (gated && pair_match(v, r, rdk, &st)) {  // a matched pattern pair: walk it (RF_MAGIC: the CPU engine)
-      if (hflags & RF_MAGIC) st = ST_FALLBACK;
-      else walk = true;
-    }
-    const unsigned long long wm = __ballot(walk);
-    if (rdk.kind == RK_PATTERN || rdk.kind == RK_ANYPATTERN) {
-      const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + blockIdx.x;
-      if (walk) {
-        wl.items[list * WAVE + __popcll(wm & ((1ull << lane) - 1))] =
-            make_uint2(r | ((hflags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), hroot);
-        KYV_ACCT_ADD(1, 8);  // work-list item
-      }
-      if (lane == 0) { wl.cnt[list] = (uint8_t)__popcll(wm); KYV_ACCT_ADD(1, 1); }
-    }
-    if (gated && !walk && st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
+    const bool m = gated && pair_match(v, r, rdk, &st);
+    match_walk_append(v, o, wl, k, rdk.kind, r, gated, m, st, hflags, hroot);
   }
 }
 
