@@ -8,7 +8,7 @@
 namespace kyvacct {
 void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
            const uint32_t* mrules, uint32_t nm);
-void match_walk(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+void match_walk(int wpe, bool mw1, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
                 const void* recs, uint32_t nm);
 void match_walk_generic(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
                         const uint32_t* mrules, uint32_t nm);

@@ -39,10 +39,12 @@ void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* 
   hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl), mrules, nm);
   check(hipGetLastError());
 }
-void match_walk(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+void match_walk(int wpe, bool mw1, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
                 const void* recs, uint32_t nm) {
   using namespace kyv_acct;
-  auto kf = wpe == 8 ? match_walk_kernel<8> : wpe == 6 ? match_walk_kernel<6> : match_walk_kernel<4>;
+  auto kf = wpe == 8 ? (mw1 ? match_walk_kernel<8, 1> : match_walk_kernel<8, 4>)
+          : wpe == 6 ? (mw1 ? match_walk_kernel<6, 1> : match_walk_kernel<6, 4>)
+                     : (mw1 ? match_walk_kernel<4, 1> : match_walk_kernel<4, 4>);
   hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl),
                      (const MRec*)recs, nm);
   check(hipGetLastError());

@@ -1343,8 +1343,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
       static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
       if (sl.nmr) {
-        auto kf = mwpe == 8 ? match_walk_kernel<8> : mwpe == 6 ? match_walk_kernel<6> : match_walk_kernel<4>;
-        if (acct) kyvacct::match_walk(mwpe, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr);
+        const bool mw1 = v.gmask_words <= 1;
+        auto kf = mwpe == 8 ? (mw1 ? match_walk_kernel<8, 1> : match_walk_kernel<8, 4>)
+                : mwpe == 6 ? (mw1 ? match_walk_kernel<6, 1> : match_walk_kernel<6, 4>)
+                            : (mw1 ? match_walk_kernel<4, 1> : match_walk_kernel<4, 4>);
+        if (acct) kyvacct::match_walk(mwpe, mw1, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr);
         else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const MRec*)sl.mrec,
                                 sl.nmr);
       }

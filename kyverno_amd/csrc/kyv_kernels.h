@@ -111,7 +111,7 @@ match_deny_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restr
 // annotations or selectors, or one whose matching kind carries a group / version, runs condition_block itself after
 // the record's checks passed; a rule the record cannot hold (exceptions, the empty-OldResource retry, more than
 // MREC_F filters / 4 kinds / 2 names / 2 namespaces, a glob without a mask) runs pair_match.
-constexpr uint32_t MREC_F = 3, MREC_CHUNK = 32, PAT_MASK = 0x80000000u;
+constexpr uint32_t MREC_F = 3, MREC_CHUNK = 16, MREC_LABELS = 8, PAT_MASK = 0x80000000u;
 enum MRecBits : uint32_t { MR_FAST = 1u, MR_MASKS = 2u };
 struct MRecFilter {   // 48 bytes
   uint32_t idx;       // Filter index (condition_block of a tail filter)
@@ -129,8 +129,9 @@ struct MRec {         // 160 bytes
 };
 static_assert(sizeof(MRec) == 160, "match record size");
 
+enum MFactFlag : uint32_t { MF_ISNS = 1u, MF_KIND_EMPTY = 2u };
 struct MFacts {       // the lane's resource: what condition_block compares, and the glob-mask words of its strings
-  uint32_t gk, rname, rns;
+  uint32_t gk, rname, rns, fl;
   uint32_t n0, n1, n2, n3;  // mask words of rname
   uint32_t s0, s1, s2, s3;  // mask words of rns
 };
@@ -148,19 +149,41 @@ KYV_HD bool pat_ns(const MFacts& mf, uint32_t p) {
   return (p & PAT_MASK) ? mf_bit(mf.s0, mf.s1, mf.s2, mf.s3, (p & 0xFFu) - 1u) : p == mf.rns;
 }
 
-// condition_block (kyv_eval.h) of a record filter
-KYV_HD bool cb_rec(const View& v, const MRecFilter& F, const MFacts& mf, const ResView& rv, const LabelSet& nsl, bool uic,
-                   bool* nd) {
+// condition_block (kyv_eval.h:500-539) after its kinds / name / namespace checks: annotations, selector (over the
+// lane's labels, staged in LDS), namespace selector, user info
+KYV_HD bool cb_tail(const View& v, const Filter& f, const ResView& rv, const LabelSet& labels, const LabelSet& nsl,
+                    bool uic, bool* nd, uint32_t fl) {
+  if (f.nann) {
+    LabelSet as{rv.R, rv.h ? rv.h->ann : NONE, nullptr, 0};
+    const uint32_t n = ls_count(as);
+    for (uint32_t q = 0; q < f.nann; q++) {
+      const uint32_t kp = v.pool[f.ann + 2 * q], vp = v.pool[f.ann + 2 * q + 1];
+      bool m = false;
+      for (uint32_t i = 0; i < n && !m; i++) m = glob_sid(v, kp, ls_key(as, i)) && glob_sid(v, vp, ls_val(as, i));
+      if (!m) return false;
+    }
+  }
+  if ((f.flags & FF_HAS_SEL) && check_selector(v, v.sels[f.sel], labels, nd) != 1) return false;
+  if ((f.flags & FF_HAS_NSSEL) && !(fl & MF_ISNS) && (!(fl & MF_KIND_EMPTY) || (f.flags & FF_KINDS_STAR))) {
+    if (check_selector(v, v.sels[f.sel + 1], nsl, nd) != 1) return false;
+  }
+  return !(uic && (f.flags & FF_USERINFO));
+}
+
+// condition_block (kyv_eval.h) of a record filter: kinds, name, names and namespaces from the record and the lane's
+// facts (a kind with a group / version that equals the resource's: kinds_match decides), then the tail
+KYV_HD bool cb_rec(const View& v, const MRecFilter& F, const MFacts& mf, const ResView& rv, const LabelSet& labels,
+                   const LabelSet& nsl, bool uic, bool* nd) {
   const uint32_t b = F.bits;
-  bool full = (b >> 28) & 1u;
   const uint32_t nk = (b >> 16) & 7u;
-  if (nk) {  // kinds_match: "*", or the first equal kind (one with a group / version: condition_block decides)
-    bool ok = false;
+  if (nk) {
+    bool ok = false, gv = false;
     for (uint32_t i = 0; i < nk && !ok; i++) {
       const uint32_t kd = F.kinds[i];
       if (kd == NONE) ok = true;
-      else if (kd == mf.gk) { ok = true; if ((b >> (24 + i)) & 1u) full = true; }
+      else if (kd == mf.gk) { ok = true; gv = (b >> (24 + i)) & 1u; }
     }
+    if (gv) ok = kinds_match(v, v.filters[F.idx], rv.h);
     if (!ok) return false;
   }
   if (((b >> 21) & 1u) && !pat_name(mf, F.pats[0])) return false;
@@ -168,23 +191,23 @@ KYV_HD bool cb_rec(const View& v, const MRecFilter& F, const MFacts& mf, const R
   if (nn && !(pat_name(mf, F.pats[1]) || (nn > 1 && pat_name(mf, F.pats[2])))) return false;
   const uint32_t ns = (b >> 22) & 3u;
   if (ns && !(pat_ns(mf, F.pats[3]) || (ns > 1 && pat_ns(mf, F.pats[4])))) return false;
-  if (full) return condition_block(v, v.filters[F.idx], rv, nsl, uic, nd);
+  if ((b >> 28) & 1u) return cb_tail(v, v.filters[F.idx], rv, labels, nsl, uic, nd, mf.fl);
   return !(uic && (b & FF_USERINFO));
 }
 
 // match_rule (kyv_eval.h) over a record
-KYV_HD bool match_rule_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& nsl,
-                           bool* nd) {
+KYV_HD bool match_rule_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& labels,
+                           const LabelSet& nsl, bool* nd) {
   const uint32_t mm = (R.bits >> 8) & 0xFFu, em = (R.bits >> 16) & 0xFFu, nmf = (R.bits >> 24) & 0xFu, nef = R.bits >> 28;
   bool failed = false;
   if (mm == MM_ANY) {
     bool one = false;
     for (uint32_t i = 0; i < nmf && !one; i++)
-      if (!(R.f[i].bits & FF_ZERO_RD) && cb_rec(v, R.f[i], mf, rv, nsl, false, nd)) one = true;
+      if (!(R.f[i].bits & FF_ZERO_RD) && cb_rec(v, R.f[i], mf, rv, labels, nsl, false, nd)) one = true;
     if (!one) failed = true;
   } else if (mm == MM_ALL || mm == MM_PLAIN) {
     for (uint32_t i = 0; i < nmf && !failed; i++)
-      if ((R.f[i].bits & FF_ZERO_RD) || !cb_rec(v, R.f[i], mf, rv, nsl, false, nd)) failed = true;
+      if ((R.f[i].bits & FF_ZERO_RD) || !cb_rec(v, R.f[i], mf, rv, labels, nsl, false, nd)) failed = true;
   } else {
     failed = true;
   }
@@ -193,13 +216,13 @@ KYV_HD bool match_rule_rec(const View& v, const MRec& R, const MFacts& mf, const
     for (uint32_t i = 0; i < nef; i++) {
       const MRecFilter& F = R.f[nmf + i];
       if ((F.bits & FF_ZERO_RD) && !(F.bits & FF_USERINFO)) continue;
-      if (cb_rec(v, F, mf, rv, nsl, true, nd)) return false;
+      if (cb_rec(v, F, mf, rv, labels, nsl, true, nd)) return false;
     }
   } else if (em == MM_ALL) {
     bool byAll = true;
     for (uint32_t i = 0; i < nef && byAll; i++) {
       const MRecFilter& F = R.f[nmf + i];
-      const bool excl = !((F.bits & FF_ZERO_RD) && !(F.bits & FF_USERINFO)) && cb_rec(v, F, mf, rv, nsl, true, nd);
+      const bool excl = !((F.bits & FF_ZERO_RD) && !(F.bits & FF_USERINFO)) && cb_rec(v, F, mf, rv, labels, nsl, true, nd);
       if (!excl) byAll = false;
     }
     if (byAll && nef > 0) return false;
@@ -208,12 +231,12 @@ KYV_HD bool match_rule_rec(const View& v, const MRec& R, const MFacts& mf, const
 }
 
 // pair_match (kyv_pss.h) of a record rule (compiled match block, no exceptions, no empty-OldResource retry)
-KYV_HD bool pair_match_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& nsl,
-                           uint8_t* st) {
+KYV_HD bool pair_match_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& labels,
+                           const LabelSet& nsl, uint8_t* st) {
   bool nd = false;
   if (!(R.flags & RD_GATE_EXACT)) {
     KYV_ACCT_ADD(0, 16);  // header words the match program compares (model, as pair_match)
-    if (!match_rule_rec(v, R, mf, rv, nsl, &nd)) { *st = ST_NONE; return false; }
+    if (!match_rule_rec(v, R, mf, rv, labels, nsl, &nd)) { *st = ST_NONE; return false; }
   }
   if (nd) { *st = ST_ND; return false; }
   if (R.kind == RK_FALLBACK) { *st = ST_FALLBACK; return false; }
@@ -249,10 +272,14 @@ KYV_HD void match_walk_append(const View& v, DevOut& o, WorkLists& wl, uint32_t 
   if (gated && !walk && st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
 }
 
-template <int kWpe>
+// kMW: glob-mask words held per string (1 when the ruleset has at most 32 mask bits, else 4)
+template <int kWpe, int kMW>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
 match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRec* __restrict__ recs, uint32_t nm) {
   __shared__ MRec s_rec[MREC_CHUNK];
+  // the lane's labels (key, value sid pairs; stride 2 * MREC_LABELS + 1 words: no bank conflicts), when it has at most
+  // MREC_LABELS of them
+  __shared__ uint32_t s_lab[BLOCK * (2 * MREC_LABELS + 1)];
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
   const uint32_t r = blockIdx.x * BLOCK + lane;
@@ -271,18 +298,30 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRe
     mf.rname = name == SID_EMPTY ? h.gen_name : name;
     const bool isNs = v.str_len[kind] == 9 && bytes_eq(sbytes(v, kind), (const uint8_t*)"Namespace", 9);
     mf.rns = isNs ? name : h.ns;
+    mf.fl = (isNs ? MF_ISNS : 0u) | (kind == SID_EMPTY ? MF_KIND_EMPTY : 0u);
     if (v.str_gmask) {  // (records with a glob-mask pattern are only built when the batch has masks)
       const uint32_t w = v.gmask_words;
       const uint32_t* a = v.str_gmask + (size_t)mf.rname * w;
       const uint32_t* b = v.str_gmask + (size_t)mf.rns * w;
       mf.n0 = a[0]; mf.s0 = b[0];
-      if (w > 1) { mf.n1 = a[1]; mf.s1 = b[1]; }
-      if (w > 2) { mf.n2 = a[2]; mf.s2 = b[2]; }
-      if (w > 3) { mf.n3 = a[3]; mf.s3 = b[3]; }
+      if (kMW > 1) {
+        if (w > 1) { mf.n1 = a[1]; mf.s1 = b[1]; }
+        if (w > 2) { mf.n2 = a[2]; mf.s2 = b[2]; }
+        if (w > 3) { mf.n3 = a[3]; mf.s3 = b[3]; }
+      }
     }
     if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
   }
   const ResView rv{NodeTab{v.nodes + hroot}, hp};
+  LabelSet labels{rv.R, hp ? hp->labels : NONE, nullptr, 0};
+  {
+    const uint32_t nl = ls_count(labels);
+    if (active && nl <= MREC_LABELS) {
+      uint32_t* kv = s_lab + lane * (2 * MREC_LABELS + 1);
+      for (uint32_t i = 0; i < nl; i++) { kv[2 * i] = ls_key(labels, i); kv[2 * i + 1] = ls_val(labels, i); }
+      labels = LabelSet{NodeTab{nullptr}, 0, kv, nl};
+    }
+  }
   for (uint32_t c0 = 0; c0 < nm; c0 += MREC_CHUNK) {
     const uint32_t n = nm - c0 < MREC_CHUNK ? nm - c0 : MREC_CHUNK;
     __syncthreads();  // the previous chunk's records are read
@@ -298,7 +337,7 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRe
       const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
       if (!__ballot(gated)) continue;
       uint8_t st = ST_NONE;
-      const bool m = gated && pair_match_rec(v, R, mf, rv, nsl, &st);
+      const bool m = gated && pair_match_rec(v, R, mf, rv, labels, nsl, &st);
       match_walk_append(v, o, wl, k, __builtin_amdgcn_readfirstlane(R.kind), r, gated, m, st, hflags, hroot);
     }
   }
