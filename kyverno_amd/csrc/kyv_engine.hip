@@ -314,6 +314,7 @@ struct SliceSched {
   uint32_t nmr = 0;              // pattern rules on match_walk_kernel, as staged match records (kyv_kernels.h MRec)
   MRec* mrec = nullptr;          // [nmr]
   uint32_t nmd = 0;              // then deny rules without JMESPath on match_deny_kernel
+  uint32_t nmp = 0;              // then pattern rules with preconditions without JMESPath on match_pre_kernel
   uint32_t nm = 0, nmj = 0, nmc = 0;  // then [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
                                  // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
   std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
@@ -1048,6 +1049,17 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       for (uint32_t q : mr) (rs.rules[q].kind == RK_DENY ? md : rest).push_back(q);
       mr.swap(rest);
     }
+    // light pattern rules with preconditions: match_pre_kernel (KYV_PRE_KERNEL=0: the light match kernel)
+    static const bool pre_k = !getenv("KYV_PRE_KERNEL") || atoi(getenv("KYV_PRE_KERNEL")) != 0;
+    std::vector<uint32_t> mp;
+    if (pre_k) {
+      std::vector<uint32_t> rest;
+      for (uint32_t q : mr) {
+        const RuleDesc& rd = rs.rules[q];
+        ((rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) && rd.pre != NONE ? mp : rest).push_back(q);
+      }
+      mr.swap(rest);
+    }
     const size_t nlight = mr.size();
     // KYV_JC_ONLY=k1,k2,...: timing experiments only (the compiled condition kernel runs just those rules; the
     // other condition rules' verdicts are left unset)
@@ -1110,8 +1122,10 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       HIP_OK(dmalloc(&sl.mrec, recs.size() * sizeof(MRec)));
       HIP_OK(hipMemcpy(sl.mrec, recs.data(), recs.size() * sizeof(MRec), hipMemcpyHostToDevice));
     }
-    sl.nmw = (uint32_t)mw.size();  // device list: [match_walk_generic_kernel rules][deny][light][JMESPath][compiled]
+    sl.nmw = (uint32_t)mw.size();  // device list: [match_walk_generic_kernel rules][deny][pre][light][JMESPath][compiled]
     sl.nmd = (uint32_t)md.size();
+    sl.nmp = (uint32_t)mp.size();
+    mr.insert(mr.begin(), mp.begin(), mp.end());
     mr.insert(mr.begin(), md.begin(), md.end());
     mr.insert(mr.begin(), mw.begin(), mw.end());
     dfree(sl.mrules);
@@ -1363,7 +1377,12 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         else hipLaunchKernelGGL(match_deny_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o,
                                 (const uint32_t*)sl.mrules + sl.nmw, sl.nmd);
       }
-      const uint32_t ml0 = sl.nmw + sl.nmd;
+      if (sl.nmp) {
+        if (acct) kyvacct::match_pre(grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw + sl.nmd, sl.nmp);
+        else hipLaunchKernelGGL(match_pre_kernel<KYV_MATCH_WPE>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
+                                (const uint32_t*)sl.mrules + sl.nmw + sl.nmd, sl.nmp);
+      }
+      const uint32_t ml0 = sl.nmw + sl.nmd + sl.nmp;
       if (sl.nm) {
         if (acct) kyvacct::match(false, grid.x, stream, d.view, &o, &d.wl, sl.mrules + ml0, sl.nm);
         else hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,

@@ -367,6 +367,40 @@ match_walk_generic_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, c
   }
 }
 
+// Pattern / anyPattern rules with preconditions and no JMESPath operands (C5): pair_match, checkPreconditions
+// (validation.go:281-288), then the work-list append -- without the PodSecurity / deny dispatch code of match_kernel,
+// whose register need spilled its rule loop (C5 round 4: match_kernel<false> 166 VGPRs + 176 B of scratch per lane;
+// 4.1 GB of scratch writes per evaluation in the match phase)
+template <int kWpe>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
+match_pre_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint32_t* __restrict__ mrules, uint32_t nm) {
+  const View& v = *vp;
+  const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
+  const bool active = r < v.nres;
+  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
+  const uint32_t hflags = active ? v.hdr[r].flags : 0u;
+  const uint32_t hroot = active ? v.hdr[r].root : 0u;
+  if (active) KYV_ACCT_ADD(0, 12);  // header: kind class, flags, root
+  for (uint32_t mi = 0; mi < nm; mi++) {
+    const uint32_t k = mrules[mi];
+    const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+    if (!__ballot(gated)) continue;
+    const RuleDesc& rd = v.rules[k];
+    uint8_t st = ST_NONE;
+    bool m = false;
+    if (gated && pair_match(v, r, rd, &st)) {
+      uint32_t ec, es, eg;
+      const int c = eval_prog<false>(v, NodeTab{v.nodes + hroot}, rd.pre, &ec, &es, &eg, NONE, r);
+      if (c == CR_FB) st = (KYV_WHY(FBW_COND), ST_FALLBACK);
+      else if (c == CR_PANIC) st = ST_PANIC;
+      else if (c == CP_ERROR) st = ST_ERROR | ST_MARK_PRE;
+      else if (c == CR_FALSE) st = ST_SKIP | ST_MARK_PRE;
+      else m = true;
+    }
+    match_walk_append(v, o, wl, k, rd.kind, r, gated, m, st, hflags, hroot);
+  }
+}
+
 // PodSecurity rules (without preconditions): one lane per resource over the match waves [w0, w0 + grid) of the rule's
 // kind gate, the match and the path-column checks inlined. The per-container checks (pss_container_facts) run with
 // one container per lane across the wave -- the 64 pods' container lists concatenated, a lane's facts OR-ed into its
