@@ -44,7 +44,8 @@ void match_walk(int wpe, bool mw1, unsigned grid, hipStream_t s, const void* vie
   using namespace kyv_acct;
   auto kf = wpe == 8 ? (mw1 ? match_walk_kernel<8, 1> : match_walk_kernel<8, 4>)
           : wpe == 6 ? (mw1 ? match_walk_kernel<6, 1> : match_walk_kernel<6, 4>)
-                     : (mw1 ? match_walk_kernel<4, 1> : match_walk_kernel<4, 4>);
+          : wpe == 4 ? (mw1 ? match_walk_kernel<4, 1> : match_walk_kernel<4, 4>)
+                     : (mw1 ? match_walk_kernel<5, 1> : match_walk_kernel<5, 4>);
   hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl),
                      (const MRec*)recs, nm);
   check(hipGetLastError());

@@ -1355,12 +1355,14 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipEventRecord(sl.evs, stream));
       HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
       HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
-      static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
+      // match_walk_kernel: 5 waves/SIMD by default (96 VGPRs); the generic kernel 4 unless KYV_MATCHW_WPE says 6 / 8
+      static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 5;
       if (sl.nmr) {
         const bool mw1 = v.gmask_words <= 1;
         auto kf = mwpe == 8 ? (mw1 ? match_walk_kernel<8, 1> : match_walk_kernel<8, 4>)
                 : mwpe == 6 ? (mw1 ? match_walk_kernel<6, 1> : match_walk_kernel<6, 4>)
-                            : (mw1 ? match_walk_kernel<4, 1> : match_walk_kernel<4, 4>);
+                : mwpe == 4 ? (mw1 ? match_walk_kernel<4, 1> : match_walk_kernel<4, 4>)
+                            : (mw1 ? match_walk_kernel<5, 1> : match_walk_kernel<5, 4>);
         if (acct) kyvacct::match_walk(mwpe, mw1, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr);
         else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const MRec*)sl.mrec,
                                 sl.nmr);

@@ -331,10 +331,20 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRe
       for (uint32_t i = lane; i < n * (uint32_t)(sizeof(MRec) / 4); i += BLOCK) dst[i] = src[i];
     }
     __syncthreads();
+    // the chunk's kind-gate bits, loaded together (independent loads: one latency per chunk, not one per rule)
+    uint32_t gm = 0;
+    if (active) {
+#pragma unroll 8
+      for (uint32_t j = 0; j < MREC_CHUNK; j++)
+        if (j < n) {
+          const uint32_t k = s_rec[j].k;
+          gm |= ((gate[k >> 5] >> (k & 31)) & 1u) << j;
+        }
+    }
     for (uint32_t j = 0; j < n; j++) {
       const MRec& R = s_rec[j];
       const uint32_t k = __builtin_amdgcn_readfirstlane(R.k);
-      const bool gated = active && ((gate[k >> 5] >> (k & 31)) & 1u);
+      const bool gated = (gm >> j) & 1u;
       if (!__ballot(gated)) continue;
       uint8_t st = ST_NONE;
       const bool m = gated && pair_match_rec(v, R, mf, rv, labels, nsl, &st);
