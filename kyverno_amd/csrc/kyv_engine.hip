@@ -881,16 +881,15 @@ static size_t slice_budget() {
 // Lay out the chunk schedules of one slice's walk kernels (see ChunkMap): runs of match waves with equal gated rule
 // sets, wave-major within a run, whole waves placed on one XCD.
 // The staged match record of match_walk rule q (kyv_kernels.h MRec): MR_FAST when its match block fits the record
-// (compiled, no PolicyException candidates, no empty-OldResource retry, at most MREC_F filters, 4 kinds, 2 names and 2
-// namespaces per filter, every wildcard pattern with a glob-mask bit); else the kernel runs pair_match for it
+// (compiled, no PolicyException candidates, at most MREC_F filters, 4 kinds, 2 names and 2 namespaces per filter,
+// every wildcard pattern with a glob-mask bit); else match_walk_generic_kernel runs pair_match for it
 static void build_mrec(const Ruleset& rs, uint32_t q, const std::vector<uint32_t>& gidx, bool masks_on, bool on, MRec& R) {
   memset(&R, 0, sizeof R);
   const RuleDesc& rd = rs.rules[q];
   R.k = q;
   R.kind = rd.kind;
   R.flags = rd.flags;
-  bool fast = on && rd.match.mode != MM_NONE && !rd.empty_may_match && rd.exc == NONE &&
-              rd.match.nfilters + rd.exclude.nfilters <= MREC_F;
+  bool fast = on && rd.match.mode != MM_NONE && rd.exc == NONE && rd.match.nfilters + rd.exclude.nfilters <= MREC_F;
   bool uses = false;
   auto pat = [&](uint32_t sid) -> uint32_t {  // glob_sid's classification (kyv_eval.h), by the string's content
     if (sid >= rs.dict.strs.size()) { fast = false; return 0; }
@@ -927,7 +926,7 @@ static void build_mrec(const Ruleset& rs, uint32_t q, const std::vector<uint32_t
     for (uint32_t i = 0; i < rd.match.nfilters; i++) fill(rd.match.filters + i, R.f[i]);
     for (uint32_t i = 0; i < rd.exclude.nfilters; i++) fill(rd.exclude.filters + i, R.f[rd.match.nfilters + i]);
   }
-  R.bits = (fast ? MR_FAST : 0u) | (uses ? MR_MASKS : 0u) | ((uint32_t)rd.match.mode << 8) |
+  R.bits = (fast ? MR_FAST : 0u) | (uses ? MR_MASKS : 0u) | (rd.empty_may_match ? MR_EMPTY : 0u) | ((uint32_t)rd.match.mode << 8) |
            ((uint32_t)rd.exclude.mode << 16) | (fast ? (rd.match.nfilters << 24) | (rd.exclude.nfilters << 28) : 0u);
 }
 

@@ -112,7 +112,7 @@ match_deny_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restr
 // the record's checks passed; a rule the record cannot hold (exceptions, the empty-OldResource retry, more than
 // MREC_F filters / 4 kinds / 2 names / 2 namespaces, a glob without a mask) runs pair_match.
 constexpr uint32_t MREC_F = 3, MREC_CHUNK = 16, MREC_LABELS = 8, PAT_MASK = 0x80000000u;
-enum MRecBits : uint32_t { MR_FAST = 1u, MR_MASKS = 2u };
+enum MRecBits : uint32_t { MR_FAST = 1u, MR_MASKS = 2u, MR_EMPTY = 4u };  // MR_EMPTY: empty_may_match
 struct MRecFilter {   // 48 bytes
   uint32_t idx;       // Filter index (condition_block of a tail filter)
   uint32_t bits;      // [0,16) FilterFlag, [16,19) kinds, [19,21) names, 21 name, [22,24) namespaces,
@@ -230,13 +230,18 @@ KYV_HD bool match_rule_rec(const View& v, const MRec& R, const MFacts& mf, const
   return true;
 }
 
-// pair_match (kyv_pss.h) of a record rule (compiled match block, no exceptions, no empty-OldResource retry)
+// pair_match (kyv_pss.h) of a record rule (compiled match block, no exceptions); a rule whose match may accept the
+// empty OldResource (MR_EMPTY, validation.go:606) retries against it: the facts of the empty resource (mf0: kind,
+// name and namespace "", no labels, no annotations)
 KYV_HD bool pair_match_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& labels,
-                           const LabelSet& nsl, uint8_t* st) {
+                           const LabelSet& nsl, const MFacts& mf0, uint8_t* st) {
   bool nd = false;
   if (!(R.flags & RD_GATE_EXACT)) {
     KYV_ACCT_ADD(0, 16);  // header words the match program compares (model, as pair_match)
-    if (!match_rule_rec(v, R, mf, rv, labels, nsl, &nd)) { *st = ST_NONE; return false; }
+    bool m = match_rule_rec(v, R, mf, rv, labels, nsl, &nd);
+    if (!m && (R.bits & MR_EMPTY))
+      m = match_rule_rec(v, R, mf0, ResView{rv.R, nullptr}, LabelSet{NodeTab{nullptr}, 0, nullptr, 0}, nsl, &nd);
+    if (!m) { *st = ST_NONE; return false; }
   }
   if (nd) { *st = ST_ND; return false; }
   if (R.kind == RK_FALLBACK) { *st = ST_FALLBACK; return false; }
@@ -312,6 +317,20 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRe
     }
     if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
   }
+  // the empty OldResource's facts (uniform): every string "", its glob-mask words those of the empty string
+  MFacts mf0{};
+  mf0.gk = mf0.rname = mf0.rns = SID_EMPTY;
+  mf0.fl = MF_KIND_EMPTY;
+  if (v.str_gmask) {
+    const uint32_t w = v.gmask_words;
+    const uint32_t* a = v.str_gmask + (size_t)SID_EMPTY * w;
+    mf0.n0 = mf0.s0 = a[0];
+    if (kMW > 1) {
+      if (w > 1) mf0.n1 = mf0.s1 = a[1];
+      if (w > 2) mf0.n2 = mf0.s2 = a[2];
+      if (w > 3) mf0.n3 = mf0.s3 = a[3];
+    }
+  }
   const ResView rv{NodeTab{v.nodes + hroot}, hp};
   LabelSet labels{rv.R, hp ? hp->labels : NONE, nullptr, 0};
   {
@@ -347,7 +366,7 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRe
       const bool gated = (gm >> j) & 1u;
       if (!__ballot(gated)) continue;
       uint8_t st = ST_NONE;
-      const bool m = gated && pair_match_rec(v, R, mf, rv, labels, nsl, &st);
+      const bool m = gated && pair_match_rec(v, R, mf, rv, labels, nsl, mf0, &st);
       match_walk_append(v, o, wl, k, __builtin_amdgcn_readfirstlane(R.kind), r, gated, m, st, hflags, hroot);
     }
   }
