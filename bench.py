@@ -562,6 +562,11 @@ def main():
     barrier(pg)
     dt = time.perf_counter() - t0
     dt_max = all_max(pg, dt)
+    # the timed evaluation's own verdicts for this rank's shard prefix (parity below), read back before any other
+    # evaluation (serialised, accounting) replaces the resident results
+    prefix_status = None
+    if not args.no_cpu_baseline:
+        prefix_status = timed_prefix_status(batch, local, 400000 if rank == 0 else 100000)
     kernel_ms = kms / max(1, args.steps)
     kernel_ms_max = all_max(pg, kernel_ms)
     phase_span = {k: v / max(1, args.steps) for k, v in phase.items()}
@@ -585,10 +590,6 @@ def main():
     total_pairs = all_sum(pg, dev_pairs)
     total_fb = all_sum(pg, cpu_pairs)
 
-    # the timed evaluation's own verdicts for this rank's shard prefix (parity below), before anything else runs
-    prefix_status = None
-    if not args.no_cpu_baseline:
-        prefix_status = timed_prefix_status(batch, local, 400000 if rank == 0 else 100000)
     # report assembly of a multi-GPU scan: RCCL all-gather of every rank's verdicts and failing-path
     # rows straight from the device-resident results of the last timed evaluation, timed after the evaluation
     gathers = None

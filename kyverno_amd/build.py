@@ -30,7 +30,7 @@ def _needs(obj, src):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def _compile(src, obj_dir=OBJ, defines=()):
+def _compile(src, obj_dir=OBJ, defines=(), host_flags=()):
     path = os.path.join(CSRC, src)
     obj = os.path.join(obj_dir, src + ".o")
     if not _needs(obj, path):
@@ -38,6 +38,10 @@ def _compile(src, obj_dir=OBJ, defines=()):
     cmd = [HIPCC] + COMMON + ["-D" + d for d in defines]
     if src.endswith(".hip"):
         cmd += ["--offload-arch=" + ARCH, "-x", "hip"]
+        for f in host_flags:  # host-side only (sanitizers): never applied to the device code
+            cmd += ["-Xarch_host", f]
+    else:
+        cmd += list(host_flags) + (["-fno-gpu-sanitize"] if host_flags else [])
     cmd += ["-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -45,14 +49,16 @@ def _compile(src, obj_dir=OBJ, defines=()):
     return obj
 
 
-def build(verbose=False, lib=LIB, defines=(), obj_dir=OBJ):
-    """Build the library; `defines`/`lib`/`obj_dir` are for kernel-variant experiments (scripts/build_variants.py)."""
+def build(verbose=False, lib=LIB, defines=(), obj_dir=OBJ, host_flags=(), link_flags=()):
+    """Build the library; `defines`/`lib`/`obj_dir` are for kernel-variant experiments (scripts/build_variants.py),
+    `host_flags`/`link_flags` for the host-sanitizer build (scripts/host_sanitize.sh)."""
     os.makedirs(obj_dir, exist_ok=True)
     srcs = HOST_SRCS + HIP_SRCS
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, obj_dir, defines), srcs))
+        objs = list(ex.map(lambda s: _compile(s, obj_dir, defines, host_flags), srcs))
     if not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread", "-L/opt/rocm/lib", "-lhiprtc", "-lrccl", "-ldl"]
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + list(link_flags) + \
+              ["-lpthread", "-L/opt/rocm/lib", "-lhiprtc", "-lrccl", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stderr[-4000:]))

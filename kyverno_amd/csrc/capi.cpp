@@ -897,6 +897,7 @@ int64_t kyv_comm_gathered_status(const kyv_comm* c, int rank, uint8_t* host_dst,
 
 int64_t kyv_comm_gathered_failures(const kyv_comm* c, int rank, int64_t* host_dst, size_t cap_rows) {
   if (!c || rank < 0 || rank >= c->nranks) return fail(KYV_EINVAL, "bad rank"), -1;
+  if ((size_t)rank >= c->row_counts.size()) return 0;  // no gather yet (or the last one failed before its counts)
   const size_t nr = (size_t)c->row_counts[rank];
   if (!host_dst) return (int64_t)nr;
   if (cap_rows < nr) return fail(KYV_ERANGE, "buffer too small"), -1;

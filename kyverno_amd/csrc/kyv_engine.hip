@@ -94,7 +94,9 @@ static void par_memcpy(void* dst, const void* src, size_t n) {
     });
   for (auto& x : th) x.join();
 }
-// host -> device through the pinned ring on `stream` (pageable hipMemcpy when the ring is off or unavailable)
+// host -> device through the pinned ring on `stream` (pageable hipMemcpy when the ring is off or unavailable). Returns
+// with up to NSLOT transfers still reading their slots: every later user of a slot (the next upload, a copy-back on
+// any thread: staged_d2h) first waits on the slot's event, under the ring's lock
 static hipError_t staged_h2d(uint8_t* dev, const void* src, size_t n, hipStream_t stream) {
   if (!n) return hipSuccess;
   int device = 0;
@@ -125,7 +127,11 @@ static hipError_t staged_d2h(void* dst, const uint8_t* dev, size_t n, hipStream_
   auto issue = [&](size_t c) -> hipError_t {
     const int sl = (int)(c % Staging::NSLOT);
     const size_t off = c * Staging::CHUNK, m = std::min(Staging::CHUNK, n - off);
-    hipError_t r = hipMemcpyAsync(g_staging.buf[sl], dev + off, m, hipMemcpyDeviceToHost, stream);
+    // the slot's previous transfer may still be in flight: an upload (staged_h2d returns with its last DMAs still
+    // reading their slots) from this or another host thread; the DMA into the slot waits for it
+    hipError_t r = hipEventSynchronize(g_staging.ev[sl]);
+    if (r != hipSuccess) return r;
+    r = hipMemcpyAsync(g_staging.buf[sl], dev + off, m, hipMemcpyDeviceToHost, stream);
     return r == hipSuccess ? hipEventRecord(g_staging.ev[sl], stream) : r;
   };
   for (size_t c = 0; c < nch && c < (size_t)Staging::NSLOT - 1; c++)

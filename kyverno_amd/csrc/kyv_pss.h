@@ -516,11 +516,11 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_container_facts(const View& v
         if (!capOK(cap)) f |= F_CAPSB;
         if (cap != KSID(NET_BIND_SERVICE)) f |= F_CAPSR;
       }
-    bool all = false;
+    uint32_t all = 0;  // (loop-carried flags are integer words throughout: see eval_pss)
     if ((uint32_t)dropl != NONE)
       for (uint32_t j = 0; j < (uint32_t)dropl; j++) {
         const PCol e = pcol(v, L[PCL_DROP_SELF], (uint32_t)(dropl >> 32) + j);
-        if (e.t == N_STR && e.a == KSID(ALL)) all = true;
+        if (e.t == N_STR && e.a == KSID(ALL)) all = 1;
       }
     if (!all) f |= F_CAPSR;
   } else {
@@ -588,7 +588,8 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
 
   bool apeBad = false, capsBaseBad = false, capsRBad = false, portsBad = false, privBad = false, procBad = false;
   bool nonRootExplicitBad = false, nonRootImplicitBad = false, userBad = false, selBad = false;
-  bool secBaseBad = false, secRExplicitBad = false, secRImplicitBad = false, hpBad = false, secAnnBad = false;
+  bool secBaseBad = false, secRExplicitBad = false, secRImplicitBad = false, hpBad = false;
+  uint32_t secAnnBad = 0;  // set inside loops: an integer word, not a bool (see eval_pss)
   const bool podNonRootTrue = podNonRoot == 1;
   const bool podSecValid = podSecSet && secValid(podSecType);
   const PCol annc = pcol(v, T[PC_ANN], row);
@@ -596,7 +597,7 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
   const bool annMap = pobj(annc);
   // one pass over the annotations: the appArmor and pod seccomp annotation checks, and whether any key carries the
   // container seccomp prefix (the per-container check below then runs only for such pods)
-  bool annSecC = false;
+  uint32_t annSecC = 0;
   // four entries per step: their node rows, then their keys' flag words, as independent loads (a loop of one entry
   // per iteration is a chain of two dependent loads per annotation)
   const uint32_t nann = annMap ? R[ann].b : 0u, ann0 = annMap ? R[ann].a : 0u;
@@ -613,8 +614,8 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
       const uint32_t key = node_key(e[j]), val = node_type(e[j]) == N_STR ? e[j].a : SID_EMPTY;
       if ((kf[j] & SF_PFX_APPARMOR) && val != KSID(RUNTIME_DEFAULT_PROFILE) && !has_pfx(v, val, SF_PFX_LOCALHOST))
         fails |= 1u << PS_APPARMOR;
-      if (key == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = true;
-      if (kf[j] & SF_PFX_SECCOMP_C) annSecC = true;
+      if (key == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = 1;
+      if (kf[j] & SF_PFX_SECCOMP_C) annSecC = 1;
     }
   }
 
@@ -639,7 +640,7 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
           const uint32_t k = node_key(e);
           if (has_pfx(v, k, SF_PFX_SECCOMP_C) && v.str_len[k] == pl + nl &&
               bytes_eq(sbytes(v, k) + pl, sbytes(v, cname), nl) && node_type(e) == N_STR && e.a == KSID(UNCONFINED_LC))
-            secAnnBad = true;
+            secAnnBad = 1;
         }
       }
     }
@@ -661,11 +662,11 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
   // two volumes per step, and each volume's first four entries (name and source) with them: the loads of one step
   // are independent of each other
   const uint32_t nvol = vols.i != NONE && vols.t == N_ARR ? R[vols.i].b : 0u, vol0 = nvol ? R[vols.i].a : 0u;
-  auto vol_entry = [&](const Node& e, bool* okv) {
+  auto vol_entry = [&](const Node& e, uint32_t* okv) {
     if (node_type(e) == N_NULL) return;
     const uint32_t k = node_key(e);
     if (k == VSID(hostPath)) fails |= 1u << PS_HOSTPATH;
-    if (k >= SID_FIRST_FREE + K_COUNT && k < SID_FIRST_FREE + K_COUNT + V_ALLOWED) *okv = true;
+    if (k >= SID_FIRST_FREE + K_COUNT && k < SID_FIRST_FREE + K_COUNT + V_ALLOWED) *okv = 1;
   };
   for (uint32_t i = 0; i < nvol; i += 2) {
     Node vn[2];
@@ -680,7 +681,7 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
 #pragma unroll
     for (uint32_t j = 0; j < 2; j++) {
       if (i + j >= nvol) break;
-      bool okv = false;
+      uint32_t okv = 0;
       if (node_type(vn[j]) == N_MAP) {
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) vol_entry(en[j][q], &okv);
@@ -764,13 +765,6 @@ KYV_HD uint8_t pss_pod(NodeTab R, uint32_t kind, bool decode, uint32_t* meta_out
   return ST_NONE;
 }
 
-// validatePodSecurity (validation.go:535-566) -> status; *fails receives the remaining failing slots
-// kCols: the decoded pod's checks through path columns only (pss_kernel: inlined, no call frame); the caller routes
-// pairs that need the map walk (exclusions, no columns, typed decode not done) elsewhere
-// (returns ST_NONE with *fails_out = 0 when the column form does not apply)
-// row: the resource's batch position (its column row), passed explicitly by every caller
-// kOol: the checks as the out-of-line pss_checks_cols_ool (eval_pss, see there)
-KYV_FN_PSS uint32_t pss_checks_cols_ool(const View& v, NodeTab R, uint32_t row, const uint32_t* T);
 // the column form's preconditions: ST_NONE with *T = the pod position's column table when the checks run over path
 // columns; ST_ERROR / ST_PANIC / ST_FALLBACK when that is the pair's status already; ST_PSS_MAP when the column form
 // does not apply (exclusion sub-pods, no columns, typed decode not done)
@@ -792,7 +786,9 @@ KYV_HD uint8_t pss_cols_table(const View& v, const PssDesc& pd, const ResHeader&
   return ST_NONE;
 }
 
-template <bool kOol = false>
+// validatePodSecurity (validation.go:535-566) over path columns -> status; *fails_out receives the remaining failing
+// slots; ST_NONE with *fails_out = 0 when the column form does not apply (the caller then takes the map walk). row: the
+// resource's batch position (its column row), passed explicitly by every caller
 KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const PssDesc& pd, const ResHeader& h,
                                                             NodeTab R, uint32_t* fails_out, uint32_t row) {
   *fails_out = 0;
@@ -801,22 +797,20 @@ KYV_HD __attribute__((always_inline)) uint8_t eval_pss_cols(const View& v, const
   if (pre == ST_PSS_MAP) return ST_NONE;
   if (pre != ST_NONE) return pre;
   const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
-  const uint32_t fails = (kOol ? pss_checks_cols_ool(v, R, row, T) : pss_checks_cols(v, R, row, T)) & mask;
+  const uint32_t fails = pss_checks_cols(v, R, row, T) & mask;
   *fails_out = fails;
   return fails ? ST_FAIL : ST_PASS;
 }
 
-// The column checks stay out of line when reached from eval_pss (itself out of line, called from the match kernel).
-// Inlined there (round 3, and again in round 4 with the row passed explicitly) the device computes wrong masks for
-// the C5 baseline rule with preconditions (c5-r006: capability-add and hostPort bits from the loops over
-// column-addressed sub-arrays set where the host instantiation has none); the same source is correct inlined into
-// pss_kernel, in the byte-accounting build (whose atomics change the schedule) and on the host under ASan + UBSan
-// (clean, round 4), and the kernel's stack is statically sized (no dynamic stack). Pinned by
-// tests/test_gpu_parity.py::test_pss_with_preconditions_gpu_equals_cpu (device bytes + masks == host, jit on / off).
-KYV_FN_PSS uint32_t pss_checks_cols_ool(const View& v, NodeTab R, uint32_t row, const uint32_t* T) {
-  return pss_checks_cols(v, R, row, T);
-}
-
+// Loop-carried flags of the PodSecurity checks are integer words, never bools. Rounds 3 / 4 kept the column checks out
+// of line in eval_pss because, inlined there (eval_pss is itself a call from match_kernel), the device set the
+// capabilities / hostPorts failure bits of pods that have neither. Round 5 found the cause on the MI355X with the
+// round-4 source ("PodSecurity miscompile"): the loaded values were right (hashes of every list-length,
+// port and capability entry equal on host and device) and no loop ran past its lane's trip count (guards on
+// optimiser-opaque copies), but the divergent bools set inside the nested container / capability / port loops came out
+// set for lanes that never set them: the lowering of loop-carried divergent i1 values (lane masks merged across nested
+// divergent loops) in the inlined, call-containing function. The same source with those flags as uint32_t words is
+// correct inlined, so the checks are inlined again, with every loop-carried flag an integer word.
 KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const ResHeader& h, uint32_t* fails_out,
                             uint32_t row) {
   *fails_out = 0;
@@ -824,7 +818,7 @@ KYV_FN_PSS uint8_t eval_pss(const View& v, const PssDesc& pd, NodeTab R, const R
   // the typed decode was done by the flattener when it could (RF_PSS_DONE); else here
   const bool done = (h.flags & RF_PSS_DONE) != 0;
   {
-    const uint8_t c = eval_pss_cols<true>(v, pd, h, R, fails_out, row);  // path-column form when it applies
+    const uint8_t c = eval_pss_cols(v, pd, h, R, fails_out, row);  // path-column form when it applies
     if (c != ST_NONE) return c;
   }
   uint32_t meta = NONE, spec = NONE;
