@@ -194,7 +194,8 @@ double kyv_results_kernel_ms(const kyv_results* r);
  * of a pattern ruleset), [3] failing-path compaction, [4] verdict histogram; returns the number of phases (5) */
 int kyv_results_phase_ms(const kyv_results* r, double* out, size_t cap);
 /* bit 0: the runtime-compiled walk kernels evaluated this result's pattern rules (else the interpreter); bit 1: the
- * runtime-compiled condition kernel evaluated its deny / foreach rules with JMESPath operands */
+ * runtime-compiled condition kernel evaluated its deny / foreach rules with JMESPath operands; bit 2: pattern-shape
+ * tables (each distinct compiled pattern walked once per resource) decided the matched pairs of record rules */
 int kyv_results_jit(const kyv_results* r);
 /* with KYV_EVAL_ACCOUNT_BYTES: algorithmic bytes of the evaluation (GPU: counted by the accounting build of the
  * kernels -- node rows, path-column entries, header fields, work lists read; verdicts, PSS masks, failing-path records,

@@ -1290,9 +1290,37 @@ bool jit_rule_fused(const Ruleset& rs, uint32_t k) {
 
 // Rules whose patterns the generator covers get a bit in `jit_rules`; the source holds their node functions,
 // a root switch and the walk kernel `kyv_jit_walk`.
-std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond) {
+bool jit_shape_eligible(const Ruleset& rs, uint32_t k) {
+  static const bool on = !getenv("KYV_SHAPES") || atoi(getenv("KYV_SHAPES")) != 0;
+  if (!on || k >= rs.rules.size()) return false;
+  const RuleDesc& rd = rs.rules[k];
+  return rd.kind == RK_PATTERN && rd.pre == NONE && !(rd.flags & RD_GATE_EXACT) && !jit_rule_fused(rs, k);
+}
+
+// the content of a rule's metadata-expansion sites (what the compiled walk reads through its site base), with pool
+// offsets resolved: two rules with one pattern shape and equal site contents walk identically
+static std::string meta_signature(const Ruleset& rs, const RuleDesc& rd) {
+  std::string o;
+  if (!rd.uses_meta) return o;
+  auto pool = [&](uint32_t at, uint32_t n) {
+    for (uint32_t i = 0; i < 2 * n && at + i < rs.pool.size(); i++) o += std::to_string(rs.pool[at + i]) + ",";
+  };
+  for (uint32_t i = 0; i < rd.nmeta && rd.meta_sites + i < rs.metas.size(); i++) {
+    const MetaSite& m = rs.metas[rd.meta_sites + i];
+    o += "[" + std::to_string(m.has_labels) + "," + std::to_string(m.has_ann) + "," + std::to_string(m.nwild_l) + ":";
+    pool(m.wild_l, m.nwild_l);
+    o += std::to_string(m.nwild_a) + ":";
+    pool(m.wild_a, m.nwild_a);
+    o += std::to_string(m.slot_l) + "," + std::to_string(m.slot_a) + "]";
+  }
+  return o;
+}
+
+std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond,
+                       std::vector<uint16_t>* jit_shape) {
   Gen g(rs);
   jit_rules->assign(rs.rules.size(), 0);
+  if (jit_shape) jit_shape->assign(rs.rules.size(), 0);
   if (jit_cond) jit_cond->assign(rs.rules.size(), 0);
   // one generated function tree per pattern: rulesets with thousands of pattern rules (C4: 10k policies) would
   // give a source too large to compile in useful time; they stay on the interpreted walk kernel
@@ -1583,8 +1611,67 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
       fused_kernels.push_back(std::make_pair(gi, pi));
     }
   }
+  // Pattern shapes shared by match-record rules (round 5): each distinct (shape, metadata-site base) of the eligible
+  // rules is walked once per resource its users' kind gates admit (kyv_jit_shapes), and the match phase decides every
+  // matched pair of those rules from that verdict and record (kyv_kernels.h mrec_shape_out): the walk of a compiled
+  // pattern is a function of the resource alone (no rule input but the metadata-site base), so rules with one shape
+  // share one walk per resource instead of one per matched pair (C4: 10,440 rules, 15 shapes, 1.03 G matched pairs).
+  // (representative root, metadata-site base of the shape's first rule); shapes are keyed by the root's code and the
+  // content of the rule's metadata-expansion sites, so rules with equal sites at other pool offsets share a shape
+  std::vector<std::pair<uint32_t, uint32_t>> shape_list;
+  {
+    std::map<std::pair<uint32_t, std::string>, uint32_t> sid;
+    for (const auto& rr : rule_roots) {
+      const uint32_t k = rr.first;
+      if (!jit_shape_eligible(rs, k) || rr.second.size() != 1) continue;
+      const auto key = std::make_pair(rep_of[rr.second[0]], meta_signature(rs, rs.rules[k]));
+      auto it = sid.find(key);
+      if (it == sid.end()) {
+        if (shape_list.size() >= JIT_MAX_SHAPES) continue;
+        it = sid.emplace(key, (uint32_t)shape_list.size()).first;
+        shape_list.push_back(std::make_pair(rep_of[rr.second[0]], rs.rules[k].meta_sites));
+      }
+      if (jit_shape) (*jit_shape)[k] = (uint16_t)(it->second + 1);
+    }
+  }
+  if (!shape_list.empty()) {
+    // every root function a shape needs is already in the source (its users are covered rules of some group)
+    src << "struct JitShapes {\n"
+           "  __device__ __forceinline__ void run(const View& v, const ShapeOut& so, uint32_t r, bool active, uint32_t hflags,\n"
+           "                                     uint32_t hroot, uint32_t cls) {\n"
+           "    const Node* R = v.nodes + hroot;\n"
+           "    const ResHeader* hp = v.hdr + r;\n"
+           "    const uint32_t row = r < v.nres ? r : NONE;\n"
+           "    const bool rootmap = (hflags & RF_ROOT_MAP) != 0;\n"
+           "    (void)hp; (void)rootmap;\n";
+    for (size_t si = 0; si < shape_list.size(); si++) {
+      const std::string S = Gen::u((uint32_t)si);
+      src << "    {\n"
+             "      const bool gated = active && ((so.gate[(size_t)cls * so.words + " << si / 32 << "u] >> " << si % 32 << "u) & 1u);\n"
+             "      if (__ballot(gated)) {\n"
+             "        const bool magic = gated && (hflags & RF_MAGIC);\n"
+             "        ShapeSink sink{so.rec + (size_t)" << S << " * v.nres + r};\n"
+             "        uint8_t st = pair_walk_alts(true, 1u, gated && !magic, r, 0u, sink, [&](uint32_t, bool wk, PatOut& po) {\n"
+             "          po.status = ST_NONE; po.idx = 0; po.tmpl = NONE; po.key0 = NONE; po.key1 = NONE;\n"
+             "          root" << shape_list[si].first << "(v, R, hp, row, " << Gen::u(shape_list[si].second) << ", rootmap, wk, po);\n"
+             "        });\n"
+             "        if (magic) st = ST_FALLBACK;\n"
+             "        if (gated) { so.st[(size_t)" << S << " * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }\n"
+             "      }\n"
+             "    }\n";
+    }
+    src << "  }\n"
+           "};\n";
+  }
   src << "}  // namespace kyv\n"
          "#ifndef KYV_JIT_WPE\n#define KYV_JIT_WPE 4\n#endif\n";
+  if (!shape_list.empty())
+    // one workgroup (one wave) per match wave, grid-stride; every shape its kind class needs, back to back
+    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JIT_WPE)))\n"
+           "kyv_jit_shapes(const kyv::View* __restrict__ vp, kyv::ShapeOut so) {\n"
+           "  kyv::JitShapes f;\n"
+           "  kyv::walk_shapes(*vp, so, f);\n"
+           "}\n";
   if (!crules.empty()) {
     // compiled condition rules, inlined (one big kernel with a switch over the rules needs an out-of-line call per
     // rule, whose callee-saved registers go through scratch memory, or, inlined, compiles for tens of minutes); one

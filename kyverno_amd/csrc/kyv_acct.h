@@ -8,8 +8,10 @@
 namespace kyvacct {
 void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
            const uint32_t* mrules, uint32_t nm);
-void match_walk(int wpe, bool mw1, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
-                const void* recs, uint32_t nm);
+void match_rec(int wpe, bool mw1, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+               const void* recs, uint32_t nm, const void* index, const void* shapes, const void* tails,
+               const void* facts);
+void facts(bool mw1, unsigned grid, hipStream_t s, const void* view, const void* cfg, void* out);
 void match_walk_generic(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
                         const uint32_t* mrules, uint32_t nm);
 void match_pre(unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl, const uint32_t* mrules,

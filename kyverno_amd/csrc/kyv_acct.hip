@@ -39,15 +39,23 @@ void match(bool kj, unsigned grid, hipStream_t s, const void* view, const void* 
   hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl), mrules, nm);
   check(hipGetLastError());
 }
-void match_walk(int wpe, bool mw1, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
-                const void* recs, uint32_t nm) {
+void match_rec(int wpe, bool mw1, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,
+               const void* recs, uint32_t nm, const void* index, const void* shapes, const void* tails,
+               const void* facts) {
   using namespace kyv_acct;
-  auto kf = wpe == 8 ? (mw1 ? match_walk_kernel<8, 1> : match_walk_kernel<8, 4>)
-          : wpe == 6 ? (mw1 ? match_walk_kernel<6, 1> : match_walk_kernel<6, 4>)
-          : wpe == 4 ? (mw1 ? match_walk_kernel<4, 1> : match_walk_kernel<4, 4>)
-                     : (mw1 ? match_walk_kernel<5, 1> : match_walk_kernel<5, 4>);
+  auto kf = wpe == 8 ? (mw1 ? match_rec_kernel<8, 1> : match_rec_kernel<8, 4>)
+          : wpe == 6 ? (mw1 ? match_rec_kernel<6, 1> : match_rec_kernel<6, 4>)
+          : wpe == 4 ? (mw1 ? match_rec_kernel<4, 1> : match_rec_kernel<4, 4>)
+                     : (mw1 ? match_rec_kernel<5, 1> : match_rec_kernel<5, 4>);
   hipLaunchKernelGGL(kf, dim3(grid), dim3(BLOCK), 0, s, (const View*)view, as<DevOut>(devout), as<WorkLists>(wl),
-                     (const MRec*)recs, nm);
+                     (const MRec*)recs, nm, as<MRecIndex>(index), as<ShapeTab>(shapes), as<TailTab>(tails),
+                     (const ResFacts*)facts);
+  check(hipGetLastError());
+}
+void facts(bool mw1, unsigned grid, hipStream_t s, const void* view, const void* cfg, void* out) {
+  using namespace kyv_acct;
+  hipLaunchKernelGGL(mw1 ? facts_kernel<1> : facts_kernel<4>, dim3(grid), dim3(256), 0, s, (const View*)view,
+                     (const TailCfg*)cfg, (ResFacts*)out);
   check(hipGetLastError());
 }
 void match_walk_generic(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <array>
+#include <map>
 #include <chrono>
 #include <cmath>
 #include <functional>
@@ -188,6 +189,7 @@ struct DevRuleset {
   // compiled condition rules in kernel groups (jit_cond_groups): [group] kyv_jit_condg_<first rule>, its members,
   // the accounting build's kernel; [rule] its group or -1
   std::vector<hipFunction_t> jcg, ajcg;
+  hipFunction_t jshapes = nullptr, ajshapes = nullptr;  // kyv_jit_shapes (pattern-shape tables) and its accounting build
   std::vector<std::vector<uint32_t>> jcg_members;
   std::vector<int32_t> jc_group;
   bool jloaded = false;
@@ -317,8 +319,12 @@ struct SliceSched {
   uint32_t* rbase = nullptr;     // [k1 - k0] first staging slot of each rule (slice-local)
   uint32_t* mrules = nullptr;    // rules of the slice the match phase evaluates (direct-walk rules excluded):
   uint32_t nmw = 0;              // leading rules of mrules on match_walk_generic_kernel (pattern rules: match only)
-  uint32_t nmr = 0;              // pattern rules on match_walk_kernel, as staged match records (kyv_kernels.h MRec)
+  uint32_t nmr = 0;              // pattern rules on match_rec_kernel, as staged match records (kyv_kernels.h MRec)
   MRec* mrec = nullptr;          // [nmr]
+  uint32_t* mcls = nullptr;      // their kind index (MRecIndex): [nclass + 1] offsets into mcrec
+  MRec* mcrec = nullptr;         // the records again, class by class
+  uint32_t nclass = 0;
+  uint8_t* tails = nullptr;      // lane tail facts of the records (TailTab): TailCfg, then the TailProgs
   uint32_t nmd = 0;              // then deny rules without JMESPath on match_deny_kernel
   uint32_t nmp = 0;              // then pattern rules with preconditions without JMESPath on match_pre_kernel
   uint32_t nm = 0, nmj = 0, nmc = 0;  // then [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
@@ -346,6 +352,7 @@ struct DeviceResults {
   FailRec* stage = nullptr;      // per-chunk staging of failing-path records (DevOut), sized for the largest slice
   uint16_t* rcnt = nullptr;
   uint32_t* tsum = nullptr;      // compaction tile sums / offsets
+  uint32_t* tseg = nullptr;      // their segment totals / offsets (compact_scan_kernel)
   unsigned long long* counts = nullptr;
   size_t max_recs = 0;
   uint32_t npss = 0;
@@ -362,6 +369,16 @@ struct DeviceResults {
   hipStream_t wstream = nullptr;
   hipEvent_t wfork = nullptr, wjoin = nullptr;
   View* view = nullptr;  // device copy of the View the kernel reads
+  // pattern-shape tables (kyv_jit_shapes, round 5): [shape][res] verdict bytes and records, the per-class shape gate
+  uint8_t* shape_st = nullptr;
+  FailRec* shape_rec = nullptr;
+  uint32_t* shape_gate = nullptr;
+  uint32_t nshapes = 0, shape_words = 0;
+  int shape_state = -1;  // what the shape gate was laid out for (0: no shapes, 1: the compiled kernels' shapes)
+  // per-evaluation resource facts of the match records (facts_kernel): the ruleset-wide tail configuration, the table
+  TailCfg* tcfg = nullptr;
+  ResFacts* facts = nullptr;
+  bool facts_on = false;
   WorkLists wl{};                // walk work lists (kyv_wave.h), slice-local rule index
   std::vector<SliceSched> slices;
   int cus = 256;
@@ -369,10 +386,11 @@ struct DeviceResults {
 
 static void free_dev_results(DeviceResults& d, int dev) {
   dfree(d.view); dfree(d.status); dfree(d.pss_fails); dfree(d.pss_slot); dfree(d.recs); dfree(d.nrecs); dfree(d.counts);
-  dfree(d.stage); dfree(d.rcnt); dfree(d.tsum);
+  dfree(d.stage); dfree(d.rcnt); dfree(d.tsum); dfree(d.tseg);
+  dfree(d.shape_st); dfree(d.shape_rec); dfree(d.shape_gate); dfree(d.tcfg); dfree(d.facts);
   dfree(d.wl.items); dfree(d.wl.cnt);
   for (auto& sl : d.slices) {
-    dfree(sl.rbase); dfree(sl.mrules); dfree(sl.mrec); dfree(sl.sched);
+    dfree(sl.rbase); dfree(sl.mrules); dfree(sl.mrec); dfree(sl.mcls); dfree(sl.mcrec); dfree(sl.tails); dfree(sl.sched);
     if (sl.evs) hipEventDestroy(sl.evs);
     for (auto e : sl.ev) if (e) hipEventDestroy(e);
     for (auto e : sl.cev) if (e) hipEventDestroy(e);
@@ -524,11 +542,12 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
 }
 
 // ---------------------------------------------------------------- kernels
-// match_kernel, match_walk_kernel, pss_kernel, walk_kernel: kyv_kernels.h
+// match_kernel, match_rec_kernel, pss_kernel, walk_kernel: kyv_kernels.h
 
 // Gather the staged failing-path records of every walk chunk into one dense list, without atomics:
 //   compact_sum_kernel   one wave per 64 consecutive chunks: the tile's record total;
-//   compact_scan_kernel  exclusive prefix over the tiles (one workgroup) and the grand total;
+//   compact_scan_kernel  exclusive prefix over the tiles, per segment of SCAN_SEG tiles, and the segment totals;
+//   compact_top_kernel   exclusive prefix of the segment totals and the grand total;
 //   compact_copy_kernel  one wave per tile: wave prefix of the chunks' counts, then the wave copies each
 //                        non-empty chunk's records cooperatively (lane i moves record i).
 __device__ __forceinline__ const FailRec* chunk_stage(const FailRec* stage, const uint32_t* rbase, const RuleDesc* rules,
@@ -545,19 +564,18 @@ __global__ void __launch_bounds__(WAVE) compact_sum_kernel(const uint16_t* __res
   for (int off = WAVE / 2; off > 0; off >>= 1) n += __shfl_xor(n, off);
   if (threadIdx.x == 0) tsum[blockIdx.x] = n;
 }
-__global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict__ tsum, uint32_t ntiles,
-                                                            uint32_t* __restrict__ nout) {
-  // rounds of 8192 consecutive tiles: each thread scans 8 consecutive tiles, wave inclusive scans of the thread
-  // totals, a scan of the 16 wave totals, carry across rounds
+// exclusive prefix over `n` values in place, one workgroup: rounds of 8192 consecutive values (each thread scans 8,
+// wave inclusive scans of the thread totals, a scan of the 16 wave totals, carry across rounds); returns the total
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* __restrict__ x0, uint32_t n) {
   __shared__ uint32_t wsum[16];
   constexpr uint32_t PER = 8;
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < ntiles; base += 1024 * PER) {
+  for (uint32_t base = 0; base < n; base += 1024 * PER) {
     const uint32_t i0 = base + t * PER;
     uint32_t x[PER], tot = 0;
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) { x[q] = i0 + q < ntiles ? tsum[i0 + q] : 0u; tot += x[q]; }
+    for (uint32_t q = 0; q < PER; q++) { x[q] = i0 + q < n ? x0[i0 + q] : 0u; tot += x[q]; }
     uint32_t v = tot;
     for (int off = 1; off < WAVE; off <<= 1) {
       const uint32_t y = __shfl_up(v, off);
@@ -574,23 +592,40 @@ __global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict
       if (lane < 16) wsum[lane] = s2;
     }
     __syncthreads();
-    uint32_t run = carry + (w ? wsum[w - 1] : 0u) + v - tot;  // exclusive offset of this thread's first tile
+    uint32_t run = carry + (w ? wsum[w - 1] : 0u) + v - tot;  // exclusive offset of this thread's first value
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) {
-      if (i0 + q < ntiles) tsum[i0 + q] = run;
+      if (i0 + q < n) x0[i0 + q] = run;
       run += x[q];
     }
     carry += wsum[15];
     __syncthreads();
   }
-  if (t == 0) *nout = carry;
+  return carry;
+}
+// tile prefix, two levels (round 5: one workgroup over every tile took 0.39 ms per C4 slice): each workgroup scans one
+// segment of SCAN_SEG tiles in place and leaves the segment total; compact_top_kernel scans the segment totals and
+// writes the grand total; the copy adds its segment's offset
+constexpr uint32_t SCAN_SEG = 8192;
+__global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict__ tsum, uint32_t ntiles,
+                                                            uint32_t* __restrict__ seg) {
+  const uint32_t base = blockIdx.x * SCAN_SEG;
+  const uint32_t n = ntiles - base < SCAN_SEG ? ntiles - base : SCAN_SEG;
+  const uint32_t tot = block_exclusive_scan(tsum + base, n);
+  if (threadIdx.x == 0) seg[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(1024) compact_top_kernel(uint32_t* __restrict__ seg, uint32_t nseg,
+                                                           uint32_t* __restrict__ nout) {
+  const uint32_t tot = block_exclusive_scan(seg, nseg);
+  if (threadIdx.x == 0) *nout = tot;
 }
 // one wave per tile of 64 chunks: every lane copies records i = lane, lane + 64, ... of the tile (the chunk of record
 // i found by a binary search over the wave's inclusive prefix of the chunk counts), so all loads are independent
 __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __restrict__ stage, const uint32_t* __restrict__ rbase,
                                                             const uint16_t* __restrict__ rcnt, const RuleDesc* __restrict__ rules,
                                                             uint32_t nwaves, size_t total, const uint32_t* __restrict__ tbase,
-                                                            FailRec* __restrict__ out, size_t max_out, uint32_t k0) {
+                                                            const uint32_t* __restrict__ seg, FailRec* __restrict__ out,
+                                                            size_t max_out, uint32_t k0) {
   const uint32_t lane = threadIdx.x;
   const size_t c = (size_t)blockIdx.x * WAVE + lane;
   const uint32_t n = c < total ? rcnt[c] : 0u;
@@ -615,7 +650,7 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
     sw[lane] = (uint32_t)(c % nwaves);
   }
   __syncthreads();
-  const uint32_t base = tbase[blockIdx.x];
+  const uint32_t base = tbase[blockIdx.x] + seg[blockIdx.x / SCAN_SEG];
   // one record per lane: whole FailRecs of wide chunks copied, StageRecs expanded; stores of consecutive lanes are
   // consecutive 32-byte records
   for (uint32_t i = lane; i < T; i += WAVE) {
@@ -772,13 +807,19 @@ static int ruleset_depth(const Ruleset& rs) {
 // per batch; `copy_back` false keeps the verdicts on the device (bench mode).
 // Compile (once per ruleset) and load (once per device) the ruleset's walk kernel; false if unavailable.
 static std::mutex g_jit_mu;
+static void mrs_clear_shapes(Ruleset& rs) {  // no shape kernel: every pattern rule walks
+  std::fill(rs.jit_shape.begin(), rs.jit_shape.end(), (uint16_t)0);
+  rs.jit_nshapes = 0;
+}
 static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   if (dr->jloaded) return true;
   std::lock_guard<std::mutex> lk(g_jit_mu);
   if (!rs.jit_tried) {
     rs.jit_tried = true;
     try {
-      std::string src = jit_source(rs, &rs.jit_rules, &rs.jit_cond);
+      std::string src = jit_source(rs, &rs.jit_rules, &rs.jit_cond, &rs.jit_shape);
+      rs.jit_nshapes = 0;
+      for (auto x : rs.jit_shape) rs.jit_nshapes = std::max<uint32_t>(rs.jit_nshapes, x);
       bool any = false;
       for (auto x : rs.jit_rules) any |= x != 0;
       for (auto x : rs.jit_cond) any |= x != 0;
@@ -806,6 +847,12 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
         break;
       dr->fparts[g].push_back(f);
     }
+  }
+  (void)hipGetLastError();
+  dr->jshapes = nullptr;
+  if (rs.jit_nshapes && hipModuleGetFunction(&dr->jshapes, dr->jmod, "kyv_jit_shapes") != hipSuccess) {
+    dr->jshapes = nullptr;
+    mrs_clear_shapes(rs);
   }
   (void)hipGetLastError();
   dr->jconds.assign(rs.rules.size(), nullptr);
@@ -856,6 +903,8 @@ static bool ensure_jit_acct(Ruleset& rs, DevRuleset* dr) {
   dr->aconds.assign(dr->jconds.size(), nullptr);
   for (size_t k = 0; k < dr->jconds.size(); k++)
     if (dr->jconds[k]) HIP_OK(hipModuleGetFunction(&dr->aconds[k], dr->amod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
+  dr->ajshapes = nullptr;
+  if (dr->jshapes) HIP_OK(hipModuleGetFunction(&dr->ajshapes, dr->amod, "kyv_jit_shapes"));
   dr->ajcg.assign(dr->jcg.size(), nullptr);
   for (size_t g = 0; g < dr->jcg.size(); g++)
     HIP_OK(hipModuleGetFunction(&dr->ajcg[g], dr->amod, ("kyv_jit_condg_" + std::to_string(dr->jcg_members[g][0])).c_str()));
@@ -936,8 +985,241 @@ static void build_mrec(const Ruleset& rs, uint32_t q, const std::vector<uint32_t
            ((uint32_t)rd.exclude.mode << 16) | (fast ? (rd.match.nfilters << 24) | (rd.exclude.nfilters << 28) : 0u);
 }
 
+// glob-mask index + 1 of every dictionary string that is a ruleset wildcard pattern (0: none)
+static std::vector<uint32_t> glob_index(const Ruleset& rs) {
+  std::vector<uint32_t> gidx(rs.dict.strs.size(), 0);
+  for (size_t g = 0; g < rs.gpats.size(); g++) if (rs.gpats[g] < gidx.size()) gidx[rs.gpats[g]] = (uint32_t)g + 1;
+  return gidx;
+}
+static bool mrec_masks_on() { static const bool on = !getenv("KYV_NO_GMASK"); return on; }
+static bool mrec_recs_on() { static const bool on = !getenv("KYV_MREC") || atoi(getenv("KYV_MREC")) != 0; return on; }
+static bool mrec_kernel_on() {
+  static const bool on = !getenv("KYV_MATCHW_KERNEL") || atoi(getenv("KYV_MATCHW_KERNEL")) != 0;
+  return on;
+}
+// 1 + the pattern shape whose tables decide rule q's matched pairs in match_rec_kernel (0: the rule walks): a shape
+// rule of the compiled kernels (jit.cpp jit_shape_eligible) whose match block fits a staged record
+static uint32_t served_shape(const Ruleset& rs, uint32_t q, const std::vector<uint32_t>& gidx, bool jit) {
+  if (!jit || !mrec_kernel_on() || q >= rs.jit_shape.size() || !rs.jit_shape[q]) return 0;
+  const RuleDesc& rd = rs.rules[q];
+  if (rd.pre != NONE || rd.kind != RK_PATTERN || (rd.flags & RD_GATE_EXACT) || rule_needs_jmes(rs, rd)) return 0;
+  MRec R;
+  build_mrec(rs, q, gidx, mrec_masks_on(), mrec_recs_on(), R);
+  return (R.bits & MR_FAST) ? rs.jit_shape[q] : 0u;
+}
+
+// The shape tables of a batch: per kind class the shapes some served rule's kind gate admits (kyv_jit_shapes computes
+// only those), and the [shape][res] verdict / record buffers
+static void setup_shapes(const Ruleset& rs, const Batch& b, DeviceResults& d, bool jit) {
+  d.shape_state = (int)jit;
+  d.nshapes = 0;
+  if (!jit || !rs.jit_nshapes || !b.gate_words) return;
+  const std::vector<uint32_t> gidx = glob_index(rs);
+  const uint32_t S = rs.jit_nshapes, words = (S + 31) / 32, gw = b.gate_words;
+  const size_t nclass = b.gate.size() / gw;
+  std::vector<uint32_t> sg(std::max<size_t>(1, nclass * words), 0);
+  bool any = false;
+  for (uint32_t k = 0; k < rs.rules.size(); k++) {
+    const uint32_t sh = served_shape(rs, k, gidx, jit);
+    if (!sh) continue;
+    for (size_t c = 0; c < nclass; c++)
+      if ((b.gate[c * gw + (k >> 5)] >> (k & 31)) & 1u) { sg[c * words + (sh - 1) / 32] |= 1u << ((sh - 1) % 32); any = true; }
+  }
+  if (!any) return;
+  dfree(d.shape_gate);
+  d.shape_gate = nullptr;
+  HIP_OK(dmalloc(&d.shape_gate, sg.size() * 4));
+  HIP_OK(hipMemcpy(d.shape_gate, sg.data(), sg.size() * 4, hipMemcpyHostToDevice));
+  if (!d.shape_st) {
+    HIP_OK(dmalloc(&d.shape_st, std::max<size_t>(1, (size_t)S * d.nres)));
+    HIP_OK(dmalloc(&d.shape_rec, std::max<size_t>(1, (size_t)S * d.nres) * sizeof(FailRec)));
+  }
+  d.nshapes = S;
+  d.shape_words = words;
+}
+
+// Lane tail facts of a slice's match records (kyv_kernels.h TailCfg): the most used exact selector keys become label
+// slots (namespace-selector keys namespace slots), distinct wildcard requirements and annotation pairs become atoms,
+// each table filled by frequency of use; a tail filter all of whose parts are covered gets a TailProg (MRecFilter.pad
+// = 1 + its index) and is decided from the lane's facts, the others run cb_tail
+static void build_tails(const Ruleset& rs, const std::vector<MRec>& all, std::vector<MRec>& recs,
+                        const std::vector<uint32_t>& gidx, bool onemask, TailCfg& cfg, std::vector<TailProg>& progs) {
+  memset(&cfg, 0, sizeof cfg);
+  progs.clear();
+  using Wild = std::array<uint32_t, 4>;
+  std::map<uint32_t, size_t> keyf, nskeyf;
+  std::map<Wild, size_t> wildf;
+  std::map<std::pair<uint32_t, uint32_t>, size_t> annf;
+  auto tails = [&](auto&& fn) {
+    for (auto& R : recs) {
+      const uint32_t nf = ((R.bits >> 24) & 0xFu) + (R.bits >> 28);
+      for (uint32_t j = 0; j < nf && j < MREC_F; j++)
+        if ((R.f[j].bits >> 28) & 1u) fn(R.f[j]);
+    }
+  };
+  auto tails_all = [&](auto&& fn) {  // the ruleset's record filters (every slice): the configuration is ruleset-wide
+    for (const auto& R : all) {
+      const uint32_t nf = ((R.bits >> 24) & 0xFu) + (R.bits >> 28);
+      for (uint32_t j = 0; j < nf && j < MREC_F; j++)
+        if ((R.f[j].bits >> 28) & 1u) fn(R.f[j]);
+    }
+  };
+  auto wild_of = [](const SelReq& r) { return Wild{r.key, r.vals, r.rkey, r.rval}; };
+  tails_all([&](const MRecFilter& F) {
+    const Filter& f = rs.filters[F.idx];
+    for (uint32_t q = 0; q < f.nann; q++) annf[{rs.pool[f.ann + 2 * q], rs.pool[f.ann + 2 * q + 1]}]++;
+    if (f.flags & FF_HAS_SEL) {
+      const SelDesc& sd = rs.sels[f.sel];
+      if (!sd.invalid)
+        for (uint32_t q = 0; q < sd.nreqs; q++) {
+          const SelReq& r = rs.reqs[sd.reqs + q];
+          if (r.op == RQ_WILD) wildf[wild_of(r)]++; else keyf[r.key]++;
+        }
+    }
+    if (f.flags & FF_HAS_NSSEL) {
+      const SelDesc& sd = rs.sels[f.sel + 1];
+      if (!sd.invalid)
+        for (uint32_t q = 0; q < sd.nreqs; q++)
+          if (rs.reqs[sd.reqs + q].op != RQ_WILD) nskeyf[rs.reqs[sd.reqs + q].key]++;
+    }
+  });
+  auto top = [](auto& freq, size_t cap) {  // the `cap` most used, ties by value (deterministic)
+    std::vector<std::pair<size_t, typename std::decay_t<decltype(freq)>::key_type>> v;
+    for (auto& x : freq) v.push_back({x.second, x.first});
+    std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first != b.first ? a.first > b.first : a.second < b.second; });
+    std::map<typename std::decay_t<decltype(freq)>::key_type, uint32_t> out;
+    for (size_t i = 0; i < v.size() && i < cap; i++) out[v[i].second] = (uint32_t)out.size();
+    return out;
+  };
+  const auto slots = top(keyf, TF_SLOTS), nsslots = top(nskeyf, TF_NSSLOTS);
+  const auto wilds = top(wildf, TF_WILD);
+  const auto anns = top(annf, TF_ANN);
+  cfg.nslot = (uint32_t)slots.size();
+  cfg.nnsslot = (uint32_t)nsslots.size();
+  cfg.nwild = (uint32_t)wilds.size();
+  cfg.nann = (uint32_t)anns.size();
+  for (auto& x : slots) cfg.slot[x.second] = x.first;
+  for (auto& x : nsslots) cfg.nsslot[x.second] = x.first;
+  for (auto& x : wilds) {
+    cfg.wkey[x.second] = x.first[0]; cfg.wval[x.second] = x.first[1];
+    cfg.wrkey[x.second] = x.first[2]; cfg.wrval[x.second] = x.first[3];
+  }
+  for (auto& x : anns) { cfg.akey[x.second] = x.first.first; cfg.aval[x.second] = x.first.second; }
+  // test codes of the atom patterns (kyv_kernels.h TailCode): glob_sid's classification by content, as build_mrec
+  auto code = [&](uint32_t sid) -> uint32_t {
+    if (sid >= rs.dict.strs.size()) return 0u;
+    const std::string& x = rs.dict.strs[sid];
+    bool globby = x.find_first_of("*?") != std::string::npos;
+    for (unsigned char ch : x) if (ch >= 0x80) globby = true;
+    if (!globby) return TC_EXACT;
+    const uint32_t g = gidx[sid];
+    return (g && g - 1 < 32 && onemask) ? (TC_MASK | (g - 1)) : 0u;
+  };
+  for (uint32_t a = 0; a < cfg.nwild; a++) { cfg.wkc[a] = code(cfg.wkey[a]); cfg.wvc[a] = code(cfg.wval[a]); }
+  for (uint32_t a = 0; a < cfg.nann; a++) { cfg.akc[a] = code(cfg.akey[a]); cfg.avc[a] = code(cfg.aval[a]); }
+  cfg.onemask = onemask ? 1u : 0u;
+  // kinds with a group / version refinement: atoms (mode, g, v); the record kind becomes sid | (atom + 1) << 24 and
+  // its group / version bit stays set (filt_fast reads the atom, cb_rec / kinds_match the filter)
+  std::map<std::array<uint32_t, 3>, uint32_t> gvs;
+  for (const auto& R : all) {  // the refinement atoms, in ruleset order
+    const uint32_t nf = ((R.bits >> 24) & 0xFu) + (R.bits >> 28);
+    for (uint32_t j = 0; j < nf && j < MREC_F; j++) {
+      const MRecFilter& F = R.f[j];
+      const Filter& f = rs.filters[F.idx];
+      const uint32_t nk = (F.bits >> 16) & 7u;
+      for (uint32_t i = 0; i < nk; i++) {
+        if (!((F.bits >> (24 + i)) & 1u)) continue;
+        const KindDesc& kd = rs.kinds[f.kinds + i];
+        const std::array<uint32_t, 3> key{kd.gv_mode, kd.g, kd.v};
+        if (gvs.count(key) || gvs.size() >= TF_GV) continue;
+        const uint32_t a = (uint32_t)gvs.size();
+        gvs.emplace(key, a);
+        cfg.gvmode[a] = kd.gv_mode; cfg.gvg[a] = kd.g; cfg.gvv[a] = kd.v;
+      }
+    }
+  }
+  for (auto& R : recs) {
+    const uint32_t nf = ((R.bits >> 24) & 0xFu) + (R.bits >> 28);
+    for (uint32_t j = 0; j < nf && j < MREC_F; j++) {
+      MRecFilter& F = R.f[j];
+      const Filter& f = rs.filters[F.idx];
+      const uint32_t nk = (F.bits >> 16) & 7u;
+      if (!((F.bits >> 24) & 0xFu)) continue;
+      bool ok = true;  // every kind sid fits 24 bits and every refinement gets an atom: the filter's kinds are packed
+      std::array<uint32_t, 4> atom{0, 0, 0, 0};
+      for (uint32_t i = 0; i < nk && ok; i++) {
+        const KindDesc& kd = rs.kinds[f.kinds + i];
+        if (kd.kind != NONE && kd.kind >= (1u << 24)) ok = false;
+        if (!((F.bits >> (24 + i)) & 1u) || !ok) continue;
+        const std::array<uint32_t, 3> key{kd.gv_mode, kd.g, kd.v};
+        auto it = gvs.find(key);
+        if (it == gvs.end()) { ok = false; continue; }
+        atom[i] = it->second + 1;
+      }
+      if (!ok) continue;
+      for (uint32_t i = 0; i < nk; i++)
+        if (F.kinds[i] != NONE) F.kinds[i] |= atom[i] << 24;
+      F.bits |= MRF_KPACK;
+    }
+  }
+  cfg.ngv = (uint32_t)gvs.size();
+  std::map<std::string, uint32_t> seen;  // program bytes -> its index
+  tails([&](MRecFilter& F) {
+    const Filter& f = rs.filters[F.idx];
+    F.pad = 0;
+    uint32_t ann = 0;
+    for (uint32_t q = 0; q < f.nann; q++) {
+      auto it = anns.find({rs.pool[f.ann + 2 * q], rs.pool[f.ann + 2 * q + 1]});
+      if (it == anns.end()) return;
+      ann |= 1u << it->second;
+    }
+    // a selector as a program: every requirement in a slot / atom, at most TP_REQ of them with TP_VALS values each
+    auto cover = [&](uint32_t si, bool ns, SelProg& sp) {
+      memset(&sp, 0, sizeof sp);
+      const SelDesc& sd = rs.sels[si];
+      if (sd.invalid) { sp.n = NONE; return true; }
+      if (sd.nreqs > TP_REQ) return false;
+      sp.n = sd.nreqs;
+      for (uint32_t q = 0; q < sd.nreqs; q++) {
+        const SelReq& r = rs.reqs[sd.reqs + q];
+        uint32_t m;
+        if (r.op == RQ_WILD) {
+          if (ns) return false;
+          auto it = wilds.find(wild_of(r));
+          if (it == wilds.end()) return false;
+          m = it->second;
+        } else {
+          auto& sl = ns ? nsslots : slots;
+          auto it = sl.find(r.key);
+          if (it == sl.end() || r.nvals > TP_VALS) return false;
+          m = it->second;
+          for (uint32_t k = 0; k < r.nvals; k++) sp.vals[q][k] = rs.pool[r.vals + k];
+        }
+        sp.req[q] = r.op | (m << 8) | ((r.op == RQ_WILD ? 0u : r.nvals) << 16);
+      }
+      return true;
+    };
+    TailProg tp;
+    memset(&tp, 0, sizeof tp);
+    tp.ann = ann;
+    if ((f.flags & FF_HAS_SEL) && !cover(f.sel, false, tp.sel)) return;
+    if ((f.flags & FF_HAS_NSSEL) && !cover(f.sel + 1, true, tp.nssel)) return;
+    std::string key((const char*)&tp, sizeof tp);
+    auto it = seen.find(key);
+    if (it == seen.end()) {
+      it = seen.emplace(key, (uint32_t)progs.size()).first;
+      progs.push_back(tp);
+    }
+    F.pad = it->second + 1;
+  });
+}
+
 static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset* dr, DeviceResults& d, SliceSched& sl,
                             bool jit) {
+  // rules of this slice whose matched pairs the shape tables decide in the match phase: no walk chunks for them
+  const std::vector<uint32_t> gidx = glob_index(rs);
+  std::vector<uint32_t> by_shape(sl.k1 - sl.k0, 0);
+  for (uint32_t k = sl.k0; k < sl.k1; k++) by_shape[k - sl.k0] = served_shape(rs, k, gidx, jit);
   const size_t nres = d.nres;
   const uint32_t WIN = getenv("KYV_WIN") ? (uint32_t)std::max(1, atoi(getenv("KYV_WIN"))) : 0xFFFFu;
   const uint32_t nw = d.wl.nwaves, gw = b.gate_words;
@@ -966,6 +1248,7 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     for (uint32_t k = sl.k0; k < sl.k1; k++) {
       if (rs.rules[k].kind != RK_PATTERN && rs.rules[k].kind != RK_ANYPATTERN) continue;
       if (jit && rs.jit_rules[k] && jit_rule_fused(rs, k)) continue;  // its group's fused kernel walks it
+      if (by_shape[k - sl.k0]) continue;  // decided in the match phase from its shape's tables
       if (!((runs[ri].second[k / 32] >> (k % 32)) & 1u)) continue;
       ks[jit ? rs.jit_rules[k] : 0].push_back(k);
     }
@@ -1028,13 +1311,13 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     // PodSecurity rules without preconditions: pss_kernel over the waves of their kind gate (KYV_PSS_KERNEL=0: the
     // match kernel)
     static const bool pss_k = !getenv("KYV_PSS_KERNEL") || atoi(getenv("KYV_PSS_KERNEL")) != 0;
-    static const bool mw_k = !getenv("KYV_MATCHW_KERNEL") || atoi(getenv("KYV_MATCHW_KERNEL")) != 0;
+    const bool mw_k = mrec_kernel_on();
     std::vector<uint32_t> mr, cj, mw;
     sl.pw.clear();
     for (uint32_t q : sl.ml) {
       const RuleDesc& rd = rs.rules[q];
       if (mw_k && rd.pre == NONE && (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN || rd.kind == RK_FALLBACK)) {
-        mw.push_back(q);  // match_walk_kernel
+        mw.push_back(q);  // match_rec_kernel (or the generic kernel)
         continue;
       }
       if (!pss_k || rd.kind != RK_PSS || rd.pre != NONE) { mr.push_back(q); continue; }
@@ -1108,21 +1391,108 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     mr.insert(mr.end(), cj.begin(), cj.end());
     dfree(sl.mrec);
     sl.mrec = nullptr;
-    {  // match_walk rules whose match block fits a staged record go to match_walk_kernel, the rest stay in mrules
+    {  // match_walk rules whose match block fits a staged record go to match_rec_kernel, the rest stay in mrules
       std::vector<MRec> recs;
-      std::vector<uint32_t> gidx(rs.dict.strs.size(), 0);
-      for (size_t g = 0; g < rs.gpats.size(); g++) if (rs.gpats[g] < gidx.size()) gidx[rs.gpats[g]] = (uint32_t)g + 1;
-      static const bool masks_on = !getenv("KYV_NO_GMASK");
-      static const bool recs_on = !getenv("KYV_MREC") || atoi(getenv("KYV_MREC")) != 0;
       std::vector<uint32_t> gen;
       for (uint32_t q : mw) {
         MRec R;
-        build_mrec(rs, q, gidx, masks_on, recs_on, R);
-        if (R.bits & MR_FAST) recs.push_back(R);
-        else gen.push_back(q);
+        build_mrec(rs, q, gidx, mrec_masks_on(), mrec_recs_on(), R);
+        if (R.bits & MR_FAST) {
+          // 1 + its shape: decided from the shape tables; bit 23: the rule stages whole records (metadata keys)
+          R.kind |= (by_shape[q - sl.k0] << 8) | (by_shape[q - sl.k0] && rs.rules[q].uses_meta ? 1u << 23 : 0u);
+          recs.push_back(R);
+        } else {
+          gen.push_back(q);
+        }
       }
       mw.swap(gen);
       sl.nmr = (uint32_t)recs.size();
+      {  // lane tail facts: one device block [TailCfg][TailProg...]
+        TailCfg cfg;
+        std::vector<TailProg> progs;
+        static const bool tails_on = !getenv("KYV_TAIL_FACTS") || atoi(getenv("KYV_TAIL_FACTS")) != 0;
+        if (tails_on) {
+          // every record rule of the ruleset (all slices): the tail configuration is ruleset-wide, so one facts table
+          // per evaluation serves every slice (facts_kernel)
+          std::vector<MRec> all;
+          for (uint32_t q = 0; q < rs.rules.size(); q++) {
+            const RuleDesc& rd = rs.rules[q];
+            if (!(mw_k && rd.pre == NONE && (rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN || rd.kind == RK_FALLBACK))) continue;
+            if ((rd.kind == RK_PATTERN || rd.kind == RK_ANYPATTERN) && (rd.flags & RD_GATE_EXACT)) continue;  // direct walk
+            if (rule_needs_jmes(rs, rd)) continue;
+            MRec R;
+            build_mrec(rs, q, gidx, mrec_masks_on(), mrec_recs_on(), R);
+            if (R.bits & MR_FAST) all.push_back(R);
+          }
+          const bool onemask = mrec_masks_on() && rs.gpats.size() + rs.gsets.size() <= 32;
+          build_tails(rs, all, recs, gidx, onemask, cfg, progs);
+        }
+        else memset(&cfg, 0, sizeof cfg);
+        const size_t bytes = sizeof(TailCfg) + std::max<size_t>(1, progs.size()) * sizeof(TailProg);
+        dfree(sl.tails);
+        sl.tails = nullptr;
+        HIP_OK(dmalloc(&sl.tails, bytes));
+        HIP_OK(hipMemcpy(sl.tails, &cfg, sizeof cfg, hipMemcpyHostToDevice));
+        if (!d.tcfg) HIP_OK(dmalloc(&d.tcfg, sizeof(TailCfg)));
+        HIP_OK(hipMemcpy(d.tcfg, &cfg, sizeof cfg, hipMemcpyHostToDevice));  // (ruleset-wide: equal for every slice)
+        d.facts_on = tails_on;
+        if (!progs.empty()) HIP_OK(hipMemcpy(sl.tails + sizeof(TailCfg), progs.data(), progs.size() * sizeof(TailProg), hipMemcpyHostToDevice));
+        // the branch-free path (MR_FASTEVAL: no group / version kinds, every tail covered) and the empty-OldResource
+        // retry as a constant of the rule (MR_ECONST: no filter reaches a namespace selector for a kind-less
+        // resource), evaluated here with the host instantiation of match_rule against the batch dictionary
+        const View hv = make_view(rs, b, nullptr, nullptr, nullptr, nullptr);
+        for (auto& R : recs) {
+          const uint32_t nf = ((R.bits >> 24) & 0xFu) + (R.bits >> 28);
+          bool fast = true, nsstar = false;
+          for (uint32_t j = 0; j < nf && j < MREC_F; j++) {
+            const MRecFilter& F = R.f[j];
+            if (((F.bits >> 24) & 0xFu) && !(F.bits & MRF_KPACK)) fast = false;  // a group / version kind without its atom
+            if (((F.bits >> 28) & 1u) && !F.pad) fast = false;
+            if ((F.bits & FF_HAS_NSSEL) && (F.bits & FF_KINDS_STAR)) nsstar = true;
+          }
+          if (fast) R.bits |= MR_FASTEVAL;
+          if ((R.bits & MR_EMPTY) && !nsstar) {
+            bool nd = false;
+            const bool em = match_rule(hv, rs.rules[R.k], ResView{NodeTab{nullptr}, nullptr},
+                                       LabelSet{NodeTab{nullptr}, 0, nullptr, 0}, &nd);
+            R.bits |= MR_ECONST | (em ? MR_EMATCH : 0u) | (nd ? MR_END : 0u);
+          }
+        }
+        if (getenv("KYV_DEBUG_STATS")) {
+          size_t nf = 0, ne = 0, nec = 0, nsh = 0;
+          for (auto& R : recs) {
+            nf += (R.bits & MR_FASTEVAL) != 0;
+            ne += (R.bits & MR_EMPTY) != 0;
+            nec += (R.bits & MR_ECONST) != 0;
+            nsh += (R.kind >> 8) != 0;
+          }
+          fprintf(stderr, "[kyvgpu] slice [%u, %u): %zu match records, %zu branch-free, %zu empty retry (%zu constant), "
+                  "%zu shape rules; tail facts: %u slots, %u ns slots, %u wildcard, %u annotation, %u group/version atoms, "
+                  "%zu covered tails\n", sl.k0, sl.k1, recs.size(), nf, ne, nec, nsh, cfg.nslot, cfg.nnsslot, cfg.nwild,
+                  cfg.nann, cfg.ngv, progs.size());
+        }
+      }
+      // the kind index: per kind class of the batch, copies of the records whose rule's kind gate admits it, one
+      // contiguous run per class (a uniform wave streams its class's run: no index load in front of each record)
+      const uint32_t gw = b.gate_words;
+      sl.nclass = gw ? (uint32_t)(b.gate.size() / gw) : 0u;
+      std::vector<uint32_t> off(sl.nclass + 1, 0);
+      std::vector<MRec> crecs;
+      for (uint32_t c = 0; c < sl.nclass; c++) {
+        for (uint32_t q = 0; q < sl.nmr; q++) {
+          const uint32_t k = recs[q].k;
+          if ((b.gate[(size_t)c * gw + (k >> 5)] >> (k & 31)) & 1u) crecs.push_back(recs[q]);
+        }
+        off[c + 1] = (uint32_t)crecs.size();
+      }
+      dfree(sl.mcls);
+      sl.mcls = nullptr;
+      HIP_OK(dmalloc(&sl.mcls, off.size() * 4));
+      HIP_OK(hipMemcpy(sl.mcls, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+      dfree(sl.mcrec);
+      sl.mcrec = nullptr;
+      HIP_OK(dmalloc(&sl.mcrec, std::max<size_t>(1, crecs.size()) * sizeof(MRec)));
+      if (!crecs.empty()) HIP_OK(hipMemcpy(sl.mcrec, crecs.data(), crecs.size() * sizeof(MRec), hipMemcpyHostToDevice));
       recs.resize(std::max<size_t>(1, recs.size()));
       HIP_OK(dmalloc(&sl.mrec, recs.size() * sizeof(MRec)));
       HIP_OK(hipMemcpy(sl.mrec, recs.data(), recs.size() * sizeof(MRec), hipMemcpyHostToDevice));
@@ -1257,6 +1627,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(dmalloc(&d.recs, d.max_recs * sizeof(FailRec)));
     HIP_OK(dmalloc(&d.rcnt, std::max<size_t>(msr * nwv, 1) * 2));
     HIP_OK(dmalloc(&d.tsum, std::max<size_t>((msr * nwv + WAVE - 1) / WAVE, 1) * 4));
+    HIP_OK(dmalloc(&d.tseg, std::max<size_t>((msr * nwv + WAVE - 1) / WAVE / SCAN_SEG + 1, 1) * 4));
     // walk work lists: one 64-slot list per (slice rule, match wave)
     HIP_OK(dmalloc(&d.wl.items, std::max<size_t>(1, msr * nwv * WAVE) * sizeof(uint2)));
     HIP_OK(dmalloc(&d.wl.cnt, std::max<size_t>(4, msr * nwv + 4)));
@@ -1284,6 +1655,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   const bool jit = use_jit && ensure_jit(mrs, dr);
   for (auto& sl : d.slices)
     if (sl.jit_state != (int)jit) layout_schedule(rs, b, dr, d, sl, jit);
+  if (d.shape_state != (int)jit) setup_shapes(rs, b, d, jit && dr->jshapes);
   const bool multi = d.slices.size() > 1;
   int depth = ruleset_depth(rs);
   size_t lds = (size_t)depth * (sizeof(UFrame) + BLOCK * sizeof(LaneFrame));
@@ -1353,6 +1725,26 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     if (acct) aphase[0] += (uint64_t)nres * nrules + (uint64_t)d.npss * nres * 4;  // verdict / PSS-mask resets
+    // pattern-shape tables (round 5): every shape walked once per resource its users admit, before the match phase
+    // that reads them (counted in the match phase: it replaces the walk of the shape rules' matched pairs)
+    if (d.nshapes && nres) {
+      const View* vp = d.view;
+      ShapeOut so{d.shape_st, d.shape_rec, d.shape_gate, d.shape_words, d.wl.nwaves};
+      void* args[] = {(void*)&vp, (void*)&so};
+      const uint32_t sgrid = (uint32_t)std::min<size_t>(d.wl.nwaves, (size_t)d.cus * 32);
+      HIP_OK(hipModuleLaunchKernel(acct ? dr->ajshapes : dr->jshapes, sgrid, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+    }
+    bool any_rec = false;
+    for (auto& sl : d.slices) any_rec = any_rec || sl.nmr;
+    const bool use_facts = any_rec && d.facts_on && d.tcfg && nres;
+    if (use_facts) {  // the match records' resource facts, once per evaluation (read by every slice)
+      if (!d.facts) HIP_OK(dmalloc(&d.facts, nres * sizeof(ResFacts)));
+      const dim3 fg((unsigned)((nres + 255) / 256));
+      const bool mw1 = v.gmask_words <= 1;
+      if (acct) kyvacct::facts(mw1, fg.x, stream, d.view, d.tcfg, d.facts);
+      else hipLaunchKernelGGL(mw1 ? facts_kernel<1> : facts_kernel<4>, fg, dim3(256), 0, stream, (const View*)d.view,
+                              (const TailCfg*)d.tcfg, d.facts);
+    }
     for (auto& sl : d.slices) {
       if (!nres || sl.k1 == sl.k0) continue;
       const size_t nsr = sl.k1 - sl.k0;
@@ -1360,17 +1752,21 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipEventRecord(sl.evs, stream));
       HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
       HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
-      // match_walk_kernel: 5 waves/SIMD by default (96 VGPRs); the generic kernel 4 unless KYV_MATCHW_WPE says 6 / 8
-      static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 5;
+      // match_rec_kernel and the generic kernel: 4 waves/SIMD by default (114 / 86 VGPRs, no scratch); KYV_MATCHW_WPE 5 / 6 / 8
+      static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
       if (sl.nmr) {
         const bool mw1 = v.gmask_words <= 1;
-        auto kf = mwpe == 8 ? (mw1 ? match_walk_kernel<8, 1> : match_walk_kernel<8, 4>)
-                : mwpe == 6 ? (mw1 ? match_walk_kernel<6, 1> : match_walk_kernel<6, 4>)
-                : mwpe == 4 ? (mw1 ? match_walk_kernel<4, 1> : match_walk_kernel<4, 4>)
-                            : (mw1 ? match_walk_kernel<5, 1> : match_walk_kernel<5, 4>);
-        if (acct) kyvacct::match_walk(mwpe, mw1, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr);
+        auto kf = mwpe == 8 ? (mw1 ? match_rec_kernel<8, 1> : match_rec_kernel<8, 4>)
+                : mwpe == 6 ? (mw1 ? match_rec_kernel<6, 1> : match_rec_kernel<6, 4>)
+                : mwpe == 4 ? (mw1 ? match_rec_kernel<4, 1> : match_rec_kernel<4, 4>)
+                            : (mw1 ? match_rec_kernel<5, 1> : match_rec_kernel<5, 4>);
+        const MRecIndex ix{sl.mcls, sl.mcrec};
+        const ShapeTab sh{d.shape_st, d.shape_rec, d.wl.nwaves, d.nshapes};
+        const TailTab tt{(const TailCfg*)sl.tails, (const TailProg*)(sl.tails + sizeof(TailCfg))};
+        const ResFacts* fp = use_facts ? d.facts : nullptr;
+        if (acct) kyvacct::match_rec(mwpe, mw1, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr, &ix, &sh, &tt, fp);
         else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const MRec*)sl.mrec,
-                                sl.nmr);
+                                sl.nmr, ix, sh, tt, fp);
       }
       if (sl.nmw) {
         auto kf = mwpe == 8 ? match_walk_generic_kernel<8> : mwpe == 6 ? match_walk_generic_kernel<6>
@@ -1490,9 +1886,11 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       const uint32_t ntiles = (uint32_t)((nchunks + WAVE - 1) / WAVE);
       const RuleDesc* drules = (const RuleDesc*)(dr->base + dr->o_rules) + sl.k0;
       hipLaunchKernelGGL(compact_sum_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.rcnt, nchunks, d.tsum);
-      hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, d.tsum, ntiles, d.nrecs);
+      const uint32_t nseg = (ntiles + SCAN_SEG - 1) / SCAN_SEG;
+      hipLaunchKernelGGL(compact_scan_kernel, dim3(std::max<uint32_t>(nseg, 1)), dim3(1024), 0, stream, d.tsum, ntiles, d.tseg);
+      hipLaunchKernelGGL(compact_top_kernel, dim3(1), dim3(1024), 0, stream, d.tseg, std::max<uint32_t>(nseg, 1), d.nrecs);
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, sl.rbase, d.rcnt, drules,
-                         d.wl.nwaves, nchunks, d.tsum, d.recs, d.max_recs, sl.k0);
+                         d.wl.nwaves, nchunks, d.tsum, d.tseg, d.recs, d.max_recs, sl.k0);
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(sl.ev[3], stream));
       if (acct) {  // compaction: chunk counts (read twice), tile sums, the staged records read, the dense records written
@@ -1551,7 +1949,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     for (int q = 0; q < 5; q++) out->phase_ms[q] = phase[q] / n;
     bool cond = false;
     for (auto& sl : d.slices) cond |= sl.nmc != 0;
-    out->jit_used = (jit ? 1 : 0) | (jit && cond ? 2 : 0);
+    out->jit_used = (jit ? 1 : 0) | (jit && cond ? 2 : 0) | (jit && d.nshapes ? 4 : 0);
     out->h2d_ms = db->upload_ms;
     if (acct) {
       out->alg_bytes = 0;

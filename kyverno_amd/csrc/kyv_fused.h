@@ -48,4 +48,36 @@ __device__ __forceinline__ void walk_fused(const View& v, DevOut o, uint32_t nwa
   }
 }
 
+// Shape tables (round 5): one record slot per (shape, resource); the shape walk emits at most one record per lane
+// (a pattern rule: one alternative), kept whole (resolved metadata keys included) for the match phase, which copies
+// it into the staging chunk of every matched FAIL pair of the shape's rules (kyv_kernels.h mrec_shape_out)
+struct ShapeSink {
+  FailRec* at;
+  __device__ __forceinline__ void emit(bool has, const FailRec& f) {
+    if (!has) return;
+    *at = f;
+    KYV_ACCT_ADD(1, sizeof(FailRec));
+  }
+};
+
+// kyv_jit_shapes: one wave per match wave (grid-stride), its resources' header words loaded once, then every shape
+// the wave's kind classes need (jit.cpp JitShapes: the verdict byte of each gated lane, its record where FAIL)
+template <class Shapes>
+__device__ __forceinline__ void walk_shapes(const View& v, const ShapeOut& so, Shapes& f) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  for (uint32_t w = blockIdx.x; w < so.nwaves; w += gridDim.x) {
+    const uint32_t r = w * WAVE + lane;
+    const bool active = r < v.nres;
+    uint32_t hflags = 0, hroot = 0, cls = 0;
+    if (active) {
+      const ResHeader* h = v.hdr + r;
+      hflags = gld32(&h->flags);
+      hroot = gld32(&h->root);
+      cls = gld32(&h->kclass);
+      KYV_ACCT_ADD(0, 12);  // header: flags, root, kind class
+    }
+    f.run(v, so, r, active, hflags, hroot, cls);
+  }
+}
+
 }  // namespace kyv

@@ -129,6 +129,8 @@ struct Ruleset {
   bool jit_tried = false;
   std::vector<uint8_t> jit_rules;   // rule k is walked by the compiled kernel
   std::vector<uint8_t> jit_cond;    // rule k (deny / foreach with JMESPath operands) runs in the compiled kyv_jit_cond
+  std::vector<uint16_t> jit_shape;  // 1 + the pattern shape of rule k in kyv_jit_shapes (0: none; jit.cpp)
+  uint32_t jit_nshapes = 0;
   std::vector<char> jit_code;       // gfx950 code object
   std::vector<char> jit_code_acct;  // the same source compiled with -DKYV_ACCT (byte-accounting evaluation only)
   std::string jit_error;
@@ -214,7 +216,12 @@ void derive_strings(Batch& b, size_t from, int threads);
 void build_path_trie(Ruleset& rs);
 void assign_glob_masks(Ruleset& rs);
 void assign_cond_sets(Ruleset& rs);
-std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond = nullptr);
+std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::vector<uint8_t>* jit_cond = nullptr,
+                       std::vector<uint16_t>* jit_shape = nullptr);
+// pattern rules the shape tables can decide (kyv_jit_shapes): a covered RK_PATTERN rule without metadata expansion,
+// preconditions or a fused walk (its match program runs in the match phase)
+bool jit_shape_eligible(const Ruleset& rs, uint32_t k);
+constexpr uint32_t JIT_MAX_SHAPES = 64;
 std::vector<char> jit_compile(const std::string& src, double* seconds, bool acct = false);
 // rule k is walked by its group's fused kernel (kyv_jit_fused_<g>) rather than the per-chunk schedule (jit.cpp)
 bool jit_rule_fused(const Ruleset& rs, uint32_t k);

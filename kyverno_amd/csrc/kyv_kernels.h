@@ -102,21 +102,28 @@ match_deny_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restr
   }
 }
 
-// Staged match records of match_walk_kernel. Every wave runs the same rule loop, so a rule's match program was a chain
-// of dependent uniform loads (rule list -> RuleDesc -> Filter -> KindDesc / pattern sids -> pattern flags -> the
-// string's glob mask) paid by every wave for every rule: the C4 loop (10,440 rules) was latency-bound (wait 0.85).
-// The host lays each rule's match block out as one fixed-size record (kinds, name / names / namespaces patterns with
-// their glob-mask bit resolved); a wave copies MREC_CHUNK records into LDS with one coalesced load and evaluates them
-// against the lane's resource facts (kind, name, namespace and their glob-mask words) held in registers. A filter with
-// annotations or selectors, or one whose matching kind carries a group / version, runs condition_block itself after
-// the record's checks passed; a rule the record cannot hold (exceptions, the empty-OldResource retry, more than
-// MREC_F filters / 4 kinds / 2 names / 2 namespaces, a glob without a mask) runs pair_match.
-constexpr uint32_t MREC_F = 3, MREC_CHUNK = 16, MREC_LABELS = 8, PAT_MASK = 0x80000000u;
-enum MRecBits : uint32_t { MR_FAST = 1u, MR_MASKS = 2u, MR_EMPTY = 4u };  // MR_EMPTY: empty_may_match
+// Staged match records of match_rec_kernel. Every wave runs a rule loop, so a rule's match program read from the rule
+// descriptors was a chain of dependent uniform loads (rule list -> RuleDesc -> Filter -> KindDesc / pattern sids ->
+// pattern flags -> the string's glob mask) paid by every wave for every rule (C4 round 4: wait 0.85). The host lays
+// each rule's match block out as one fixed-size record (kinds, name / names / namespaces patterns with their glob-mask
+// bit resolved); a wave reads it with scalar loads and evaluates it against the lane's resource facts (kind, name,
+// namespace and their glob-mask words) held in registers. A filter with annotations or selectors, or one whose matching
+// kind carries a group / version, runs condition_block's tail itself after the record's checks passed; a rule the
+// record cannot hold (exceptions, more than MREC_F filters / 4 kinds / 2 names / 2 namespaces, a glob without a mask)
+// runs pair_match in match_walk_generic_kernel.
+constexpr uint32_t MREC_F = 3, MREC_LABELS = 8, PAT_MASK = 0x80000000u;
+// MR_EMPTY: empty_may_match; MR_ECONST: the empty-OldResource retry's outcome is a constant of the rule (no filter can
+// reach a namespace selector for a kind-less resource), precomputed on the host as MR_EMATCH / MR_END (matched /
+// nondeterministic); MR_FASTEVAL: every filter is decided by the branch-free path (kinds without group / version,
+// tails covered by the lane tail facts)
+enum MRecBits : uint32_t { MR_FAST = 1u, MR_MASKS = 2u, MR_EMPTY = 4u, MR_ECONST = 8u, MR_EMATCH = 16u, MR_END = 32u,
+                           MR_FASTEVAL = 64u };
+constexpr uint32_t MRF_KPACK = 1u << 29;  // the filter's kinds are packed: sid | (group / version atom + 1) << 24
 struct MRecFilter {   // 48 bytes
   uint32_t idx;       // Filter index (condition_block of a tail filter)
   uint32_t bits;      // [0,16) FilterFlag, [16,19) kinds, [19,21) names, 21 name, [22,24) namespaces,
-                      // [24,28) kind i has a group / version, 28 tail (annotations / selector / namespace selector)
+                      // [24,28) kind i has a group / version, 28 tail (annotations / selector / namespace selector),
+                      // 29 MRF_KPACK
   uint32_t kinds[4];  // kind sids (NONE: "*")
   uint32_t pats[5];   // name, names[2], namespaces[2]: PAT_MASK | glob-mask index + 1, or the exact sid
   uint32_t pad;
@@ -170,18 +177,235 @@ KYV_HD bool cb_tail(const View& v, const Filter& f, const ResView& rv, const Lab
   return !(uic && (f.flags & FF_USERINFO));
 }
 
+// Lane tail facts (round 5). The tail of a filter (annotations, selector, namespace selector: condition_block after its
+// kinds / name / namespace checks) was evaluated per (rule, resource) from the resource's label and annotation maps,
+// each test a chain of dependent loads (label row -> its string's glob-mask word); C4 (10,440 rules) spent ~3,000 SIMD
+// cycles per (wave, rule) there. The slice's tail filters are reduced on the host to a few ruleset-wide facts -- label
+// values of the most used selector keys (slots), namespace-label values of the namespace-selector keys, the outcome
+// of each distinct wildcard selector requirement (ReplaceInSelector, pkg/utils/wildcards/wildcards.go:13-50) and of
+// each distinct annotation pair -- which every lane computes once from its resource (tail_facts); a covered filter
+// (MRecFilter.pad = 1 + its TailProg) then tests registers. Filters with anything else keep cb_tail.
+constexpr uint32_t TF_SLOTS = 8, TF_NSSLOTS = 4, TF_WILD = 16, TF_ANN = 32, TF_GV = 16;
+struct TailCfg {  // per slice (scalar loads)
+  uint32_t nslot, nnsslot, nwild, nann;
+  uint32_t slot[TF_SLOTS];      // label keys read by exact-key requirements
+  uint32_t nsslot[TF_NSSLOTS];  // namespace-label keys of the namespace selectors
+  uint32_t wkey[TF_WILD], wval[TF_WILD], wrkey[TF_WILD], wrval[TF_WILD];  // wildcard requirements (SelReq RQ_WILD)
+  uint32_t akey[TF_ANN], aval[TF_ANN];  // annotation (key glob, value glob) pairs
+  uint32_t ngv;
+  uint32_t gvmode[TF_GV], gvg[TF_GV], gvv[TF_GV];  // group / version refinements of record kinds (KindDesc)
+  // how each atom's key / value pattern is tested against a string (glob_sid, kyv_eval.h): TC_EXACT | sid compare
+  // (a pattern without '*' / '?'), TC_MASK | glob-mask bit (< 32: one mask word), else the pattern sid for glob_sid
+  uint32_t wkc[TF_WILD], wvc[TF_WILD], akc[TF_ANN], avc[TF_ANN];
+  uint32_t onemask;  // the batch keeps one glob-mask word per string: TC_MASK codes are valid
+};
+enum TailCode : uint32_t { TC_EXACT = 0x40000000u, TC_MASK = 0x80000000u };
+// a covered tail filter, flattened so one group of scalar loads fetches it: the annotation atoms that must all match
+// and the selector / namespace-selector requirements with their slot or atom and literal values
+constexpr uint32_t TP_REQ = 4, TP_VALS = 4;
+struct SelProg {
+  uint32_t n;                       // requirements; NONE: statically invalid selector (error)
+  uint32_t req[TP_REQ];             // op | slot or atom << 8 | nvals << 16
+  uint32_t vals[TP_REQ][TP_VALS];   // exact requirements' values
+};
+struct TailProg {                   // 48 words
+  uint32_t ann;
+  SelProg sel, nssel;
+  uint32_t pad[5];
+};
+static_assert(sizeof(TailProg) == 192, "tail program size");
+struct TailTab {
+  const TailCfg* cfg;
+  const TailProg* prog;
+};
+// the facts of one resource (or of the empty OldResource: no labels, no annotations, the lane's namespace labels)
+struct LaneTail {
+  uint32_t sv[TF_SLOTS];    // label value of slot key (NONE: absent)
+  uint32_t nv[TF_NSSLOTS];  // namespace-label value of namespace slot key
+  uint32_t wno, werr, wnd;  // wildcard requirement a: bit a = selector result 0 / error / nondeterministic
+  uint32_t ann;             // annotation atom a: bit a = some annotation matches both globs
+  uint32_t gv;              // kind refinement a: bit a = the resource's group / version satisfy it (kinds_match)
+};
+template <int N>
+KYV_HD __attribute__((always_inline)) uint32_t pick(const uint32_t (&a)[N], uint32_t i) {  // a[i], i uniform, no scratch
+  uint32_t x = NONE;
+#pragma unroll
+  for (int j = 0; j < N; j++) x = i == (uint32_t)j ? a[j] : x;
+  return x;
+}
+KYV_HD uint32_t tf_ld(const uint32_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return sld32(p);
+#else
+  return *p;
+#endif
+}
+// glob_sid(pattern, s) through an atom's test code, the string's glob-mask word `m` loaded once by the caller
+KYV_HD __attribute__((always_inline)) bool tc_test(const View& v, uint32_t code, uint32_t pat, uint32_t s, uint32_t m) {
+  if (code & TC_MASK) return (m >> (code & 31u)) & 1u;
+  if (code & TC_EXACT) return s == pat;
+  return glob_sid(v, pat, s);
+}
+KYV_HD __attribute__((always_inline)) uint32_t mask0(const View& v, uint32_t s) {
+  return v.str_gmask ? v.str_gmask[(size_t)s * v.gmask_words] : 0u;
+}
+// the facts of labels `ls`, annotations `as`, namespace labels `nsl` (CheckSelector's requirement loop per wildcard
+// requirement, as check_selector in kyv_eval.h). Each label / annotation string's mask word is loaded once and every
+// atom tested against it (round 5: an atom loop calling glob_sid reloaded it per atom -- a dependent global load per
+// (atom, annotation) pair)
+KYV_HD void tail_facts(const View& v, const TailCfg* c, const LabelSet& ls, const LabelSet& as, const LabelSet& nsl,
+                       const ResHeader* h, LaneTail& t) {
+  const uint32_t nslot = tf_ld(&c->nslot), nns = tf_ld(&c->nnsslot), nw = tf_ld(&c->nwild), na = tf_ld(&c->nann);
+  const bool one = tf_ld(&c->onemask) != 0 && v.str_gmask && v.gmask_words == 1;
+  const uint32_t nl = ls_count(ls);
+#pragma unroll
+  for (uint32_t s = 0; s < TF_SLOTS; s++) t.sv[s] = NONE;
+#pragma unroll
+  for (uint32_t s = 0; s < TF_NSSLOTS; s++) t.nv[s] = NONE;
+  // wildcard requirements over the labels: per atom the hit count and whether hits are valid label pairs
+  uint32_t hit1 = 0, hit2 = 0, valid = 0, invalid = 0;  // bit a: >= 1 hit, >= 2 hits, a valid hit, an invalid hit
+  for (uint32_t i = 0; i < nl; i++) {
+    const uint32_t k = ls_key(ls, i), val = ls_val(ls, i);
+#pragma unroll
+    for (uint32_t q = 0; q < TF_SLOTS; q++)
+      if (q < nslot && t.sv[q] == NONE && k == tf_ld(&c->slot[q])) t.sv[q] = val;  // ls_find: the first such label
+    if (!nw) continue;
+    const uint32_t km = one ? mask0(v, k) : 0u, vm = one ? mask0(v, val) : 0u;
+    const bool ok = (v.str_flags[k] & SF_LKEY) && (v.str_flags[val] & SF_LVAL);
+    for (uint32_t a = 0; a < nw; a++) {
+      const uint32_t kc = one ? tf_ld(&c->wkc[a]) : 0u, vc = one ? tf_ld(&c->wvc[a]) : 0u;
+      if (tc_test(v, kc, tf_ld(&c->wkey[a]), k, km) && tc_test(v, vc, tf_ld(&c->wval[a]), val, vm)) {
+        const uint32_t bit = 1u << a;
+        hit2 |= hit1 & bit;
+        hit1 |= bit;
+        if (ok) valid |= bit; else invalid |= bit;
+      }
+    }
+  }
+  const uint32_t nn = ls_count(nsl);
+  for (uint32_t i = 0; i < nn && nns; i++) {
+    const uint32_t k = ls_key(nsl, i);
+#pragma unroll
+    for (uint32_t q = 0; q < TF_NSSLOTS; q++)
+      if (q < nns && t.nv[q] == NONE && k == tf_ld(&c->nsslot[q])) t.nv[q] = ls_val(nsl, i);
+  }
+  t.wno = t.werr = 0;
+  t.wnd = hit2 & valid & invalid;
+  for (uint32_t a = 0; a < nw; a++) {
+    const uint32_t bit = 1u << a;
+    if (!(hit1 & bit)) {
+      const uint32_t rk = tf_ld(&c->wrkey[a]), rv = tf_ld(&c->wrval[a]);
+      if (rk == NONE) t.werr |= bit;
+      else {
+        const uint32_t i = ls_find(ls, rk);
+        if (!(i != NONE && ls_val(ls, i) == rv)) t.wno |= bit;
+      }
+    } else if ((invalid & bit) && !(valid & bit)) {
+      t.werr |= bit;
+    }
+  }
+  // kinds_match's group / version refinement of kind entry a (kyv_eval.h), for this resource
+  t.gv = 0;
+  const uint32_t ngv = tf_ld(&c->ngv);
+  for (uint32_t a = 0; a < ngv; a++) {
+    const uint32_t mode = tf_ld(&c->gvmode[a]), kg = tf_ld(&c->gvg[a]), kv = tf_ld(&c->gvv[a]);
+    const uint32_t g = h ? h->group : SID_EMPTY, ver = h ? h->version : SID_EMPTY, gvs = h ? h->gv : SID_EMPTY;
+    bool r;
+    if (mode == 1) r = kg == g && kv == ver;
+    else if (mode == 2) {
+      const uint32_t ln = v.str_len[kg], sn = v.str_len[gvs];
+      r = sn >= ln && bytes_eq(sbytes(v, gvs), sbytes(v, kg), ln);
+    } else r = false;
+    if (r) t.gv |= 1u << a;
+  }
+  t.ann = 0;
+  const uint32_t nan = ls_count(as);
+  for (uint32_t i = 0; i < nan && na; i++) {
+    const uint32_t k = ls_key(as, i), val = ls_val(as, i);
+    const uint32_t km = one ? mask0(v, k) : 0u, vm = one ? mask0(v, val) : 0u;
+    for (uint32_t a = 0; a < na; a++) {
+      const uint32_t kc = one ? tf_ld(&c->akc[a]) : 0u, vc = one ? tf_ld(&c->avc[a]) : 0u;
+      if (tc_test(v, kc, tf_ld(&c->akey[a]), k, km) && tc_test(v, vc, tf_ld(&c->aval[a]), val, vm)) t.ann |= 1u << a;
+    }
+  }
+}
+
+// check_selector (kyv_eval.h) from the facts over a selector program: *r_out 1 match, 0 no, -1 error (per lane) and
+// *nd as check_selector raises it: requirements after an erroring wildcard requirement are not evaluated; branch-free
+// per lane, the program's fields uniform
+KYV_HD __attribute__((always_inline)) void sel_prog(const SelProg& sp, const LaneTail& t, bool ns, int* r_out, bool* nd) {
+  if (sp.n == NONE) { *r_out = -1; return; }
+  bool err = false, no = false, n = false;
+#pragma unroll
+  for (uint32_t q = 0; q < TP_REQ; q++) {
+    if (q >= sp.n) continue;
+    const uint32_t op = sp.req[q] & 0xFFu, m = (sp.req[q] >> 8) & 0xFFu, nv = sp.req[q] >> 16;
+    if (op == RQ_WILD) {
+      n = n | (!err & (((t.wnd >> m) & 1u) != 0));
+      no = no | (((t.wno >> m) & 1u) != 0);
+      err = err | (((t.werr >> m) & 1u) != 0);
+      continue;
+    }
+    const uint32_t val = ns ? pick(t.nv, m) : pick(t.sv, m);
+    const bool has = val != NONE;
+    bool inset = false;
+#pragma unroll
+    for (uint32_t k = 0; k < TP_VALS; k++)
+      if (k < nv) inset = inset | (sp.vals[q][k] == val);
+    inset = inset & has;
+    const bool ok = (op == RQ_EQ || op == RQ_IN) ? inset : op == RQ_NOTIN ? (!has | !inset) : op == RQ_EXISTS ? has : !has;
+    no = no | !ok;
+  }
+  *nd = *nd | n;
+  *r_out = err ? -1 : no ? 0 : 1;
+}
+KYV_HD __attribute__((always_inline)) SelProg ld_selprog(const SelProg* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return sld(p);
+#else
+  return *p;
+#endif
+}
+// cb_tail (above) of a covered filter (program pi), from the lane's facts; *fnd: the nondeterminism cb_tail would raise
+KYV_HD __attribute__((always_inline)) bool tail_prog(const TailTab& tt, uint32_t pi, uint32_t b, const LaneTail& t,
+                                                     uint32_t fl, bool uic, bool* fnd) {
+  const TailProg* tp = tt.prog + pi;
+  const uint32_t ann = tf_ld(&tp->ann);
+  const bool annok = (t.ann & ann) == ann;
+  bool sok = true, n1 = false;
+  if (b & FF_HAS_SEL) {
+    int r;
+    sel_prog(ld_selprog(&tp->sel), t, false, &r, &n1);
+    sok = r == 1;
+  }
+  bool nsok = true, n2 = false, nscond = false;
+  if (b & FF_HAS_NSSEL) {
+    nscond = !(fl & MF_ISNS) & (!(fl & MF_KIND_EMPTY) | ((b & FF_KINDS_STAR) != 0));
+    int r;
+    sel_prog(ld_selprog(&tp->nssel), t, true, &r, &n2);
+    nsok = !nscond | (r == 1);
+  }
+  *fnd = annok & (n1 | (sok & nscond & n2));
+  return annok & sok & nsok & !(uic && (b & FF_USERINFO));
+}
+
 // condition_block (kyv_eval.h) of a record filter: kinds, name, names and namespaces from the record and the lane's
-// facts (a kind with a group / version that equals the resource's: kinds_match decides), then the tail
-KYV_HD bool cb_rec(const View& v, const MRecFilter& F, const MFacts& mf, const ResView& rv, const LabelSet& labels,
-                   const LabelSet& nsl, bool uic, bool* nd) {
+// facts (a kind with a group / version that equals the resource's: kinds_match decides), then the tail. Loops over the
+// record's fixed-size arrays are unrolled with static indices: the record stays in scalar registers (a dynamic index
+// would copy it to per-lane scratch)
+KYV_HD __attribute__((always_inline)) bool cb_rec(const View& v, const MRecFilter& F, const MFacts& mf, const ResView& rv, const LabelSet& labels,
+                   const LabelSet& nsl, bool uic, bool* nd, const TailTab& tt, const LaneTail& lt) {
   const uint32_t b = F.bits;
   const uint32_t nk = (b >> 16) & 7u;
   if (nk) {
     bool ok = false, gv = false;
-    for (uint32_t i = 0; i < nk && !ok; i++) {
-      const uint32_t kd = F.kinds[i];
-      if (kd == NONE) ok = true;
-      else if (kd == mf.gk) { ok = true; gv = (b >> (24 + i)) & 1u; }
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+      if (i < nk && !ok) {
+        const uint32_t kd = (F.kinds[i] != NONE && (b & MRF_KPACK)) ? F.kinds[i] & 0xFFFFFFu : F.kinds[i];
+        if (kd == NONE) ok = true;
+        else if (kd == mf.gk) { ok = true; gv = (b >> (24 + i)) & 1u; }
+      }
     }
     if (gv) ok = kinds_match(v, v.filters[F.idx], rv.h);
     if (!ok) return false;
@@ -191,68 +415,173 @@ KYV_HD bool cb_rec(const View& v, const MRecFilter& F, const MFacts& mf, const R
   if (nn && !(pat_name(mf, F.pats[1]) || (nn > 1 && pat_name(mf, F.pats[2])))) return false;
   const uint32_t ns = (b >> 22) & 3u;
   if (ns && !(pat_ns(mf, F.pats[3]) || (ns > 1 && pat_ns(mf, F.pats[4])))) return false;
-  if ((b >> 28) & 1u) return cb_tail(v, v.filters[F.idx], rv, labels, nsl, uic, nd, mf.fl);
+  if ((b >> 28) & 1u) {
+    if (F.pad) {
+      bool fnd;
+      const bool c = tail_prog(tt, F.pad - 1, b, lt, mf.fl, uic, &fnd);
+      *nd = *nd | fnd;
+      return c;
+    }
+    return cb_tail(v, v.filters[F.idx], rv, labels, nsl, uic, nd, mf.fl);
+  }
   return !(uic && (b & FF_USERINFO));
 }
 
-// match_rule (kyv_eval.h) over a record
-KYV_HD bool match_rule_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& labels,
-                           const LabelSet& nsl, bool* nd) {
-  const uint32_t mm = (R.bits >> 8) & 0xFFu, em = (R.bits >> 16) & 0xFFu, nmf = (R.bits >> 24) & 0xFu, nef = R.bits >> 28;
-  bool failed = false;
-  if (mm == MM_ANY) {
-    bool one = false;
-    for (uint32_t i = 0; i < nmf && !one; i++)
-      if (!(R.f[i].bits & FF_ZERO_RD) && cb_rec(v, R.f[i], mf, rv, labels, nsl, false, nd)) one = true;
-    if (!one) failed = true;
-  } else if (mm == MM_ALL || mm == MM_PLAIN) {
-    for (uint32_t i = 0; i < nmf && !failed; i++)
-      if ((R.f[i].bits & FF_ZERO_RD) || !cb_rec(v, R.f[i], mf, rv, labels, nsl, false, nd)) failed = true;
-  } else {
-    failed = true;
-  }
-  if (failed) return false;
-  if (em == MM_ANY || em == MM_PLAIN) {
-    for (uint32_t i = 0; i < nef; i++) {
-      const MRecFilter& F = R.f[nmf + i];
-      if ((F.bits & FF_ZERO_RD) && !(F.bits & FF_USERINFO)) continue;
-      if (cb_rec(v, F, mf, rv, labels, nsl, true, nd)) return false;
+// The record's header words (k, bits, kind, flags) and its filter slots are read with scalar loads from the record
+// array (wave-uniform addresses) where they are needed: a local copy of the whole record indexed by the slot number
+// would live in per-lane scratch memory
+struct MRecHead { uint32_t k, bits, kind, flags; };
+
+// match_rule (kyv_eval.h) over a record: slot j of the record's filters is match filter j (j < nmf) or exclude filter
+// j - nmf, visited in order with match_rule's short-circuits (a filter is not evaluated once the block's outcome is
+// known, so its nondeterminism flag is not raised either): ANY stops at the first matching filter, ALL / plain at the
+// first failing one (a filter without resource description fails it); a failed match block ends the rule before its
+// exclude block; exclude ANY / plain excludes on the first excluding filter, exclude ALL only when every filter excludes
+KYV_HD __attribute__((always_inline)) bool match_rule_rec(const View& v, const MRec* Rp, uint32_t bits, const MFacts& mf,
+                                                          const ResView& rv, const LabelSet& labels, const LabelSet& nsl,
+                                                          bool* nd, const TailTab& tt, const LaneTail& lt) {
+  const uint32_t mm = (bits >> 8) & 0xFFu, em = (bits >> 16) & 0xFFu, nmf = (bits >> 24) & 0xFu, nef = bits >> 28;
+  const bool any = mm == MM_ANY, all = mm == MM_ALL || mm == MM_PLAIN;
+  if (!any && !all) return false;
+  const bool eany = em == MM_ANY || em == MM_PLAIN, eall = em == MM_ALL;
+  bool one = false, failed = false, excluded = false, byAll = true;
+  const uint32_t n = nmf + nef;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n; j++) {
+    const bool ism = j < nmf;
+    if (ism) {
+      if (any ? one : failed) continue;
+    } else {
+      if (any ? !one : failed) break;  // the match block failed: the exclude block is not evaluated
+      if (eany ? excluded : (!eall || !byAll)) break;
     }
-  } else if (em == MM_ALL) {
-    bool byAll = true;
-    for (uint32_t i = 0; i < nef && byAll; i++) {
-      const MRecFilter& F = R.f[nmf + i];
-      const bool excl = !((F.bits & FF_ZERO_RD) && !(F.bits & FF_USERINFO)) && cb_rec(v, F, mf, rv, labels, nsl, true, nd);
-      if (!excl) byAll = false;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const MRecFilter F = sld(&Rp->f[j]);
+#else
+    const MRecFilter F = Rp->f[j];
+#endif
+    const bool skip = ism ? (F.bits & FF_ZERO_RD) != 0 : ((F.bits & FF_ZERO_RD) && !(F.bits & FF_USERINFO));
+    const bool c = !skip && cb_rec(v, F, mf, rv, labels, nsl, !ism, nd, tt, lt);
+    if (ism) {
+      if (any) { if (c) one = true; }
+      else if (!c) failed = true;
+    } else if (eany) {
+      if (c) excluded = true;
+    } else if (!c) {
+      byAll = false;
     }
-    if (byAll && nef > 0) return false;
   }
+  if (any ? !one : failed) return false;
+  if (eany && excluded) return false;
+  if (eall && byAll && nef > 0) return false;
   return true;
 }
 
 // pair_match (kyv_pss.h) of a record rule (compiled match block, no exceptions); a rule whose match may accept the
 // empty OldResource (MR_EMPTY, validation.go:606) retries against it: the facts of the empty resource (mf0: kind,
 // name and namespace "", no labels, no annotations)
-KYV_HD bool pair_match_rec(const View& v, const MRec& R, const MFacts& mf, const ResView& rv, const LabelSet& labels,
-                           const LabelSet& nsl, const MFacts& mf0, uint8_t* st) {
+KYV_HD __attribute__((always_inline)) bool pair_match_rec(const View& v, const MRec* Rp, const MRecHead& H, const MFacts& mf,
+                                                          const ResView& rv, const LabelSet& labels, const LabelSet& nsl,
+                                                          const MFacts& mf0, uint8_t* st, const TailTab& tt,
+                                                          const LaneTail& lt, const LaneTail& lt0) {
   bool nd = false;
-  if (!(R.flags & RD_GATE_EXACT)) {
+  if (!(H.flags & RD_GATE_EXACT)) {
     KYV_ACCT_ADD(0, 16);  // header words the match program compares (model, as pair_match)
-    bool m = match_rule_rec(v, R, mf, rv, labels, nsl, &nd);
-    if (!m && (R.bits & MR_EMPTY))
-      m = match_rule_rec(v, R, mf0, ResView{rv.R, nullptr}, LabelSet{NodeTab{nullptr}, 0, nullptr, 0}, nsl, &nd);
+    bool m = match_rule_rec(v, Rp, H.bits, mf, rv, labels, nsl, &nd, tt, lt);
+    if (!m && (H.bits & MR_EMPTY))
+      m = match_rule_rec(v, Rp, H.bits, mf0, ResView{rv.R, nullptr}, LabelSet{NodeTab{nullptr}, 0, nullptr, 0}, nsl, &nd,
+                         tt, lt0);
     if (!m) { *st = ST_NONE; return false; }
   }
   if (nd) { *st = ST_ND; return false; }
-  if (R.kind == RK_FALLBACK) { *st = ST_FALLBACK; return false; }
+  if ((H.kind & 0xFFu) == RK_FALLBACK) { *st = ST_FALLBACK; return false; }
   return true;
+}
+
+// ---- branch-free record evaluation (round 5). The general path above decides a filter with a divergent branch per
+// test (exec-mask juggling dominated the C4 match kernel: ~650 instructions per (wave, rule), 40 % of them exec-mask
+// and spill moves). For MR_FASTEVAL records every per-lane condition is a boolean combined with & / |; branches remain
+// only on the record's uniform fields. The short-circuits of match_rule / condition_block / check_selector are kept as
+// masks: a filter's or requirement's nondeterminism flag counts only on lanes where the reference would have evaluated
+// it.
+// condition_block of a record filter (uic: an exclude filter), branch-free per lane; *fnd: its nondeterminism
+KYV_HD __attribute__((always_inline)) bool filt_fast(const MRecFilter& F, const MFacts& mf, const TailTab& tt,
+                                                     const LaneTail& t, bool uic, bool* fnd) {
+  const uint32_t b = F.bits, nk = (b >> 16) & 7u;
+  bool kok = nk == 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++)
+    if (i < nk) {
+      const uint32_t kd = F.kinds[i];
+      if (kd == NONE) kok = true;
+      else if (!(b & MRF_KPACK)) kok = kok | (kd == mf.gk);  // (MR_FASTEVAL: no group / version kinds then)
+      else if (!((b >> (24 + i)) & 1u)) kok = kok | ((kd & 0xFFFFFFu) == mf.gk);
+      else kok = kok | (((kd & 0xFFFFFFu) == mf.gk) & (((t.gv >> ((kd >> 24) - 1)) & 1u) != 0));  // sid | (atom + 1) << 24
+    }
+  bool nok = true;
+  if ((b >> 21) & 1u) nok = pat_name(mf, F.pats[0]);
+  const uint32_t nn = (b >> 19) & 3u;
+  if (nn) nok = nok & (pat_name(mf, F.pats[1]) | (nn > 1 && pat_name(mf, F.pats[2])));
+  bool sok = true;
+  const uint32_t ns = (b >> 22) & 3u;
+  if (ns) sok = pat_ns(mf, F.pats[3]) | (ns > 1 && pat_ns(mf, F.pats[4]));
+  const bool head = kok & nok & sok;
+  *fnd = false;
+  if (!((b >> 28) & 1u)) return head & !(uic && (b & FF_USERINFO));
+  bool tnd;
+  const bool c = tail_prog(tt, F.pad - 1, b, t, mf.fl, uic, &tnd);
+  *fnd = head & tnd;
+  return head & c;
+}
+// match_rule over an MR_FASTEVAL record (filter slots F[0..2]), branch-free per lane
+KYV_HD __attribute__((always_inline)) bool match_fast(const View& v, uint32_t bits, const MRecFilter* F, const MFacts& mf,
+                                                      const TailTab& tt, const LaneTail& t, bool* nd) {
+  const uint32_t mm = (bits >> 8) & 0xFFu, em = (bits >> 16) & 0xFFu, nmf = (bits >> 24) & 0xFu, nef = bits >> 28;
+  const bool any = mm == MM_ANY, all = mm == MM_ALL || mm == MM_PLAIN;
+  if (!any && !all) return false;
+  bool one = false, failed = false, n = false;
+#pragma unroll
+  for (uint32_t j = 0; j < MREC_F; j++) {
+    if (j < nmf) {
+      const bool zero = (F[j].bits & FF_ZERO_RD) != 0;
+      const bool ev = any ? !one : !failed;  // the reference reaches this filter
+      bool c = false;
+      if (!zero) {
+        bool fnd;
+        c = filt_fast(F[j], mf, tt, t, false, &fnd);
+        n = n | (ev & fnd);
+      }
+      if (any) one = one | (ev & c);
+      else failed = failed | (ev & (zero | !c));
+    }
+  }
+  const bool matched = any ? one : !failed;
+  const bool eany = em == MM_ANY || em == MM_PLAIN, eall = em == MM_ALL;
+  bool excluded = false, byAll = true;
+#pragma unroll
+  for (uint32_t j = 0; j < MREC_F; j++) {
+    if (j >= nmf && j < nmf + nef && (eany || eall)) {
+      const bool skip = (F[j].bits & FF_ZERO_RD) && !(F[j].bits & FF_USERINFO);
+      const bool ev = matched & (eany ? !excluded : byAll);
+      bool c = false;
+      if (!skip) {
+        bool fnd;
+        c = filt_fast(F[j], mf, tt, t, true, &fnd);
+        n = n | (ev & fnd);
+      }
+      if (eany) excluded = excluded | (ev & c);
+      else byAll = byAll & !(ev & !c);
+    }
+  }
+  *nd = *nd | n;
+  return matched & !(eany & excluded) & !(eall & byAll & (nef > 0));
 }
 
 // Pattern / anyPattern rules without preconditions (and compile-time fallback rules): the match phase is only
 // pair_match (kind gate, match / exclude program, PolicyException candidates) and the work-list append, so these
 // kernels carry none of the dispatch code (conditions, PodSecurity calls) whose register need made the rule loop
 // of match_kernel spill every iteration (C4: 10,440 rules per wave, 252 GB of scratch writes per evaluation).
-// match_walk_kernel takes the rules as staged match records (above), MREC_CHUNK at a time through LDS;
+// match_rec_kernel takes the rules as staged match records (above) through a kind index;
 // match_walk_generic_kernel the rules whose match block does not fit a record (pair_match; one kernel for both needs
 // both match programs' registers: 111 VGPRs, 4 waves/SIMD).
 // kWpe: occupancy target (KYV_MATCHW_WPE = 4 / 6 / 8 at run time; 4 by default)
@@ -277,58 +606,167 @@ KYV_HD void match_walk_append(const View& v, DevOut& o, WorkLists& wl, uint32_t 
   if (gated && !walk && st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
 }
 
-// kMW: glob-mask words held per string (1 when the ruleset has at most 32 mask bits, else 4)
+// Shape rules (jit.cpp, round 5): pattern rules whose compiled pattern is one of the ruleset's deduplicated shapes
+// (structurally identical patterns: same keys, handlers, leaves, path templates and columns; C4's 10,440 rules use 15)
+// get their walk verdict from the shape tables (ShapeTab, kyv_wave.h), computed once per (shape, resource) by
+// kyv_jit_shapes: a matched pair's verdict byte is its shape's, and a FAIL pair's staged failing-path record is its
+// shape's record (the record carries no rule: StageRec). The pair is decided here; no work-list item, no walk.
+constexpr uint32_t SHAPE_REGS = 16;  // shape verdicts a lane keeps in registers (4 words of bytes)
+KYV_HD void mrec_shape_out(const View& v, DevOut& o, const ShapeTab& sh, uint32_t s, bool wide, uint32_t k, uint32_t r,
+                           bool gated, bool m, uint8_t st, uint32_t hflags, uint32_t w, const uint32_t (&sv)[4]) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  bool rec = false;
+  if (m) {
+    if (hflags & RF_MAGIC) {
+      st = ST_FALLBACK;  // pattern pairs on such resources go to the CPU engine (as match_walk_append)
+    } else {
+      st = s < SHAPE_REGS ? (uint8_t)(pick(sv, s >> 2) >> (8 * (s & 3))) : sh.st[(size_t)s * v.nres + r];
+      rec = (st & 7u) == ST_FAIL;
+      KYV_ACCT_ADD(0, 1 + (rec ? sizeof(FailRec) : 0));  // the shape's verdict (and record) for this resource
+    }
+  }
+  const unsigned long long rm = __ballot(rec);
+  if (rm) {
+    FailRec* chunk = o.stage + o.rbase[k - o.rule_lo] + (size_t)w * WAVE;  // chunk (k, w): one alternative
+    if (rec) {
+      const uint32_t at = (uint32_t)__popcll(rm & ((1ull << lane) - 1));
+      FailRec f = sh.rec[(size_t)s * v.nres + r];
+      if (wide) {  // a rule with metadata-expansion sites: whole records (resolved keys), as the walk stages them
+        f.rule = k;
+        chunk[at] = f;
+        KYV_ACCT_ADD(2, sizeof(FailRec));
+      } else {
+        StageRec x;
+        x.tmpl = f.tmpl;
+        x.lane_alt = lane | ((uint32_t)f.alt << 8);
+        for (int i = 0; i < MAX_IDX; i++) x.idx[i] = f.idx[i];
+        reinterpret_cast<StageRec*>(chunk)[at] = x;
+        KYV_ACCT_ADD(2, sizeof(StageRec));
+      }
+    }
+    if (lane == 0) { o.rcnt[(size_t)(k - o.rule_lo) * sh.nwaves + w] = (uint16_t)__popcll(rm); KYV_ACCT_ADD(1, 2); }
+  }
+  if (gated && st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
+}
+
+// Kind index of a slice's match records (round 5): records recs[off[c], off[c + 1]) are (copies of) those whose rule's
+// kind gate admits kind class c (policycache's kind -> policies index, pkg/policycache/store.go:96-170, at compile time)
+struct MRecIndex {
+  const uint32_t* off;  // [nclass + 1]
+  const MRec* recs;     // the records of class c at [off[c], off[c + 1])
+};
+
+// A resource's match facts (round 5): what the record path compares (MFacts) and its lane tail facts, computed once
+// per evaluation by facts_kernel (the tail configuration is ruleset-wide) and read by every slice's match_rec_kernel
+struct ResFacts {
+  MFacts mf;
+  LaneTail lt;
+  uint32_t hflags, hroot, pad;
+};
+static_assert(sizeof(ResFacts) == 128, "resource facts size");
+
+// the lane's record-path facts (kind, name, namespace, their glob-mask words)
+template <int kMW>
+KYV_HD __attribute__((always_inline)) MFacts res_mfacts(const View& v, const ResHeader& h) {
+  MFacts mf{};
+  const uint32_t name = h.name, kind = h.kind;
+  mf.gk = h.gvk_kind;
+  mf.rname = name == SID_EMPTY ? h.gen_name : name;
+  const bool isNs = v.str_len[kind] == 9 && bytes_eq(sbytes(v, kind), (const uint8_t*)"Namespace", 9);
+  mf.rns = isNs ? name : h.ns;
+  mf.fl = (isNs ? MF_ISNS : 0u) | (kind == SID_EMPTY ? MF_KIND_EMPTY : 0u);
+  if (v.str_gmask) {  // (records with a glob-mask pattern are only built when the batch has masks)
+    const uint32_t gw = v.gmask_words;
+    const uint32_t* a = v.str_gmask + (size_t)mf.rname * gw;
+    const uint32_t* b = v.str_gmask + (size_t)mf.rns * gw;
+    mf.n0 = a[0]; mf.s0 = b[0];
+    if (kMW > 1) {
+      if (gw > 1) { mf.n1 = a[1]; mf.s1 = b[1]; }
+      if (gw > 2) { mf.n2 = a[2]; mf.s2 = b[2]; }
+      if (gw > 3) { mf.n3 = a[3]; mf.s3 = b[3]; }
+    }
+  }
+  return mf;
+}
+KYV_HD LabelSet res_nsl(const View& v, const ResHeader& h) {
+  LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
+  if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
+  return nsl;
+}
+template <int kMW>
+__global__ void __launch_bounds__(256) facts_kernel(const View* __restrict__ vp, const TailCfg* __restrict__ cfg,
+                                                    ResFacts* __restrict__ out) {
+  const View& v = *vp;
+  const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+  if (r >= v.nres) return;
+  const ResHeader& h = v.hdr[r];
+  KYV_ACCT_ADD(0, 48);  // header fields, label / annotation / namespace-label rows (model)
+  ResFacts f;
+  f.mf = res_mfacts<kMW>(v, h);
+  const NodeTab R{v.nodes + h.root};
+  tail_facts(v, cfg, LabelSet{R, h.labels, nullptr, 0}, LabelSet{R, h.ann, nullptr, 0}, res_nsl(v, h), &h, f.lt);
+  f.hflags = h.flags;
+  f.hroot = h.root;
+  f.pad = 0;
+  out[r] = f;
+  KYV_ACCT_ADD(1, sizeof(ResFacts));
+}
+
+// Pattern / anyPattern rules without preconditions whose match block fits a staged record (MRec). One lane per
+// resource, one wave per workgroup; the lane holds its resource's facts (kind, name, namespace and their glob-mask
+// words) in registers and its labels in LDS. The rule loop is kind-indexed: a wave whose resources share one kind class
+// (kind-major batches: all but the waves at class boundaries) walks only the records of that class (C4: ~40 % of the
+// rules for a Pod wave); a mixed wave walks every record with a per-lane kind-gate test. Records come through scalar
+// loads (wave-uniform addresses: the scalar cache and L2 serve every wave of the class from one copy), so a rule's
+// kinds / name / namespace checks are register compares and its selector / annotation tail a scan of LDS. Matched pairs
+// of shape rules are decided here from the shape tables (mrec_shape_out), the rest go to the walk's work lists.
+// kWpe: occupancy target (KYV_MATCHW_WPE); kMW: glob-mask words held per string (1 when the ruleset has <= 32 bits)
 template <int kWpe, int kMW>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
-match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRec* __restrict__ recs, uint32_t nm) {
-  __shared__ MRec s_rec[MREC_CHUNK];
+match_rec_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRec* __restrict__ recs, uint32_t nm,
+                 MRecIndex ix, ShapeTab sh, TailTab tt, const ResFacts* __restrict__ facts) {
   // the lane's labels (key, value sid pairs; stride 2 * MREC_LABELS + 1 words: no bank conflicts), when it has at most
   // MREC_LABELS of them
   __shared__ uint32_t s_lab[BLOCK * (2 * MREC_LABELS + 1)];
   const View& v = *vp;
   const uint32_t lane = threadIdx.x;
-  const uint32_t r = blockIdx.x * BLOCK + lane;
+  const uint32_t w = blockIdx.x;
+  const uint32_t r = w * BLOCK + lane;
   const bool active = r < v.nres;
-  const uint32_t* gate = active ? v.gate + (size_t)v.hdr[r].kclass * v.gate_words : nullptr;
-  const uint32_t hflags = active ? v.hdr[r].flags : 0u;
-  const uint32_t hroot = active ? v.hdr[r].root : 0u;
-  if (active) KYV_ACCT_ADD(0, 12);  // header: kind class, flags, root
-  MFacts mf{};
-  LabelSet nsl{NodeTab{nullptr}, 0, nullptr, 0};
   const ResHeader* hp = active ? &v.hdr[r] : nullptr;
-  if (active) {
-    const ResHeader& h = *hp;
-    const uint32_t name = h.name, kind = h.kind;
-    mf.gk = h.gvk_kind;
-    mf.rname = name == SID_EMPTY ? h.gen_name : name;
-    const bool isNs = v.str_len[kind] == 9 && bytes_eq(sbytes(v, kind), (const uint8_t*)"Namespace", 9);
-    mf.rns = isNs ? name : h.ns;
-    mf.fl = (isNs ? MF_ISNS : 0u) | (kind == SID_EMPTY ? MF_KIND_EMPTY : 0u);
-    if (v.str_gmask) {  // (records with a glob-mask pattern are only built when the batch has masks)
-      const uint32_t w = v.gmask_words;
-      const uint32_t* a = v.str_gmask + (size_t)mf.rname * w;
-      const uint32_t* b = v.str_gmask + (size_t)mf.rns * w;
-      mf.n0 = a[0]; mf.s0 = b[0];
-      if (kMW > 1) {
-        if (w > 1) { mf.n1 = a[1]; mf.s1 = b[1]; }
-        if (w > 2) { mf.n2 = a[2]; mf.s2 = b[2]; }
-        if (w > 3) { mf.n3 = a[3]; mf.s3 = b[3]; }
-      }
-    }
-    if (h.nsl != NONE) { nsl.kv = v.nsl_kv + 2 * v.nsl_off[h.nsl]; nsl.n = v.nsl_off[h.nsl + 1] - v.nsl_off[h.nsl]; }
+  const uint32_t cls = active ? hp->kclass : 0u;
+  const uint32_t hflags = active ? hp->flags : 0u;
+  const uint32_t hroot = active ? hp->root : 0u;
+  if (active) KYV_ACCT_ADD(0, 12);  // header: kind class, flags, root
+  const uint32_t c0 = __builtin_amdgcn_readfirstlane(cls);
+  const bool uni = __ballot(active && cls != c0) == 0;  // (lane 0 is active whenever any lane is)
+  const uint32_t* gate = active ? v.gate + (size_t)cls * v.gate_words : nullptr;
+  // the lane's facts: from the per-evaluation facts table, else computed here
+  MFacts mf{};
+  LaneTail lt{};
+  bool have = false;
+  if (facts && active) {
+    const ResFacts F = facts[r];
+    KYV_ACCT_ADD(0, sizeof(ResFacts));
+    mf = F.mf;
+    lt = F.lt;
+    have = true;
+  } else if (active) {
+    mf = res_mfacts<kMW>(v, *hp);
   }
+  const LabelSet nsl = active ? res_nsl(v, *hp) : LabelSet{NodeTab{nullptr}, 0, nullptr, 0};
   // the empty OldResource's facts (uniform): every string "", its glob-mask words those of the empty string
   MFacts mf0{};
   mf0.gk = mf0.rname = mf0.rns = SID_EMPTY;
   mf0.fl = MF_KIND_EMPTY;
   if (v.str_gmask) {
-    const uint32_t w = v.gmask_words;
-    const uint32_t* a = v.str_gmask + (size_t)SID_EMPTY * w;
+    const uint32_t gw = v.gmask_words;
+    const uint32_t* a = v.str_gmask + (size_t)SID_EMPTY * gw;
     mf0.n0 = mf0.s0 = a[0];
     if (kMW > 1) {
-      if (w > 1) mf0.n1 = mf0.s1 = a[1];
-      if (w > 2) mf0.n2 = mf0.s2 = a[2];
-      if (w > 3) mf0.n3 = mf0.s3 = a[3];
+      if (gw > 1) mf0.n1 = mf0.s1 = a[1];
+      if (gw > 2) mf0.n2 = mf0.s2 = a[2];
+      if (gw > 3) mf0.n3 = mf0.s3 = a[3];
     }
   }
   const ResView rv{NodeTab{v.nodes + hroot}, hp};
@@ -341,34 +779,54 @@ match_walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRe
       labels = LabelSet{NodeTab{nullptr}, 0, kv, nl};
     }
   }
-  for (uint32_t c0 = 0; c0 < nm; c0 += MREC_CHUNK) {
-    const uint32_t n = nm - c0 < MREC_CHUNK ? nm - c0 : MREC_CHUNK;
-    __syncthreads();  // the previous chunk's records are read
-    {
-      const uint32_t* src = (const uint32_t*)(recs + c0);
-      uint32_t* dst = (uint32_t*)s_rec;
-      for (uint32_t i = lane; i < n * (uint32_t)(sizeof(MRec) / 4); i += BLOCK) dst[i] = src[i];
+  if (!__ballot(active)) return;
+  // the lane's tail facts (unless read above), and the empty OldResource's: no labels or annotations, the lane's
+  // namespace labels
+  const LabelSet none{NodeTab{nullptr}, 0, nullptr, 0};
+  if (!have) tail_facts(v, tt.cfg, labels, LabelSet{rv.R, hp ? hp->ann : NONE, nullptr, 0}, nsl, hp, lt);
+  LaneTail lt0;
+  tail_facts(v, tt.cfg, none, none, none, nullptr, lt0);
+#pragma unroll
+  for (uint32_t q = 0; q < TF_NSSLOTS; q++) lt0.nv[q] = lt.nv[q];
+  // this resource's verdicts of the first SHAPE_REGS shapes, one byte each (loaded once, read per matched pair)
+  uint32_t sv[4] = {0, 0, 0, 0};
+  if (active)
+#pragma unroll
+    for (uint32_t q = 0; q < SHAPE_REGS; q++)
+      if (q < sh.nshapes) sv[q >> 2] |= (uint32_t)sh.st[(size_t)q * v.nres + r] << (8 * (q & 3));
+  const uint32_t i0 = uni ? sld32(ix.off + c0) : 0u, i1 = uni ? sld32(ix.off + c0 + 1) : nm;
+  const MRec* base = uni ? ix.recs : recs;
+  for (uint32_t i = i0; i < i1; i++) {
+    const MRec* Rp = base + i;
+    const MRecHead H = sld(reinterpret_cast<const MRecHead*>(Rp));
+    const uint32_t k = H.k;
+    const bool gated = active && (uni || ((gate[k >> 5] >> (k & 31)) & 1u));
+    if (!__ballot(gated)) continue;
+    uint8_t st = ST_NONE;
+    bool m;
+    if ((H.bits & MR_FASTEVAL) && (!(H.bits & MR_EMPTY) || (H.bits & MR_ECONST)) && !(H.flags & RD_GATE_EXACT)) {
+      // branch-free path: the record's filter slots with scalar loads (independent: one latency)
+      const uint32_t nf = ((H.bits >> 24) & 0xFu) + (H.bits >> 28);
+      MRecFilter F[MREC_F];
+#pragma unroll
+      for (uint32_t j = 0; j < MREC_F; j++)
+        if (j < nf) F[j] = sld(&Rp->f[j]);
+      KYV_ACCT_ADD(0, 16);  // header words the match program compares (model, as pair_match)
+      bool nd = false;
+      bool mt = match_fast(v, H.bits, F, mf, tt, lt, &nd);
+      if (H.bits & MR_EMPTY) {  // the retry against the empty OldResource: a constant of the rule
+        nd = nd | (!mt & ((H.bits & MR_END) != 0));
+        mt = mt | ((H.bits & MR_EMATCH) != 0);
+      }
+      st = !mt ? (uint8_t)ST_NONE : nd ? (uint8_t)ST_ND : (H.kind & 0xFFu) == RK_FALLBACK ? (uint8_t)ST_FALLBACK : (uint8_t)ST_NONE;
+      m = gated & mt & !nd & ((H.kind & 0xFFu) != RK_FALLBACK);
+      if (!gated) st = ST_NONE;
+    } else {
+      m = gated && pair_match_rec(v, Rp, H, mf, rv, labels, nsl, mf0, &st, tt, lt, lt0);
     }
-    __syncthreads();
-    // the chunk's kind-gate bits, loaded together (independent loads: one latency per chunk, not one per rule)
-    uint32_t gm = 0;
-    if (active) {
-#pragma unroll 8
-      for (uint32_t j = 0; j < MREC_CHUNK; j++)
-        if (j < n) {
-          const uint32_t k = s_rec[j].k;
-          gm |= ((gate[k >> 5] >> (k & 31)) & 1u) << j;
-        }
-    }
-    for (uint32_t j = 0; j < n; j++) {
-      const MRec& R = s_rec[j];
-      const uint32_t k = __builtin_amdgcn_readfirstlane(R.k);
-      const bool gated = (gm >> j) & 1u;
-      if (!__ballot(gated)) continue;
-      uint8_t st = ST_NONE;
-      const bool m = gated && pair_match_rec(v, R, mf, rv, labels, nsl, mf0, &st);
-      match_walk_append(v, o, wl, k, __builtin_amdgcn_readfirstlane(R.kind), r, gated, m, st, hflags, hroot);
-    }
+    const uint32_t shape = (H.kind >> 8) & 0x7FFFu;  // 1 + shape of a shape rule, else 0; bit 23: wide records
+    if (shape) mrec_shape_out(v, o, sh, shape - 1, (H.kind >> 23) & 1u, k, r, gated, m, st, hflags, w, sv);
+    else match_walk_append(v, o, wl, k, H.kind & 0xFFu, r, gated, m, st, hflags, hroot);
   }
 }
 

@@ -701,6 +701,23 @@ struct DevOut {
   uint32_t rule_lo, rule_hi;   // rule slice of this launch: work lists, rbase and rcnt are indexed by k - rule_lo
 };
 
+// Shape tables (round 5, jit.cpp kyv_jit_shapes): the walk verdict of each deduplicated pattern shape for every resource
+// its users' kind gates admit, and the shape's failing-path record where that verdict is FAIL; read by match_rec_kernel
+// (ShapeTab), written by the runtime-compiled kyv_jit_shapes (ShapeOut: per kind class, the shapes to compute)
+struct ShapeTab {
+  const uint8_t* st;      // [shape][res] verdict byte
+  const FailRec* rec;     // [shape][res] failing-path record (valid where the verdict is ST_FAIL; rule field unset)
+  uint32_t nwaves;        // match waves of the batch (rcnt row length)
+  uint32_t nshapes;
+};
+struct ShapeOut {
+  uint8_t* st;
+  FailRec* rec;
+  const uint32_t* gate;   // [kind class][words]: bit s = some user of shape s admits the class
+  uint32_t words;
+  uint32_t nwaves;
+};
+
 // Failing-path records of one walk chunk, packed with wave ballots into the chunk's own staging slots (no
 // atomics, no waiting); compact_kernel gathers the chunks' records afterwards.
 struct WaveSink {

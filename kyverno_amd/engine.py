@@ -141,6 +141,7 @@ class Results:
         ju = L.kyv_results_jit(h)
         self.jit = bool(ju & 1)          # runtime-compiled walk kernels ran
         self.jit_cond = bool(ju & 2)     # runtime-compiled condition kernel (deny / foreach rules) ran
+        self.jit_shapes = bool(ju & 4)   # pattern-shape tables (kyv_jit_shapes) decided matched pairs
         rc = np.zeros(len(ruleset.rules) * 8, dtype=np.int64)
         if rc.size:
             K.check(L.kyv_results_rule_counts(h, rc.ctypes.data, rc.size))

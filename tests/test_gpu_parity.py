@@ -187,6 +187,31 @@ def test_c4_rule_slices_gpu(monkeypatch):
         assert one.message(int(r), int(k)) == res.message(int(r), int(k))
 
 
+def test_c4_shape_tables_jit_gpu(monkeypatch):
+    """configs[3] through the compiled kernels at a size the oracle checks in full: the 10,000 generated policies
+    over 3,000 mixed resources with the kind-indexed match records and the pattern-shape tables (every distinct
+    compiled pattern walked once per resource, matched pairs decided in the match phase): every pair's status and every
+    FAIL pair's path and message against the oracle; then the same with ~40 rule slices (KYV_SLICE_MB=16), which must
+    equal the one-slice evaluation byte for byte"""
+    import parity_util as PU
+    pols = synth.c4_policies(10000)
+    docs, nsl = synth.mixed(3000, seed=63, edge=True)
+    st, res = PU.compare_matrix(pols, docs, nsl, backend="gpu", jit=True, threads=_oracle_threads())
+    assert st["nbad"] == 0, st["bad"]
+    assert res.jit and res.jit_shapes
+    assert st["matched"] > 100_000
+    monkeypatch.setenv("KYV_SLICE_MB", "16")
+    rs = E.Ruleset(pols)
+    b = E.Batch(rs, docs, nsl)
+    sl = E.evaluate(rs, b, backend="gpu", jit=True)
+    assert sl.jit_shapes
+    assert np.array_equal(sl.raw, res.raw)
+    fail = np.argwhere(sl.status == K.ST_FAIL)
+    rng = np.random.default_rng(2)
+    for k, r in fail[rng.choice(len(fail), size=min(300, len(fail)), replace=False)]:
+        assert sl.path(int(r), int(k)) == res.path(int(r), int(k))
+
+
 def test_c4_at_scale_gpu():
     """configs[3] at scale: 10,000 generated policies (~10.4k compiled rules) over 100k mixed resources on one
     MI355X (buffers beyond the slice budget -> rule slices); the oracle (0.9 M pairs/s on C4) checks a spread
