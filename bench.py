@@ -365,11 +365,13 @@ PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::
 
 def pmc_traffic(config, phase):
     """Memory-side bytes per launch of the dominant kernel (phase) from the newest committed PMC summary
-    (profiles/pmc_latest.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc passes of this same
+    (profiles/pmc_latest_<workload>.json, else profiles/pmc_latest.json; written by scripts/pmc_summary.py from separate rocprofv3 --pmc passes of this same
     command), used only when it was measured on the same workload configuration; else None. Returns
     (summary, tag) with summary = {traffic raw, traffic with the guide's x2 read correction, kernel ns}, all per
     evaluation (every launch of the phase's kernels in one evaluation)."""
-    f = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    f = os.path.join(ROOT, "profiles", "pmc_latest_%s.json" % str(config.get("workload", "")).split(":")[0].strip().lower())
+    if not os.path.exists(f):
+        f = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(f):
         return None, None
     with open(f) as fh:

@@ -16,6 +16,8 @@ void match_walk_generic(int wpe, unsigned grid, hipStream_t s, const void* view,
                         const uint32_t* mrules, uint32_t nm);
 void match_pre(unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl, const uint32_t* mrules,
                uint32_t nm);
+void match_pre_j(unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl, const uint32_t* mrules,
+                 uint32_t nm);
 void pss(bool exact, int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0);
 void match_deny(unsigned grid, hipStream_t s, const void* view, const void* devout, const uint32_t* mrules, uint32_t nm);
 void pss_map(unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0);

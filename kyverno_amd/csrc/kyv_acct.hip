@@ -72,6 +72,13 @@ void match_pre(unsigned grid, hipStream_t s, const void* view, const void* devou
                      as<WorkLists>(wl), mrules, nm);
   check(hipGetLastError());
 }
+void match_pre_j(unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl, const uint32_t* mrules,
+                 uint32_t nm) {
+  using namespace kyv_acct;
+  hipLaunchKernelGGL((match_pre_kernel<KYV_MATCH_WPE, true>), dim3(grid), dim3(BLOCK), 0, s, (const View*)view,
+                     as<DevOut>(devout), as<WorkLists>(wl), mrules, nm);
+  check(hipGetLastError());
+}
 void pss(bool exact, int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, uint32_t k, uint32_t w0) {
   using namespace kyv_acct;
   auto kf = exact ? (wpe == 4 ? pss_kernel<true, 4> : wpe == 6 ? pss_kernel<true, 6> : pss_kernel<true, 8>)

@@ -777,9 +777,12 @@ KYV_HD int eval_cond(const View& v, NodeTab R, const Cond& c, const CV& k, const
 // kJ = false instantiates the program without the JMESPath interpreter (no projection lists on the stack): the
 // light match kernel evaluates only rules whose programs hold no OK_JMES operand (the host routes the others).
 constexpr int CP_ERROR = 5;
+// eval_prog_inl: the body, always inlined (the match kernels call it from ONE site each, so the program is inline code
+// instead of a call whose frame goes through scratch memory); eval_prog: the same, left to the inliner (foreach)
 template <bool kJ = true>
-KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond, uint32_t* err_side, uint32_t* err_seg,
-                     uint32_t elem = NONE, uint32_t row = NONE) {
+KYV_HD __attribute__((always_inline)) int eval_prog_inl(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond,
+                                                        uint32_t* err_side, uint32_t* err_seg, uint32_t elem = NONE,
+                                                        uint32_t row = NONE) {
   const CondProg& p = v.cprogs[prog];
   const uint32_t nany = p.nany == NONE ? 0u : p.nany;
   for (uint32_t blk = 0; blk < 2; blk++) {
@@ -808,36 +811,40 @@ KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond
       }
     }
   }
-  auto one = [&](uint32_t ci) -> int {
-    const Cond& c = v.conds[ci];
+  // the any / all evaluation (evaluate.go:42-69) as ONE loop over the conditions, per-lane state instead of two loops
+  // around a per-condition callable: the compiler kept that callable out of line (two call sites), and every call saved
+  // the caller's registers to scratch memory (C5 round 4: 1.8 GB of scratch writes per evaluation in match_deny_kernel)
+  const uint32_t na = p.nany == NONE ? 0u : p.nany;
+  uint32_t any = 0;  // (a loop-carried flag: an integer word, kyv_pss.h eval_pss)
+  for (uint32_t q = 0; q < na + p.nall; q++) {
+    const bool isany = q < na;
+    if (!isany && q == na && p.nany != NONE && !any) return CR_FALSE;  // no any-condition held
+    if (isany && any) continue;
+    const Cond& c = v.conds[isany ? p.any0 + q : p.all0 + (q - na)];
     CV k, x;
     uint32_t miss;
+    int r;
     if constexpr (kJ) {
       JList lk, lx;
       operand_cv(v, R, c.key, elem, lk, &k, &miss, row);
       operand_cv(v, R, c.value, elem, lx, &x, &miss, row);
-      return eval_cond(v, R, c, k, x);
+      r = eval_cond(v, R, c, k, x);
     } else {
       cv_operand(v, R, c.key, &k, &miss, row);
       cv_operand(v, R, c.value, &x, &miss, row);
-      return eval_cond(v, R, c, k, x);
+      r = eval_cond(v, R, c, k, x);
     }
-  };
-  if (p.nany != NONE) {
-    bool any = false;
-    for (uint32_t i = 0; i < p.nany; i++) {
-      int r = one(p.any0 + i);
-      if (r == CR_FB || r == CR_PANIC) return r;
-      if (r == CR_TRUE) { any = true; break; }
-    }
-    if (!any) return CR_FALSE;
-  }
-  for (uint32_t i = 0; i < p.nall; i++) {
-    int r = one(p.all0 + i);
     if (r == CR_FB || r == CR_PANIC) return r;
-    if (r == CR_FALSE) return CR_FALSE;
+    if (isany) { if (r == CR_TRUE) any = 1; }
+    else if (r == CR_FALSE) return CR_FALSE;
   }
+  if (p.nany != NONE && !any) return CR_FALSE;
   return CR_TRUE;
+}
+template <bool kJ = true>
+KYV_HD int eval_prog(const View& v, NodeTab R, uint32_t prog, uint32_t* err_cond, uint32_t* err_side, uint32_t* err_seg,
+                     uint32_t elem = NONE, uint32_t row = NONE) {
+  return eval_prog_inl<kJ>(v, R, prog, err_cond, err_side, err_seg, elem, row);
 }
 
 }  // namespace kyv

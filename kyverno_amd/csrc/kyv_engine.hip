@@ -327,6 +327,7 @@ struct SliceSched {
   uint8_t* tails = nullptr;      // lane tail facts of the records (TailTab): TailCfg, then the TailProgs
   uint32_t nmd = 0;              // then deny rules without JMESPath on match_deny_kernel
   uint32_t nmp = 0;              // then pattern rules with preconditions without JMESPath on match_pre_kernel
+  uint32_t nmpj = 0;             // then those with JMESPath preconditions (no compiled kernel) on match_pre_kernel<.., true>
   uint32_t nm = 0, nmj = 0, nmc = 0;  // then [0, nm) light, [nm, nm + nmj) with JMESPath operands / foreach on the
                                  // interpreted match_kernel<true>, then nmc of those in the compiled kyv_jit_cond
   std::vector<uint32_t> ml, mj;  // host copies: light rules, JMESPath / foreach rules
@@ -1339,7 +1340,7 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     }
     // light pattern rules with preconditions: match_pre_kernel (KYV_PRE_KERNEL=0: the light match kernel)
     static const bool pre_k = !getenv("KYV_PRE_KERNEL") || atoi(getenv("KYV_PRE_KERNEL")) != 0;
-    std::vector<uint32_t> mp;
+    std::vector<uint32_t> mp, mpj;
     if (pre_k) {
       std::vector<uint32_t> rest;
       for (uint32_t q : mr) {
@@ -1379,6 +1380,8 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
         uint32_t lo = nw, hi = 0;
         gate_range(q, lo, hi);
         if (lo < hi) { sl.cw.push_back(make_uint3(q, lo, hi - lo)); sl.cwm.push_back(0); }
+      } else if (pre_k && (rs.rules[q].kind == RK_PATTERN || rs.rules[q].kind == RK_ANYPATTERN) && rs.rules[q].pre != NONE) {
+        mpj.push_back(q);  // a pattern rule with JMESPath preconditions: match_pre_kernel<JMESPath>
       } else {
         mr.push_back(q);
       }
@@ -1497,9 +1500,11 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       HIP_OK(dmalloc(&sl.mrec, recs.size() * sizeof(MRec)));
       HIP_OK(hipMemcpy(sl.mrec, recs.data(), recs.size() * sizeof(MRec), hipMemcpyHostToDevice));
     }
-    sl.nmw = (uint32_t)mw.size();  // device list: [match_walk_generic_kernel rules][deny][pre][light][JMESPath][compiled]
+    sl.nmw = (uint32_t)mw.size();  // device list: [generic][deny][pre][pre JMESPath][light][JMESPath][compiled]
     sl.nmd = (uint32_t)md.size();
     sl.nmp = (uint32_t)mp.size();
+    sl.nmpj = (uint32_t)mpj.size();
+    mr.insert(mr.begin(), mpj.begin(), mpj.end());
     mr.insert(mr.begin(), mp.begin(), mp.end());
     mr.insert(mr.begin(), md.begin(), md.end());
     mr.insert(mr.begin(), mw.begin(), mw.end());
@@ -1785,7 +1790,12 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         else hipLaunchKernelGGL(match_pre_kernel<KYV_MATCH_WPE>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
                                 (const uint32_t*)sl.mrules + sl.nmw + sl.nmd, sl.nmp);
       }
-      const uint32_t ml0 = sl.nmw + sl.nmd + sl.nmp;
+      if (sl.nmpj) {
+        if (acct) kyvacct::match_pre_j(grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw + sl.nmd + sl.nmp, sl.nmpj);
+        else hipLaunchKernelGGL((match_pre_kernel<KYV_MATCH_WPE, true>), grid, dim3(BLOCK), 0, stream, (const View*)d.view, o,
+                                d.wl, (const uint32_t*)sl.mrules + sl.nmw + sl.nmd + sl.nmp, sl.nmpj);
+      }
+      const uint32_t ml0 = sl.nmw + sl.nmd + sl.nmp + sl.nmpj;
       if (sl.nm) {
         if (acct) kyvacct::match(false, grid.x, stream, d.view, &o, &d.wl, sl.mrules + ml0, sl.nm);
         else hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,

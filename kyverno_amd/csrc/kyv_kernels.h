@@ -86,16 +86,17 @@ match_deny_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restr
       const NodeTab R{v.nodes + v.hdr[r].root};
       KYV_ACCT_ADD(0, 4);  // header: root
       uint32_t ec, es, eg;
-      int c = CR_TRUE;
-      if (rd.pre != NONE) c = eval_prog<false>(v, R, rd.pre, &ec, &es, &eg, NONE, r);
-      if (c == CR_FB) st = (KYV_WHY(FBW_COND), ST_FALLBACK);
-      else if (c == CR_PANIC) st = ST_PANIC;
-      else if (c == CP_ERROR) st = ST_ERROR | ST_MARK_PRE;
-      else if (c == CR_FALSE) st = ST_SKIP | ST_MARK_PRE;
-      else {
-        c = eval_prog<false>(v, R, rd.root, &ec, &es, &eg, NONE, r);
-        st = c == CR_FB ? (KYV_WHY(FBW_COND), ST_FALLBACK) : c == CR_PANIC ? ST_PANIC : c == CP_ERROR ? ST_ERROR
-           : c == CR_TRUE ? ST_FAIL : ST_PASS;
+      // preconditions (pass 0, when the rule has them) then the deny program (pass 1): one inlined evaluation site
+      for (uint32_t pass = rd.pre != NONE ? 0u : 1u; pass < 2; pass++) {
+        const int c = eval_prog_inl<false>(v, R, pass ? rd.root : rd.pre, &ec, &es, &eg, NONE, r);
+        if (c == CR_FB) { st = (KYV_WHY(FBW_COND), ST_FALLBACK); break; }
+        if (c == CR_PANIC) { st = ST_PANIC; break; }
+        if (pass == 0) {
+          if (c == CP_ERROR) { st = ST_ERROR | ST_MARK_PRE; break; }
+          if (c == CR_FALSE) { st = ST_SKIP | ST_MARK_PRE; break; }
+        } else {
+          st = c == CP_ERROR ? ST_ERROR : c == CR_TRUE ? ST_FAIL : ST_PASS;
+        }
       }
     }
     if (st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
@@ -858,7 +859,9 @@ match_walk_generic_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, c
 // (validation.go:281-288), then the work-list append -- without the PodSecurity / deny dispatch code of match_kernel,
 // whose register need spilled its rule loop (C5 round 4: match_kernel<false> 166 VGPRs + 176 B of scratch per lane;
 // 4.1 GB of scratch writes per evaluation in the match phase)
-template <int kWpe>
+// kJ: the preconditions hold JMESPath operands (rules the compiled condition kernels do not take; the interpreter's
+// projection lists live in scratch, so these rules get their own instantiation instead of match_kernel<true>)
+template <int kWpe, bool kJ = false>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
 match_pre_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint32_t* __restrict__ mrules, uint32_t nm) {
   const View& v = *vp;
@@ -877,7 +880,7 @@ match_pre_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint
     bool m = false;
     if (gated && pair_match(v, r, rd, &st)) {
       uint32_t ec, es, eg;
-      const int c = eval_prog<false>(v, NodeTab{v.nodes + hroot}, rd.pre, &ec, &es, &eg, NONE, r);
+      const int c = eval_prog_inl<kJ>(v, NodeTab{v.nodes + hroot}, rd.pre, &ec, &es, &eg, NONE, r);
       if (c == CR_FB) st = (KYV_WHY(FBW_COND), ST_FALLBACK);
       else if (c == CR_PANIC) st = ST_PANIC;
       else if (c == CP_ERROR) st = ST_ERROR | ST_MARK_PRE;

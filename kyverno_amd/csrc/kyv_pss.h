@@ -1079,23 +1079,25 @@ KYV_HD uint8_t pair_dispatch(const View& v, bool active, uint32_t r, uint32_t k,
   const ResHeader& h = v.hdr[r];
   NodeTab R{v.nodes + h.root};
   uint32_t ec, es, eg;
-  if (rd.pre != NONE) {  // checkPreconditions (validation.go:281-288)
-    int c = eval_prog<kJ>(v, R, rd.pre, &ec, &es, &eg, NONE, r);
+  // checkPreconditions (validation.go:281-288), then for a deny rule validateDeny (validation.go:437-464): one
+  // program evaluation site for both (pass 0 / 1), inlined
+  const uint32_t p0 = rd.pre != NONE ? 0u : 1u, p1 = rd.kind == RK_DENY ? 2u : 1u;
+  for (uint32_t pass = p0; pass < p1; pass++) {
+    const int c = eval_prog_inl<kJ>(v, R, pass ? rd.root : rd.pre, &ec, &es, &eg, NONE, r);
     if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
     if (c == CR_PANIC) return ST_PANIC;
-    if (c == CP_ERROR) return ST_ERROR | ST_MARK_PRE;
-    if (c == CR_FALSE) return ST_SKIP | ST_MARK_PRE;
+    if (pass == 0) {
+      if (c == CP_ERROR) return ST_ERROR | ST_MARK_PRE;
+      if (c == CR_FALSE) return ST_SKIP | ST_MARK_PRE;
+    } else {
+      if (c == CP_ERROR) return ST_ERROR;
+      return c == CR_TRUE ? ST_FAIL : ST_PASS;
+    }
   }
   switch (rd.kind) {
     case RK_PANIC: return ST_PANIC;
     case RK_ERROR: return ST_ERROR;
-    case RK_DENY: {  // validateDeny (validation.go:437-464)
-      int c = eval_prog<kJ>(v, R, rd.root, &ec, &es, &eg, NONE, r);
-      if (c == CR_FB) return KYV_WHY(FBW_COND), ST_FALLBACK;
-      if (c == CR_PANIC) return ST_PANIC;
-      if (c == CP_ERROR) return ST_ERROR;
-      return c == CR_TRUE ? ST_FAIL : ST_PASS;
-    }
+    case RK_DENY: return ST_NONE;  // (decided above)
     case RK_PSS: return eval_pss(v, v.pss[rd.root], R, h, pss_fails, r);
     case RK_FOREACH:
       if constexpr (kJ) return eval_foreach(v, R, rd, r);

@@ -14,8 +14,9 @@ run() {  # name, env...
   grep "^{" $OUT/$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$n', 'ms/step %.2f' % d['ms_per_step'], {k: round(v,2) for k,v in r['phase_ms'].items()})"
 }
 run base KYV_X=0
-run notail KYV_TAIL_FACTS=0
+#run notail KYV_TAIL_FACTS=0
 run wpe5 KYV_MATCHW_WPE=5
+
 cd /tmp && export TMPDIR=/tmp
 i=0
 for C in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \

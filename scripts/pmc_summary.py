@@ -4,7 +4,7 @@
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats), profiles/<tag>_pmc.csv (per-dispatch
 counters of the dominant kernel, one row per PMC pass and dispatch) and profiles/<tag>_summary.json (averages
-per launch). bench.py reads profiles/pmc_latest.json (a copy of the newest summary) for roofline.traffic.
+per launch). bench.py reads profiles/pmc_latest_<workload>.json (a copy of the newest summary of that workload) for roofline.traffic.
 
 Units: rocprofv3 FETCH_SIZE / WRITE_SIZE are KiB per dispatch. MI355X_MICROARCH.md (HBM section) notes that on
 gfx950 FETCH_SIZE reports half the bytes of a wide 16-B/lane coalesced stream; this kernel's reads are 16-B
@@ -117,7 +117,10 @@ def main(tag):
                 out["bench_value"] = b.get("value")
     js = json.dumps(out, indent=1, sort_keys=True)
     open(os.path.join(dst, tag + "_summary.json"), "w").write(js + "\n")
-    open(os.path.join(dst, "pmc_latest.json"), "w").write(js + "\n")
+    # one "latest" per workload (bench.py reads the one of the workload it runs), so profiling C4 / C5 does not
+    # displace the headline workload's summary
+    wl = ((out.get("bench_config") or {}).get("workload") or "").split(":")[0].strip().lower()
+    open(os.path.join(dst, "pmc_latest_%s.json" % wl if wl else "pmc_latest.json"), "w").write(js + "\n")
     print(js)
 
 
