@@ -148,12 +148,13 @@ def time_gathers(batch, local, rank, world):
     return out
 
 
-def native_gathers(batch, local, rank, world, pg, res_offset):
+def native_gathers(batch, local, rank, world, pg, res_offset, own_counts=None):
     """Report assembly over the device-resident results of the last timed evaluation with the
-    library's own RCCL communicator (kyv_comm_*; no torch in the process): all-gather of every rank's packed verdicts
-    and failing-path rows, each timed with HIP events on the communicator's stream after a warm-up gather, plus the
-    wall time of the call; max over ranks. Checked: this rank's gathered segment equals the host packing of its
-    resident verdicts, and every rank sees every segment with the checksum its owner computed."""
+    library's own RCCL communicator (kyv_comm_*; no torch in the process): every rank's packed verdicts and its
+    failing-path rows (16 B each) sent to rank 0, the report's consumer (kyv_comm_gather_report), and the per-rule
+    verdict tallies all-reduced (kyv_comm_reduce_counts); each timed after a warm-up, max over ranks. Checked: the
+    root's copy of every rank's verdicts has the checksum its owner computed, every rank's row count arrived, and the
+    reduced tallies equal the sum of the ranks' own."""
     import zlib
     import numpy as np
     from kyverno_amd import scan
@@ -164,24 +165,36 @@ def native_gathers(batch, local, rank, world, pg, res_offset):
         uid = box[0]
     comm = scan.Comm(uid, world, rank, local)
     try:
-        comm.gather(batch, res_offset)  # warm-up: communicator setup, buffers
+        comm.gather_report(batch, res_offset, root=0)  # warm-up: communicator setup, buffers
         barrier(pg)
         t0 = time.perf_counter()
-        st = comm.gather(batch, res_offset)
+        st = comm.gather_report(batch, res_offset, root=0)
         wall = time.perf_counter() - t0
         barrier(pg)
+        t1 = time.perf_counter()
+        tot = comm.reduce_counts(batch)
+        reduce_ms = (time.perf_counter() - t1) * 1e3
         own = scan.pack_status(batch.resident_status(device=local))
-        seg = comm.status_of(rank)
-        own_ok = bool(np.array_equal(seg[:own.size], own))
-        owners = all_gather_obj(pg, (rank, zlib.crc32(own.tobytes()), int(own.size)))
-        seen_ok = all(zlib.crc32(comm.status_of(q)[:n].tobytes()) == c for q, c, n in owners)
+        mine = None if own_counts is None else np.asarray(own_counts)
+        owners = all_gather_obj(pg, (rank, zlib.crc32(own.tobytes()), int(own.size),
+                                     None if mine is None else mine.tolist()))
+        seen_ok = True
+        if rank == 0:
+            seen_ok = all(zlib.crc32(comm.status_of(q)[:n].tobytes()) == c for q, c, n, _ in owners)
+        sum_ok = None
+        if all(m is not None for *_, m in owners):
+            sum_ok = bool(np.array_equal(tot, np.sum([np.asarray(m) for *_, m in owners], axis=0)))
+        rows_seen = int(st["failure_rows_total"])
     finally:
         comm.close()
-    return {"backend": "RCCL (kyv_comm, library-owned communicator)", "world": world,
+    return {"backend": "RCCL (kyv_comm, library-owned communicator): verdicts + 16-B failing-path rows to rank 0, "
+                       "tallies all-reduced", "world": world,
             "verdicts_ms": st["status_ms"], "failures_ms": st["failures_ms"], "wall_ms": wall * 1e3,
-            "verdict_wire_bytes_per_rank": st["status_bytes_per_rank"], "failure_rows_total": st["failure_rows_total"],
-            "failure_rows_per_rank_max": st["failure_rows_per_rank_max"], "own_segment_ok": own_ok,
-            "segments_ok": bool(seen_ok)}
+            "reduce_counts_ms": reduce_ms,
+            "verdict_wire_bytes_per_rank": st["status_bytes_per_rank"], "failure_rows_total": rows_seen,
+            "failure_row_wire_bytes": 16 * rows_seen,
+            "failure_rows_per_rank_max": st["failure_rows_per_rank_max"], "segments_ok": bool(seen_ok),
+            "rows_complete": st["failures_ms"] >= 0, "counts_sum_ok": sum_ok}
 
 
 def barrier(pg):
@@ -359,8 +372,29 @@ def shard_parity(policies, rs, data, nsl, timed_status, cap=100000):
 
 
 # device phase -> kernel-name prefixes of that phase in a rocprofv3 kernel trace
-PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::pss_kernel", "kyv::pss_map_kernel", "kyv::match_deny_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv::walk_kernel"),
+PHASE_KERNELS = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::match_walk_generic", "kyv::match_rec_kernel", "kyv::match_pre_kernel", "kyv::facts_kernel", "kyv::pss_kernel", "kyv::pss_map_kernel", "kyv::match_deny_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv_jit_shapes", "kyv::walk_kernel"),
                  "compact": ("kyv::compact",), "hist": ("kyv::status_hist",)}
+
+
+def largest_kernel(s, pre):
+    """The phase's longest kernel per evaluation in a PMC summary: its name, launches and time per evaluation and its
+    own memory-side bytes (TCC_EA FETCH_SIZE + WRITE_SIZE) and counter roofline fraction (bytes / its time / peak)."""
+    kern = s.get("kernels") or {}
+    nev = s.get("evaluations") or sum(k["calls"] for kn, k in kern.items() if "status_hist" in kn) or 1
+    best = None
+    for kn, k in kern.items():
+        n = kn[5:] if kn.startswith("void ") else kn
+        if not n.startswith(pre):
+            continue
+        ns = k["avg_ns"] * k["calls"] / nev
+        if best is None or ns > best[1]:
+            best = (kn, ns, k["calls"] / nev)
+    if best is None:
+        return None
+    c = (s.get("counters_avg_per_launch") or {}).get(best[0]) or {}
+    b = (c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) * 1024 * best[2]
+    return {"name": best[0], "launches_per_eval": best[2], "ms_per_eval": best[1] / 1e6, "counter_bytes_per_eval": b,
+            "counter_frac": b / (best[1] / 1e9) / 1e9 / HBM_PEAK_GBS if best[1] > 0 else None}
 
 
 def pmc_traffic(config, phase):
@@ -380,12 +414,12 @@ def pmc_traffic(config, phase):
     keys = ("workload", "resources_per_gpu", "compiled_rules")
     if any(bc.get(k) != config.get(k) for k in keys):
         return None, s.get("tag")
+    pre = PHASE_KERNELS[phase]
     ph = (s.get("phases") or {}).get(phase)
     if ph:  # scripts/pmc_summary.py: per-evaluation totals of the phase's kernels
         return {"raw": ph["traffic_bytes"], "x2read": 2 * ph["fetch_bytes"] + ph["write_bytes"], "fetch": ph["fetch_bytes"],
                 "write": ph["write_bytes"], "avg_ns": ph["ns"], "wait_frac": ph.get("wait_frac"),
-                "l2_hit": ph.get("l2_hit_rate")}, s.get("tag")
-    pre = PHASE_KERNELS[phase]
+                "l2_hit": ph.get("l2_hit_rate"), "largest": largest_kernel(s, pre)}, s.get("tag")
     fetch = write = ns = 0.0
     found = False
     kern = s.get("kernels") or {}
@@ -407,7 +441,8 @@ def pmc_traffic(config, phase):
     if not found:
         return None, s.get("tag")
     return {"raw": fetch + write, "x2read": 2 * fetch + write, "fetch": fetch, "write": write, "avg_ns": ns,
-            "wait_frac": s.get("dominant_wait_frac"), "l2_hit": s.get("dominant_l2_hit_rate")}, s.get("tag")
+            "wait_frac": s.get("dominant_wait_frac"), "l2_hit": s.get("dominant_l2_hit_rate"),
+            "largest": largest_kernel(s, pre)}, s.get("tag")
 
 
 def _split_ndjson(data, parts):
@@ -532,6 +567,9 @@ def main():
     counts = first.counts
     timed_jit = bool(first.jit)
     fb_reasons = fallback_by_reason(rs, first)
+    batch_dev = {"upload_ms": first.upload_ms, "gmask_kernel_ms": first.gmask_ms,
+                 "note": "per-batch device work before the batch's first evaluation (outside `value`): the batch "
+                         "image upload through the pinned ring and the glob-mask kernel over its dictionary"}
     log("rank %d: first GPU evaluation (incl. upload) %.2f s, kernel %.2f ms" % (rank, t_upload, first.kernel_ms))
     del first
     for _ in range(max(0, args.warmup - 1)):
@@ -600,7 +638,7 @@ def main():
         log("rank %d: device-resident gathers %s" % (rank, gathers))
     elif not args.no_gather:  # the library's own RCCL communicator
         try:
-            gathers = native_gathers(batch, local, rank, world, pg, lo)
+            gathers = native_gathers(batch, local, rank, world, pg, lo, own_counts=r.rule_counts)
         except Exception as e:  # reported, never fatal for the timed line
             gathers = {"error": str(e)[:300]}
         log("rank %d: device-resident gathers %s" % (rank, gathers))
@@ -681,10 +719,15 @@ def main():
                          "profiled_kernel_ms": tr["avg_ns"] / 1e6 if tr else None,
                          "profiled_wait_frac": tr.get("wait_frac") if tr else None,
                          "profiled_l2_hit_rate": tr.get("l2_hit") if tr else None,
-                         "kernel": {"walk": "kyv_jit_walk (runtime-compiled pattern walk)",
-                                    "cond": "kyv_jit_cond (runtime-compiled deny / foreach conditions)",
-                                    "match": "kyv::match_walk_kernel / match_kernel / pss_kernel (match / exclude, "
-                                             "podSecurity, plain conditions)",
+                         "largest_kernel": tr.get("largest") if tr else None,
+                         "kernel": {"walk": "the pattern-walk phase: kyv_jit_fused_<group>[p<part>] (runtime-compiled "
+                                            "fused walks, one kernel per rule group and part), kyv_jit_shapes (shape "
+                                            "tables), kyv_jit_walk_<k> (per-chunk walks); frac is the phase's (all its "
+                                            "kernels' bytes / their summed time), largest_kernel the longest one's own",
+                                    "cond": "kyv_jit_condg_<rule> / kyv_jit_cond_<rule> (runtime-compiled deny / foreach "
+                                            "conditions)",
+                                    "match": "kyv::match_rec_kernel / match_deny_kernel / match_pre_kernel / match_kernel "
+                                             "/ pss_kernel (match / exclude, podSecurity, plain conditions)",
                                     "compact": "kyv::compact_* (failing-path record compaction)",
                                     "hist": "kyv::status_hist_kernel (verdict totals)"}[dom],
                          "kernel_ms": dom_ms,
@@ -723,13 +766,16 @@ def main():
                 "failures_ms_max_rank": max(g.get("failures_ms", 0.0) for g in gather_ranks),
                 "ranks": gather_ranks,
                 "ok": all(g.get("own_segment_ok", True) and g.get("segments_ok", True) and "error" not in g
-                          for g in gather_ranks),
-                "note": "timed after the evaluation, outside `value`: RCCL all-gather of the packed verdicts and the "
-                        "failing-path rows from the device-resident results (kyv_comm_gather_results; --gather: "
-                        "torch.distributed's RCCL, kyverno_amd/scan.py)"},
+                          and g.get("rows_complete", True) and g.get("counts_sum_ok") is not False
+                          and g.get("failures_ms", 0.0) >= 0 for g in gather_ranks),
+                "note": "timed after the evaluation, outside `value`: the packed verdicts and 16-B failing-path rows "
+                        "of every rank sent to rank 0 from the device-resident results (kyv_comm_gather_report), the "
+                        "per-rule tallies all-reduced (kyv_comm_reduce_counts); --gather: torch.distributed's RCCL "
+                        "all-gathers, kyverno_amd/scan.py"},
             "host": {"generate_s": t_gen, "compile_s": t_compile, "flatten_s": t_flat,
                      "flatten_resources_per_s": batch.n / max(t_flat, 1e-9),
                      "first_eval_incl_upload_s": t_upload, "batch_device_bytes": batch.stats()["device_bytes"],
+                     "per_batch_device_ms": batch_dev,
                      "e2e": e2e},
         }
         print(json.dumps(line), flush=True)

@@ -61,7 +61,8 @@ enum {
   KYV_ST_ERROR = 4,
   KYV_ST_FALLBACK = 5,   /* rule needs the reference CPU engine */
   KYV_ST_PANIC = 6,      /* the reference would panic on this input */
-  KYV_ST_ND = 7          /* the reference result depends on Go map iteration order */
+  KYV_ST_ND = 7,         /* the reference result depends on Go map iteration order */
+  KYV_NSTATUS = 8        /* number of verdict values (per-rule tally tables) */
 };
 
 /* rule kinds */
@@ -189,6 +190,9 @@ int64_t kyv_results_count(const kyv_results* r, int status);
  * CalculateSummary (pkg/utils/report/results.go:38-54) over a background-scan batch; returns KYV_OK */
 int kyv_results_rule_counts(const kyv_results* r, int64_t* out, size_t cap);
 double kyv_results_kernel_ms(const kyv_results* r);
+/* per-batch device work outside the evaluation (paid once per batch and device, before its first evaluation):
+ * what = 0 the batch image upload (host -> HBM, ms), 1 the glob-mask kernel over the batch dictionary (ms) */
+double kyv_results_batch_ms(const kyv_results* r, int what);
 /* GPU evaluation time split by phase (HIP events on the evaluation stream, ms averaged over the launches):
  * out[0] verdict resets + match kernels, [1] compiled condition kernel, [2] pattern walk kernels (the dominant kernel
  * of a pattern ruleset), [3] failing-path compaction, [4] verdict histogram; returns the number of phases (5) */
@@ -221,8 +225,9 @@ int64_t kyv_results_failures(const kyv_results* r, kyv_failure* out, size_t cap)
  * kyv_batch_export_status: two 3-bit verdicts per byte (low nibble = even resource), rule-major rows of
  *   ceil(nres / 2) bytes; returns the byte count (dst NULL: only the count), -1 on error.
  * kyv_batch_export_failures: int64 rows (resource index + res_offset, rule, anyPattern alternative, path template,
- *   idx[4]) of every failing-path record; returns the row count (dst NULL: only the count), -1 on error or when
- *   the evaluation was rule-sliced (its records are gathered on the host: use kyv_results_failures). */
+ *   idx[4]) of every failing-path record; returns the row count (dst NULL: only the count), -1 on error. A
+ *   rule-sliced evaluation appends every slice's records to one resident list (error when they exceed its buffer);
+ *   one evaluated with copy-back gathered them slice by slice on the host, and they are uploaded from there. */
 int64_t kyv_batch_export_status(const kyv_batch* b, int device, uint8_t* dst, size_t cap, void* stream);
 /* the verdict bytes (KYV_ST_*, marks cleared) of input-order resources [res0, res0 + nres) of every rule, rule-major
  * [rules][nres], from the batch's last GPU evaluation on `device` into HOST memory (a parity check of that very
@@ -239,8 +244,7 @@ int64_t kyv_batch_export_failures(const kyv_batch* b, int device, int64_t res_of
  * assembly of pkg/controllers/report (one process there; one rank per GPU here). */
 typedef struct kyv_comm kyv_comm;
 typedef struct {
-  double status_ms, failures_ms;       /* export + all-gather, HIP-event time on the communicator's stream (failures_ms -1:
-                                          a rule-sliced evaluation, whose failing-path rows are not resident) */
+  double status_ms, failures_ms;       /* export + transfer, HIP-event time on the communicator's stream */
   uint64_t status_bytes_per_rank;      /* padded verdict bytes per rank */
   uint64_t failure_rows_per_rank_max;  /* padded rows per rank */
   uint64_t failure_rows_total;
@@ -253,6 +257,19 @@ int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset,
    8 int64); dst NULL: only the size */
 int64_t kyv_comm_gathered_status(const kyv_comm* c, int rank, uint8_t* host_dst, size_t cap);
 int64_t kyv_comm_gathered_failures(const kyv_comm* c, int rank, int64_t* host_dst, size_t cap_rows);
+/* report assembly to ONE consumer rank (the process that writes the PolicyReports): every rank's packed verdicts and
+ * its failing-path rows as 16-byte records go to `root` with grouped point-to-point sends at exact sizes (no padding,
+ * nothing copied to the other ranks). Afterwards kyv_comm_gathered_status / kyv_comm_gathered_failures on the root
+ * return rank q's segment (rows expanded to the 8 x int64 form, res_offset of rank q added); on other ranks they fail.
+ * A rule-sliced evaluation's rows are resident too (every slice appended). Every rank reports its sizes and an ok flag
+ * first: when any rank has no exportable results, every rank returns the same error (no rank left in a collective).
+ * Replaces the report controller's per-process assembly (pkg/controllers/report/utils/scanner.go:60-110 callers). */
+int kyv_comm_gather_report(kyv_comm* c, const kyv_batch* b, int64_t res_offset, int root, kyv_gather_stats* st);
+/* cluster-wide per-rule verdict tallies of the batch's last evaluation: one ncclAllReduce of the device-resident
+ * [rules][KYV_NSTATUS] tallies (none derived from the summed resource count) -- the PolicyReport summary counts of a
+ * sharded background scan. host_out [rules * KYV_NSTATUS]; returns the entry count (host_out NULL: only
+ * the count), -1 on error. A collective: every rank calls it. */
+int64_t kyv_comm_reduce_counts(kyv_comm* c, const kyv_batch* b, int64_t* host_out, size_t cap);
 
 /* failing path of a single-pattern FAIL ("" otherwise); returns the full length */
 int64_t kyv_results_path(const kyv_results* r, const kyv_ruleset* rs, const kyv_batch* b, uint32_t res, uint32_t rule,

@@ -64,7 +64,7 @@ EXPORTS = [
     "kyv_results_fallback_reason", "kyv_results_pss_checks", "kyv_results_failures", "kyv_ruleset_rule_flags",
     "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase", "kyv_results_alg_bytes_class", "kyv_batch_export_status", "kyv_batch_copy_status",
     "kyv_batch_export_failures", "kyv_comm_unique_id", "kyv_comm_init", "kyv_comm_free", "kyv_comm_gather_results",
-    "kyv_comm_gathered_status", "kyv_comm_gathered_failures",
+    "kyv_comm_gathered_status", "kyv_comm_gathered_failures", "kyv_comm_gather_report", "kyv_comm_reduce_counts", "kyv_results_batch_ms",
 ]
 
 
@@ -121,6 +121,11 @@ def lib():
     L.kyv_comm_gathered_status.restype = i64
     L.kyv_comm_gathered_failures.argtypes = [vp, ctypes.c_int, vp, sz]
     L.kyv_comm_gathered_failures.restype = i64
+    L.kyv_comm_gather_report.argtypes = [vp, vp, i64, ctypes.c_int, ctypes.POINTER(GatherStats)]
+    L.kyv_comm_reduce_counts.argtypes = [vp, vp, vp, sz]
+    L.kyv_comm_reduce_counts.restype = i64
+    L.kyv_results_batch_ms.argtypes = [vp, ctypes.c_int]
+    L.kyv_results_batch_ms.restype = ctypes.c_double
     L.kyv_ruleset_rule_flags.argtypes = [vp, u32]
     L.kyv_ruleset_rule_flags.restype = u32
     L.kyv_ruleset_free.argtypes = [vp]

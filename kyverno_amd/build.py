@@ -16,18 +16,37 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KYV_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["pjson.cpp", "compiler.cpp", "batch.cpp", "capi.cpp", "jit.cpp", "pss_msg.cpp", "typed.cpp"]
-HIP_SRCS = ["kyv_engine.hip", "kyv_acct.hip"]
-HEADERS = ["kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_host.h", "pjson.h", "kyv_wave.h", "kyv_walk.h", "kyv_jcond.h", "kyv_kernels.h", "kyv_acct.h", "kyv_fused.h", "k8s_types.h"]
+HIP_SRCS = ["kyv_prod_j.hip", "kyv_acct_j.hip", "kyv_prod.hip", "kyv_acct.hip", "kyv_engine.hip"]
+HEADERS = ["kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_host.h", "pjson.h", "kyv_wave.h", "kyv_walk.h", "kyv_jcond.h", "kyv_kernels.h", "kyv_acct.h", "kyv_fused.h", "k8s_types.h", "kyv_launch.inc"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-value", "-Wno-unused-function", "-Wno-unused-variable",
           "-Wno-unused-but-set-variable", "-I" + os.path.join(ROOT, "include")]
+
+
+def _deps(path, seen=None):
+    """path and every local header it includes, transitively (#include "..." resolved in csrc/ or include/): a source
+    is rebuilt only when something it actually includes changed (the kernels' translation units take minutes)"""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path, errors="replace") as f:
+        for line in f:
+            t = line.strip()
+            if t.startswith("#include") and '"' in t:
+                name = t.split('"')[1]
+                for d in (os.path.dirname(path), CSRC, os.path.join(ROOT, "include")):
+                    q = os.path.join(d, name)
+                    if os.path.exists(q):
+                        _deps(q, seen)
+                        break
+    return seen
 
 
 def _needs(obj, src):
     if not os.path.exists(obj):
         return True
     t = os.path.getmtime(obj)
-    deps = [src] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "kyvgpu.h")]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return any(os.path.getmtime(d) > t for d in _deps(src))
 
 
 def _compile(src, obj_dir=OBJ, defines=(), host_flags=()):

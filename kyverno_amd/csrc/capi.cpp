@@ -23,6 +23,9 @@ bool pattern_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uint32_
 int64_t export_status(const Batch& b, int device, uint8_t* dst, size_t cap, void* stream);
 int64_t export_failures(const Batch& b, int device, int64_t off, int64_t* dst, size_t cap_rows, void* stream);
 int64_t copy_status(const Batch& b, int device, size_t res0, size_t n, uint8_t* host_dst, size_t cap);
+int64_t export_report_rows(const Batch& b, int device, uint32_t* rows, uint32_t* wide, uint32_t* nwide_dev,
+                           size_t cap_rows, size_t cap_wide, void* stream);
+const unsigned long long* device_counts(const Batch& b, int device, size_t* nrules, size_t* nres);
 bool pss_checks_render(const Ruleset& rs, const Batch& b, uint32_t pos, uint32_t rule, uint32_t mask,
                        std::vector<std::array<std::string, 3>>* out);
 }  // namespace kyv
@@ -328,6 +331,10 @@ int kyv_results_rule_counts(const kyv_results* r, int64_t* out, size_t cap) {
 }
 
 double kyv_results_kernel_ms(const kyv_results* r) { return r ? r->r.kernel_ms : 0; }
+double kyv_results_batch_ms(const kyv_results* r, int what) {
+  if (!r) return 0;
+  return what == 0 ? r->r.h2d_ms : what == 1 ? r->r.gmask_ms : 0;
+}
 
 int kyv_results_phase_ms(const kyv_results* r, double* out, size_t cap) {
   if (!r || !out) return fail(KYV_EINVAL, "null argument"), -1;
@@ -411,20 +418,25 @@ static bool cond_error_text(const Ruleset& rs, const Batch& b, uint32_t res, uin
   return false;
 }
 
-// getDenyMessage (validation.go:466-479) with the message's request.object references resolved; -1: not renderable
-static bool deny_message(const RuleMeta& m, const Batch& b, uint32_t res, std::string* o) {
-  if (m.message.empty()) return *o = "validation error: rule " + m.name + " failed", true;
-  if (m.msg_parts.empty()) return *o = m.message, true;
+// SubstituteAll of a rule message's request.object references (vars.go; validation.go:469 getDenyMessage, :731
+// buildErrorMessage) for the resource at kind-major position `res`: SM_OK with the text in *o; SM_MISSING when a
+// reference does not resolve (a substitution error); SM_NOT_STRING when the whole message is one reference to a
+// non-string; SM_UNRENDERABLE when the text needs the reference engine (a map / array value, nested variables)
+enum SubstMsg { SM_OK = 0, SM_MISSING = 1, SM_NOT_STRING = 2, SM_UNRENDERABLE = 3 };
+static int subst_message(const RuleMeta& m, const Batch& b, uint32_t res, std::string* o) {
+  if (m.msg_parts.empty()) return *o = m.message, SM_OK;
   const Node* R = b.nodes.data() + b.hdr[res].root;
   std::string out;
   for (auto& part : m.msg_parts) {
     if (!part.var) { out += part.text; continue; }
     uint32_t node, miss;
-    if (!host_resolve(b, res, part.segs, &node, &miss)) return *o = m.message, true;  // substitution error
+    if (!host_resolve(b, res, part.segs, &node, &miss)) return SM_MISSING;
     std::string sub;
     uint32_t t = node == NONE ? N_NULL : node_type(R[node]);
-    if (m.msg_whole_var)
-      return *o = t == N_STR ? b.dict.strs[R[node].a] : "the produced message didn't resolve to a string, check your policy definition.", true;
+    if (m.msg_whole_var) {
+      if (t != N_STR) return SM_NOT_STRING;
+      return *o = b.dict.strs[R[node].a], SM_OK;
+    }
     switch (t) {
       case N_STR: sub = b.dict.strs[R[node].a]; break;
       case N_NULL: sub = "null"; break;
@@ -438,12 +450,32 @@ static bool deny_message(const RuleMeta& m, const Batch& b, uint32_t res, std::s
         sub = pj::go_fmt_json(f);
         break;
       }
-      default: return false;  // json.Marshal of a map / array
+      default: return SM_UNRENDERABLE;  // json.Marshal of a map / array
     }
-    if (sub.find("{{") != std::string::npos) return false;  // nested variables are substituted again
+    if (sub.find("{{") != std::string::npos) return SM_UNRENDERABLE;  // nested variables are substituted again
     out += sub;
   }
-  return *o = out, true;
+  return *o = out, SM_OK;
+}
+
+// getDenyMessage (validation.go:461-479): a substitution error leaves the message as written
+static bool deny_message(const RuleMeta& m, const Batch& b, uint32_t res, std::string* o) {
+  if (m.message.empty()) return *o = "validation error: rule " + m.name + " failed", true;
+  switch (subst_message(m, b, res, o)) {
+    case SM_OK: return true;
+    case SM_MISSING: return *o = m.message, true;
+    case SM_NOT_STRING: return *o = "the produced message didn't resolve to a string, check your policy definition.", true;
+    default: return false;
+  }
+}
+
+// buildErrorMessage's message part (validation.go:731-741): the substituted message with a trailing '.'; false when
+// the text needs the reference engine (a substitution error embeds the Go error string, a non-string whole-message
+// reference panics on the type assertion)
+static bool error_message_head(const RuleMeta& m, const Batch& b, uint32_t res, std::string* o) {
+  if (subst_message(m, b, res, o) != SM_OK) return false;
+  if (o->empty() || o->back() != '.') *o += ".";
+  return true;
 }
 
 static uint32_t pss_mask_at(const kyv_results* r, const Ruleset& rs, uint32_t pos, uint32_t rule) {
@@ -477,8 +509,8 @@ static bool walk_text_message(const Ruleset& rs, const Batch& b, uint32_t res, u
     if (st != ST_ERROR) return false;
     if (m.message.empty()) return *o = "validation error: rule " + m.name + " execution error: " + text, true;
     if (m.message_vars) return false;
-    std::string mm = m.message;
-    if (mm.back() != '.') mm += ".";
+    std::string mm;
+    if (!error_message_head(m, b, res, &mm)) return false;
     return *o = "validation error: " + mm + " rule " + m.name + " execution error: " + text, true;
   }
   if (d.kind != RK_ANYPATTERN) return false;
@@ -572,8 +604,8 @@ static bool render_message(kyv_results* r, const Ruleset& rs, const Batch& b, ui
   if (d.kind == RK_PATTERN) {
     std::string path = format_path(rs, b, recs[0]->tmpl, recs[0]->idx, recs[0]->key);
     if (m.message.empty()) return *o = "validation error: rule " + m.name + " failed at path " + path, true;
-    std::string mm = m.message;
-    if (mm.back() != '.') mm += ".";
+    std::string mm;
+    if (!error_message_head(m, b, res, &mm)) return false;
     return *o = "validation error: " + mm + " rule " + m.name + " failed at path " + path, true;
   }
   std::string joined;
@@ -761,6 +793,18 @@ struct kyv_comm {
   int64_t* rows = nullptr;     // [nranks][rows_max][8]
   size_t rows_cap = 0, rows_max = 0;
   std::vector<int64_t> row_counts;
+  // kyv_comm_gather_report (to one consumer rank): per rank, its packed verdicts and its 16-byte rows at exact sizes
+  int mode = 0;                // last gather: 0 none, 1 all-gather (gather_results), 2 to `root` (gather_report)
+  int root = 0;
+  std::vector<int64_t> seg_status, seg_rows, seg_wide, res_off;  // per rank: sizes, offsets below, resource offset
+  std::vector<size_t> at_status, at_rows, at_wide;
+  uint32_t* rrows = nullptr;   // root: every rank's rows, uint32 x 4 each; other ranks: their own (send buffer)
+  size_t rrows_cap = 0;
+  uint32_t* rwide = nullptr;   // side entries of the rows that do not fit 16 bytes
+  size_t rwide_cap = 0;
+  uint32_t* nwide = nullptr;   // [1] side-entry count (report_rows_kernel)
+  unsigned long long* sums = nullptr;  // kyv_comm_reduce_counts: [rules * NSTATUS + 1]
+  size_t sums_cap = 0;
 };
 
 namespace {
@@ -812,9 +856,37 @@ void kyv_comm_free(kyv_comm* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->status) (void)hipFree(c->status);
   if (c->rows) (void)hipFree(c->rows);
+  if (c->rrows) (void)hipFree(c->rrows);
+  if (c->rwide) (void)hipFree(c->rwide);
+  if (c->nwide) (void)hipFree(c->nwide);
+  if (c->sums) (void)hipFree(c->sums);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
+
+namespace {
+// one small all-gather of k int64 per rank (sizes and flags) -> out[nranks * k]
+int exchange_sizes(kyv_comm* c, const int64_t* mine, int k, std::vector<int64_t>* out) {
+  const int n = c->nranks;
+  int64_t* dsz = nullptr;
+  KYV_HIPC(hipMalloc((void**)&dsz, sizeof(int64_t) * k * (n + 1)));
+  struct Free { void* p; ~Free() { (void)hipFree(p); } } fz{dsz};
+  KYV_HIPC(hipMemcpyAsync(dsz + (size_t)k * n, mine, sizeof(int64_t) * k, hipMemcpyHostToDevice, c->stream));
+  KYV_NCCL(ncclAllGather(dsz + (size_t)k * n, dsz, k, ncclInt64, c->comm, c->stream));
+  out->assign((size_t)k * n, 0);
+  KYV_HIPC(hipMemcpyAsync(out->data(), dsz, sizeof(int64_t) * k * n, hipMemcpyDeviceToHost, c->stream));
+  KYV_HIPC(hipStreamSynchronize(c->stream));
+  return KYV_OK;
+}
+// every rank's ok flag (field f of k per rank): all ranks return the same error when any is 0
+int check_flags(kyv_comm* c, const std::vector<int64_t>& sz, int k, int f, const std::string& why) {
+  for (int q = 0; q < c->nranks; q++)
+    if (!sz[(size_t)k * q + f])
+      return fail(KYV_EDEVICE, "report gather: rank " + std::to_string(q) + " has no exportable results" +
+                               (q == c->rank && !why.empty() ? ": " + why : std::string()));
+  return KYV_OK;
+}
+}  // namespace
 
 int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset, kyv_gather_stats* st) {
   if (!c || !b || !st) return fail(KYV_EINVAL, "null argument");
@@ -827,32 +899,30 @@ int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset,
     KYV_HIPC(hipEventCreate(&e2));
     struct Ev { hipEvent_t a, b, c; ~Ev() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); (void)hipEventDestroy(c); } } ev{e0, e1, e2};
     const int n = c->nranks;
-    // sizes of every rank (one small all-gather): verdict bytes and failing-path rows
-    // a rule-sliced evaluation keeps no resident failing-path rows (they were gathered per slice on the host): its
-    // rows are not part of the gather (failures_ms = -1)
-    bool rows_ok = true;
-    int64_t nrows = 0;
+    c->mode = 0;
+    c->row_counts.clear();
+    // sizes of every rank (one small all-gather): verdict bytes, failing-path rows and an ok flag. A rank that cannot
+    // take part (no resident results, rows over the resident buffer) still joins this exchange with flag 0, and every
+    // rank returns the same error: no rank is left waiting in a collective its peers never enter
+    int64_t mine[3] = {0, 0, 1};
+    std::string why;
     try {
-      nrows = export_failures(*b->b, c->device, res_offset, nullptr, 0, c->stream);
-    } catch (std::exception&) {
-      rows_ok = false;
+      mine[0] = export_status(*b->b, c->device, nullptr, 0, c->stream);
+      mine[1] = export_failures(*b->b, c->device, res_offset, nullptr, 0, c->stream);
+    } catch (std::exception& e) {
+      mine[2] = 0;
+      why = e.what();
     }
-    const int64_t mine[2] = {export_status(*b->b, c->device, nullptr, 0, c->stream), nrows};
-    int64_t* dsz = nullptr;
-    KYV_HIPC(hipMalloc((void**)&dsz, sizeof(int64_t) * 2 * (n + 1)));
-    struct Free { void* p; ~Free() { (void)hipFree(p); } } fz{dsz};
-    KYV_HIPC(hipMemcpyAsync(dsz + 2 * n, mine, sizeof mine, hipMemcpyHostToDevice, c->stream));
-    KYV_NCCL(ncclAllGather(dsz + 2 * n, dsz, 2, ncclInt64, c->comm, c->stream));
-    std::vector<int64_t> sz(2 * n);
-    KYV_HIPC(hipMemcpyAsync(sz.data(), dsz, sizeof(int64_t) * 2 * n, hipMemcpyDeviceToHost, c->stream));
-    KYV_HIPC(hipStreamSynchronize(c->stream));
+    std::vector<int64_t> sz;
+    if (int rc = exchange_sizes(c, mine, 3, &sz)) return rc;
+    if (int rc = check_flags(c, sz, 3, 2, why)) return rc;
     size_t smax = 0, rmax = 0;
     c->row_counts.assign(n, 0);
     for (int q = 0; q < n; q++) {
-      smax = std::max<size_t>(smax, (size_t)sz[2 * q]);
-      rmax = std::max<size_t>(rmax, (size_t)sz[2 * q + 1]);
-      c->row_counts[q] = sz[2 * q + 1];
-      st->failure_rows_total += (uint64_t)sz[2 * q + 1];
+      smax = std::max<size_t>(smax, (size_t)sz[3 * q]);
+      rmax = std::max<size_t>(rmax, (size_t)sz[3 * q + 1]);
+      c->row_counts[q] = sz[3 * q + 1];
+      st->failure_rows_total += (uint64_t)sz[3 * q + 1];
     }
     if (int rc = grow(&c->status, &c->status_cap, smax * (n + 1))) return rc;
     if (int rc = grow(&c->rows, &c->rows_cap, rmax * 8 * (n + 1))) return rc;
@@ -867,7 +937,7 @@ int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset,
     }
     KYV_HIPC(hipEventRecord(e1, c->stream));
     if (rmax) {
-      if (rows_ok) export_failures(*b->b, c->device, res_offset, sendr, rmax, c->stream);
+      export_failures(*b->b, c->device, res_offset, sendr, rmax, c->stream);
       KYV_NCCL(ncclAllGather(sendr, c->rows, rmax * 8, ncclInt64, c->comm, c->stream));
     }
     KYV_HIPC(hipEventRecord(e2, c->stream));
@@ -876,9 +946,10 @@ int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset,
     KYV_HIPC(hipEventElapsedTime(&t0, e0, e1));
     KYV_HIPC(hipEventElapsedTime(&t1, e1, e2));
     st->status_ms = t0;
-    st->failures_ms = rows_ok ? t1 : -1.0;
+    st->failures_ms = t1;
     st->status_bytes_per_rank = smax;
     st->failure_rows_per_rank_max = rmax;
+    c->mode = 1;
     return KYV_OK;
   } catch (std::exception& e) {
     return fail(KYV_EINVAL, e.what());
@@ -887,6 +958,16 @@ int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset,
 
 int64_t kyv_comm_gathered_status(const kyv_comm* c, int rank, uint8_t* host_dst, size_t cap) {
   if (!c || rank < 0 || rank >= c->nranks) return fail(KYV_EINVAL, "bad rank"), -1;
+  if (c->mode == 2) {  // gather_report: exact segments, on the root only
+    if (c->rank != c->root) return fail(KYV_EINVAL, "the report was gathered to another rank"), -1;
+    const size_t nb = (size_t)c->seg_status[rank];
+    if (!host_dst) return (int64_t)nb;
+    if (cap < nb) return fail(KYV_ERANGE, "buffer too small"), -1;
+    if (nb && (hipSetDevice(c->device) != hipSuccess ||
+               hipMemcpy(host_dst, c->status + c->at_status[rank], nb, hipMemcpyDeviceToHost) != hipSuccess))
+      return fail(KYV_EDEVICE, "copy of the gathered verdicts failed"), -1;
+    return (int64_t)nb;
+  }
   if (!host_dst) return (int64_t)c->status_bytes;
   if (cap < c->status_bytes) return fail(KYV_ERANGE, "buffer too small"), -1;
   if (hipSetDevice(c->device) != hipSuccess ||
@@ -897,6 +978,38 @@ int64_t kyv_comm_gathered_status(const kyv_comm* c, int rank, uint8_t* host_dst,
 
 int64_t kyv_comm_gathered_failures(const kyv_comm* c, int rank, int64_t* host_dst, size_t cap_rows) {
   if (!c || rank < 0 || rank >= c->nranks) return fail(KYV_EINVAL, "bad rank"), -1;
+  if (c->mode == 2) {  // gather_report: the 16-byte rows (and side entries) expanded to the 8 x int64 row form
+    if (c->rank != c->root) return fail(KYV_EINVAL, "the report was gathered to another rank"), -1;
+    const size_t nr = (size_t)c->seg_rows[rank], nw = (size_t)c->seg_wide[rank];
+    if (!host_dst) return (int64_t)nr;
+    if (cap_rows < nr) return fail(KYV_ERANGE, "buffer too small"), -1;
+    std::vector<uint32_t> rw(nr * 4), wd(nw * 4);
+    if (hipSetDevice(c->device) != hipSuccess ||
+        (nr && hipMemcpy(rw.data(), c->rrows + c->at_rows[rank] * 4, nr * 16, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (nw && hipMemcpy(wd.data(), c->rwide + c->at_wide[rank] * 4, nw * 16, hipMemcpyDeviceToHost) != hipSuccess))
+      return fail(KYV_EDEVICE, "copy of the gathered rows failed"), -1;
+    for (size_t i = 0; i < nr; i++) {
+      const uint32_t* r = &rw[i * 4];
+      int64_t* o = host_dst + i * 8;
+      o[0] = (int64_t)r[0] + c->res_off[rank];
+      o[3] = r[2];
+      if (r[1] & 0x80000000u) {
+        if (r[3] >= nw) return fail(KYV_EINTERNAL, "report row side entry out of range"), -1;
+        const uint32_t* w = &wd[(size_t)r[3] * 4];
+        o[1] = w[0];
+        o[2] = w[1];
+        o[4] = w[2] & 0xFFFF; o[5] = w[2] >> 16; o[6] = w[3] & 0xFFFF; o[7] = w[3] >> 16;
+      } else {
+        o[1] = r[1] & 0xFFFFFF;
+        o[2] = r[1] >> 24;
+        for (int q = 0; q < 4; q++) {
+          const uint32_t x = (r[3] >> (8 * q)) & 255u;
+          o[4 + q] = x == 255u ? 0xFFFF : x;
+        }
+      }
+    }
+    return (int64_t)nr;
+  }
   if ((size_t)rank >= c->row_counts.size()) return 0;  // no gather yet (or the last one failed before its counts)
   const size_t nr = (size_t)c->row_counts[rank];
   if (!host_dst) return (int64_t)nr;
@@ -905,4 +1018,193 @@ int64_t kyv_comm_gathered_failures(const kyv_comm* c, int rank, int64_t* host_ds
              hipMemcpy(host_dst, c->rows + c->rows_max * 8 * rank, nr * 8 * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess))
     return fail(KYV_EDEVICE, "copy of the gathered rows failed"), -1;
   return (int64_t)nr;
+}
+
+// Report assembly to ONE consumer rank (the report controller's process; pkg/controllers/report builds the
+// PolicyReports in one place): every rank's packed verdicts and its failing-path rows as 16-byte records (plus 16-byte
+// side entries for the rare rows that do not fit) go to `root` with grouped point-to-point sends at their exact sizes
+// -- no padding and no copy on the ranks that do not consume them. Bytes on the wire per rank: its packed verdicts
+// (2 bits per pair) + 16 B per failing-path row; the root receives the sum over the other ranks.
+int kyv_comm_gather_report(kyv_comm* c, const kyv_batch* b, int64_t res_offset, int root, kyv_gather_stats* st) {
+  if (!c || !b || !st) return fail(KYV_EINVAL, "null argument");
+  if (root < 0 || root >= c->nranks) return fail(KYV_EINVAL, "bad root rank");
+  try {
+    KYV_HIPC(hipSetDevice(c->device));
+    *st = kyv_gather_stats{};
+    c->mode = 0;
+    const int n = c->nranks;
+    if (!c->nwide) KYV_HIPC(hipMalloc((void**)&c->nwide, 4));
+    // this rank's rows, packed now (their side-entry count is part of the size exchange)
+    int64_t mine[5] = {0, 0, 0, 1, res_offset};
+    std::string why;
+    try {
+      mine[0] = export_status(*b->b, c->device, nullptr, 0, c->stream);
+      mine[1] = export_report_rows(*b->b, c->device, nullptr, nullptr, nullptr, 0, 0, c->stream);
+    } catch (std::exception& e) {
+      mine[3] = 0;
+      why = e.what();
+    }
+    hipEvent_t e0, e1, e2;
+    KYV_HIPC(hipEventCreate(&e0));
+    KYV_HIPC(hipEventCreate(&e1));
+    KYV_HIPC(hipEventCreate(&e2));
+    struct Ev { hipEvent_t a, b, c; ~Ev() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); (void)hipEventDestroy(c); } } ev{e0, e1, e2};
+    const bool me_root = c->rank == root;
+    // receive layout on the root: every rank's segment at exact offsets; elsewhere: this rank's own data only
+    const size_t own_rows = mine[3] ? (size_t)std::max<int64_t>(mine[1], 0) : 0;
+    std::vector<int64_t> sz;
+    // this rank's rows and side entries are packed before the exchange (the side-entry count is part of it) into
+    // temporaries: the senders send from them, the root moves its own into its receive segments
+    uint32_t *packed = nullptr, *pwide = nullptr;
+    struct Free { void* p; ~Free() { if (p) (void)hipFree(p); } } fp{nullptr}, fw{nullptr};
+    if (own_rows) {
+      KYV_HIPC(hipMalloc((void**)&packed, own_rows * 16));
+      fp.p = packed;
+      KYV_HIPC(hipMalloc((void**)&pwide, own_rows * 16));
+      fw.p = pwide;
+      try {
+        export_report_rows(*b->b, c->device, packed, pwide, c->nwide, own_rows, own_rows, c->stream);
+        uint32_t nw = 0;
+        KYV_HIPC(hipMemcpyAsync(&nw, c->nwide, 4, hipMemcpyDeviceToHost, c->stream));
+        KYV_HIPC(hipStreamSynchronize(c->stream));
+        mine[2] = nw;
+      } catch (std::exception& e) {
+        mine[3] = 0;
+        why = e.what();
+      }
+    }
+    if (int rc = exchange_sizes(c, mine, 5, &sz)) return rc;
+    if (int rc = check_flags(c, sz, 5, 3, why)) return rc;
+    c->root = root;
+    c->seg_status.assign(n, 0);
+    c->seg_rows.assign(n, 0);
+    c->seg_wide.assign(n, 0);
+    c->res_off.assign(n, 0);
+    c->at_status.assign(n, 0);
+    c->at_rows.assign(n, 0);
+    c->at_wide.assign(n, 0);
+    size_t ts = 0, tr = 0, tw = 0;
+    for (int q = 0; q < n; q++) {
+      c->seg_status[q] = sz[5 * q];
+      c->seg_rows[q] = sz[5 * q + 1];
+      c->seg_wide[q] = sz[5 * q + 2];
+      c->res_off[q] = sz[5 * q + 4];
+      c->at_status[q] = ts;
+      c->at_rows[q] = tr;
+      c->at_wide[q] = tw;
+      ts += (size_t)sz[5 * q];
+      tr += (size_t)sz[5 * q + 1];
+      tw += (size_t)sz[5 * q + 2];
+      st->failure_rows_total += (uint64_t)sz[5 * q + 1];
+    }
+    const size_t my_s = (size_t)mine[0], my_w = (size_t)mine[2];
+    // buffers: the root holds every segment; a sender only its own verdicts (the rows are sent from `packed`)
+    if (int rc = grow(&c->status, &c->status_cap, me_root ? ts : my_s)) return rc;
+    if (me_root) {
+      if (int rc = grow(&c->rrows, &c->rrows_cap, tr * 4)) return rc;
+      if (int rc = grow(&c->rwide, &c->rwide_cap, tw * 4)) return rc;
+    }
+    KYV_HIPC(hipEventRecord(e0, c->stream));
+    uint8_t* my_status = c->status + (me_root ? c->at_status[root] : 0);
+    if (my_s) export_status(*b->b, c->device, my_status, my_s, c->stream);
+    KYV_NCCL(ncclGroupStart());
+    if (me_root) {
+      for (int q = 0; q < n; q++)
+        if (q != root && c->seg_status[q])
+          KYV_NCCL(ncclRecv(c->status + c->at_status[q], (size_t)c->seg_status[q], ncclUint8, q, c->comm, c->stream));
+    } else if (my_s) {
+      KYV_NCCL(ncclSend(my_status, my_s, ncclUint8, root, c->comm, c->stream));
+    }
+    KYV_NCCL(ncclGroupEnd());
+    KYV_HIPC(hipEventRecord(e1, c->stream));
+    if (me_root && own_rows)
+      KYV_HIPC(hipMemcpyAsync(c->rrows + c->at_rows[root] * 4, packed, own_rows * 16, hipMemcpyDeviceToDevice, c->stream));
+    if (me_root && my_w)
+      KYV_HIPC(hipMemcpyAsync(c->rwide + c->at_wide[root] * 4, pwide, my_w * 16, hipMemcpyDeviceToDevice, c->stream));
+    KYV_NCCL(ncclGroupStart());
+    if (me_root) {
+      for (int q = 0; q < n; q++) {
+        if (q == root) continue;
+        if (c->seg_rows[q])
+          KYV_NCCL(ncclRecv(c->rrows + c->at_rows[q] * 4, (size_t)c->seg_rows[q] * 4, ncclUint32, q, c->comm, c->stream));
+        if (c->seg_wide[q])
+          KYV_NCCL(ncclRecv(c->rwide + c->at_wide[q] * 4, (size_t)c->seg_wide[q] * 4, ncclUint32, q, c->comm, c->stream));
+      }
+    } else {
+      if (own_rows) KYV_NCCL(ncclSend(packed, own_rows * 4, ncclUint32, root, c->comm, c->stream));
+      if (my_w) KYV_NCCL(ncclSend(pwide, my_w * 4, ncclUint32, root, c->comm, c->stream));
+    }
+    KYV_NCCL(ncclGroupEnd());
+    KYV_HIPC(hipEventRecord(e2, c->stream));
+    KYV_HIPC(hipStreamSynchronize(c->stream));
+    float t0 = 0, t1 = 0;
+    KYV_HIPC(hipEventElapsedTime(&t0, e0, e1));
+    KYV_HIPC(hipEventElapsedTime(&t1, e1, e2));
+    st->status_ms = t0;
+    st->failures_ms = t1;
+    st->status_bytes_per_rank = my_s;
+    st->failure_rows_per_rank_max = 0;
+    for (int q = 0; q < n; q++) st->failure_rows_per_rank_max = std::max<uint64_t>(st->failure_rows_per_rank_max, (uint64_t)c->seg_rows[q]);
+    c->mode = 2;
+    return KYV_OK;
+  } catch (std::exception& e) {
+    return fail(KYV_EINVAL, e.what());
+  }
+}
+
+// Cluster-wide per-rule verdict tallies (the summary all-reduce of a sharded background scan, the
+// PolicyReport summary counts of pkg/controllers/report): the device-resident [rules][KYV_NSTATUS] tallies of the
+// batch's last evaluation summed over ranks with one ncclAllReduce; the none column (not tallied on the device) is
+// derived from the summed resource count. host_out [rules * KYV_NSTATUS] int64; returns the entry count (host_out
+// NULL: only the count), -1 on error. Every rank must call it (a collective); a rank without results joins with zeros
+// and every rank then returns an error.
+int64_t kyv_comm_reduce_counts(kyv_comm* c, const kyv_batch* b, int64_t* host_out, size_t cap) {
+  if (!c || !b) return fail(KYV_EINVAL, "null argument"), -1;
+  try {
+    if (hipSetDevice(c->device) != hipSuccess) return fail(KYV_EDEVICE, "hipSetDevice"), -1;
+    size_t nrules = 0, nres = 0;
+    const unsigned long long* cnt = nullptr;
+    std::string why;
+    try {
+      cnt = device_counts(*b->b, c->device, &nrules, &nres);
+    } catch (std::exception& e) {
+      why = e.what();
+    }
+    const size_t ne = nrules * NSTATUS;
+    if (!host_out) {
+      if (!cnt) return fail(KYV_EINVAL, why), -1;
+      return (int64_t)ne;
+    }
+    // sizes + flags first: every rank must reduce the same element count
+    int64_t mine[2] = {(int64_t)ne, cnt ? 1 : 0};
+    std::vector<int64_t> sz;
+    if (exchange_sizes(c, mine, 2, &sz)) return -1;
+    if (check_flags(c, sz, 2, 1, why)) return -1;
+    for (int q = 0; q < c->nranks; q++)
+      if (sz[2 * q] != (int64_t)ne) return fail(KYV_EINVAL, "ranks evaluated different rulesets"), -1;
+    if (cap < ne) return fail(KYV_ERANGE, "buffer too small"), -1;
+    if (grow(&c->sums, &c->sums_cap, ne + 1)) return -1;
+    const unsigned long long nr = nres;
+    if (ne && hipMemcpyAsync(c->sums, cnt, ne * 8, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+      return fail(KYV_EDEVICE, "copy of the verdict tallies failed"), -1;
+    if (hipMemcpyAsync(c->sums + ne, &nr, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+      return fail(KYV_EDEVICE, "copy of the resource count failed"), -1;
+    ncclResult_t r = ncclAllReduce(c->sums, c->sums, ne + 1, ncclUint64, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclAllReduce"), -1;
+    std::vector<unsigned long long> h(ne + 1);
+    if (hipMemcpyAsync(h.data(), c->sums, (ne + 1) * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      return fail(KYV_EDEVICE, "copy of the reduced tallies failed"), -1;
+    for (size_t k = 0; k < nrules; k++) {
+      unsigned long long counted = 0;
+      for (int s = 1; s < NSTATUS; s++) {
+        host_out[k * NSTATUS + s] = (int64_t)h[k * NSTATUS + s];
+        counted += h[k * NSTATUS + s];
+      }
+      host_out[k * NSTATUS + ST_NONE] = (int64_t)(h[ne] - counted);
+    }
+    return (int64_t)ne;
+  } catch (std::exception& e) {
+    return fail(KYV_EINTERNAL, e.what()), -1;
+  }
 }

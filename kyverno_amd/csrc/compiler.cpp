@@ -1675,7 +1675,7 @@ uint32_t compile_conds(Cx& c, const Value* doc) {
 // level). Context entries and other variables stay on the CPU. Returns the pool offset of [n, entries...].
 uint32_t compile_foreach_entries(Cx& c, const Value& fe, int depth, bool* plain_deny) {
   if (fe.t != T::Arr || fe.a.empty()) throw Fallback{"foreach"};
-  if (depth > 1) throw Fallback{"foreach: nested deeper than one level"};
+  if (depth > (int)FOREACH_MAX_NEST) throw Fallback{"foreach: nested deeper than the device evaluates"};
   std::vector<ForeachEntry> ents;
   for (auto& e : fe.a) {
     if (e.t != T::Obj) throw Fallback{"foreach"};
@@ -2130,6 +2130,9 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
           } else if (val && !nil(val->get("pattern"))) {
             rd.kind = RK_PATTERN;
             rd.root = compile_pattern_root(c, *rval->get("pattern"));
+            // buildErrorMessage substitutes the message's variables (validation.go:722-745): request.object
+            // references are rendered on the host from the resource (capi.cpp subst_message)
+            rm.message_vars = !compile_message(c, rm.message, rm);
           } else if (val && !nil(val->get("anyPattern"))) {
             const Value* ap = rval->get("anyPattern");
             if (ap->t != T::Arr) {
@@ -2143,12 +2146,15 @@ Ruleset* compile_ruleset(const char* json, size_t len, std::string* err, const c
               rd.root = (uint32_t)rs->pool.size();
               rd.nalts = (uint32_t)roots.size();
               for (auto x : roots) rs->pool.push_back(x);
+              rm.message_vars = false;  // buildAnyPatternErrorMessage / the pass response take the message as written
+                                        // (validation.go:701, 747-758): no substitution
             }
           } else if (val && !nil(val->get("podSecurity"))) {
             rd.kind = RK_PSS;
             rd.root = compile_pss(c, *val->get("podSecurity"));
             rm.pss_level = val->get("podSecurity")->str_or("level");
             rm.pss_version = val->get("podSecurity")->str_or("version");
+            rm.message_vars = false;  // the PodSecurity responses do not use the message (validation.go:560-566)
           } else if (val && nonempty(val->get("foreach"))) {
             rd.kind = RK_FOREACH;
             rd.root = compile_foreach(c, *val->get("foreach"), rm.message, &rm.foreach_texts);

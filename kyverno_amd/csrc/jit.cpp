@@ -1488,6 +1488,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
   }
   const size_t ngroups = groups.size();
   std::vector<std::pair<size_t, size_t>> fused_kernels;  // (group, part): kyv_jit_fused_<g>[p<part>]
+  std::vector<size_t> merged_groups;                      // groups with a kyv_jit_fusedm_<g> (KYV_FUSED_MERGE)
   for (size_t gi = 0; gi < ngroups; gi++) {
     std::vector<uint32_t> roots, chunk_roots;  // every root of the group; those of its per-chunk (non-fused) rules
     std::vector<size_t> fused;                 // rule_roots indices of the group's fused rules
@@ -1609,6 +1610,27 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
       src << "  }\n"
              "};\n";
       fused_kernels.push_back(std::make_pair(gi, pi));
+    }
+    // KYV_FUSED_MERGE=1 (experiment): the parts once more as ONE kernel, kyv_jit_fusedm_<g>, run back to back for the
+    // same wave, each part's resource index and root laundered through an empty asm so its loads are its own (no value
+    // kept live from one part's rules into the next: the register need stays that of one part). The resource rows and
+    // columns a later part reads again were just read by this wave: L2 hits instead of a second pass over HBM.
+    if (nparts > 1 && getenv("KYV_FUSED_MERGE") && atoi(getenv("KYV_FUSED_MERGE")) != 0) {
+      src << "struct JitFusedM" << gi << " {\n"
+             "  __device__ __forceinline__ void run(const View& v, const DevOut& o, uint32_t nwaves, uint32_t w, uint32_t r,\n"
+             "                                     bool active, uint32_t hflags, uint32_t hroot, const uint32_t* gw) {\n";
+      for (size_t pi = 0; pi < nparts; pi++) {
+        const std::string sname = "JitFused" + std::to_string(gi) + (pi ? "p" + std::to_string(pi) : std::string());
+        src << "    {\n"
+               "      uint32_t r2 = r, h2 = hroot;\n"
+               "      asm volatile(\"\" : \"+v\"(r2), \"+v\"(h2));\n"
+               "      " << sname << " f;\n"
+               "      f.run(v, o, nwaves, w, r2, active, hflags, h2, gw);\n"
+               "    }\n";
+      }
+      src << "  }\n"
+             "};\n";
+      merged_groups.push_back(gi);
     }
   }
   // Pattern shapes shared by match-record rules (round 5): each distinct (shape, metadata-site base) of the eligible
@@ -1743,6 +1765,15 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
         << ")))\n"
            "kyv_jit_fused_" << sfx << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t nwaves) {\n"
            "  kyv::JitFused" << sfx << " f;\n"
+           "  kyv::walk_fused(*vp, o, nwaves, f);\n"
+           "}\n";
+  }
+  for (size_t gi : merged_groups) {
+    src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu("
+        << (gwpe[gi] == -1 && std::count(gwpe.begin(), gwpe.end(), -2) ? "KYV_JIT_WPE_FUSED_HEAVY" : "KYV_JIT_WPE_FUSED")
+        << ")))\n"
+           "kyv_jit_fusedm_" << gi << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t nwaves) {\n"
+           "  kyv::JitFusedM" << gi << " f;\n"
            "  kyv::walk_fused(*vp, o, nwaves, f);\n"
            "}\n";
   }

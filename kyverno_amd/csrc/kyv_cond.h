@@ -598,19 +598,20 @@ KYV_HD int op_in(const View& v, NodeTab R, const Cond& c, const CV& k, const CV&
   const uint32_t n = k.n;
   int kr = key_list(v, R, k, true);
   if (kr != CR_TRUE) return kr;
-  // setExistsInArray (in.go:104-143)
-  auto found = [&](uint32_t s, const CV* arr, const CondOperand* lst) {
-    if (arr) {
-      for (uint32_t j = 0; j < arr->n; j++) if (cv_elem(v, R, *arr, j).sid == s) return true;
+  // setExistsInArray (in.go:104-143). The value side is x itself or the condition's literal list, chosen by a flag:
+  // a pointer that may point at the caller's CV forces that CV into scratch memory (round 5: 165 scratch
+  // instructions in match_deny_kernel)
+  const bool use_arr = x.t == CT_ARR;
+  auto found = [&](uint32_t s) {
+    if (use_arr) {
+      for (uint32_t j = 0; j < x.n; j++) if (cv_elem(v, R, x, j).sid == s) return true;
       return false;
     }
-    for (uint32_t j = 0; j < lst->nlist; j++) if (v.pool[lst->list + j] == s) return true;
+    for (uint32_t j = 0; j < c.value.nlist; j++) if (v.pool[c.value.list + j] == s) return true;
     return false;
   };
-  const CV* arr = nullptr;
-  if (x.t == CT_ARR) {
+  if (use_arr) {
     for (uint32_t j = 0; j < x.n; j++) if (cv_elem(v, R, x, j).t != CT_STR) return CR_FALSE;  // invalidType
-    arr = &x;
   } else if (x.t == CT_STR) {
     if (n == 1 && key_at(v, R, k, 0) == x.sid) return CR_TRUE;
     if (x.res) return CR_FB;
@@ -619,7 +620,7 @@ KYV_HD int op_in(const View& v, NodeTab R, const Cond& c, const CV& k, const CV&
     return CR_FALSE;
   }
   bool all_in = true;
-  for (uint32_t i = 0; i < n; i++) if (!found(key_at(v, R, k, i), arr, &c.value)) { all_in = false; break; }
+  for (uint32_t i = 0; i < n; i++) if (!found(key_at(v, R, k, i))) { all_in = false; break; }
   return (notin ? !all_in : all_in) ? CR_TRUE : CR_FALSE;
 }
 

@@ -31,6 +31,7 @@
 
 #include "kyv_acct.h"
 #include "kyv_host.h"
+#define KYV_NO_KERNELS 1  // the evaluation kernels are compiled in kyv_prod.hip / kyv_acct.hip (kyv_launch.inc)
 #include "kyv_kernels.h"
 
 namespace kyv {
@@ -185,6 +186,7 @@ struct DevRuleset {
   std::vector<hipFunction_t> jfns;  // kyv_jit_walk_<g> per rule group
   std::vector<hipFunction_t> ffns;  // kyv_jit_fused_<g> per rule group, or null (the group has no fused rule)
   std::vector<std::vector<hipFunction_t>> fparts, afparts;  // its further parts kyv_jit_fused_<g>p<1..> (KYV_FUSED_SPLIT)
+  std::vector<hipFunction_t> fmfns, afmfns;  // kyv_jit_fusedm_<g>: the parts as one kernel (KYV_FUSED_MERGE), or null
   std::vector<hipFunction_t> jconds;  // [rule] kyv_jit_cond_<k> (compiled deny / foreach rule k) or null
   // compiled condition rules in kernel groups (jit_cond_groups): [group] kyv_jit_condg_<first rule>, its members,
   // the accounting build's kernel; [rule] its group or -1
@@ -349,7 +351,12 @@ struct DeviceResults {
   uint32_t* pss_fails = nullptr;
   uint32_t* pss_slot = nullptr;
   FailRec* recs = nullptr;       // compacted records of the current slice
-  uint32_t* nrecs = nullptr;
+  uint32_t* nrecs = nullptr;       // [3]: last slice's records, their offset, the evaluation's total (compact_top_kernel)
+  bool recs_resident = false;       // the last evaluation's failing-path records are all in recs (a rule-sliced
+                                    // evaluation with copy-back gathers them slice by slice into host_recs instead)
+  std::vector<FailRec> host_recs;   // that host copy (export_failures serves it)
+  FailRec* hrecs_dev = nullptr;     // its upload for an export (every slice's records: may exceed max_recs)
+  size_t hrecs_cap = 0;
   FailRec* stage = nullptr;      // per-chunk staging of failing-path records (DevOut), sized for the largest slice
   uint16_t* rcnt = nullptr;
   uint32_t* tsum = nullptr;      // compaction tile sums / offsets
@@ -387,6 +394,7 @@ struct DeviceResults {
 
 static void free_dev_results(DeviceResults& d, int dev) {
   dfree(d.view); dfree(d.status); dfree(d.pss_fails); dfree(d.pss_slot); dfree(d.recs); dfree(d.nrecs); dfree(d.counts);
+  dfree(d.hrecs_dev);
   dfree(d.stage); dfree(d.rcnt); dfree(d.tsum); dfree(d.tseg);
   dfree(d.shape_st); dfree(d.shape_rec); dfree(d.shape_gate); dfree(d.tcfg); dfree(d.facts);
   dfree(d.wl.items); dfree(d.wl.cnt);
@@ -414,6 +422,7 @@ struct DevBatch {
   uint32_t* inv = nullptr;     // input index -> kind-major position, and its inverse: uploaded by the first export
   uint32_t* order = nullptr;   // of device-resident results (export_status / export_failures)
   double upload_ms = 0;
+  double gmask_ms = 0;  // glob-mask kernel of this batch (once per batch and device), HIP events
 };
 
 static DevRuleset* upload_ruleset(const Ruleset& rs, int device) {
@@ -615,10 +624,18 @@ __global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict
   const uint32_t tot = block_exclusive_scan(tsum + base, n);
   if (threadIdx.x == 0) seg[blockIdx.x] = tot;
 }
+// nout[0]: the slice's record count; nout[1]: where its records start in the output (0, or with `accumulate` the
+// records of the evaluation's earlier slices: a rule-sliced evaluation keeps every slice's records resident, one
+// dense list); nout[2]: the running total
 __global__ void __launch_bounds__(1024) compact_top_kernel(uint32_t* __restrict__ seg, uint32_t nseg,
-                                                           uint32_t* __restrict__ nout) {
+                                                           uint32_t* __restrict__ nout, uint32_t accumulate) {
   const uint32_t tot = block_exclusive_scan(seg, nseg);
-  if (threadIdx.x == 0) *nout = tot;
+  if (threadIdx.x == 0) {
+    const uint32_t b = accumulate ? nout[2] : 0u;
+    nout[0] = tot;
+    nout[1] = b;
+    nout[2] = b + tot;
+  }
 }
 // one wave per tile of 64 chunks: every lane copies records i = lane, lane + 64, ... of the tile (the chunk of record
 // i found by a binary search over the wave's inclusive prefix of the chunk counts), so all loads are independent
@@ -626,7 +643,7 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
                                                             const uint16_t* __restrict__ rcnt, const RuleDesc* __restrict__ rules,
                                                             uint32_t nwaves, size_t total, const uint32_t* __restrict__ tbase,
                                                             const uint32_t* __restrict__ seg, FailRec* __restrict__ out,
-                                                            size_t max_out, uint32_t k0) {
+                                                            size_t max_out, uint32_t k0, const uint32_t* __restrict__ nout) {
   const uint32_t lane = threadIdx.x;
   const size_t c = (size_t)blockIdx.x * WAVE + lane;
   const uint32_t n = c < total ? rcnt[c] : 0u;
@@ -651,7 +668,7 @@ __global__ void __launch_bounds__(WAVE) compact_copy_kernel(const FailRec* __res
     sw[lane] = (uint32_t)(c % nwaves);
   }
   __syncthreads();
-  const uint32_t base = tbase[blockIdx.x] + seg[blockIdx.x / SCAN_SEG];
+  const size_t base = (size_t)nout[1] + tbase[blockIdx.x] + seg[blockIdx.x / SCAN_SEG];
   // one record per lane: whole FailRecs of wide chunks copied, StageRecs expanded; stores of consecutive lanes are
   // consecutive 32-byte records
   for (uint32_t i = lane; i < T; i += WAVE) {
@@ -848,6 +865,9 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
         break;
       dr->fparts[g].push_back(f);
     }
+    dr->fmfns.resize(ng, nullptr);
+    if (hipModuleGetFunction(&dr->fmfns[g], dr->jmod, ("kyv_jit_fusedm_" + std::to_string(g)).c_str()) != hipSuccess)
+      dr->fmfns[g] = nullptr;
   }
   (void)hipGetLastError();
   dr->jshapes = nullptr;
@@ -900,6 +920,9 @@ static bool ensure_jit_acct(Ruleset& rs, DevRuleset* dr) {
     for (size_t p = 0; p < dr->afparts[g].size(); p++)
       HIP_OK(hipModuleGetFunction(&dr->afparts[g][p], dr->amod,
                                   ("kyv_jit_fused_" + std::to_string(g) + "p" + std::to_string(p + 1)).c_str()));
+    dr->afmfns.resize(dr->jfns.size(), nullptr);
+    if (g < dr->fmfns.size() && dr->fmfns[g])
+      HIP_OK(hipModuleGetFunction(&dr->afmfns[g], dr->amod, ("kyv_jit_fusedm_" + std::to_string(g)).c_str()));
   }
   dr->aconds.assign(dr->jconds.size(), nullptr);
   for (size_t k = 0; k < dr->jconds.size(); k++)
@@ -1321,7 +1344,8 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
         mw.push_back(q);  // match_rec_kernel (or the generic kernel)
         continue;
       }
-      if (!pss_k || rd.kind != RK_PSS || rd.pre != NONE) { mr.push_back(q); continue; }
+      // (a rule with preconditions too, when they need no JMESPath: evaluated inline, pss_kernel<.., kPre>)
+      if (!pss_k || rd.kind != RK_PSS || (rd.pre != NONE && prog_jmes(rs, rd.pre))) { mr.push_back(q); continue; }
       uint32_t lo = nw, hi = 0;
       for (size_t ri = 0; ri < runs.size(); ri++) {
         if (!((runs[ri].second[q / 32] >> (q % 32)) & 1u)) continue;
@@ -1508,6 +1532,16 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     mr.insert(mr.begin(), mp.begin(), mp.end());
     mr.insert(mr.begin(), md.begin(), md.end());
     mr.insert(mr.begin(), mw.begin(), mw.end());
+    if (getenv("KYV_DEBUG_STATS")) {
+      fprintf(stderr, "[kyvgpu] slice [%u, %u) match lists: %u generic/records, %u deny, %u pre, %u pre-JMESPath, %u light, "
+              "%u JMESPath (interpreted:", sl.k0, sl.k1, sl.nmw, sl.nmd, sl.nmp, sl.nmpj, sl.nm, sl.nmj);
+      for (uint32_t i = 0; i < sl.nmj; i++) {
+        const RuleDesc& rd = rs.rules[mr[sl.nmw + sl.nmd + sl.nmp + sl.nmpj + sl.nm + i]];
+        fprintf(stderr, " %u/k%u%s", mr[sl.nmw + sl.nmd + sl.nmp + sl.nmpj + sl.nm + i], (unsigned)rd.kind,
+                rd.pre != NONE ? "p" : "");
+      }
+      fprintf(stderr, "), %u compiled, %zu pss-kernel\n", sl.nmc, sl.pw.size());
+    }
     dfree(sl.mrules);
     sl.mrules = nullptr;
     HIP_OK(dmalloc(&sl.mrules, std::max<size_t>(1, mr.size()) * 4));
@@ -1562,10 +1596,20 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(hipMemcpy(dv, &tv, sizeof(View), hipMemcpyHostToDevice));
     const uint32_t* gp = (const uint32_t*)(dr->base + dr->o_gpats);
     const uint32_t* gs = (const uint32_t*)(dr->base + dr->o_gsets);
+    hipEvent_t g0, g1;
+    HIP_OK(hipEventCreate(&g0));
+    HIP_OK(hipEventCreate(&g1));
+    HIP_OK(hipEventRecord(g0, 0));
     hipLaunchKernelGGL(gmask_kernel, dim3((unsigned)((nstr + 255) / 256)), dim3(256), 0, 0, (const View*)dv, gp,
                        (uint32_t)rs.gpats.size(), gs, (uint32_t)rs.gsets.size(), (uint32_t)nstr, db->gmask_words, db->gmask);
     HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(g1, 0));
     HIP_OK(hipDeviceSynchronize());
+    float gms = 0;
+    HIP_OK(hipEventElapsedTime(&gms, g0, g1));
+    db->gmask_ms = gms;
+    (void)hipEventDestroy(g0);
+    (void)hipEventDestroy(g1);
     dfree(dv);
   }
   View v = make_view(rs, b, dr->base, dr, db->base, db);
@@ -1580,7 +1624,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     HIP_OK(dmalloc(&d.status, std::max<size_t>(1, nres * nrules)));
     HIP_OK(dmalloc(&d.pss_fails, std::max<size_t>(4, (size_t)d.npss * nres * 4)));
     HIP_OK(dmalloc(&d.pss_slot, std::max<size_t>(4, nrules * 4)));
-    HIP_OK(dmalloc(&d.nrecs, 4));
+    HIP_OK(dmalloc(&d.nrecs, 16));
     HIP_OK(dmalloc(&d.counts, std::max<size_t>(1, nrules) * NSTATUS * 8));
     HIP_OK(hipMemcpy(d.pss_slot, pss_slot.data(), nrules * 4, hipMemcpyHostToDevice));
     stream_get(&d.stream, &d.e0, &d.e1);
@@ -1681,13 +1725,13 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   const bool acct = account;
   uint64_t aphase[5] = {0, 0, 0, 0, 0};
   uint64_t aclass[3] = {0, 0, 0};
-  unsigned long long* acnt_lib = nullptr;
+  unsigned long long *acnt_lib = nullptr, *acnt_lib_j = nullptr;
   bool ajit = false;
   std::vector<unsigned long long> ahost(3 * KYV_ACCT_SLOTS);
   auto acct_take = [&]() -> std::array<uint64_t, 3> {  // counters since the last call, by class; then zeroed
     std::array<uint64_t, 3> c{0, 0, 0};
     HIP_OK(hipStreamSynchronize(stream));
-    for (unsigned long long* dc : {acnt_lib, ajit ? dr->acnt : nullptr}) {
+    for (unsigned long long* dc : {acnt_lib, acnt_lib_j, ajit ? dr->acnt : nullptr}) {
       if (!dc) continue;
       // on the evaluation stream (a non-blocking stream: null-stream copies / memsets would not order with its
       // kernels, and a counter reset could land after the next phase's first adds)
@@ -1703,6 +1747,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   if (acct) {
     n = 1;
     acnt_lib = kyvacct::counters();
+    acnt_lib_j = kyvacct::counters_j();
     ajit = jit && ensure_jit_acct(mrs, dr);
     if (jit && !ajit) throw std::runtime_error("accounting build of the runtime-compiled kernels unavailable");
     acct_take();
@@ -1724,9 +1769,14 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     const double sum_before = phase[0] + phase[1] + phase[2] + phase[3];
     bool joined = false;
     host_recs.clear();
+    d.host_recs.clear();
+    d.recs_resident = !(multi && collect);
     HIP_OK(hipEventRecord(d.e0, stream));  // the resets are part of the evaluation
     HIP_OK(hipMemsetAsync(d.counts, 0, std::max<size_t>(1, nrules) * NSTATUS * 8, stream));
-    HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));  // also when no slice runs (no rules / no resources)
+    HIP_OK(hipMemsetAsync(d.nrecs, 0, 16, stream));  // also when no slice runs (no rules / no resources)
+    // rule slices append to one resident record list, except when copy-back gathers each slice's records on the host
+    // (then each slice starts at 0: the buffer holds one slice's worst case)
+    const uint32_t accumulate = multi && !collect ? 1u : 0u;
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     if (acct) aphase[0] += (uint64_t)nres * nrules + (uint64_t)d.npss * nres * 4;  // verdict / PSS-mask resets
@@ -1746,65 +1796,46 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       if (!d.facts) HIP_OK(dmalloc(&d.facts, nres * sizeof(ResFacts)));
       const dim3 fg((unsigned)((nres + 255) / 256));
       const bool mw1 = v.gmask_words <= 1;
-      if (acct) kyvacct::facts(mw1, fg.x, stream, d.view, d.tcfg, d.facts);
-      else hipLaunchKernelGGL(mw1 ? facts_kernel<1> : facts_kernel<4>, fg, dim3(256), 0, stream, (const View*)d.view,
-                              (const TailCfg*)d.tcfg, d.facts);
+      (acct ? kyvacct::facts : kyvprod::facts)(mw1, fg.x, stream, d.view, d.tcfg, d.facts);
     }
     for (auto& sl : d.slices) {
       if (!nres || sl.k1 == sl.k0) continue;
       const size_t nsr = sl.k1 - sl.k0;
       DevOut o{d.status, d.pss_fails, d.pss_slot, d.stage, sl.rbase, d.rcnt, sl.k0, sl.k1};
       HIP_OK(hipEventRecord(sl.evs, stream));
-      HIP_OK(hipMemsetAsync(d.nrecs, 0, 4, stream));
       HIP_OK(hipMemsetAsync(d.rcnt, 0, std::max<size_t>(nsr * (size_t)d.wl.nwaves, 1) * 2, stream));
       // match_rec_kernel and the generic kernel: 4 waves/SIMD by default (114 / 86 VGPRs, no scratch); KYV_MATCHW_WPE 5 / 6 / 8
       static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
       if (sl.nmr) {
         const bool mw1 = v.gmask_words <= 1;
-        auto kf = mwpe == 8 ? (mw1 ? match_rec_kernel<8, 1> : match_rec_kernel<8, 4>)
-                : mwpe == 6 ? (mw1 ? match_rec_kernel<6, 1> : match_rec_kernel<6, 4>)
-                : mwpe == 4 ? (mw1 ? match_rec_kernel<4, 1> : match_rec_kernel<4, 4>)
-                            : (mw1 ? match_rec_kernel<5, 1> : match_rec_kernel<5, 4>);
         const MRecIndex ix{sl.mcls, sl.mcrec};
         const ShapeTab sh{d.shape_st, d.shape_rec, d.wl.nwaves, d.nshapes};
         const TailTab tt{(const TailCfg*)sl.tails, (const TailProg*)(sl.tails + sizeof(TailCfg))};
         const ResFacts* fp = use_facts ? d.facts : nullptr;
-        if (acct) kyvacct::match_rec(mwpe, mw1, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr, &ix, &sh, &tt, fp);
-        else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const MRec*)sl.mrec,
-                                sl.nmr, ix, sh, tt, fp);
+        (acct ? kyvacct::match_rec : kyvprod::match_rec)(mwpe, mw1, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr,
+                                                         &ix, &sh, &tt, fp);
       }
       if (sl.nmw) {
-        auto kf = mwpe == 8 ? match_walk_generic_kernel<8> : mwpe == 6 ? match_walk_generic_kernel<6>
-                                                                         : match_walk_generic_kernel<4>;
-        if (acct) kyvacct::match_walk_generic(mwpe, grid.x, stream, d.view, &o, &d.wl, sl.mrules, sl.nmw);
-        else hipLaunchKernelGGL(kf, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl, (const uint32_t*)sl.mrules,
-                                sl.nmw);
+        (acct ? kyvacct::match_walk_generic : kyvprod::match_walk_generic)(mwpe, grid.x, stream, d.view, &o, &d.wl,
+                                                                           sl.mrules, sl.nmw);
       }
       if (sl.nmd) {
-        if (acct) kyvacct::match_deny(grid.x, stream, d.view, &o, sl.mrules + sl.nmw, sl.nmd);
-        else hipLaunchKernelGGL(match_deny_kernel, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o,
-                                (const uint32_t*)sl.mrules + sl.nmw, sl.nmd);
+        (acct ? kyvacct::match_deny : kyvprod::match_deny)(grid.x, stream, d.view, &o, sl.mrules + sl.nmw, sl.nmd);
       }
       if (sl.nmp) {
-        if (acct) kyvacct::match_pre(grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw + sl.nmd, sl.nmp);
-        else hipLaunchKernelGGL(match_pre_kernel<KYV_MATCH_WPE>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
-                                (const uint32_t*)sl.mrules + sl.nmw + sl.nmd, sl.nmp);
+        (acct ? kyvacct::match_pre : kyvprod::match_pre)(grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw + sl.nmd,
+                                                         sl.nmp);
       }
       if (sl.nmpj) {
-        if (acct) kyvacct::match_pre_j(grid.x, stream, d.view, &o, &d.wl, sl.mrules + sl.nmw + sl.nmd + sl.nmp, sl.nmpj);
-        else hipLaunchKernelGGL((match_pre_kernel<KYV_MATCH_WPE, true>), grid, dim3(BLOCK), 0, stream, (const View*)d.view, o,
-                                d.wl, (const uint32_t*)sl.mrules + sl.nmw + sl.nmd + sl.nmp, sl.nmpj);
+        (acct ? kyvacct::match_pre_j : kyvprod::match_pre_j)(grid.x, stream, d.view, &o, &d.wl,
+                                                             sl.mrules + sl.nmw + sl.nmd + sl.nmp, sl.nmpj);
       }
       const uint32_t ml0 = sl.nmw + sl.nmd + sl.nmp + sl.nmpj;
       if (sl.nm) {
-        if (acct) kyvacct::match(false, grid.x, stream, d.view, &o, &d.wl, sl.mrules + ml0, sl.nm);
-        else hipLaunchKernelGGL(match_kernel<false>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
-                                (const uint32_t*)sl.mrules + ml0, sl.nm);
+        (acct ? kyvacct::match : kyvprod::match)(grid.x, stream, d.view, &o, &d.wl, sl.mrules + ml0, sl.nm);
       }
       if (sl.nmj) {
-        if (acct) kyvacct::match(true, grid.x, stream, d.view, &o, &d.wl, sl.mrules + ml0 + sl.nm, sl.nmj);
-        else hipLaunchKernelGGL(match_kernel<true>, grid, dim3(BLOCK), 0, stream, (const View*)d.view, o, d.wl,
-                                (const uint32_t*)sl.mrules + ml0 + sl.nm, sl.nmj);
+        (acct ? kyvacct::match_j : kyvprod::match_j)(grid.x, stream, d.view, &o, &d.wl, sl.mrules + ml0 + sl.nm, sl.nmj);
       }
       {
         // C2 (round 3, map walk inlined): 4 0.586, 6 0.587, 8 0.514 ms; round 4: the column-only kernel with the
@@ -1812,13 +1843,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         static const int pwpe = getenv("KYV_PSS_WPE") ? atoi(getenv("KYV_PSS_WPE")) : 8;
         for (const uint3& c : sl.pw) {
           const bool ex = (rs.rules[c.x].flags & RD_GATE_EXACT) && rs.rules[c.x].match.mode != MM_NONE;
-          auto kf = ex ? (pwpe == 4 ? pss_kernel<true, 4> : pwpe == 6 ? pss_kernel<true, 6> : pss_kernel<true, 8>)
-                       : (pwpe == 4 ? pss_kernel<false, 4> : pwpe == 6 ? pss_kernel<false, 6> : pss_kernel<false, 8>);
-          if (acct) kyvacct::pss(ex, pwpe, c.z, stream, d.view, &o, c.x, c.y);
-          else hipLaunchKernelGGL(kf, dim3(c.z), dim3(BLOCK), 0, stream, (const View*)d.view, o, c.x, c.y);
+          const bool pre = rs.rules[c.x].pre != NONE;
+          (acct ? kyvacct::pss : kyvprod::pss)(ex, pre, pwpe, c.z, stream, d.view, &o, c.x, c.y);
           // the pairs it marked ST_PSS_MAP (exclusions, no path columns): the map walk
-          if (acct) kyvacct::pss_map(c.z, stream, d.view, &o, c.x, c.y);
-          else hipLaunchKernelGGL(pss_map_kernel, dim3(c.z), dim3(BLOCK), 0, stream, (const View*)d.view, o, c.x, c.y);
+          (acct ? kyvacct::pss_map : kyvprod::pss_map)(c.z, stream, d.view, &o, c.x, c.y);
         }
       }
       HIP_OK(hipGetLastError());
@@ -1850,9 +1878,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       }
       HIP_OK(hipEventRecord(sl.ev[1], stream));
       if (sl.grid[0]) {
-        if (acct) kyvacct::walk(sl.grid[0], lds, stream, d.view, &o, &d.wl, &sl.cm[0], depth);
-        else hipLaunchKernelGGL(walk_kernel, dim3(sl.grid[0]), dim3(BLOCK), lds, stream, (const View*)d.view, o, d.wl,
-                                sl.cm[0], depth);
+        (acct ? kyvacct::walk : kyvprod::walk)(sl.grid[0], lds, stream, d.view, &o, &d.wl, &sl.cm[0], depth);
         HIP_OK(hipGetLastError());
       }
       bool wforked = false;
@@ -1879,6 +1905,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         const View* vp = d.view;
         uint32_t nw = d.wl.nwaves;
         void* args[] = {(void*)&vp, (void*)&o, (void*)&nw};
+        if (g < dr->fmfns.size() && dr->fmfns[g]) {  // the parts as one kernel (KYV_FUSED_MERGE)
+          HIP_OK(hipModuleLaunchKernel(acct ? dr->afmfns[g] : dr->fmfns[g], nw, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
+          continue;
+        }
         HIP_OK(hipModuleLaunchKernel(acct ? dr->affns[g] : dr->ffns[g], nw, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
         if (g < dr->fparts.size())
           for (size_t p = 0; p < dr->fparts[g].size(); p++)
@@ -1898,9 +1928,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       hipLaunchKernelGGL(compact_sum_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.rcnt, nchunks, d.tsum);
       const uint32_t nseg = (ntiles + SCAN_SEG - 1) / SCAN_SEG;
       hipLaunchKernelGGL(compact_scan_kernel, dim3(std::max<uint32_t>(nseg, 1)), dim3(1024), 0, stream, d.tsum, ntiles, d.tseg);
-      hipLaunchKernelGGL(compact_top_kernel, dim3(1), dim3(1024), 0, stream, d.tseg, std::max<uint32_t>(nseg, 1), d.nrecs);
+      hipLaunchKernelGGL(compact_top_kernel, dim3(1), dim3(1024), 0, stream, d.tseg, std::max<uint32_t>(nseg, 1), d.nrecs,
+                         accumulate);
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, sl.rbase, d.rcnt, drules,
-                         d.wl.nwaves, nchunks, d.tsum, d.tseg, d.recs, d.max_recs, sl.k0);
+                         d.wl.nwaves, nchunks, d.tsum, d.tseg, d.recs, d.max_recs, sl.k0, (const uint32_t*)d.nrecs);
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(sl.ev[3], stream));
       if (acct) {  // compaction: chunk counts (read twice), tile sums, the staged records read, the dense records written
@@ -1910,7 +1941,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         aphase[3] += 4ull * nchunks + 12ull * ntiles + staged + (uint64_t)nr * sizeof(FailRec);
       }
       // (no host synchronisation between slices: every slice has its own events, read after the evaluation)
-      if (collect && multi) {  // gather this slice's records before the next slice reuses the buffers
+      if (collect && multi) {  // gather this slice's records before the next slice reuses the buffers (offset 0)
         uint32_t nr = 0;
         HIP_OK(hipMemcpyAsync(&nr, d.nrecs, 4, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
@@ -1961,6 +1992,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     for (auto& sl : d.slices) cond |= sl.nmc != 0;
     out->jit_used = (jit ? 1 : 0) | (jit && cond ? 2 : 0) | (jit && d.nshapes ? 4 : 0);
     out->h2d_ms = db->upload_ms;
+    out->gmask_ms = db->gmask_ms;
     if (acct) {
       out->alg_bytes = 0;
       for (int q = 0; q < 5; q++) { out->alg_bytes_phase[q] = aphase[q]; out->alg_bytes += aphase[q]; }
@@ -1988,6 +2020,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       out->pss_fails.resize((size_t)d.npss * nres);
       if (d.npss) HIP_OK(hipMemcpy(out->pss_fails.data(), d.pss_fails, out->pss_fails.size() * 4, hipMemcpyDeviceToHost));
       if (multi) {
+        d.host_recs = host_recs;  // export_failures serves the rows of this evaluation from the host copy
         out->fails.swap(host_recs);
       } else {
         uint32_t nr = 0;
@@ -2499,22 +2532,114 @@ int64_t copy_status(const Batch& b, int device, size_t res0, size_t n, uint8_t* 
   return (int64_t)total;
 }
 
+// The last evaluation's failing-path records: device-resident (one dense list, every rule slice appended), or for a
+// rule-sliced evaluation with copy-back the host copy its slices were gathered into (uploaded for the export)
+static const FailRec* failure_records(const Batch& b, int device, uint32_t* n, void* stream) {
+  DevBatch* db = resident(b, device);
+  DeviceResults& d = *db->out;
+  if (!d.recs_resident) {
+    if (d.host_recs.size() > 0xFFFFFFFFull) throw std::runtime_error("too many failing-path records for one export");
+    *n = (uint32_t)d.host_recs.size();
+    if (*n > d.hrecs_cap) {
+      dfree(d.hrecs_dev);
+      d.hrecs_dev = nullptr;
+      d.hrecs_cap = 0;
+      HIP_OK(dmalloc(&d.hrecs_dev, (size_t)*n * sizeof(FailRec)));
+      d.hrecs_cap = *n;
+    }
+    if (*n) HIP_OK(hipMemcpyAsync(d.hrecs_dev, d.host_recs.data(), (size_t)*n * sizeof(FailRec), hipMemcpyHostToDevice,
+                                  (hipStream_t)stream));
+    return (const FailRec*)d.hrecs_dev;
+  }
+  uint32_t c[3] = {0, 0, 0};
+  HIP_OK(hipMemcpy(c, d.nrecs, 12, hipMemcpyDeviceToHost));
+  if (c[2] > d.max_recs)
+    throw std::runtime_error("the evaluation's failing-path records exceed the resident record buffer (" +
+                             std::to_string(c[2]) + " > " + std::to_string(d.max_recs) +
+                             "): evaluate with copy-back to gather them slice by slice");
+  *n = c[2];
+  return (const FailRec*)d.recs;
+}
+
 int64_t export_failures(const Batch& b, int device, int64_t off, int64_t* dst, size_t cap_rows, void* stream) {
   DevBatch* db = resident(b, device);
-  const DeviceResults& d = *db->out;
-  if (d.slices.size() > 1)
-    throw std::runtime_error("failing-path records of a rule-sliced evaluation are gathered on the host, not resident");
   uint32_t nr = 0;
-  HIP_OK(hipMemcpy(&nr, d.nrecs, 4, hipMemcpyDeviceToHost));
-  if (nr > d.max_recs) throw std::runtime_error("failure record buffer overflow");
-  if (!dst) return nr;
+  if (!dst) {  // the count only (no upload of a host copy)
+    const DeviceResults& d = *db->out;
+    if (!d.recs_resident) return (int64_t)d.host_recs.size();
+    failure_records(b, device, &nr, stream);
+    return nr;
+  }
+  const FailRec* recs = failure_records(b, device, &nr, stream);
   if (cap_rows < nr) throw std::runtime_error("export buffer too small");
   if (nr) {
     hipLaunchKernelGGL(failure_rows_kernel, dim3((nr + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                       (const FailRec*)d.recs, nr, (const uint32_t*)db->order, (long long)off, (long long*)dst);
+                       recs, nr, (const uint32_t*)db->order, (long long)off, (long long*)dst);
     HIP_OK(hipGetLastError());
   }
   return nr;
+}
+
+// The same rows packed to 16 bytes for the report gather to one consumer rank (kyv_comm_gather_report): per record
+// uint32 {input-order resource index on this rank, rule | alternative << 24, path template, four 8-bit path indices};
+// a record whose rule, alternative or indices do not fit (rule >= 2^24, alternative >= 128, an index >= 255 other
+// than the 0xFFFF "unused" value) sets bit 31 of word 1 and carries the index of a 16-byte side entry {rule,
+// alternative, indices as 16-bit values} in word 3 instead (the side list's order is not deterministic; the index
+// ties each entry to its row)
+__global__ void __launch_bounds__(256) report_rows_kernel(const FailRec* __restrict__ recs, uint32_t n,
+                                                          const uint32_t* __restrict__ order, uint4* __restrict__ rows,
+                                                          uint4* __restrict__ wide, uint32_t* __restrict__ nwide,
+                                                          uint32_t cap_wide) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const FailRec f = recs[i];
+  bool fit = f.rule < (1u << 24) && f.alt < 128;
+  uint32_t packed = 0;
+  for (int q = 0; q < MAX_IDX; q++) {
+    const uint32_t x = f.idx[q];
+    fit = fit && (x < 255 || x == 0xFFFF);
+    packed |= (x == 0xFFFF ? 255u : (x & 255u)) << (8 * q);
+  }
+  uint4 r;
+  r.x = order[f.res];
+  r.z = f.tmpl;
+  if (fit) {
+    r.y = f.rule | ((uint32_t)f.alt << 24);
+    r.w = packed;
+  } else {
+    const uint32_t j = atomicAdd(nwide, 1u);
+    r.y = 0x80000000u;
+    r.w = j;
+    if (j < cap_wide)
+      wide[j] = make_uint4(f.rule, f.alt, (uint32_t)f.idx[0] | ((uint32_t)f.idx[1] << 16),
+                           (uint32_t)f.idx[2] | ((uint32_t)f.idx[3] << 16));
+  }
+  rows[i] = r;
+}
+
+int64_t export_report_rows(const Batch& b, int device, uint32_t* rows, uint32_t* wide, uint32_t* nwide_dev,
+                           size_t cap_rows, size_t cap_wide, void* stream) {
+  DevBatch* db = resident(b, device);
+  uint32_t nr = 0;
+  const FailRec* recs = failure_records(b, device, &nr, stream);
+  if (!rows) return nr;
+  if (cap_rows < nr) throw std::runtime_error("export buffer too small");
+  HIP_OK(hipMemsetAsync(nwide_dev, 0, 4, (hipStream_t)stream));
+  if (nr) {
+    hipLaunchKernelGGL(report_rows_kernel, dim3((nr + 255) / 256), dim3(256), 0, (hipStream_t)stream, recs, nr,
+                       (const uint32_t*)db->order, (uint4*)rows, (uint4*)wide, nwide_dev, (uint32_t)cap_wide);
+    HIP_OK(hipGetLastError());
+  }
+  return nr;
+}
+
+// the per-rule verdict tallies of the last evaluation, device-resident ([rules][NSTATUS] uint64, ST_NONE not
+// tallied: the caller derives it from the resource count)
+const unsigned long long* device_counts(const Batch& b, int device, size_t* nrules, size_t* nres) {
+  DevBatch* db = resident(b, device);
+  *nrules = db->out->nrules;
+  *nres = db->out->nres;
+  return (const unsigned long long*)db->out->counts;
 }
 
 void free_device_images(Ruleset& rs, Batch* b) {

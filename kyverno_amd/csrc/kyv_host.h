@@ -193,6 +193,7 @@ struct Results {
   int64_t counts[NSTATUS] = {0};
   std::vector<int64_t> rule_counts;  // [rule][status] (report summaries)
   double kernel_ms = 0, h2d_ms = 0, d2h_ms = 0;
+  double gmask_ms = 0;  // per-batch device work outside the evaluation: the glob-mask kernel (h2d_ms: the image upload)
   // GPU evaluation split by phase (HIP events on the evaluation stream, averaged over the timed launches):
   // [0] verdict resets + match_kernel(s), [1] compiled condition kernel, [2] pattern walk kernels,
   // [3] failing-path compaction, [4] verdict histogram

@@ -66,6 +66,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_
 // pair_match, then the preconditions and deny programs of validateDeny (validation.go:281-288, 437-464), without
 // the PodSecurity call and work-list code of match_kernel's dispatch, whose call frame and register need spilled the
 // rule loop (C5 round 4: match_kernel<false> 4.47 ms, 5.3 GB of scratch writes per evaluation)
+#ifndef KYV_NO_KERNELS  // (kyv_engine.hip launches the kernels through kyv_launch.inc)
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_MATCH_WPE)))
 match_deny_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restrict__ mrules, uint32_t nm) {
   const View& v = *vp;
@@ -102,6 +103,7 @@ match_deny_kernel(const View* __restrict__ vp, DevOut o, const uint32_t* __restr
     if (st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
   }
 }
+#endif
 
 // Staged match records of match_rec_kernel. Every wave runs a rule loop, so a rule's match program read from the rule
 // descriptors was a chain of dependent uniform loads (rule list -> RuleDesc -> Filter -> KindDesc / pattern sids ->
@@ -901,8 +903,10 @@ match_pre_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const uint
 // walk (eval_pss) is a call whose frame and spills would otherwise sit in this kernel's scratch and write traffic
 // (round 3 C2 profile: 13x write amplification). kExact: the rule's match block is its kind gate (RD_GATE_EXACT), no
 // match program compiled in; kWpe: occupancy target (KYV_PSS_WPE = 4 / 6 / 8 at run time; 8 by default: 41 VGPRs, no
-// scratch)
-template <bool kExact, int kWpe>
+// scratch). kPre (round 5): the rule has preconditions without JMESPath operands, evaluated inline first
+// (checkPreconditions, validation.go:281-288) -- C5's PodSecurity rules behind preconditions ran in match_kernel<false>
+// with eval_pss as a call (its frame in scratch memory)
+template <bool kExact, int kWpe, bool kPre = false>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(kWpe)))
 pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
   // the wave's containers, one per lane (lists of all 64 pods concatenated): per list the pods' counts, exclusive
@@ -924,6 +928,19 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
     m = rd.kind == RK_PSS;  // pair_match of a kind-gate rule: matched (a fallback rule never gets here)
   } else {
     m = gated && pair_match(v, r, rd, &st);
+  }
+  if constexpr (kPre) {
+    if (gated && m) {  // the precondition program first; only a true outcome reaches the PodSecurity checks
+      uint32_t ec, es, eg;
+      KYV_ACCT_ADD(0, 4);  // header: root
+      const int c = eval_prog_inl<false>(v, NodeTab{v.nodes + v.hdr[r].root}, rd.pre, &ec, &es, &eg, NONE, r);
+      if (c != CR_TRUE) {
+        m = false;
+        st = c == CR_FB ? (uint8_t)(KYV_WHY(FBW_COND), ST_FALLBACK)
+           : c == CR_PANIC ? (uint8_t)ST_PANIC
+           : c == CP_ERROR ? (uint8_t)(ST_ERROR | ST_MARK_PRE) : (uint8_t)(ST_SKIP | ST_MARK_PRE);
+      }
+    }
   }
   const uint32_t* T = nullptr;
   uint32_t hroot = 0;
@@ -992,6 +1009,7 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
 
 // The PodSecurity pairs pss_kernel marked ST_PSS_MAP (same grid): the map walk with the typed pod view, exclusion
 // sub-pods included (eval_pss, validation.go:535-566 + pkg/pss/evaluate.go:83-108)
+#ifndef KYV_NO_KERNELS
 __global__ void __launch_bounds__(BLOCK) pss_map_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
   const View& v = *vp;
   const uint32_t r = (w0 + blockIdx.x) * BLOCK + threadIdx.x;
@@ -1007,15 +1025,18 @@ __global__ void __launch_bounds__(BLOCK) pss_map_kernel(const View* __restrict__
   if (ps != NONE && pf) o.pss_fails[(size_t)ps * v.nres + r] = pf;
   KYV_ACCT_ADD(1, 1 + ((ps != NONE && pf) ? 4 : 0));
 }
+#endif
 
 // Phase 2 (pattern_eval): each wave takes chunks of 64 work items of ONE rule (grid-stride over all rules'
 // chunks), so every lane walks the same compiled pattern over a different resource with the wave-uniform
 // walker; verdict bytes as in phase 1, failing-path records staged in the chunk's own slots.
+#ifndef KYV_NO_KERNELS
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(KYV_WPE)))
 walk_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, ChunkMap cm, int depth) {
   extern __shared__ uint4 lds_raw[];  // [depth] UFrame, then [depth][BLOCK] LaneFrame
   WaveWalker wk{(LaneFrame*)((UFrame*)lds_raw + depth), (UFrame*)lds_raw, depth, false};
   walk_chunks(*vp, o, wl, cm, wk);
 }
+#endif
 
 }  // namespace kyv

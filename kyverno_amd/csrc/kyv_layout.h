@@ -223,6 +223,7 @@ constexpr uint32_t COL_INDEX_MASK = (1u << COL_TYPE_SHIFT) - 1;
 // holds its slot in the entry's dynamic-value list, resolved per element before the walk (vars.go:352-431 substitutes
 // a whole-string variable by its typed value)
 enum LeafType : uint8_t { L_NIL = 0, L_BOOL = 1, L_FLOAT = 2, L_STR = 3, L_MAP = 4, L_ARR = 5, L_DYN = 6 };
+constexpr uint32_t FOREACH_MAX_NEST = 3;  // nested foreach levels below the top the device evaluates (deeper -> CPU)
 constexpr uint32_t MAX_DYN = 4;  // element variables per foreach pattern entry (more -> CPU fallback)
 struct Leaf {           // 32 bytes
   uint8_t type;

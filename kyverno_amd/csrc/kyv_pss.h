@@ -913,11 +913,11 @@ KYV_HD bool fe_dyn_value(const View& v, NodeTab R, const uint32_t* d, uint32_t e
   return true;
 }
 
-// one entry list at nesting level D (levels beyond the compiled maximum never occur: the compiler keeps them on the
-// CPU engine)
+// one entry list at nesting level D (levels beyond FOREACH_MAX_NEST never occur: the compiler keeps them on the CPU
+// engine; each level is its own instantiation, so only kernels with nested rules carry the deeper levels)
 template <int D>
 KYV_HD uint8_t foreach_level(const View& v, NodeTab R, const RuleDesc& rd, uint32_t entries, FeCtx up, uint32_t row) {
-  if constexpr (D > 1) {
+  if constexpr (D > (int)FOREACH_MAX_NEST) {
     return KYV_WHY(FBW_COND), ST_FALLBACK;
   } else {
     const uint32_t nent = v.pool[entries];

@@ -127,6 +127,9 @@ class Results:
         L = K.lib()
         self.counts = {K.STATUS_NAMES[s]: L.kyv_results_count(h, s) for s in range(8)}
         self.kernel_ms = L.kyv_results_kernel_ms(h)
+        # per-batch device work before the batch's first evaluation: image upload and glob-mask kernel (ms)
+        self.upload_ms = L.kyv_results_batch_ms(h, 0)
+        self.gmask_ms = L.kyv_results_batch_ms(h, 1)
         ph = (ctypes.c_double * 5)()
         L.kyv_results_phase_ms(h, ph, 5)
         # match (incl. verdict resets), cond (compiled condition kernel), walk, compact, hist -- ms per launch

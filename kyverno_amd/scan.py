@@ -366,6 +366,30 @@ class Comm:
                 "failure_rows_per_rank_max": int(st.failure_rows_per_rank_max),
                 "failure_rows_total": int(st.failure_rows_total)}
 
+    def gather_report(self, batch, res_offset=0, root=0):
+        """report assembly to one consumer rank (kyv_comm_gather_report): every rank's packed verdicts and its
+        failing-path rows (16 B each on the wire) sent to `root` at exact sizes; status_of / failures_of then work on
+        the root only"""
+        import ctypes
+        st = K.GatherStats()
+        K.check(K.lib().kyv_comm_gather_report(self._h, batch.h, int(res_offset), int(root), ctypes.byref(st)))
+        return {"status_ms": st.status_ms, "failures_ms": st.failures_ms,
+                "status_bytes_per_rank": int(st.status_bytes_per_rank),
+                "failure_rows_per_rank_max": int(st.failure_rows_per_rank_max),
+                "failure_rows_total": int(st.failure_rows_total)}
+
+    def reduce_counts(self, batch):
+        """cluster-wide per-rule verdict tallies of the batch's last evaluation (kyv_comm_reduce_counts: one
+        ncclAllReduce of the device-resident tallies): int64 [rules, 8]; a collective, every rank calls it"""
+        L = K.lib()
+        n = L.kyv_comm_reduce_counts(self._h, batch.h, None, 0)
+        if n < 0:
+            raise K.KyvError(L.kyv_last_error().decode())
+        out = np.zeros(n, dtype=np.int64)
+        if L.kyv_comm_reduce_counts(self._h, batch.h, out.ctypes.data, n) != n:
+            raise K.KyvError(L.kyv_last_error().decode())
+        return out.reshape(-1, 8)
+
     def status_of(self, q):
         """rank q's packed verdicts from the last gather (kyv_batch_export_status layout, padded)"""
         L = K.lib()

@@ -380,7 +380,8 @@ def c5_policies(n=50, seed=SEED):
     variables. About 60% use only `{{ request.object.<path> }}` operands with the condition operators (the
     device-compilable subset: Equals / NotEquals / In / AnyIn / AllIn / NotIn / AnyNotIn / AllNotIn / numeric,
     old-list and any/all forms, literal ranges, JSON-string lists, quantities, durations, message variables);
-    the rest use JMESPath projections, functions, `||` defaults or other context variables (CPU fallback)."""
+    the rest use JMESPath projections, length(), `||` defaults or request.operation (device-compiled too), and
+    regex_match / to_upper, which stay outside the device subset (their pairs are CPU fallback, counted)."""
     r = random.Random(seed ^ 0xC5)
     pod = {"any": [{"resources": {"kinds": ["Pod"]}}]}
     wl = {"any": [{"resources": {"kinds": ["Deployment", "StatefulSet"]}}]}
@@ -427,6 +428,12 @@ def c5_policies(n=50, seed=SEED):
         lambda: ("deny", pod, {"any": [c("{{ length(request.object.spec.containers) }}", "GreaterThan", 2)]}, None, "many"),
         lambda: ("deny", pod, {"any": [c("{{ request.object.metadata.labels.app || '' }}", "Equals", "")]}, None, "app"),
         lambda: ("pattern", pod, None, {"any": [c("{{ request.operation }}", "Equals", "CREATE")]}, "owner"),
+        # outside the device subset (JMESPath functions other than keys / length): the rule's pairs are handed to the
+        # CPU engine (ST_FALLBACK, counted in the bench line's cpu_fallback_pairs_per_step and never timed as device work)
+        lambda: ("deny", pod, {"any": [c("{{ regex_match('^team-[0-9]+$', request.object.metadata.labels.owner || '') }}",
+                                         "Equals", False)]}, None, "owner format"),
+        lambda: ("deny", pod, {"any": [c("{{ to_upper(request.object.metadata.labels.tier || '') }}", "Equals", "DATA")]},
+                 None, "tier case"),
     ]
     out = []
     for i in range(n):

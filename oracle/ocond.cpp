@@ -718,38 +718,51 @@ static VP substitute(const VP& v, const VarCtx& cx, const std::string& path, Sub
   return v;
 }
 
-std::string render_message(const std::string& msg, const VP& resource, bool* unpinned) {
-  *unpinned = false;
-  if (!has_var_syntax(msg)) return msg;
-  if (msg.find("$(") != std::string::npos || msg.find("\\{{") != std::string::npos) { *unpinned = true; return msg; }
-  // whole message is one variable: the typed value
+// SubstituteAll of a message's `{{ request.object... }}` references (vars.go): 0 the text in *out; 1 a reference does
+// not resolve (NotFoundError); 2 the whole message is one reference whose value is not a string; 3 outside the
+// restated subset ($() references, escapes, other variables, nested variables in a value)
+int substitute_message(const std::string& msg, const VP& resource, std::string* out) {
+  if (!has_var_syntax(msg)) return *out = msg, 0;
+  if (msg.find("$(") != std::string::npos || msg.find("\\{{") != std::string::npos) return 3;
   std::vector<std::string> segs;
-  if (parse_object_var(msg, segs)) {
+  if (parse_object_var(msg, segs)) {  // whole message is one variable: the typed value
     std::string missing;
     VP r = resolve(segs, resource, &missing);
-    if (!r) return msg;
-    if (r->t == T::Str) return r->s;
-    return "the produced message didn't resolve to a string, check your policy definition.";
+    if (!r) return 1;
+    if (r->t == T::Str) return *out = r->s, 0;
+    return 2;
   }
-  std::string out;
+  std::string o;
   size_t i = 0;
   while (i < msg.size()) {
     size_t a = msg.find("{{", i);
-    if (a == std::string::npos) { out += msg.substr(i); break; }
+    if (a == std::string::npos) { o += msg.substr(i); break; }
     size_t b = msg.find("}}", a + 2);
-    if (b == std::string::npos) { *unpinned = true; return msg; }
+    if (b == std::string::npos) return 3;
     std::string var = msg.substr(a, b + 2 - a);
-    if (!parse_object_var(var, segs)) { *unpinned = true; return msg; }
+    if (!parse_object_var(var, segs)) return 3;
     std::string missing;
     VP r = resolve(segs, resource, &missing);
-    if (!r) return msg;  // substitution error -> the raw message
-    out += msg.substr(i, a - i);
+    if (!r) return 1;
+    o += msg.substr(i, a - i);
     std::string sub = r->t == T::Str ? r->s : oj::dump(r);
-    if (sub.find("{{") != std::string::npos) { *unpinned = true; return msg; }  // nested variables re-scanned
-    out += sub;
+    if (sub.find("{{") != std::string::npos) return 3;  // nested variables are re-scanned
+    o += sub;
     i = b + 2;
   }
-  return out;
+  return *out = o, 0;
+}
+
+// getDenyMessage (validation.go:461-479): a substitution error leaves the message as written
+std::string render_message(const std::string& msg, const VP& resource, bool* unpinned) {
+  *unpinned = false;
+  std::string o;
+  switch (substitute_message(msg, resource, &o)) {
+    case 0: return o;
+    case 1: return msg;
+    case 2: return "the produced message didn't resolve to a string, check your policy definition.";
+    default: *unpinned = true; return msg;
+  }
 }
 
 static bool valid_op_exact(const std::string& op) {  // kyvernov1.ConditionOperators values (common_types.go:225-244)

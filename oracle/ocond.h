@@ -47,6 +47,7 @@ bool conditions_supported_element(const oj::VP& conditions);
 // getDenyMessage's SubstituteAll(msg) (validation.go:466-479) for messages whose variables are request.object
 // references; *unpinned when the message uses anything else (other variables, references, escapes).
 std::string render_message(const std::string& msg, const oj::VP& resource, bool* unpinned);
+int substitute_message(const std::string& msg, const oj::VP& resource, std::string* out);
 
 // true when every string in `conditions` is either variable-free or exactly one supported request.object
 // reference (the device subset); false -> the rule is CPU fallback

@@ -722,10 +722,11 @@ static bool foreach_pattern_ok(const VP& p) {
 
 // foreach entries the restatement covers: a JMESPath-subset list (over request.object, and over the enclosing
 // element inside a nested foreach), per-element preconditions / elementScope, and one of deny conditions, pattern,
-// anyPattern (element variables as whole-string values) or a nested foreach (one level); context entries and other
+// anyPattern (element variables as whole-string values) or a nested foreach (three levels below the top: the
+// recursion itself has no limit, deeper rules are just not run on the device); context entries and other
 // variables are not restated
 static bool foreach_entries_supported(const VP& fe, int depth) {
-  if (!fe || fe->t != T::Arr || depth > 1) return false;
+  if (!fe || fe->t != T::Arr || depth > 3) return false;  // (the device's FOREACH_MAX_NEST: deeper is not exercised)
   for (auto& e : fe->a) {
     if (!e || e->t != T::Obj) return false;
     for (auto& kv : e->o)
@@ -1047,10 +1048,14 @@ static RuleResult validate_rule_body(const VP& rule, const VP& resource) {
       out.nondeterministic |= fl.nondeterministic;
       if (pr.ok) { out.status = "pass"; out.message = "validation rule '" + out.name + "' passed."; return out; }
       if (pr.skip) { out.status = "skip"; out.message = pr.err; return out; }
-      if (pr.path.empty()) { out.status = "error"; out.message = build_error_message(out.name, msg, pr.err, ""); return out; }
+      // buildErrorMessage substitutes the message (validation.go:731-745); its substitution-error text embeds the Go
+      // error string of the pattern failure and a non-string whole-message value panics: unpinned here
+      std::string head = msg;
+      if (!msg.empty() && substitute_message(msg, resource, &head) != 0) { head = msg; out.message_unpinned = true; }
+      if (pr.path.empty()) { out.status = "error"; out.message = build_error_message(out.name, head, pr.err, ""); return out; }
       out.status = "fail";
       out.path = pr.path;
-      out.message = build_error_message(out.name, msg, pr.err, pr.path);
+      out.message = build_error_message(out.name, head, pr.err, pr.path);
       return out;
     }
     if (!isnil(any_pattern)) {  // validation.go:644-701

@@ -63,7 +63,7 @@ def main(tag):
     write = sum(a.get("WRITE_SIZE", 0.0) * fac.get(kn, 1.0) for kn, a in avg.items()) * 1024
     eval_ns = sum(k["avg_ns"] * fac[kn] for kn, k in per_kernel.items())
     # per device phase (bench.py PHASE_KERNELS): time, memory-side bytes, stall fraction and L2 hit rate per evaluation
-    phases = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::pss_kernel", "kyv::pss_map_kernel", "kyv::match_deny_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv::walk_kernel"),
+    phases = {"match": ("kyv::match_kernel", "kyv::match_walk_kernel", "kyv::match_walk_generic", "kyv::match_rec_kernel", "kyv::match_pre_kernel", "kyv::facts_kernel", "kyv::pss_kernel", "kyv::pss_map_kernel", "kyv::match_deny_kernel"), "cond": ("kyv_jit_cond",), "walk": ("kyv_jit_walk", "kyv_jit_fused", "kyv_jit_shapes", "kyv::walk_kernel"),
               "compact": ("kyv::compact",), "hist": ("kyv::status_hist",)}
     ph = {}
     for name, pre in phases.items():

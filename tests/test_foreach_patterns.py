@@ -149,3 +149,58 @@ def test_foreach_patterns_gpu_vs_oracle(jit):
     assert st["nbad"] == 0, st["bad"]
     assert st["compared"] > 20000
     assert res.counts["fallback"] == 0
+
+
+def nested_policies():
+    """foreach nested two and three levels deep (newForEachValidator(..., nesting+1), validation.go:360 -- the
+    reference recurses without limit; the device compiles up to FOREACH_MAX_NEST levels below the top), and one four
+    levels deep, which stays on the CPU engine"""
+    C = "request.object.spec.containers"
+    mounts_tmp = {"list": "element.mountPath", "pattern": {"mountPath": "/tmp/*"}}
+    vol_deny = {"list": "request.object.spec.volumes", "deny": {"conditions": {"any": [
+        {"key": "{{element.name}}", "operator": "AnyIn", "value": ["host*", "vol2"]}]}}}
+    return [
+        # containers -> their mounts -> the mount path (a string: not element-scoped, the pattern validates the mount)
+        _pol("fe-nest2", [{"list": C, "foreach": [{"list": "element.volumeMounts", "foreach": [mounts_tmp]}]}]),
+        # ... -> the pod's volumes (a list from the resource root at the third level), deny per volume
+        _pol("fe-nest3", [{"list": C, "foreach": [{"list": "element.volumeMounts", "foreach": [
+            {"list": "element.mountPath", "foreach": [vol_deny]}]}]}]),
+        # mixed entries: a nested level beside a pattern entry, preconditions inside the nesting
+        _pol("fe-nest2-mixed", [{"list": C, "pattern": {"name": "?*"}},
+                                {"list": C, "foreach": [{"list": "element.volumeMounts",
+                                                         "preconditions": {"all": [{"key": "{{element.name}}",
+                                                                                    "operator": "NotEquals",
+                                                                                    "value": "v0"}]},
+                                                         "foreach": [mounts_tmp]}]}]),
+        # four levels below the top: beyond the compiled depth (CPU engine)
+        _pol("fe-nest4", [{"list": C, "foreach": [{"list": "element.volumeMounts", "foreach": [
+            {"list": "element.mountPath", "foreach": [{"list": "request.object.spec.volumes", "foreach": [
+                {"list": "element.name", "pattern": {"name": "?*"}}]}]}]}]}]),
+    ]
+
+
+def test_foreach_nesting_vs_oracle():
+    pols = nested_policies()
+    rs = E.Ruleset(pols)
+    fb = {r["name"]: r["reason"] for r in rs.rules if r["kind"] == "fallback"}
+    assert fb and all(n.endswith("fe-nest4-r") for n in fb), fb  # (with its autogen rules)
+    docs, nsl = synth.mixed(3000, seed=73, edge=True)
+    docs = with_mounts(docs, 73)
+    st, res = PU.compare(pols, docs, nsl, backend="cpu")
+    assert st["nbad"] == 0, st["bad"]
+    status = np.asarray(res.status)
+    for k, rule in enumerate(rs.rules):
+        if not rule["name"].endswith("fe-nest4-r") and rule["name"].startswith("fe-"):
+            vals = set((status[k] & 7).tolist())
+            assert K.ST_PASS in vals and K.ST_FAIL in vals, (rule["name"], vals)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [False, True])
+def test_foreach_nesting_gpu_vs_oracle(jit):
+    pols = nested_policies()
+    docs, nsl = synth.mixed(20000, seed=74, edge=True)
+    docs = with_mounts(docs, 74)
+    st, res = PU.compare(pols, docs, nsl, backend="gpu", jit=jit)
+    assert st["nbad"] == 0, st["bad"]
+    assert st["compared"] > 20000

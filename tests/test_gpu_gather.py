@@ -82,8 +82,33 @@ want = sorted(zip((f["res"].astype(np.int64) + 1000).tolist(), f["rule"].tolist(
                   f["path_template"].tolist(), map(tuple, f["idx"].tolist())))
 got = sorted((int(r[0]), int(r[1]), int(r[2]), int(r[3]), tuple(int(x) for x in r[4:8])) for r in rows)
 assert got == want and len(got) > 100 and st["failure_rows_total"] == len(got), (len(got), len(want), st)
+# report assembly to one consumer rank: 16-byte rows on the wire, expanded on the root to the same rows
+st2 = comm.gather_report(b, 1000, root=0)
+assert np.array_equal(comm.status_of(0)[:packed.size], packed), "reported verdicts differ"
+got2 = sorted((int(r[0]), int(r[1]), int(r[2]), int(r[3]), tuple(int(x) for x in r[4:8])) for r in comm.failures_of(0))
+assert got2 == want and st2["failure_rows_total"] == len(want), (len(got2), st2)
+# the per-rule tallies summed over ranks (one rank here): the evaluation's own counts
+tot = comm.reduce_counts(b)
+assert np.array_equal(tot, np.asarray(res.rule_counts)), "reduced tallies differ"
+# a rule-sliced evaluation keeps every slice's failing-path rows resident (no copy-back), in the rows of the
+# copy-back evaluation of the same batch
+os.environ["KYV_SLICE_MB"] = "1"
+rs2 = E.Ruleset(cases.best_practices() + cases.quirk_policies())
+b2 = E.Batch(rs2, docs, nsl)
+ref = E.evaluate(rs2, b2, backend="gpu", device=0)
+f2 = ref.failures()
+want2 = sorted(zip((f2["res"].astype(np.int64) + 1000).tolist(), f2["rule"].tolist(), f2["alt"].tolist(),
+                   f2["path_template"].tolist(), map(tuple, f2["idx"].tolist())))
+assert sorted(want2) == sorted(want), "sliced evaluation rows differ from the one-slice evaluation"
+comm.gather_report(b2, 1000, root=0)  # rows of the copy-back evaluation (host copy of its slices)
+got3 = sorted((int(r[0]), int(r[1]), int(r[2]), int(r[3]), tuple(int(x) for x in r[4:8])) for r in comm.failures_of(0))
+assert got3 == want2, (len(got3), len(want2))
+E.evaluate(rs2, b2, backend="gpu", device=0, copy_back=False)  # resident rows
+comm.gather_report(b2, 1000, root=0)
+got4 = sorted((int(r[0]), int(r[1]), int(r[2]), int(r[3]), tuple(int(x) for x in r[4:8])) for r in comm.failures_of(0))
+assert got4 == want2, (len(got4), len(want2))
 comm.close()
-print("native gather ok", packed.size, len(got), st)
+print("native gather ok", packed.size, len(got), st, st2)
 """
 
 
