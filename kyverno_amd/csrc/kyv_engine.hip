@@ -325,6 +325,9 @@ struct SliceSched {
   MRec* mrec = nullptr;          // [nmr]
   uint32_t* mcls = nullptr;      // their kind index (MRecIndex): [nclass + 1] offsets into mcrec
   MRec* mcrec = nullptr;         // the records again, class by class
+  uint32_t *tcls = nullptr, *rcls = nullptr;  // the same split (match_tile_kernel): its records (branch-free path) and
+  MRec *tcrec = nullptr, *rcrec = nullptr;    // the rest, per class (match_rec_kernel's uniform waves then)
+  size_t ntile = 0;
   uint32_t nclass = 0;
   uint8_t* tails = nullptr;      // lane tail facts of the records (TailTab): TailCfg, then the TailProgs
   uint32_t nmd = 0;              // then deny rules without JMESPath on match_deny_kernel
@@ -362,7 +365,9 @@ struct DeviceResults {
   uint32_t* tsum = nullptr;      // compaction tile sums / offsets
   uint32_t* tseg = nullptr;      // their segment totals / offsets (compact_scan_kernel)
   unsigned long long* counts = nullptr;
-  size_t max_recs = 0;
+  size_t max_recs = 0;             // staging slots of the largest slice (d.stage)
+  size_t recs_cap = 0;             // records d.recs holds (>= max_recs; grown between slices when a rule-sliced
+                                   // evaluation's appended records could outgrow it)
   uint32_t npss = 0;
   size_t nres = 0, nrules = 0;
   size_t max_slice_rules = 0;
@@ -400,6 +405,7 @@ static void free_dev_results(DeviceResults& d, int dev) {
   dfree(d.wl.items); dfree(d.wl.cnt);
   for (auto& sl : d.slices) {
     dfree(sl.rbase); dfree(sl.mrules); dfree(sl.mrec); dfree(sl.mcls); dfree(sl.mcrec); dfree(sl.tails); dfree(sl.sched);
+    dfree(sl.tcls); dfree(sl.rcls); dfree(sl.tcrec); dfree(sl.rcrec);
     if (sl.evs) hipEventDestroy(sl.evs);
     for (auto e : sl.ev) if (e) hipEventDestroy(e);
     for (auto e : sl.cev) if (e) hipEventDestroy(e);
@@ -1520,6 +1526,32 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       sl.mcrec = nullptr;
       HIP_OK(dmalloc(&sl.mcrec, std::max<size_t>(1, crecs.size()) * sizeof(MRec)));
       if (!crecs.empty()) HIP_OK(hipMemcpy(sl.mcrec, crecs.data(), crecs.size() * sizeof(MRec), hipMemcpyHostToDevice));
+      {  // the split for match_tile_kernel: records of the branch-free path / the rest, per class
+        auto tile_ok = [](const MRec& R) {
+          return (R.bits & MR_FASTEVAL) && (!(R.bits & MR_EMPTY) || (R.bits & MR_ECONST)) && !(R.flags & RD_GATE_EXACT);
+        };
+        std::vector<uint32_t> toff(sl.nclass + 1, 0), roff(sl.nclass + 1, 0);
+        std::vector<MRec> trec, rrec;
+        for (uint32_t c = 0; c < sl.nclass; c++) {
+          for (uint32_t q = off[c]; q < off[c + 1]; q++) (tile_ok(crecs[q]) ? trec : rrec).push_back(crecs[q]);
+          toff[c + 1] = (uint32_t)trec.size();
+          roff[c + 1] = (uint32_t)rrec.size();
+        }
+        sl.ntile = trec.size();
+        for (auto* p : {&sl.tcls, &sl.rcls}) { dfree(*p); *p = nullptr; }
+        for (auto* p : {&sl.tcrec, &sl.rcrec}) { dfree(*p); *p = nullptr; }
+        HIP_OK(dmalloc(&sl.tcls, toff.size() * 4));
+        HIP_OK(hipMemcpy(sl.tcls, toff.data(), toff.size() * 4, hipMemcpyHostToDevice));
+        HIP_OK(dmalloc(&sl.rcls, roff.size() * 4));
+        HIP_OK(hipMemcpy(sl.rcls, roff.data(), roff.size() * 4, hipMemcpyHostToDevice));
+        HIP_OK(dmalloc(&sl.tcrec, std::max<size_t>(1, trec.size()) * sizeof(MRec)));
+        if (!trec.empty()) HIP_OK(hipMemcpy(sl.tcrec, trec.data(), trec.size() * sizeof(MRec), hipMemcpyHostToDevice));
+        HIP_OK(dmalloc(&sl.rcrec, std::max<size_t>(1, rrec.size()) * sizeof(MRec)));
+        if (!rrec.empty()) HIP_OK(hipMemcpy(sl.rcrec, rrec.data(), rrec.size() * sizeof(MRec), hipMemcpyHostToDevice));
+        if (getenv("KYV_DEBUG_STATS"))
+          fprintf(stderr, "[kyvgpu] slice [%u, %u): %zu class-record copies, %zu on match_tile_kernel\n", sl.k0, sl.k1,
+                  crecs.size(), trec.size());
+      }
       recs.resize(std::max<size_t>(1, recs.size()));
       HIP_OK(dmalloc(&sl.mrec, recs.size() * sizeof(MRec)));
       HIP_OK(hipMemcpy(sl.mrec, recs.data(), recs.size() * sizeof(MRec), hipMemcpyHostToDevice));
@@ -1674,6 +1706,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     const size_t msr = std::max<size_t>(d.max_slice_rules, 1);
     HIP_OK(dmalloc(&d.stage, d.max_recs * sizeof(FailRec)));
     HIP_OK(dmalloc(&d.recs, d.max_recs * sizeof(FailRec)));
+    d.recs_cap = d.max_recs;
     HIP_OK(dmalloc(&d.rcnt, std::max<size_t>(msr * nwv, 1) * 2));
     HIP_OK(dmalloc(&d.tsum, std::max<size_t>((msr * nwv + WAVE - 1) / WAVE, 1) * 4));
     HIP_OK(dmalloc(&d.tseg, std::max<size_t>((msr * nwv + WAVE - 1) / WAVE / SCAN_SEG + 1, 1) * 4));
@@ -1711,6 +1744,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
   double total_ms = 0;
   double phase[5] = {0, 0, 0, 0, 0};
+  bool redone = false;  // a rule-sliced evaluation re-run once after its resident record list was grown
   for (auto& sl : d.slices) {
     if (!sl.evs) HIP_OK(hipEventCreate(&sl.evs));
     for (auto& e : sl.ev) if (!e) HIP_OK(hipEventCreate(&e));
@@ -1808,12 +1842,20 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
       if (sl.nmr) {
         const bool mw1 = v.gmask_words <= 1;
-        const MRecIndex ix{sl.mcls, sl.mcrec};
+        // KYV_MATCH_TILE=1 (experiment): match_tile_kernel (lanes = records) for the branch-free records of kind-uniform
+        // waves, match_rec_kernel for the rest; default off: match_rec_kernel alone
+        static const bool tile_on = getenv("KYV_MATCH_TILE") && atoi(getenv("KYV_MATCH_TILE")) != 0;
+        const bool tile = tile_on && use_facts && sl.ntile;
+        const MRecIndex ix = tile ? MRecIndex{sl.rcls, sl.rcrec} : MRecIndex{sl.mcls, sl.mcrec};
         const ShapeTab sh{d.shape_st, d.shape_rec, d.wl.nwaves, d.nshapes};
         const TailTab tt{(const TailCfg*)sl.tails, (const TailProg*)(sl.tails + sizeof(TailCfg))};
         const ResFacts* fp = use_facts ? d.facts : nullptr;
         (acct ? kyvacct::match_rec : kyvprod::match_rec)(mwpe, mw1, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr,
                                                          &ix, &sh, &tt, fp);
+        if (tile) {
+          const MRecIndex tix{sl.tcls, sl.tcrec};
+          (acct ? kyvacct::match_tile : kyvprod::match_tile)(mw1, grid.x, stream, d.view, &o, &d.wl, &tix, &sh, &tt, fp);
+        }
       }
       if (sl.nmw) {
         (acct ? kyvacct::match_walk_generic : kyvprod::match_walk_generic)(mwpe, grid.x, stream, d.view, &o, &d.wl,
@@ -1931,7 +1973,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       hipLaunchKernelGGL(compact_top_kernel, dim3(1), dim3(1024), 0, stream, d.tseg, std::max<uint32_t>(nseg, 1), d.nrecs,
                          accumulate);
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, sl.rbase, d.rcnt, drules,
-                         d.wl.nwaves, nchunks, d.tsum, d.tseg, d.recs, d.max_recs, sl.k0, (const uint32_t*)d.nrecs);
+                         d.wl.nwaves, nchunks, d.tsum, d.tseg, d.recs, d.recs_cap, sl.k0, (const uint32_t*)d.nrecs);
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(sl.ev[3], stream));
       if (acct) {  // compaction: chunk counts (read twice), tile sums, the staged records read, the dense records written
@@ -1961,6 +2003,24 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     if (acct) aphase[4] += (uint64_t)nres * nrules;  // the histogram reads every verdict byte
     HIP_OK(hipEventRecord(d.e1, stream));
     HIP_OK(hipEventSynchronize(d.e1));
+    if (accumulate) {  // the slices' appended records outgrew the resident list: grow it and run this evaluation again
+      uint32_t c[3] = {0, 0, 0};
+      HIP_OK(hipMemcpy(c, d.nrecs, 12, hipMemcpyDeviceToHost));
+      if (c[2] > d.recs_cap) {
+        if (redone) throw std::runtime_error("failure record buffer overflow");
+        dfree(d.recs);
+        d.recs = nullptr;
+        d.recs_cap = 0;
+        const size_t cap = (size_t)c[2] + c[2] / 4 + 1024;
+        HIP_OK(dmalloc(&d.recs, cap * sizeof(FailRec)));
+        d.recs_cap = cap;
+        redone = true;
+        for (auto& x : aphase) x = 0;  // (the accounting counters of the discarded run)
+        for (auto& x : aclass) x = 0;
+        it--;
+        continue;
+      }
+    }
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, d.e0, d.e1));
     total_ms += ms;
@@ -2553,9 +2613,9 @@ static const FailRec* failure_records(const Batch& b, int device, uint32_t* n, v
   }
   uint32_t c[3] = {0, 0, 0};
   HIP_OK(hipMemcpy(c, d.nrecs, 12, hipMemcpyDeviceToHost));
-  if (c[2] > d.max_recs)
+  if (c[2] > d.recs_cap)
     throw std::runtime_error("the evaluation's failing-path records exceed the resident record buffer (" +
-                             std::to_string(c[2]) + " > " + std::to_string(d.max_recs) +
+                             std::to_string(c[2]) + " > " + std::to_string(d.recs_cap) +
                              "): evaluate with copy-back to gather them slice by slice");
   *n = c[2];
   return (const FailRec*)d.recs;
