@@ -1252,14 +1252,25 @@ struct CondGen {
 
 // rules the light match kernel cannot evaluate (kyv_engine.hip rule_needs_jmes): foreach, or a precondition / deny
 // program with a JMESPath operand
+// (length(<field chain>) operands run in the light kernels too: kyv_cond.h jmes_len_chain / jmes_len_cv)
+static bool heavy_jmes(const Ruleset& rs, const CondOperand& o) {
+  if (o.kind != OK_JMES) return false;
+  const uint32_t* p = rs.pool.data() + o.a;
+  const uint32_t n = o.nseg;
+  if (n < 2 || (p[0] & 0xFFu) != JR_OBJECT || p[n - 1] != JO_LENGTH) return true;
+  uint32_t i = 1;
+  for (; i + 1 < n; i += 2)
+    if (p[i] != JO_FIELD) return true;
+  return i != n - 1;
+}
 bool prog_has_jmes(const Ruleset& rs, uint32_t prog) {
   if (prog == NONE) return false;
   const CondProg& p = rs.cprogs[prog];
   const uint32_t nany = p.nany == NONE ? 0u : p.nany;
   for (uint32_t i = 0; i < nany; i++)
-    if (rs.conds[p.any0 + i].key.kind == OK_JMES || rs.conds[p.any0 + i].value.kind == OK_JMES) return true;
+    if (heavy_jmes(rs, rs.conds[p.any0 + i].key) || heavy_jmes(rs, rs.conds[p.any0 + i].value)) return true;
   for (uint32_t i = 0; i < p.nall; i++)
-    if (rs.conds[p.all0 + i].key.kind == OK_JMES || rs.conds[p.all0 + i].value.kind == OK_JMES) return true;
+    if (heavy_jmes(rs, rs.conds[p.all0 + i].key) || heavy_jmes(rs, rs.conds[p.all0 + i].value)) return true;
   return false;
 }
 

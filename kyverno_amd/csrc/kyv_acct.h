@@ -14,8 +14,6 @@
   void match_rec(int wpe, bool mw1, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,\
                  const void* recs, uint32_t nm, const void* index, const void* shapes, const void* tails,\
                  const void* facts);\
-  void match_tile(bool mw1, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,\
-                  const void* index, const void* shapes, const void* tails, const void* facts);\
   void facts(bool mw1, unsigned grid, hipStream_t s, const void* view, const void* cfg, void* out);\
   void match_walk_generic(int wpe, unsigned grid, hipStream_t s, const void* view, const void* devout, const void* wl,\
                           const uint32_t* mrules, uint32_t nm);\

@@ -400,6 +400,47 @@ KYV_HD CV jres_cv(const View& v, NodeTab R, const JRes& r, const JList& L) {
 }
 
 // any operand -> CV (JS_OK / JS_NOTFOUND with *miss / JS_FB); L backs a projection list result
+// length(<field chain of request.object>) -- the one JMESPath function of C5's rules -- without the interpreter's
+// projection list, for the light kernels (kJ = false): the same steps as jmes_run over [JR_OBJECT, JO_FIELD k...,
+// JO_LENGTH] (a field of a non-map is null, a missing key NotFound only for a JF_PURE program; jpfLength of an
+// array / object is its element count, of an ASCII string its length, of anything else an error)
+KYV_HD bool jmes_len_chain(const uint32_t* p, uint32_t n) {
+  if (n < 2 || (p[0] & 0xFFu) != JR_OBJECT || p[n - 1] != JO_LENGTH) return false;
+  uint32_t i = 1;
+  for (; i + 1 < n; i += 2)
+    if (p[i] != JO_FIELD) return false;
+  return i == n - 1;
+}
+KYV_HD int jmes_len_cv(const View& v, NodeTab R, const CondOperand& o, CV* out, uint32_t* miss) {
+  const uint32_t* p = v.pool + o.a;
+  const uint32_t n = o.nseg;
+  const bool pure = (p[0] & JF_PURE) != 0;
+  uint32_t cur = 0, fields = 0;
+  for (uint32_t i = 1; i + 1 < n; i += 2) {
+    bool missing;
+    cur = j_field(R, cur, p[i + 1], &missing);
+    if (missing && pure) { *miss = fields; return JS_NOTFOUND; }
+    fields++;
+  }
+  if (cur == NONE) return JS_ERR;
+  const Node& x = R[cur];
+  uint32_t cnt;
+  if (node_type(x) == N_ARR || node_type(x) == N_MAP) {
+    cnt = x.b;
+  } else if (node_type(x) == N_STR) {
+    const uint32_t ln = v.str_len[x.a];
+    const uint8_t* b = sbytes(v, x.a);
+    for (uint32_t q = 0; q < ln; q++) if (b[q] >= 0x80) return JS_FB;  // (other strings: the CPU engine)
+    cnt = ln;
+  } else {
+    return JS_ERR;
+  }
+  CV c = cv_node(Node{N_NULL, 0, 0, 0}, true);
+  c.t = CT_INT; c.i = cnt; c.sid = NONE;  // a float64 count, integral: an int after the JSON context round trip
+  *out = c;
+  return JS_OK;
+}
+
 KYV_HD int operand_cv(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, CV* out, uint32_t* miss,
                       uint32_t row = NONE) {
   if (o.kind != OK_JMES) return cv_operand(v, R, o, out, miss, row) ? JS_OK : JS_NOTFOUND;
@@ -800,7 +841,11 @@ KYV_HD __attribute__((always_inline)) int eval_prog_inl(const View& v, NodeTab R
         }
         if (o.kind == OK_JMES) {
           if constexpr (!kJ) {
-            return CR_FB;
+            if (!jmes_len_chain(v.pool + o.a, o.nseg)) return CR_FB;
+            const int st = jmes_len_cv(v, R, o, &tmp, &miss);
+            if (st == JS_FB) return CR_FB;
+            if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
+            if (st == JS_ERR) { *err_cond = c0 + i; *err_side = side; *err_seg = NONE; return CP_ERROR; }
           } else {
             JList L;
             const int st = operand_cv(v, R, o, elem, L, &tmp, &miss, row);
@@ -831,8 +876,10 @@ KYV_HD __attribute__((always_inline)) int eval_prog_inl(const View& v, NodeTab R
       operand_cv(v, R, c.value, elem, lx, &x, &miss, row);
       r = eval_cond(v, R, c, k, x);
     } else {
-      cv_operand(v, R, c.key, &k, &miss, row);
-      cv_operand(v, R, c.value, &x, &miss, row);
+      if (c.key.kind == OK_JMES) jmes_len_cv(v, R, c.key, &k, &miss);  // (a length chain: checked in the first pass)
+      else cv_operand(v, R, c.key, &k, &miss, row);
+      if (c.value.kind == OK_JMES) jmes_len_cv(v, R, c.value, &x, &miss);
+      else cv_operand(v, R, c.value, &x, &miss, row);
       r = eval_cond(v, R, c, k, x);
     }
     if (r == CR_FB || r == CR_PANIC) return r;

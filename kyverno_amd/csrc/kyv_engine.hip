@@ -298,9 +298,13 @@ static void stream_put(int dev, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
 static bool prog_jmes(const Ruleset& rs, uint32_t prog) {
   if (prog == NONE) return false;
   const CondProg& p = rs.cprogs[prog];
+  // (length(<field chain>) runs in the light kernels too: kyv_cond.h jmes_len_cv)
+  auto heavy = [&](const CondOperand& o) {
+    return o.kind == OK_JMES && !jmes_len_chain(rs.pool.data() + o.a, o.nseg);
+  };
   auto blk = [&](uint32_t c0, uint32_t n) {
     for (uint32_t i = 0; i < n; i++)
-      if (rs.conds[c0 + i].key.kind == OK_JMES || rs.conds[c0 + i].value.kind == OK_JMES) return true;
+      if (heavy(rs.conds[c0 + i].key) || heavy(rs.conds[c0 + i].value)) return true;
     return false;
   };
   return blk(p.any0, p.nany == NONE ? 0u : p.nany) || blk(p.all0, p.nall);
@@ -325,9 +329,6 @@ struct SliceSched {
   MRec* mrec = nullptr;          // [nmr]
   uint32_t* mcls = nullptr;      // their kind index (MRecIndex): [nclass + 1] offsets into mcrec
   MRec* mcrec = nullptr;         // the records again, class by class
-  uint32_t *tcls = nullptr, *rcls = nullptr;  // the same split (match_tile_kernel): its records (branch-free path) and
-  MRec *tcrec = nullptr, *rcrec = nullptr;    // the rest, per class (match_rec_kernel's uniform waves then)
-  size_t ntile = 0;
   uint32_t nclass = 0;
   uint8_t* tails = nullptr;      // lane tail facts of the records (TailTab): TailCfg, then the TailProgs
   uint32_t nmd = 0;              // then deny rules without JMESPath on match_deny_kernel
@@ -405,7 +406,6 @@ static void free_dev_results(DeviceResults& d, int dev) {
   dfree(d.wl.items); dfree(d.wl.cnt);
   for (auto& sl : d.slices) {
     dfree(sl.rbase); dfree(sl.mrules); dfree(sl.mrec); dfree(sl.mcls); dfree(sl.mcrec); dfree(sl.tails); dfree(sl.sched);
-    dfree(sl.tcls); dfree(sl.rcls); dfree(sl.tcrec); dfree(sl.rcrec);
     if (sl.evs) hipEventDestroy(sl.evs);
     for (auto e : sl.ev) if (e) hipEventDestroy(e);
     for (auto e : sl.cev) if (e) hipEventDestroy(e);
@@ -1038,6 +1038,57 @@ static uint32_t served_shape(const Ruleset& rs, uint32_t q, const std::vector<ui
   return (R.bits & MR_FAST) ? rs.jit_shape[q] : 0u;
 }
 
+// A kind-class copy of a match record (round 5): every resource of the class has the same GVK kind, so a filter's
+// kinds test (condition_block's checkKind, kyv_eval.h) is a constant of the copy unless a kind of the filter carries a
+// group / version refinement. A filter whose kinds accept the class loses the test (no kinds: every kind); one whose
+// kinds can never accept it is removed when that cannot change the outcome -- a match filter of an ANY block or an
+// exclude filter of an ANY / plain block (it never contributes, and a filter rejected on its kinds raises no
+// nondeterminism); an ALL exclude block with such a filter can never exclude and is dropped whole. The empty-OldResource
+// retry evaluated on the device (MR_EMPTY without a constant outcome) compares kinds against the empty resource: such
+// records keep their filters.
+static void fold_kinds(MRec& R, uint32_t ck, size_t* nfold, size_t* ndrop) {
+  if ((R.bits & MR_EMPTY) && !(R.bits & MR_ECONST)) return;
+  const uint32_t mm = (R.bits >> 8) & 0xFFu, em = (R.bits >> 16) & 0xFFu;
+  uint32_t nmf = (R.bits >> 24) & 0xFu, nef = R.bits >> 28;
+  MRecFilter out[MREC_F];
+  uint32_t no = 0, omf = 0, oef = 0;
+  bool drop_excl = false;
+  for (uint32_t j = 0; j < nmf + nef; j++) {
+    MRecFilter F = R.f[j];
+    const bool ism = j < nmf;
+    const uint32_t nk = (F.bits >> 16) & 7u;
+    int acc = -1;  // 1: the kinds accept the class, 0: they never do, -1: it depends on the resource (group / version)
+    if (nk && !(F.bits & FF_ZERO_RD)) {
+      bool yes = false, dep = false;
+      for (uint32_t i = 0; i < nk && i < 4; i++) {
+        const uint32_t kd = F.kinds[i];
+        if (kd == NONE) { yes = true; continue; }
+        const uint32_t sid = (F.bits & MRF_KPACK) ? (kd & 0xFFFFFFu) : kd;
+        const bool gv = (F.bits >> (24 + i)) & 1u;
+        if (sid == ck) { if (gv) dep = true; else yes = true; }
+      }
+      acc = yes ? 1 : dep ? -1 : 0;
+    }
+    if (acc == 1) {
+      F.bits &= ~((7u << 16) | (0xFu << 24) | MRF_KPACK);  // no kinds: the test passes (group / version bits cleared)
+      (*nfold)++;
+    } else if (acc == 0) {
+      if (ism && mm == MM_ANY) { (*ndrop)++; continue; }
+      if (!ism && (em == MM_ANY || em == MM_PLAIN)) { (*ndrop)++; continue; }
+      if (!ism && em == MM_ALL) drop_excl = true;
+    }
+    out[no++] = F;
+    if (ism) omf++; else oef++;
+  }
+  if (drop_excl) {  // an ALL exclude block with a filter that never excludes: never excluded
+    no = omf;
+    oef = 0;
+    (*ndrop)++;
+  }
+  for (uint32_t j = 0; j < MREC_F; j++) R.f[j] = j < no ? out[j] : MRecFilter{};
+  R.bits = (R.bits & 0x00FFFFFFu) | (omf << 24) | (oef << 28);
+}
+
 // The shape tables of a batch: per kind class the shapes some served rule's kind gate admits (kyv_jit_shapes computes
 // only those), and the [shape][res] verdict / record buffers
 static void setup_shapes(const Ruleset& rs, const Batch& b, DeviceResults& d, bool jit) {
@@ -1511,13 +1562,25 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       sl.nclass = gw ? (uint32_t)(b.gate.size() / gw) : 0u;
       std::vector<uint32_t> off(sl.nclass + 1, 0);
       std::vector<MRec> crecs;
+      // a class is one GVK kind (order_by_kind): its kind sid, from the first resource of the class
+      std::vector<uint32_t> ckind(sl.nclass, NONE);
+      for (const ResHeader& h : b.hdr)
+        if (h.kclass < sl.nclass && ckind[h.kclass] == NONE) ckind[h.kclass] = h.gvk_kind;
+      static const bool kfold = !getenv("KYV_KIND_FOLD") || atoi(getenv("KYV_KIND_FOLD")) != 0;
+      size_t nfold = 0, ndrop = 0;
       for (uint32_t c = 0; c < sl.nclass; c++) {
         for (uint32_t q = 0; q < sl.nmr; q++) {
           const uint32_t k = recs[q].k;
-          if ((b.gate[(size_t)c * gw + (k >> 5)] >> (k & 31)) & 1u) crecs.push_back(recs[q]);
+          if (!((b.gate[(size_t)c * gw + (k >> 5)] >> (k & 31)) & 1u)) continue;
+          MRec R = recs[q];
+          if (kfold && ckind[c] != NONE) fold_kinds(R, ckind[c], &nfold, &ndrop);
+          crecs.push_back(R);
         }
         off[c + 1] = (uint32_t)crecs.size();
       }
+      if (getenv("KYV_DEBUG_STATS"))
+        fprintf(stderr, "[kyvgpu] slice [%u, %u): %zu class-record copies, kind checks folded in %zu filters, %zu "
+                "filters that cannot accept their class removed\n", sl.k0, sl.k1, crecs.size(), nfold, ndrop);
       dfree(sl.mcls);
       sl.mcls = nullptr;
       HIP_OK(dmalloc(&sl.mcls, off.size() * 4));
@@ -1526,32 +1589,6 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
       sl.mcrec = nullptr;
       HIP_OK(dmalloc(&sl.mcrec, std::max<size_t>(1, crecs.size()) * sizeof(MRec)));
       if (!crecs.empty()) HIP_OK(hipMemcpy(sl.mcrec, crecs.data(), crecs.size() * sizeof(MRec), hipMemcpyHostToDevice));
-      {  // the split for match_tile_kernel: records of the branch-free path / the rest, per class
-        auto tile_ok = [](const MRec& R) {
-          return (R.bits & MR_FASTEVAL) && (!(R.bits & MR_EMPTY) || (R.bits & MR_ECONST)) && !(R.flags & RD_GATE_EXACT);
-        };
-        std::vector<uint32_t> toff(sl.nclass + 1, 0), roff(sl.nclass + 1, 0);
-        std::vector<MRec> trec, rrec;
-        for (uint32_t c = 0; c < sl.nclass; c++) {
-          for (uint32_t q = off[c]; q < off[c + 1]; q++) (tile_ok(crecs[q]) ? trec : rrec).push_back(crecs[q]);
-          toff[c + 1] = (uint32_t)trec.size();
-          roff[c + 1] = (uint32_t)rrec.size();
-        }
-        sl.ntile = trec.size();
-        for (auto* p : {&sl.tcls, &sl.rcls}) { dfree(*p); *p = nullptr; }
-        for (auto* p : {&sl.tcrec, &sl.rcrec}) { dfree(*p); *p = nullptr; }
-        HIP_OK(dmalloc(&sl.tcls, toff.size() * 4));
-        HIP_OK(hipMemcpy(sl.tcls, toff.data(), toff.size() * 4, hipMemcpyHostToDevice));
-        HIP_OK(dmalloc(&sl.rcls, roff.size() * 4));
-        HIP_OK(hipMemcpy(sl.rcls, roff.data(), roff.size() * 4, hipMemcpyHostToDevice));
-        HIP_OK(dmalloc(&sl.tcrec, std::max<size_t>(1, trec.size()) * sizeof(MRec)));
-        if (!trec.empty()) HIP_OK(hipMemcpy(sl.tcrec, trec.data(), trec.size() * sizeof(MRec), hipMemcpyHostToDevice));
-        HIP_OK(dmalloc(&sl.rcrec, std::max<size_t>(1, rrec.size()) * sizeof(MRec)));
-        if (!rrec.empty()) HIP_OK(hipMemcpy(sl.rcrec, rrec.data(), rrec.size() * sizeof(MRec), hipMemcpyHostToDevice));
-        if (getenv("KYV_DEBUG_STATS"))
-          fprintf(stderr, "[kyvgpu] slice [%u, %u): %zu class-record copies, %zu on match_tile_kernel\n", sl.k0, sl.k1,
-                  crecs.size(), trec.size());
-      }
       recs.resize(std::max<size_t>(1, recs.size()));
       HIP_OK(dmalloc(&sl.mrec, recs.size() * sizeof(MRec)));
       HIP_OK(hipMemcpy(sl.mrec, recs.data(), recs.size() * sizeof(MRec), hipMemcpyHostToDevice));
@@ -1842,20 +1879,12 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       static const int mwpe = getenv("KYV_MATCHW_WPE") ? atoi(getenv("KYV_MATCHW_WPE")) : 4;
       if (sl.nmr) {
         const bool mw1 = v.gmask_words <= 1;
-        // KYV_MATCH_TILE=1 (experiment): match_tile_kernel (lanes = records) for the branch-free records of kind-uniform
-        // waves, match_rec_kernel for the rest; default off: match_rec_kernel alone
-        static const bool tile_on = getenv("KYV_MATCH_TILE") && atoi(getenv("KYV_MATCH_TILE")) != 0;
-        const bool tile = tile_on && use_facts && sl.ntile;
-        const MRecIndex ix = tile ? MRecIndex{sl.rcls, sl.rcrec} : MRecIndex{sl.mcls, sl.mcrec};
+        const MRecIndex ix{sl.mcls, sl.mcrec};
         const ShapeTab sh{d.shape_st, d.shape_rec, d.wl.nwaves, d.nshapes};
         const TailTab tt{(const TailCfg*)sl.tails, (const TailProg*)(sl.tails + sizeof(TailCfg))};
         const ResFacts* fp = use_facts ? d.facts : nullptr;
         (acct ? kyvacct::match_rec : kyvprod::match_rec)(mwpe, mw1, grid.x, stream, d.view, &o, &d.wl, sl.mrec, sl.nmr,
                                                          &ix, &sh, &tt, fp);
-        if (tile) {
-          const MRecIndex tix{sl.tcls, sl.tcrec};
-          (acct ? kyvacct::match_tile : kyvprod::match_tile)(mw1, grid.x, stream, d.view, &o, &d.wl, &tix, &sh, &tt, fp);
-        }
       }
       if (sl.nmw) {
         (acct ? kyvacct::match_walk_generic : kyvprod::match_walk_generic)(mwpe, grid.x, stream, d.view, &o, &d.wl,

@@ -369,25 +369,23 @@ KYV_HD __attribute__((always_inline)) SelProg ld_selprog(const SelProg* p) {
   return *p;
 #endif
 }
-// cb_tail (above) of a covered filter (program pi), from the lane's facts; *fnd: the nondeterminism cb_tail would raise.
-// kV: the program index differs per lane (match_tile_kernel: lanes are records), so its words are vector loads
-template <bool kV = false>
+// cb_tail (above) of a covered filter (program pi), from the lane's facts; *fnd: the nondeterminism cb_tail would raise
 KYV_HD __attribute__((always_inline)) bool tail_prog(const TailTab& tt, uint32_t pi, uint32_t b, const LaneTail& t,
                                                      uint32_t fl, bool uic, bool* fnd) {
   const TailProg* tp = tt.prog + pi;
-  const uint32_t ann = kV ? tp->ann : tf_ld(&tp->ann);
+  const uint32_t ann = tf_ld(&tp->ann);
   const bool annok = (t.ann & ann) == ann;
   bool sok = true, n1 = false;
   if (b & FF_HAS_SEL) {
     int r;
-    sel_prog(kV ? tp->sel : ld_selprog(&tp->sel), t, false, &r, &n1);
+    sel_prog(ld_selprog(&tp->sel), t, false, &r, &n1);
     sok = r == 1;
   }
   bool nsok = true, n2 = false, nscond = false;
   if (b & FF_HAS_NSSEL) {
     nscond = !(fl & MF_ISNS) & (!(fl & MF_KIND_EMPTY) | ((b & FF_KINDS_STAR) != 0));
     int r;
-    sel_prog(kV ? tp->nssel : ld_selprog(&tp->nssel), t, true, &r, &n2);
+    sel_prog(ld_selprog(&tp->nssel), t, true, &r, &n2);
     nsok = !nscond | (r == 1);
   }
   *fnd = annok & (n1 | (sok & nscond & n2));
@@ -510,7 +508,6 @@ KYV_HD __attribute__((always_inline)) bool pair_match_rec(const View& v, const M
 // masks: a filter's or requirement's nondeterminism flag counts only on lanes where the reference would have evaluated
 // it.
 // condition_block of a record filter (uic: an exclude filter), branch-free per lane; *fnd: its nondeterminism
-template <bool kV = false>
 KYV_HD __attribute__((always_inline)) bool filt_fast(const MRecFilter& F, const MFacts& mf, const TailTab& tt,
                                                      const LaneTail& t, bool uic, bool* fnd) {
   const uint32_t b = F.bits, nk = (b >> 16) & 7u;
@@ -535,12 +532,11 @@ KYV_HD __attribute__((always_inline)) bool filt_fast(const MRecFilter& F, const 
   *fnd = false;
   if (!((b >> 28) & 1u)) return head & !(uic && (b & FF_USERINFO));
   bool tnd;
-  const bool c = tail_prog<kV>(tt, F.pad - 1, b, t, mf.fl, uic, &tnd);
+  const bool c = tail_prog(tt, F.pad - 1, b, t, mf.fl, uic, &tnd);
   *fnd = head & tnd;
   return head & c;
 }
-// match_rule over an MR_FASTEVAL record (filter slots F[0..2]), branch-free per lane (kV: the record per lane)
-template <bool kV = false>
+// match_rule over an MR_FASTEVAL record (filter slots F[0..2]), branch-free per lane
 KYV_HD __attribute__((always_inline)) bool match_fast(const View& v, uint32_t bits, const MRecFilter* F, const MFacts& mf,
                                                       const TailTab& tt, const LaneTail& t, bool* nd) {
   const uint32_t mm = (bits >> 8) & 0xFFu, em = (bits >> 16) & 0xFFu, nmf = (bits >> 24) & 0xFu, nef = bits >> 28;
@@ -555,7 +551,7 @@ KYV_HD __attribute__((always_inline)) bool match_fast(const View& v, uint32_t bi
       bool c = false;
       if (!zero) {
         bool fnd;
-        c = filt_fast<kV>(F[j], mf, tt, t, false, &fnd);
+        c = filt_fast(F[j], mf, tt, t, false, &fnd);
         n = n | (ev & fnd);
       }
       if (any) one = one | (ev & c);
@@ -573,7 +569,7 @@ KYV_HD __attribute__((always_inline)) bool match_fast(const View& v, uint32_t bi
       bool c = false;
       if (!skip) {
         bool fnd;
-        c = filt_fast<kV>(F[j], mf, tt, t, true, &fnd);
+        c = filt_fast(F[j], mf, tt, t, true, &fnd);
         n = n | (ev & fnd);
       }
       if (eany) excluded = excluded | (ev & c);
@@ -834,113 +830,6 @@ match_rec_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, const MRec
     const uint32_t shape = (H.kind >> 8) & 0x7FFFu;  // 1 + shape of a shape rule, else 0; bit 23: wide records
     if (shape) mrec_shape_out(v, o, sh, shape - 1, (H.kind >> 23) & 1u, k, r, gated, m, st, hflags, w, sv);
     else match_walk_append(v, o, wl, k, H.kind & 0xFFu, r, gated, m, st, hflags, hroot);
-  }
-}
-
-// Lanes = records (round 5). match_rec_kernel spends ~390 instructions per (wave, record), most of them scalar: every
-// record is parsed and branched on by every wave, for 64 resources at a time (C4: 10,440 records, 43 ms, issue-bound).
-// Here the lanes of a wave are 64 RECORDS of the wave's kind class and the loop runs over the wave's 64 resources: a
-// record is loaded once per tile (per-lane vector loads), a resource's facts once per iteration (scalar loads, wave-
-// uniform), and each instruction decides 64 (record, resource) pairs of the branch-free path. Only kind-uniform waves
-// and MR_FASTEVAL records (the branch-free path of match_rec_kernel: filter tails covered by the lane tail facts, a
-// constant empty-OldResource retry, a compiled match block) come here; the rest stay on match_rec_kernel (its uniform
-// lists hold the other records, its mixed waves every record). Per lane (= rule k) the outputs of chunk (k, wave) are
-// produced in resource order, exactly as the ballot-compacted appends of match_rec_kernel order them: staged
-// failing-path records of shape rules, work-list items of the other pattern rules, and their counts.
-template <int kMW>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
-match_tile_kernel(const View* __restrict__ vp, DevOut o, WorkLists wl, MRecIndex tix, ShapeTab sh, TailTab tt,
-                  const ResFacts* __restrict__ facts) {
-  __shared__ uint8_t s_sv[SHAPE_REGS][BLOCK];  // the wave's resources' verdicts of the first SHAPE_REGS shapes
-  const View& v = *vp;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t w = blockIdx.x;
-  const uint32_t r0 = w * BLOCK;
-  const uint32_t rr = r0 + lane;
-  const bool active = rr < v.nres;
-  const uint32_t cls = active ? v.hdr[rr].kclass : 0u;
-  const uint32_t c0 = __builtin_amdgcn_readfirstlane(cls);
-  if (__ballot(active && cls != c0)) return;  // a mixed wave: match_rec_kernel
-  if (active) KYV_ACCT_ADD(0, 4 + sizeof(ResFacts));  // header: kind class; the resource's facts (read per tile below)
-#pragma unroll
-  for (uint32_t q = 0; q < SHAPE_REGS; q++)
-    if (q < sh.nshapes) s_sv[q][lane] = active ? sh.st[(size_t)q * v.nres + rr] : (uint8_t)0;
-  __syncthreads();
-  const uint32_t nact = v.nres - r0 < BLOCK ? v.nres - r0 : BLOCK;
-  const uint32_t i0 = sld32(tix.off + c0), i1 = sld32(tix.off + c0 + 1);
-  for (uint32_t t = i0; t < i1; t += BLOCK) {
-    const uint32_t i = t + lane;
-    const bool has = i < i1;
-    MRec R;
-    if (has) {
-      R = tix.recs[i];
-    } else {
-      R.k = 0; R.bits = 0; R.kind = 0; R.flags = 0;
-    }
-    const uint32_t k = R.k;
-    const uint32_t shape = (R.kind >> 8) & 0x7FFFu, rkind = R.kind & 0xFFu;
-    const bool wide = (R.kind >> 23) & 1u;
-    const bool fb = rkind == RK_FALLBACK;
-    const size_t list = (size_t)(k - o.rule_lo) * wl.nwaves + w;
-    FailRec* chunk = has && shape ? o.stage + o.rbase[k - o.rule_lo] + (size_t)w * WAVE : nullptr;
-    uint32_t nrec = 0, nwalk = 0;
-    for (uint32_t j = 0; j < nact; j++) {
-      const uint32_t r = r0 + j;
-      const ResFacts* fp = facts + r;
-      const MFacts mf = sld(&fp->mf);
-      const LaneTail lt = sld(&fp->lt);
-      const uint32_t hflags = sld32(&fp->hflags), hroot = sld32(&fp->hroot);
-      KYV_ACCT_ADD(0, has ? 16 : 0);  // header words the match program compares (model, as pair_match)
-      bool nd = false;
-      bool mt = has && match_fast<true>(v, R.bits, R.f, mf, tt, lt, &nd);
-      if (R.bits & MR_EMPTY) {  // the retry against the empty OldResource: a constant of the rule
-        nd = nd | (!mt & ((R.bits & MR_END) != 0));
-        mt = mt | ((R.bits & MR_EMATCH) != 0);
-      }
-      mt = mt & has;
-      uint8_t st = !mt ? (uint8_t)ST_NONE : nd ? (uint8_t)ST_ND : fb ? (uint8_t)ST_FALLBACK : (uint8_t)ST_NONE;
-      const bool m = mt & !nd & !fb;
-      if (m) {
-        if (hflags & RF_MAGIC) {
-          st = ST_FALLBACK;  // pattern pairs on such resources go to the CPU engine
-        } else if (shape) {
-          const uint32_t sx = shape - 1;
-          st = sx < SHAPE_REGS ? s_sv[sx][j] : sh.st[(size_t)sx * v.nres + r];
-          KYV_ACCT_ADD(0, 1);
-          if ((st & 7u) == ST_FAIL) {
-            FailRec f = sh.rec[(size_t)sx * v.nres + r];
-            KYV_ACCT_ADD(0, sizeof(FailRec));
-            if (wide) {  // a rule with metadata-expansion sites: whole records (resolved keys)
-              f.rule = k;
-              chunk[nrec] = f;
-              KYV_ACCT_ADD(2, sizeof(FailRec));
-            } else {
-              StageRec x;
-              x.tmpl = f.tmpl;
-              x.lane_alt = j | ((uint32_t)f.alt << 8);
-              for (int q = 0; q < MAX_IDX; q++) x.idx[q] = f.idx[q];
-              reinterpret_cast<StageRec*>(chunk)[nrec] = x;
-              KYV_ACCT_ADD(2, sizeof(StageRec));
-            }
-            nrec++;
-          }
-        } else if (rkind == RK_PATTERN || rkind == RK_ANYPATTERN) {
-          wl.items[list * WAVE + nwalk] = make_uint2(r | ((hflags & RF_ROOT_MAP) ? ITEM_ROOT_MAP : 0u), hroot);
-          KYV_ACCT_ADD(1, 8);  // work-list item
-          nwalk++;
-        }
-      }
-      const bool walked = m && !shape && !(hflags & RF_MAGIC) && (rkind == RK_PATTERN || rkind == RK_ANYPATTERN);
-      if (!walked && st != ST_NONE) { o.status[(size_t)k * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }
-    }
-    if (has) {
-      if (shape) {
-        if (nrec) { o.rcnt[(size_t)(k - o.rule_lo) * sh.nwaves + w] = (uint16_t)nrec; KYV_ACCT_ADD(1, 2); }
-      } else if (rkind == RK_PATTERN || rkind == RK_ANYPATTERN) {
-        wl.cnt[list] = (uint8_t)nwalk;
-        KYV_ACCT_ADD(1, 1);
-      }
-    }
   }
 }
 
