@@ -1861,12 +1861,8 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       HIP_OK(hipModuleLaunchKernel(acct ? dr->ajshapes : dr->jshapes, sgrid, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr));
     }
     bool any_rec = false;
-    size_t nrec_all = 0;
-    for (auto& sl : d.slices) { any_rec = any_rec || sl.nmr; nrec_all += sl.nmr; }
-    // the facts table pays off when many records (or several slices) read it; a handful of records compute the lane's
-    // facts in match_rec_kernel itself (C5: 8 records -- the table's 128 MB write cost more than it saved)
-    static const size_t facts_min = getenv("KYV_FACTS_MIN") ? (size_t)atol(getenv("KYV_FACTS_MIN")) : 64;
-    const bool use_facts = any_rec && d.facts_on && d.tcfg && nres && (d.slices.size() > 1 || nrec_all >= facts_min);
+    for (auto& sl : d.slices) any_rec = any_rec || sl.nmr;
+    const bool use_facts = any_rec && d.facts_on && d.tcfg && nres;
     if (use_facts) {  // the match records' resource facts, once per evaluation (read by every slice)
       if (!d.facts) HIP_OK(dmalloc(&d.facts, nres * sizeof(ResFacts)));
       const dim3 fg((unsigned)((nres + 255) / 256));
