@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "libkyvgpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KYV_OFFLOAD_ARCH", "gfx950")
 
-HOST_SRCS = ["pjson.cpp", "compiler.cpp", "batch.cpp", "capi.cpp", "jit.cpp", "pss_msg.cpp", "typed.cpp"]
+HOST_SRCS = ["pjson.cpp", "compiler.cpp", "batch.cpp", "capi.cpp", "jit.cpp", "pss_msg.cpp", "typed.cpp", "regex.cpp"]
 HIP_SRCS = ["kyv_prod_j.hip", "kyv_acct_j.hip", "kyv_prod.hip", "kyv_acct.hip", "kyv_engine.hip"]
 HEADERS = ["kyv_layout.h", "kyv_eval.h", "kyv_cond.h", "kyv_pss.h", "kyv_host.h", "pjson.h", "kyv_wave.h", "kyv_walk.h", "kyv_jcond.h", "kyv_kernels.h", "kyv_acct.h", "kyv_fused.h", "k8s_types.h", "kyv_launch.inc"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-value", "-Wno-unused-function", "-Wno-unused-variable",

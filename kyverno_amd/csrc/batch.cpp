@@ -953,6 +953,44 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
           b->nsl_off.push_back((uint32_t)b->nsl_kv.size() / 2);
         }
     }
+    // to_upper on the dictionary (round 6, kyverno functions.go:681-689 strings.ToUpper): every string's upper-case
+    // form, interned so that a result compares, globs and parses like any other dictionary string; strings with no
+    // lowercase letter map to themselves, non-ASCII strings to NONE (their pairs go to the CPU engine). The lookups run
+    // in parallel over the finished shards; only strings the batch does not hold yet are interned, serially.
+    if (rs->uses_upper) {
+      const size_t n0 = b->dict.strs.size();
+      std::vector<uint32_t> up(n0, NONE);
+      std::vector<uint8_t> todo(n0, 0);
+      parallel_for(std::max<size_t>(1, std::min<size_t>((size_t)T * 4, n0 / 4096 + 1)), T, [&](size_t k) {
+        const size_t nk = std::max<size_t>(1, std::min<size_t>((size_t)T * 4, n0 / 4096 + 1));
+        for (size_t s2 = n0 * k / nk; s2 < n0 * (k + 1) / nk; s2++) {
+          const std::string& x = b->dict.strs[s2];
+          bool lower = false, ascii = true;
+          for (unsigned char ch : x) { ascii = ascii && ch < 0x80; lower = lower || (ch >= 'a' && ch <= 'z'); }
+          if (!ascii) continue;
+          if (!lower) { up[s2] = (uint32_t)s2; continue; }
+          std::string u = x;
+          for (char& ch : u) if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 'a' + 'A');
+          const uint64_t h = hash_bytes(u.data(), u.size());
+          uint32_t id = seedtab.find(u, h);
+          if (id == NONE) {
+            id = shard[shard_of(h)].find(u, h);
+            if (id != NONE) id = (uint32_t)(shbase[shard_of(h)] + id);
+          }
+          if (id != NONE) up[s2] = id;
+          else todo[s2] = 1;
+        }
+      });
+      for (size_t s2 = 0; s2 < n0; s2++)
+        if (todo[s2]) {
+          std::string u = b->dict.strs[s2];
+          for (char& ch : u) if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 'a' + 'A');
+          up[s2] = intern(u);
+        }
+      b->str_upper.assign(b->dict.strs.size(), 0);
+      for (size_t s2 = 0; s2 < b->dict.strs.size(); s2++) b->str_upper[s2] = s2 < n0 ? up[s2] : (uint32_t)s2;
+      phase("upper");
+    }
     // concatenate + remap + sort map entries by key id (+ labels / annotations entries found again after the sort)
     size_t total_nodes = 0, total_res = 0, total_faux = 0;
     std::vector<size_t> node_base(nchunks), res_base(nchunks), faux_base(nchunks);
@@ -1043,10 +1081,34 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
     phase("remap");
     derive_strings(*b, 0, std::max(1, std::min(T, (int)(b->dict.strs.size() / 8192) + 1)));
     phase("strings");
+    // regex_match on the dictionary (round 6, kyverno functions.go:786-799 regexp.Match): bit q of a string = its match
+    // by the ruleset's regex q (regex.cpp DFA, the device subset), RX_FB for a string with a byte outside printable
+    // ASCII (its pairs go to the CPU engine)
+    if (!rs->rxs.empty()) {
+      const size_t ns = b->dict.strs.size();
+      b->str_rx.assign(ns, 0);
+      const size_t nk = std::max<size_t>(1, std::min<size_t>((size_t)T * 4, ns / 4096 + 1));
+      parallel_for(nk, T, [&](size_t k) {
+        for (size_t s2 = ns * k / nk; s2 < ns * (k + 1) / nk; s2++) {
+          const std::string& x = b->dict.strs[s2];
+          uint32_t bits = 0;
+          for (size_t q = 0; q < rs->rxs.size(); q++) {
+            const int m = rx_match(rs->rxs[q], (const uint8_t*)x.data(), x.size());
+            if (m < 0) { bits = RX_FB; break; }
+            if (m) bits |= 1u << q;
+          }
+          b->str_rx[s2] = bits;
+        }
+      });
+      phase("regex");
+    }
     order_by_kind(*b);
     phase("kind-order");
     resolve_path_columns(*b, T);
     phase("path-cols");
+    if ((!b->str_upper.empty() && b->str_upper.size() != b->dict.strs.size()) ||
+        (!b->str_rx.empty() && b->str_rx.size() != b->dict.strs.size()))
+      throw std::runtime_error("internal: per-string JMESPath columns do not cover the dictionary");
     return b.release();
   } catch (std::exception& e) {
     if (err) *err = e.what();

@@ -805,9 +805,13 @@ struct kyv_comm {
   uint32_t* nwide = nullptr;   // [1] side-entry count (report_rows_kernel)
   unsigned long long* sums = nullptr;  // kyv_comm_reduce_counts: [rules * NSTATUS + 1]
   size_t sums_cap = 0;
+  // device buffer of the size / flag exchanges ([nranks + 1][kXK] int64), allocated once in kyv_comm_init so that an
+  // exchange never allocates: a rank always reaches the exchange's all-gather once it has called the collective
+  int64_t* xbuf = nullptr;
 };
 
 namespace {
+constexpr int kXK = 8;  // int64 fields per rank one size / flag exchange carries at most
 int nccl_fail(ncclResult_t r, const char* what) {
   return fail(KYV_EDEVICE, std::string(what) + ": " + ncclGetErrorString(r));
 }
@@ -843,9 +847,19 @@ int kyv_comm_init(const uint8_t* id, size_t len, int nranks, int rank, int devic
   memcpy(&u, id, sizeof u);
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e != hipSuccess) { delete c; return fail(KYV_EDEVICE, std::string("comm stream: ") + hipGetErrorString(e)); }
+  if (e == hipSuccess) e = hipMalloc((void**)&c->xbuf, sizeof(int64_t) * kXK * (nranks + 1));
+  if (e != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return fail(KYV_EDEVICE, std::string("comm stream / exchange buffer: ") + hipGetErrorString(e));
+  }
   ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
-  if (r != ncclSuccess) { (void)hipStreamDestroy(c->stream); delete c; return nccl_fail(r, "ncclCommInitRank"); }
+  if (r != ncclSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    (void)hipFree(c->xbuf);
+    delete c;
+    return nccl_fail(r, "ncclCommInitRank");
+  }
   *out = c;
   return KYV_OK;
 }
@@ -860,62 +874,98 @@ void kyv_comm_free(kyv_comm* c) {
   if (c->rwide) (void)hipFree(c->rwide);
   if (c->nwide) (void)hipFree(c->nwide);
   if (c->sums) (void)hipFree(c->sums);
+  if (c->xbuf) (void)hipFree(c->xbuf);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
 namespace {
-// one small all-gather of k int64 per rank (sizes and flags) -> out[nranks * k]
+// One small all-gather of k int64 per rank (sizes and ok flags) -> out[nranks * k], through the communicator's own
+// exchange buffer (no allocation). The all-gather is posted whatever happened before it on this rank: the collectives
+// of a report gather are only ever entered behind such an exchange, and every rank leaves the exchange with the same
+// view of every rank's flags (a failed upload of this rank's entries returns an error here after the collective).
 int exchange_sizes(kyv_comm* c, const int64_t* mine, int k, std::vector<int64_t>* out) {
   const int n = c->nranks;
-  int64_t* dsz = nullptr;
-  KYV_HIPC(hipMalloc((void**)&dsz, sizeof(int64_t) * k * (n + 1)));
-  struct Free { void* p; ~Free() { (void)hipFree(p); } } fz{dsz};
-  KYV_HIPC(hipMemcpyAsync(dsz + (size_t)k * n, mine, sizeof(int64_t) * k, hipMemcpyHostToDevice, c->stream));
-  KYV_NCCL(ncclAllGather(dsz + (size_t)k * n, dsz, k, ncclInt64, c->comm, c->stream));
+  if (k < 1 || k > kXK) return fail(KYV_EINTERNAL, "size exchange wider than the exchange buffer");
+  int64_t* send = c->xbuf + (size_t)kXK * n;
+  const hipError_t up = hipMemcpyAsync(send, mine, sizeof(int64_t) * k, hipMemcpyHostToDevice, c->stream);
+  KYV_NCCL(ncclAllGather(send, c->xbuf, k, ncclInt64, c->comm, c->stream));
   out->assign((size_t)k * n, 0);
-  KYV_HIPC(hipMemcpyAsync(out->data(), dsz, sizeof(int64_t) * k * n, hipMemcpyDeviceToHost, c->stream));
+  KYV_HIPC(hipMemcpyAsync(out->data(), c->xbuf, sizeof(int64_t) * k * n, hipMemcpyDeviceToHost, c->stream));
   KYV_HIPC(hipStreamSynchronize(c->stream));
+  if (up != hipSuccess) return fail(KYV_EDEVICE, std::string("upload of the exchanged sizes: ") + hipGetErrorString(up));
   return KYV_OK;
 }
 // every rank's ok flag (field f of k per rank): all ranks return the same error when any is 0
-int check_flags(kyv_comm* c, const std::vector<int64_t>& sz, int k, int f, const std::string& why) {
+int check_flags(kyv_comm* c, const std::vector<int64_t>& sz, int k, int f, const std::string& why,
+                const char* what = "has no exportable results") {
   for (int q = 0; q < c->nranks; q++)
     if (!sz[(size_t)k * q + f])
-      return fail(KYV_EDEVICE, "report gather: rank " + std::to_string(q) + " has no exportable results" +
+      return fail(KYV_EDEVICE, "report gather: rank " + std::to_string(q) + " " + what +
                                (q == c->rank && !why.empty() ? ": " + why : std::string()));
   return KYV_OK;
 }
+// one flag exchange: every rank continues only when every rank's local step (buffers, exports) succeeded
+int agree(kyv_comm* c, bool ok, const std::string& why) {
+  const int64_t f = ok ? 1 : 0;
+  std::vector<int64_t> sz;
+  if (int rc = exchange_sizes(c, &f, 1, &sz)) return rc;
+  return check_flags(c, sz, 1, 0, why, "could not prepare its buffers");
+}
+// HIP-event timing of a gather; a failure to create or record an event costs the timing only, never the collective
+struct GatherTimer {
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  GatherTimer() {
+    for (auto& x : e)
+      if (hipEventCreate(&x) != hipSuccess) x = nullptr;
+  }
+  ~GatherTimer() { for (auto x : e) if (x) (void)hipEventDestroy(x); }
+  void mark(int i, hipStream_t s) { if (e[i] && hipEventRecord(e[i], s) != hipSuccess) e[i] = nullptr; }
+  float ms(int a, int b) const {
+    float t = 0;
+    return e[a] && e[b] && hipEventElapsedTime(&t, e[a], e[b]) == hipSuccess ? t : 0.f;
+  }
+};
+// the local preparation steps of a gather record their first failure here instead of returning: the rank still joins
+// the flag exchange that follows (a rank returning early would leave its peers inside the collective)
+struct LocalOk {
+  bool ok = true;
+  std::string why;
+  void hip(hipError_t e, const char* what) {
+    if (ok && e != hipSuccess) { ok = false; why = std::string(what) + ": " + hipGetErrorString(e); }
+  }
+  void rc(int r, const char* what) {
+    if (ok && r != KYV_OK) { ok = false; why = std::string(what) + ": " + kyv_last_error(); }
+  }
+  void ex(const std::exception& e) { if (ok) { ok = false; why = e.what(); } }
+};
 }  // namespace
 
 int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset, kyv_gather_stats* st) {
   if (!c || !b || !st) return fail(KYV_EINVAL, "null argument");
   try {
-    KYV_HIPC(hipSetDevice(c->device));
     *st = kyv_gather_stats{};
-    hipEvent_t e0, e1, e2;
-    KYV_HIPC(hipEventCreate(&e0));
-    KYV_HIPC(hipEventCreate(&e1));
-    KYV_HIPC(hipEventCreate(&e2));
-    struct Ev { hipEvent_t a, b, c; ~Ev() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); (void)hipEventDestroy(c); } } ev{e0, e1, e2};
     const int n = c->nranks;
     c->mode = 0;
     c->row_counts.clear();
     // sizes of every rank (one small all-gather): verdict bytes, failing-path rows and an ok flag. A rank that cannot
     // take part (no resident results, rows over the resident buffer) still joins this exchange with flag 0, and every
     // rank returns the same error: no rank is left waiting in a collective its peers never enter
-    int64_t mine[3] = {0, 0, 1};
-    std::string why;
-    try {
-      mine[0] = export_status(*b->b, c->device, nullptr, 0, c->stream);
-      mine[1] = export_failures(*b->b, c->device, res_offset, nullptr, 0, c->stream);
-    } catch (std::exception& e) {
-      mine[2] = 0;
-      why = e.what();
+    LocalOk lk;
+    lk.hip(hipSetDevice(c->device), "hipSetDevice");
+    int64_t mine[3] = {0, 0, 0};
+    if (lk.ok) {
+      try {
+        mine[0] = export_status(*b->b, c->device, nullptr, 0, c->stream);
+        mine[1] = export_failures(*b->b, c->device, res_offset, nullptr, 0, c->stream);
+      } catch (std::exception& e) {
+        lk.ex(e);
+      }
     }
+    mine[2] = lk.ok ? 1 : 0;
     std::vector<int64_t> sz;
     if (int rc = exchange_sizes(c, mine, 3, &sz)) return rc;
-    if (int rc = check_flags(c, sz, 3, 2, why)) return rc;
+    if (int rc = check_flags(c, sz, 3, 2, lk.why)) return rc;
     size_t smax = 0, rmax = 0;
     c->row_counts.assign(n, 0);
     for (int q = 0; q < n; q++) {
@@ -924,29 +974,32 @@ int kyv_comm_gather_results(kyv_comm* c, const kyv_batch* b, int64_t res_offset,
       c->row_counts[q] = sz[3 * q + 1];
       st->failure_rows_total += (uint64_t)sz[3 * q + 1];
     }
-    if (int rc = grow(&c->status, &c->status_cap, smax * (n + 1))) return rc;
-    if (int rc = grow(&c->rows, &c->rows_cap, rmax * 8 * (n + 1))) return rc;
+    // local: the buffers and this rank's send data; then every rank agrees before the all-gathers
+    GatherTimer tm;
+    lk.rc(grow(&c->status, &c->status_cap, smax * (n + 1)), "verdict buffer");
+    lk.rc(grow(&c->rows, &c->rows_cap, rmax * 8 * (n + 1)), "row buffer");
+    uint8_t* sendv = lk.ok ? c->status + smax * n : nullptr;  // this rank's packed verdicts, all-gathered into [0, n * smax)
+    int64_t* sendr = lk.ok ? c->rows + rmax * 8 * n : nullptr;
+    tm.mark(0, c->stream);
+    if (lk.ok) {
+      try {
+        if (smax) export_status(*b->b, c->device, sendv, smax, c->stream);
+        if (rmax) export_failures(*b->b, c->device, res_offset, sendr, rmax, c->stream);
+      } catch (std::exception& e) {
+        lk.ex(e);
+      }
+    }
+    if (int rc = agree(c, lk.ok, lk.why)) return rc;
     c->status_bytes = smax;
     c->rows_max = rmax;
-    uint8_t* sendv = c->status + smax * n;  // this rank's packed verdicts, then the all-gather into [0, n * smax)
-    int64_t* sendr = c->rows + rmax * 8 * n;
-    KYV_HIPC(hipEventRecord(e0, c->stream));
-    if (smax) {
-      export_status(*b->b, c->device, sendv, smax, c->stream);
-      KYV_NCCL(ncclAllGather(sendv, c->status, smax, ncclUint8, c->comm, c->stream));
-    }
-    KYV_HIPC(hipEventRecord(e1, c->stream));
-    if (rmax) {
-      export_failures(*b->b, c->device, res_offset, sendr, rmax, c->stream);
-      KYV_NCCL(ncclAllGather(sendr, c->rows, rmax * 8, ncclInt64, c->comm, c->stream));
-    }
-    KYV_HIPC(hipEventRecord(e2, c->stream));
+    // only collectives from here on
+    if (smax) KYV_NCCL(ncclAllGather(sendv, c->status, smax, ncclUint8, c->comm, c->stream));
+    tm.mark(1, c->stream);
+    if (rmax) KYV_NCCL(ncclAllGather(sendr, c->rows, rmax * 8, ncclInt64, c->comm, c->stream));
+    tm.mark(2, c->stream);
     KYV_HIPC(hipStreamSynchronize(c->stream));
-    float t0 = 0, t1 = 0;
-    KYV_HIPC(hipEventElapsedTime(&t0, e0, e1));
-    KYV_HIPC(hipEventElapsedTime(&t1, e1, e2));
-    st->status_ms = t0;
-    st->failures_ms = t1;
+    st->status_ms = tm.ms(0, 1);
+    st->failures_ms = tm.ms(1, 2);
     st->status_bytes_per_rank = smax;
     st->failure_rows_per_rank_max = rmax;
     c->mode = 1;
@@ -1027,54 +1080,52 @@ int64_t kyv_comm_gathered_failures(const kyv_comm* c, int rank, int64_t* host_ds
 // (2 bits per pair) + 16 B per failing-path row; the root receives the sum over the other ranks.
 int kyv_comm_gather_report(kyv_comm* c, const kyv_batch* b, int64_t res_offset, int root, kyv_gather_stats* st) {
   if (!c || !b || !st) return fail(KYV_EINVAL, "null argument");
-  if (root < 0 || root >= c->nranks) return fail(KYV_EINVAL, "bad root rank");
+  if (root < 0 || root >= c->nranks) return fail(KYV_EINVAL, "bad root rank");  // the same on every rank
   try {
-    KYV_HIPC(hipSetDevice(c->device));
     *st = kyv_gather_stats{};
     c->mode = 0;
     const int n = c->nranks;
-    if (!c->nwide) KYV_HIPC(hipMalloc((void**)&c->nwide, 4));
-    // this rank's rows, packed now (their side-entry count is part of the size exchange)
-    int64_t mine[5] = {0, 0, 0, 1, res_offset};
-    std::string why;
-    try {
-      mine[0] = export_status(*b->b, c->device, nullptr, 0, c->stream);
-      mine[1] = export_report_rows(*b->b, c->device, nullptr, nullptr, nullptr, 0, 0, c->stream);
-    } catch (std::exception& e) {
-      mine[3] = 0;
-      why = e.what();
-    }
-    hipEvent_t e0, e1, e2;
-    KYV_HIPC(hipEventCreate(&e0));
-    KYV_HIPC(hipEventCreate(&e1));
-    KYV_HIPC(hipEventCreate(&e2));
-    struct Ev { hipEvent_t a, b, c; ~Ev() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); (void)hipEventDestroy(c); } } ev{e0, e1, e2};
     const bool me_root = c->rank == root;
-    // receive layout on the root: every rank's segment at exact offsets; elsewhere: this rank's own data only
-    const size_t own_rows = mine[3] ? (size_t)std::max<int64_t>(mine[1], 0) : 0;
-    std::vector<int64_t> sz;
-    // this rank's rows and side entries are packed before the exchange (the side-entry count is part of it) into
-    // temporaries: the senders send from them, the root moves its own into its receive segments
+    // Local steps before the size exchange (each failure joins the exchange with flag 0): the device, this rank's
+    // sizes, and its rows packed now into temporaries (the side-entry count is part of the exchange); the senders send
+    // from them, the root moves its own into its receive segments
+    LocalOk lk;
+    lk.hip(hipSetDevice(c->device), "hipSetDevice");
+    if (lk.ok && !c->nwide) lk.hip(hipMalloc((void**)&c->nwide, 4), "side-entry counter");
+    int64_t mine[5] = {0, 0, 0, 0, res_offset};
+    if (lk.ok) {
+      try {
+        mine[0] = export_status(*b->b, c->device, nullptr, 0, c->stream);
+        mine[1] = export_report_rows(*b->b, c->device, nullptr, nullptr, nullptr, 0, 0, c->stream);
+      } catch (std::exception& e) {
+        lk.ex(e);
+      }
+    }
+    const size_t own_rows = lk.ok ? (size_t)std::max<int64_t>(mine[1], 0) : 0;
     uint32_t *packed = nullptr, *pwide = nullptr;
     struct Free { void* p; ~Free() { if (p) (void)hipFree(p); } } fp{nullptr}, fw{nullptr};
     if (own_rows) {
-      KYV_HIPC(hipMalloc((void**)&packed, own_rows * 16));
-      fp.p = packed;
-      KYV_HIPC(hipMalloc((void**)&pwide, own_rows * 16));
-      fw.p = pwide;
-      try {
-        export_report_rows(*b->b, c->device, packed, pwide, c->nwide, own_rows, own_rows, c->stream);
-        uint32_t nw = 0;
-        KYV_HIPC(hipMemcpyAsync(&nw, c->nwide, 4, hipMemcpyDeviceToHost, c->stream));
-        KYV_HIPC(hipStreamSynchronize(c->stream));
-        mine[2] = nw;
-      } catch (std::exception& e) {
-        mine[3] = 0;
-        why = e.what();
+      lk.hip(hipMalloc((void**)&packed, own_rows * 16), "row buffer");
+      if (lk.ok) fp.p = packed;
+      if (lk.ok) lk.hip(hipMalloc((void**)&pwide, own_rows * 16), "side-entry buffer");
+      if (lk.ok) fw.p = pwide;
+      if (lk.ok) {
+        try {
+          export_report_rows(*b->b, c->device, packed, pwide, c->nwide, own_rows, own_rows, c->stream);
+          uint32_t nw = 0;
+          lk.hip(hipMemcpyAsync(&nw, c->nwide, 4, hipMemcpyDeviceToHost, c->stream), "side-entry count");
+          if (lk.ok) lk.hip(hipStreamSynchronize(c->stream), "row export");
+          mine[2] = nw;
+        } catch (std::exception& e) {
+          lk.ex(e);
+        }
       }
     }
+    mine[3] = lk.ok ? 1 : 0;
+    std::vector<int64_t> sz;
     if (int rc = exchange_sizes(c, mine, 5, &sz)) return rc;
-    if (int rc = check_flags(c, sz, 5, 3, why)) return rc;
+    if (int rc = check_flags(c, sz, 5, 3, lk.why)) return rc;
+    // receive layout on the root: every rank's segment at exact offsets (the same on every rank: from the exchange)
     c->root = root;
     c->seg_status.assign(n, 0);
     c->seg_rows.assign(n, 0);
@@ -1098,15 +1149,31 @@ int kyv_comm_gather_report(kyv_comm* c, const kyv_batch* b, int64_t res_offset, 
       st->failure_rows_total += (uint64_t)sz[5 * q + 1];
     }
     const size_t my_s = (size_t)mine[0], my_w = (size_t)mine[2];
-    // buffers: the root holds every segment; a sender only its own verdicts (the rows are sent from `packed`)
-    if (int rc = grow(&c->status, &c->status_cap, me_root ? ts : my_s)) return rc;
+    // Local steps after the size exchange: the buffers (the root holds every segment; a sender only its own verdicts,
+    // its rows are sent from `packed`), this rank's packed verdicts exported into place and the root's own rows moved
+    // into its segments -- then one flag exchange, and from there only the grouped sends / receives
+    GatherTimer tm;
+    lk.rc(grow(&c->status, &c->status_cap, me_root ? ts : my_s), "verdict buffer");
     if (me_root) {
-      if (int rc = grow(&c->rrows, &c->rrows_cap, tr * 4)) return rc;
-      if (int rc = grow(&c->rwide, &c->rwide_cap, tw * 4)) return rc;
+      lk.rc(grow(&c->rrows, &c->rrows_cap, tr * 4), "row receive buffer");
+      lk.rc(grow(&c->rwide, &c->rwide_cap, tw * 4), "side-entry receive buffer");
     }
-    KYV_HIPC(hipEventRecord(e0, c->stream));
-    uint8_t* my_status = c->status + (me_root ? c->at_status[root] : 0);
-    if (my_s) export_status(*b->b, c->device, my_status, my_s, c->stream);
+    uint8_t* my_status = lk.ok ? c->status + (me_root ? c->at_status[root] : 0) : nullptr;
+    tm.mark(0, c->stream);
+    if (lk.ok && my_s) {
+      try {
+        export_status(*b->b, c->device, my_status, my_s, c->stream);
+      } catch (std::exception& e) {
+        lk.ex(e);
+      }
+    }
+    if (lk.ok && me_root && own_rows)
+      lk.hip(hipMemcpyAsync(c->rrows + c->at_rows[root] * 4, packed, own_rows * 16, hipMemcpyDeviceToDevice, c->stream),
+             "root's own rows");
+    if (lk.ok && me_root && my_w)
+      lk.hip(hipMemcpyAsync(c->rwide + c->at_wide[root] * 4, pwide, my_w * 16, hipMemcpyDeviceToDevice, c->stream),
+             "root's own side entries");
+    if (int rc = agree(c, lk.ok, lk.why)) return rc;
     KYV_NCCL(ncclGroupStart());
     if (me_root) {
       for (int q = 0; q < n; q++)
@@ -1116,11 +1183,7 @@ int kyv_comm_gather_report(kyv_comm* c, const kyv_batch* b, int64_t res_offset, 
       KYV_NCCL(ncclSend(my_status, my_s, ncclUint8, root, c->comm, c->stream));
     }
     KYV_NCCL(ncclGroupEnd());
-    KYV_HIPC(hipEventRecord(e1, c->stream));
-    if (me_root && own_rows)
-      KYV_HIPC(hipMemcpyAsync(c->rrows + c->at_rows[root] * 4, packed, own_rows * 16, hipMemcpyDeviceToDevice, c->stream));
-    if (me_root && my_w)
-      KYV_HIPC(hipMemcpyAsync(c->rwide + c->at_wide[root] * 4, pwide, my_w * 16, hipMemcpyDeviceToDevice, c->stream));
+    tm.mark(1, c->stream);
     KYV_NCCL(ncclGroupStart());
     if (me_root) {
       for (int q = 0; q < n; q++) {
@@ -1135,13 +1198,10 @@ int kyv_comm_gather_report(kyv_comm* c, const kyv_batch* b, int64_t res_offset, 
       if (my_w) KYV_NCCL(ncclSend(pwide, my_w * 4, ncclUint32, root, c->comm, c->stream));
     }
     KYV_NCCL(ncclGroupEnd());
-    KYV_HIPC(hipEventRecord(e2, c->stream));
+    tm.mark(2, c->stream);
     KYV_HIPC(hipStreamSynchronize(c->stream));
-    float t0 = 0, t1 = 0;
-    KYV_HIPC(hipEventElapsedTime(&t0, e0, e1));
-    KYV_HIPC(hipEventElapsedTime(&t1, e1, e2));
-    st->status_ms = t0;
-    st->failures_ms = t1;
+    st->status_ms = tm.ms(0, 1);
+    st->failures_ms = tm.ms(1, 2);
     st->status_bytes_per_rank = my_s;
     st->failure_rows_per_rank_max = 0;
     for (int q = 0; q < n; q++) st->failure_rows_per_rank_max = std::max<uint64_t>(st->failure_rows_per_rank_max, (uint64_t)c->seg_rows[q]);
@@ -1161,34 +1221,35 @@ int kyv_comm_gather_report(kyv_comm* c, const kyv_batch* b, int64_t res_offset, 
 int64_t kyv_comm_reduce_counts(kyv_comm* c, const kyv_batch* b, int64_t* host_out, size_t cap) {
   if (!c || !b) return fail(KYV_EINVAL, "null argument"), -1;
   try {
-    if (hipSetDevice(c->device) != hipSuccess) return fail(KYV_EDEVICE, "hipSetDevice"), -1;
+    LocalOk lk;
+    lk.hip(hipSetDevice(c->device), "hipSetDevice");
     size_t nrules = 0, nres = 0;
     const unsigned long long* cnt = nullptr;
-    std::string why;
-    try {
-      cnt = device_counts(*b->b, c->device, &nrules, &nres);
-    } catch (std::exception& e) {
-      why = e.what();
+    if (lk.ok) {
+      try {
+        cnt = device_counts(*b->b, c->device, &nrules, &nres);
+      } catch (std::exception& e) {
+        lk.ex(e);
+      }
     }
     const size_t ne = nrules * NSTATUS;
-    if (!host_out) {
-      if (!cnt) return fail(KYV_EINVAL, why), -1;
-      return (int64_t)ne;
-    }
-    // sizes + flags first: every rank must reduce the same element count
-    int64_t mine[2] = {(int64_t)ne, cnt ? 1 : 0};
+    // size query (no collective): never an error, so that a caller sizing its buffer always goes on to make the
+    // collective call; a rank without results answers 0 and fails below together with its peers
+    if (!host_out) return cnt ? (int64_t)ne : 0;
+    // local steps first (every rank must reduce the same element count, into a buffer large enough): their outcome
+    // is the ok flag of the size exchange
+    if (lk.ok && !cnt) { lk.ok = false; lk.why = "no device-resident verdict tallies"; }
+    if (lk.ok && cap < ne) { lk.ok = false; lk.why = "buffer too small"; }
+    lk.rc(grow(&c->sums, &c->sums_cap, ne + 1), "tally buffer");
+    const unsigned long long nr = nres;
+    if (lk.ok && ne) lk.hip(hipMemcpyAsync(c->sums, cnt, ne * 8, hipMemcpyDeviceToDevice, c->stream), "tally copy");
+    if (lk.ok) lk.hip(hipMemcpyAsync(c->sums + ne, &nr, 8, hipMemcpyHostToDevice, c->stream), "resource count copy");
+    int64_t mine[2] = {(int64_t)ne, lk.ok ? 1 : 0};
     std::vector<int64_t> sz;
     if (exchange_sizes(c, mine, 2, &sz)) return -1;
-    if (check_flags(c, sz, 2, 1, why)) return -1;
+    if (check_flags(c, sz, 2, 1, lk.why, "cannot reduce its tallies")) return -1;
     for (int q = 0; q < c->nranks; q++)
       if (sz[2 * q] != (int64_t)ne) return fail(KYV_EINVAL, "ranks evaluated different rulesets"), -1;
-    if (cap < ne) return fail(KYV_ERANGE, "buffer too small"), -1;
-    if (grow(&c->sums, &c->sums_cap, ne + 1)) return -1;
-    const unsigned long long nr = nres;
-    if (ne && hipMemcpyAsync(c->sums, cnt, ne * 8, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
-      return fail(KYV_EDEVICE, "copy of the verdict tallies failed"), -1;
-    if (hipMemcpyAsync(c->sums + ne, &nr, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
-      return fail(KYV_EDEVICE, "copy of the resource count failed"), -1;
     ncclResult_t r = ncclAllReduce(c->sums, c->sums, ne + 1, ncclUint64, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) return nccl_fail(r, "ncclAllReduce"), -1;
     std::vector<unsigned long long> h(ne + 1);

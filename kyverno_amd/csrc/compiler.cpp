@@ -1131,11 +1131,23 @@ struct JParser {
         i = j;
         continue;
       }
-      if (c == '"' || c == '\'' || c == '`') {
+      if (c == '\'') {  // raw string (lexer.go consumeRawStringLiteral): \' is a quote, other backslashes stay
+        std::string v;
+        size_t j = i + 1;
+        for (; j < s.size() && s[j] != '\''; j++) {
+          if (s[j] == '\\' && j + 1 < s.size() && s[j + 1] == '\'') { v += '\''; j++; continue; }
+          v += s[j];
+        }
+        if (j >= s.size()) throw Fallback{"JMESPath: unterminated literal"};
+        toks.push_back({Raw, v});
+        i = j + 1;
+        continue;
+      }
+      if (c == '"' || c == '`') {
         size_t j = i + 1;
         while (j < s.size() && s[j] != c) { if (s[j] == '\\') throw Fallback{"JMESPath: escapes"}; j++; }
         if (j >= s.size()) throw Fallback{"JMESPath: unterminated literal"};
-        toks.push_back({c == '"' ? Quoted : c == '\'' ? Raw : Json, s.substr(i + 1, j - i - 1)});
+        toks.push_back({c == '"' ? Quoted : Json, s.substr(i + 1, j - i - 1)});
         i = j + 1;
         continue;
       }
@@ -1315,6 +1327,14 @@ void jfilter(Cx& c, const JP& cond, std::vector<uint32_t>& out) {
   throw Fallback{"JMESPath: filter predicate"};
 }
 
+// the ops of a chain program before its function: fields, then an optional `|| literal` (kyv_layout.h jmes_chain_form)
+static bool jmes_chain_form_ops(const std::vector<uint32_t>& ops) {
+  size_t i = 0;
+  while (i + 1 < ops.size() && ops[i] == JO_FIELD) i += 2;
+  if (i + 1 < ops.size() && ops[i] == JO_OR) i += 2;
+  return i == ops.size();
+}
+
 // `{{ <expr> }}` -> OK_JMES operand (false: not a single-variable string; throws Fallback outside the subset);
 // *uses_op when the expression reads request.operation
 bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, std::string* text, bool* uses_op) {
@@ -1341,6 +1361,45 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
     if (n->kids.size() != 1) throw Fallback{"JMESPath: function"};
     n = n->kids[0];
     has_len = true;
+  }
+  // to_upper(<arg>) / regex_match('<pattern>', <arg>) (kyverno pkg/engine/jmespath/functions.go:681-689, 786-799),
+  // <arg> a field chain of request.object with an optional `|| <literal>`: the chain's ops, the default, then JO_UPPER /
+  // JO_REGEX q, evaluated on the dictionary (Batch::str_upper / str_rx, regex.cpp; kyv_cond.h jmes_chain_cv). A pattern
+  // outside the device regex subset leaves the rule on the CPU engine.
+  uint32_t post = NONE, post_q = 0;
+  if (n->k == JNode::Func && (n->name == "to_upper" || n->name == "regex_match")) {
+    if (has_or) throw Fallback{"JMESPath: function result with ||"};
+    JP arg;
+    if (n->name == "to_upper") {
+      if (n->kids.size() != 1) throw Fallback{"JMESPath: function"};
+      arg = n->kids[0];
+      post = JO_UPPER;
+    } else {
+      if (n->kids.size() != 2 || n->kids[0]->k != JNode::Lit || !n->kids[0]->lit.is(pj::T::Str))
+        throw Fallback{"JMESPath: regex_match pattern"};
+      const std::string& re = n->kids[0]->lit.s;
+      auto it = std::find(c.rs.rx_src.begin(), c.rs.rx_src.end(), re);
+      if (it == c.rs.rx_src.end()) {
+        RxDfa d;
+        std::string why;
+        if (!rx_compile(re, &d, &why)) throw Fallback{"JMESPath: regex_match pattern outside the device subset (" + why + ")"};
+        if (c.rs.rx_src.size() >= RX_MAX) throw Fallback{"JMESPath: too many regex_match patterns"};
+        c.rs.rx_src.push_back(re);
+        c.rs.rxs.push_back(std::move(d));
+        post_q = (uint32_t)c.rs.rx_src.size() - 1;
+      } else {
+        post_q = (uint32_t)(it - c.rs.rx_src.begin());
+      }
+      arg = n->kids[1];
+      post = JO_REGEX;
+    }
+    if (arg->k == JNode::Or) {
+      if (arg->kids[1]->k != JNode::Lit) throw Fallback{"JMESPath: || with a non-literal"};
+      orlit = arg->kids[1]->lit;
+      has_or = true;
+      arg = arg->kids[0];
+    }
+    n = arg;
   }
   // split the root off the left spine: request.object / request.operation / element
   std::vector<JNode*> spine;
@@ -1462,6 +1521,13 @@ bool jmes_var(Cx& c, const std::string& s, bool allow_element, CondOperand* o, s
     Value lit = pj::parse(pj::dump(orlit), false);
     fused.push_back(JO_OR);
     fused.push_back(emit_cnode(c, lit));
+  }
+  if (post != NONE) {  // the function's argument: a missing key is null, not NotFoundError
+    if (root != JR_OBJECT || !jmes_chain_form_ops(fused)) throw Fallback{"JMESPath: function of a projection / element"};
+    fused.push_back(post);
+    if (post == JO_REGEX) fused.push_back(post_q);
+    pure = false;
+    if (post == JO_UPPER) c.rs.uses_upper = true;
   }
   // request.operation: the background scan's JSON context holds "CREATE" (scanner.go:97; CLI default common.go:287)
   const uint32_t oplit = root == JR_OPERATION ? emit_cnode(c, Value::S("CREATE")) : NONE;

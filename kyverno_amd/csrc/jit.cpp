@@ -766,7 +766,8 @@ struct CondGen {
       V x = root == JR_OBJECT ? decl("0u", "T_UNK", "0u", "r", 0u, false) : decl("ei", "et", "ea", "erow", etpos, false);
       PEND = n;
       for (uint32_t q = 1; q < n;) {  // a trailing `|| lit` ends the ops
-        if (p[q] == JO_OR) { PEND = q; orlit = p[q + 1]; break; }
+        if (p[q] == JO_OR) { PEND = q; orlit = p[q + 1]; if (q + 2 < n) ok = false; break; }
+        if (p[q] == JO_UPPER || p[q] == JO_REGEX) ok = false;
         q += jop_width(p + q);
       }
       P = p;
@@ -794,7 +795,7 @@ struct CondGen {
   std::string stream_fn(const CondOperand& o, uint32_t etpos, const std::string& acc) {
     const uint32_t* p = rs.pool.data() + o.a;
     const uint32_t n = o.nseg, root = p[0] & 0xFFu;
-    if (root == JR_OPERATION || (p[0] & JF_PURE)) return "";  // never a list
+    if (root == JR_OPERATION || (p[0] & JF_PURE) || jmes_chain_form(p, n)) return "";  // never a list
     const std::string name = fresh("js");
     const uint32_t* saveP = P;
     const uint32_t savePEND = PEND;
@@ -897,7 +898,7 @@ struct CondGen {
     if (root == JR_OPERATION) return true;
     if (p[0] & JF_PURE) return false;
     for (uint32_t q = 1; q < o.nseg;) {
-      if (p[q] == JO_OR) break;
+      if (p[q] == JO_OR) return q + 2 >= o.nseg;  // a function applied after the default can fail
       if (p[q] != JO_FIELD) return false;
       q += 2;
     }
@@ -928,6 +929,14 @@ struct CondGen {
         return;
       }
       case OK_JMES: {
+        if (jmes_chain_form(rs.pool.data() + o.a, o.nseg)) {  // the light kernels' evaluator (kyv_cond.h jmes_chain_cv)
+          const std::string m = fresh("ms"), s = fresh("js");
+          out << "  CV " << cv << "; uint32_t " << m << ";\n"
+              << "  const int " << s << " = jmes_chain_cv(v, NodeTab{R}, " << C << ", &" << cv << ", &" << m << ");\n";
+          if (check) out << "  if (" << s << " == JS_FB) return CR_FB;\n  if (" << s << " != JS_OK) return CP_ERROR;\n";
+          else out << "  (void)" << s << ";\n";
+          return;
+        }
         lds_used = true;
         const std::string f = operand_fn(o, etpos);
         const std::string l = fresh("jl"), c = fresh("jc"), n = fresh("jn"), t = fresh("jt"), s = fresh("js");
@@ -1252,16 +1261,10 @@ struct CondGen {
 
 // rules the light match kernel cannot evaluate (kyv_engine.hip rule_needs_jmes): foreach, or a precondition / deny
 // program with a JMESPath operand
-// (length(<field chain>) operands run in the light kernels too: kyv_cond.h jmes_len_chain / jmes_len_cv)
+// (chain programs -- a field chain, `|| literal`, length() / to_upper() / regex_match() -- run in the light kernels
+// too: kyv_layout.h jmes_chain_form, kyv_cond.h jmes_chain_cv)
 static bool heavy_jmes(const Ruleset& rs, const CondOperand& o) {
-  if (o.kind != OK_JMES) return false;
-  const uint32_t* p = rs.pool.data() + o.a;
-  const uint32_t n = o.nseg;
-  if (n < 2 || (p[0] & 0xFFu) != JR_OBJECT || p[n - 1] != JO_LENGTH) return true;
-  uint32_t i = 1;
-  for (; i + 1 < n; i += 2)
-    if (p[i] != JO_FIELD) return true;
-  return i != n - 1;
+  return o.kind == OK_JMES && !jmes_chain_form(rs.pool.data() + o.a, o.nseg);
 }
 bool prog_has_jmes(const Ruleset& rs, uint32_t prog) {
   if (prog == NONE) return false;
@@ -1498,6 +1501,10 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     if (!heavy.empty()) { groups.push_back(heavy); gwpe.push_back(-1); }
   }
   const size_t ngroups = groups.size();
+  // round 6: root-scope column prefetch of the fused walk (kyv_fused.h): the first pf_cols columns of every fused
+  // pattern rule's root scope (0: off)
+  const size_t pf_cols = getenv("KYV_FUSED_PREFETCH") ? (size_t)std::max(0, atoi(getenv("KYV_FUSED_PREFETCH"))) : 0;
+  std::set<uint32_t> pf_root_done;
   std::vector<std::pair<size_t, size_t>> fused_kernels;  // (group, part): kyv_jit_fused_<g>[p<part>]
   std::vector<size_t> merged_groups;                      // groups with a kyv_jit_fusedm_<g> (KYV_FUSED_MERGE)
   for (size_t gi = 0; gi < ngroups; gi++) {
@@ -1523,6 +1530,30 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
              "  jfinish(w, r, out);\n"
              "}\n";
+    // KYV_FUSED_PREFETCH=n: the fused pattern rules' root functions also in a form that takes the first n root-scope
+    // columns from the caller (read from the wave's LDS prefetch slots, kyv_fused.h kyv_pf_col) and loads the rest
+    if (pf_cols)
+      for (size_t i : fused) {
+        const RuleDesc& rd = rs.rules[rule_roots[i].first];
+        if (rd.kind != RK_PATTERN || rule_roots[i].second.size() != 1) continue;
+        const uint32_t r = rep_of[rule_roots[i].second[0]];
+        const auto& L = g.scope_cols(r);
+        if (L.empty() || !pf_root_done.insert(r).second) continue;
+        src << "static __device__ __forceinline__ void rootP" << r
+            << "(const View& v, const Node* R, const ResHeader* hp, uint32_t row, uint32_t mbase, bool rootmap, bool walk,\n"
+               "    PatOut& out, const uint64_t* pfx) {\n"
+               "  uint64_t pc[" << L.size() << "];";
+        for (size_t q = 0; q < L.size(); q++) {
+          if (q < pf_cols) src << " pc[" << q << "] = pfx[" << q << "];";
+          else src << " pc[" << q << "] = jc_col(v, " << Gen::u(L[q]) << ", row);";
+        }
+        src << "\n"
+               "  if (!walk) return;\n"
+               "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
+               "  Ret rr = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
+               "  jfinish(w, rr, out);\n"
+               "}\n";
+      }
     if (roots.size() > 256) {
       std::map<uint32_t, std::vector<uint32_t>> br2;
       for (uint32_t r : roots) br2[rep_of[r]].push_back(r);
@@ -1576,6 +1607,26 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     for (size_t pi = 0; pi < nparts; pi++) {
       const std::vector<size_t> part(fused.begin() + fused.size() * pi / nparts, fused.begin() + fused.size() * (pi + 1) / nparts);
       const std::string sname = "JitFused" + std::to_string(gi) + (pi ? "p" + std::to_string(pi) : std::string());
+      // prefetching rules of the part (KYV_FUSED_PREFETCH): pattern rules with one root whose scope has columns; at
+      // most 64 per part (one bit each of the wave's uniform mask `gm` of the rules it will walk)
+      std::vector<std::vector<uint32_t>> pfl(part.size());
+      size_t pfmax = 0;
+      if (pf_cols)
+        for (size_t j = 0; j < part.size() && j < 64; j++) {
+          const RuleDesc& rd = rs.rules[rule_roots[part[j]].first];
+          if (rd.kind != RK_PATTERN || rule_roots[part[j]].second.size() != 1) continue;
+          const auto& L = g.scope_cols(rep_of[rule_roots[part[j]].second[0]]);
+          pfl[j].assign(L.begin(), L.begin() + std::min(L.size(), pf_cols));
+          pfmax = std::max(pfmax, pfl[j].size());
+        }
+      if (pfmax) {  // [rule of the part][column count, its first pfmax root-scope columns]
+        src << "__device__ const uint32_t kyv_pfc_" << sname << "[" << part.size() * (pfmax + 1) << "] = {";
+        for (size_t j = 0; j < part.size(); j++) {
+          src << (j ? ", " : "") << pfl[j].size() << "u";
+          for (size_t q = 0; q < pfmax; q++) src << ", " << (q < pfl[j].size() ? pfl[j][q] : 0u) << "u";
+        }
+        src << "};\n";
+      }
       src << "struct " << sname << " {\n"
              "  __device__ __forceinline__ void run(const View& v, const DevOut& o, uint32_t nwaves, uint32_t w, uint32_t r,\n"
              "                                     bool active, uint32_t hflags, uint32_t hroot, const uint32_t* gw) {\n"
@@ -1585,6 +1636,25 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "    const uint32_t row = r < v.nres ? r : NONE;\n"
              "    const bool rootmap = (hflags & RF_ROOT_MAP) != 0;\n"
              "    (void)lane; (void)hp; (void)rootmap;\n";
+      if (pfmax) {
+        // the wave's LDS slots, the uniform mask of the prefetching rules it walks, and the issue of one rule's columns
+        src << "    __shared__ uint64_t kpf[" << pfmax * 64 << "];\n"
+               "    const uint32_t row0 = w * 64u;\n"
+               "    uint64_t gm = 0;\n";
+        for (size_t j = 0; j < part.size(); j++) {
+          if (pfl[j].empty()) continue;
+          const uint32_t k = rule_roots[part[j]].first;
+          src << "    if (" << k << "u >= o.rule_lo && " << k << "u < o.rule_hi && __ballot(active && ((gw[" << k / 32 << "] >> "
+              << k % 32 << "u) & 1u))) gm |= 1ull << " << j << ";\n";
+        }
+        // one table-driven issue loop (uniform: the rule index comes from `gm`), not a switch per call site
+        src << "    auto pf_issue = [&](uint32_t jj) {\n"
+               "      const uint32_t* t = kyv_pfc_" << sname << " + jj * " << pfmax + 1 << "u;\n"
+               "      const uint32_t nc = t[0];\n"
+               "      for (uint32_t q = 0; q < nc; q++) kyv_pf_col(v, t[1 + q], row0, lane, kpf + q * 64u);\n"
+               "    };\n"
+               "    if (gm) pf_issue((uint32_t)__builtin_ctzll(gm));\n";
+      }
       for (size_t j = 0; j < part.size(); j++) {
       const size_t i = part[j];
       const uint32_t k = rule_roots[i].first;
@@ -1594,8 +1664,17 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
       const std::string K = Gen::u(k);
       src << "    if (" << K << " >= o.rule_lo && " << K << " < o.rule_hi) {\n"
              "      const bool gated = active && ((gw[" << k / 32 << "] >> " << k % 32 << "u) & 1u);\n"
-             "      if (__ballot(gated)) {\n"
-             "        const bool magic = gated && (hflags & RF_MAGIC);\n"
+             "      if (__ballot(gated)) {\n";
+      if (!pfl[j].empty()) {
+        // this rule's columns were issued by the previous prefetching rule (or before the first): wait, read them into
+        // registers, release the slots and issue the next rule's columns before this rule's own loads
+        src << "        kyv_pf_wait();\n"
+               "        uint64_t pfx[" << pfl[j].size() << "];\n";
+        for (size_t q = 0; q < pfl[j].size(); q++) src << "        pfx[" << q << "] = kpf[" << q * 64 << "u + lane];\n";
+        src << "        kyv_pf_release();\n"
+               "        { const uint64_t nx = gm & ~((2ull << " << j << ") - 1ull); if (nx) pf_issue((uint32_t)__builtin_ctzll(nx)); }\n";
+      }
+      src << "        const bool magic = gated && (hflags & RF_MAGIC);\n"
              "        WaveSink sink{o.stage + sld32(o.rbase + (" << K << " - o.rule_lo)) + (size_t)w * 64u * " << alts
           << "u, 0u, " << (rd.uses_meta ? "true" : "false") << "};\n"
              "        uint8_t st = pair_walk_alts(" << (pat ? "true" : "false") << ", " << nalts << "u, gated && !magic, r, " << K
@@ -1604,8 +1683,12 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "          switch (a) {\n";
       for (uint32_t a = 0; a < nalts; a++) {
         const uint32_t root = rule_roots[i].second[a];
-        src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
-            << ", rootmap, wk, po); break;\n";
+        if (!pfl[j].empty())
+          src << "            case " << a << "u: rootP" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+              << ", rootmap, wk, po, pfx); break;\n";
+        else
+          src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+              << ", rootmap, wk, po); break;\n";
       }
       src << "            default: break;\n"
              "          }\n"

@@ -399,51 +399,79 @@ KYV_HD CV jres_cv(const View& v, NodeTab R, const JRes& r, const JList& L) {
   return x;
 }
 
-// any operand -> CV (JS_OK / JS_NOTFOUND with *miss / JS_FB); L backs a projection list result
-// length(<field chain of request.object>) -- the one JMESPath function of C5's rules -- without the interpreter's
-// projection list, for the light kernels (kJ = false): the same steps as jmes_run over [JR_OBJECT, JO_FIELD k...,
-// JO_LENGTH] (a field of a non-map is null, a missing key NotFound only for a JF_PURE program; jpfLength of an
-// array / object is its element count, of an ASCII string its length, of anything else an error)
-KYV_HD bool jmes_len_chain(const uint32_t* p, uint32_t n) {
-  if (n < 2 || (p[0] & 0xFFu) != JR_OBJECT || p[n - 1] != JO_LENGTH) return false;
-  uint32_t i = 1;
-  for (; i + 1 < n; i += 2)
-    if (p[i] != JO_FIELD) return false;
-  return i == n - 1;
-}
-KYV_HD int jmes_len_cv(const View& v, NodeTab R, const CondOperand& o, CV* out, uint32_t* miss) {
+// A chain-form program (kyv_layout.h jmes_chain_form) -> CV: the field chain as j_field walks it (a missing key is
+// NotFound only for a JF_PURE program), `|| literal` when the value is false-like (util.go isFalse), then the function:
+//  - length(): jpfLength -- element count of an array / object, rune count of a string (ASCII here; other strings go to
+//    the CPU engine), an error for anything else;
+//  - to_upper(): jpfToUpper (functions.go:681-689) -- the argument must be a string (else the argument type error), the
+//    result is the dictionary string strings.ToUpper(s) (Batch::str_upper; a non-ASCII string goes to the CPU engine);
+//  - regex_match(re, x): jpRegexMatch (functions.go:786-799) -- x must be a string or a number (else the type error); a
+//    string's result is its precomputed bit (Batch::str_rx, regex.cpp), a number (ifaceToString's float32 formatting)
+//    or a string outside printable ASCII goes to the CPU engine
+KYV_HD int jmes_chain_cv(const View& v, NodeTab R, const CondOperand& o, CV* out, uint32_t* miss) {
   const uint32_t* p = v.pool + o.a;
   const uint32_t n = o.nseg;
   const bool pure = (p[0] & JF_PURE) != 0;
-  uint32_t cur = 0, fields = 0;
-  for (uint32_t i = 1; i + 1 < n; i += 2) {
+  uint32_t cur = 0, fields = 0, i = 1;
+  for (; i + 1 < n && p[i] == JO_FIELD; i += 2) {
     bool missing;
     cur = j_field(R, cur, p[i + 1], &missing);
     if (missing && pure) { *miss = fields; return JS_NOTFOUND; }
     fields++;
   }
-  if (cur == NONE) return JS_ERR;
-  const Node& x = R[cur];
-  uint32_t cnt;
-  if (node_type(x) == N_ARR || node_type(x) == N_MAP) {
-    cnt = x.b;
-  } else if (node_type(x) == N_STR) {
-    const uint32_t ln = v.str_len[x.a];
-    const uint8_t* b = sbytes(v, x.a);
-    for (uint32_t q = 0; q < ln; q++) if (b[q] >= 0x80) return JS_FB;  // (other strings: the CPU engine)
-    cnt = ln;
-  } else {
-    return JS_ERR;
+  uint32_t lit = NONE;
+  if (i + 1 < n && p[i] == JO_OR) {
+    JRes r;
+    r.lst = false; r.cur = cur; r.lit = NONE; r.num = NONE;
+    JList none;
+    none.n = 0;
+    if (j_false(v, R, r, none)) { lit = p[i + 1]; cur = NONE; }
+    i += 2;
   }
-  CV c = cv_node(Node{N_NULL, 0, 0, 0}, true);
-  c.t = CT_INT; c.i = cnt; c.sid = NONE;  // a float64 count, integral: an int after the JSON context round trip
-  *out = c;
+  CV x = lit != NONE ? cv_node(v.cnodes[lit], false) : cur == NONE ? cv_node(Node{N_NULL, 0, 0, 0}, true) : cv_node(R[cur], true);
+  if (x.t == CT_ARR) x.node = lit != NONE ? lit : cur;
+  if (i < n) {
+    const uint32_t op = p[i];
+    if (op == JO_LENGTH) {
+      if (lit != NONE || cur == NONE) return JS_ERR;
+      const Node& y = R[cur];
+      uint32_t cnt;
+      if (node_type(y) == N_ARR || node_type(y) == N_MAP) {
+        cnt = y.b;
+      } else if (node_type(y) == N_STR) {
+        const uint32_t ln = v.str_len[y.a];
+        const uint8_t* b = sbytes(v, y.a);
+        for (uint32_t q = 0; q < ln; q++) if (b[q] >= 0x80) return JS_FB;  // (other strings: the CPU engine)
+        cnt = ln;
+      } else {
+        return JS_ERR;
+      }
+      CV c = cv_node(Node{N_NULL, 0, 0, 0}, true);
+      c.t = CT_INT; c.i = cnt; c.sid = NONE;  // a float64 count, integral: an int after the JSON context round trip
+      x = c;
+    } else if (op == JO_UPPER) {
+      if (x.t != CT_STR) return JS_ERR;
+      const uint32_t u = v.str_upper ? v.str_upper[x.sid] : NONE;
+      if (u == NONE) return JS_FB;
+      CV c = cv_node(Node{N_NULL, 0, 0, 0}, true);
+      c.t = CT_STR; c.sid = u;
+      x = c;
+    } else if (op == JO_REGEX) {
+      if (x.t == CT_INT || x.t == CT_FLOAT) return JS_FB;
+      if (x.t != CT_STR) return JS_ERR;
+      const uint32_t bits = v.str_rx ? v.str_rx[x.sid] : RX_FB;
+      if (bits & RX_FB) return JS_FB;
+      x = cv_node(Node{((bits >> p[i + 1]) & 1u) ? (uint32_t)N_TRUE : (uint32_t)N_FALSE, 0, 0, 0}, true);
+    }
+  }
+  *out = x;
   return JS_OK;
 }
 
 KYV_HD int operand_cv(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, CV* out, uint32_t* miss,
                       uint32_t row = NONE) {
   if (o.kind != OK_JMES) return cv_operand(v, R, o, out, miss, row) ? JS_OK : JS_NOTFOUND;
+  if (jmes_chain_form(v.pool + o.a, o.nseg)) return jmes_chain_cv(v, R, o, out, miss);
   JRes r;
   const int st = jmes_run(v, R, o, elem, L, &r, miss);
   if (st != JS_OK) return st;
@@ -841,8 +869,8 @@ KYV_HD __attribute__((always_inline)) int eval_prog_inl(const View& v, NodeTab R
         }
         if (o.kind == OK_JMES) {
           if constexpr (!kJ) {
-            if (!jmes_len_chain(v.pool + o.a, o.nseg)) return CR_FB;
-            const int st = jmes_len_cv(v, R, o, &tmp, &miss);
+            if (!jmes_chain_form(v.pool + o.a, o.nseg)) return CR_FB;
+            const int st = jmes_chain_cv(v, R, o, &tmp, &miss);
             if (st == JS_FB) return CR_FB;
             if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
             if (st == JS_ERR) { *err_cond = c0 + i; *err_side = side; *err_seg = NONE; return CP_ERROR; }
@@ -876,9 +904,9 @@ KYV_HD __attribute__((always_inline)) int eval_prog_inl(const View& v, NodeTab R
       operand_cv(v, R, c.value, elem, lx, &x, &miss, row);
       r = eval_cond(v, R, c, k, x);
     } else {
-      if (c.key.kind == OK_JMES) jmes_len_cv(v, R, c.key, &k, &miss);  // (a length chain: checked in the first pass)
+      if (c.key.kind == OK_JMES) jmes_chain_cv(v, R, c.key, &k, &miss);  // (a chain program: checked in the first pass)
       else cv_operand(v, R, c.key, &k, &miss, row);
-      if (c.value.kind == OK_JMES) jmes_len_cv(v, R, c.value, &x, &miss);
+      if (c.value.kind == OK_JMES) jmes_chain_cv(v, R, c.value, &x, &miss);
       else cv_operand(v, R, c.value, &x, &miss, row);
       r = eval_cond(v, R, c, k, x);
     }

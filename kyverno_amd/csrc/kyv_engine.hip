@@ -163,6 +163,7 @@ struct Packer {
     size = off + bytes + 16;
     return off;
   }
+  void pad(size_t bytes) { size += bytes; }  // zeroed bytes behind the last part added
   hipError_t copy_to(uint8_t* dev) const {
     hipStream_t s = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
@@ -300,7 +301,7 @@ static bool prog_jmes(const Ruleset& rs, uint32_t prog) {
   const CondProg& p = rs.cprogs[prog];
   // (length(<field chain>) runs in the light kernels too: kyv_cond.h jmes_len_cv)
   auto heavy = [&](const CondOperand& o) {
-    return o.kind == OK_JMES && !jmes_len_chain(rs.pool.data() + o.a, o.nseg);
+    return o.kind == OK_JMES && !jmes_chain_form(rs.pool.data() + o.a, o.nseg);
   };
   auto blk = [&](uint32_t c0, uint32_t n) {
     for (uint32_t i = 0; i < n; i++)
@@ -422,7 +423,7 @@ struct DevBatch {
   uint8_t* base = nullptr;
   size_t bytes = 0;
   size_t o_nodes, o_hdr, o_faux, o_soff, o_slen, o_sflags, o_sdur, o_sqty, o_sf64, o_heap, o_nsloff, o_nslkv, o_gate,
-      o_colv, o_coloff, o_pe;
+      o_colv, o_coloff, o_pe, o_supper = SIZE_MAX, o_srx = SIZE_MAX;
   uint32_t* gmask = nullptr;   // [string][words] glob-mask bits, computed on the device once per batch
   uint32_t gmask_words = 0;
   uint32_t* inv = nullptr;     // input index -> kind-major position, and its inverse: uploaded by the first export
@@ -482,7 +483,10 @@ static DevBatch* upload_batch(const Batch& b, int device) {
   d->o_nsloff = p.add(b.nsl_off);
   d->o_nslkv = p.add(b.nsl_kv);
   d->o_gate = p.add(b.gate);
+  d->o_supper = b.str_upper.empty() ? SIZE_MAX : p.add(b.str_upper);
+  d->o_srx = b.str_rx.empty() ? SIZE_MAX : p.add(b.str_rx);
   d->o_colv = p.add(b.colv);
+  p.pad(512);  // the fused walk's column prefetch reads a whole match wave's 64 rows (kyv_fused.h kyv_pf_col)
   d->o_coloff = p.add(b.col_off);
   // batch-specialised copy of the pattern entries: `col` holds the column's absolute offset into colv, so the
   // walker reads a lookup's column without first reading the batch's column offset table
@@ -515,6 +519,8 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
     v.gate = (const uint32_t*)(bbase + db->o_gate);
     v.colv = (const uint64_t*)(bbase + db->o_colv);
     v.col_off = (const uint32_t*)(bbase + db->o_coloff);
+    v.str_upper = db->o_supper == SIZE_MAX ? nullptr : (const uint32_t*)(bbase + db->o_supper);
+    v.str_rx = db->o_srx == SIZE_MAX ? nullptr : (const uint32_t*)(bbase + db->o_srx);
     v.str_gmask = db->gmask;
     v.gmask_words = db->gmask_words;
   } else {
@@ -525,6 +531,8 @@ static View make_view(const Ruleset& rs, const Batch& b, const uint8_t* rbase, c
     v.str_dur = b.str_dur.data(); v.str_qty = b.str_qty.data(); v.str_f64 = b.str_f64.data();
     v.heap = b.heap.data(); v.nsl_off = b.nsl_off.data(); v.nsl_kv = b.nsl_kv.data();
     v.gate = b.gate.data();
+    v.str_upper = b.str_upper.empty() ? nullptr : b.str_upper.data();
+    v.str_rx = b.str_rx.empty() ? nullptr : b.str_rx.data();
     v.colv = b.colv.data();
     v.col_off = b.col_off.data();
   }
@@ -1781,7 +1789,6 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
   dim3 grid((unsigned)((nres + BLOCK - 1) / BLOCK));
   double total_ms = 0;
   double phase[5] = {0, 0, 0, 0, 0};
-  bool redone = false;  // a rule-sliced evaluation re-run once after its resident record list was grown
   for (auto& sl : d.slices) {
     if (!sl.evs) HIP_OK(hipEventCreate(&sl.evs));
     for (auto& e : sl.ev) if (!e) HIP_OK(hipEventCreate(&e));
@@ -1848,6 +1855,7 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     // rule slices append to one resident record list, except when copy-back gathers each slice's records on the host
     // (then each slice starts at 0: the buffer holds one slice's worst case)
     const uint32_t accumulate = multi && !collect ? 1u : 0u;
+    size_t appended = 0;  // upper bound of the records the slices have appended so far (accumulate)
     HIP_OK(hipMemsetAsync(d.status, ST_NONE, nres * nrules, stream));
     if (d.npss) HIP_OK(hipMemsetAsync(d.pss_fails, 0, (size_t)d.npss * nres * 4, stream));
     if (acct) aphase[0] += (uint64_t)nres * nrules + (uint64_t)d.npss * nres * 4;  // verdict / PSS-mask resets
@@ -2001,6 +2009,33 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
       hipLaunchKernelGGL(compact_scan_kernel, dim3(std::max<uint32_t>(nseg, 1)), dim3(1024), 0, stream, d.tsum, ntiles, d.tseg);
       hipLaunchKernelGGL(compact_top_kernel, dim3(1), dim3(1024), 0, stream, d.tseg, std::max<uint32_t>(nseg, 1), d.nrecs,
                          accumulate);
+      if (accumulate) {
+        // a rule-sliced evaluation appends every slice's records to one resident list. The host keeps an upper bound of
+        // the records appended so far (a slice stages at most d.max_recs); only when that bound could outgrow the
+        // list does it read the exact running total compact_top_kernel just computed and, if needed, grow the list
+        // in place (earlier slices' records copied over) before this slice's copy -- never a second evaluation
+        if (appended + d.max_recs > d.recs_cap) {
+          uint32_t c3[3] = {0, 0, 0};
+          HIP_OK(hipMemcpyAsync(c3, d.nrecs, 12, hipMemcpyDeviceToHost, stream));
+          HIP_OK(hipStreamSynchronize(stream));
+          if (c3[2] > d.recs_cap) {
+            const size_t left = (size_t)(&d.slices.back() - &sl);  // slices still to come
+            const size_t cap = (size_t)c3[2] + std::min<size_t>(left * d.max_recs, (size_t)c3[2] / 4 + 1024);
+            FailRec* nr = nullptr;
+            HIP_OK(dmalloc(&nr, cap * sizeof(FailRec)));
+            if (c3[1]) HIP_OK(hipMemcpyAsync(nr, d.recs, (size_t)c3[1] * sizeof(FailRec), hipMemcpyDeviceToDevice, stream));
+            HIP_OK(hipStreamSynchronize(stream));
+            dfree(d.recs);
+            d.recs = nr;
+            d.recs_cap = cap;
+            if (getenv("KYV_DEBUG_STATS"))
+              fprintf(stderr, "[kyvgpu] resident failure records grown to %zu before slice [%u, %u)\n", cap, sl.k0, sl.k1);
+          }
+          appended = c3[2];
+        } else {
+          appended += d.max_recs;
+        }
+      }
       hipLaunchKernelGGL(compact_copy_kernel, dim3(ntiles), dim3(WAVE), 0, stream, d.stage, sl.rbase, d.rcnt, drules,
                          d.wl.nwaves, nchunks, d.tsum, d.tseg, d.recs, d.recs_cap, sl.k0, (const uint32_t*)d.nrecs);
       HIP_OK(hipGetLastError());
@@ -2032,23 +2067,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     if (acct) aphase[4] += (uint64_t)nres * nrules;  // the histogram reads every verdict byte
     HIP_OK(hipEventRecord(d.e1, stream));
     HIP_OK(hipEventSynchronize(d.e1));
-    if (accumulate) {  // the slices' appended records outgrew the resident list: grow it and run this evaluation again
+    if (accumulate) {  // grown between slices above when needed: the list always holds every appended record
       uint32_t c[3] = {0, 0, 0};
       HIP_OK(hipMemcpy(c, d.nrecs, 12, hipMemcpyDeviceToHost));
-      if (c[2] > d.recs_cap) {
-        if (redone) throw std::runtime_error("failure record buffer overflow");
-        dfree(d.recs);
-        d.recs = nullptr;
-        d.recs_cap = 0;
-        const size_t cap = (size_t)c[2] + c[2] / 4 + 1024;
-        HIP_OK(dmalloc(&d.recs, cap * sizeof(FailRec)));
-        d.recs_cap = cap;
-        redone = true;
-        for (auto& x : aphase) x = 0;  // (the accounting counters of the discarded run)
-        for (auto& x : aclass) x = 0;
-        it--;
-        continue;
-      }
+      if (c[2] > d.recs_cap) throw std::runtime_error("failure record buffer overflow");
     }
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, d.e0, d.e1));

@@ -108,6 +108,8 @@ struct View {
   uint32_t gate_words;
   const uint32_t* str_gmask;  // [string][gmask_words] glob-mask bits (device only; nullptr: match bytes)
   uint32_t gmask_words;
+  const uint32_t* str_upper;  // [string] id of strings.ToUpper(s) (NONE: not ASCII), or nullptr (no to_upper rule)
+  const uint32_t* str_rx;     // [string] regex_match bits of the ruleset's regexes (RX_FB: outside printable ASCII)
   const uint64_t* colv;     // path columns (kyv_layout.h): colv[col_off[c] + row]
   const uint32_t* col_off;  // (device View: pe[].col already holds col_off[col])
   // ruleset

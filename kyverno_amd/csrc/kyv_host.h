@@ -82,6 +82,18 @@ struct PolicyMeta {
   std::vector<std::string> all_rule_names;  // every computed rule name in order (CLI "rule absent -> skip")
 };
 
+// regex_match pattern as a DFA over printable ASCII (regex.cpp): next[state * RX_SYMS + (c - 0x20)], state 0 the start
+struct RxDfa {
+  uint32_t nstates = 0;
+  std::vector<uint16_t> next;
+  std::vector<uint8_t> accept;
+  bool end_anchor = false;  // '$': accept only at the end of the subject (else as soon as an accepting state is reached)
+};
+// compile a regex_match pattern (false + *why outside the device subset, regex.cpp)
+bool rx_compile(const std::string& re, RxDfa* out, std::string* why);
+// regexp.Match of the compiled pattern on a subject: 1 / 0, -1 when the subject has a byte outside printable ASCII
+int rx_match(const RxDfa& d, const uint8_t* s, size_t n);
+
 struct Ruleset {
   Dict dict;                    // seed dictionary (fixed ids + literals)
   std::vector<RuleDesc> rules;
@@ -119,6 +131,11 @@ struct Ruleset {
   // some literal sid e of the set; cond_set[ci] = set index + 1 of condition ci, 0 none
   std::vector<std::vector<uint32_t>> gsets;
   std::vector<uint32_t> cond_set;
+  // round 6: JMESPath functions on the dictionary -- regex_match patterns (JO_REGEX q = rxs[q]) and whether some
+  // program applies to_upper (JO_UPPER): the batch then computes Batch::str_rx / str_upper once per string
+  std::vector<std::string> rx_src;
+  std::vector<RxDfa> rxs;
+  bool uses_upper = false;
   uint32_t ncols = 0, nrowspaces = 1;
   std::vector<uint32_t> col_rowspace;
   std::vector<uint32_t> pn_self;  // array pnode -> self column of its elements (NONE: none)
@@ -159,6 +176,7 @@ struct Batch {
   bulk_vector<ResHeader> hdr;
   std::vector<FloatAux> faux;
   std::vector<uint32_t> str_off, str_len, str_flags;
+  std::vector<uint32_t> str_upper, str_rx;  // JMESPath functions on the dictionary (empty: the ruleset uses none)
   std::vector<int64_t> str_dur, str_qty;
   std::vector<double> str_f64;
   std::vector<uint8_t> heap;

@@ -377,7 +377,9 @@ enum JmesOp : uint32_t { JO_FIELD = 1,     // + key sid
                          JO_KEYS_FLAT = 5, // projection keys(@) then flatten
                          JO_OR = 6,        // + cnode literal: `|| <literal>` when the result is false-like
                          JO_LENGTH = 7,    // length(<the ops before>): a number (go-jmespath jpfLength)
-                         JO_FILTER = 8 };  // + FilterKind, literal, n, n key sids: filter projection `[?<pred>]`
+                         JO_FILTER = 8,    // + FilterKind, literal, n, n key sids: filter projection `[?<pred>]`
+                         JO_UPPER = 9,     // to_upper(<the ops before>): Batch::str_upper of the string (round 6)
+                         JO_REGEX = 10 };  // + q: regex_match(<ruleset regex q>, <the ops before>): bit q of Batch::str_rx
 // filter predicates the device evaluates per element (the compiler keeps other predicates on the CPU engine):
 //   FK_HASKEY  contains(keys(@), '<lit>')  literal = key sid; an element that is not a map: keys() type error
 //   FK_EQ/NE   <field chain> == / != <literal>  literal = cnode (string, boolean or null)
@@ -387,8 +389,32 @@ enum FilterKind : uint32_t { FK_HASKEY = 0, FK_EQ = 1, FK_NE = 2 };
 __host__ __device__
 #endif
 inline uint32_t jop_width(const uint32_t* p) {
-  return p[0] == JO_FIELD || p[0] == JO_OR ? 2u : p[0] == JO_MULTI ? 2u + p[1] : p[0] == JO_FILTER ? 4u + p[3] : 1u;
+  return p[0] == JO_FIELD || p[0] == JO_OR || p[0] == JO_REGEX ? 2u : p[0] == JO_MULTI ? 2u + p[1] :
+         p[0] == JO_FILTER ? 4u + p[3] : 1u;
 }
+// Programs the light kernels evaluate without the interpreter's list state (kyv_cond.h jmes_chain_cv): a field chain
+// of request.object, an optional `|| literal`, and an optional function applied last -- length() (go-jmespath
+// jpfLength), to_upper() / regex_match() (kyverno pkg/engine/jmespath/functions.go:681-689, 786-799):
+//   [JR_OBJECT | JF_PURE?] (JO_FIELD key)* (JO_OR lit)? (JO_LENGTH | JO_UPPER | JO_REGEX q)?   (at least one of the two)
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+__host__ __device__
+#endif
+inline bool jmes_chain_form(const uint32_t* p, uint32_t n) {
+  if (n < 2 || (p[0] & 0xFFu) != JR_OBJECT) return false;
+  uint32_t i = 1;
+  while (i + 1 < n && p[i] == JO_FIELD) i += 2;
+  bool extra = false;
+  if (i + 1 < n && p[i] == JO_OR) { i += 2; extra = true; }
+  if (i < n && (p[i] == JO_LENGTH || p[i] == JO_UPPER)) { i += 1; extra = true; }
+  else if (i + 1 < n && p[i] == JO_REGEX) { i += 2; extra = true; }
+  return extra && i == n;
+}
+// regex_match precompute (regex.cpp, Batch::str_rx): at most RX_MAX regexes per ruleset (bits 0..RX_MAX-1 of a
+// string's word); RX_FB: the string has a byte outside printable ASCII (its pairs go to the CPU engine)
+constexpr uint32_t RX_MAX = 31;
+constexpr uint32_t RX_FB = 1u << 31;
+constexpr uint32_t RX_SYMS = 95;          // DFA alphabet: printable ASCII 0x20..0x7E
+constexpr uint32_t RX_MAX_STATES = 1024;
 constexpr uint32_t JMES_MAX_LIST = 32;     // virtual list capacity (longer -> CPU fallback)
 constexpr uint32_t JMES_KEYBIT = 1u << 31; // virtual list element: the key of map entry node (index & ~KEYBIT)
 constexpr uint32_t JMES_SIDBIT = 1u << 30; // virtual list element: a string value, by dictionary id (& ~SIDBIT)

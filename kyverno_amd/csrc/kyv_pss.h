@@ -300,9 +300,16 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
   auto selValid = [&](uint32_t u, uint32_t r, uint32_t t) { return str_in(t, selOK, 4) && u == SID_EMPTY && r == SID_EMPTY; };
   auto secValid = [&](uint32_t t) { return t == KSID(LOCALHOST) || t == KSID(RUNTIMEDEFAULT); };
 
-  bool apeBad = false, capsBaseBad = false, capsRBad = false, portsBad = false, privBad = false, procBad = false;
-  bool nonRootExplicitBad = false, nonRootImplicitBad = false, userBad = false, selBad = false;
-  bool secBaseBad = false, secRExplicitBad = false, secRImplicitBad = false, hpBad = false, secAnnBad = false;
+  // Every flag set inside the container / capability / port / annotation / volume loops is a bit of one integer word
+  // (`bad`, `all`, `hn`, `okv`), never a loop-carried bool: divergent loop-carried bools in these nested loops were
+  // lowered as lane masks and merged wrongly at divergent loop exits (profiles/r5_pss_miscompile/README.md; the
+  // column form pss_checks_cols follows the same rule)
+  enum : uint32_t {
+    B_APE = 1u << 0, B_CAPS_BASE = 1u << 1, B_CAPS_R = 1u << 2, B_PORTS = 1u << 3, B_PRIV = 1u << 4, B_PROC = 1u << 5,
+    B_NONROOT_X = 1u << 6, B_NONROOT_I = 1u << 7, B_USER = 1u << 8, B_SEL = 1u << 9, B_SEC_BASE = 1u << 10,
+    B_SEC_RX = 1u << 11, B_SEC_RI = 1u << 12, B_HP = 1u << 13, B_SEC_ANN = 1u << 14
+  };
+  uint32_t bad = 0;
   bool podNonRootTrue = podNonRoot == 1;
   bool podSecValid = podSecSet && secValid(podSecType);
   uint32_t ann = pv.meta == NONE ? NONE : get(R, pv.meta, KSID(ANNOTATIONS));
@@ -320,48 +327,48 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
       uint32_t nm = get(R, c, KSID(NAME));
       cname = nil(R, nm) ? SID_EMPTY : R[nm].a;
     }
-    if (!s.set || s.ape != 0) apeBad = true;
+    if (!s.set || s.ape != 0) bad |= B_APE;
     if (s.set && s.caps != NONE) {
       uint32_t add = get(R, s.caps, KSID(ADD));
       if (!nil(R, add))
         for (uint32_t i = 0; i < R[add].b; i++) {
           uint32_t cap = R[R[add].a + i].a;
           if (node_type(R[R[add].a + i]) != N_STR) cap = SID_EMPTY;
-          if (!str_in(cap, capsOK, 13)) capsBaseBad = true;
-          if (cap != KSID(NET_BIND_SERVICE)) capsRBad = true;
+          if (!str_in(cap, capsOK, 13)) bad |= B_CAPS_BASE;
+          if (cap != KSID(NET_BIND_SERVICE)) bad |= B_CAPS_R;
         }
-      bool all = false;
+      uint32_t all = 0;
       uint32_t drop = get(R, s.caps, KSID(DROP));
       if (!nil(R, drop))
         for (uint32_t i = 0; i < R[drop].b; i++) {
           const Node& e = R[R[drop].a + i];
-          if (node_type(e) == N_STR && e.a == KSID(ALL)) all = true;
+          if (node_type(e) == N_STR && e.a == KSID(ALL)) all = 1u;
         }
-      if (!all) capsRBad = true;
+      if (!all) bad |= B_CAPS_R;
     } else {
-      capsRBad = true;
+      bad |= B_CAPS_R;
     }
     if (!fake) {
       uint32_t ports = get(R, c, KSID(PORTS));
       if (!nil(R, ports))
         for (uint32_t i = 0; i < R[ports].b; i++) {
           uint32_t hp = get(R, R[ports].a + i, KSID(HOSTPORT));
-          if (!nil(R, hp) && node_type(R[hp]) == N_INT && (R[hp].a | R[hp].b) != 0) portsBad = true;
+          if (!nil(R, hp) && node_type(R[hp]) == N_INT && (R[hp].a | R[hp].b) != 0) bad |= B_PORTS;
         }
     }
-    if (s.set && s.privileged == 1) privBad = true;
-    if (s.set && s.procSet && s.proc != KSID(DEFAULT)) procBad = true;
-    if (s.set && s.runAsNonRoot != -1) { if (s.runAsNonRoot == 0) nonRootExplicitBad = true; }
-    else if (!podNonRootTrue) nonRootImplicitBad = true;
-    if (s.set && s.hasRunAsUser && s.runAsUser == 0) userBad = true;
-    if (s.set && s.selSet && !selValid(s.selUser, s.selRole, s.selType)) selBad = true;
+    if (s.set && s.privileged == 1) bad |= B_PRIV;
+    if (s.set && s.procSet && s.proc != KSID(DEFAULT)) bad |= B_PROC;
+    if (s.set && s.runAsNonRoot != -1) { if (s.runAsNonRoot == 0) bad |= B_NONROOT_X; }
+    else if (!podNonRootTrue) bad |= B_NONROOT_I;
+    if (s.set && s.hasRunAsUser && s.runAsUser == 0) bad |= B_USER;
+    if (s.set && s.selSet && !selValid(s.selUser, s.selRole, s.selType)) bad |= B_SEL;
     if (s.set && s.secSet) {
-      if (s.secType == KSID(UNCONFINED)) secBaseBad = true;
-      if (!secValid(s.secType)) secRExplicitBad = true;
+      if (s.secType == KSID(UNCONFINED)) bad |= B_SEC_BASE;
+      if (!secValid(s.secType)) bad |= B_SEC_RX;
     } else if (!podSecValid) {
-      secRImplicitBad = true;
+      bad |= B_SEC_RI;
     }
-    if (s.set && s.hostProcess == 1) hpBad = true;
+    if (s.set && s.hostProcess == 1) bad |= B_HP;
     // container seccomp annotation: container.seccomp.security.alpha.kubernetes.io/<name> == "unconfined"
     if (annMap) {
       uint32_t pl = v.str_len[KSID(SECCOMP_CONTAINER_PREFIX)], nl = v.str_len[cname];
@@ -370,7 +377,7 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
         uint32_t k = node_key(e);
         if (has_pfx(v, k, SF_PFX_SECCOMP_C) && v.str_len[k] == pl + nl &&
             bytes_eq(sbytes(v, k) + pl, sbytes(v, cname), nl) && node_type(e) == N_STR && e.a == KSID(UNCONFINED_LC))
-          secAnnBad = true;
+          bad |= B_SEC_ANN;
       }
     }
   };
@@ -387,8 +394,8 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
       }
     }
   }
-  if (apeBad) fails |= 1u << PS_APE_1_8;
-  if (apeBad && !windows) fails |= 1u << PS_APE_1_25;
+  if (bad & B_APE) fails |= 1u << PS_APE_1_8;
+  if ((bad & B_APE) && !windows) fails |= 1u << PS_APE_1_25;
   // appArmorProfile: annotations with the apparmor prefix whose value is neither runtime/default nor localhost/*
   if (annMap)
     for (uint32_t i = 0; i < R[ann].b; i++) {
@@ -397,17 +404,17 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
       if (has_pfx(v, node_key(e), SF_PFX_APPARMOR) && val != KSID(RUNTIME_DEFAULT_PROFILE) &&
           !has_pfx(v, val, SF_PFX_LOCALHOST))
         fails |= 1u << PS_APPARMOR;
-      if (node_key(e) == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) secAnnBad = true;
+      if (node_key(e) == KSID(SECCOMP_POD_ANN) && val == KSID(UNCONFINED_LC)) bad |= B_SEC_ANN;
     }
-  if (capsBaseBad) fails |= 1u << PS_CAPS_BASE;
-  if (capsRBad) fails |= 1u << PS_CAPS_R_1_22;
-  if (capsRBad && !windows) fails |= 1u << PS_CAPS_R_1_25;
+  if (bad & B_CAPS_BASE) fails |= 1u << PS_CAPS_BASE;
+  if (bad & B_CAPS_R) fails |= 1u << PS_CAPS_R_1_22;
+  if ((bad & B_CAPS_R) && !windows) fails |= 1u << PS_CAPS_R_1_25;
   {
-    bool hn = false;
+    uint32_t hn = 0;
     const uint32_t hkeys[3] = {KSID(HOSTNETWORK), KSID(HOSTPID), KSID(HOSTIPC)};
     for (uint32_t key : hkeys) {
       uint32_t n = get(R, spec, key);
-      if (!nil(R, n) && node_type(R[n]) == N_TRUE) hn = true;
+      if (!nil(R, n) && node_type(R[n]) == N_TRUE) hn = 1u;
     }
     if (hn) fails |= 1u << PS_HOSTNS;
   }
@@ -417,26 +424,26 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
       // one pass over the volume's entries (keys are unique): a non-null hostPath entry, and whether some allowed
       // source (the first V_ALLOWED volume-source sids) is set
       uint32_t vn = R[vols].a + i;
-      bool okv = false;
+      uint32_t okv = 0;
       if (node_type(R[vn]) == N_MAP)
         for (uint32_t q = 0; q < R[vn].b; q++) {
           const Node& e = R[R[vn].a + q];
           if (node_type(e) == N_NULL) continue;
           const uint32_t k = node_key(e);
           if (k == VSID(hostPath)) fails |= 1u << PS_HOSTPATH;
-          if (k >= SID_FIRST_FREE + K_COUNT && k < SID_FIRST_FREE + K_COUNT + V_ALLOWED) okv = true;
+          if (k >= SID_FIRST_FREE + K_COUNT && k < SID_FIRST_FREE + K_COUNT + V_ALLOWED) okv = 1u;
         }
       if (!okv) fails |= 1u << PS_RVOLUMES;
     }
-  if (portsBad) fails |= 1u << PS_HOSTPORTS;
-  if (privBad) fails |= 1u << PS_PRIVILEGED;
-  if (procBad) fails |= 1u << PS_PROCMOUNT;
-  if (podNonRoot == 0 || nonRootExplicitBad || nonRootImplicitBad) fails |= 1u << PS_RUNASNONROOT;
-  if ((podHasUser && podUser == 0) || userBad) fails |= 1u << PS_RUNASUSER;
-  if ((podSelSet && !selValid(pu, pr, pt)) || selBad) fails |= 1u << PS_SELINUX;
-  if (secAnnBad) fails |= 1u << PS_SECCOMP_B_1_0;
-  if ((podSecSet && podSecType == KSID(UNCONFINED)) || secBaseBad) fails |= 1u << PS_SECCOMP_B_1_19;
-  bool secR = (podSecSet && !secValid(podSecType)) || secRExplicitBad || secRImplicitBad;
+  if (bad & B_PORTS) fails |= 1u << PS_HOSTPORTS;
+  if (bad & B_PRIV) fails |= 1u << PS_PRIVILEGED;
+  if (bad & B_PROC) fails |= 1u << PS_PROCMOUNT;
+  if (podNonRoot == 0 || (bad & (B_NONROOT_X | B_NONROOT_I))) fails |= 1u << PS_RUNASNONROOT;
+  if ((podHasUser && podUser == 0) || (bad & B_USER)) fails |= 1u << PS_RUNASUSER;
+  if ((podSelSet && !selValid(pu, pr, pt)) || (bad & B_SEL)) fails |= 1u << PS_SELINUX;
+  if (bad & B_SEC_ANN) fails |= 1u << PS_SECCOMP_B_1_0;
+  if ((podSecSet && podSecType == KSID(UNCONFINED)) || (bad & B_SEC_BASE)) fails |= 1u << PS_SECCOMP_B_1_19;
+  const bool secR = (podSecSet && !secValid(podSecType)) || (bad & (B_SEC_RX | B_SEC_RI));
   if (secR) fails |= 1u << PS_SECCOMP_R_1_19;
   if (secR && !windows) fails |= 1u << PS_SECCOMP_R_1_25;
   if (pscSet) {
@@ -450,7 +457,7 @@ KYV_FN_PSS uint32_t pss_checks(const View& v, NodeTab R, const PodView& pv) {
         if (!str_in(s, ok5, 5)) fails |= 1u << PS_SYSCTLS;
       }
   }
-  if (podHostProcess == 1 || hpBad) fails |= 1u << PS_WINHOSTPROCESS;
+  if (podHostProcess == 1 || (bad & B_HP)) fails |= 1u << PS_WINHOSTPROCESS;
   return fails;
 }
 

@@ -382,13 +382,14 @@ class Comm:
         """cluster-wide per-rule verdict tallies of the batch's last evaluation (kyv_comm_reduce_counts: one
         ncclAllReduce of the device-resident tallies): int64 [rules, 8]; a collective, every rank calls it"""
         L = K.lib()
-        n = L.kyv_comm_reduce_counts(self._h, batch.h, None, 0)
-        if n < 0:
+        # the size query never fails (0 when this rank has no results); the collective call is made in every case, so
+        # a rank without results fails together with its peers instead of leaving them in the all-reduce
+        n = max(0, L.kyv_comm_reduce_counts(self._h, batch.h, None, 0))
+        out = np.zeros(max(n, 1), dtype=np.int64)
+        got = L.kyv_comm_reduce_counts(self._h, batch.h, out.ctypes.data, n)
+        if got < 0 or got != n:
             raise K.KyvError(L.kyv_last_error().decode())
-        out = np.zeros(n, dtype=np.int64)
-        if L.kyv_comm_reduce_counts(self._h, batch.h, out.ctypes.data, n) != n:
-            raise K.KyvError(L.kyv_last_error().decode())
-        return out.reshape(-1, 8)
+        return out[:n].reshape(-1, 8)
 
     def status_of(self, q):
         """rank q's packed verdicts from the last gather (kyv_batch_export_status layout, padded)"""

@@ -381,7 +381,7 @@ def c5_policies(n=50, seed=SEED):
     device-compilable subset: Equals / NotEquals / In / AnyIn / AllIn / NotIn / AnyNotIn / AllNotIn / numeric,
     old-list and any/all forms, literal ranges, JSON-string lists, quantities, durations, message variables);
     the rest use JMESPath projections, length(), `||` defaults or request.operation (device-compiled too), and
-    regex_match / to_upper, which stay outside the device subset (their pairs are CPU fallback, counted)."""
+    regex_match / to_upper (round 6: device-compiled as per-string columns of the batch dictionary)."""
     r = random.Random(seed ^ 0xC5)
     pod = {"any": [{"resources": {"kinds": ["Pod"]}}]}
     wl = {"any": [{"resources": {"kinds": ["Deployment", "StatefulSet"]}}]}
@@ -428,8 +428,8 @@ def c5_policies(n=50, seed=SEED):
         lambda: ("deny", pod, {"any": [c("{{ length(request.object.spec.containers) }}", "GreaterThan", 2)]}, None, "many"),
         lambda: ("deny", pod, {"any": [c("{{ request.object.metadata.labels.app || '' }}", "Equals", "")]}, None, "app"),
         lambda: ("pattern", pod, None, {"any": [c("{{ request.operation }}", "Equals", "CREATE")]}, "owner"),
-        # outside the device subset (JMESPath functions other than keys / length): the rule's pairs are handed to the
-        # CPU engine (ST_FALLBACK, counted in the bench line's cpu_fallback_pairs_per_step and never timed as device work)
+        # kyverno's JMESPath functions on one string (round 6: Batch::str_rx / str_upper, evaluated on the device; until
+        # round 5 these rules were CPU fallback)
         lambda: ("deny", pod, {"any": [c("{{ regex_match('^team-[0-9]+$', request.object.metadata.labels.owner || '') }}",
                                          "Equals", False)]}, None, "owner format"),
         lambda: ("deny", pod, {"any": [c("{{ to_upper(request.object.metadata.labels.tier || '') }}", "Equals", "DATA")]},

@@ -795,7 +795,13 @@ CondResult eval_conditions_element(const VP& conditions, const VP& resource, con
   CondResult r;
   if (!conditions_supported_in(conditions, element != nullptr)) { r.r = CondOutcome::Unsupported; return r; }
   SubstErr se;
-  VP doc = substitute(conditions, VarCtx{resource, element, index}, "", se);
+  VP doc;
+  try {
+    doc = substitute(conditions, VarCtx{resource, element, index}, "", se);
+  } catch (JmesUnsupported&) {  // a value outside the restatement at run time (to_upper / regex_match subjects)
+    r.r = CondOutcome::Unsupported;
+    return r;
+  }
   if (se.n) { r.r = CondOutcome::Error; r.err = se.first; r.err_unpinned = se.n > 1 || se.unpinned; return r; }
   if (isnil(doc)) { r.r = CondOutcome::True; return r; }  // null -> empty old-style list -> all true
   if (doc->t == T::Arr) {  // []Condition (evaluate.go:72-81), operators checked exactly (json.go:57-72)

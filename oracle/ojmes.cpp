@@ -3,6 +3,7 @@
 
 #include <functional>
 #include <memory>
+#include <regex>
 #include <vector>
 
 #include "goutil.h"
@@ -38,11 +39,15 @@ std::vector<Token> lex(const std::string& s) {
       if (j >= s.size()) throw JmesUnsupported{"unterminated quoted identifier"};
       out.push_back({tQuoted, s.substr(i + 1, j - i - 1)});
       i = j + 1;
-    } else if (c == '\'') {
+    } else if (c == '\'') {  // lexer.go consumeRawStringLiteral: \' is a quote, any other backslash is kept
+      std::string v;
       size_t j = i + 1;
-      while (j < s.size() && s[j] != '\'') { if (s[j] == '\\') throw JmesUnsupported{"escaped raw string"}; j++; }
+      for (; j < s.size() && s[j] != '\''; j++) {
+        if (s[j] == '\\' && j + 1 < s.size() && s[j + 1] == '\'') { v += '\''; j++; continue; }
+        v += s[j];
+      }
       if (j >= s.size()) throw JmesUnsupported{"unterminated raw string"};
-      out.push_back({tRaw, s.substr(i + 1, j - i - 1)});
+      out.push_back({tRaw, v});
       i = j + 1;
     } else if (c == '`') {
       size_t j = i + 1;
@@ -306,6 +311,32 @@ VP eval(const NP& n, const VP& value) {
         }
         return Value::boolean(false);
       }
+      if (n->name == "to_upper" && n->kids.size() == 1) {
+        // jpfToUpper (kyverno pkg/engine/jmespath/functions.go:681-689): the argument type check (JpString) first, then
+        // strings.ToUpper; restated for ASCII strings (Unicode case mapping: outside the restatement)
+        VP arg = eval(n->kids[0], value);
+        if (!arg || arg->t != T::Str) throw JmesError{"invalid type for: <nil>, expected: []jpType{\"string\"}"};
+        std::string u = arg->s;
+        for (char& ch : u) {
+          if ((unsigned char)ch >= 0x80) throw JmesUnsupported{"to_upper of a non-ASCII string"};
+          if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 'a' + 'A');
+        }
+        return Value::str(u);
+      }
+      if (n->name == "regex_match" && n->kids.size() == 2) {
+        // jpRegexMatch (functions.go:786-799): argument types (JpString, JpString | JpNumber), then
+        // regexp.Match(regex, []byte(ifaceToString(src))) -- an unanchored search. The pattern is checked against the
+        // restated subset by nodes_ok (rx_restated); subjects outside printable ASCII and numbers (ifaceToString's
+        // FormatFloat(f, 'f', -1, 32)) are outside the restatement
+        VP re = eval(n->kids[0], value), src = eval(n->kids[1], value);
+        if (!re || re->t != T::Str) throw JmesError{"invalid type for: <nil>, expected: []jpType{\"string\"}"};
+        if (!src || (src->t != T::Str && src->t != T::Int && src->t != T::Float))
+          throw JmesError{"invalid type for: <nil>, expected: []jpType{\"string\", \"number\"}"};
+        if (src->t != T::Str) throw JmesUnsupported{"regex_match of a number"};
+        for (unsigned char ch : src->s)
+          if (ch < 0x20 || ch > 0x7E) throw JmesUnsupported{"regex_match subject outside printable ASCII"};
+        return Value::boolean(std::regex_search(src->s, std::regex(re->s, std::regex::ECMAScript)));
+      }
       if (n->name != "keys" || n->kids.size() != 1) throw JmesUnsupported{"function " + n->name};
       VP arg = eval(n->kids[0], value);
       if (!arg || arg->t != T::Obj) throw JmesError{"invalid type for: <nil>, expected: []jpType{\"object\"}"};
@@ -377,11 +408,134 @@ VP floats(const VP& v) {  // encoding/json decode of the JSON context: every num
 
 VP json_floats(const VP& v) { return floats(v); }
 
-// every node within the restated interpreter (functions: keys(@) and length())
-static bool nodes_ok(const NP& n) {
-  if (n->k == NFunction && !(n->name == "length" && n->kids.size() == 1) && !(n->name == "contains" && n->kids.size() == 2) &&
-      (n->name != "keys" || n->kids.size() != 1 || n->kids[0]->k != NCurrent))
+// The regex_match patterns the restatement evaluates with std::regex (ECMAScript): a subset of Go's RE2 syntax whose
+// matches coincide with RE2's on printable-ASCII subjects -- literal characters, `.`, escaped metacharacters (and '/',
+// '-'), \d \D \w \W \s \S, bracket classes (ranges, negation; no POSIX classes, no ']' first), ( ) and (?: ) groups,
+// `|`, the quantifiers * + ? {n} {n,} {n,m} (bounds <= 64, one per atom, an optional lazy '?'), '^' only as the first
+// and '$' only as the last pattern character (then no '|' outside parentheses). Anything else: JmesUnsupported.
+static bool rx_restated(const std::string& re) {
+  std::string b = re;
+  bool anchored = false;
+  if (!b.empty() && b[0] == '^') { b.erase(0, 1); anchored = true; }
+  if (!b.empty() && b.back() == '$') {
+    size_t bs = 0;
+    for (size_t j = b.size() - 1; j > 0 && b[j - 1] == '\\'; j--) bs++;
+    if (bs % 2 == 0) { b.pop_back(); anchored = true; }
+  }
+  const std::string meta = "^$\\.*+?()[]{}|";
+  auto esc_ok = [&](char e) { return std::string("dDwWsS").find(e) != std::string::npos || meta.find(e) != std::string::npos ||
+                                     e == '/' || e == '-'; };
+  int depth = 0;
+  bool atom = false, quant = false;  // an atom precedes (a quantifier may follow); the atom is quantified already
+  for (size_t i = 0; i < b.size(); i++) {
+    const unsigned char c = (unsigned char)b[i];
+    if (c < 0x20 || c > 0x7E) return false;
+    if (c == '\\') {
+      if (i + 1 >= b.size() || !esc_ok(b[i + 1])) return false;
+      i++;
+      atom = true; quant = false;
+    } else if (c == '[') {
+      size_t j = i + 1;
+      if (j < b.size() && b[j] == '^') j++;
+      if (j >= b.size() || b[j] == ']') return false;
+      bool closed = false;
+      int prev = -1;  // last single character of the class (a range's start)
+      for (; j < b.size(); j++) {
+        if (b[j] == ']') { closed = true; break; }
+        if (b[j] == '[') return false;
+        int ch;
+        if (b[j] == '\\') {
+          if (j + 1 >= b.size() || !esc_ok(b[j + 1])) return false;
+          ch = std::string("dDwWsS").find(b[j + 1]) != std::string::npos ? -1 : (unsigned char)b[j + 1];
+          j++;
+        } else {
+          ch = (unsigned char)b[j];
+          if (ch < 0x20 || ch > 0x7E) return false;
+        }
+        if (ch == '-' && prev >= 0 && j + 1 < b.size() && b[j + 1] != ']') {  // range prev-next
+          int hi;
+          if (b[j + 1] == '\\') {
+            if (j + 2 >= b.size() || std::string("dDwWsS").find(b[j + 2]) != std::string::npos || !esc_ok(b[j + 2])) return false;
+            hi = (unsigned char)b[j + 2];
+            j += 2;
+          } else {
+            if (b[j + 1] == '[') return false;
+            hi = (unsigned char)b[j + 1];
+            j++;
+          }
+          if (hi < prev) return false;
+          prev = -1;
+          continue;
+        }
+        prev = ch;
+      }
+      if (!closed) return false;
+      i = j;
+      atom = true; quant = false;
+    } else if (c == '(') {
+      if (i + 1 < b.size() && b[i + 1] == '?') {
+        if (i + 2 >= b.size() || b[i + 2] != ':') return false;
+        i += 2;
+      }
+      depth++;
+      atom = false; quant = false;
+    } else if (c == ')') {
+      if (--depth < 0) return false;
+      atom = true; quant = false;
+    } else if (c == '|') {
+      if (depth == 0 && anchored) return false;
+      atom = false; quant = false;
+    } else if (c == '*' || c == '+' || c == '?' || c == '{') {
+      if (!atom || quant) return false;
+      if (c == '{') {
+        size_t j = i + 1;
+        int lo = 0, hi = -2, nd = 0;
+        while (j < b.size() && isdigit((unsigned char)b[j]) && nd < 4) { lo = lo * 10 + (b[j++] - '0'); nd++; }
+        if (!nd) return false;
+        hi = lo;
+        if (j < b.size() && b[j] == ',') {
+          j++;
+          if (j < b.size() && b[j] == '}') hi = -1;
+          else {
+            int h = 0, hd = 0;
+            while (j < b.size() && isdigit((unsigned char)b[j]) && hd < 4) { h = h * 10 + (b[j++] - '0'); hd++; }
+            if (!hd) return false;
+            hi = h;
+          }
+        }
+        if (j >= b.size() || b[j] != '}' || lo > 64 || hi > 64 || (hi >= 0 && hi < lo)) return false;
+        i = j;
+      }
+      if (i + 1 < b.size() && b[i + 1] == '?') i++;      // lazy
+      if (i + 1 < b.size() && b[i + 1] == '+') return false;  // possessive: not RE2
+      quant = true;
+    } else if (c == '^' || c == '$' || c == ']' || c == '}') {
+      return false;
+    } else {
+      atom = true; quant = false;
+    }
+  }
+  if (depth != 0) return false;
+  try {
+    std::regex x(re, std::regex::ECMAScript);
+  } catch (std::regex_error&) {
     return false;
+  }
+  return true;
+}
+
+// every node within the restated interpreter (functions: keys(@), length(), contains(), to_upper() and regex_match()
+// with a raw-string pattern of the restated subset)
+static bool nodes_ok(const NP& n) {
+  if (n->k == NFunction && n->name == "regex_match") {
+    if (n->kids.size() != 2 || n->kids[0]->k != NLiteral || !n->kids[0]->lit || n->kids[0]->lit->t != T::Str ||
+        !rx_restated(n->kids[0]->lit->s))
+      return false;
+  } else if (n->k == NFunction && !(n->name == "length" && n->kids.size() == 1) &&
+             !(n->name == "contains" && n->kids.size() == 2) && !(n->name == "to_upper" && n->kids.size() == 1) &&
+             (n->name != "keys" || n->kids.size() != 1 || n->kids[0]->k != NCurrent)) {
+    return false;
+  }
   for (auto& k : n->kids) if (!nodes_ok(k)) return false;
   return true;
 }
@@ -395,7 +549,9 @@ bool jmes_supported(const std::string& expr, bool allow_element) {
     if (c->k == NField) return c->name == "element" && allow_element;
     for (;;) {
       if (c->kids.empty()) return false;
-      const Node* l = c->kids[0].get();
+      // a function's subject: regex_match's second argument (its first is the pattern literal), else the first
+      const Node* l = (c->k == NFunction && c->name == "regex_match" && c->kids.size() == 2) ? c->kids[1].get()
+                                                                                          : c->kids[0].get();
       if (l->k == NField) break;
       if (l->k != NSubexpr && l->k != NProjection && l->k != NFlatten && l->k != NOr && l->k != NFilterProjection)
         return false;

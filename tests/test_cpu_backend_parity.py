@@ -49,14 +49,13 @@ def test_condition_goldens_cpu():
 
 
 def test_c5_conditions_cpu():
-    """configs[4]: deny / preconditions with request.object variables, length() included, on the device; the rules
-    with regex_match / to_upper are handed to the CPU engine (every pair of theirs FALLBACK on both sides, counted)"""
+    """configs[4]: deny / preconditions with request.object variables, length() included, on the device; since round 6
+    the regex_match / to_upper rules too (per-string columns of the dictionary): no rule is handed to the CPU engine"""
     from kyverno_amd import synth
     from kyverno_amd import engine as E
     pols = synth.c5_policies(50)
     st, _ = S.run_synthetic("cpu", pols, 500, seed=12)
-    assert st["compared"] > 5000 and st["fallback"] > 0
+    assert st["compared"] > 5000
     rs = E.Ruleset(pols)
     fb = [r for r in rs.rules if r["kind"] == "fallback"]
-    assert fb and all(r["reason"] for r in fb), fb[:3]
-    assert len(fb) < len(rs.rules) // 4
+    assert not fb, fb[:3]

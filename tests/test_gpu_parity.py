@@ -112,10 +112,15 @@ def test_c5_oracle_matrix_at_scale():
     st, res = PU.compare_matrix(pols, data, nsl, backend="gpu", threads=_oracle_threads())
     assert st["nbad"] == 0, st["bad"]
     assert st["matched"] > 1_000_000
-    # length() / || / projections compile to the device; only the regex_match / to_upper rules are CPU fallback
-    cpu = {p["spec"]["rules"][0]["name"] for p in pols if "regex_match" in json.dumps(p) or "to_upper" in json.dumps(p)}
+    # length() / || / projections and (round 6) regex_match / to_upper on the dictionary compile to the device: no
+    # rule is CPU fallback, and the function rules decide pairs on the device
     fb = [r["name"] for r in res.ruleset.rules if r["kind"] == "fallback"]
-    assert fb and all(any(n.endswith(c) for c in cpu) for n in fb), (fb, cpu)
+    assert not fb, fb
+    fn = [k for k, r in enumerate(res.ruleset.rules)
+          if any(f in json.dumps(pols[r["policy"]]) for f in ("regex_match", "to_upper"))]
+    assert fn
+    st_fn = np.asarray(res.status)[fn] & 7
+    assert ((st_fn == K.ST_PASS) | (st_fn == K.ST_FAIL)).sum() > 100_000
 
 
 def test_repeat_launches_deterministic():
@@ -316,3 +321,79 @@ def test_pss_with_preconditions_gpu_equals_cpu(jit):
             for i in fails[:: max(1, len(fails) // 200)].tolist():
                 assert g.pss_mask(i, k) == c.pss_mask(i, k), (r["name"], i)
         assert nfail > 0
+
+
+def _pss_excl_policies():
+    """PodSecurity rules whose exclusions send pairs to pss_map_kernel (eval_pss's map walk over exclusion sub-pods):
+    the exclusion shapes of pkg/pss/evaluate_test.go (control-only, and control + images matching init, regular and
+    ephemeral containers) on baseline and restricted, pinned and latest versions (pkg/pss/evaluate.go:16-60,83-108)"""
+    def pol(name, level, version, excl, kinds=("Pod",)):
+        return {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": name},
+                "spec": {"rules": [{"name": name, "match": {"any": [{"resources": {"kinds": list(kinds)}}]},
+                                    "validate": {"podSecurity": {"level": level, "version": version, "exclude": excl}}}]}}
+    team1 = ["registry.example.com/team1*"]
+    return [
+        pol("bl-caps-img", "baseline", "latest", [{"controlName": "Capabilities", "images": team1}]),
+        pol("bl-ctl", "baseline", "v1.24", [{"controlName": "Host Namespaces"}, {"controlName": "HostPath Volumes"},
+                                            {"controlName": "Host Ports", "images": ["*:latest"]}]),
+        pol("bl-mixed", "baseline", "latest", [{"controlName": "Privileged Containers", "images": ["*"]},
+                                               {"controlName": "SELinux", "images": ["registry.example.com/team2?/*"]},
+                                               {"controlName": "Seccomp"}, {"controlName": "AppArmor"},
+                                               {"controlName": "/proc Mount Type", "images": team1}]),
+        pol("rs-img", "restricted", "latest", [{"controlName": "Running as Non-root", "images": team1},
+                                               {"controlName": "Privilege Escalation", "images": ["*:1.*"]},
+                                               {"controlName": "Capabilities", "images": ["registry.example.com/team3*"]}]),
+        pol("rs-ctl", "restricted", "v1.24", [{"controlName": "Volume Types"}, {"controlName": "Running as Non-root user"},
+                                              {"controlName": "Seccomp", "images": ["*"]}]),
+        pol("rs-wl", "restricted", "latest", [{"controlName": "Running as Non-root user", "images": team1},
+                                              {"controlName": "Privilege Escalation"}],
+            kinds=("Pod", "Deployment", "StatefulSet", "Job", "CronJob")),
+    ]
+
+
+# kyv_pss.h PssSlot order (pss_msg.cpp kSlots): the check id of each bit of a PodSecurity failure mask
+_PSS_SLOT_IDS = ["allowPrivilegeEscalation", "allowPrivilegeEscalation", "appArmorProfile", "capabilities_baseline",
+                 "capabilities_restricted", "capabilities_restricted", "hostNamespaces", "hostPathVolumes", "hostPorts",
+                 "privileged", "procMount", "restrictedVolumes", "runAsNonRoot", "runAsUser", "seLinuxOptions",
+                 "seccompProfile_baseline", "seccompProfile_baseline", "seccompProfile_restricted",
+                 "seccompProfile_restricted", "sysctls", "windowsHostProcess"]
+
+
+def test_pss_map_kernel_exclusions_at_scale_gpu():
+    """pss_map_kernel at scale (round-6 item: the map-form checks, pss_checks, use integer flag words like the column
+    form): 200k pods x six PodSecurity rules with exclusions against the oracle's verdict matrix; every FAIL pair's
+    check mask against the host instantiation of the same evaluator, and a sample of 20k FAIL pairs' failed-check sets
+    against the oracle's EvaluatePod (exclusion rules have no rendered message: exemptKyvernoExclusion orders its
+    checks by Go map iteration, evaluate.go:39-60)"""
+    import json
+    import parity_util as PU
+    from oracle import oracle as O
+    pols = _pss_excl_policies()
+    data, nsl = synth.corpus_ndjson(200_000, kind="pods", seed=61, edge=True)
+    st, res = PU.compare_matrix(pols, data, nsl, backend="gpu", threads=_oracle_threads(), texts=False)
+    assert st["nbad"] == 0, st["bad"]
+    assert st["matched"] >= 6 * 200_000
+    assert res.counts["fail"] > 100_000 and res.counts["pass"] > 0
+    rs = E.Ruleset(pols)
+    b = E.Batch(rs, data, nsl)
+    g = E.evaluate(rs, b, backend="gpu")
+    c = E.evaluate(rs, b, backend="cpu")
+    assert np.array_equal(g.raw, c.raw)
+    lines = [x for x in data.split(b"\n") if x.strip()]
+    rng = np.random.default_rng(6)
+    nmask, noracle = 0, 0
+    for k, r in enumerate(rs.rules):
+        assert r["kind"] == "podSecurity"
+        pname = rs.policies[r["policy"]]["name"]
+        psr = [p for p in pols if p["metadata"]["name"] == pname][0]["spec"]["rules"][0]["validate"]["podSecurity"]
+        fails = np.nonzero(np.asarray(g.status[k]) == K.ST_FAIL)[0]
+        for i in fails.tolist():
+            assert g.pss_mask(i, k) == c.pss_mask(i, k), (r["name"], i)
+        nmask += len(fails)
+        for i in rng.choice(fails, size=min(len(fails), 4000), replace=False).tolist() if len(fails) else []:
+            m = g.pss_mask(i, k)
+            got = {_PSS_SLOT_IDS[s] for s in range(len(_PSS_SLOT_IDS)) if (m >> s) & 1}
+            want = {x["id"] for x in O.pss(psr, json.loads(lines[i]))["checks"]}
+            assert got == want, (r["name"], i, sorted(got), sorted(want))
+            noracle += 1
+    assert nmask > 100_000 and noracle >= 20_000
