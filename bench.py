@@ -643,6 +643,14 @@ def main():
             gathers = {"error": str(e)[:300]}
         log("rank %d: device-resident gathers %s" % (rank, gathers))
 
+    # FETCH_SIZE calibration for the profiling runs (scripts/profile_box.sh sets KYV_CALIB=1): launches of known byte
+    # counts at the access widths the evaluation kernels use, read back by scripts/pmc_summary.py
+    if os.environ.get("KYV_CALIB") == "1" and rank == 0:
+        from kyverno_amd import _lib as KL
+        for mode in (4, 8, 16, 116):
+            ms = KL.lib().kyv_calibrate_fetch(local, 1 << 30, mode)
+            log("calibration launch: mode %d, 1 GiB in %.3f ms" % (mode, ms))
+
     # end to end on this rank: JSON -> flatten -> H2D -> evaluate -> D2H of every verdict (walk kernel already loaded)
     e2e = None
     if not args.no_e2e:

@@ -298,6 +298,12 @@ int64_t kyv_results_pss_checks(const kyv_results* r, const kyv_ruleset* rs, cons
 /* PodSecurity rules: failing (check, version) slot mask after exclusions */
 uint32_t kyv_results_pss_mask(const kyv_results* r, const kyv_ruleset* rs, uint32_t res, uint32_t rule);
 
+/* measurement only (not a reference interface): one streaming-read launch of `bytes` on `device` -- mode 4 / 8 / 16
+ * bytes per lane coalesced, 116 a gather of 16-byte rows -- whose known byte count calibrates rocprofv3's FETCH_SIZE
+ * for the access widths the evaluation kernels use (bench.py KYV_CALIB=1, scripts/pmc_summary.py). Returns device ms,
+ * -1 on error. */
+double kyv_calibrate_fetch(int device, uint64_t bytes, int mode);
+
 const char* kyv_last_error(void);
 const char* kyv_version(void);
 

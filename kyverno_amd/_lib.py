@@ -65,6 +65,7 @@ EXPORTS = [
     "kyv_results_texts", "kyv_results_phase_ms", "kyv_results_alg_bytes_phase", "kyv_results_alg_bytes_class", "kyv_batch_export_status", "kyv_batch_copy_status",
     "kyv_batch_export_failures", "kyv_comm_unique_id", "kyv_comm_init", "kyv_comm_free", "kyv_comm_gather_results",
     "kyv_comm_gathered_status", "kyv_comm_gathered_failures", "kyv_comm_gather_report", "kyv_comm_reduce_counts", "kyv_results_batch_ms",
+    "kyv_calibrate_fetch",
 ]
 
 
@@ -149,6 +150,8 @@ def lib():
     L.kyv_results_count.restype = i64
     L.kyv_results_kernel_ms.argtypes = [vp]
     L.kyv_results_kernel_ms.restype = ctypes.c_double
+    L.kyv_calibrate_fetch.argtypes = [i32, ctypes.c_uint64, i32]
+    L.kyv_calibrate_fetch.restype = ctypes.c_double
     L.kyv_results_alg_bytes.argtypes = [vp]
     L.kyv_results_alg_bytes.restype = ctypes.c_uint64
     L.kyv_results_message.argtypes = [vp, vp, vp, u32, u32, ctypes.c_char_p, sz]

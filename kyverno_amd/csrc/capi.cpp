@@ -28,6 +28,7 @@ int64_t export_report_rows(const Batch& b, int device, uint32_t* rows, uint32_t*
 const unsigned long long* device_counts(const Batch& b, int device, size_t* nrules, size_t* nres);
 bool pss_checks_render(const Ruleset& rs, const Batch& b, uint32_t pos, uint32_t rule, uint32_t mask,
                        std::vector<std::array<std::string, 3>>* out);
+double calibrate_fetch(int device, size_t bytes, int mode);
 }  // namespace kyv
 
 using namespace kyv;
@@ -331,6 +332,14 @@ int kyv_results_rule_counts(const kyv_results* r, int64_t* out, size_t cap) {
 }
 
 double kyv_results_kernel_ms(const kyv_results* r) { return r ? r->r.kernel_ms : 0; }
+double kyv_calibrate_fetch(int device, uint64_t bytes, int mode) {
+  try {
+    return calibrate_fetch(device, (size_t)bytes, mode);
+  } catch (std::exception& e) {
+    fail(KYV_EDEVICE, e.what());
+    return -1;
+  }
+}
 double kyv_results_batch_ms(const kyv_results* r, int what) {
   if (!r) return 0;
   return what == 0 ? r->r.h2d_ms : what == 1 ? r->r.gmask_ms : 0;

@@ -1501,10 +1501,6 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     if (!heavy.empty()) { groups.push_back(heavy); gwpe.push_back(-1); }
   }
   const size_t ngroups = groups.size();
-  // round 6: root-scope column prefetch of the fused walk (kyv_fused.h): the first pf_cols columns of every fused
-  // pattern rule's root scope (0: off)
-  const size_t pf_cols = getenv("KYV_FUSED_PREFETCH") ? (size_t)std::max(0, atoi(getenv("KYV_FUSED_PREFETCH"))) : 0;
-  std::set<uint32_t> pf_root_done;
   std::vector<std::pair<size_t, size_t>> fused_kernels;  // (group, part): kyv_jit_fused_<g>[p<part>]
   std::vector<size_t> merged_groups;                      // groups with a kyv_jit_fusedm_<g> (KYV_FUSED_MERGE)
   for (size_t gi = 0; gi < ngroups; gi++) {
@@ -1530,30 +1526,6 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
              "  jfinish(w, r, out);\n"
              "}\n";
-    // KYV_FUSED_PREFETCH=n: the fused pattern rules' root functions also in a form that takes the first n root-scope
-    // columns from the caller (read from the wave's LDS prefetch slots, kyv_fused.h kyv_pf_col) and loads the rest
-    if (pf_cols)
-      for (size_t i : fused) {
-        const RuleDesc& rd = rs.rules[rule_roots[i].first];
-        if (rd.kind != RK_PATTERN || rule_roots[i].second.size() != 1) continue;
-        const uint32_t r = rep_of[rule_roots[i].second[0]];
-        const auto& L = g.scope_cols(r);
-        if (L.empty() || !pf_root_done.insert(r).second) continue;
-        src << "static __device__ __forceinline__ void rootP" << r
-            << "(const View& v, const Node* R, const ResHeader* hp, uint32_t row, uint32_t mbase, bool rootmap, bool walk,\n"
-               "    PatOut& out, const uint64_t* pfx) {\n"
-               "  uint64_t pc[" << L.size() << "];";
-        for (size_t q = 0; q < L.size(); q++) {
-          if (q < pf_cols) src << " pc[" << q << "] = pfx[" << q << "];";
-          else src << " pc[" << q << "] = jc_col(v, " << Gen::u(L[q]) << ", row);";
-        }
-        src << "\n"
-               "  if (!walk) return;\n"
-               "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
-               "  Ret rr = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
-               "  jfinish(w, rr, out);\n"
-               "}\n";
-      }
     if (roots.size() > 256) {
       std::map<uint32_t, std::vector<uint32_t>> br2;
       for (uint32_t r : roots) br2[rep_of[r]].push_back(r);
@@ -1607,26 +1579,6 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     for (size_t pi = 0; pi < nparts; pi++) {
       const std::vector<size_t> part(fused.begin() + fused.size() * pi / nparts, fused.begin() + fused.size() * (pi + 1) / nparts);
       const std::string sname = "JitFused" + std::to_string(gi) + (pi ? "p" + std::to_string(pi) : std::string());
-      // prefetching rules of the part (KYV_FUSED_PREFETCH): pattern rules with one root whose scope has columns; at
-      // most 64 per part (one bit each of the wave's uniform mask `gm` of the rules it will walk)
-      std::vector<std::vector<uint32_t>> pfl(part.size());
-      size_t pfmax = 0;
-      if (pf_cols)
-        for (size_t j = 0; j < part.size() && j < 64; j++) {
-          const RuleDesc& rd = rs.rules[rule_roots[part[j]].first];
-          if (rd.kind != RK_PATTERN || rule_roots[part[j]].second.size() != 1) continue;
-          const auto& L = g.scope_cols(rep_of[rule_roots[part[j]].second[0]]);
-          pfl[j].assign(L.begin(), L.begin() + std::min(L.size(), pf_cols));
-          pfmax = std::max(pfmax, pfl[j].size());
-        }
-      if (pfmax) {  // [rule of the part][column count, its first pfmax root-scope columns]
-        src << "__device__ const uint32_t kyv_pfc_" << sname << "[" << part.size() * (pfmax + 1) << "] = {";
-        for (size_t j = 0; j < part.size(); j++) {
-          src << (j ? ", " : "") << pfl[j].size() << "u";
-          for (size_t q = 0; q < pfmax; q++) src << ", " << (q < pfl[j].size() ? pfl[j][q] : 0u) << "u";
-        }
-        src << "};\n";
-      }
       src << "struct " << sname << " {\n"
              "  __device__ __forceinline__ void run(const View& v, const DevOut& o, uint32_t nwaves, uint32_t w, uint32_t r,\n"
              "                                     bool active, uint32_t hflags, uint32_t hroot, const uint32_t* gw) {\n"
@@ -1636,25 +1588,6 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "    const uint32_t row = r < v.nres ? r : NONE;\n"
              "    const bool rootmap = (hflags & RF_ROOT_MAP) != 0;\n"
              "    (void)lane; (void)hp; (void)rootmap;\n";
-      if (pfmax) {
-        // the wave's LDS slots, the uniform mask of the prefetching rules it walks, and the issue of one rule's columns
-        src << "    __shared__ uint64_t kpf[" << pfmax * 64 << "];\n"
-               "    const uint32_t row0 = w * 64u;\n"
-               "    uint64_t gm = 0;\n";
-        for (size_t j = 0; j < part.size(); j++) {
-          if (pfl[j].empty()) continue;
-          const uint32_t k = rule_roots[part[j]].first;
-          src << "    if (" << k << "u >= o.rule_lo && " << k << "u < o.rule_hi && __ballot(active && ((gw[" << k / 32 << "] >> "
-              << k % 32 << "u) & 1u))) gm |= 1ull << " << j << ";\n";
-        }
-        // one table-driven issue loop (uniform: the rule index comes from `gm`), not a switch per call site
-        src << "    auto pf_issue = [&](uint32_t jj) {\n"
-               "      const uint32_t* t = kyv_pfc_" << sname << " + jj * " << pfmax + 1 << "u;\n"
-               "      const uint32_t nc = t[0];\n"
-               "      for (uint32_t q = 0; q < nc; q++) kyv_pf_col(v, t[1 + q], row0, lane, kpf + q * 64u);\n"
-               "    };\n"
-               "    if (gm) pf_issue((uint32_t)__builtin_ctzll(gm));\n";
-      }
       for (size_t j = 0; j < part.size(); j++) {
       const size_t i = part[j];
       const uint32_t k = rule_roots[i].first;
@@ -1665,15 +1598,6 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
       src << "    if (" << K << " >= o.rule_lo && " << K << " < o.rule_hi) {\n"
              "      const bool gated = active && ((gw[" << k / 32 << "] >> " << k % 32 << "u) & 1u);\n"
              "      if (__ballot(gated)) {\n";
-      if (!pfl[j].empty()) {
-        // this rule's columns were issued by the previous prefetching rule (or before the first): wait, read them into
-        // registers, release the slots and issue the next rule's columns before this rule's own loads
-        src << "        kyv_pf_wait();\n"
-               "        uint64_t pfx[" << pfl[j].size() << "];\n";
-        for (size_t q = 0; q < pfl[j].size(); q++) src << "        pfx[" << q << "] = kpf[" << q * 64 << "u + lane];\n";
-        src << "        kyv_pf_release();\n"
-               "        { const uint64_t nx = gm & ~((2ull << " << j << ") - 1ull); if (nx) pf_issue((uint32_t)__builtin_ctzll(nx)); }\n";
-      }
       src << "        const bool magic = gated && (hflags & RF_MAGIC);\n"
              "        WaveSink sink{o.stage + sld32(o.rbase + (" << K << " - o.rule_lo)) + (size_t)w * 64u * " << alts
           << "u, 0u, " << (rd.uses_meta ? "true" : "false") << "};\n"
@@ -1683,12 +1607,8 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "          switch (a) {\n";
       for (uint32_t a = 0; a < nalts; a++) {
         const uint32_t root = rule_roots[i].second[a];
-        if (!pfl[j].empty())
-          src << "            case " << a << "u: rootP" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
-              << ", rootmap, wk, po, pfx); break;\n";
-        else
-          src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
-              << ", rootmap, wk, po); break;\n";
+        src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+            << ", rootmap, wk, po); break;\n";
       }
       src << "            default: break;\n"
              "          }\n"

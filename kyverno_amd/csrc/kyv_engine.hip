@@ -163,7 +163,6 @@ struct Packer {
     size = off + bytes + 16;
     return off;
   }
-  void pad(size_t bytes) { size += bytes; }  // zeroed bytes behind the last part added
   hipError_t copy_to(uint8_t* dev) const {
     hipStream_t s = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
@@ -486,7 +485,6 @@ static DevBatch* upload_batch(const Batch& b, int device) {
   d->o_supper = b.str_upper.empty() ? SIZE_MAX : p.add(b.str_upper);
   d->o_srx = b.str_rx.empty() ? SIZE_MAX : p.add(b.str_rx);
   d->o_colv = p.add(b.colv);
-  p.pad(512);  // the fused walk's column prefetch reads a whole match wave's 64 rows (kyv_fused.h kyv_pf_col)
   d->o_coloff = p.add(b.col_off);
   // batch-specialised copy of the pattern entries: `col` holds the column's absolute offset into colv, so the
   // walker reads a lookup's column without first reading the batch's column offset table
@@ -768,6 +766,39 @@ __global__ void __launch_bounds__(HIST_BLOCK) status_hist_kernel(const uint8_t* 
 }
 
 // wildcard.Match(pattern g, string s) for every dictionary string (one thread each) and masked pattern; then the
+// FETCH_SIZE calibration (bench.py KYV_CALIB=1, scripts/pmc_summary.py): streaming reads of a known byte count at W
+// bytes per lane (coalesced, grid-stride), and a gather of 16-byte rows (every row once, in a scrambled order) -- the
+// guide leaves these access widths uncalibrated (MI355X_MICROARCH.md, HBM), and the walk's reads are 8-byte column
+// entries, 16-byte node rows and 4-byte fields
+template <int W>
+__global__ void __launch_bounds__(256) calib_read_kernel(const uint8_t* __restrict__ p, size_t n, uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x * W;
+  for (size_t off = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * W; off + W <= n; off += stride) {
+    if constexpr (W == 4) {
+      acc ^= *(const uint32_t*)(p + off);
+    } else if constexpr (W == 8) {
+      const uint2 x = *(const uint2*)(p + off);
+      acc ^= x.x ^ x.y;
+    } else {
+      const uint4 x = *(const uint4*)(p + off);
+      acc ^= x.x ^ x.y ^ x.z ^ x.w;
+    }
+  }
+  if (acc == 0x9E3779B9u) out[0] = acc;  // (keeps the loads)
+}
+__global__ void __launch_bounds__(256) calib_gather_kernel(const uint4* __restrict__ rows, size_t nrows,
+                                                           uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrows; i += stride) {
+    const size_t j = (i * 0x9E3779B97F4A7C15ull) & (nrows - 1);  // odd multiplier mod 2^k: a permutation of the rows
+    const uint4 x = rows[j];
+    acc ^= x.x ^ x.y ^ x.z ^ x.w;
+  }
+  if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
 // condition sets (compiler.cpp assign_cond_sets): bit ng + q = wild2(s, e) for some literal e of set q (kyv_cond.h wild2,
 // both match directions)
 __global__ void __launch_bounds__(256) gmask_kernel(const View* __restrict__ vp, const uint32_t* __restrict__ gpats,
@@ -2778,6 +2809,39 @@ void free_device_images(Ruleset& rs, Batch* b) {
       }
     rs.dev.clear();
   }
+}
+
+// one calibration launch (see calib_read_kernel): mode 4 / 8 / 16 = coalesced reads of that many bytes per lane, 116 =
+// gather of 16-byte rows; bytes rounded down to a power of two for the gather. Returns the launch's device time (ms)
+double calibrate_fetch(int device, size_t bytes, int mode) {
+  HIP_OK(hipSetDevice(device));
+  if (mode == 116) { size_t b = 16; while (b * 2 <= bytes) b *= 2; bytes = b; }
+  uint8_t* p = nullptr;
+  uint32_t* out = nullptr;
+  HIP_OK(hipMalloc(&p, bytes));
+  HIP_OK(hipMalloc(&out, 4));
+  struct Free { void* a; void* b; ~Free() { (void)hipFree(a); (void)hipFree(b); } } fr{p, out};
+  HIP_OK(hipMemset(p, 1, bytes));
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  const unsigned grid = 256 * 32;
+  HIP_OK(hipEventRecord(e0, nullptr));
+  switch (mode) {
+    case 4: hipLaunchKernelGGL(calib_read_kernel<4>, dim3(grid), dim3(256), 0, nullptr, p, bytes, out); break;
+    case 8: hipLaunchKernelGGL(calib_read_kernel<8>, dim3(grid), dim3(256), 0, nullptr, p, bytes, out); break;
+    case 16: hipLaunchKernelGGL(calib_read_kernel<16>, dim3(grid), dim3(256), 0, nullptr, p, bytes, out); break;
+    case 116: hipLaunchKernelGGL(calib_gather_kernel, dim3(grid), dim3(256), 0, nullptr, (const uint4*)p, bytes / 16, out); break;
+    default: throw std::runtime_error("calibrate_fetch: mode 4, 8, 16 or 116");
+  }
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(e1, nullptr));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ms;
 }
 
 }  // namespace kyv

@@ -17,24 +17,6 @@ namespace kyv {
 #define KYV_FUSED_GW 8  // kind-gate words a fused wave keeps in registers (rulesets of <= 256 rules)
 #endif
 
-// Root-scope column prefetch of the fused walk (round 6, KYV_FUSED_PREFETCH=n at source generation, jit.cpp): while a
-// wave walks rule j, the first n root-scope columns of the next rule it will walk are already on their way into the
-// wave's LDS slots by LDS-DMA (global_load_lds: no VGPR holds them in flight). A match wave's 64 resources are 64
-// consecutive rows, so one column's entries are 512 contiguous bytes: 32 lanes x 16 B. The batch image keeps 512 B of
-// padding behind the column array (upload_batch), so the last, partial match wave reads in bounds (its rows past nres
-// belong to no lane that walks).
-__device__ __forceinline__ void kyv_pf_col(const View& v, uint32_t col, uint32_t row0, uint32_t lane, uint64_t* slot) {
-  const uint32_t off = sld32(v.col_off + col);
-  if (lane < 32u)
-    __builtin_amdgcn_global_load_lds((const void*)(v.colv + (size_t)off + row0 + 2u * lane),
-                                     (__attribute__((address_space(3))) void*)slot, 16, 0, 0);
-  KYV_ACCT_ADD(0, 8);  // the lane's row of the column, as jc_col counts it
-}
-// the compiler does not order an LDS read behind an LDS-DMA write: wait for every vector memory operation first
-__device__ __forceinline__ void kyv_pf_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// the wave's LDS reads of the slots have returned: the slots may be refilled
-__device__ __forceinline__ void kyv_pf_release() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 template <class Fused>
 __device__ __forceinline__ void walk_fused(const View& v, DevOut o, uint32_t nwaves, Fused& f) {
   const uint32_t lane = threadIdx.x & (WAVE - 1);

@@ -25,6 +25,8 @@ def is_eval(name):
     n = name[5:] if name.startswith("void ") else name  # templates: "void kyv::match_kernel<true>(...)"
     if n.startswith("kyv::gmask_kernel"):  # once per batch (glob masks of the dictionary), not per evaluation
         return False
+    if n.startswith("kyv::calib_"):  # FETCH_SIZE calibration launches (bench.py KYV_CALIB=1), reported apart
+        return False
     return n.startswith("kyv::") or n.startswith("kyv_jit")
 
 
@@ -36,12 +38,16 @@ def main(tag):
     stats = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))) if is_eval(r["Name"])]
     per_kernel = {r["Name"].split("(")[0]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])} for r in stats}
     counters = {}  # kernel -> counter -> values
+    calib = {}     # calibration kernel -> FETCH_SIZE bytes per launch (each launch reads exactly 1 GiB)
     rows_out = []
     for p in sorted(os.listdir(src)):
         f = os.path.join(src, p, "run_counter_collection.csv")
         if not p.startswith("pmc_") or not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
+            kname = r["Kernel_Name"][5:] if r["Kernel_Name"].startswith("void ") else r["Kernel_Name"]
+            if kname.startswith("kyv::calib_") and r["Counter_Name"] == "FETCH_SIZE":
+                calib.setdefault(kname.split("(")[0], []).append(float(r["Counter_Value"]) * 1024)
             if not is_eval(r["Kernel_Name"]):
                 continue
             kn = r["Kernel_Name"].split("(")[0]
@@ -105,6 +111,12 @@ def main(tag):
         "traffic_note": "memory-side bytes of one evaluation (every launch of its kernels) from TCC_EA (FETCH_SIZE + "
                         "WRITE_SIZE, KiB x 1024); traffic_bytes_x2read applies the guide's x2 wide-stream read correction",
     }
+    if calib:  # known bytes / counted bytes per access width (bench.py KYV_CALIB=1: 1 GiB per launch)
+        out["fetch_calibration"] = {k: {"bytes": float(1 << 30), "fetch_size_bytes": sum(v) / len(v),
+                                        "factor": float(1 << 30) / max(1.0, sum(v) / len(v))} for k, v in calib.items()}
+        out["fetch_calibration_note"] = ("factor = true bytes / FETCH_SIZE bytes of a launch that reads a known 1 GiB: "
+                                         "calib_read_kernel<W> coalesced W bytes per lane, calib_gather_kernel 16-byte "
+                                         "rows in scrambled order")
     if dom_phase in ph:
         out["dominant_l2_hit_rate"] = ph[dom_phase].get("l2_hit_rate")
         out["dominant_wait_frac"] = ph[dom_phase].get("wait_frac")
