@@ -953,44 +953,6 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
           b->nsl_off.push_back((uint32_t)b->nsl_kv.size() / 2);
         }
     }
-    // to_upper on the dictionary (round 6, kyverno functions.go:681-689 strings.ToUpper): every string's upper-case
-    // form, interned so that a result compares, globs and parses like any other dictionary string; strings with no
-    // lowercase letter map to themselves, non-ASCII strings to NONE (their pairs go to the CPU engine). The lookups run
-    // in parallel over the finished shards; only strings the batch does not hold yet are interned, serially.
-    if (rs->uses_upper) {
-      const size_t n0 = b->dict.strs.size();
-      std::vector<uint32_t> up(n0, NONE);
-      std::vector<uint8_t> todo(n0, 0);
-      parallel_for(std::max<size_t>(1, std::min<size_t>((size_t)T * 4, n0 / 4096 + 1)), T, [&](size_t k) {
-        const size_t nk = std::max<size_t>(1, std::min<size_t>((size_t)T * 4, n0 / 4096 + 1));
-        for (size_t s2 = n0 * k / nk; s2 < n0 * (k + 1) / nk; s2++) {
-          const std::string& x = b->dict.strs[s2];
-          bool lower = false, ascii = true;
-          for (unsigned char ch : x) { ascii = ascii && ch < 0x80; lower = lower || (ch >= 'a' && ch <= 'z'); }
-          if (!ascii) continue;
-          if (!lower) { up[s2] = (uint32_t)s2; continue; }
-          std::string u = x;
-          for (char& ch : u) if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 'a' + 'A');
-          const uint64_t h = hash_bytes(u.data(), u.size());
-          uint32_t id = seedtab.find(u, h);
-          if (id == NONE) {
-            id = shard[shard_of(h)].find(u, h);
-            if (id != NONE) id = (uint32_t)(shbase[shard_of(h)] + id);
-          }
-          if (id != NONE) up[s2] = id;
-          else todo[s2] = 1;
-        }
-      });
-      for (size_t s2 = 0; s2 < n0; s2++)
-        if (todo[s2]) {
-          std::string u = b->dict.strs[s2];
-          for (char& ch : u) if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 'a' + 'A');
-          up[s2] = intern(u);
-        }
-      b->str_upper.assign(b->dict.strs.size(), 0);
-      for (size_t s2 = 0; s2 < b->dict.strs.size(); s2++) b->str_upper[s2] = s2 < n0 ? up[s2] : (uint32_t)s2;
-      phase("upper");
-    }
     // concatenate + remap + sort map entries by key id (+ labels / annotations entries found again after the sort)
     size_t total_nodes = 0, total_res = 0, total_faux = 0;
     std::vector<size_t> node_base(nchunks), res_base(nchunks), faux_base(nchunks);
@@ -1081,6 +1043,79 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
     phase("remap");
     derive_strings(*b, 0, std::max(1, std::min(T, (int)(b->dict.strs.size() / 8192) + 1)));
     phase("strings");
+    order_by_kind(*b);
+    phase("kind-order");
+    resolve_path_columns(*b, T);
+    phase("path-cols");
+    // to_upper on the dictionary (round 6, kyverno functions.go:681-689 strings.ToUpper): the upper-case form of every
+    // string that can reach a to_upper argument -- the values of the argument's field chain (its path column, filled
+    // above) and the ruleset's literals (`|| 'default'`) -- interned, so that a result compares, globs and parses like
+    // any other dictionary string (the new strings' derived columns are computed here). Strings with no lowercase
+    // letter map to themselves; non-ASCII strings and strings outside that domain to NONE (the pair goes to the CPU
+    // engine: a value the column does not hold, e.g. of a resource without path columns).
+    if (rs->uses_upper) {
+      const size_t n0 = b->dict.strs.size();
+      std::vector<uint8_t> want(n0, 0);
+      for (size_t s2 = 0; s2 < rs->dict.strs.size() && s2 < n0; s2++) want[s2] = 1;
+      bool all = false;
+      auto mark_operand = [&](const CondOperand& o) {
+        if (o.kind != OK_JMES) return;
+        const uint32_t* p = rs->pool.data() + o.a;
+        if (!jmes_chain_form(p, o.nseg)) return;
+        bool up = false;
+        for (uint32_t q = 1; q < o.nseg; q += jop_width(p + q)) up = up || p[q] == JO_UPPER;
+        if (!up) return;
+        uint32_t t = 0;  // the chain's trie position (request.object = the resource root)
+        for (uint32_t q = 1; q + 1 < o.nseg && p[q] == JO_FIELD && t != NONE; q += 2) {
+          uint32_t nx = NONE;
+          for (const auto& kv : rs->trie[t].kids) if (kv.first == p[q + 1]) nx = kv.second;
+          t = nx;
+        }
+        const uint32_t col = t == NONE ? NONE : rs->trie[t].col;
+        if (col == NONE || col >= b->col_off.size()) { all = true; return; }
+        const size_t rows = b->rs_rows[rs->col_rowspace[col]];
+        const uint64_t* cv = b->colv.data() + b->col_off[col];
+        for (size_t r2 = 0; r2 < rows; r2++) {
+          const uint32_t lo = (uint32_t)cv[r2];
+          if (lo != NONE && (lo >> COL_TYPE_SHIFT) == N_STR && (uint32_t)(cv[r2] >> 32) < n0) want[(uint32_t)(cv[r2] >> 32)] = 1;
+        }
+      };
+      for (const Cond& c : rs->conds) { mark_operand(c.key); mark_operand(c.value); }
+      std::vector<uint32_t> up(n0, NONE);
+      std::vector<uint8_t> todo(n0, 0);
+      const size_t nk = std::max<size_t>(1, std::min<size_t>((size_t)T * 4, n0 / 4096 + 1));
+      parallel_for(nk, T, [&](size_t k) {
+        for (size_t s2 = n0 * k / nk; s2 < n0 * (k + 1) / nk; s2++) {
+          if (!all && !want[s2]) continue;
+          const std::string& x = b->dict.strs[s2];
+          bool lower = false, ascii = true;
+          for (unsigned char ch : x) { ascii = ascii && ch < 0x80; lower = lower || (ch >= 'a' && ch <= 'z'); }
+          if (!ascii) continue;
+          if (!lower) { up[s2] = (uint32_t)s2; continue; }
+          std::string u = x;
+          for (char& ch : u) if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 'a' + 'A');
+          const uint64_t h = hash_bytes(u.data(), u.size());
+          uint32_t id = seedtab.find(u, h);
+          if (id == NONE) {
+            id = shard[shard_of(h)].find(u, h);
+            if (id != NONE) id = (uint32_t)(shbase[shard_of(h)] + id);
+          }
+          if (id != NONE) up[s2] = id;
+          else todo[s2] = 1;
+        }
+      });
+      for (size_t s2 = 0; s2 < n0; s2++)
+        if (todo[s2]) {
+          std::string u = b->dict.strs[s2];
+          for (char& ch : u) if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 'a' + 'A');
+          up[s2] = intern(u);
+        }
+      const size_t n1 = b->dict.strs.size();
+      if (n1 > n0) derive_strings(*b, n0, std::max(1, std::min(T, (int)((n1 - n0) / 8192) + 1)));
+      b->str_upper.assign(n1, NONE);
+      for (size_t s2 = 0; s2 < n1; s2++) b->str_upper[s2] = s2 < n0 ? up[s2] : (uint32_t)s2;
+      phase("upper");
+    }
     // regex_match on the dictionary (round 6, kyverno functions.go:786-799 regexp.Match): bit q of a string = its match
     // by the ruleset's regex q (regex.cpp DFA, the device subset), RX_FB for a string with a byte outside printable
     // ASCII (its pairs go to the CPU engine)
@@ -1102,10 +1137,6 @@ Batch* build_batch(const Ruleset* rs, const char* json, size_t len, const char* 
       });
       phase("regex");
     }
-    order_by_kind(*b);
-    phase("kind-order");
-    resolve_path_columns(*b, T);
-    phase("path-cols");
     if ((!b->str_upper.empty() && b->str_upper.size() != b->dict.strs.size()) ||
         (!b->str_rx.empty() && b->str_rx.size() != b->dict.strs.size()))
       throw std::runtime_error("internal: per-string JMESPath columns do not cover the dictionary");

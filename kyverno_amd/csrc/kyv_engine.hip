@@ -54,6 +54,13 @@ struct Staging {
   std::mutex mu;
   void* buf[NSLOT] = {nullptr, nullptr, nullptr};
   hipEvent_t ev[NSLOT] = {nullptr, nullptr, nullptr};
+  // The ring's DMAs run on its own stream (round 6): a slot event is only ever recorded on this stream, never on a
+  // caller's stream that may be destroyed before the slot is reused (HIP then failed the next hipEventSynchronize of
+  // the slot with "operation not permitted on an event last recorded in a capturing stream": a batch upload right
+  // after an evaluation whose stream was gone). `pre` orders the ring after the caller's stream, `join` the caller's
+  // stream after the ring.
+  hipStream_t st = nullptr;
+  hipEvent_t pre = nullptr, join = nullptr;
   int dev = -1;
   bool ok = false;
   bool init(int device) {
@@ -64,8 +71,24 @@ struct Staging {
       if (hipHostMalloc(&buf[i], CHUNK, hipHostMallocDefault) != hipSuccess) { release(); return false; }
       if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) { release(); return false; }
     }
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&pre, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess) {
+      release();
+      return false;
+    }
     ok = true;
     return true;
+  }
+  // the ring's stream starts after everything queued on `caller` so far
+  hipError_t after(hipStream_t caller) {
+    hipError_t e = hipEventRecord(pre, caller);
+    return e == hipSuccess ? hipStreamWaitEvent(st, pre, 0) : e;
+  }
+  // `caller` continues after everything queued on the ring's stream so far
+  hipError_t before(hipStream_t caller) {
+    hipError_t e = hipEventRecord(join, st);
+    return e == hipSuccess ? hipStreamWaitEvent(caller, join, 0) : e;
   }
   void release() {
     for (int i = 0; i < NSLOT; i++) {
@@ -75,6 +98,11 @@ struct Staging {
       buf[i] = nullptr;
       ev[i] = nullptr;
     }
+    if (st) { (void)hipStreamSynchronize(st); (void)hipStreamDestroy(st); }
+    if (pre) (void)hipEventDestroy(pre);
+    if (join) (void)hipEventDestroy(join);
+    st = nullptr;
+    pre = join = nullptr;
     ok = false;
   }
 };
@@ -107,15 +135,17 @@ static hipError_t staged_h2d(uint8_t* dev, const void* src, size_t n, hipStream_
   std::unique_lock<std::mutex> lk(g_staging.mu);
   if (staging_off() || !g_staging.init(device)) return hipMemcpy(dev, src, n, hipMemcpyHostToDevice);
   static int slot = 0;
+  if ((e = g_staging.after(stream)) != hipSuccess) return e;
+  const hipStream_t rs = g_staging.st;
   for (size_t off = 0; off < n; off += Staging::CHUNK) {
     const size_t m = std::min(Staging::CHUNK, n - off);
     if ((e = hipEventSynchronize(g_staging.ev[slot])) != hipSuccess) return e;  // the slot's last transfer is done
     par_memcpy(g_staging.buf[slot], (const uint8_t*)src + off, m);
-    if ((e = hipMemcpyAsync(dev + off, g_staging.buf[slot], m, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
-    if ((e = hipEventRecord(g_staging.ev[slot], stream)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(dev + off, g_staging.buf[slot], m, hipMemcpyHostToDevice, rs)) != hipSuccess) return e;
+    if ((e = hipEventRecord(g_staging.ev[slot], rs)) != hipSuccess) return e;
     slot = (slot + 1) % Staging::NSLOT;
   }
-  return hipSuccess;
+  return g_staging.before(stream);
 }
 // device -> host through the pinned ring: chunk i's DMA overlaps the copy-out of chunk i-1
 static hipError_t staged_d2h(void* dst, const uint8_t* dev, size_t n, hipStream_t stream) {
@@ -133,9 +163,10 @@ static hipError_t staged_d2h(void* dst, const uint8_t* dev, size_t n, hipStream_
     // reading their slots) from this or another host thread; the DMA into the slot waits for it
     hipError_t r = hipEventSynchronize(g_staging.ev[sl]);
     if (r != hipSuccess) return r;
-    r = hipMemcpyAsync(g_staging.buf[sl], dev + off, m, hipMemcpyDeviceToHost, stream);
-    return r == hipSuccess ? hipEventRecord(g_staging.ev[sl], stream) : r;
+    r = hipMemcpyAsync(g_staging.buf[sl], dev + off, m, hipMemcpyDeviceToHost, g_staging.st);
+    return r == hipSuccess ? hipEventRecord(g_staging.ev[sl], g_staging.st) : r;
   };
+  if ((e = g_staging.after(stream)) != hipSuccess) return e;
   for (size_t c = 0; c < nch && c < (size_t)Staging::NSLOT - 1; c++)
     if ((e = issue(c)) != hipSuccess) return e;
   for (size_t c = 0; c < nch; c++) {
@@ -145,7 +176,7 @@ static hipError_t staged_d2h(void* dst, const uint8_t* dev, size_t n, hipStream_
     const size_t off = c * Staging::CHUNK, m = std::min(Staging::CHUNK, n - off);
     par_memcpy((uint8_t*)dst + off, g_staging.buf[sl], m);
   }
-  return hipSuccess;
+  return g_staging.before(stream);
 }
 
 // ---------------------------------------------------------------- device images

@@ -950,15 +950,32 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
     hroot = h.root;
     st = pss_cols_table(v, pd, h, &T);
   }
+  // round 6: in kind-major batches the pods of a wave share their pod position, so their column table T is one
+  // pointer: taken as a wave-uniform value, the table words and column offsets the checks look up are scalar loads
+  // (scalar cache) instead of per-lane vector loads in front of every column read (C2: wait 0.92)
+  const unsigned long long tmask = __ballot(T != nullptr);
+  const uint32_t* Tu = nullptr;
+  bool tuni = false;
+  if (tmask) {
+    const uint64_t tb = (uint64_t)(uintptr_t)T;
+    const uint64_t first = __shfl(tb, __ffsll((long long)tmask) - 1);
+    tuni = __ballot(T != nullptr && tb != first) == 0;
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)first);
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(first >> 32));
+    Tu = (const uint32_t*)(uintptr_t)(((uint64_t)hi32 << 32) | lo32);
+  }
   uint32_t tot[PSS_NLISTS];
 #pragma unroll
   for (uint32_t l = 0; l < PSS_NLISTS; l++) {
     uint32_t cnt = 0, eb = 0;
     if (T) {
-      const uint32_t* L = T + PC_LISTS + l * PCL_COUNT;
-      if (L[PCL_LEN] != NONE) {
+      uint32_t lc;
+      if (tuni) lc = Tu[PC_LISTS + l * PCL_COUNT + PCL_LEN];
+      else lc = T[PC_LISTS + l * PCL_COUNT + PCL_LEN];
+      if (lc != NONE) {
         KYV_ACCT_ADD(0, 8);
-        const uint64_t ln = v.colv[(size_t)v.col_off[L[PCL_LEN]] + r];  // (count, row of element 0)
+        const uint32_t co = tuni ? sld32(v.col_off + __builtin_amdgcn_readfirstlane(lc)) : v.col_off[lc];
+        const uint64_t ln = v.colv[(size_t)co + r];  // (count, row of element 0)
         if ((uint32_t)ln != NONE) { cnt = (uint32_t)ln; eb = (uint32_t)(ln >> 32); }
       }
     }
@@ -996,7 +1013,8 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
   __syncthreads();
   if (T) {
     const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
-    pf = pss_checks_cols(v, NodeTab{v.nodes + hroot}, r, T, s_fact[lane], true) & mask;
+    if (tuni) pf = pss_checks_cols(v, NodeTab{v.nodes + hroot}, r, Tu, s_fact[lane], true) & mask;
+    else pf = pss_checks_cols(v, NodeTab{v.nodes + hroot}, r, T, s_fact[lane], true) & mask;
     st = pf ? ST_FAIL : ST_PASS;
   }
   if (gated && st != ST_NONE) {
