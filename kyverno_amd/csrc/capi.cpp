@@ -225,7 +225,9 @@ int kyv_batch_stats_get(const kyv_batch* b, kyv_batch_stats* out) {
   out->strings = x.dict.strs.size();
   out->heap_bytes = x.heap.size();
   out->device_bytes = x.nodes.size() * sizeof(Node) + x.hdr.size() * sizeof(ResHeader) + x.heap.size() +
-                      x.dict.strs.size() * (4 + 4 + 4 + 8 + 16 + 8) + x.faux.size() * sizeof(FloatAux);
+                      x.dict.strs.size() * (4 + 4 + 4 + 8 + 16 + 8) + x.faux.size() * sizeof(FloatAux) +
+                      x.colv.size() * sizeof(uint64_t) + x.col_off.size() * 4 + x.gate.size() * 4 +
+                      (x.str_upper.size() + x.str_rx.size()) * 4;
   return KYV_OK;
 }
 

@@ -46,8 +46,8 @@ def main(tag):
             continue
         for r in csv.DictReader(open(f)):
             kname = r["Kernel_Name"][5:] if r["Kernel_Name"].startswith("void ") else r["Kernel_Name"]
-            if kname.startswith("kyv::calib_") and r["Counter_Name"] == "FETCH_SIZE":
-                calib.setdefault(kname.split("(")[0], []).append(float(r["Counter_Value"]) * 1024)
+            if kname.startswith("kyv::calib_"):
+                calib.setdefault(kname.split("(")[0], {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
             if not is_eval(r["Kernel_Name"]):
                 continue
             kn = r["Kernel_Name"].split("(")[0]
@@ -87,6 +87,9 @@ def main(tag):
         e["traffic_GBs"] = e["traffic_bytes"] / max(t, 1.0)
         if acc.get("SQ_WAVE_CYCLES"):
             e["wait_frac"] = acc.get("SQ_WAIT_ANY", 0.0) / acc["SQ_WAVE_CYCLES"]
+        rq = {c: x for c, x in acc.items() if c.startswith("TCC_EA0_RDREQ")}
+        if rq:
+            e["read_requests"] = rq
         if "TCC_HIT_sum" in acc:
             e["l2_hit_rate"] = acc["TCC_HIT_sum"] / max(1.0, acc["TCC_HIT_sum"] + acc.get("TCC_MISS_sum", 0.0))
         ph[name] = e
@@ -112,8 +115,14 @@ def main(tag):
                         "WRITE_SIZE, KiB x 1024); traffic_bytes_x2read applies the guide's x2 wide-stream read correction",
     }
     if calib:  # known bytes / counted bytes per access width (bench.py KYV_CALIB=1: 1 GiB per launch)
-        out["fetch_calibration"] = {k: {"bytes": float(1 << 30), "fetch_size_bytes": sum(v) / len(v),
-                                        "factor": float(1 << 30) / max(1.0, sum(v) / len(v))} for k, v in calib.items()}
+        out["fetch_calibration"] = {}
+        for k, cs in calib.items():
+            c = {n: sum(v) / len(v) for n, v in cs.items()}
+            e = {"bytes": float(1 << 30), "counters": c}
+            if "FETCH_SIZE" in c:
+                e["fetch_size_bytes"] = c["FETCH_SIZE"] * 1024
+                e["factor"] = float(1 << 30) / max(1.0, c["FETCH_SIZE"] * 1024)
+            out["fetch_calibration"][k] = e
         out["fetch_calibration_note"] = ("factor = true bytes / FETCH_SIZE bytes of a launch that reads a known 1 GiB: "
                                          "calib_read_kernel<W> coalesced W bytes per lane, calib_gather_kernel 16-byte "
                                          "rows in scrambled order")
