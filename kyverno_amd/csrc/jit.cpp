@@ -1501,6 +1501,28 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     if (!heavy.empty()) { groups.push_back(heavy); gwpe.push_back(-1); }
   }
   const size_t ngroups = groups.size();
+  // Compiled condition rules folded into the fused walk (round 6): a fused wave runs them for its 64 resources after the
+  // pattern rules of its part, so the kind-gate words and headers it already holds serve them too and the container
+  // rows the pattern rules just read are cache hits; no separate condition kernel re-streams its kind's waves
+  // (kyv_jit_condg_<k> at C3: 3.06 ms, wait 0.80, and no overlap with the walk on the second stream: every wave slot is
+  // taken by the fused kernels). KYV_FOLD_COND=0 (default): the condition kernels; 1: round-robin over the light
+  // group's parts; 2: all in its last part. jit_cond[k] = 2 + group for a folded rule.
+  // Measured (r6 A/B, C3 10M): folded walk 11.16 ms against walk 6.99 + conditions 3.07 ms separate (evaluation 12.32
+  // vs 11.24 ms): the condition code in the 64-VGPR fused parts costs more than the shared loads save, and the parts'
+  // hipRTC compile grows from ~3 to ~27 min. Kept as an experiment, off.
+  static const int fold_mode = getenv("KYV_FOLD_COND") ? atoi(getenv("KYV_FOLD_COND")) : 0;
+  size_t fold_group = SIZE_MAX;
+  std::vector<uint32_t> folded;
+  if (fold_mode && !crules.empty() && rs.rules.size() <= 32u * kFusedGW) {
+    for (int pass = 0; pass < 2 && fold_group == SIZE_MAX; pass++)  // the light group first, else any with fused rules
+      for (size_t gi = 0; gi < ngroups && fold_group == SIZE_MAX; gi++) {
+        if (pass == 0 && gwpe[gi] != -2) continue;
+        for (size_t i : groups[gi])
+          if (jit_rule_fused(rs, rule_roots[i].first)) { fold_group = gi; break; }
+      }
+    if (fold_group != SIZE_MAX) folded = crules;
+  }
+  const std::string jc_lds = std::to_string(cg.lds_used ? cg.nslots : 0u) + "u * kyv::JCAP * 64u + 64u";
   std::vector<std::pair<size_t, size_t>> fused_kernels;  // (group, part): kyv_jit_fused_<g>[p<part>]
   std::vector<size_t> merged_groups;                      // groups with a kyv_jit_fusedm_<g> (KYV_FUSED_MERGE)
   for (size_t gi = 0; gi < ngroups; gi++) {
@@ -1526,6 +1548,82 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
              "  jfinish(w, r, out);\n"
              "}\n";
+    // Root-column cache of the fused parts (round 6). The rules of a part preload their root-scope path columns one
+    // rule after another, and most of those entries are the same few columns (C3 pod rules: spec and the three
+    // container lists' entry and length columns; 141 root-column loads per pod over the light group's three parts,
+    // 45 distinct): each reload is a 512-B wave read that, with ~1,000 waves per XCD streaming through its 4 MB L2,
+    // has usually left the cache again (measured: root-column preloads are 13.5 of the walk's 25.6 GB per C3
+    // evaluation, accounting build with KYV_ACCT_SEL). A fused wave now loads each column that two or more of the
+    // group's rules read once per part into an LDS slot (8 B per lane, the lane's own entry: no sharing between
+    // lanes, so no barrier), and the rules' root functions (rootc<r>_<g>) read it from there. Columns whose rules'
+    // kind gates are disjoint share a slot (a lane's kind admits at most one of them: the pod rules' container
+    // columns and the workload rules' template columns). KYV_COLCACHE = slots per wave (default 8: 4 KB of LDS per
+    // wave, 128 KB per CU at 8 waves/SIMD); 0: off.
+    static const uint32_t cc_max = getenv("KYV_COLCACHE") ? (uint32_t)std::max(0, atoi(getenv("KYV_COLCACHE"))) : 8u;
+    std::map<uint32_t, uint32_t> cslot;                 // cached root column -> its LDS slot
+    std::map<size_t, std::vector<uint32_t>> rule_cols;  // rule_roots index -> its roots' preload columns
+    uint32_t ncslots = 0;
+    if (cc_max && !fused.empty()) {
+      std::map<uint32_t, size_t> cnt;
+      std::map<uint32_t, std::set<uint32_t>> ckinds;  // column -> kinds of the rules reading it
+      std::set<uint32_t> call;                        // columns a kind-unrestricted rule reads (share no slot)
+      for (size_t i : fused) {
+        std::set<uint32_t> cols;
+        for (uint32_t r : rule_roots[i].second) {
+          g.scope(rep_of[r]);
+          for (uint32_t c : g.scope_of[rep_of[r]]) cols.insert(c);
+        }
+        rule_cols[i].assign(cols.begin(), cols.end());
+        const KindGate kg = rule_gate(rs, rs.rules[rule_roots[i].first]);
+        for (uint32_t c : cols) {
+          cnt[c]++;
+          if (kg.any || kg.kinds.empty()) call.insert(c);
+          else ckinds[c].insert(kg.kinds.begin(), kg.kinds.end());
+        }
+      }
+      std::vector<uint32_t> cand;
+      for (const auto& e : cnt) if (e.second >= 2) cand.push_back(e.first);
+      std::stable_sort(cand.begin(), cand.end(), [&](uint32_t a, uint32_t b) { return cnt[a] > cnt[b]; });
+      std::vector<std::vector<uint32_t>> slots;
+      for (uint32_t c : cand) {
+        for (uint32_t s = 0; s < cc_max; s++) {
+          if (s == slots.size()) slots.emplace_back();
+          bool ok = true;
+          for (uint32_t c2 : slots[s]) {
+            if (call.count(c) || call.count(c2)) ok = false;
+            else for (uint32_t kk : ckinds[c]) if (ckinds[c2].count(kk)) { ok = false; break; }
+            if (!ok) break;
+          }
+          if (ok) { slots[s].push_back(c); cslot[c] = s; break; }
+        }
+      }
+      ncslots = (uint32_t)slots.size();
+      if (cslot.empty()) ncslots = 0;
+    }
+    if (ncslots) {
+      std::set<uint32_t> reps;
+      for (size_t i : fused) for (uint32_t r : rule_roots[i].second) reps.insert(rep_of[r]);
+      for (uint32_t r : reps) {
+        const auto& L = g.scope_of[r];
+        src << "static __device__ __forceinline__ void rootc" << r << "_" << gi
+            << "(const View& v, const Node* R, const ResHeader* hp, uint32_t row, uint32_t mbase, bool rootmap, bool walk,\n"
+               "    PatOut& out, const uint64_t* jcc) {\n"
+               "  const uint32_t lane = threadIdx.x & 63u;\n"
+               "  (void)lane;\n"
+               "  uint64_t pc[" << std::max<size_t>(1, L.size()) << "];";
+        for (size_t i = 0; i < L.size(); i++) {
+          auto it = cslot.find(L[i]);
+          if (it != cslot.end()) src << " pc[" << i << "] = jcc[" << it->second * 64u << "u + lane];";
+          else src << " pc[" << i << "] = jc_col(v, " << Gen::u(L[i]) << ", row);";
+        }
+        src << "\n"
+               "  if (!walk) return;\n"
+               "  JW w{v, R, hp, 0ull, 0ull, Keys{NONE, NONE}, 0ull, mbase, (uint8_t)ST_NONE};\n"
+               "  Ret r = p" << r << "(w, 0u, rootmap ? (uint32_t)N_MAP : T_UNK, 0u, row, pc);\n"
+               "  jfinish(w, r, out);\n"
+               "}\n";
+      }
+    }
     if (roots.size() > 256) {
       std::map<uint32_t, std::vector<uint32_t>> br2;
       for (uint32_t r : roots) br2[rep_of[r]].push_back(r);
@@ -1579,6 +1677,10 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     for (size_t pi = 0; pi < nparts; pi++) {
       const std::vector<size_t> part(fused.begin() + fused.size() * pi / nparts, fused.begin() + fused.size() * (pi + 1) / nparts);
       const std::string sname = "JitFused" + std::to_string(gi) + (pi ? "p" + std::to_string(pi) : std::string());
+      std::vector<uint32_t> conds;  // the folded condition rules this part runs after its pattern rules
+      if (gi == fold_group)
+        for (size_t j = 0; j < folded.size(); j++)
+          if (fold_mode == 2 ? pi + 1 == nparts : j % nparts == pi) conds.push_back(folded[j]);
       src << "struct " << sname << " {\n"
              "  __device__ __forceinline__ void run(const View& v, const DevOut& o, uint32_t nwaves, uint32_t w, uint32_t r,\n"
              "                                     bool active, uint32_t hflags, uint32_t hroot, const uint32_t* gw) {\n"
@@ -1588,6 +1690,32 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "    const uint32_t row = r < v.nres ? r : NONE;\n"
              "    const bool rootmap = (hflags & RF_ROOT_MAP) != 0;\n"
              "    (void)lane; (void)hp; (void)rootmap;\n";
+      if (!conds.empty()) src << "    __shared__ uint32_t jl[" << jc_lds << "];\n";
+      if (ncslots) {
+        // the part's cached root columns, each loaded by the lanes some rule of this part (in this rule slice) walks
+        std::map<uint32_t, std::vector<uint32_t>> users;  // column -> rules of this part reading it
+        for (size_t i : part)
+          for (uint32_t c : rule_cols[i]) if (cslot.count(c)) users[c].push_back(rule_roots[i].first);
+        // (a lane needs a column when a rule reading it is in the rule slice and its kind gate admits the lane: one
+        // mask test per gate word over the slice's rule bits, not the rules' own gate expressions, which the compiler
+        // would otherwise evaluate once here for every rule and keep live through the part)
+        src << "    __shared__ uint64_t jcc[" << ncslots * 64u << "u];\n"
+               "    uint32_t jsl[KYV_FUSED_GW];\n"
+               "#pragma unroll\n"
+               "    for (uint32_t i = 0; i < KYV_FUSED_GW; i++) {\n"
+               "      const uint32_t b0 = 32u * i, lo = o.rule_lo > b0 ? o.rule_lo - b0 : 0u, hi = o.rule_hi > b0 ? o.rule_hi - b0 : 0u;\n"
+               "      const uint32_t mlo = lo >= 32u ? 0u : (0xFFFFFFFFu << lo), mhi = hi >= 32u ? 0xFFFFFFFFu : ((1u << hi) - 1u);\n"
+               "      jsl[i] = active ? (gw[i] & mlo & mhi) : 0u;\n"
+               "    }\n";
+        for (const auto& cu : users) {
+          std::map<uint32_t, uint32_t> wm;  // gate word -> bits of the column's rules
+          for (uint32_t k : cu.second) wm[k / 32] |= 1u << (k % 32);
+          src << "    if (";
+          size_t j = 0;
+          for (const auto& e : wm) src << (j++ ? " | " : "") << "(jsl[" << e.first << "] & " << e.second << "u)";
+          src << ") jcc[" << cslot[cu.first] * 64u << "u + lane] = jc_col(v, " << Gen::u(cu.first) << ", row);\n";
+        }
+      }
       for (size_t j = 0; j < part.size(); j++) {
       const size_t i = part[j];
       const uint32_t k = rule_roots[i].first;
@@ -1607,8 +1735,12 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "          switch (a) {\n";
       for (uint32_t a = 0; a < nalts; a++) {
         const uint32_t root = rule_roots[i].second[a];
-        src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
-            << ", rootmap, wk, po); break;\n";
+        if (ncslots)
+          src << "            case " << a << "u: rootc" << rep_of[root] << "_" << gi << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+              << ", rootmap, wk, po, jcc); break;\n";
+        else
+          src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+              << ", rootmap, wk, po); break;\n";
       }
       src << "            default: break;\n"
              "          }\n"
@@ -1621,6 +1753,18 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "      }\n"
              "    }\n";
     }
+      // folded condition rules: the kyv_jit_condg_<k> member body for this wave's lanes (same gate, same verdict store)
+      for (uint32_t k : conds) {
+        const std::string K = Gen::u(k);
+        src << "    if (" << K << " >= o.rule_lo && " << K << " < o.rule_hi) {\n"
+               "      const bool gated = active && ((gw[" << k / 32 << "] >> " << k % 32 << "u) & 1u);\n"
+               "      if (__ballot(gated)) {\n"
+               "        uint8_t st = ST_NONE;\n"
+               "        if (gated) st = jr" << k << "(v, r, jl + lane);\n"
+               "        if (gated && st != ST_NONE) { o.status[(size_t)" << K << " * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }\n"
+               "      }\n"
+               "    }\n";
+      }
       src << "  }\n"
              "};\n";
       fused_kernels.push_back(std::make_pair(gi, pi));
@@ -1719,7 +1863,9 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // 5 waves/SIMD: measured 1.30 -> 1.05 ms on C3 with the round-2 kernel (4: 1.11, 6: 1.08)
     src << "#ifndef KYV_JC_WPE\n#define KYV_JC_WPE 5\n#endif\n";
     const bool grouped = !getenv("KYV_JC_GROUP") || atoi(getenv("KYV_JC_GROUP")) != 0;
-    const std::string lds = std::to_string(cg.lds_used ? cg.nslots : 0u) + "u * kyv::JCAP * 64u + 64u";
+    const std::string& lds = jc_lds;
+    std::vector<uint32_t> kept;  // the rules the fused walk does not run
+    for (uint32_t k : crules) if (std::find(folded.begin(), folded.end(), k) == folded.end()) kept.push_back(k);
     auto member = [&](uint32_t k, const std::string& on) {
       src << "  {\n"
              "    const bool gated = " << on << "((gw[" << k / 32 << "u] >> " << k % 32 << "u) & 1u);\n"
@@ -1731,7 +1877,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "  }\n";
     };
     if (grouped) {
-      for (const auto& grp : jit_cond_groups(rs, crules)) {
+      for (const auto& grp : jit_cond_groups(rs, kept)) {
         src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JC_WPE)))\n"
                "kyv_jit_condg_" << grp[0] << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t w0, uint32_t mask) {\n"
                "  __shared__ uint32_t jl[" << lds << "];\n"
@@ -1743,7 +1889,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
         src << "}\n";
       }
     } else {
-      for (uint32_t k : crules) {
+      for (uint32_t k : kept) {
         src << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KYV_JC_WPE)))\n"
                "kyv_jit_cond_" << k << "(const kyv::View* __restrict__ vp, kyv::DevOut o, uint32_t w0) {\n"
                "  __shared__ uint32_t jl[" << lds << "];\n"
@@ -1756,6 +1902,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
       }
     }
     for (uint32_t k : crules) if (jit_cond) (*jit_cond)[k] = 1;
+    for (uint32_t k : folded) if (jit_cond) (*jit_cond)[k] = (uint8_t)(2 + fold_group);
   }
   src << "#ifndef KYV_JIT_WPE_LIGHT\n#define KYV_JIT_WPE_LIGHT 8\n#endif\n";
   for (size_t gi = 0; gi < ngroups; gi++)

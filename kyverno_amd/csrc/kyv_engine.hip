@@ -958,7 +958,7 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
   dr->jcg_members.clear();
   {
     std::vector<uint32_t> crules;
-    for (size_t k = 0; k < rs.jit_cond.size(); k++) if (rs.jit_cond[k]) crules.push_back((uint32_t)k);
+    for (size_t k = 0; k < rs.jit_cond.size(); k++) if (rs.jit_cond[k] == 1) crules.push_back((uint32_t)k);
     for (auto& grp : jit_cond_groups(rs, crules)) {
       hipFunction_t f = nullptr;
       if (hipModuleGetFunction(&f, dr->jmod, ("kyv_jit_condg_" + std::to_string(grp[0])).c_str()) != hipSuccess) continue;
@@ -969,7 +969,7 @@ static bool ensure_jit(Ruleset& rs, DevRuleset* dr) {
     (void)hipGetLastError();
   }
   for (size_t k = 0; k < rs.jit_cond.size(); k++)
-    if (rs.jit_cond[k] && dr->jc_group[k] < 0)
+    if (rs.jit_cond[k] == 1 && dr->jc_group[k] < 0)
       HIP_OK(hipModuleGetFunction(&dr->jconds[k], dr->jmod, ("kyv_jit_cond_" + std::to_string(k)).c_str()));
   dr->jloaded = true;
   return true;
@@ -1392,6 +1392,8 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
   if (jit)
     for (uint32_t k = sl.k0; k < sl.k1; k++)
       if (rs.jit_rules[k] && jit_rule_fused(rs, k) && dr->ffns[rs.jit_rules[k] - 1]) sl.fg[rs.jit_rules[k] - 1] = 1;
+      else if (k < rs.jit_cond.size() && rs.jit_cond[k] >= 2 && dr->ffns[rs.jit_cond[k] - 2])
+        sl.fg[rs.jit_cond[k] - 2] = 1;  // a condition rule folded into that group's fused walk (jit.cpp)
   std::vector<std::vector<uint2>> slots(ncls);
   for (size_t ri = 0; ri < runs.size(); ri++) {
     const uint32_t wb = runs[ri].first, we = ri + 1 < runs.size() ? runs[ri + 1].first : nw;
@@ -1519,6 +1521,10 @@ static void layout_schedule(const Ruleset& rs, const Batch& b, const DevRuleset*
     std::vector<uint32_t> gmask(dr->jcg.size(), 0), glo(dr->jcg.size(), nw), ghi(dr->jcg.size(), 0);
     for (uint32_t q : sl.mj) {
       const int32_t grp = jit && q < dr->jc_group.size() ? dr->jc_group[q] : -1;
+      if (jit && q < rs.jit_cond.size() && rs.jit_cond[q] >= 2 && dr->ffns[rs.jit_cond[q] - 2]) {
+        if (only.empty() || std::find(only.begin(), only.end(), q) != only.end()) cj.push_back(q);
+        continue;  // folded into the fused walk of its group (sl.fg)
+      }
       if (jit && (grp >= 0 || (q < dr->jconds.size() && dr->jconds[q]))) {
         if (!only.empty() && std::find(only.begin(), only.end(), q) == only.end()) continue;
         cj.push_back(q);

@@ -60,9 +60,19 @@ __device__ unsigned long long kyv_acct_bytes[3 * KYV_ACCT_SLOTS];
 #else
 #define KYV_ACCT_ADD(cls, b) ((void)0)
 #endif
+// accounting experiments (KYV_JIT_DEFS=-DKYV_ACCT_SEL=<bits>, runtime-compiled kernels): count only the selected kinds of
+// resource-data loads -- 1 node rows, 2 path-column entries by column id (jc_col, wcol), 4 pattern-entry columns (jraw),
+// 8 element self columns (jself) -- besides every other counted access; default: all
+#ifndef KYV_ACCT_SEL
+#define KYV_ACCT_SEL 15u
+#endif
+#define KYV_ACCT_ADDK(kind, cls, b) \
+  do {                              \
+    if ((KYV_ACCT_SEL) & (kind)) KYV_ACCT_ADD(cls, b); \
+  } while (0)
 
 #if defined(__HIP_DEVICE_COMPILE__)
-KYV_HD void touch_row(uint32_t) { KYV_ACCT_ADD(0, 16); }
+KYV_HD void touch_row(uint32_t) { KYV_ACCT_ADDK(1u, 0, 16); }
 #else
 KYV_HD void touch_row(uint32_t i) {
   TouchAcct* t = g_touch;

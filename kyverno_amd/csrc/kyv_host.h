@@ -145,7 +145,7 @@ struct Ruleset {
   // runtime-compiled walk kernel (jit.cpp): generated once per ruleset, compiled on first use
   bool jit_tried = false;
   std::vector<uint8_t> jit_rules;   // rule k is walked by the compiled kernel
-  std::vector<uint8_t> jit_cond;    // rule k (deny / foreach with JMESPath operands) runs in the compiled kyv_jit_cond
+  std::vector<uint8_t> jit_cond;    // rule k (deny / foreach with JMESPath operands) runs in the compiled kyv_jit_cond (1), or folded into fused group g's walk (2 + g)
   std::vector<uint16_t> jit_shape;  // 1 + the pattern shape of rule k in kyv_jit_shapes (0: none; jit.cpp)
   uint32_t jit_nshapes = 0;
   std::vector<char> jit_code;       // gfx950 code object

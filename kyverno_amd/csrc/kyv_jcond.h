@@ -24,7 +24,7 @@ constexpr uint32_t JCAP = 16;  // lane list capacity of an operand (longer -> th
 
 __device__ __forceinline__ uint64_t jc_col(const View& v, uint32_t col, uint32_t row) {
   if (row == NONE) return COL_NONE;
-  KYV_ACCT_ADD(0, 8);
+  KYV_ACCT_ADDK(2u, 0, 8);
   const uint32_t off = sld32(v.col_off + col);
   return *(const KYV_AS_GLOBAL uint64_t*)(v.colv + (size_t)off + row);
 }

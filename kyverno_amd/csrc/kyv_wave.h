@@ -42,7 +42,7 @@ __device__ __forceinline__ T sld(const T* p) {
 __device__ __forceinline__ uint32_t sld32(const uint32_t* p) { return *(const KYV_AS_CONST uint32_t*)p; }
 typedef uint32_t kyv_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ Node gnode(const Node* p) {
-  KYV_ACCT_ADD(0, 16);
+  KYV_ACCT_ADDK(1u, 0, 16);
   const KYV_AS_GLOBAL kyv_u32x4* q = (const KYV_AS_GLOBAL kyv_u32x4*)p;
   kyv_u32x4 x = *q;
   Node n;
@@ -50,7 +50,7 @@ __device__ __forceinline__ Node gnode(const Node* p) {
   return n;
 }
 __device__ __forceinline__ uint32_t gtk(const Node* p) {
-  KYV_ACCT_ADD(0, 4);
+  KYV_ACCT_ADDK(1u, 0, 4);
   return *(const KYV_AS_GLOBAL uint32_t*)p;
 }
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -77,7 +77,7 @@ __device__ __forceinline__ uint32_t gld32(const uint32_t* p) { return *(const KY
 
 // Column entry of one map-entry lookup (the device entry table holds absolute column offsets in `col`)
 __device__ __forceinline__ uint32_t wcol(const View& v, const PEntry& E, bool al, uint32_t row) {
-  if (al) KYV_ACCT_ADD(0, 4);
+  if (al) KYV_ACCT_ADDK(2u, 0, 4);
   return al ? gld32((const uint32_t*)(v.colv + (size_t)E.col + row)) : NONE;
 }
 __device__ __forceinline__ uint32_t col_decode(uint32_t enc, uint32_t* ctype) {
@@ -643,13 +643,13 @@ constexpr uint64_t COL_NONE = 0xFFFFFFFFull;
 // device entry table holds the column's absolute offset in `col`
 __device__ __forceinline__ uint64_t jraw(const JW& w, uint32_t e, uint32_t row) {
   const uint32_t off = sld32(&w.v.pe[e].col);
-  if (row != NONE) KYV_ACCT_ADD(0, 8);
+  if (row != NONE) KYV_ACCT_ADDK(4u, 0, 8);
   return row == NONE ? COL_NONE : *(const KYV_AS_GLOBAL uint64_t*)(w.v.colv + (size_t)off + row);
 }
 // self column (array elements) by column id
 __device__ __forceinline__ uint64_t jself(const JW& w, uint32_t col, uint32_t row) {
   const uint32_t off = sld32(w.v.col_off + col);
-  if (row != NONE) KYV_ACCT_ADD(0, 8);
+  if (row != NONE) KYV_ACCT_ADDK(8u, 0, 8);
   return row == NONE ? COL_NONE : *(const KYV_AS_GLOBAL uint64_t*)(w.v.colv + (size_t)off + row);
 }
 // entry -> node index (NONE absent), type (T_UNK absent) and the node's `a`
