@@ -590,7 +590,7 @@ struct CondGen {
         << "  if (" << (x.key ? "false" : "jc_arr(v, R, " + x.i + ", " + x.t + ", " + x.a + ", " + x.row + ", " +
                                               (tlen(x.tpos) == NONE ? std::string("NONE") : u(tlen(x.tpos))) + ", &" + cnt +
                                               ", &" + aa + ", &" + eb + ")")
-        << ") {\n" << on_arr << (unroll ? "  #pragma unroll 4\n" : "")
+        << ") {\n" << on_arr << (unroll ? "  KYV_JC_UNROLL\n" : "")
         << "  for (uint32_t " << j << " = 0; " << j << " < " << cnt << "; " << j << "++) {\n";
     V e{fresh("vi"), fresh("vt"), fresh("va"), fresh("vr"), st, false};
     out << "  uint32_t " << e.i << ", " << e.t << ", " << e.a << ", " << e.row << ";\n"
@@ -711,7 +711,7 @@ struct CondGen {
         out << "  if (" << (x.key ? std::string("true") : x.i + " == NONE || jc_type(R, " + x.i + ", " + x.t + ") != N_MAP")
             << ") return JS_FB;\n"
             << "  { const Node " << m << " = gnode(R + " << x.i << ");\n"
-            << "  #pragma unroll 4\n"
+            << "  KYV_JC_UNROLL\n"
             << "  for (uint32_t " << j << " = 0; " << j << " < " << m << ".b; " << j << "++) {\n";
         V k = decl(m + ".a + " + j, "T_UNK", "0u", "NONE", NONE, true);
         jgen(pos + 1, k, true, true, guard + 1);
@@ -1434,8 +1434,24 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     rule_roots.push_back({(uint32_t)k, rr});
   }
   std::ostringstream src;
-  src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n#define KYV_FUSED_GW " << kFusedGW
+  // KYV_JC_UNROLL: the condition programs' element loops, not unrolled. Unrolled 4x (rounds 2-5, so that consecutive
+  // elements' loads overlap) the C3 condition kernels held ~136k instructions each (every unrolled body inlines the
+  // operand conversions and glob calls) with 7k SGPR / 74 VGPR spills at 8 waves/SIMD; round 6 A/B, C3 10M condition
+  // phase: unroll 4 2.82 ms, 2 2.76, 1 2.53 (2.6k SGPR / 10 VGPR spills, half the code).
+  // KYV_JIT_DEFS='-DKYV_JC_UNROLL=_Pragma("unroll 4")' for experiments
+  src << "// generated by kyverno_amd/csrc/jit.cpp for one ruleset\n"
+         "#ifndef KYV_JC_UNROLL\n#define KYV_JC_UNROLL _Pragma(\"unroll 1\")\n#endif\n"
+         "#define KYV_FUSED_GW " << kFusedGW
       << "\n#include \"kyv_jcond.h\"\n#include \"kyv_fused.h\"\nnamespace kyv {\n";
+  // KYV_RULE_VIEW: the View reference each rule of a multi-rule kernel (fused part, condition group) walks with. The
+  // View's tables (column offsets, entry columns) are read-only uniform loads the compiler hoists to the kernel entry
+  // and keeps live in SGPRs for the whole kernel (C3: 1.4-7k SGPR spills per kernel into VGPR lanes). Experiment
+  // (round 6): KYV_JIT_DEFS='-DKYV_RULE_VIEW(x)=(*::kyv::kyv_launder(&(x)))' passes it through an empty asm at each
+  // rule's start, so each rule reads the few it uses itself: 20-30 % fewer SGPR spills, but each rule then waits for a
+  // chain of three dependent scalar loads before its first column read and VGPR spills grow (condition kernel 10 ->
+  // 368): C3 walk 6.86 -> 10.67 ms, conditions 2.53 -> 3.95 ms. Default: the plain reference.
+  src << "__device__ __forceinline__ const View* kyv_launder(const View* p) { asm volatile(\"\" : \"+s\"(p)); return p; }\n"
+         "#ifndef KYV_RULE_VIEW\n#define KYV_RULE_VIEW(x) (x)\n#endif\n";
   src << body.str();
   if (!crules.empty()) {
     // the match part of pair_dispatch, out of line (one copy for every rule that needs more than the kind gate):
@@ -1725,7 +1741,8 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
       const std::string K = Gen::u(k);
       src << "    if (" << K << " >= o.rule_lo && " << K << " < o.rule_hi) {\n"
              "      const bool gated = active && ((gw[" << k / 32 << "] >> " << k % 32 << "u) & 1u);\n"
-             "      if (__ballot(gated)) {\n";
+             "      if (__ballot(gated)) {\n"
+             "        const View& vl = KYV_RULE_VIEW(v);\n";
       src << "        const bool magic = gated && (hflags & RF_MAGIC);\n"
              "        WaveSink sink{o.stage + sld32(o.rbase + (" << K << " - o.rule_lo)) + (size_t)w * 64u * " << alts
           << "u, 0u, " << (rd.uses_meta ? "true" : "false") << "};\n"
@@ -1736,10 +1753,10 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
       for (uint32_t a = 0; a < nalts; a++) {
         const uint32_t root = rule_roots[i].second[a];
         if (ncslots)
-          src << "            case " << a << "u: rootc" << rep_of[root] << "_" << gi << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+          src << "            case " << a << "u: rootc" << rep_of[root] << "_" << gi << "(vl, R, hp, row, " << Gen::u(rd.meta_sites)
               << ", rootmap, wk, po, jcc); break;\n";
         else
-          src << "            case " << a << "u: root" << rep_of[root] << "(v, R, hp, row, " << Gen::u(rd.meta_sites)
+          src << "            case " << a << "u: root" << rep_of[root] << "(vl, R, hp, row, " << Gen::u(rd.meta_sites)
               << ", rootmap, wk, po); break;\n";
       }
       src << "            default: break;\n"
@@ -1760,7 +1777,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
                "      const bool gated = active && ((gw[" << k / 32 << "] >> " << k % 32 << "u) & 1u);\n"
                "      if (__ballot(gated)) {\n"
                "        uint8_t st = ST_NONE;\n"
-               "        if (gated) st = jr" << k << "(v, r, jl + lane);\n"
+               "        if (gated) st = jr" << k << "(KYV_RULE_VIEW(v), r, jl + lane);\n"
                "        if (gated && st != ST_NONE) { o.status[(size_t)" << K << " * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }\n"
                "      }\n"
                "    }\n";
@@ -1860,8 +1877,9 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // `mask`: the members the launch runs, those of the current rule slice): a wave loads its resources' header once
     // for all of them and the later rules find the lists the first one read (C3: the three capability rules of a pod
     // kind read the same container lists) in the caches. KYV_JC_GROUP=0: one kernel per rule (kyv_jit_cond_<k>)
-    // 5 waves/SIMD: measured 1.30 -> 1.05 ms on C3 with the round-2 kernel (4: 1.11, 6: 1.08)
-    src << "#ifndef KYV_JC_WPE\n#define KYV_JC_WPE 5\n#endif\n";
+    // 5 waves/SIMD: measured 1.30 -> 1.05 ms on C3 with the round-2 kernel (4: 1.11, 6: 1.08); round 6 (12 rules in 3
+    // kernels, C3 10M, condition phase ms): 5 (77 VGPRs) 3.05, 6 3.07, 7 2.88, 8 (64 VGPRs, 74 spills) 2.82
+    src << "#ifndef KYV_JC_WPE\n#define KYV_JC_WPE 8\n#endif\n";
     const bool grouped = !getenv("KYV_JC_GROUP") || atoi(getenv("KYV_JC_GROUP")) != 0;
     const std::string& lds = jc_lds;
     std::vector<uint32_t> kept;  // the rules the fused walk does not run
@@ -1871,7 +1889,7 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
              "    const bool gated = " << on << "((gw[" << k / 32 << "u] >> " << k % 32 << "u) & 1u);\n"
              "    if (__ballot(gated)) {\n"
              "      uint8_t st = kyv::ST_NONE;\n"
-             "      if (gated) st = kyv::jr" << k << "(v, r, jl + lane);\n"
+             "      if (gated) st = kyv::jr" << k << "(KYV_RULE_VIEW(v), r, jl + lane);\n"
              "      if (gated && st != kyv::ST_NONE) { o.status[(size_t)" << k << "u * v.nres + r] = st; KYV_ACCT_ADD(1, 1); }\n"
              "    }\n"
              "  }\n";

@@ -1898,8 +1898,10 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
     if (jit && !ajit) throw std::runtime_error("accounting build of the runtime-compiled kernels unavailable");
     acct_take();
   }
-  // concurrent condition stream (KYV_COND_STREAM=0: the evaluation stream)
-  static const bool cond_conc = !getenv("KYV_COND_STREAM") || atoi(getenv("KYV_COND_STREAM")) != 0;
+  // concurrent condition stream (KYV_COND_STREAM=1; default: the evaluation stream). The fused walk kernels take every
+  // wave slot, so the condition kernels found nothing to overlap: C3 10M evaluation 10.88 (second stream) vs 10.82 ms
+  // (round 6; round 5: 11.24 vs 11.19)
+  static const bool cond_conc = getenv("KYV_COND_STREAM") && atoi(getenv("KYV_COND_STREAM")) != 0;
   bool conc = false;
   for (auto& sl : d.slices) conc = conc || !sl.cw.empty();
   conc = conc && cond_conc && !acct && !serial;
