@@ -1573,9 +1573,11 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // group's rules read once per part into an LDS slot (8 B per lane, the lane's own entry: no sharing between
     // lanes, so no barrier), and the rules' root functions (rootc<r>_<g>) read it from there. Columns whose rules'
     // kind gates are disjoint share a slot (a lane's kind admits at most one of them: the pod rules' container
-    // columns and the workload rules' template columns). KYV_COLCACHE = slots per wave (default 8: 4 KB of LDS per
-    // wave, 128 KB per CU at 8 waves/SIMD); 0: off.
-    static const uint32_t cc_max = getenv("KYV_COLCACHE") ? (uint32_t)std::max(0, atoi(getenv("KYV_COLCACHE"))) : 8u;
+    // columns and the workload rules' template columns). KYV_COLCACHE = slots per wave (default 4: 2 KB of LDS per
+    // wave); 0: off. C3 10M walk ms by slots (round 6 A/B): 0 6.94, 2 6.79, 3 6.71, 4 6.66, 5 6.69, 8 6.81, 12 (at 6
+    // waves/SIMD) 7.12 -- the slots beyond the most shared columns cost more in registers (the slot reads' addresses
+    // and the fill) than the reloads they save.
+    static const uint32_t cc_max = getenv("KYV_COLCACHE") ? (uint32_t)std::max(0, atoi(getenv("KYV_COLCACHE"))) : 4u;
     std::map<uint32_t, uint32_t> cslot;                 // cached root column -> its LDS slot
     std::map<size_t, std::vector<uint32_t>> rule_cols;  // rule_roots index -> its roots' preload columns
     uint32_t ncslots = 0;
