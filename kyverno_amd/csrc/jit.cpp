@@ -1553,7 +1553,8 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // KYV_FUSED_ORDER (experiment): the group's fused rules reordered before they are cut into parts -- 1: by (kind
     // gate, root-scope columns), 2: by (root-scope columns, kind gate) -- so that rules reading the same columns run in
     // one part, back to back. The order of a wave's rules is free: each writes only its own verdicts and staging chunk.
-    // Measured slower (round 6, C3 10M walk ms): policy order 6.56, order 1 8.79, order 2 7.97, order 1 in 4 parts 7.83
+    // Measured slower (round 6, C3 10M walk ms): policy order 6.56, order 1 8.79, order 2 7.97, order 1 in 4 parts 7.83,
+    // order 3 8.14 (policy order 6.70 in that run)
     // -- a part then holds one kind family's rules, so a wave finds all its work in one kernel and none in the others,
     // and the column cache's slots cover fewer of that kernel's columns.
     static const int forder = getenv("KYV_FUSED_ORDER") ? atoi(getenv("KYV_FUSED_ORDER")) : 0;
@@ -1572,6 +1573,13 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
         key[i] = forder == 2 ? std::make_pair(cv, kg.kinds) : std::make_pair(kg.kinds, cv);
       }
       std::stable_sort(fused.begin(), fused.end(), [&](size_t a, size_t b) { return key[a] < key[b]; });
+      if (forder == 3) {  // 3: the mode-1 order dealt round-robin over the parts (each part an equal share of every kind)
+        const size_t np = std::max<size_t>(1, std::min<size_t>(fused.size(), getenv("KYV_FUSED_SPLIT") ? (size_t)atoi(getenv("KYV_FUSED_SPLIT")) : 3));
+        std::vector<size_t> dealt;
+        for (size_t p = 0; p < np; p++)
+          for (size_t j = p; j < fused.size(); j += np) dealt.push_back(fused[j]);
+        fused.swap(dealt);
+      }
     }
     // the root scope's column preload is issued before the lane's walk predicate is known: it depends on the
     // resource row only, so its loads overlap the header loads the predicate waits for (one memory round, not two)
