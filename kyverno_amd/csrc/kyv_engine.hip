@@ -1123,6 +1123,7 @@ static void fold_kinds(MRec& R, uint32_t ck, size_t* nfold, size_t* ndrop) {
   MRecFilter out[MREC_F];
   uint32_t no = 0, omf = 0, oef = 0;
   bool drop_excl = false;
+  bool excl_tail = false;  // an exclude filter ahead of this one has a tail (selector / annotations: it can raise ND)
   for (uint32_t j = 0; j < nmf + nef; j++) {
     MRecFilter F = R.f[j];
     const bool ism = j < nmf;
@@ -1145,8 +1146,11 @@ static void fold_kinds(MRec& R, uint32_t ck, size_t* nfold, size_t* ndrop) {
     } else if (acc == 0) {
       if (ism && mm == MM_ANY) { (*ndrop)++; continue; }
       if (!ism && (em == MM_ANY || em == MM_PLAIN)) { (*ndrop)++; continue; }
-      if (!ism && em == MM_ALL) drop_excl = true;
+      // exclude ALL: the reference evaluates the filters ahead of this one while they all exclude, and their
+      // nondeterminism counts (match_fast / match_rule_rec), so the block goes only when none of them has a tail
+      if (!ism && em == MM_ALL && !excl_tail) drop_excl = true;
     }
+    if (!ism && ((F.bits >> 28) & 1u)) excl_tail = true;
     out[no++] = F;
     if (ism) omf++; else oef++;
   }

@@ -397,3 +397,29 @@ def test_pss_map_kernel_exclusions_at_scale_gpu():
             assert got == want, (r["name"], i, sorted(got), sorted(want))
             noracle += 1
     assert nmask > 100_000 and noracle >= 20_000
+
+
+def test_exclude_all_nondeterminism_in_kind_folded_records_gpu():
+    """An exclude.all block whose later filter can never accept the wave's kind: the match records folded per kind
+    class (kyv_engine.hip fold_kinds) keep the block when a filter ahead of it has a selector, so the nondeterminism
+    that filter raises (a wildcard selector key matching a valid and an invalid label: Go map order decides,
+    pkg/utils/wildcards/wildcards.go:13-50) is the reference's in single-kind waves too. The mirrored order (the
+    never-accepting filter first) still drops the block."""
+    def pol(name, excl):
+        return {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy",
+                "metadata": {"name": name, "annotations": {"pod-policies.kyverno.io/autogen-controllers": "none"}},
+                "spec": {"rules": [{"name": "r", "match": {"any": [{"resources": {"kinds": ["Pod", "Deployment"]}}]},
+                                    "exclude": {"all": excl},
+                                    "validate": {"message": "m", "pattern": {"metadata": {"name": "?*"}}}}]}}
+    sel = {"matchLabels": {"app-*": "x*"}}
+    pols = [pol("nd-excl-all", [{"resources": {"kinds": ["Pod"], "selector": sel}}, {"resources": {"kinds": ["Deployment"]}}]),
+            pol("nd-excl-all2", [{"resources": {"kinds": ["Deployment"]}}, {"resources": {"kinds": ["Pod"], "selector": sel}}])]
+    docs = []
+    for i in range(256):  # pods only: every wave is one kind class (folded records)
+        labels = [{"app-a": "x1", "app-b": "x!!"}, {"app-a": "x1"}, {"app-a": "y", "app-b": "x2"}, {}][i % 4]
+        docs.append({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p%d" % i, "namespace": "default", "labels": labels},
+                     "spec": {"containers": [{"name": "c", "image": "x"}]}})
+    import parity_util as PU
+    st, res = PU.compare(pols, docs, {}, backend="gpu")
+    assert st["nbad"] == 0, st["bad"]
+    assert st["nd"] == 64, st
