@@ -2412,11 +2412,22 @@ struct TrieBuilder {
     for (uint32_t s = 0; s < o.nseg && t != NONE; s++) t = ch(t, rs.pool[o.a + s]);
     o.list = (t == NONE || o.nseg == 0) ? 0u : rs.trie[t].col + 1;
   }
+  // a chain-form JMESPath operand (kyv_layout.h jmes_chain_form: fields, then `|| lit` and / or one function) whose
+  // fields jmes() registered: the column of the field chain (o.list = column + 1), which the light kernels' chain
+  // evaluator reads instead of searching the maps field by field (kyv_cond.h jmes_chain_cv)
+  void chain(CondOperand& o) {
+    if (o.kind != OK_JMES || o.sv || !jmes_chain_form(rs.pool.data() + o.a, o.nseg)) return;
+    const uint32_t* p = rs.pool.data() + o.a;
+    if (p[0] & JF_PURE) return;  // (pure programs are not registered: jmes())
+    uint32_t t = 0, nf = 0;
+    for (uint32_t q = 1; q + 1 < o.nseg && p[q] == JO_FIELD && t != NONE; q += 2, nf++) t = ch(t, p[q + 1]);
+    o.list = (t == NONE || nf == 0) ? 0u : rs.trie[t].col + 1;
+  }
   void prog(uint32_t pr, const std::vector<uint32_t>& elem) {
     if (pr == NONE || pr >= rs.cprogs.size()) return;
     const CondProg& P = rs.cprogs[pr];
     const uint32_t nany = P.nany == NONE ? 0u : P.nany;
-    auto one = [&](Cond& c) { jmes(c.key, elem); jmes(c.value, elem); path(c.key); path(c.value); };
+    auto one = [&](Cond& c) { jmes(c.key, elem); jmes(c.value, elem); path(c.key); path(c.value); chain(c.key); chain(c.value); };
     for (uint32_t i = 0; i < nany; i++) one(rs.conds[P.any0 + i]);
     for (uint32_t i = 0; i < P.nall; i++) one(rs.conds[P.all0 + i]);
   }

@@ -408,11 +408,23 @@ KYV_HD CV jres_cv(const View& v, NodeTab R, const JRes& r, const JList& L) {
 //  - regex_match(re, x): jpRegexMatch (functions.go:786-799) -- x must be a string or a number (else the type error); a
 //    string's result is its precomputed bit (Batch::str_rx, regex.cpp), a number (ifaceToString's float32 formatting)
 //    or a string outside printable ASCII goes to the CPU engine
-KYV_HD int jmes_chain_cv(const View& v, NodeTab R, const CondOperand& o, CV* out, uint32_t* miss) {
+// row: the resource's batch position; with the field chain's path column (o.list = column + 1, compiler.cpp
+// TrieBuilder::chain) an entry present there is the node the chain reaches -- one coalesced load instead of a map
+// search per field (round 6: C5's regex_match / to_upper rules walked metadata.labels.<key> by binary searches, 8x the
+// cost of a path-column rule per pair); an absent entry (missing or null on the way, a non-map parent) takes the walk
+KYV_HD int jmes_chain_cv(const View& v, NodeTab R, const CondOperand& o, CV* out, uint32_t* miss, uint32_t row = NONE) {
   const uint32_t* p = v.pool + o.a;
   const uint32_t n = o.nseg;
   const bool pure = (p[0] & JF_PURE) != 0;
   uint32_t cur = 0, fields = 0, i = 1;
+  if (o.list && row != NONE && v.colv) {
+    KYV_ACCT_ADD(0, 8);
+    const uint32_t e = (uint32_t)v.colv[(size_t)v.col_off[o.list - 1] + row];
+    if (e != NONE) {
+      cur = e & COL_INDEX_MASK;
+      for (; i + 1 < n && p[i] == JO_FIELD; i += 2) fields++;
+    }
+  }
   for (; i + 1 < n && p[i] == JO_FIELD; i += 2) {
     bool missing;
     cur = j_field(R, cur, p[i + 1], &missing);
@@ -471,7 +483,7 @@ KYV_HD int jmes_chain_cv(const View& v, NodeTab R, const CondOperand& o, CV* out
 KYV_HD int operand_cv(const View& v, NodeTab R, const CondOperand& o, uint32_t elem, JList& L, CV* out, uint32_t* miss,
                       uint32_t row = NONE) {
   if (o.kind != OK_JMES) return cv_operand(v, R, o, out, miss, row) ? JS_OK : JS_NOTFOUND;
-  if (jmes_chain_form(v.pool + o.a, o.nseg)) return jmes_chain_cv(v, R, o, out, miss);
+  if (jmes_chain_form(v.pool + o.a, o.nseg)) return jmes_chain_cv(v, R, o, out, miss, row);
   JRes r;
   const int st = jmes_run(v, R, o, elem, L, &r, miss);
   if (st != JS_OK) return st;
@@ -870,7 +882,7 @@ KYV_HD __attribute__((always_inline)) int eval_prog_inl(const View& v, NodeTab R
         if (o.kind == OK_JMES) {
           if constexpr (!kJ) {
             if (!jmes_chain_form(v.pool + o.a, o.nseg)) return CR_FB;
-            const int st = jmes_chain_cv(v, R, o, &tmp, &miss);
+            const int st = jmes_chain_cv(v, R, o, &tmp, &miss, row);
             if (st == JS_FB) return CR_FB;
             if (st == JS_NOTFOUND) { *err_cond = c0 + i; *err_side = side; *err_seg = miss; return CP_ERROR; }
             if (st == JS_ERR) { *err_cond = c0 + i; *err_side = side; *err_seg = NONE; return CP_ERROR; }
@@ -904,9 +916,9 @@ KYV_HD __attribute__((always_inline)) int eval_prog_inl(const View& v, NodeTab R
       operand_cv(v, R, c.value, elem, lx, &x, &miss, row);
       r = eval_cond(v, R, c, k, x);
     } else {
-      if (c.key.kind == OK_JMES) jmes_chain_cv(v, R, c.key, &k, &miss);  // (a chain program: checked in the first pass)
+      if (c.key.kind == OK_JMES) jmes_chain_cv(v, R, c.key, &k, &miss, row);  // (a chain program: checked in the first pass)
       else cv_operand(v, R, c.key, &k, &miss, row);
-      if (c.value.kind == OK_JMES) jmes_chain_cv(v, R, c.value, &x, &miss);
+      if (c.value.kind == OK_JMES) jmes_chain_cv(v, R, c.value, &x, &miss, row);
       else cv_operand(v, R, c.value, &x, &miss, row);
       r = eval_cond(v, R, c, k, x);
     }
