@@ -932,7 +932,7 @@ struct CondGen {
         if (jmes_chain_form(rs.pool.data() + o.a, o.nseg)) {  // the light kernels' evaluator (kyv_cond.h jmes_chain_cv)
           const std::string m = fresh("ms"), s = fresh("js");
           out << "  CV " << cv << "; uint32_t " << m << ";\n"
-              << "  const int " << s << " = jmes_chain_cv(v, NodeTab{R}, " << C << ", &" << cv << ", &" << m << ");\n";
+              << "  const int " << s << " = jmes_chain_cv(v, NodeTab{R}, " << C << ", &" << cv << ", &" << m << ", r);\n";
           if (check) out << "  if (" << s << " == JS_FB) return CR_FB;\n  if (" << s << " != JS_OK) return CP_ERROR;\n";
           else out << "  (void)" << s << ";\n";
           return;
