@@ -668,6 +668,31 @@ struct Stack {
 KYV_HD Ret mkerr(uint8_t code, uint8_t mask, uint32_t tmpl) { Ret r; r.err = true; r.code = code; r.mask = mask; r.tmpl = tmpl; return r; }
 KYV_HD Ret ok_ret() { Ret r; r.err = false; r.code = EC_NONE; r.mask = 0; r.tmpl = NONE; return r; }
 
+// The keys of a labels / annotations map L that glob pattern gp matches: the first one and how many. Four entries per
+// step, their key words first and then (a pattern with a glob-mask bit) their mask words, as independent loads: an
+// entry at a time was a chain of two dependent loads per annotation (round 6: C3's app-armor rules, one rule 0.63 ms
+// over 7 M pods)
+KYV_HD __attribute__((always_inline)) void meta_wild_scan(const View& v, NodeTab R, const Node& L, uint32_t gp,
+                                                         uint32_t* hit, uint32_t* n) {
+  const uint32_t f = v.str_flags[gp];
+  const uint32_t gi1 = (f & SF_GLOBBY) ? (f >> SF_GIDX_SHIFT) & 0xFFu : 0u;
+  const bool mask = gi1 && v.str_gmask;
+  for (uint32_t i = 0; i < L.b; i += 4) {
+    uint32_t k[4], m[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) k[j] = i + j < L.b ? node_key(R[L.a + i + j]) : NONE;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++)
+      m[j] = mask && k[j] != NONE ? v.str_gmask[(size_t)k[j] * v.gmask_words + (gi1 - 1) / 32] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      if (i + j >= L.b) break;
+      const bool g = mask ? (k[j] == gp || ((m[j] >> ((gi1 - 1) % 32)) & 1u)) : glob_sid(v, gp, k[j]);
+      if (g) { if (*hit == NONE) *hit = k[j]; (*n)++; }
+    }
+  }
+}
+
 // ExpandInMetadata at one map level (wildcards.go:62-83): resolves wildcard keys into slots; returns a
 // status override (ST_PANIC / ST_ND / ST_FALLBACK) or ST_NONE.
 KYV_BIG uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32_t rn, const ResHeader& h, Keys& keys) {
@@ -688,12 +713,8 @@ KYV_BIG uint8_t expand_meta(const View& v, const MetaSite& ms, NodeTab R, uint32
     uint32_t wild = tag == 0 ? ms.wild_l : ms.wild_a, nw = tag == 0 ? ms.nwild_l : ms.nwild_a;
     uint32_t slot0 = tag == 0 ? ms.slot_l : ms.slot_a;
     for (uint32_t w = 0; w < nw; w++) {
-      uint32_t gp = v.pool[wild + 2 * w];
       uint32_t hit = NONE, n = 0;
-      for (uint32_t i = 0; i < L.b; i++) {
-        uint32_t k = node_key(R[L.a + i]);
-        if (glob_sid(v, gp, k)) { if (hit == NONE) hit = k; n++; }
-      }
+      meta_wild_scan(v, R, L, v.pool[wild + 2 * w], &hit, &n);
       if (n > 1) return ST_ND;
       if (n == 1) keys.set(slot0 + w, hit);
     }
@@ -719,12 +740,8 @@ KYV_HD uint8_t expand_meta_root(const View& v, const MetaSite& ms, NodeTab R, co
     uint32_t wild = tag == 0 ? ms.wild_l : ms.wild_a, nw = tag == 0 ? ms.nwild_l : ms.nwild_a;
     uint32_t slot0 = tag == 0 ? ms.slot_l : ms.slot_a;
     for (uint32_t w = 0; w < nw; w++) {
-      uint32_t gp = v.pool[wild + 2 * w];
       uint32_t hit = NONE, n = 0;
-      for (uint32_t i = 0; i < L.b; i++) {
-        uint32_t k = node_key(R[L.a + i]);
-        if (glob_sid(v, gp, k)) { if (hit == NONE) hit = k; n++; }
-      }
+      meta_wild_scan(v, R, L, v.pool[wild + 2 * w], &hit, &n);
       if (n > 1) return ST_ND;
       if (n == 1) keys.set(slot0 + w, hit);
     }
