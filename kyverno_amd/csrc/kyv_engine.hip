@@ -1997,7 +1997,9 @@ void eval_gpu(const Ruleset& rs, const Batch& b, int device, int iters, Results*
         for (const uint3& c : sl.pw) {
           const bool ex = (rs.rules[c.x].flags & RD_GATE_EXACT) && rs.rules[c.x].match.mode != MM_NONE;
           const bool pre = rs.rules[c.x].pre != NONE;
-          (acct ? kyvacct::pss : kyvprod::pss)(ex, pre, pwpe, c.z, stream, d.view, &o, c.x, c.y);
+          // rules with preconditions: KYV_PSS_PRE_WPE (6 by default; at 6 the condition code spills 223 VGPRs)
+          static const int ppwpe = getenv("KYV_PSS_PRE_WPE") ? atoi(getenv("KYV_PSS_PRE_WPE")) : 6;
+          (acct ? kyvacct::pss : kyvprod::pss)(ex, pre, pre ? ppwpe : pwpe, c.z, stream, d.view, &o, c.x, c.y);
           // the pairs it marked ST_PSS_MAP (exclusions, no path columns): the map walk
           (acct ? kyvacct::pss_map : kyvprod::pss_map)(c.z, stream, d.view, &o, c.x, c.y);
         }

@@ -1005,15 +1005,38 @@ pss_kernel(const View* __restrict__ vp, DevOut o, uint32_t k, uint32_t w0) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         if (s_pre[l][mid] <= q) lo = mid; else hi = mid - 1;
       }
-      const uint32_t* L = v.pool + pd.cols + s_pos[lo] * PC_COUNT + PC_LISTS + l * PCL_COUNT;
-      const uint32_t f = pss_container_facts(v, NodeTab{v.nodes + s_root[lo]}, L, s_eb[l][lo] + (q - s_pre[l][lo]));
+      const uint32_t er = s_eb[l][lo] + (q - s_pre[l][lo]);
+      uint32_t f;
+      if (tuni) {
+        // one table for the wave's pods (kind-major batch): the three lists' column offsets as scalar loads, the
+        // lane's list selected, so each container field is one vector load (round 6; per-lane table words and
+        // column offsets were two dependent gathers in front of every field)
+        const uint32_t* T0 = Tu + PC_LISTS;
+        auto co = [&](uint32_t F) -> uint32_t {
+          const uint32_t c0 = sld32(T0 + F), c1 = sld32(T0 + PCL_COUNT + F), c2 = sld32(T0 + 2 * PCL_COUNT + F);
+          const uint32_t o0 = c0 == NONE ? NONE : sld32(v.col_off + c0);
+          const uint32_t o1 = c1 == NONE ? NONE : sld32(v.col_off + c1);
+          const uint32_t o2 = c2 == NONE ? NONE : sld32(v.col_off + c2);
+          return l == 0 ? o0 : l == 1 ? o1 : o2;
+        };
+        f = pss_container_facts_g(v, NodeTab{v.nodes + s_root[lo]}, co, er);
+      } else {
+        const uint32_t* L = v.pool + pd.cols + s_pos[lo] * PC_COUNT + PC_LISTS + l * PCL_COUNT;
+        f = pss_container_facts(v, NodeTab{v.nodes + s_root[lo]}, L, er);
+      }
       atomicOr(&s_fact[lo], f);
     }
   }
   __syncthreads();
   if (T) {
     const uint32_t mask = (pd.flags & PSS_BASELINE) ? ~PSS_RESTRICTED_SLOTS : 0xFFFFFFFFu;
-    if (tuni) pf = pss_checks_cols(v, NodeTab{v.nodes + hroot}, r, Tu, s_fact[lane], true) & mask;
+    if (tuni) {
+      auto po = [&](uint32_t X) -> uint32_t {  // the shared table's column offsets: scalar loads
+        const uint32_t c = sld32(Tu + X);
+        return c == NONE ? NONE : sld32(v.col_off + c);
+      };
+      pf = pss_checks_cols_g(v, NodeTab{v.nodes + hroot}, r, Tu, po, s_fact[lane], true) & mask;
+    }
     else pf = pss_checks_cols(v, NodeTab{v.nodes + hroot}, r, T, s_fact[lane], true) & mask;
     st = pf ? ST_FAIL : ST_PASS;
   }

@@ -494,7 +494,25 @@ enum PssFact : uint32_t {
   F_NREXP = 1u << 6, F_NRUNSET = 1u << 7, F_USER = 1u << 8, F_SEL = 1u << 9, F_SECB = 1u << 10, F_SECREXP = 1u << 11,
   F_SECUNSET = 1u << 12, F_HP = 1u << 13,
 };
-KYV_HD __attribute__((always_inline)) uint32_t pss_container_facts(const View& v, NodeTab R, const uint32_t* L, uint32_t er) {
+// a column entry read through the column's absolute colv offset (NONE: no column)
+KYV_HD PCol pcol_at(const View& v, uint32_t off, uint32_t row) {
+  PCol c{NONE, 0u, 0u};
+  if (off == NONE || row == NONE) return c;
+  KYV_ACCT_ADD(0, 8);
+  const uint64_t x = v.colv[(size_t)off + row];
+  const uint32_t lo = (uint32_t)x;
+  if (lo == NONE) return c;
+  c.i = lo & COL_INDEX_MASK;
+  c.t = lo >> COL_TYPE_SHIFT;
+  c.a = (uint32_t)(x >> 32);
+  return c;
+}
+// The checks of one container (element row `er`); co(F) is the colv offset of the container list's field F (PCL_*),
+// NONE when the table has no such column. pss_container_facts reads the offsets through the list's table words
+// (L[F] -> col_off); pss_kernel (round 6), when the wave's pods share their table, passes offsets it read with scalar
+// loads, so each field is one vector load instead of a chain of three.
+template <class ColOff>
+KYV_HD __attribute__((always_inline)) uint32_t pss_container_facts_g(const View& v, NodeTab R, ColOff co, uint32_t er) {
   auto capOK = [](uint32_t c) {
     return (c >= KSID(CAP_AUDIT_WRITE) && c <= KSID(CAP_SYS_CHROOT)) || c == KSID(NET_BIND_SERVICE);
   };
@@ -504,85 +522,98 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_container_facts(const View& v
   auto secValid = [&](uint32_t t) { return t == KSID(LOCALHOST) || t == KSID(RUNTIMEDEFAULT); };
   uint32_t f = 0;
   // every field of the container: independent loads
-  const PCol sc = pcol(v, L[PCL_SC], er);
-  const PCol priv = pcol(v, L[PCL_PRIV], er), ape = pcol(v, L[PCL_APE], er), nr = pcol(v, L[PCL_NONROOT], er);
-  const PCol us = pcol(v, L[PCL_USER], er), sel = pcol(v, L[PCL_SEL], er), sec = pcol(v, L[PCL_SEC], er);
-  const PCol win = pcol(v, L[PCL_WIN], er), caps = pcol(v, L[PCL_CAPS], er), pm = pcol(v, L[PCL_PROC], er);
-  const uint64_t addl = L[PCL_ADD_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_ADD_LEN]] + er];
-  const uint64_t dropl = L[PCL_DROP_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_DROP_LEN]] + er];
-  const uint64_t portl = L[PCL_PORTS_LEN] == NONE ? ~0ull : v.colv[(size_t)v.col_off[L[PCL_PORTS_LEN]] + er];
-  KYV_ACCT_ADD(0, 8 * ((L[PCL_ADD_LEN] != NONE) + (L[PCL_DROP_LEN] != NONE) + (L[PCL_PORTS_LEN] != NONE)));
+  const PCol sc = pcol_at(v, co(PCL_SC), er);
+  const PCol priv = pcol_at(v, co(PCL_PRIV), er), ape = pcol_at(v, co(PCL_APE), er), nr = pcol_at(v, co(PCL_NONROOT), er);
+  const PCol us = pcol_at(v, co(PCL_USER), er), sel = pcol_at(v, co(PCL_SEL), er), sec = pcol_at(v, co(PCL_SEC), er);
+  const PCol win = pcol_at(v, co(PCL_WIN), er), caps = pcol_at(v, co(PCL_CAPS), er), pm = pcol_at(v, co(PCL_PROC), er);
+  const uint32_t oadd = co(PCL_ADD_LEN), odrop = co(PCL_DROP_LEN), oport = co(PCL_PORTS_LEN);
+  const uint64_t addl = oadd == NONE ? ~0ull : v.colv[(size_t)oadd + er];
+  const uint64_t dropl = odrop == NONE ? ~0ull : v.colv[(size_t)odrop + er];
+  const uint64_t portl = oport == NONE ? ~0ull : v.colv[(size_t)oport + er];
+  KYV_ACCT_ADD(0, 8 * ((oadd != NONE) + (odrop != NONE) + (oport != NONE)));
   const bool set = pobj(sc);
   const int privileged = set ? pbool(priv) : -1, apev = set ? pbool(ape) : -1, nonRoot = set ? pbool(nr) : -1;
   if (!set || apev != 0) f |= F_APE;
   if (set && pobj(caps)) {
-    if ((uint32_t)addl != NONE)
+    if ((uint32_t)addl != NONE) {
+      const uint32_t oself = co(PCL_ADD_SELF);
       for (uint32_t j = 0; j < (uint32_t)addl; j++) {
-        const PCol e = pcol(v, L[PCL_ADD_SELF], (uint32_t)(addl >> 32) + j);
+        const PCol e = pcol_at(v, oself, (uint32_t)(addl >> 32) + j);
         const uint32_t cap = e.t == N_STR ? e.a : SID_EMPTY;
         if (!capOK(cap)) f |= F_CAPSB;
         if (cap != KSID(NET_BIND_SERVICE)) f |= F_CAPSR;
       }
+    }
     uint32_t all = 0;  // (loop-carried flags are integer words throughout: see eval_pss)
-    if ((uint32_t)dropl != NONE)
+    if ((uint32_t)dropl != NONE) {
+      const uint32_t oself = co(PCL_DROP_SELF);
       for (uint32_t j = 0; j < (uint32_t)dropl; j++) {
-        const PCol e = pcol(v, L[PCL_DROP_SELF], (uint32_t)(dropl >> 32) + j);
+        const PCol e = pcol_at(v, oself, (uint32_t)(dropl >> 32) + j);
         if (e.t == N_STR && e.a == KSID(ALL)) all = 1;
       }
+    }
     if (!all) f |= F_CAPSR;
   } else {
     f |= F_CAPSR;
   }
-  if ((uint32_t)portl != NONE)
+  if ((uint32_t)portl != NONE) {
+    const uint32_t ohp = co(PCL_PORT_HOSTPORT);
     for (uint32_t j = 0; j < (uint32_t)portl; j++) {
-      const PCol hp = pcol(v, L[PCL_PORT_HOSTPORT], (uint32_t)(portl >> 32) + j);
+      const PCol hp = pcol_at(v, ohp, (uint32_t)(portl >> 32) + j);
       if (hp.i != NONE && hp.t == N_INT && (hp.a != 0 || R[hp.i].b != 0)) f |= F_PORTS;
     }
+  }
   if (set && privileged == 1) f |= F_PRIV;
   if (set && !pnil(pm) && pstr(pm) != KSID(DEFAULT)) f |= F_PROC;
   if (set && nonRoot != -1) { if (nonRoot == 0) f |= F_NREXP; }
   else f |= F_NRUNSET;
   if (set && us.i != NONE && us.t == N_INT && pzero(R, us)) f |= F_USER;
-  if (set && pobj(sel) && !selValid(pstr(pcol(v, L[PCL_SEL_USER], er)), pstr(pcol(v, L[PCL_SEL_ROLE], er)),
-                                    pstr(pcol(v, L[PCL_SEL_TYPE], er))))
+  if (set && pobj(sel) && !selValid(pstr(pcol_at(v, co(PCL_SEL_USER), er)), pstr(pcol_at(v, co(PCL_SEL_ROLE), er)),
+                                    pstr(pcol_at(v, co(PCL_SEL_TYPE), er))))
     f |= F_SEL;
   if (set && pobj(sec)) {
-    const uint32_t st = pstr(pcol(v, L[PCL_SEC_TYPE], er));
+    const uint32_t st = pstr(pcol_at(v, co(PCL_SEC_TYPE), er));
     if (st == KSID(UNCONFINED)) f |= F_SECB;
     if (!secValid(st)) f |= F_SECREXP;
   } else {
     f |= F_SECUNSET;
   }
-  if (set && pobj(win) && pbool(pcol(v, L[PCL_WIN_HP], er)) == 1) f |= F_HP;
+  if (set && pobj(win) && pbool(pcol_at(v, co(PCL_WIN_HP), er)) == 1) f |= F_HP;
   return f;
+}
+KYV_HD __attribute__((always_inline)) uint32_t pss_container_facts(const View& v, NodeTab R, const uint32_t* L, uint32_t er) {
+  return pss_container_facts_g(v, R, [&](uint32_t F) -> uint32_t { return L[F] == NONE ? NONE : v.col_off[L[F]]; }, er);
 }
 
 // cf_given: the OR of every container's facts (pss_kernel computes them with one container per lane across the
 // wave); else the containers are visited here, one after the other
-KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, const uint32_t* T,
-                                                              uint32_t cf = 0, bool cf_given = false) {
+// po(X): the colv offset of pod field X of table T (NONE: no column) -- pss_checks_cols reads it through the table
+// word and col_off; pss_kernel (round 6) passes offsets read with scalar loads when the wave's pods share one table
+template <class PodOff>
+KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols_g(const View& v, NodeTab R, uint32_t row, const uint32_t* T,
+                                                                PodOff po, uint32_t cf = 0, bool cf_given = false) {
   uint32_t fails = 0;
 
-  const PCol psc = pcol(v, T[PC_PSC], row);
+  const PCol psc = pcol_at(v, po(PC_PSC), row);
   const bool pscSet = pobj(psc);
-  const PCol osn = pcol(v, T[PC_OS_NAME], row);
+  const PCol osn = pcol_at(v, po(PC_OS_NAME), row);
   const bool windows = osn.i != NONE && osn.t == N_STR && osn.a == KSID(WINDOWS);
   // pod-level security context (the columns of a non-map securityContext have no entries)
-  const PCol pnr = pcol(v, T[PC_PSC_NONROOT], row), pus = pcol(v, T[PC_PSC_USER], row);
-  const PCol psel = pcol(v, T[PC_PSC_SEL], row), psec = pcol(v, T[PC_PSC_SEC], row), pwin = pcol(v, T[PC_PSC_WIN], row);
+  const PCol pnr = pcol_at(v, po(PC_PSC_NONROOT), row), pus = pcol_at(v, po(PC_PSC_USER), row);
+  const PCol psel = pcol_at(v, po(PC_PSC_SEL), row), psec = pcol_at(v, po(PC_PSC_SEC), row), pwin = pcol_at(v, po(PC_PSC_WIN), row);
   const int podNonRoot = pscSet ? pbool(pnr) : -1;
   const bool podHasUser = pscSet && pus.i != NONE && pus.t == N_INT;
   const bool podUserZero = podHasUser && pzero(R, pus);
   const bool podSelSet = pscSet && pobj(psel);
   uint32_t pu = SID_EMPTY, pr = SID_EMPTY, pt = SID_EMPTY;
   if (podSelSet) {
-    pu = pstr(pcol(v, T[PC_PSC_SEL_USER], row));
-    pr = pstr(pcol(v, T[PC_PSC_SEL_ROLE], row));
-    pt = pstr(pcol(v, T[PC_PSC_SEL_TYPE], row));
+    pu = pstr(pcol_at(v, po(PC_PSC_SEL_USER), row));
+    pr = pstr(pcol_at(v, po(PC_PSC_SEL_ROLE), row));
+    pt = pstr(pcol_at(v, po(PC_PSC_SEL_TYPE), row));
   }
   const bool podSecSet = pscSet && pobj(psec);
-  const uint32_t podSecType = podSecSet ? pstr(pcol(v, T[PC_PSC_SEC_TYPE], row)) : SID_EMPTY;
-  const int podHostProcess = pscSet && pobj(pwin) ? pbool(pcol(v, T[PC_PSC_WIN_HP], row)) : -1;
+  const uint32_t podSecType = podSecSet ? pstr(pcol_at(v, po(PC_PSC_SEC_TYPE), row)) : SID_EMPTY;
+  const int podHostProcess = pscSet && pobj(pwin) ? pbool(pcol_at(v, po(PC_PSC_WIN_HP), row)) : -1;
 
   // the allowed sets as sid ranges of the seeded well-known strings (no local arrays: they would live in scratch)
   auto capOK = [](uint32_t c) {
@@ -599,7 +630,7 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
   uint32_t secAnnBad = 0;  // set inside loops: an integer word, not a bool (see eval_pss)
   const bool podNonRootTrue = podNonRoot == 1;
   const bool podSecValid = podSecSet && secValid(podSecType);
-  const PCol annc = pcol(v, T[PC_ANN], row);
+  const PCol annc = pcol_at(v, po(PC_ANN), row);
   const uint32_t ann = annc.i;
   const bool annMap = pobj(annc);
   // one pass over the annotations: the appArmor and pod seccomp annotation checks, and whether any key carries the
@@ -662,10 +693,10 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
   if (capsBaseBad) fails |= 1u << PS_CAPS_BASE;
   if (capsRBad) fails |= 1u << PS_CAPS_R_1_22;
   if (capsRBad && !windows) fails |= 1u << PS_CAPS_R_1_25;
-  if (pcol(v, T[PC_HOSTNET], row).t == N_TRUE || pcol(v, T[PC_HOSTPID], row).t == N_TRUE ||
-      pcol(v, T[PC_HOSTIPC], row).t == N_TRUE)
+  if (pcol_at(v, po(PC_HOSTNET), row).t == N_TRUE || pcol_at(v, po(PC_HOSTPID), row).t == N_TRUE ||
+      pcol_at(v, po(PC_HOSTIPC), row).t == N_TRUE)
     fails |= 1u << PS_HOSTNS;
-  const PCol vols = pcol(v, T[PC_VOLUMES], row);
+  const PCol vols = pcol_at(v, po(PC_VOLUMES), row);
   // two volumes per step, and each volume's first four entries (name and source) with them: the loads of one step
   // are independent of each other
   const uint32_t nvol = vols.i != NONE && vols.t == N_ARR ? R[vols.i].b : 0u, vol0 = nvol ? R[vols.i].a : 0u;
@@ -709,7 +740,7 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
   if (secR) fails |= 1u << PS_SECCOMP_R_1_19;
   if (secR && !windows) fails |= 1u << PS_SECCOMP_R_1_25;
   if (pscSet) {
-    const PCol sy = pcol(v, T[PC_PSC_SYSCTLS], row);
+    const PCol sy = pcol_at(v, po(PC_PSC_SYSCTLS), row);
     if (sy.i != NONE && sy.t == N_ARR)
       for (uint32_t i = 0; i < R[sy.i].b; i++) {
         const uint32_t nm = get(R, R[sy.i].a + i, KSID(NAME));
@@ -719,6 +750,12 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, No
   }
   if (podHostProcess == 1 || hpBad) fails |= 1u << PS_WINHOSTPROCESS;
   return fails;
+}
+
+KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols(const View& v, NodeTab R, uint32_t row, const uint32_t* T,
+                                                              uint32_t cf = 0, bool cf_given = false) {
+  return pss_checks_cols_g(v, R, row, T, [&](uint32_t X) -> uint32_t { return T[X] == NONE ? NONE : v.col_off[T[X]]; },
+                           cf, cf_given);
 }
 
 // check-id groups: slots belonging to one check ID (exemptKyvernoExclusion removes whole IDs)
