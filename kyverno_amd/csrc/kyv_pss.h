@@ -633,6 +633,16 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols_g(const View& v, 
   const PCol annc = pcol_at(v, po(PC_ANN), row);
   const uint32_t ann = annc.i;
   const bool annMap = pobj(annc);
+  // (round 6) the host-namespace fields, the volumes list and its first two volume nodes are loaded here, beside the
+  // annotations map, so the volume chain's first steps overlap the annotation pass instead of following it
+  const PCol hnet = pcol_at(v, po(PC_HOSTNET), row), hpid = pcol_at(v, po(PC_HOSTPID), row);
+  const PCol hipc = pcol_at(v, po(PC_HOSTIPC), row);
+  const PCol vols = pcol_at(v, po(PC_VOLUMES), row);
+  const Node vlist = vols.i != NONE && vols.t == N_ARR ? R[vols.i] : Node{N_NULL, 0, 0, 0};
+  const uint32_t nvol = node_type(vlist) == N_ARR ? vlist.b : 0u, vol0 = nvol ? vlist.a : 0u;
+  Node vpre[2];
+#pragma unroll
+  for (uint32_t j = 0; j < 2; j++) vpre[j] = j < nvol ? R[vol0 + j] : Node{N_NULL, 0, 0, 0};
   // one pass over the annotations: the appArmor and pod seccomp annotation checks, and whether any key carries the
   // container seccomp prefix (the per-container check below then runs only for such pods)
   uint32_t annSecC = 0;
@@ -693,13 +703,9 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols_g(const View& v, 
   if (capsBaseBad) fails |= 1u << PS_CAPS_BASE;
   if (capsRBad) fails |= 1u << PS_CAPS_R_1_22;
   if (capsRBad && !windows) fails |= 1u << PS_CAPS_R_1_25;
-  if (pcol_at(v, po(PC_HOSTNET), row).t == N_TRUE || pcol_at(v, po(PC_HOSTPID), row).t == N_TRUE ||
-      pcol_at(v, po(PC_HOSTIPC), row).t == N_TRUE)
-    fails |= 1u << PS_HOSTNS;
-  const PCol vols = pcol_at(v, po(PC_VOLUMES), row);
+  if (hnet.t == N_TRUE || hpid.t == N_TRUE || hipc.t == N_TRUE) fails |= 1u << PS_HOSTNS;
   // two volumes per step, and each volume's first four entries (name and source) with them: the loads of one step
-  // are independent of each other
-  const uint32_t nvol = vols.i != NONE && vols.t == N_ARR ? R[vols.i].b : 0u, vol0 = nvol ? R[vols.i].a : 0u;
+  // are independent of each other (the first step's volume nodes were loaded before the annotation pass)
   auto vol_entry = [&](const Node& e, uint32_t* okv) {
     if (node_type(e) == N_NULL) return;
     const uint32_t k = node_key(e);
@@ -709,7 +715,7 @@ KYV_HD __attribute__((always_inline)) uint32_t pss_checks_cols_g(const View& v, 
   for (uint32_t i = 0; i < nvol; i += 2) {
     Node vn[2];
 #pragma unroll
-    for (uint32_t j = 0; j < 2; j++) vn[j] = i + j < nvol ? R[vol0 + i + j] : Node{N_NULL, 0, 0, 0};
+    for (uint32_t j = 0; j < 2; j++) vn[j] = i == 0 ? vpre[j] : i + j < nvol ? R[vol0 + i + j] : Node{N_NULL, 0, 0, 0};
     Node en[2][4];
 #pragma unroll
     for (uint32_t j = 0; j < 2; j++)
