@@ -1722,7 +1722,12 @@ std::string jit_source(const Ruleset& rs, std::vector<uint8_t>* jit_rules, std::
     // C3 (r4 A/B, evaluation / walk ms): one kernel at 6 waves/EU 12.04 / 7.74; 2 parts at 8 waves 11.35 / 7.43; 3 at 8
     // 11.25 / 7.34; 4 at 8 11.33 / 7.26 (smaller kernels: fewer spills at 8 waves, and they interleave with the
     // condition kernels on the other stream)
-    const size_t nparts = std::max<size_t>(1, std::min<size_t>(fused.size(), getenv("KYV_FUSED_SPLIT") ? (size_t)atoi(getenv("KYV_FUSED_SPLIT")) : 3));
+    // KYV_FUSED_SPLIT_HEAVY: the parts of the wildcard-metadata group, whose kernels run at the heavy target. Default 1:
+    // its few rules (C3: app-armor for pods, workloads, CronJobs) have disjoint kind gates, so as parts every kernel
+    // but one passed over the whole batch for nothing (round 6, C3 walk 6.56-6.67 -> 6.39 ms as one kernel)
+    const bool heavy_grp = gwpe[gi] == -1 && std::count(gwpe.begin(), gwpe.end(), -2);
+    const char* split_env = heavy_grp ? getenv("KYV_FUSED_SPLIT_HEAVY") : getenv("KYV_FUSED_SPLIT");
+    const size_t nparts = std::max<size_t>(1, std::min<size_t>(fused.size(), split_env ? (size_t)atoi(split_env) : heavy_grp ? 1 : 3));
     for (size_t pi = 0; pi < nparts; pi++) {
       const std::vector<size_t> part(fused.begin() + fused.size() * pi / nparts, fused.begin() + fused.size() * (pi + 1) / nparts);
       const std::string sname = "JitFused" + std::to_string(gi) + (pi ? "p" + std::to_string(pi) : std::string());
